@@ -1,0 +1,245 @@
+"""SFNO-Block forward throughput on MI355X (BASELINE.json metric / config 2).
+
+Workload (one "step"): one SFNO-Block forward — FourierNeuralOperatorBlock_Filmed
+with the reference-default non-linear spectral filter, middle-block wiring
+(inner skip 1x1 conv, outer identity skip, MLP ratio 2), InstanceNorm eps 1e-6,
+FiLM on — over one synthetic 721x1440x256 field per GPU (x ~ N(0,1), seed 0),
+lmax=360/mmax=361 equiangular SHT with the reference's ×1e5 rescale, random
+init weights of that architecture (reference init recipe, seed 1).
+
+Multi-GPU (torchrun, one process per GPU): replicas — each rank runs its own
+field through the block; no data-path collective ("scaling": "weak"); the timed
+region is bracketed by barrier + synchronize and the max over ranks is used.
+
+Prints ONE JSON line (rank 0) with the roofline of the dominant kernel (timed
+with hipEvents on the block's stream over the timed region) and the oracle's
+CPU timing on a bounded sample (rank 0, N=1).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+PKG_DIR = os.path.join(REPO, "modulated-spherical-fourier-neural-operator_amd")
+for _p in (REPO, PKG_DIR):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+import torch  # noqa: E402
+
+PEAK_FP32_MFMA_TFLOPS = 157.3   # MI355X_MICROARCH.md: f32 MFMA 157.3 TF (spec)
+PEAK_HBM_GBS = 8000.0           # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=1, help="fields per GPU per step")
+    ap.add_argument("--filter", default="non-linear", choices=["non-linear", "linear"])
+    ap.add_argument("--C", type=int, default=256)
+    ap.add_argument("--nlat", type=int, default=721)
+    ap.add_argument("--nlon", type=int, default=1440)
+    ap.add_argument("--lmax", type=int, default=360)
+    ap.add_argument("--cpu-baseline", type=int, default=1, help="time the oracle on CPU (rank 0, N=1)")
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--stages", action="store_true", help="print per-stage timings to stderr")
+    return ap.parse_args()
+
+
+def stage_work(name, B, C, nlat, nlon, lmax, mmax, hid, shid):
+    """Algorithmic work per launch: ('mfma', flops) or ('hbm', bytes)."""
+    T = sum(max(lmax - m, 0) for m in range(mmax))
+    P = nlat * nlon
+    BC = B * C
+    tab = {
+        "mlp_fc1": ("mfma", 2 * B * P * C * hid),
+        "mlp_fc2": ("mfma", 2 * B * P * C * hid),
+        "inner_skip": ("mfma", 2 * B * P * C * C),
+        "spectral_l0": ("mfma", 8 * B * T * C * shid),
+        "spectral_l1": ("mfma", 8 * B * T * shid * shid),
+        "spectral_l2": ("mfma", 8 * B * T * shid * shid),
+        "spectral_out": ("mfma", 8 * B * T * shid * C),
+        "legendre_fwd": ("mfma", 2 * (2 * BC) * nlat * T),
+        "legendre_inv": ("mfma", 2 * (2 * BC) * nlat * T),
+        # HBM-bound stages: compulsory bytes moved
+        "fft_fwd": ("hbm", BC * nlat * (nlon * 4 + mmax * 8)),
+        "fft_inv": ("hbm", BC * nlat * (nlon * 4 + mmax * 8)),
+        "transpose_fwd": ("hbm", 2 * BC * nlat * mmax * 8),
+        "transpose_inv": ("hbm", 2 * BC * nlat * mmax * 8),
+        "linear_contract": ("hbm", 8 * C * C * T + 2 * 8 * BC * T),
+    }
+    return tab.get(name)
+
+
+def build_block(args, dev):
+    from functools import partial
+
+    from oracle import sfno_ref  # parameter recipe only (same numbers as the parity tests)
+    from msfno_amd.harmonics import InverseRealSHT, RealSHT
+    from msfno_amd.sfno import FourierNeuralOperatorBlock_Filmed
+
+    C, nlat, nlon, lmax = args.C, args.nlat, args.nlon, args.lmax
+    mmax = lmax + 1
+    cfg = sfno_ref.BlockCfg(filter_type=args.filter)
+    p = sfno_ref.make_block_params(C, lmax, mmax, cfg, seed=1)
+    sht = RealSHT(nlat, nlon, lmax=lmax, mmax=mmax, grid="equiangular").float()
+    isht = InverseRealSHT(nlat, nlon, lmax=lmax, mmax=mmax, grid="equiangular").float()
+    sht.weights = sht.weights * 1e5
+    isht.pct = isht.pct / 1e5
+    norm = partial(torch.nn.InstanceNorm2d, num_features=C, eps=1e-6, affine=True,
+                   track_running_stats=False)
+    blk = FourierNeuralOperatorBlock_Filmed(sht, isht, C, filter_type=args.filter, mlp_ratio=2.0,
+                                            norm_layer=(norm, norm), inner_skip="linear",
+                                            outer_skip="identity", mlp_mode="distributed",
+                                            spectral_layers=3)
+    blk.load_state_dict(p, strict=False)
+    return blk.eval().to(dev), p, cfg
+
+
+def cpu_baseline(args, p, cfg):
+    """Oracle (torch-CPU restatement of the reference block) on a bounded sample."""
+    from oracle import sfno_ref
+    threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
+    torch.set_num_threads(threads)
+    C, nlat, nlon, lmax = args.C, args.nlat, args.nlon, args.lmax
+    sht, isht = sfno_ref.make_transforms(nlat, nlon, lmax, lmax + 1)
+    g = torch.Generator().manual_seed(0)
+    x = torch.randn(1, C, nlat, nlon, generator=g)
+    gamma = 0.1 * torch.randn(1, C, generator=g)
+    beta = 0.1 * torch.randn(1, C, generator=g)
+    with torch.no_grad():
+        sfno_ref.block_forward(p, x, sht, isht, cfg, gamma, beta, 1.0)   # warm-up
+        t0 = time.perf_counter()
+        sfno_ref.block_forward(p, x, sht, isht, cfg, gamma, beta, 1.0)
+        dt = time.perf_counter() - t0
+    return {"value": 1.0 / dt, "unit": "fields/s", "cores": threads, "kind": "port",
+            "sample": f"1 field ({nlat}x{nlon}x{C}, lmax={lmax}, {args.filter} filter) after 1 "
+                      f"warm-up; oracle/sfno_ref.py torch-CPU restatement, {threads} threads; "
+                      f"{dt:.2f} s/field"}
+
+
+def main():
+    args = parse()
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = world > 1
+    if dist:
+        import torch.distributed as td
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        td.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    from msfno_amd import _native as N
+
+    blk, p, cfg = build_block(args, dev)
+    B, C = args.batch, args.C
+    g = torch.Generator().manual_seed(1000 * rank)
+    x = torch.randn(B, C, args.nlat, args.nlon, generator=g).to(dev)
+    gamma = (0.1 * torch.randn(B, C, generator=g)).to(dev)
+    beta = (0.1 * torch.randn(B, C, generator=g)).to(dev)
+
+    def barrier():
+        if dist:
+            torch.distributed.barrier()
+
+    with torch.no_grad():
+        for _ in range(args.warmup):
+            y = blk(x, gamma, beta, 1.0)
+        torch.cuda.synchronize()
+        N.profile_collect()  # discard
+        N.profile_enable(True)
+        barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            y = blk(x, gamma, beta, 1.0)
+        torch.cuda.synchronize()
+        barrier()
+        t1 = time.perf_counter()
+        N.profile_enable(False)
+        stages = N.profile_collect()
+    elapsed = t1 - t0
+    if dist:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        elapsed = t.item()
+    assert torch.isfinite(y).all()
+
+    fields = world * B * args.steps
+    value = fields / elapsed
+    ms_per_step = 1000.0 * elapsed / args.steps
+
+    mmax = args.lmax + 1
+    hid = shid = 2 * C
+    # dominant kernel = stage with the largest device time in the timed region
+    dom = max(stages.items(), key=lambda kv: kv[1][0]) if stages else None
+    roof = None
+    if dom is not None:
+        name, (tot_ms, cnt) = dom
+        avg_s = tot_ms / cnt / 1000.0
+        w = stage_work(name, B, C, args.nlat, args.nlon, args.lmax, mmax, hid, shid)
+        if w is not None:
+            kind, amount = w
+            if kind == "mfma":
+                ach = amount / avg_s / 1e12
+                roof = {"bound": "mfma", "achieved": round(ach, 2), "peak": PEAK_FP32_MFMA_TFLOPS,
+                        "unit": "TFLOP/s", "frac": round(ach / PEAK_FP32_MFMA_TFLOPS, 4),
+                        "traffic": None, "kernel": name, "avg_ms": round(avg_s * 1e3, 4)}
+            else:
+                ach = amount / avg_s / 1e9
+                roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": PEAK_HBM_GBS,
+                        "unit": "GB/s", "frac": round(ach / PEAK_HBM_GBS, 4), "traffic": None,
+                        "kernel": name, "avg_ms": round(avg_s * 1e3, 4)}
+    if args.stages and rank == 0:
+        for k, (ms, c) in sorted(stages.items(), key=lambda kv: -kv[1][0]):
+            w = stage_work(k, B, C, args.nlat, args.nlon, args.lmax, mmax, hid, shid)
+            extra = ""
+            if w:
+                a = w[1] / (ms / c / 1e3)
+                extra = f" {a / 1e12:.1f} TFLOP/s" if w[0] == "mfma" else f" {a / 1e9:.0f} GB/s"
+            print(f"  stage {k:18s} {ms / c:8.3f} ms x{c}{extra}", file=sys.stderr)
+
+    cpu = None
+    if rank == 0 and world == 1 and args.cpu_baseline:
+        del blk
+        torch.cuda.empty_cache()
+        cpu = cpu_baseline(args, p, cfg)
+
+    if rank == 0:
+        out = {
+            "metric": "SFNO-Block forward fields/sec on 721x1440x256; rocprof HBM GB/s vs peak",
+            "value": round(value, 3),
+            "unit": "fields/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (x~N(0,1), random-init weights of the reference block)",
+            "config": {"workload": f"sfno_block_fwd_{args.nlat}x{args.nlon}_C{C}_lmax{args.lmax}_"
+                                   f"{args.filter}_filmed",
+                       "batch_per_gpu": B, "filter": args.filter,
+                       "parallelism": f"replicas{world}" if world > 1 else "single"},
+            "roofline": roof,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out), flush=True)
+    if dist:
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

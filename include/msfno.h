@@ -1,0 +1,161 @@
+/*
+ * msfno.h — C-ABI of libmsfno.so, the MI355X (gfx950) implementation of the
+ * SFNO-Block forward hot path of Slusny/Modulated-Spherical-Fourier-Neural-Operator.
+ *
+ * The reference path is pure Python/PyTorch (no FFI).  Every entry point below
+ * replaces one stock-torch / torch-harmonics call of the reference; the
+ * replaced interface is cited on each declaration (paths relative to the
+ * reference repo).  The Python host layer (msfno_amd/, ctypes) mirrors the
+ * reference module API on top of these functions.
+ *
+ * Conventions
+ *   - Plain pointers + sizes; every device pointer is caller-owned (PyTorch
+ *     tensors); the library owns only plans (tables, twiddles, descriptors).
+ *   - All work is stream-ordered on the hipStream_t passed as `stream`
+ *     (void*); no call synchronises the device, allocates device memory or
+ *     copies to the host, except *_plan_create/_load_* (one-time setup).
+ *   - Return value: 0 = ok, otherwise an MSFNO_E* code; msfno_last_error()
+ *     returns a thread-local message.  The Python layer re-raises the
+ *     reference's exception types (NotImplementedError / ValueError /
+ *     AssertionError) from these codes.
+ *   - fp32 arithmetic throughout (complex64 in spectral space), as the
+ *     reference runs its transforms with autocast disabled
+ *     (MSFNO/Models/sfno/layers.py:403-422, 627-637).
+ */
+#ifndef MSFNO_H
+#define MSFNO_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MSFNO_OK 0
+#define MSFNO_EINVAL 1         /* bad argument / shape   -> ValueError / AssertionError */
+#define MSFNO_EUNSUPPORTED 2   /* unsupported config    -> NotImplementedError        */
+#define MSFNO_EHIP 3           /* HIP runtime failure   -> RuntimeError               */
+#define MSFNO_EWORKSPACE 4     /* workspace too small    -> ValueError                 */
+
+#define MSFNO_GRID_EQUIANGULAR 0
+#define MSFNO_GRID_LEGENDRE_GAUSS 1
+
+typedef struct msfno_sht_plan_s* msfno_sht_plan_t;
+
+const char* msfno_last_error(void);
+int msfno_abi_version(void);
+
+/* ---------------------------------------------------------------------------
+ * Host-side plan math (fp64).  Replaces torch_harmonics.quadrature
+ * (used at MSFNO/Models/losses.py:90,129) and torch_harmonics.legendre as
+ * used by RealSHT/InverseRealSHT.__init__ (constructed at
+ * MSFNO/Models/sfno/sfnonet.py:537-548).
+ * ------------------------------------------------------------------------- */
+/* nodes ascending in [-1,1] (cos of colatitude, before the north->south flip) */
+int msfno_quadrature(int nlat, int grid, double* nodes, double* weights);
+/* table (mmax, lmax, nlat) float64, colatitudes north->south:
+ *   inverse == 0 : P̄_l^m(cos θ_k) · w_k   (RealSHT.weights)
+ *   inverse == 1 : P̄_l^m(cos θ_k)         (InverseRealSHT.pct)
+ * orthonormal ("ortho") normalisation, Condon–Shortley phase if csphase. */
+int msfno_legendre_table(int mmax, int lmax, int nlat, int grid, int inverse, int csphase,
+                         double* table);
+
+/* ---------------------------------------------------------------------------
+ * SHT plans.  One plan per transform object (RealSHT / InverseRealSHT).
+ * ------------------------------------------------------------------------- */
+int msfno_sht_plan_create(int nlat, int nlon, int lmax, int mmax, int inverse,
+                          msfno_sht_plan_t* plan);
+int msfno_sht_plan_destroy(msfno_sht_plan_t plan);
+/* Copy + re-lay-out the module's table (mmax,lmax,nlat) fp32 device buffer
+ * (RealSHT.weights incl. the ×1e5 of sfnonet.py:552/554, or
+ * InverseRealSHT.pct incl. the ÷1e5 of :553/:555) into the plan's GEMM layout. */
+int msfno_sht_plan_load_table(msfno_sht_plan_t plan, const float* table, void* stream);
+
+/* RealSHT.forward  (torch_harmonics RealSHT; called at layers.py:405,629):
+ *   x (bc, nlat, nlon) fp32  ->  out (bc, lmax, mmax) complex64 interleaved */
+size_t msfno_sht_workspace_size(msfno_sht_plan_t plan, int bc);
+int msfno_sht_forward(msfno_sht_plan_t plan, const float* x, float* out, int bc,
+                      void* ws, size_t ws_bytes, void* stream);
+/* InverseRealSHT.forward (called at layers.py:421,638):
+ *   in (bc, lmax, mmax) complex64 -> x (bc, nlat, nlon) fp32 */
+int msfno_sht_inverse(msfno_sht_plan_t plan, const float* in, float* x, int bc,
+                      void* ws, size_t ws_bytes, void* stream);
+
+/* ---------------------------------------------------------------------------
+ * Contractions (MSFNO/Models/sfno/contractions.py)
+ * ------------------------------------------------------------------------- */
+/* compl_contract_fwd_c  (contractions.py:37-41, einsum "bin,kin->bkn"):
+ *   a (B,Ci,T,2), w (Co,Ci,T,2) -> y (B,Co,T,2)   [linear filter, layers.py:410-413] */
+int msfno_compl_contract_fwd_c(const float* a, const float* w, float* y, int B, int Ci,
+                               int Co, int T, void* stream);
+/* compl_mul2d_fwd_c (contractions.py:132-137, einsum "bixy,io->boxy"):
+ *   a (B,Ci,XY,2), w (Ci,Co,2) -> y (B,Co,XY,2); relu_real != 0 fuses
+ *   ComplexReLU(mode="real") (activations.py:42-46) */
+int msfno_compl_mul2d_fwd_c(const float* a, const float* w, float* y, int B, int Ci, int Co,
+                            long long XY, int relu_real, void* stream);
+
+/* ---------------------------------------------------------------------------
+ * Fused SFNO-Block forward.
+ * Replaces FourierNeuralOperatorBlock.forward (sfnonet.py:221-251) and
+ * FourierNeuralOperatorBlock_Filmed.forward (sfnonet.py:359-393) including
+ * SpectralFilterLayer (:56-133), SpectralAttentionS2 (layers.py:536-639) /
+ * SpectralConvS2 (layers.py:336-427), InstanceNorm2d ×2, FiLM (:689-697) and
+ * MLP (layers.py:145-178).
+ * ------------------------------------------------------------------------- */
+#define MSFNO_FILTER_NONLINEAR 0
+#define MSFNO_FILTER_LINEAR 1
+#define MSFNO_SKIP_NONE 0
+#define MSFNO_SKIP_LINEAR 1
+#define MSFNO_SKIP_IDENTITY 2
+
+typedef struct msfno_block_desc {
+  int C;                    /* embed_dim_sfno                                       */
+  int filter_type;          /* MSFNO_FILTER_*                                       */
+  int inner_skip;           /* MSFNO_SKIP_*   (sfnonet.py:304-307)                  */
+  int outer_skip;           /* MSFNO_SKIP_NONE / _IDENTITY (sfnonet.py:333-336)      */
+  int has_mlp;              /* mlp_mode != "none" (sfnonet.py:323)                  */
+  int mlp_hidden;           /* int(C*mlp_ratio)                                      */
+  int spectral_layers;      /* non-linear: number of hidden complex layers (w.0..)  */
+  int spec_hidden;          /* non-linear: int(hidden_size_factor*C)               */
+  float norm_eps;           /* InstanceNorm2d eps (1e-6, sfnonet.py:494)            */
+  const float* norm0_w; const float* norm0_b;       /* (C)                          */
+  const float* norm1_w; const float* norm1_b;       /* (C)                          */
+  const float* spec_w[8];   /* non-linear: w.l  (Cin_l, Cout_l, 2)                  */
+  const float* spec_wout;   /* non-linear: wout (spec_hidden, C, 2)                 */
+  const float* lin_w;       /* linear: w (C, C, T, 2), T = #tril(lmax,mmax)         */
+  const float* skip_w; const float* skip_b;         /* inner_skip (C,C,1,1), (C)    */
+  const float* fc1_w; const float* fc1_b;           /* mlp.fwd.0 (H,C,1,1), (H)     */
+  const float* fc2_w; const float* fc2_b;           /* mlp.fwd.2 (C,H,1,1), (C)     */
+} msfno_block_desc;
+
+size_t msfno_block_workspace_size(const msfno_block_desc* d, msfno_sht_plan_t fwd,
+                                  msfno_sht_plan_t inv, int B);
+/* x (B,C,nlat_in,nlon_in) -> out (B,C,nlat_out,nlon_out).  gamma/beta (B,C) may
+ * be NULL (unfilmed block); FiLM is (1+γ·scale)·x + β·scale after norm1. */
+int msfno_block_forward(const msfno_block_desc* d, msfno_sht_plan_t fwd, msfno_sht_plan_t inv,
+                        const float* x, const float* gamma, const float* beta, float film_scale,
+                        float* out, int B, void* ws, size_t ws_bytes, void* stream);
+/* SpectralFilterLayer.forward alone (sfnonet.py:132-133): SHT -> filter -> ISHT,
+ * no norms.  x (B,C,nlat_in,nlon_in) -> y (B,C,nlat_out,nlon_out). */
+int msfno_filter_forward(const msfno_block_desc* d, msfno_sht_plan_t fwd, msfno_sht_plan_t inv,
+                         const float* x, float* y, int B, void* ws, size_t ws_bytes,
+                         void* stream);
+
+/* ---------------------------------------------------------------------------
+ * Instrumentation (not a reference interface): per-stage device time of the
+ * fused block measured with hipEvents recorded on the caller's stream between
+ * stages.  Used by bench.py to time the dominant kernel inside the timed region.
+ * ------------------------------------------------------------------------- */
+#define MSFNO_PROF_NSTAGES 32
+int msfno_profile_enable(int on);
+/* synchronises on the recorded events, adds per-stage milliseconds / launch
+ * counts since the last collect into total_ms[stage] / counts[stage] (arrays of
+ * MSFNO_PROF_NSTAGES), and clears the recorded marks */
+int msfno_profile_collect(double* total_ms, int* counts);
+const char* msfno_profile_stage_name(int stage);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MSFNO_H */

@@ -1,0 +1,669 @@
+// libmsfno C-ABI: plans (fp64 host math + device tables), standalone SHT
+// transforms, contractions and the fused SFNO-Block forward orchestration.
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+
+#include "kernels.h"
+
+namespace msfno {
+
+static thread_local std::string g_last_error;
+void set_error(const std::string& msg) { g_last_error = msg; }
+
+void SpecLayout::build(int lmax_, int mmax_) {
+  lmax = lmax_;
+  mmax = mmax_;
+  L.assign(mmax, 0);
+  Lp.assign(mmax, 0);
+  off.assign(mmax, 0);
+  T = Tp = 0;
+  mact = 0;
+  for (int m = 0; m < mmax; ++m) {
+    const int l = std::max(lmax - m, 0);
+    L[m] = l;
+    Lp[m] = (int)round_up(l, 4);
+    off[m] = (int)Tp;
+    T += l;
+    Tp += Lp[m];
+    if (l > 0) mact = m + 1;
+  }
+  ldT = round_up(std::max<int64_t>(Tp, 4), 4);
+}
+
+// ---------------------------------------------------------------------------
+// host-side fp64 plan math ([TH] torch_harmonics.quadrature / .legendre)
+// ---------------------------------------------------------------------------
+static void gauss_legendre(int n, std::vector<double>& x, std::vector<double>& w) {
+  x.assign(n, 0.0);
+  w.assign(n, 0.0);
+  for (int i = 0; i < n; ++i) {
+    double z = std::cos(M_PI * (i + 0.75) / (n + 0.5));
+    double pp = 0.0;
+    for (int it = 0; it < 100; ++it) {
+      double p1 = 1.0, p2 = 0.0;
+      for (int j = 1; j <= n; ++j) {
+        const double p3 = p2;
+        p2 = p1;
+        p1 = ((2.0 * j - 1.0) * z * p2 - (j - 1.0) * p3) / j;
+      }
+      pp = n * (z * p1 - p2) / (z * z - 1.0);
+      const double z1 = z;
+      z = z1 - p1 / pp;
+      if (std::fabs(z - z1) < 1e-16) break;
+    }
+    // recompute derivative at the converged root
+    double p1 = 1.0, p2 = 0.0;
+    for (int j = 1; j <= n; ++j) {
+      const double p3 = p2;
+      p2 = p1;
+      p1 = ((2.0 * j - 1.0) * z * p2 - (j - 1.0) * p3) / j;
+    }
+    pp = n * (z * p1 - p2) / (z * z - 1.0);
+    x[n - 1 - i] = z;  // ascending
+    w[n - 1 - i] = 2.0 / ((1.0 - z * z) * pp * pp);
+  }
+}
+
+static void clenshaw_curtis(int n, std::vector<double>& x, std::vector<double>& w) {
+  x.assign(n, 0.0);
+  w.assign(n, 0.0);
+  if (n == 2) {
+    x[0] = -1.0; x[1] = 1.0;
+    w[0] = w[1] = 1.0;
+    return;
+  }
+  const int N = n - 1;
+  for (int j = 0; j < n; ++j) {
+    const double th = M_PI - (double)j * M_PI / N;  // cos(linspace(pi, 0, n))
+    x[j] = std::cos(th);
+    const double tj = (double)j * M_PI / N;
+    double s = 0.0;
+    for (int k = 1; k <= N / 2; ++k) {
+      const double bk = (2 * k == N) ? 1.0 : 2.0;
+      s += bk / (4.0 * k * k - 1.0) * std::cos(2.0 * k * tj);
+    }
+    const double cj = (j == 0 || j == N) ? 1.0 : 2.0;
+    w[j] = cj / N * (1.0 - s);
+  }
+}
+
+static int quadrature(int nlat, int grid, std::vector<double>& x, std::vector<double>& w) {
+  if (grid == MSFNO_GRID_LEGENDRE_GAUSS) {
+    MSFNO_REQUIRE(nlat >= 1, MSFNO_EINVAL, "nlat must be >= 1");
+    gauss_legendre(nlat, x, w);
+  } else if (grid == MSFNO_GRID_EQUIANGULAR) {
+    MSFNO_REQUIRE(nlat >= 2, MSFNO_EINVAL, "equiangular grid needs nlat >= 2");
+    clenshaw_curtis(nlat, x, w);
+  } else {
+    set_error("Unknown quadrature mode");
+    return MSFNO_EUNSUPPORTED;
+  }
+  return MSFNO_OK;
+}
+
+// (-1)^m c_l^m P_l^m at cos(theta_k), same recurrence and operation order as [TH] legpoly
+static int legendre_table(int mmax, int lmax, int nlat, int grid, int inverse, int csphase,
+                          double* out) {
+  std::vector<double> x, w;
+  MSFNO_TRY(quadrature(nlat, grid, x, w));
+  const int nmax = std::max(mmax, lmax);
+  // k-independent recurrence coefficients (same expressions as [TH] legpoly)
+  std::vector<double> ca((size_t)nmax * nmax, 0.0), cb((size_t)nmax * nmax, 0.0);
+  for (int l = 2; l < nmax; ++l)
+    for (int m = 0; m < l - 1; ++m) {
+      ca[(size_t)m * nmax + l] = std::sqrt((2.0 * l - 1) / (l - m) * (2.0 * l + 1) / (l + m));
+      cb[(size_t)m * nmax + l] = std::sqrt((double)(l + m - 1) / (l - m) * (2.0 * l + 1) /
+                                           (2.0 * l - 3) * (l - m - 1) / (l + m));
+    }
+  std::vector<double> vdm((size_t)nmax * nmax);
+  for (int k = 0; k < nlat; ++k) {
+    // theta = flip(arccos(nodes)): colatitude index k uses node nlat-1-k
+    const double xk = std::cos(std::acos(x[nlat - 1 - k]));
+    std::fill(vdm.begin(), vdm.end(), 0.0);
+    auto V = [&](int m, int l) -> double& { return vdm[(size_t)m * nmax + l]; };
+    V(0, 0) = 1.0 / std::sqrt(4.0 * M_PI);  // ortho norm; inverse factor is 1 as well
+    for (int l = 1; l < nmax; ++l) {
+      V(l - 1, l) = std::sqrt(2.0 * l + 1) * xk * V(l - 1, l - 1);
+      V(l, l) = std::sqrt((2.0 * l + 1) * (1 + xk) * (1 - xk) / 2.0 / l) * V(l - 1, l - 1);
+    }
+    for (int m = 0; m < nmax; ++m) {
+      const double* a = &ca[(size_t)m * nmax];
+      const double* b = &cb[(size_t)m * nmax];
+      double* v = &vdm[(size_t)m * nmax];
+      for (int l = m + 2; l < nmax; ++l) v[l] = xk * a[l] * v[l - 1] - b[l] * v[l - 2];
+    }
+    const double wk = inverse ? 1.0 : w[k];  // weights are symmetric (unflipped in [TH])
+    for (int m = 0; m < mmax; ++m) {
+      const double sgn = (csphase && (m & 1)) ? -1.0 : 1.0;
+      for (int l = 0; l < lmax; ++l)
+        out[((size_t)m * lmax + l) * nlat + k] = sgn * V(m, l) * wk;
+    }
+  }
+  return MSFNO_OK;
+}
+
+// ---------------------------------------------------------------------------
+// stage profiler (hipEvents on the caller's stream)
+// ---------------------------------------------------------------------------
+enum Stage {
+  ST_FFT_FWD = 0, ST_NORM0, ST_TRANSPOSE_FWD, ST_LEG_FWD, ST_SPEC_PREP, ST_SPEC_L0, ST_SPEC_L1,
+  ST_SPEC_L2, ST_SPEC_L3, ST_SPEC_OUT, ST_LIN_GATHER, ST_LIN_CONTRACT, ST_LIN_SCATTER, ST_LEG_INV,
+  ST_TRANSPOSE_INV, ST_FFT_INV, ST_SKIP, ST_NORM1, ST_FC1, ST_FC2, ST_OUT_AFFINE, ST_END
+};
+static const char* kStageNames[MSFNO_PROF_NSTAGES] = {
+    "fft_fwd", "norm0_stats", "transpose_fwd", "legendre_fwd", "spectral_prep", "spectral_l0",
+    "spectral_l1", "spectral_l2", "spectral_l3", "spectral_out", "linear_gather",
+    "linear_contract", "linear_scatter", "legendre_inv", "transpose_inv", "fft_inv",
+    "inner_skip", "norm1_film_fold", "mlp_fc1", "mlp_fc2", "out_affine", "end"};
+
+struct Profiler {
+  bool on = false;
+  std::vector<std::pair<int, hipEvent_t>> marks;
+  std::vector<hipEvent_t> pool;
+  void mark(int stage, hipStream_t s) {
+    if (!on) return;
+    hipEvent_t e;
+    if (!pool.empty()) {
+      e = pool.back();
+      pool.pop_back();
+    } else if (hipEventCreate(&e) != hipSuccess) {
+      return;
+    }
+    if (hipEventRecord(e, s) != hipSuccess) {
+      pool.push_back(e);
+      return;
+    }
+    marks.emplace_back(stage, e);
+  }
+};
+static Profiler g_prof;
+static inline void prof(int stage, hipStream_t s) { g_prof.mark(stage, s); }
+
+// ---------------------------------------------------------------------------
+// workspace carving
+// ---------------------------------------------------------------------------
+struct Carve {
+  size_t off = 0;
+  char* base = nullptr;
+  template <typename T>
+  T* take(size_t count) {
+    const size_t o = off;
+    off = (size_t)round_up((int64_t)(off + count * sizeof(T)), 256);
+    return base ? reinterpret_cast<T*>(base + o) : nullptr;
+  }
+};
+
+static int ensure_desc(msfno_sht_plan_s* p, int R, int other_ld, int64_t ldT) {
+  // forward plan: A = Xt (R x nlat, ld ldk), B = table, C = S (ld ldT)
+  // inverse plan: A = S (ld ldT), B = table, C = Yt (R x nlat, ld ldk)
+  if (p->desc_R == R && p->d_desc) return MSFNO_OK;
+  int bm, bn;
+  gemm_tile_dims(TILE_128x64, &bm, &bn);
+  std::vector<GemmDesc> d;
+  int tiles = 0;
+  const SpecLayout& L = p->spec;
+  for (int m = 0; m < L.mact; ++m) {
+    GemmDesc g{};
+    g.M = R;
+    if (!p->inverse) {
+      g.N = L.Lp[m]; g.K = p->nlat;
+      g.lda = p->ldk; g.ldb = L.Lp[m]; g.ldc = (int)ldT;
+      g.offA = (int64_t)m * R * p->ldk; g.offB = p->tab_off[m]; g.offC = L.off[m];
+    } else {
+      g.N = p->nlat; g.K = L.L[m];
+      g.lda = (int)ldT; g.ldb = p->ldk; g.ldc = p->ldk;
+      g.offA = L.off[m]; g.offB = p->tab_off[m]; g.offC = (int64_t)m * R * p->ldk;
+    }
+    g.tiles_m = (int)cdiv(g.M, bm);
+    g.tiles_n = (int)cdiv(g.N, bn);
+    g.tile_start = tiles;
+    tiles += g.tiles_m * g.tiles_n;
+    d.push_back(g);
+  }
+  (void)other_ld;
+  if (p->d_desc) MSFNO_CHECK_HIP(hipFree(p->d_desc));
+  p->d_desc = nullptr;
+  MSFNO_CHECK_HIP(hipMalloc(&p->d_desc, std::max<size_t>(1, d.size()) * sizeof(GemmDesc)));
+  if (!d.empty())
+    MSFNO_CHECK_HIP(hipMemcpy(p->d_desc, d.data(), d.size() * sizeof(GemmDesc), hipMemcpyHostToDevice));
+  p->ndesc = (int)d.size();
+  p->desc_tiles = tiles;
+  p->desc_R = R;
+  return MSFNO_OK;
+}
+
+static int legendre_fwd(msfno_sht_plan_s* f, const float* Xt, float* S, int R, hipStream_t s) {
+  MSFNO_TRY(ensure_desc(f, R, 0, f->spec.ldT));
+  GemmEpi e;
+  return gemm_desc(TILE_128x64, Xt, f->table, S, f->d_desc, f->ndesc, f->desc_tiles, e, s);
+}
+
+static int legendre_inv(msfno_sht_plan_s* g, const float* S, float* Yt, int R, hipStream_t s) {
+  MSFNO_TRY(ensure_desc(g, R, 0, g->spec.ldT));
+  GemmEpi e;
+  return gemm_desc(TILE_128x64, S, g->table, Yt, g->d_desc, g->ndesc, g->desc_tiles, e, s);
+}
+
+// ---------------------------------------------------------------------------
+// block workspace layout (shared by size query and forward)
+// ---------------------------------------------------------------------------
+struct BlockBufs {
+  float2* Xn; float* Xt; float2* rs0; float* sc0; float* sh0;
+  float* Sa; float* Sb; float* Sc; float* Wexp[9];
+  float* xt; float* yt;
+  float* Yt; float2* Yn; float* filt; float* x1;
+  float2* st1; float* sc1; float* sh1;
+  float* W1f; float* b1f; float* h;
+};
+
+static constexpr int kStatTile = 128;  // BN of the 1x1-conv GEMM tile
+
+static void carve_block(Carve& cv, BlockBufs& b, const msfno_block_desc* d,
+                        const msfno_sht_plan_s* f, const msfno_sht_plan_s* g, int B,
+                        bool with_norms) {
+  const int64_t C = d->C, BC = (int64_t)B * C, R = 2 * BC;
+  const int64_t P = (int64_t)g->nlat * g->nlon;
+  const SpecLayout& L = f->spec;
+  b.Xn = cv.take<float2>(BC * f->nlat * f->mmax);
+  b.Xt = cv.take<float>((int64_t)f->mmax * R * f->ldk);
+  b.rs0 = cv.take<float2>(BC * f->nlat);
+  b.sc0 = cv.take<float>(BC);
+  b.sh0 = cv.take<float>(BC);
+  b.Sa = cv.take<float>(R * L.ldT);
+  b.Sb = b.Sc = nullptr;
+  for (auto& w : b.Wexp) w = nullptr;
+  b.xt = b.yt = nullptr;
+  if (d->filter_type == MSFNO_FILTER_NONLINEAR) {
+    const int64_t Hs = d->spec_hidden;
+    b.Sb = cv.take<float>((int64_t)B * 2 * Hs * L.ldT);
+    b.Sc = cv.take<float>((int64_t)B * 2 * Hs * L.ldT);
+    for (int l = 0; l <= d->spectral_layers; ++l) {
+      const int64_t ci = (l == 0) ? C : Hs;
+      const int64_t co = (l == d->spectral_layers) ? C : Hs;
+      b.Wexp[l] = cv.take<float>(4 * ci * co);
+    }
+  } else {
+    b.xt = cv.take<float>(BC * L.T * 2);
+    b.yt = cv.take<float>(BC * L.T * 2);
+  }
+  b.Yt = cv.take<float>((int64_t)g->mmax * R * g->ldk);
+  b.Yn = cv.take<float2>(BC * g->nlat * g->mmax);
+  b.filt = cv.take<float>(BC * P);
+  b.x1 = nullptr;
+  b.st1 = nullptr;
+  b.sc1 = b.sh1 = b.W1f = b.b1f = b.h = nullptr;
+  if (!with_norms) return;
+  b.x1 = cv.take<float>(BC * P);
+  const int64_t np = std::max<int64_t>({cdiv(P, kStatTile), (int64_t)g->nlat, cdiv(P, 1024)});
+  b.st1 = cv.take<float2>(BC * np);
+  b.sc1 = cv.take<float>(BC);
+  b.sh1 = cv.take<float>(BC);
+  if (d->has_mlp) {
+    const int64_t Hd = d->mlp_hidden;
+    b.W1f = cv.take<float>((int64_t)B * Hd * C);
+    b.b1f = cv.take<float>((int64_t)B * Hd);
+    b.h = cv.take<float>((int64_t)B * Hd * P);
+  }
+}
+
+static int check_pair(const msfno_block_desc* d, const msfno_sht_plan_s* f,
+                      const msfno_sht_plan_s* g) {
+  MSFNO_REQUIRE(d && f && g, MSFNO_EINVAL, "null descriptor or plan");
+  MSFNO_REQUIRE(!f->inverse && g->inverse, MSFNO_EINVAL,
+                "forward plan must be a RealSHT plan and inverse an InverseRealSHT plan");
+  MSFNO_REQUIRE(f->lmax == g->lmax && f->mmax == g->mmax, MSFNO_EINVAL,
+                "inverse_transform lmax/mmax must equal forward_transform's (layers.py:364-365)");
+  MSFNO_REQUIRE(f->table_loaded && g->table_loaded, MSFNO_EINVAL, "plan tables not loaded");
+  MSFNO_REQUIRE(d->C > 0, MSFNO_EINVAL, "C must be > 0");
+  if (d->filter_type == MSFNO_FILTER_NONLINEAR) {
+    MSFNO_REQUIRE(d->spectral_layers >= 1 && d->spectral_layers <= 8, MSFNO_EUNSUPPORTED,
+                  "spectral_layers must be in [1, 8]");
+    MSFNO_REQUIRE(d->spec_hidden > 0, MSFNO_EINVAL, "spec_hidden must be > 0");
+  } else {
+    MSFNO_REQUIRE(d->filter_type == MSFNO_FILTER_LINEAR, MSFNO_EUNSUPPORTED, "unknown filter_type");
+  }
+  return MSFNO_OK;
+}
+
+static int run_filter(const msfno_block_desc* d, msfno_sht_plan_s* f, msfno_sht_plan_s* g,
+                      const BlockBufs& b, int B, hipStream_t s) {
+  const int64_t C = d->C;
+  const SpecLayout& L = f->spec;
+  if (d->filter_type == MSFNO_FILTER_NONLINEAR) {
+    const int nl = d->spectral_layers;
+    const int64_t Hs = d->spec_hidden;
+    prof(ST_SPEC_PREP, s);
+    for (int l = 0; l <= nl; ++l) {
+      const int ci = (l == 0) ? (int)C : (int)Hs;
+      const int co = (l == nl) ? (int)C : (int)Hs;
+      const float* w = (l == nl) ? d->spec_wout : d->spec_w[l];
+      MSFNO_REQUIRE(w, MSFNO_EINVAL, "missing spectral weight");
+      MSFNO_TRY(launch_expand_complex_weight(w, b.Wexp[l], ci, co, s));
+    }
+    const float* in = b.Sa;
+    for (int l = 0; l <= nl; ++l) {
+      const int ci = (l == 0) ? (int)C : (int)Hs;
+      const int co = (l == nl) ? (int)C : (int)Hs;
+      float* out = (l == nl) ? b.Sa : ((l & 1) ? b.Sc : b.Sb);
+      prof(l == nl ? ST_SPEC_OUT : ST_SPEC_L0 + std::min(l, 3), s);
+      GemmEpi e;
+      if (l < nl) {  // ComplexReLU(mode="real") on the real rows of each batch block
+        e.relu_period = 2 * co;
+        e.relu_rows = co;
+      }
+      MSFNO_TRY(gemm_uniform(TILE_128x128, b.Wexp[l], in, out, 2 * co, (int)L.Tp, 2 * ci, 2 * ci,
+                             (int)L.ldT, (int)L.ldT, 0, 2LL * ci * L.ldT, 2LL * co * L.ldT, B, e,
+                             s));
+      in = out;
+    }
+  } else {
+    MSFNO_REQUIRE(d->lin_w, MSFNO_EINVAL, "missing linear spectral weight");
+    prof(ST_LIN_GATHER, s);
+    MSFNO_TRY(launch_spec_to_tril(L, b.Sa, b.xt, B, (int)C, f->d_off, s));
+    prof(ST_LIN_CONTRACT, s);
+    MSFNO_TRY(launch_compl_contract(b.xt, d->lin_w, b.yt, B, (int)C, (int)C, L.T, s));
+    prof(ST_LIN_SCATTER, s);
+    MSFNO_TRY(launch_tril_to_spec(L, b.yt, b.Sa, B, (int)C, f->d_off, s));
+  }
+  (void)g;
+  return MSFNO_OK;
+}
+
+// x -> (FFT, norm0 folded) -> Legendre -> filter -> inverse Legendre -> Yn
+static int run_spectral(const msfno_block_desc* d, msfno_sht_plan_s* f, msfno_sht_plan_s* g,
+                        const BlockBufs& b, const float* x, int B, bool norm0, hipStream_t s) {
+  const int64_t C = d->C, BC = (int64_t)B * C, R = 2 * BC;
+  prof(ST_FFT_FWD, s);
+  MSFNO_TRY(launch_fft_r2c_rows(f->fft, x, b.Xn, norm0 ? b.rs0 : nullptr, BC * f->nlat, f->mmax,
+                                (float)(2.0 * M_PI / f->nlon), s));
+  if (norm0) {
+    prof(ST_NORM0, s);
+    MSFNO_TRY(launch_chan_affine(b.rs0, f->nlat, f->nlon, f->nlon, B, (int)C, d->norm0_w,
+                                 d->norm0_b, d->norm_eps, nullptr, nullptr, 0.f, b.sc0, b.sh0, s));
+  }
+  prof(ST_TRANSPOSE_FWD, s);
+  MSFNO_TRY(launch_transpose_fwd(b.Xn, b.Xt, B, (int)C, f->nlat, f->mmax, f->ldk,
+                                 norm0 ? b.sc0 : nullptr, norm0 ? b.sh0 : nullptr, s));
+  prof(ST_LEG_FWD, s);
+  MSFNO_TRY(legendre_fwd(f, b.Xt, b.Sa, (int)R, s));
+  MSFNO_TRY(run_filter(d, f, g, b, B, s));
+  prof(ST_LEG_INV, s);
+  MSFNO_TRY(legendre_inv(g, b.Sa, b.Yt, (int)R, s));
+  prof(ST_TRANSPOSE_INV, s);
+  MSFNO_TRY(launch_transpose_inv(b.Yt, b.Yn, B, (int)C, g->nlat, g->mmax, g->spec.mact, g->ldk, s));
+  return MSFNO_OK;
+}
+
+}  // namespace msfno
+
+using namespace msfno;
+
+extern "C" {
+
+const char* msfno_last_error(void) { return g_last_error.c_str(); }
+int msfno_abi_version(void) { return 1; }
+
+int msfno_quadrature(int nlat, int grid, double* nodes, double* weights) {
+  std::vector<double> x, w;
+  MSFNO_TRY(quadrature(nlat, grid, x, w));
+  std::memcpy(nodes, x.data(), nlat * sizeof(double));
+  std::memcpy(weights, w.data(), nlat * sizeof(double));
+  return MSFNO_OK;
+}
+
+int msfno_legendre_table(int mmax, int lmax, int nlat, int grid, int inverse, int csphase,
+                         double* table) {
+  MSFNO_REQUIRE(mmax > 0 && lmax > 0 && nlat > 0 && table, MSFNO_EINVAL, "bad table arguments");
+  return legendre_table(mmax, lmax, nlat, grid, inverse, csphase, table);
+}
+
+int msfno_sht_plan_create(int nlat, int nlon, int lmax, int mmax, int inverse,
+                          msfno_sht_plan_t* plan) {
+  MSFNO_REQUIRE(plan, MSFNO_EINVAL, "null plan pointer");
+  MSFNO_REQUIRE(nlat > 0 && nlon > 1 && lmax > 0 && mmax > 0, MSFNO_EINVAL, "bad SHT dims");
+  MSFNO_REQUIRE(mmax <= nlon / 2 + 1, MSFNO_EINVAL, "mmax must be <= nlon//2 + 1");
+  auto* p = new msfno_sht_plan_s();
+  p->nlat = nlat; p->nlon = nlon; p->lmax = lmax; p->mmax = mmax; p->inverse = inverse ? 1 : 0;
+  p->ldk = (int)round_up(nlat, 4);
+  p->spec.build(lmax, mmax);
+  int rc = fft_plan_build(p->fft, nlon);
+  if (rc != MSFNO_OK) { delete p; return rc; }
+  p->tab_off.assign(mmax, 0);
+  int64_t acc = 0;
+  for (int m = 0; m < mmax; ++m) {
+    p->tab_off[m] = acc;
+    acc += p->inverse ? (int64_t)p->spec.L[m] * p->ldk : (int64_t)nlat * p->spec.Lp[m];
+  }
+  p->table_elems = acc;
+  hipError_t e = hipMalloc(&p->table, std::max<int64_t>(acc, 4) * sizeof(float));
+  if (e == hipSuccess) e = hipMalloc(&p->d_tab_off, mmax * sizeof(int64_t));
+  if (e == hipSuccess) e = hipMalloc(&p->d_Lp, mmax * sizeof(int));
+  if (e == hipSuccess) e = hipMalloc(&p->d_off, mmax * sizeof(int));
+  if (e == hipSuccess) e = hipMemcpy(p->d_tab_off, p->tab_off.data(), mmax * sizeof(int64_t), hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMemcpy(p->d_Lp, p->spec.Lp.data(), mmax * sizeof(int), hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMemcpy(p->d_off, p->spec.off.data(), mmax * sizeof(int), hipMemcpyHostToDevice);
+  if (e != hipSuccess) {
+    set_error(std::string("plan allocation failed: ") + hipGetErrorString(e));
+    msfno_sht_plan_destroy(p);
+    return MSFNO_EHIP;
+  }
+  *plan = p;
+  return MSFNO_OK;
+}
+
+int msfno_sht_plan_destroy(msfno_sht_plan_t p) {
+  if (!p) return MSFNO_OK;
+  fft_plan_free(p->fft);
+  if (p->table) (void)hipFree(p->table);
+  if (p->d_tab_off) (void)hipFree(p->d_tab_off);
+  if (p->d_Lp) (void)hipFree(p->d_Lp);
+  if (p->d_off) (void)hipFree(p->d_off);
+  if (p->d_desc) (void)hipFree(p->d_desc);
+  delete p;
+  return MSFNO_OK;
+}
+
+int msfno_sht_plan_load_table(msfno_sht_plan_t p, const float* table, void* stream) {
+  MSFNO_REQUIRE(p && table, MSFNO_EINVAL, "null plan or table");
+  MSFNO_TRY(launch_relayout_table(*p, table, (hipStream_t)stream));
+  p->table_loaded = 1;
+  return MSFNO_OK;
+}
+
+size_t msfno_sht_workspace_size(msfno_sht_plan_t p, int bc) {
+  if (!p) return 0;
+  Carve cv;
+  const int64_t R = 2LL * bc;
+  cv.take<float2>((int64_t)bc * p->nlat * p->mmax);   // Xn / Yn
+  cv.take<float>((int64_t)p->mmax * R * p->ldk);       // Xt / Yt
+  cv.take<float>(R * p->spec.ldT);                     // S
+  return cv.off;
+}
+
+int msfno_sht_forward(msfno_sht_plan_t p, const float* x, float* out, int bc, void* ws,
+                      size_t ws_bytes, void* stream) {
+  MSFNO_REQUIRE(p && !p->inverse, MSFNO_EINVAL, "msfno_sht_forward needs a forward plan");
+  MSFNO_REQUIRE(p->table_loaded, MSFNO_EINVAL, "plan table not loaded");
+  MSFNO_REQUIRE(ws_bytes >= msfno_sht_workspace_size(p, bc), MSFNO_EWORKSPACE, "workspace too small");
+  hipStream_t s = (hipStream_t)stream;
+  Carve cv;
+  cv.base = (char*)ws;
+  const int64_t R = 2LL * bc;
+  float2* Xn = cv.take<float2>((int64_t)bc * p->nlat * p->mmax);
+  float* Xt = cv.take<float>((int64_t)p->mmax * R * p->ldk);
+  float* S = cv.take<float>(R * p->spec.ldT);
+  MSFNO_TRY(launch_fft_r2c_rows(p->fft, x, Xn, nullptr, (int64_t)bc * p->nlat, p->mmax,
+                                (float)(2.0 * M_PI / p->nlon), s));
+  MSFNO_TRY(launch_transpose_fwd(Xn, Xt, 1, bc, p->nlat, p->mmax, p->ldk, nullptr, nullptr, s));
+  MSFNO_TRY(legendre_fwd(p, Xt, S, (int)R, s));
+  MSFNO_TRY(launch_spec_to_ref(*p, S, reinterpret_cast<float2*>(out), 1, bc, p->d_off, s));
+  return MSFNO_OK;
+}
+
+int msfno_sht_inverse(msfno_sht_plan_t p, const float* in, float* x, int bc, void* ws,
+                      size_t ws_bytes, void* stream) {
+  MSFNO_REQUIRE(p && p->inverse, MSFNO_EINVAL, "msfno_sht_inverse needs an inverse plan");
+  MSFNO_REQUIRE(p->table_loaded, MSFNO_EINVAL, "plan table not loaded");
+  MSFNO_REQUIRE(ws_bytes >= msfno_sht_workspace_size(p, bc), MSFNO_EWORKSPACE, "workspace too small");
+  hipStream_t s = (hipStream_t)stream;
+  Carve cv;
+  cv.base = (char*)ws;
+  const int64_t R = 2LL * bc;
+  float2* Yn = cv.take<float2>((int64_t)bc * p->nlat * p->mmax);
+  float* Yt = cv.take<float>((int64_t)p->mmax * R * p->ldk);
+  float* S = cv.take<float>(R * p->spec.ldT);
+  MSFNO_TRY(launch_ref_to_spec(*p, reinterpret_cast<const float2*>(in), S, 1, bc, p->d_off, s));
+  MSFNO_TRY(legendre_inv(p, S, Yt, (int)R, s));
+  MSFNO_TRY(launch_transpose_inv(Yt, Yn, 1, bc, p->nlat, p->mmax, p->spec.mact, p->ldk, s));
+  MSFNO_TRY(launch_fft_c2r_rows(p->fft, Yn, x, nullptr, (int64_t)bc * p->nlat, p->mmax, 0, s));
+  return MSFNO_OK;
+}
+
+int msfno_compl_contract_fwd_c(const float* a, const float* w, float* y, int B, int Ci, int Co,
+                               int T, void* stream) {
+  MSFNO_REQUIRE(a && w && y && B > 0 && Ci > 0 && Co > 0 && T > 0, MSFNO_EINVAL,
+                "bad compl_contract_fwd_c arguments");
+  return launch_compl_contract(a, w, y, B, Ci, Co, T, (hipStream_t)stream);
+}
+
+int msfno_compl_mul2d_fwd_c(const float* a, const float* w, float* y, int B, int Ci, int Co,
+                            long long XY, int relu_real, void* stream) {
+  MSFNO_REQUIRE(a && w && y && B > 0 && Ci > 0 && Co > 0 && XY > 0, MSFNO_EINVAL,
+                "bad compl_mul2d_fwd_c arguments");
+  return launch_compl_mul2d(a, w, y, B, Ci, Co, XY, relu_real, (hipStream_t)stream);
+}
+
+size_t msfno_block_workspace_size(const msfno_block_desc* d, msfno_sht_plan_t f,
+                                  msfno_sht_plan_t g, int B) {
+  if (!d || !f || !g) return 0;
+  Carve cv;
+  BlockBufs b;
+  carve_block(cv, b, d, f, g, B, true);
+  return cv.off;
+}
+
+int msfno_filter_forward(const msfno_block_desc* d, msfno_sht_plan_t f, msfno_sht_plan_t g,
+                         const float* x, float* y, int B, void* ws, size_t ws_bytes,
+                         void* stream) {
+  MSFNO_TRY(check_pair(d, f, g));
+  MSFNO_REQUIRE(ws_bytes >= msfno_block_workspace_size(d, f, g, B), MSFNO_EWORKSPACE,
+                "workspace too small");
+  hipStream_t s = (hipStream_t)stream;
+  Carve cv;
+  cv.base = (char*)ws;
+  BlockBufs b;
+  carve_block(cv, b, d, f, g, B, false);
+  MSFNO_TRY(run_spectral(d, f, g, b, x, B, false, s));
+  const int64_t BC = (int64_t)B * d->C;
+  MSFNO_TRY(launch_fft_c2r_rows(g->fft, b.Yn, y, nullptr, BC * g->nlat, g->mmax, 0, s));
+  return MSFNO_OK;
+}
+
+int msfno_block_forward(const msfno_block_desc* d, msfno_sht_plan_t f, msfno_sht_plan_t g,
+                        const float* x, const float* gamma, const float* beta, float film_scale,
+                        float* out, int B, void* ws, size_t ws_bytes, void* stream) {
+  MSFNO_TRY(check_pair(d, f, g));
+  MSFNO_REQUIRE(ws_bytes >= msfno_block_workspace_size(d, f, g, B), MSFNO_EWORKSPACE,
+                "workspace too small");
+  MSFNO_REQUIRE((gamma == nullptr) == (beta == nullptr), MSFNO_EINVAL,
+                "gamma and beta must both be given or both be NULL");
+  MSFNO_REQUIRE(d->outer_skip != MSFNO_SKIP_LINEAR, MSFNO_EUNSUPPORTED,
+                "outer_skip='linear' is not supported by the fused block");
+  const bool resample = (f->nlat != g->nlat) || (f->nlon != g->nlon);
+  MSFNO_REQUIRE(!resample || (d->inner_skip == MSFNO_SKIP_NONE && d->outer_skip == MSFNO_SKIP_NONE),
+                MSFNO_EINVAL, "skips require equal input and output grids");
+  hipStream_t s = (hipStream_t)stream;
+  Carve cv;
+  cv.base = (char*)ws;
+  BlockBufs b;
+  carve_block(cv, b, d, f, g, B, true);
+  const int64_t C = d->C, BC = (int64_t)B * C;
+  const int64_t P = (int64_t)g->nlat * g->nlon;
+  const int act = d->filter_type == MSFNO_FILTER_LINEAR ? 1 : 0;  // GELU after skip (linear only)
+
+  MSFNO_TRY(run_spectral(d, f, g, b, x, B, true, s));
+
+  // ---- inner skip + activation -> x1 (with norm1 partial statistics) -----------
+  int64_t np = 0, cnt = 0, cnt_last = 0;
+  float* x1 = b.x1;
+  prof(ST_FFT_INV, s);
+  if (d->inner_skip == MSFNO_SKIP_NONE) {
+    MSFNO_TRY(launch_fft_c2r_rows(g->fft, b.Yn, x1, b.st1, BC * g->nlat, g->mmax, act, s));
+    np = g->nlat; cnt = cnt_last = g->nlon;
+  } else {
+    MSFNO_TRY(launch_fft_c2r_rows(g->fft, b.Yn, b.filt, nullptr, BC * g->nlat, g->mmax, 0, s));
+    prof(ST_SKIP, s);
+    if (d->inner_skip == MSFNO_SKIP_LINEAR) {
+      MSFNO_REQUIRE(d->skip_w, MSFNO_EINVAL, "missing inner_skip weight");
+      np = cdiv(P, kStatTile);
+      GemmEpi e;
+      e.bias = d->skip_b;
+      e.addend = b.filt; e.sD = C * P; e.ldd = (int)P;
+      e.act = act;
+      e.stats = b.st1; e.sStats = C * np; e.stats_ld = (int)np;
+      MSFNO_TRY(gemm_uniform(TILE_128x128, d->skip_w, x, x1, (int)C, (int)P, (int)C, (int)C,
+                             (int)P, (int)P, 0, C * P, C * P, B, e, s));
+      cnt = kStatTile; cnt_last = P - (np - 1) * kStatTile;
+    } else {
+      np = cdiv(P, 1024);
+      MSFNO_TRY(launch_affine_rows(b.filt, nullptr, nullptr, x, x1, BC, P, act, b.st1, (int)np, s));
+      cnt = 1024; cnt_last = P - (np - 1) * 1024;
+    }
+  }
+  // ---- norm1 (+ FiLM) as a per-(b,c) affine --------------------------------------
+  prof(ST_NORM1, s);
+  MSFNO_TRY(launch_chan_affine(b.st1, np, cnt, cnt_last, B, (int)C, d->norm1_w, d->norm1_b,
+                               d->norm_eps, gamma, beta, film_scale, b.sc1, b.sh1, s));
+  const float* resid = d->outer_skip == MSFNO_SKIP_IDENTITY ? x : nullptr;
+  if (d->has_mlp) {
+    MSFNO_REQUIRE(d->fc1_w && d->fc2_w, MSFNO_EINVAL, "missing MLP weights");
+    const int64_t Hd = d->mlp_hidden;
+    MSFNO_TRY(launch_fold_affine(d->fc1_w, d->fc1_b, b.sc1, b.sh1, b.W1f, b.b1f, B, (int)Hd,
+                                 (int)C, s));
+    prof(ST_FC1, s);
+    GemmEpi e1;
+    e1.bias = b.b1f; e1.sBias = Hd; e1.act = 1;
+    MSFNO_TRY(gemm_uniform(TILE_128x128, b.W1f, x1, b.h, (int)Hd, (int)P, (int)C, (int)C, (int)P,
+                           (int)P, Hd * C, C * P, Hd * P, B, e1, s));
+    prof(ST_FC2, s);
+    GemmEpi e2;
+    e2.bias = d->fc2_b;
+    if (resid) { e2.addend = resid; e2.sD = C * P; e2.ldd = (int)P; }
+    MSFNO_TRY(gemm_uniform(TILE_128x128, d->fc2_w, b.h, out, (int)C, (int)P, (int)Hd, (int)Hd,
+                           (int)P, (int)P, 0, Hd * P, C * P, B, e2, s));
+  } else {
+    prof(ST_OUT_AFFINE, s);
+    MSFNO_TRY(launch_affine_rows(x1, b.sc1, b.sh1, resid, out, BC, P, 0, nullptr, 0, s));
+  }
+  prof(ST_END, s);
+  return MSFNO_OK;
+}
+
+int msfno_profile_enable(int on) {
+  g_prof.on = on != 0;
+  return MSFNO_OK;
+}
+
+const char* msfno_profile_stage_name(int stage) {
+  if (stage < 0 || stage >= MSFNO_PROF_NSTAGES || !kStageNames[stage]) return "";
+  return kStageNames[stage];
+}
+
+int msfno_profile_collect(double* total_ms, int* counts) {
+  auto& mk = g_prof.marks;
+  if (!mk.empty()) MSFNO_CHECK_HIP(hipEventSynchronize(mk.back().second));
+  for (size_t i = 0; i + 1 < mk.size(); ++i) {
+    const int st = mk[i].first;
+    if (st == ST_END) continue;
+    float ms = 0.f;
+    MSFNO_CHECK_HIP(hipEventElapsedTime(&ms, mk[i].second, mk[i + 1].second));
+    if (total_ms) total_ms[st] += ms;
+    if (counts) counts[st] += 1;
+  }
+  for (auto& p : mk) g_prof.pool.push_back(p.second);
+  mk.clear();
+  return MSFNO_OK;
+}
+
+}  // extern "C"

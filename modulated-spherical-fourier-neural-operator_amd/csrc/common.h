@@ -1,0 +1,141 @@
+// Internal helpers shared by the libmsfno translation units (not part of the ABI).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdio>
+#include <string>
+#include <vector>
+
+#include "../../include/msfno.h"
+
+namespace msfno {
+
+void set_error(const std::string& msg);
+
+struct Status {
+  int code = MSFNO_OK;
+};
+
+#define MSFNO_CHECK_HIP(expr)                                                       \
+  do {                                                                              \
+    hipError_t _e = (expr);                                                         \
+    if (_e != hipSuccess) {                                                         \
+      ::msfno::set_error(std::string("HIP error '") + hipGetErrorString(_e) +       \
+                         "' at " + __FILE__ + ":" + std::to_string(__LINE__) +      \
+                         " in " #expr);                                             \
+      return MSFNO_EHIP;                                                            \
+    }                                                                               \
+  } while (0)
+
+#define MSFNO_REQUIRE(cond, code, msg)          \
+  do {                                          \
+    if (!(cond)) {                              \
+      ::msfno::set_error(msg);                  \
+      return (code);                            \
+    }                                           \
+  } while (0)
+
+#define MSFNO_TRY(expr)              \
+  do {                               \
+    int _rc = (expr);                \
+    if (_rc != MSFNO_OK) return _rc; \
+  } while (0)
+
+inline int launch_check(const char* what) {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    set_error(std::string("kernel launch failed (") + what + "): " + hipGetErrorString(e));
+    return MSFNO_EHIP;
+  }
+  return MSFNO_OK;
+}
+
+inline int64_t round_up(int64_t v, int64_t m) { return (v + m - 1) / m * m; }
+inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+// ---------------------------------------------------------------------------
+// Spectral ("S") layout, m-major packed triangle:
+//   row r = (b*2 + ri)*C + c ;  column t = off[m] + (l - m),  l in [m, lmax)
+//   each m block is padded to Lp_m = round_up(lmax-m, 4) columns (zeros).
+// ---------------------------------------------------------------------------
+struct SpecLayout {
+  int lmax = 0, mmax = 0;
+  int mact = 0;                 // number of m with lmax - m > 0
+  std::vector<int> L, Lp, off;  // per m (size mmax)
+  int64_t T = 0;                // number of (l,m) with l>=m (tril count)
+  int64_t Tp = 0;               // total padded columns
+  int64_t ldT = 0;              // row stride of S buffers (multiple of 4)
+  void build(int lmax_, int mmax_);
+};
+
+// ---------------------------------------------------------------------------
+// FFT plan part (longitude transform of length nlon)
+// ---------------------------------------------------------------------------
+constexpr int kMaxRadices = 24;
+struct FFTPlan {
+  int N = 0;         // nlon
+  int H = 0;         // complex length actually transformed (N/2 if packed)
+  int packed = 0;    // real-input packing (N even)
+  int nrad = 0;
+  int radices[kMaxRadices] = {0};
+  float2* twH = nullptr;  // e^{-2πi t/H}, t < H      (device)
+  float2* twN = nullptr;  // e^{-2πi k/N}, k <= N/2   (device)
+};
+int fft_plan_build(FFTPlan& p, int N);
+void fft_plan_free(FFTPlan& p);
+
+// ---------------------------------------------------------------------------
+// Batched GEMM descriptors (per-m Legendre problems)
+// ---------------------------------------------------------------------------
+struct GemmDesc {
+  int64_t offA, offB, offC;
+  int M, N, K;
+  int lda, ldb, ldc;
+  int tiles_m, tiles_n;
+  int tile_start;
+  int pad_;
+};
+
+struct GemmEpi {
+  const float* bias = nullptr;      // per row (batch stride sBias)
+  const float* addend = nullptr;    // matrix, ld = ldd (batch stride sD)
+  float2* stats = nullptr;          // per (row, tile_n) partial (mean, M2) (batch stride sStats)
+  int64_t sBias = 0, sD = 0, sStats = 0;
+  int ldd = 0;
+  int act = 0;                      // 0 none, 1 GELU(erf)
+  int relu_period = 0, relu_rows = 0;  // ReLU rows where (row % period) < relu_rows
+  int stats_ld = 0;                 // partials per row
+};
+
+enum GemmTile { TILE_128x128 = 0, TILE_128x64 = 1, TILE_64x64 = 2 };
+
+// C[M,N] = A[M,K] · B[K,N] (+ epilogue), row-major, fp32 MFMA.
+// Uniform batched mode: batch index = grid.z, operand batch strides sA/sB/sC.
+int gemm_uniform(GemmTile tile, const float* A, const float* B, float* C, int M, int N, int K,
+                 int lda, int ldb, int ldc, int64_t sA, int64_t sB, int64_t sC, int batch,
+                 const GemmEpi& epi, hipStream_t s);
+// Descriptor mode: per-problem dims/offsets from `descs` (device), tiles laid out 1-D.
+int gemm_desc(GemmTile tile, const float* A, const float* B, float* C, const GemmDesc* descs,
+              int ndesc, int total_tiles, const GemmEpi& epi, hipStream_t s);
+void gemm_tile_dims(GemmTile tile, int* bm, int* bn);
+
+}  // namespace msfno
+
+struct msfno_sht_plan_s {
+  int nlat, nlon, lmax, mmax, inverse;
+  int ldk;                       // padded latitude stride (multiple of 4)
+  msfno::SpecLayout spec;
+  msfno::FFTPlan fft;
+  float* table = nullptr;        // device, plan GEMM layout
+  int64_t table_elems = 0;
+  std::vector<int64_t> tab_off;  // per m offsets into table
+  int64_t* d_tab_off = nullptr;  // device copies of the per-m metadata
+  int* d_Lp = nullptr;
+  int* d_off = nullptr;          // S-layout column offsets off[m]
+  int table_loaded = 0;
+  // cached Legendre GEMM descriptors for a given row count R
+  int desc_R = -1;
+  msfno::GemmDesc* d_desc = nullptr;
+  int ndesc = 0, desc_tiles = 0;
+};

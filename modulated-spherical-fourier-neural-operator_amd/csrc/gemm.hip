@@ -1,0 +1,319 @@
+// fp32 MFMA GEMM for gfx950 (v_mfma_f32_32x32x2_f32: exact fp32 fma chain, the
+// chip's fp32 matrix peak).  Used for every dense contraction of the block:
+//   * per-m Legendre contractions of the forward / inverse SHT (descriptor mode),
+//   * the non-linear spectral MLP layers (complex GEMMs real-ified),
+//   * the 1x1 convolutions (inner skip, MLP fc1/fc2) with fused epilogues.
+// C[M,N] = A[M,K]·B[K,N], all row-major fp32.  Block tile BM×BN×16, 4 waves in
+// a 2×2 arrangement, each wave owning (BM/2)×(BN/2) as 32×32 MFMA tiles.
+// LDS is double buffered with one barrier per K-tile; A is staged k-major
+// (transposed) so both MFMA operands are read as conflict-free ds_read_b32.
+#include "common.h"
+
+namespace msfno {
+
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+
+struct GemmParams {
+  const float* A;
+  const float* B;
+  float* C;
+  int M, N, K, lda, ldb, ldc;
+  int64_t sA, sB, sC;
+  int tiles_m, tiles_n;
+  const GemmDesc* descs;
+  int ndesc;
+  int vecA, vecB;
+  // epilogue
+  const float* bias;
+  const float* addend;
+  float2* stats;
+  int64_t sBias, sD, sStats;
+  int ldd, act, relu_period, relu_rows, stats_ld;
+};
+
+__device__ __forceinline__ int xcd_remap(int orig, int nwg) {
+  // bijective: blocks that share an XCD (orig % 8) get contiguous logical ids
+  const int xcd = orig & 7;
+  const int q = nwg >> 3, r = nwg & 7;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
+}
+
+__device__ __forceinline__ float gelu_erf(float v) {
+  return 0.5f * v * (1.0f + erff(v * 0.70710678118654752440f));
+}
+
+constexpr int BK = 16;
+
+template <int BM, int BN>
+__global__ __launch_bounds__(256) void gemm_f32_kernel(GemmParams p) {
+  constexpr int WM = BM / 2, WN = BN / 2;
+  constexpr int MT = WM / 32, NT = WN / 32;
+  constexpr int LDA_S = BM + 2;  // staging-write conflict-free (see header)
+  constexpr int LDB_S = BN;
+  constexpr int A_LD = BM / 64;  // float4 staging loads per thread
+  constexpr int B_LD = BN / 64;
+  __shared__ float As[2][BK * LDA_S];
+  __shared__ float Bs[2][BK * LDB_S];
+  __shared__ float red[2 * BM];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+
+  // ---- tile -> problem mapping ----------------------------------------------
+  const float* A = p.A;
+  const float* B = p.B;
+  float* C = p.C;
+  int M = p.M, N = p.N, K = p.K, lda = p.lda, ldb = p.ldb, ldc = p.ldc;
+  int tm, tn;
+  const float* bias = p.bias;
+  const float* addend = p.addend;
+  float2* stats = p.stats;
+  if (p.descs) {
+    const int lin = xcd_remap(blockIdx.x, gridDim.x);
+    int lo = 0, hi = p.ndesc - 1;
+    while (lo < hi) {  // last desc with tile_start <= lin
+      const int mid = (lo + hi + 1) >> 1;
+      if (p.descs[mid].tile_start <= lin) lo = mid; else hi = mid - 1;
+    }
+    const GemmDesc d = p.descs[lo];
+    A += d.offA; B += d.offB; C += d.offC;
+    M = d.M; N = d.N; K = d.K; lda = d.lda; ldb = d.ldb; ldc = d.ldc;
+    const int local = lin - d.tile_start;
+    tm = local % d.tiles_m;
+    tn = local / d.tiles_m;
+  } else {
+    const int lin = xcd_remap(blockIdx.x, gridDim.x);
+    tm = lin % p.tiles_m;
+    tn = lin / p.tiles_m;
+    const int z = blockIdx.z;
+    A += z * p.sA; B += z * p.sB; C += z * p.sC;
+    if (bias) bias += z * p.sBias;
+    if (addend) addend += z * p.sD;
+    if (stats) stats += z * p.sStats;
+  }
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int nk = (K + BK - 1) / BK;
+
+  if (stats && tid < BM) { red[tid] = 0.f; red[BM + tid] = 0.f; }
+
+  float4 ra[A_LD], rb[B_LD];
+
+  auto load_tile = [&](int kt) {
+    const int k0 = kt * BK;
+#pragma unroll
+    for (int q = 0; q < A_LD; ++q) {
+      const int idx = tid + 256 * q;
+      const int row = m0 + idx / 4;
+      const int k = k0 + (idx % 4) * 4;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (row < M) {
+        const float* src = A + (int64_t)row * lda + k;
+        if (p.vecA && k + 3 < K) {
+          v = *reinterpret_cast<const float4*>(src);
+        } else {
+          if (k + 0 < K) v.x = src[0];
+          if (k + 1 < K) v.y = src[1];
+          if (k + 2 < K) v.z = src[2];
+          if (k + 3 < K) v.w = src[3];
+        }
+      }
+      ra[q] = v;
+    }
+#pragma unroll
+    for (int q = 0; q < B_LD; ++q) {
+      const int idx = tid + 256 * q;
+      const int kr = k0 + idx / (BN / 4);
+      const int col = n0 + (idx % (BN / 4)) * 4;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (kr < K) {
+        const float* src = B + (int64_t)kr * ldb + col;
+        if (p.vecB && col + 3 < N) {
+          v = *reinterpret_cast<const float4*>(src);
+        } else {
+          if (col + 0 < N) v.x = src[0];
+          if (col + 1 < N) v.y = src[1];
+          if (col + 2 < N) v.z = src[2];
+          if (col + 3 < N) v.w = src[3];
+        }
+      }
+      rb[q] = v;
+    }
+  };
+  auto store_tile = [&](int buf) {
+#pragma unroll
+    for (int q = 0; q < A_LD; ++q) {
+      const int idx = tid + 256 * q;
+      const int row = idx / 4;
+      const int k = (idx % 4) * 4;
+      float* dst = &As[buf][k * LDA_S + row];
+      dst[0] = ra[q].x;
+      dst[LDA_S] = ra[q].y;
+      dst[2 * LDA_S] = ra[q].z;
+      dst[3 * LDA_S] = ra[q].w;
+    }
+#pragma unroll
+    for (int q = 0; q < B_LD; ++q) {
+      const int idx = tid + 256 * q;
+      const int kr = idx / (BN / 4);
+      const int col = (idx % (BN / 4)) * 4;
+      *reinterpret_cast<float4*>(&Bs[buf][kr * LDB_S + col]) = rb[q];
+    }
+  };
+
+  floatx16 acc[MT][NT];
+#pragma unroll
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int j = 0; j < NT; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  if (nk > 0) {
+    load_tile(0);
+    store_tile(0);
+  }
+  __syncthreads();
+  const int half = lane >> 5;
+  const int l32 = lane & 31;
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) load_tile(kt + 1);
+    const float* as = &As[cur][0];
+    const float* bs = &Bs[cur][0];
+#pragma unroll
+    for (int kk = 0; kk < BK / 2; ++kk) {
+      const int k = 2 * kk + half;
+      float a[MT], b[NT];
+#pragma unroll
+      for (int i = 0; i < MT; ++i) a[i] = as[k * LDA_S + wm * WM + i * 32 + l32];
+#pragma unroll
+      for (int j = 0; j < NT; ++j) b[j] = bs[k * LDB_S + wn * WN + j * 32 + l32];
+#pragma unroll
+      for (int i = 0; i < MT; ++i)
+#pragma unroll
+        for (int j = 0; j < NT; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i], b[j], acc[i][j], 0, 0, 0);
+    }
+    if (kt + 1 < nk) store_tile(cur ^ 1);
+    __syncthreads();
+  }
+
+  // ---- epilogue ---------------------------------------------------------------
+  const bool do_stats = stats != nullptr;
+#pragma unroll
+  for (int i = 0; i < MT; ++i) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int lrow = wm * WM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
+      const int row = m0 + lrow;
+      float s = 0.f, sq = 0.f;
+#pragma unroll
+      for (int j = 0; j < NT; ++j) {
+        const int col = n0 + wn * WN + j * 32 + l32;
+        float v = acc[i][j][r];
+        const bool ok = row < M && col < N;
+        if (ok) {
+          if (bias) v += bias[row];
+          if (addend) v += addend[(int64_t)row * p.ldd + col];
+          if (p.act == 1) v = gelu_erf(v);
+          if (p.relu_period && (row % p.relu_period) < p.relu_rows) v = fmaxf(v, 0.f);
+          C[(int64_t)row * ldc + col] = v;
+          s += v;
+          sq += v * v;
+        }
+      }
+      if (do_stats) {
+#pragma unroll
+        for (int o = 1; o < 32; o <<= 1) {
+          s += __shfl_xor(s, o);
+          sq += __shfl_xor(sq, o);
+        }
+        if (l32 == 0) {
+          atomicAdd(&red[lrow], s);
+          atomicAdd(&red[BM + lrow], sq);
+        }
+      }
+    }
+  }
+  if (do_stats) {
+    __syncthreads();
+    if (tid < BM) {
+      const int row = m0 + tid;
+      if (row < M) {
+        const float n = (float)min(BN, N - n0);
+        const float sm = red[tid];
+        const float mean = sm / n;
+        const float m2 = fmaxf(red[BM + tid] - sm * mean, 0.f);
+        stats[(int64_t)row * p.stats_ld + tn] = make_float2(mean, m2);
+      }
+    }
+  }
+}
+
+void gemm_tile_dims(GemmTile tile, int* bm, int* bn) {
+  switch (tile) {
+    case TILE_128x128: *bm = 128; *bn = 128; break;
+    case TILE_128x64: *bm = 128; *bn = 64; break;
+    default: *bm = 64; *bn = 64; break;
+  }
+}
+
+static GemmParams make_params(const float* A, const float* B, float* C, const GemmEpi& e) {
+  GemmParams p{};
+  p.A = A; p.B = B; p.C = C;
+  p.bias = e.bias; p.addend = e.addend; p.stats = e.stats;
+  p.sBias = e.sBias; p.sD = e.sD; p.sStats = e.sStats;
+  p.ldd = e.ldd; p.act = e.act; p.relu_period = e.relu_period; p.relu_rows = e.relu_rows;
+  p.stats_ld = e.stats_ld;
+  return p;
+}
+
+template <int BM, int BN>
+static void launch(const GemmParams& p, dim3 grid, hipStream_t s) {
+  hipLaunchKernelGGL((gemm_f32_kernel<BM, BN>), grid, dim3(256), 0, s, p);
+}
+
+static int dispatch(GemmTile tile, const GemmParams& p, dim3 grid, hipStream_t s) {
+  switch (tile) {
+    case TILE_128x128: launch<128, 128>(p, grid, s); break;
+    case TILE_128x64: launch<128, 64>(p, grid, s); break;
+    default: launch<64, 64>(p, grid, s); break;
+  }
+  return launch_check("gemm_f32");
+}
+
+static bool aligned16(const void* ptr) { return (reinterpret_cast<uintptr_t>(ptr) & 15) == 0; }
+
+int gemm_uniform(GemmTile tile, const float* A, const float* B, float* C, int M, int N, int K,
+                 int lda, int ldb, int ldc, int64_t sA, int64_t sB, int64_t sC, int batch,
+                 const GemmEpi& epi, hipStream_t s) {
+  if (M <= 0 || N <= 0 || batch <= 0) return MSFNO_OK;
+  int bm, bn;
+  gemm_tile_dims(tile, &bm, &bn);
+  GemmParams p = make_params(A, B, C, epi);
+  p.M = M; p.N = N; p.K = K; p.lda = lda; p.ldb = ldb; p.ldc = ldc;
+  p.sA = sA; p.sB = sB; p.sC = sC;
+  p.tiles_m = (int)cdiv(M, bm);
+  p.tiles_n = (int)cdiv(N, bn);
+  p.vecA = (lda % 4 == 0) && (sA % 4 == 0) && aligned16(A);
+  p.vecB = (ldb % 4 == 0) && (sB % 4 == 0) && aligned16(B);
+  MSFNO_REQUIRE(batch <= 65535, MSFNO_EINVAL, "gemm: batch too large");
+  dim3 grid(p.tiles_m * p.tiles_n, 1, batch);
+  return dispatch(tile, p, grid, s);
+}
+
+int gemm_desc(GemmTile tile, const float* A, const float* B, float* C, const GemmDesc* descs,
+              int ndesc, int total_tiles, const GemmEpi& epi, hipStream_t s) {
+  if (total_tiles <= 0) return MSFNO_OK;
+  GemmParams p = make_params(A, B, C, epi);
+  p.descs = descs;
+  p.ndesc = ndesc;
+  // descriptor problems are laid out with lda/ldb/offsets that are multiples of 4
+  p.vecA = aligned16(A);
+  p.vecB = aligned16(B);
+  return dispatch(tile, p, dim3(total_tiles), s);
+}
+
+}  // namespace msfno

@@ -1,0 +1,60 @@
+// Internal launcher declarations (host-callable, stream-ordered).
+#pragma once
+#include "common.h"
+
+namespace msfno {
+
+// ---- fft.hip ----------------------------------------------------------------
+// x (rows, N) fp32 -> out (rows, mmax) complex, scaled by `scale`; optional
+// per-row (mean, M2) over the N inputs.
+int launch_fft_r2c_rows(const FFTPlan& f, const float* x, float2* out, float2* rowstats,
+                        int64_t rows, int mmax, float scale, hipStream_t s);
+// in (rows, mmax) complex (Hermitian half spectrum, zero beyond mmax) -> x (rows, N);
+// act: 0 none, 1 GELU; optional per-row (mean, M2) of the outputs.
+int launch_fft_c2r_rows(const FFTPlan& f, const float2* in, float* x, float2* rowstats,
+                        int64_t rows, int mmax, int act, hipStream_t s);
+
+// ---- spectral.hip ------------------------------------------------------------
+// Xn (BC, nlat, mmax) complex -> Xt (mmax, R=2BC, ldk); per-bc affine of the
+// spatial field folded in: m>0 -> s·X, m=0 -> s·X + 2π·t (real part).
+int launch_transpose_fwd(const float2* Xn, float* Xt, int B, int C, int nlat, int mmax, int ldk,
+                         const float* nscale, const float* nshift, hipStream_t s);
+// Yt (mmax, R, ldk) -> Yn (BC, nlat, mmax); m >= mact written as 0.
+int launch_transpose_inv(const float* Yt, float2* Yn, int B, int C, int nlat, int mmax, int mact,
+                         int ldk, hipStream_t s);
+// Combine per-(bc) partial (mean, M2) statistics (np partials, each over `cnt`
+// elements except the last over `cnt_last`) and produce the affine that
+// implements InstanceNorm (+ optional FiLM): y = scale·x + shift.
+int launch_chan_affine(const float2* partials, int64_t np, int64_t cnt, int64_t cnt_last,
+                       int B, int C, const float* w, const float* b, float eps,
+                       const float* gamma, const float* beta, float film_scale, float* scale,
+                       float* shift, hipStream_t s);
+// W' [b] = W·diag(scale[b]),  b'[b] = bias + W·shift[b]
+int launch_fold_affine(const float* W, const float* bias, const float* scale, const float* shift,
+                       float* Wf, float* bf, int B, int O, int I, hipStream_t s);
+// out[bc][p] = act(scale[bc]·x[bc][p] + shift[bc] + addend[bc][p]) with optional stats
+int launch_affine_rows(const float* x, const float* scale, const float* shift,
+                       const float* addend, float* out, int64_t BC, int64_t P, int act,
+                       float2* stats, int stats_ld, hipStream_t s);
+// complex (Ci,Co,2) weight -> real (2Co x 2Ci) block matrix [[Wr^T,-Wi^T],[Wi^T,Wr^T]]
+int launch_expand_complex_weight(const float* w, float* Wexp, int Ci, int Co, hipStream_t s);
+// (mmax,lmax,nlat) reference table -> plan GEMM layout
+int launch_relayout_table(const msfno_sht_plan_s& p, const float* table, hipStream_t s);
+// S layout <-> reference (bc, lmax, mmax) complex dense
+int launch_spec_to_ref(const msfno_sht_plan_s& p, const float* S, float2* out, int B, int C,
+                       const int* d_off, hipStream_t s);
+int launch_ref_to_spec(const msfno_sht_plan_s& p, const float2* in, float* S, int B, int C,
+                       const int* d_off, hipStream_t s);
+// S layout <-> tril (B,C,T,2) (torch.tril_indices(lmax,mmax) order, layers.py:368)
+int launch_spec_to_tril(const SpecLayout& L, const float* S, float* xt, int B, int C,
+                        const int* d_off, hipStream_t s);
+int launch_tril_to_spec(const SpecLayout& L, const float* yt, float* S, int B, int C,
+                        const int* d_off, hipStream_t s);
+// compl_contract_fwd_c: a (B,Ci,T,2), w (Co,Ci,T,2) -> y (B,Co,T,2)
+int launch_compl_contract(const float* a, const float* w, float* y, int B, int Ci, int Co,
+                          int64_t T, hipStream_t s);
+// compl_mul2d_fwd_c reference layout (standalone op)
+int launch_compl_mul2d(const float* a, const float* w, float* y, int B, int Ci, int Co,
+                       int64_t XY, int relu_real, hipStream_t s);
+
+}  // namespace msfno

@@ -1,0 +1,623 @@
+// Layout, statistics and streaming kernels around the Legendre/spectral GEMMs:
+//   * Xn <-> Xt transposes (natural per-row spectrum <-> m-major GEMM operand),
+//     with InstanceNorm-0 folded into the forward one,
+//   * InstanceNorm statistics combination (Chan/Welford in fp64) + FiLM fold,
+//   * weight preparation (complex block expansion, norm/FiLM folding into fc1),
+//   * the linear filter's per-mode complex contraction (HBM weight stream),
+//   * S-layout conversions (reference dense (l,m) / torch.tril_indices order).
+#include "kernels.h"
+
+namespace msfno {
+
+constexpr float kTwoPi = 6.28318530717958647692f;
+
+// ---------------------------------------------------------------------------
+// transposes
+// ---------------------------------------------------------------------------
+constexpr int TK = 64, TMM = 32;
+
+__global__ __launch_bounds__(256) void transpose_fwd_kernel(const float2* __restrict__ Xn,
+                                                            float* __restrict__ Xt, int B, int C,
+                                                            int nlat, int mmax, int ldk,
+                                                            const float* __restrict__ nscale,
+                                                            const float* __restrict__ nshift) {
+  __shared__ float2 tile[TMM][TK + 1];
+  const int k0 = blockIdx.x * TK, m0 = blockIdx.y * TMM;
+  const int bc = blockIdx.z;
+  const int b = bc / C, c = bc - b * C;
+  const float2* src = Xn + (int64_t)bc * nlat * mmax;
+  for (int i = threadIdx.x; i < TK * TMM; i += 256) {
+    const int kk = i / TMM, mm = i - kk * TMM;
+    const int k = k0 + kk, m = m0 + mm;
+    float2 v = make_float2(0.f, 0.f);
+    if (k < nlat && m < mmax) v = src[(int64_t)k * mmax + m];
+    tile[mm][kk] = v;
+  }
+  __syncthreads();
+  const float sc = nscale ? nscale[bc] : 1.f;
+  const float sh = nshift ? nshift[bc] * kTwoPi : 0.f;
+  const int64_t R = 2LL * B * C;
+  const int64_t rre = (int64_t)(b * 2 + 0) * C + c;
+  const int64_t rim = (int64_t)(b * 2 + 1) * C + c;
+  for (int i = threadIdx.x; i < TK * TMM; i += 256) {
+    const int mm = i / TK, kk = i - mm * TK;
+    const int k = k0 + kk, m = m0 + mm;
+    if (k < nlat && m < mmax) {
+      float2 v = tile[mm][kk];
+      v.x = v.x * sc + (m == 0 ? sh : 0.f);
+      v.y = v.y * sc;
+      float* dst = Xt + (int64_t)m * R * ldk;
+      dst[rre * ldk + k] = v.x;
+      dst[rim * ldk + k] = v.y;
+    }
+  }
+}
+
+int launch_transpose_fwd(const float2* Xn, float* Xt, int B, int C, int nlat, int mmax, int ldk,
+                         const float* nscale, const float* nshift, hipStream_t s) {
+  dim3 grid((unsigned)cdiv(nlat, TK), (unsigned)cdiv(mmax, TMM), (unsigned)(B * C));
+  hipLaunchKernelGGL(transpose_fwd_kernel, grid, dim3(256), 0, s, Xn, Xt, B, C, nlat, mmax, ldk,
+                     nscale, nshift);
+  return launch_check("transpose_fwd");
+}
+
+__global__ __launch_bounds__(256) void transpose_inv_kernel(const float* __restrict__ Yt,
+                                                            float2* __restrict__ Yn, int B, int C,
+                                                            int nlat, int mmax, int mact,
+                                                            int ldk) {
+  __shared__ float2 tile[TMM][TK + 1];
+  const int k0 = blockIdx.x * TK, m0 = blockIdx.y * TMM;
+  const int bc = blockIdx.z;
+  const int b = bc / C, c = bc - b * C;
+  const int64_t R = 2LL * B * C;
+  const int64_t rre = (int64_t)(b * 2 + 0) * C + c;
+  const int64_t rim = (int64_t)(b * 2 + 1) * C + c;
+  for (int i = threadIdx.x; i < TK * TMM; i += 256) {
+    const int mm = i / TK, kk = i - mm * TK;
+    const int k = k0 + kk, m = m0 + mm;
+    float2 v = make_float2(0.f, 0.f);
+    if (k < nlat && m < mact) {
+      const float* src = Yt + (int64_t)m * R * ldk;
+      v = make_float2(src[rre * ldk + k], src[rim * ldk + k]);
+    }
+    tile[mm][kk] = v;
+  }
+  __syncthreads();
+  float2* dst = Yn + (int64_t)bc * nlat * mmax;
+  for (int i = threadIdx.x; i < TK * TMM; i += 256) {
+    const int kk = i / TMM, mm = i - kk * TMM;
+    const int k = k0 + kk, m = m0 + mm;
+    if (k < nlat && m < mmax) dst[(int64_t)k * mmax + m] = tile[mm][kk];
+  }
+}
+
+int launch_transpose_inv(const float* Yt, float2* Yn, int B, int C, int nlat, int mmax, int mact,
+                         int ldk, hipStream_t s) {
+  dim3 grid((unsigned)cdiv(nlat, TK), (unsigned)cdiv(mmax, TMM), (unsigned)(B * C));
+  hipLaunchKernelGGL(transpose_inv_kernel, grid, dim3(256), 0, s, Yt, Yn, B, C, nlat, mmax, mact,
+                     ldk);
+  return launch_check("transpose_inv");
+}
+
+// ---------------------------------------------------------------------------
+// statistics: combine (mean, M2) partials per channel, fp64 (Chan et al.)
+// ---------------------------------------------------------------------------
+struct Welford {
+  double n, mean, m2;
+};
+__device__ __forceinline__ Welford wcombine(Welford a, Welford b) {
+  if (b.n == 0) return a;
+  if (a.n == 0) return b;
+  const double n = a.n + b.n;
+  const double d = b.mean - a.mean;
+  Welford r;
+  r.n = n;
+  r.mean = a.mean + d * (b.n / n);
+  r.m2 = a.m2 + b.m2 + d * d * (a.n * b.n / n);
+  return r;
+}
+
+__global__ __launch_bounds__(256) void chan_affine_kernel(
+    const float2* __restrict__ part, int64_t np, int64_t cnt, int64_t cnt_last, int C,
+    const float* __restrict__ w, const float* __restrict__ bsh, float eps,
+    const float* __restrict__ gamma, const float* __restrict__ beta, float film_scale,
+    float* __restrict__ scale, float* __restrict__ shift) {
+  __shared__ double sn[256], smean[256], sm2[256];
+  const int bc = blockIdx.x;
+  const int c = bc % C;
+  const float2* p = part + (int64_t)bc * np;
+  Welford acc{0.0, 0.0, 0.0};
+  for (int64_t i = threadIdx.x; i < np; i += 256) {
+    const float2 v = p[i];
+    Welford x{(double)(i == np - 1 ? cnt_last : cnt), (double)v.x, (double)v.y};
+    acc = wcombine(acc, x);
+  }
+  sn[threadIdx.x] = acc.n;
+  smean[threadIdx.x] = acc.mean;
+  sm2[threadIdx.x] = acc.m2;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) {
+      Welford a{sn[threadIdx.x], smean[threadIdx.x], sm2[threadIdx.x]};
+      Welford b{sn[threadIdx.x + o], smean[threadIdx.x + o], sm2[threadIdx.x + o]};
+      a = wcombine(a, b);
+      sn[threadIdx.x] = a.n;
+      smean[threadIdx.x] = a.mean;
+      sm2[threadIdx.x] = a.m2;
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    const double var = sm2[0] / sn[0];  // biased, as InstanceNorm
+    const double rstd = 1.0 / sqrt(var + (double)eps);
+    const double mu = smean[0];
+    double sc = (w ? (double)w[c] : 1.0) * rstd;
+    double sh = (bsh ? (double)bsh[c] : 0.0) - sc * mu;
+    if (gamma) {  // FiLM: (1 + γ·s)·x̂ + β·s   (sfnonet.py:694-697)
+      const double g = 1.0 + (double)gamma[bc] * (double)film_scale;
+      sc *= g;
+      sh = sh * g + (double)beta[bc] * (double)film_scale;
+    }
+    scale[bc] = (float)sc;
+    shift[bc] = (float)sh;
+  }
+}
+
+int launch_chan_affine(const float2* partials, int64_t np, int64_t cnt, int64_t cnt_last, int B,
+                       int C, const float* w, const float* b, float eps, const float* gamma,
+                       const float* beta, float film_scale, float* scale, float* shift,
+                       hipStream_t s) {
+  hipLaunchKernelGGL(chan_affine_kernel, dim3(B * C), dim3(256), 0, s, partials, np, cnt,
+                     cnt_last, C, w, b, eps, gamma, beta, film_scale, scale, shift);
+  return launch_check("chan_affine");
+}
+
+// W'[b][o][i] = W[o][i]·scale[b][i];  b'[b][o] = bias[o] + Σ_i W[o][i]·shift[b][i]
+__global__ __launch_bounds__(256) void fold_affine_kernel(const float* __restrict__ W,
+                                                          const float* __restrict__ bias,
+                                                          const float* __restrict__ scale,
+                                                          const float* __restrict__ shift,
+                                                          float* __restrict__ Wf,
+                                                          float* __restrict__ bf, int O, int I) {
+  __shared__ float red[256];
+  const int o = blockIdx.x, b = blockIdx.y;
+  const float* wr = W + (int64_t)o * I;
+  float* wo = Wf + ((int64_t)b * O + o) * I;
+  const float* sc = scale + (int64_t)b * I;
+  const float* sh = shift + (int64_t)b * I;
+  float acc = 0.f;
+  for (int i = threadIdx.x; i < I; i += 256) {
+    const float wv = wr[i];
+    wo[i] = wv * sc[i];
+    acc += wv * sh[i];
+  }
+  red[threadIdx.x] = acc;
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if ((int)threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) bf[(int64_t)b * O + o] = (bias ? bias[o] : 0.f) + red[0];
+}
+
+int launch_fold_affine(const float* W, const float* bias, const float* scale, const float* shift,
+                       float* Wf, float* bf, int B, int O, int I, hipStream_t s) {
+  hipLaunchKernelGGL(fold_affine_kernel, dim3(O, B), dim3(256), 0, s, W, bias, scale, shift, Wf,
+                     bf, O, I);
+  return launch_check("fold_affine");
+}
+
+__device__ __forceinline__ float gelu_erf(float v) {
+  return 0.5f * v * (1.0f + erff(v * 0.70710678118654752440f));
+}
+
+// one block-row of 1024 elements per workgroup; stats partial per (bc, tile)
+__global__ __launch_bounds__(256) void affine_rows_kernel(
+    const float* __restrict__ x, const float* __restrict__ scale, const float* __restrict__ shift,
+    const float* __restrict__ addend, float* __restrict__ out, int64_t P, int act,
+    float2* __restrict__ stats, int stats_ld) {
+  __shared__ float rs[256], rq[256];
+  const int64_t bc = blockIdx.y;
+  const int64_t p0 = (int64_t)blockIdx.x * 1024;
+  const float sc = scale ? scale[bc] : 1.f;
+  const float sh = shift ? shift[bc] : 0.f;
+  const float* xr = x + bc * P;
+  const float* ar = addend ? addend + bc * P : nullptr;
+  float* orow = out + bc * P;
+  float s = 0.f, q = 0.f;
+  for (int i = threadIdx.x; i < 1024; i += 256) {
+    const int64_t p = p0 + i;
+    if (p < P) {
+      float v = xr[p] * sc + sh;
+      if (ar) v += ar[p];
+      if (act == 1) v = gelu_erf(v);
+      orow[p] = v;
+      s += v;
+      q += v * v;
+    }
+  }
+  if (!stats) return;
+  rs[threadIdx.x] = s;
+  rq[threadIdx.x] = q;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) {
+      rs[threadIdx.x] += rs[threadIdx.x + o];
+      rq[threadIdx.x] += rq[threadIdx.x + o];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    const float n = (float)min((int64_t)1024, P - p0);
+    const float mean = rs[0] / n;
+    stats[bc * stats_ld + blockIdx.x] = make_float2(mean, fmaxf(rq[0] - rs[0] * mean, 0.f));
+  }
+}
+
+int launch_affine_rows(const float* x, const float* scale, const float* shift,
+                       const float* addend, float* out, int64_t BC, int64_t P, int act,
+                       float2* stats, int stats_ld, hipStream_t s) {
+  dim3 grid((unsigned)cdiv(P, 1024), (unsigned)BC);
+  hipLaunchKernelGGL(affine_rows_kernel, grid, dim3(256), 0, s, x, scale, shift, addend, out, P,
+                     act, stats, stats_ld);
+  return launch_check("affine_rows");
+}
+
+// ---------------------------------------------------------------------------
+// weight preparation
+// ---------------------------------------------------------------------------
+__global__ void expand_complex_weight_kernel(const float* __restrict__ w, float* __restrict__ We,
+                                             int Ci, int Co) {
+  const int64_t n = 4LL * Ci * Co;
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < n;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t row = e / (2 * Ci), col = e - row * (2 * Ci);
+    const int ro = (int)(row / Co), o = (int)(row - (int64_t)ro * Co);
+    const int ri = (int)(col / Ci), i = (int)(col - (int64_t)ri * Ci);
+    const float wr = w[((int64_t)i * Co + o) * 2 + 0];
+    const float wi = w[((int64_t)i * Co + o) * 2 + 1];
+    float v;
+    if (ro == 0) v = (ri == 0) ? wr : -wi;   // Re y = Σ xr·wr − xi·wi
+    else v = (ri == 0) ? wi : wr;            // Im y = Σ xr·wi + xi·wr
+    We[e] = v;
+  }
+}
+
+int launch_expand_complex_weight(const float* w, float* Wexp, int Ci, int Co, hipStream_t s) {
+  const int64_t n = 4LL * Ci * Co;
+  hipLaunchKernelGGL(expand_complex_weight_kernel, dim3((unsigned)std::min<int64_t>(cdiv(n, 256), 4096)),
+                     dim3(256), 0, s, w, Wexp, Ci, Co);
+  return launch_check("expand_complex_weight");
+}
+
+// forward table:  Wf[m][k][j] = weights[m][m+j][k]   (ld Lp_m, zero pad j >= L_m)
+// inverse table:  Pi[m][j][k] = pct[m][m+j][k]       (ld ldk,  zero pad k >= nlat)
+__global__ void relayout_table_kernel(const float* __restrict__ tab, float* __restrict__ out,
+                                      const int64_t* __restrict__ tab_off,
+                                      const int* __restrict__ Lp, int lmax, int nlat, int ldk,
+                                      int inverse) {
+  const int m = blockIdx.y;
+  const int L = lmax - m;
+  if (L <= 0) return;
+  const int lp = Lp[m];
+  float* o = out + tab_off[m];
+  const int64_t n = inverse ? (int64_t)L * ldk : (int64_t)nlat * lp;
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < n;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    float v = 0.f;
+    if (inverse) {
+      const int j = (int)(e / ldk), k = (int)(e - (int64_t)j * ldk);
+      if (k < nlat) v = tab[((int64_t)m * lmax + (m + j)) * nlat + k];
+    } else {
+      const int k = (int)(e / lp), j = (int)(e - (int64_t)k * lp);
+      if (j < L) v = tab[((int64_t)m * lmax + (m + j)) * nlat + k];
+    }
+    o[e] = v;
+  }
+}
+
+int launch_relayout_table(const msfno_sht_plan_s& p, const float* table, hipStream_t s) {
+  dim3 grid(256, (unsigned)p.mmax);
+  hipLaunchKernelGGL(relayout_table_kernel, grid, dim3(256), 0, s, table, p.table, p.d_tab_off,
+                     p.d_Lp, p.lmax, p.nlat, p.ldk, p.inverse);
+  return launch_check("relayout_table");
+}
+
+// ---------------------------------------------------------------------------
+// S layout conversions
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ int find_m(const int* off, int mact, int64_t t) {
+  int lo = 0, hi = mact - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (off[mid] <= t) lo = mid; else hi = mid - 1;
+  }
+  return lo;
+}
+
+// out (bc, lmax, mmax) complex dense (zeros where l < m)
+__global__ void spec_to_ref_kernel(const float* __restrict__ S, float2* __restrict__ out, int B,
+                                   int C, int lmax, int mmax, int mact, int64_t ldT,
+                                   const int* __restrict__ off) {
+  const int64_t n = (int64_t)B * C * lmax * mmax;
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < n;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const int m = (int)(e % mmax);
+    const int l = (int)((e / mmax) % lmax);
+    const int64_t bc = e / ((int64_t)mmax * lmax);
+    const int b = (int)(bc / C), c = (int)(bc % C);
+    float2 v = make_float2(0.f, 0.f);
+    if (l >= m && m < mact) {
+      const int64_t t = off[m] + (l - m);
+      v.x = S[((int64_t)(b * 2 + 0) * C + c) * ldT + t];
+      v.y = S[((int64_t)(b * 2 + 1) * C + c) * ldT + t];
+    }
+    out[e] = v;
+  }
+}
+
+int launch_spec_to_ref(const msfno_sht_plan_s& p, const float* S, float2* out, int B, int C,
+                       const int* d_off, hipStream_t s) {
+  const int64_t n = (int64_t)B * C * p.lmax * p.mmax;
+  hipLaunchKernelGGL(spec_to_ref_kernel, dim3((unsigned)std::min<int64_t>(cdiv(n, 256), 65535)),
+                     dim3(256), 0, s, S, out, B, C, p.lmax, p.mmax, p.spec.mact, p.spec.ldT,
+                     d_off);
+  return launch_check("spec_to_ref");
+}
+
+__global__ void ref_to_spec_kernel(const float2* __restrict__ in, float* __restrict__ S, int B,
+                                   int C, int lmax, int mmax, int mact, int64_t Tp, int64_t ldT,
+                                   const int* __restrict__ off) {
+  const int64_t n = (int64_t)B * C * Tp;
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < n;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t t = e % Tp;
+    const int64_t bc = e / Tp;
+    const int b = (int)(bc / C), c = (int)(bc % C);
+    const int m = find_m(off, mact, t);
+    const int l = m + (int)(t - off[m]);
+    float2 v = make_float2(0.f, 0.f);
+    if (l < lmax) v = in[(bc * lmax + l) * mmax + m];
+    S[((int64_t)(b * 2 + 0) * C + c) * ldT + t] = v.x;
+    S[((int64_t)(b * 2 + 1) * C + c) * ldT + t] = v.y;
+  }
+}
+
+int launch_ref_to_spec(const msfno_sht_plan_s& p, const float2* in, float* S, int B, int C,
+                       const int* d_off, hipStream_t s) {
+  const int64_t n = (int64_t)B * C * p.spec.Tp;
+  hipLaunchKernelGGL(ref_to_spec_kernel, dim3((unsigned)std::min<int64_t>(cdiv(n, 256), 65535)),
+                     dim3(256), 0, s, in, S, B, C, p.lmax, p.mmax, p.spec.mact, p.spec.Tp,
+                     p.spec.ldT, d_off);
+  return launch_check("ref_to_spec");
+}
+
+// tril order (torch.tril_indices(lmax, mmax)): row l holds m = 0..min(l, mmax-1)
+__device__ __forceinline__ int64_t tril_row_off(int l, int mmax) {
+  if (l <= mmax) return (int64_t)l * (l + 1) / 2;
+  return (int64_t)mmax * (mmax + 1) / 2 + (int64_t)(l - mmax) * mmax;
+}
+
+// S -> xt (B, C, T, 2);  one thread per (bc, t) of the S row (coalesced reads)
+__global__ void spec_to_tril_kernel(const float* __restrict__ S, float* __restrict__ xt, int B,
+                                    int C, int lmax, int mmax, int mact, int64_t Tp, int64_t T,
+                                    int64_t ldT, const int* __restrict__ off) {
+  const int64_t n = (int64_t)B * C * Tp;
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < n;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t t = e % Tp;
+    const int64_t bc = e / Tp;
+    const int b = (int)(bc / C), c = (int)(bc % C);
+    const int m = find_m(off, mact, t);
+    const int l = m + (int)(t - off[m]);
+    if (l >= lmax) continue;
+    const int64_t nn = tril_row_off(l, mmax) + m;
+    const float re = S[((int64_t)(b * 2 + 0) * C + c) * ldT + t];
+    const float im = S[((int64_t)(b * 2 + 1) * C + c) * ldT + t];
+    reinterpret_cast<float2*>(xt)[bc * T + nn] = make_float2(re, im);
+  }
+}
+
+__global__ void tril_to_spec_kernel(const float* __restrict__ yt, float* __restrict__ S, int B,
+                                    int C, int lmax, int mmax, int mact, int64_t Tp, int64_t T,
+                                    int64_t ldT, const int* __restrict__ off) {
+  const int64_t n = (int64_t)B * C * Tp;
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < n;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t t = e % Tp;
+    const int64_t bc = e / Tp;
+    const int b = (int)(bc / C), c = (int)(bc % C);
+    const int m = find_m(off, mact, t);
+    const int l = m + (int)(t - off[m]);
+    float2 v = make_float2(0.f, 0.f);
+    if (l < lmax) v = reinterpret_cast<const float2*>(yt)[bc * T + tril_row_off(l, mmax) + m];
+    S[((int64_t)(b * 2 + 0) * C + c) * ldT + t] = v.x;
+    S[((int64_t)(b * 2 + 1) * C + c) * ldT + t] = v.y;
+  }
+}
+
+int launch_spec_to_tril(const SpecLayout& L, const float* S, float* xt, int B, int C,
+                        const int* d_off, hipStream_t s) {
+  const int64_t n = (int64_t)B * C * L.Tp;
+  hipLaunchKernelGGL(spec_to_tril_kernel, dim3((unsigned)std::min<int64_t>(cdiv(n, 256), 65535)),
+                     dim3(256), 0, s, S, xt, B, C, L.lmax, L.mmax, L.mact, L.Tp, L.T, L.ldT,
+                     d_off);
+  return launch_check("spec_to_tril");
+}
+
+int launch_tril_to_spec(const SpecLayout& L, const float* yt, float* S, int B, int C,
+                        const int* d_off, hipStream_t s) {
+  const int64_t n = (int64_t)B * C * L.Tp;
+  hipLaunchKernelGGL(tril_to_spec_kernel, dim3((unsigned)std::min<int64_t>(cdiv(n, 256), 65535)),
+                     dim3(256), 0, s, yt, S, B, C, L.lmax, L.mmax, L.mact, L.Tp, L.T, L.ldT,
+                     d_off);
+  return launch_check("tril_to_spec");
+}
+
+// ---------------------------------------------------------------------------
+// linear filter: y[b,k,n] = Σ_i a[b,i,n]·w[k,i,n]   (complex, per mode n)
+// HBM-bound on w (C·C·T complex).  Each thread owns MPT consecutive modes and
+// KC output channels for NB batch entries; every weight element is read once
+// (16-B loads, 1 KiB per wave instruction), activations re-read Co/KC times
+// from L2.
+// ---------------------------------------------------------------------------
+template <int NB, int KC, int MPT>
+__global__ __launch_bounds__(256) void compl_contract_kernel(const float* __restrict__ a,
+                                                             const float* __restrict__ w,
+                                                             float* __restrict__ y, int B, int Ci,
+                                                             int Co, int64_t T, int nkc) {
+  const int nmt = (int)gridDim.x / nkc;  // mode tiles
+  // consecutive block ids -> same mode tile (shared activations stay in L2)
+  const int kc = blockIdx.x % nkc;
+  const int mt = blockIdx.x / nkc;
+  (void)nmt;
+  const int64_t n0 = ((int64_t)mt * 256 + threadIdx.x) * MPT;
+  const int b0 = blockIdx.y * NB;
+  const int k0 = kc * KC;
+  if (n0 >= T) return;
+  const bool full = (n0 + MPT <= T);
+  float2 acc[NB][KC][MPT];
+#pragma unroll
+  for (int b = 0; b < NB; ++b)
+#pragma unroll
+    for (int k = 0; k < KC; ++k)
+#pragma unroll
+      for (int q = 0; q < MPT; ++q) acc[b][k][q] = make_float2(0.f, 0.f);
+  const float2* a2 = reinterpret_cast<const float2*>(a);
+  const float2* w2 = reinterpret_cast<const float2*>(w);
+  for (int i = 0; i < Ci; ++i) {
+    float2 xv[NB][MPT];
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+      const int bb = b0 + b;
+      const float2* src = a2 + ((int64_t)(bb < B ? bb : 0) * Ci + i) * T + n0;
+      if (MPT == 2 && full) {
+        const float4 v = *reinterpret_cast<const float4*>(src);
+        xv[b][0] = make_float2(v.x, v.y);
+        xv[b][MPT - 1] = make_float2(v.z, v.w);
+      } else {
+#pragma unroll
+        for (int q = 0; q < MPT; ++q) xv[b][q] = (n0 + q < T) ? src[q] : make_float2(0.f, 0.f);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < KC; ++k) {
+      const int kk = k0 + k < Co ? k0 + k : 0;
+      const float2* ws = w2 + ((int64_t)kk * Ci + i) * T + n0;
+      float2 wv[MPT];
+      if (MPT == 2 && full) {
+        const float4 v = *reinterpret_cast<const float4*>(ws);
+        wv[0] = make_float2(v.x, v.y);
+        wv[MPT - 1] = make_float2(v.z, v.w);
+      } else {
+#pragma unroll
+        for (int q = 0; q < MPT; ++q) wv[q] = (n0 + q < T) ? ws[q] : make_float2(0.f, 0.f);
+      }
+#pragma unroll
+      for (int b = 0; b < NB; ++b)
+#pragma unroll
+        for (int q = 0; q < MPT; ++q) {
+          acc[b][k][q].x += xv[b][q].x * wv[q].x - xv[b][q].y * wv[q].y;
+          acc[b][k][q].y += xv[b][q].x * wv[q].y + xv[b][q].y * wv[q].x;
+        }
+    }
+  }
+  float2* y2 = reinterpret_cast<float2*>(y);
+#pragma unroll
+  for (int b = 0; b < NB; ++b) {
+    const int bb = b0 + b;
+    if (bb >= B) continue;
+#pragma unroll
+    for (int k = 0; k < KC; ++k) {
+      if (k0 + k >= Co) continue;
+      float2* dst = y2 + ((int64_t)bb * Co + k0 + k) * T + n0;
+      if (MPT == 2 && full) {
+        *reinterpret_cast<float4*>(dst) =
+            make_float4(acc[b][k][0].x, acc[b][k][0].y, acc[b][k][MPT - 1].x, acc[b][k][MPT - 1].y);
+      } else {
+#pragma unroll
+        for (int q = 0; q < MPT; ++q)
+          if (n0 + q < T) dst[q] = acc[b][k][q];
+      }
+    }
+  }
+}
+
+template <int NB, int KC, int MPT>
+static int launch_contract_t(const float* a, const float* w, float* y, int B, int Ci, int Co,
+                             int64_t T, hipStream_t s) {
+  const int nkc = (int)cdiv(Co, KC);
+  const int64_t nmt = cdiv(T, 256 * MPT);
+  MSFNO_REQUIRE(nmt * nkc < (1LL << 31), MSFNO_EINVAL, "contract grid too large");
+  dim3 grid((unsigned)(nmt * nkc), (unsigned)cdiv(B, NB));
+  hipLaunchKernelGGL((compl_contract_kernel<NB, KC, MPT>), grid, dim3(256), 0, s, a, w, y, B, Ci,
+                     Co, T, nkc);
+  return launch_check("compl_contract");
+}
+
+int launch_compl_contract(const float* a, const float* w, float* y, int B, int Ci, int Co,
+                          int64_t T, hipStream_t s) {
+  const bool even = (T % 2 == 0) && ((reinterpret_cast<uintptr_t>(a) | reinterpret_cast<uintptr_t>(w) |
+                                      reinterpret_cast<uintptr_t>(y)) & 15) == 0;
+  if (B >= 8) {
+    return even ? launch_contract_t<8, 4, 2>(a, w, y, B, Ci, Co, T, s)
+                : launch_contract_t<8, 4, 1>(a, w, y, B, Ci, Co, T, s);
+  }
+  if (B >= 4) {
+    return even ? launch_contract_t<4, 8, 2>(a, w, y, B, Ci, Co, T, s)
+                : launch_contract_t<4, 8, 1>(a, w, y, B, Ci, Co, T, s);
+  }
+  if (B == 2 || B == 3) {
+    return even ? launch_contract_t<2, 8, 2>(a, w, y, B, Ci, Co, T, s)
+                : launch_contract_t<2, 8, 1>(a, w, y, B, Ci, Co, T, s);
+  }
+  return even ? launch_contract_t<1, 16, 2>(a, w, y, B, Ci, Co, T, s)
+              : launch_contract_t<1, 16, 1>(a, w, y, B, Ci, Co, T, s);
+}
+
+// compl_mul2d_fwd_c in reference layout (standalone op, not on the fused path):
+// y[b,o,p] = Σ_i a[b,i,p]·w[i,o]; one thread per (b, p), 8 outputs per pass.
+__global__ __launch_bounds__(256) void compl_mul2d_kernel(const float2* __restrict__ a,
+                                                          const float2* __restrict__ w,
+                                                          float2* __restrict__ y, int B, int Ci,
+                                                          int Co, int64_t XY, int relu) {
+  const int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  const int b = blockIdx.y;
+  if (p >= XY) return;
+  const float2* ab = a + (int64_t)b * Ci * XY + p;
+  for (int o0 = 0; o0 < Co; o0 += 8) {
+    float2 acc[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) acc[q] = make_float2(0.f, 0.f);
+    for (int i = 0; i < Ci; ++i) {
+      const float2 x = ab[(int64_t)i * XY];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        if (o0 + q < Co) {
+          const float2 wv = w[(int64_t)i * Co + o0 + q];
+          acc[q].x += x.x * wv.x - x.y * wv.y;
+          acc[q].y += x.x * wv.y + x.y * wv.x;
+        }
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      if (o0 + q < Co) {
+        float2 v = acc[q];
+        if (relu) v.x = fmaxf(v.x, 0.f);
+        y[((int64_t)b * Co + o0 + q) * XY + p] = v;
+      }
+    }
+  }
+}
+
+int launch_compl_mul2d(const float* a, const float* w, float* y, int B, int Ci, int Co,
+                       int64_t XY, int relu_real, hipStream_t s) {
+  dim3 grid((unsigned)cdiv(XY, 256), (unsigned)B);
+  hipLaunchKernelGGL(compl_mul2d_kernel, grid, dim3(256), 0, s,
+                     reinterpret_cast<const float2*>(a), reinterpret_cast<const float2*>(w),
+                     reinterpret_cast<float2*>(y), B, Ci, Co, XY, relu_real);
+  return launch_check("compl_mul2d");
+}
+
+}  // namespace msfno

@@ -1,0 +1,219 @@
+"""Spherical spectral filters and the channel MLP — mirror of
+MSFNO/Models/sfno/layers.py (SpectralConvS2 :336-427, SpectralAttentionS2
+:536-639, MLP :145-178, trunc_normal_ :29-84, DropPath :88-118).
+
+Constructor signatures, parameter/buffer names and shapes follow the reference
+so state dicts load unchanged.  ``forward`` runs SHT → filter → inverse SHT as
+one native call (``msfno_filter_forward``): HIP longitude FFTs, MFMA Legendre
+contractions and either the MFMA spectral MLP (non-linear) or the per-mode
+weight-streaming contraction (linear)."""
+from __future__ import annotations
+
+import math
+import warnings
+
+import torch
+import torch.nn as nn
+
+from .. import _native as N
+from ..harmonics import InverseRealSHT, RealSHT
+from .activations import ComplexReLU
+
+
+def _no_grad_trunc_normal_(tensor, mean, std, a, b):
+    def norm_cdf(x):
+        return (1.0 + math.erf(x / math.sqrt(2.0))) / 2.0
+
+    if (mean < a - 2 * std) or (mean > b + 2 * std):
+        warnings.warn("mean is more than 2 std from [a, b] in nn.init.trunc_normal_.", stacklevel=2)
+    with torch.no_grad():
+        lo = norm_cdf((a - mean) / std)
+        hi = norm_cdf((b - mean) / std)
+        tensor.uniform_(2 * lo - 1, 2 * hi - 1)
+        tensor.erfinv_()
+        tensor.mul_(std * math.sqrt(2.0))
+        tensor.add_(mean)
+        tensor.clamp_(min=a, max=b)
+        return tensor
+
+
+def trunc_normal_(tensor, mean=0.0, std=1.0, a=-2.0, b=2.0):
+    return _no_grad_trunc_normal_(tensor, mean, std, a, b)
+
+
+class DropPath(nn.Module):
+    """Stochastic depth; identity at inference (the only mode of the fused path)."""
+
+    def __init__(self, drop_prob=None):
+        super().__init__()
+        self.drop_prob = drop_prob
+
+    def forward(self, x):
+        if not self.drop_prob or not self.training:
+            return x
+        keep = 1.0 - self.drop_prob
+        mask = (keep + torch.rand((x.shape[0],) + (1,) * (x.ndim - 1), dtype=x.dtype,
+                                  device=x.device)).floor_()
+        return x.div(keep) * mask
+
+
+class MLP(nn.Module):
+    """Conv1x1 → act → Conv1x1 (state-dict keys fwd.0.*, fwd.2.*).  Inside a
+    block it is executed by the fused native block (two MFMA GEMMs with the
+    norm1/FiLM affine folded into fc1 and GELU / bias / residual in epilogues)."""
+
+    def __init__(self, in_features, hidden_features=None, out_features=None, act_layer=nn.GELU,
+                 output_bias=True, drop_rate=0.0, checkpointing_mlp=False):
+        super().__init__()
+        self.checkpointing_mlp = checkpointing_mlp
+        out_features = out_features or in_features
+        hidden_features = hidden_features or in_features
+        fc1 = nn.Conv2d(in_features, hidden_features, 1, bias=True)
+        act = act_layer()
+        fc2 = nn.Conv2d(hidden_features, out_features, 1, bias=output_bias)
+        if drop_rate > 0.0:
+            drop = nn.Dropout(drop_rate)
+            self.fwd = nn.Sequential(fc1, act, drop, fc2, drop)
+        else:
+            self.fwd = nn.Sequential(fc1, act, fc2)
+
+    def forward(self, x):
+        return self.fwd(x)
+
+
+def _check_transforms(fwd, inv):
+    if not isinstance(fwd, RealSHT) or not isinstance(inv, InverseRealSHT):
+        raise NotImplementedError("MI355X spectral filters require msfno_amd.harmonics transforms")
+    assert inv.lmax == fwd.lmax
+    assert inv.mmax == fwd.mmax
+
+
+class _S2FilterBase(nn.Module):
+    """Shared native dispatch for the two S2 filters."""
+
+    def _fill_desc(self, d: N.BlockDesc, keep: list):  # pragma: no cover - overridden
+        raise NotImplementedError
+
+    def native_desc(self, C):
+        d = N.BlockDesc()
+        keep = []
+        d.C = C
+        d.norm_eps = 1e-6
+        self._fill_desc(d, keep)
+        return d, keep
+
+    def forward(self, x):
+        dtype = x.dtype
+        x = N.require_device_f32(x, "filter input")
+        B, C, H, W = x.shape
+        fwd, inv = self._transforms()
+        assert H == fwd.nlat and W == fwd.nlon
+        pf = fwd._plan(x.device)
+        pi = inv._plan(x.device)
+        d, keep = self.native_desc(C)
+        L = N.lib()
+        nbytes = L.msfno_block_workspace_size(d, pf.handle, pi.handle, B)
+        ws = torch.empty(nbytes, dtype=torch.uint8, device=x.device)
+        y = torch.empty(B, C, inv.nlat, inv.nlon, dtype=torch.float32, device=x.device)
+        N.check(L.msfno_filter_forward(d, pf.handle, pi.handle, x.data_ptr(), y.data_ptr(), B,
+                                       ws.data_ptr(), nbytes, N.stream_of(x.device)),
+                type(self).__name__ + ".forward")
+        del keep
+        return y.to(dtype)
+
+
+class SpectralConvS2(_S2FilterBase):
+    """Linear spectral filter: per-(l,m) complex C×C weights on the tril modes."""
+
+    def __init__(self, forward_transform, inverse_transform, hidden_size, sparsity_threshold=0.0,
+                 use_complex_kernels=False, compression=None, rank=128, bias=False):
+        super().__init__()
+        self.hidden_size = hidden_size
+        self.sparsity_threshold = sparsity_threshold
+        self.scale = 0.02
+        self.forward_transform = forward_transform
+        self.inverse_transform = inverse_transform
+        self.modes_lat = self.forward_transform.lmax
+        self.modes_lon = self.forward_transform.mmax
+        assert self.inverse_transform.lmax == self.modes_lat
+        assert self.inverse_transform.mmax == self.modes_lon
+        ii, jj = torch.tril_indices(self.modes_lat, self.modes_lon)
+        self.register_buffer("ii", ii)
+        self.register_buffer("jj", jj)
+        if compression == "tt":
+            raise NotImplementedError("compression='tt' is not on the MI355X path (SURVEY §2 row 3)")
+        self.w = nn.Parameter(self.scale * torch.randn(self.hidden_size, self.hidden_size,
+                                                       len(ii), 2))
+        if bias:
+            raise NotImplementedError("SpectralConvS2(bias=True) is not on the MI355X path")
+
+    def _transforms(self):
+        _check_transforms(self.forward_transform, self.inverse_transform)
+        return self.forward_transform, self.inverse_transform
+
+    def _fill_desc(self, d, keep):
+        if self.sparsity_threshold != 0.0:
+            raise NotImplementedError("softshrink with a non-zero threshold is not fused")
+        ref_ii, ref_jj = torch.tril_indices(self.modes_lat, self.modes_lon)
+        if not (torch.equal(self.ii.cpu(), ref_ii) and torch.equal(self.jj.cpu(), ref_jj)):
+            raise NotImplementedError("ii/jj must be torch.tril_indices(lmax, mmax)")
+        w = self.w.detach()
+        if w.dtype != torch.float32 or not w.is_contiguous():
+            w = w.float().contiguous()
+        keep.append(w)
+        d.filter_type = N.FILTER_LINEAR
+        d.lin_w = w.data_ptr()
+
+
+class SpectralAttentionS2(_S2FilterBase):
+    """Non-linear spectral filter: complex MLP shared over all (l,m) modes."""
+
+    def __init__(self, forward_transform, inverse_transform, embed_dim, sparsity_threshold=0.0,
+                 hidden_size_factor=2, use_complex_network=True, use_complex_kernels=False,
+                 complex_activation="real", bias=False, spectral_layers=1, drop_rate=0.0):
+        super().__init__()
+        self.embed_dim = embed_dim
+        self.sparsity_threshold = sparsity_threshold
+        self.hidden_size = int(hidden_size_factor * self.embed_dim)
+        self.scale = 0.02
+        self.spectral_layers = spectral_layers
+        self.modes_lat = forward_transform.lmax
+        self.modes_lon = forward_transform.mmax
+        # the reference stores only the bound forward methods (layers.py:573-574)
+        self.forward_transform = forward_transform.forward
+        self.inverse_transform = inverse_transform.forward
+        assert inverse_transform.lmax == self.modes_lat
+        assert inverse_transform.mmax == self.modes_lon
+        w = [self.scale * torch.randn(self.embed_dim, self.hidden_size, 2)]
+        for _ in range(1, self.spectral_layers):
+            w.append(self.scale * torch.randn(self.hidden_size, self.hidden_size, 2))
+        self.w = nn.ParameterList(w)
+        if bias:
+            raise NotImplementedError("SpectralAttentionS2(bias=True) is not on the MI355X path")
+        self.wout = nn.Parameter(self.scale * torch.randn(self.hidden_size, self.embed_dim, 2))
+        self.drop = nn.Dropout(drop_rate) if drop_rate > 0.0 else nn.Identity()
+        self.activation = ComplexReLU(mode=complex_activation, bias_shape=(self.hidden_size, 1, 1))
+
+    def _transforms(self):
+        fwd = self.forward_transform.__self__
+        inv = self.inverse_transform.__self__
+        _check_transforms(fwd, inv)
+        return fwd, inv
+
+    def _fill_desc(self, d, keep):
+        if self.activation.mode != "real":
+            raise NotImplementedError("only complex_activation='real' is fused")
+        if self.training and not isinstance(self.drop, nn.Identity):
+            raise NotImplementedError("spectral dropout in training mode is not fused")
+        if self.spectral_layers > 8:
+            raise NotImplementedError("spectral_layers > 8")
+        d.filter_type = N.FILTER_NONLINEAR
+        d.spectral_layers = self.spectral_layers
+        d.spec_hidden = self.hidden_size
+        for l, p in enumerate(self.w):
+            t = p.detach().float().contiguous()
+            keep.append(t)
+            d.spec_w[l] = t.data_ptr()
+        t = self.wout.detach().float().contiguous()
+        keep.append(t)
+        d.spec_wout = t.data_ptr()
