@@ -38,20 +38,43 @@ __device__ __forceinline__ int xcd_remap(int orig, int nwg) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
 }
 
-__device__ __forceinline__ float gelu_erf(float v) {
-  return 0.5f * v * (1.0f + erff(v * 0.70710678118654752440f));
+// erf with the coefficients of ROCm's ocml erff, evaluated branch-free (both
+// polynomial regimes, then a select) with the hardware exp2; |err| < 2e-7.
+__device__ __forceinline__ float erf_fast(float x) {
+  const float t = fabsf(x);
+  const float s = t * t;
+  float p = fmaf(__uint_as_float(0xba1345e1u), s, __uint_as_float(0x3ba10414u));
+  p = fmaf(s, p, __uint_as_float(0xbcdac9b8u));
+  p = fmaf(s, p, __uint_as_float(0x3de703beu));
+  p = fmaf(s, p, __uint_as_float(0xbec09330u));
+  p = fmaf(s, p, __uint_as_float(0x3e0375d0u));
+  const float small = fmaf(t, p, t);
+  float q = fmaf(__uint_as_float(0x378e98abu), t, __uint_as_float(0xb9c68948u));
+  q = fmaf(t, q, __uint_as_float(0x3b7cd369u));
+  q = fmaf(t, q, __uint_as_float(0xbcc618b2u));
+  q = fmaf(t, q, __uint_as_float(0x3dda74e4u));
+  q = fmaf(t, q, __uint_as_float(0x3f228afdu));
+  q = fmaf(t, q, __uint_as_float(0x3e03c728u));
+  q = fmaf(t, q, t);
+  const float large = 1.0f - __builtin_amdgcn_exp2f(-1.44269504088896341f * q);
+  const float r = t < 1.0f ? small : large;
+  return copysignf(r, x);
 }
 
-constexpr int BK = 16;
+__device__ __forceinline__ float gelu_erf(float v) {
+  return 0.5f * v * (1.0f + erf_fast(v * 0.70710678118654752440f));
+}
 
-template <int BM, int BN>
+enum : int { EPI_BIAS = 1, EPI_ADD = 2, EPI_GELU = 4, EPI_RELU = 8, EPI_STATS = 16 };
+
+template <int BM, int BN, int BK, bool VEC, int EPI>
 __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmParams p) {
   constexpr int WM = BM / 2, WN = BN / 2;
   constexpr int MT = WM / 32, NT = WN / 32;
   constexpr int LDA_S = BM + 2;  // staging-write conflict-free (see header)
   constexpr int LDB_S = BN;
-  constexpr int A_LD = BM / 64;  // float4 staging loads per thread
-  constexpr int B_LD = BN / 64;
+  constexpr int A_LD = BM * BK / 1024;  // float4 staging loads per thread
+  constexpr int B_LD = BN * BK / 1024;
   __shared__ float As[2][BK * LDA_S];
   __shared__ float Bs[2][BK * LDB_S];
   __shared__ float red[2 * BM];
@@ -96,69 +119,75 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmParams p) {
   const int m0 = tm * BM, n0 = tn * BN;
   const int nk = (K + BK - 1) / BK;
 
-  if (stats && tid < BM) { red[tid] = 0.f; red[BM + tid] = 0.f; }
+  if constexpr ((EPI & EPI_STATS) != 0) {
+    if (tid < BM) { red[tid] = 0.f; red[BM + tid] = 0.f; }
+  }
 
   float4 ra[A_LD], rb[B_LD];
 
+  // Branch-free staging: loads use clamped (always in-bounds) addresses and the
+  // out-of-range elements are zeroed only when the registers are written to LDS
+  // (after the MFMAs of the current tile), so hipcc neither predicates the loads
+  // nor waits for them before the compute.  With VEC, rows are padded to a
+  // multiple of 4 floats (ld % 4 == 0), so a float4 at k < K stays in its row.
+  const int Mc = M > 0 ? M - 1 : 0, Kc = K > 0 ? K - 1 : 0, Nc = N > 0 ? N - 1 : 0;
   auto load_tile = [&](int kt) {
     const int k0 = kt * BK;
 #pragma unroll
     for (int q = 0; q < A_LD; ++q) {
       const int idx = tid + 256 * q;
-      const int row = m0 + idx / 4;
-      const int k = k0 + (idx % 4) * 4;
-      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (row < M) {
-        const float* src = A + (int64_t)row * lda + k;
-        if (p.vecA && k + 3 < K) {
-          v = *reinterpret_cast<const float4*>(src);
-        } else {
-          if (k + 0 < K) v.x = src[0];
-          if (k + 1 < K) v.y = src[1];
-          if (k + 2 < K) v.z = src[2];
-          if (k + 3 < K) v.w = src[3];
-        }
+      const int row = min(m0 + idx / (BK / 4), Mc);
+      const int k = k0 + (idx % (BK / 4)) * 4;
+      const float* src = A + (int64_t)row * lda;
+      if constexpr (VEC) {
+        ra[q] = *reinterpret_cast<const float4*>(src + min(k, Kc & ~3));
+      } else {
+        ra[q] = make_float4(src[min(k, Kc)], src[min(k + 1, Kc)], src[min(k + 2, Kc)],
+                            src[min(k + 3, Kc)]);
       }
-      ra[q] = v;
     }
 #pragma unroll
     for (int q = 0; q < B_LD; ++q) {
       const int idx = tid + 256 * q;
-      const int kr = k0 + idx / (BN / 4);
+      const int kr = min(k0 + idx / (BN / 4), Kc);
       const int col = n0 + (idx % (BN / 4)) * 4;
-      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (kr < K) {
-        const float* src = B + (int64_t)kr * ldb + col;
-        if (p.vecB && col + 3 < N) {
-          v = *reinterpret_cast<const float4*>(src);
-        } else {
-          if (col + 0 < N) v.x = src[0];
-          if (col + 1 < N) v.y = src[1];
-          if (col + 2 < N) v.z = src[2];
-          if (col + 3 < N) v.w = src[3];
-        }
+      const float* src = B + (int64_t)kr * ldb;
+      if constexpr (VEC) {
+        rb[q] = *reinterpret_cast<const float4*>(src + min(col, Nc & ~3));
+      } else {
+        rb[q] = make_float4(src[min(col, Nc)], src[min(col + 1, Nc)], src[min(col + 2, Nc)],
+                            src[min(col + 3, Nc)]);
       }
-      rb[q] = v;
     }
   };
-  auto store_tile = [&](int buf) {
+  auto store_tile = [&](int buf, int kt) {
+    const int k0 = kt * BK;
 #pragma unroll
     for (int q = 0; q < A_LD; ++q) {
       const int idx = tid + 256 * q;
-      const int row = idx / 4;
-      const int k = (idx % 4) * 4;
+      const int row = idx / (BK / 4);
+      const int k = (idx % (BK / 4)) * 4;
+      const bool rok = m0 + row < M;
+      const int kg = k0 + k;
       float* dst = &As[buf][k * LDA_S + row];
-      dst[0] = ra[q].x;
-      dst[LDA_S] = ra[q].y;
-      dst[2 * LDA_S] = ra[q].z;
-      dst[3 * LDA_S] = ra[q].w;
+      dst[0] = (rok && kg + 0 < K) ? ra[q].x : 0.f;
+      dst[LDA_S] = (rok && kg + 1 < K) ? ra[q].y : 0.f;
+      dst[2 * LDA_S] = (rok && kg + 2 < K) ? ra[q].z : 0.f;
+      dst[3 * LDA_S] = (rok && kg + 3 < K) ? ra[q].w : 0.f;
     }
 #pragma unroll
     for (int q = 0; q < B_LD; ++q) {
       const int idx = tid + 256 * q;
       const int kr = idx / (BN / 4);
       const int col = (idx % (BN / 4)) * 4;
-      *reinterpret_cast<float4*>(&Bs[buf][kr * LDB_S + col]) = rb[q];
+      const bool kok = k0 + kr < K;
+      const int cg = n0 + col;
+      float4 v;
+      v.x = (kok && cg + 0 < N) ? rb[q].x : 0.f;
+      v.y = (kok && cg + 1 < N) ? rb[q].y : 0.f;
+      v.z = (kok && cg + 2 < N) ? rb[q].z : 0.f;
+      v.w = (kok && cg + 3 < N) ? rb[q].w : 0.f;
+      *reinterpret_cast<float4*>(&Bs[buf][kr * LDB_S + col]) = v;
     }
   };
 
@@ -172,7 +201,7 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmParams p) {
 
   if (nk > 0) {
     load_tile(0);
-    store_tile(0);
+    store_tile(0, 0);
   }
   __syncthreads();
   const int half = lane >> 5;
@@ -196,48 +225,73 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmParams p) {
         for (int j = 0; j < NT; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i], b[j], acc[i][j], 0, 0, 0);
     }
-    if (kt + 1 < nk) store_tile(cur ^ 1);
+    if (kt + 1 < nk) store_tile(cur ^ 1, kt + 1);
     __syncthreads();
   }
 
-  // ---- epilogue ---------------------------------------------------------------
-  const bool do_stats = stats != nullptr;
+  // ---- epilogue (compile-time specialised; one 32x32 tile at a time) ---------
+  constexpr bool kStats = (EPI & EPI_STATS) != 0;
 #pragma unroll
   for (int i = 0; i < MT; ++i) {
+    float bv[16];
+    int rowv[16];
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int lrow = wm * WM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
-      const int row = m0 + lrow;
-      float s = 0.f, sq = 0.f;
+      rowv[r] = m0 + lrow;
+      if constexpr ((EPI & EPI_BIAS) != 0) bv[r] = bias[min(rowv[r], M - 1)];
+    }
+    float s[16], sq[16];
+    if constexpr (kStats) {
 #pragma unroll
-      for (int j = 0; j < NT; ++j) {
-        const int col = n0 + wn * WN + j * 32 + l32;
+      for (int r = 0; r < 16; ++r) s[r] = sq[r] = 0.f;
+    }
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+      const int col = n0 + wn * WN + j * 32 + l32;
+      const bool cok = col < N;
+      float add[16];
+      if constexpr ((EPI & EPI_ADD) != 0) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          add[r] = addend[(int64_t)min(rowv[r], M - 1) * p.ldd + min(col, N - 1)];
+      }
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
         float v = acc[i][j][r];
-        const bool ok = row < M && col < N;
-        if (ok) {
-          if (bias) v += bias[row];
-          if (addend) v += addend[(int64_t)row * p.ldd + col];
-          if (p.act == 1) v = gelu_erf(v);
-          if (p.relu_period && (row % p.relu_period) < p.relu_rows) v = fmaxf(v, 0.f);
-          C[(int64_t)row * ldc + col] = v;
-          s += v;
-          sq += v * v;
+        if constexpr ((EPI & EPI_BIAS) != 0) v += bv[r];
+        if constexpr ((EPI & EPI_ADD) != 0) v += add[r];
+        if constexpr ((EPI & EPI_GELU) != 0) v = gelu_erf(v);
+        if constexpr ((EPI & EPI_RELU) != 0) {
+          if ((unsigned)rowv[r] % (unsigned)p.relu_period < (unsigned)p.relu_rows) v = fmaxf(v, 0.f);
+        }
+        const bool ok = cok && rowv[r] < M;
+        if (ok) C[(int64_t)rowv[r] * ldc + col] = v;
+        if constexpr (kStats) {
+          const float vz = ok ? v : 0.f;
+          s[r] += vz;
+          sq[r] += vz * vz;
         }
       }
-      if (do_stats) {
+    }
+    if constexpr (kStats) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        float a = s[r], q = sq[r];
 #pragma unroll
         for (int o = 1; o < 32; o <<= 1) {
-          s += __shfl_xor(s, o);
-          sq += __shfl_xor(sq, o);
+          a += __shfl_xor(a, o);
+          q += __shfl_xor(q, o);
         }
         if (l32 == 0) {
-          atomicAdd(&red[lrow], s);
-          atomicAdd(&red[BM + lrow], sq);
+          const int lrow = rowv[r] - m0;
+          atomicAdd(&red[lrow], a);
+          atomicAdd(&red[BM + lrow], q);
         }
       }
     }
   }
-  if (do_stats) {
+  if constexpr (kStats) {
     __syncthreads();
     if (tid < BM) {
       const int row = m0 + tid;
@@ -270,17 +324,55 @@ static GemmParams make_params(const float* A, const float* B, float* C, const Ge
   return p;
 }
 
-template <int BM, int BN>
-static void launch(const GemmParams& p, dim3 grid, hipStream_t s) {
-  hipLaunchKernelGGL((gemm_f32_kernel<BM, BN>), grid, dim3(256), 0, s, p);
+template <int BM, int BN, int BK, int EPI>
+static void launch_e(const GemmParams& p, dim3 grid, hipStream_t s) {
+  if (p.vecA && p.vecB)
+    hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, BK, true, EPI>), grid, dim3(256), 0, s, p);
+  else
+    hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, BK, false, EPI>), grid, dim3(256), 0, s, p);
 }
 
-static int dispatch(GemmTile tile, const GemmParams& p, dim3 grid, hipStream_t s) {
-  switch (tile) {
-    case TILE_128x128: launch<128, 128>(p, grid, s); break;
-    case TILE_128x64: launch<128, 64>(p, grid, s); break;
-    default: launch<64, 64>(p, grid, s); break;
+static int epi_code(const GemmParams& p) {
+  return (p.bias ? EPI_BIAS : 0) | (p.addend ? EPI_ADD : 0) | (p.act == 1 ? EPI_GELU : 0) |
+         (p.relu_period ? EPI_RELU : 0) | (p.stats ? EPI_STATS : 0);
+}
+
+// the epilogue combinations the block uses (anything else is rejected)
+template <int BM, int BN, int BK>
+static int launch(const GemmParams& p, dim3 grid, hipStream_t s) {
+  switch (epi_code(p)) {
+    case 0: launch_e<BM, BN, BK, 0>(p, grid, s); break;
+    case EPI_RELU: launch_e<BM, BN, BK, EPI_RELU>(p, grid, s); break;
+    case EPI_BIAS: launch_e<BM, BN, BK, EPI_BIAS>(p, grid, s); break;
+    case EPI_BIAS | EPI_GELU: launch_e<BM, BN, BK, EPI_BIAS | EPI_GELU>(p, grid, s); break;
+    case EPI_BIAS | EPI_ADD: launch_e<BM, BN, BK, EPI_BIAS | EPI_ADD>(p, grid, s); break;
+    case EPI_ADD: launch_e<BM, BN, BK, EPI_ADD>(p, grid, s); break;
+    case EPI_BIAS | EPI_ADD | EPI_STATS:
+      launch_e<BM, BN, BK, EPI_BIAS | EPI_ADD | EPI_STATS>(p, grid, s); break;
+    case EPI_BIAS | EPI_ADD | EPI_GELU | EPI_STATS:
+      launch_e<BM, BN, BK, EPI_BIAS | EPI_ADD | EPI_GELU | EPI_STATS>(p, grid, s); break;
+    case EPI_ADD | EPI_STATS: launch_e<BM, BN, BK, EPI_ADD | EPI_STATS>(p, grid, s); break;
+    case EPI_ADD | EPI_GELU | EPI_STATS:
+      launch_e<BM, BN, BK, EPI_ADD | EPI_GELU | EPI_STATS>(p, grid, s); break;
+    default:
+      set_error("gemm: unsupported epilogue combination");
+      return MSFNO_EUNSUPPORTED;
   }
+  return MSFNO_OK;
+}
+
+#ifndef MSFNO_GEMM_BK
+#define MSFNO_GEMM_BK 16
+#endif
+
+static int dispatch(GemmTile tile, const GemmParams& p, dim3 grid, hipStream_t s) {
+  int rc;
+  switch (tile) {
+    case TILE_128x128: rc = launch<128, 128, MSFNO_GEMM_BK>(p, grid, s); break;
+    case TILE_128x64: rc = launch<128, 64, MSFNO_GEMM_BK>(p, grid, s); break;
+    default: rc = launch<64, 64, MSFNO_GEMM_BK>(p, grid, s); break;
+  }
+  if (rc != MSFNO_OK) return rc;
   return launch_check("gemm_f32");
 }
 

@@ -53,11 +53,12 @@ class _SHTBase(nn.Module):
         if plan is None:
             plan = N.SHTPlan(self.nlat, self.nlon, self.lmax, self.mmax, self._inverse, idx)
             self._plans[idx] = plan
-        t = table
-        if t.device != device or t.dtype != torch.float32 or not t.is_contiguous():
-            t = t.to(device=device, dtype=torch.float32).contiguous()
         key = (table.data_ptr(), table._version, table.dtype, str(table.device))
-        plan.load(t, key)
+        if key != plan.key:  # (re)load only when the buffer tensor changed
+            t = table
+            if t.device != device or t.dtype != torch.float32 or not t.is_contiguous():
+                t = t.to(device=device, dtype=torch.float32).contiguous()
+            plan.load(t, key)
         return plan
 
     def __getstate__(self):

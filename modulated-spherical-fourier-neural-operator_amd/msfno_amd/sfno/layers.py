@@ -154,9 +154,12 @@ class SpectralConvS2(_S2FilterBase):
     def _fill_desc(self, d, keep):
         if self.sparsity_threshold != 0.0:
             raise NotImplementedError("softshrink with a non-zero threshold is not fused")
-        ref_ii, ref_jj = torch.tril_indices(self.modes_lat, self.modes_lon)
-        if not (torch.equal(self.ii.cpu(), ref_ii) and torch.equal(self.jj.cpu(), ref_jj)):
-            raise NotImplementedError("ii/jj must be torch.tril_indices(lmax, mmax)")
+        key = (self.ii.data_ptr(), self.ii._version, self.jj.data_ptr(), self.jj._version)
+        if getattr(self, "_tril_checked", None) != key:  # validated once (avoids a D2H sync per call)
+            ref_ii, ref_jj = torch.tril_indices(self.modes_lat, self.modes_lon)
+            if not (torch.equal(self.ii.cpu(), ref_ii) and torch.equal(self.jj.cpu(), ref_jj)):
+                raise NotImplementedError("ii/jj must be torch.tril_indices(lmax, mmax)")
+            self._tril_checked = key
         w = self.w.detach()
         if w.dtype != torch.float32 or not w.is_contiguous():
             w = w.float().contiguous()
