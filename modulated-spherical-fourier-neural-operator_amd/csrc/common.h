@@ -77,6 +77,8 @@ struct FFTPlan {
   int N = 0;         // nlon
   int H = 0;         // complex length actually transformed (N/2 if packed)
   int packed = 0;    // real-input packing (N even)
+  int inplace = 1;   // all passes fit the in-register in-place scheme
+  int codelet = 0;   // compiled fixed-size FFT (0 = generic runtime-radix path)
   int nrad = 0;
   int radices[kMaxRadices] = {0};
   float2* twH = nullptr;  // e^{-2πi t/H}, t < H      (device)
