@@ -2,6 +2,7 @@
 // transforms, contractions and the fused SFNO-Block forward orchestration.
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 
 #include "kernels.h"
@@ -159,8 +160,14 @@ static const char* kStageNames[MSFNO_PROF_NSTAGES] = {
 
 struct Profiler {
   bool on = false;
-  std::vector<std::pair<int, hipEvent_t>> marks;
+  struct Mark {
+    int stage;
+    hipStream_t stream;
+    hipEvent_t ev;
+  };
+  std::vector<Mark> marks;
   std::vector<hipEvent_t> pool;
+  // a stage lasts from its mark to the next mark recorded on the same stream
   void mark(int stage, hipStream_t s) {
     if (!on) return;
     hipEvent_t e;
@@ -174,11 +181,43 @@ struct Profiler {
       pool.push_back(e);
       return;
     }
-    marks.emplace_back(stage, e);
+    marks.push_back({stage, s, e});
   }
 };
 static Profiler g_prof;
 static inline void prof(int stage, hipStream_t s) { g_prof.mark(stage, s); }
+
+// ---------------------------------------------------------------------------
+// per-device side stream: the inner-skip 1x1 conv (MFMA-bound, depends only on
+// the block input) runs concurrently with the HBM-bound SHT stages (fork/join
+// through events; capture-safe).  MSFNO_SIDE_STREAM=0 disables it.
+// ---------------------------------------------------------------------------
+struct SideCtx {
+  hipStream_t side = nullptr;
+  hipEvent_t fork = nullptr, join = nullptr;
+};
+
+static int side_ctx(SideCtx** out) {
+  static int enabled = -1;
+  if (enabled < 0) {
+    const char* e = getenv("MSFNO_SIDE_STREAM");
+    enabled = (e && e[0] == '0') ? 0 : 1;
+  }
+  *out = nullptr;
+  if (!enabled) return MSFNO_OK;
+  static std::vector<SideCtx> ctx(64);
+  int dev = 0;
+  MSFNO_CHECK_HIP(hipGetDevice(&dev));
+  MSFNO_REQUIRE(dev >= 0 && dev < 64, MSFNO_EINVAL, "device index out of range");
+  SideCtx& c = ctx[dev];
+  if (!c.side) {
+    MSFNO_CHECK_HIP(hipStreamCreateWithFlags(&c.side, hipStreamNonBlocking));
+    MSFNO_CHECK_HIP(hipEventCreateWithFlags(&c.fork, hipEventDisableTiming));
+    MSFNO_CHECK_HIP(hipEventCreateWithFlags(&c.join, hipEventDisableTiming));
+  }
+  *out = &c;
+  return MSFNO_OK;
+}
 
 // ---------------------------------------------------------------------------
 // workspace carving
@@ -218,6 +257,7 @@ static int ensure_desc(msfno_sht_plan_s* p, int R, int other_ld, int64_t ldT) {
     g.tiles_m = (int)cdiv(g.M, bm);
     g.tiles_n = (int)cdiv(g.N, bn);
     g.tile_start = tiles;
+    g.flags = (!p->inverse && m > 0) ? 1 : 0;  // m = 0 is normalised by dc_fixup
     tiles += g.tiles_m * g.tiles_n;
     d.push_back(g);
   }
@@ -233,9 +273,24 @@ static int ensure_desc(msfno_sht_plan_s* p, int R, int other_ld, int64_t ldT) {
   return MSFNO_OK;
 }
 
-static int legendre_fwd(msfno_sht_plan_s* f, const float* Xt, float* S, int R, hipStream_t s) {
+// MSFNO_FFT_TILE=1 selects the fused FFT+transpose tile kernels instead of the
+// row FFT + separate transpose kernels (measured slower on MI355X at 721x1440:
+// DESIGN.md §5); kept as an A/B switch.
+static bool use_fft_tile(const FFTPlan& f) {
+  static int mode = -1;
+  if (mode < 0) {
+    const char* e = getenv("MSFNO_FFT_TILE");
+    mode = (e && e[0] == '1') ? 1 : 0;
+  }
+  return mode == 1 && fft_tile_supported(f);
+}
+
+static int legendre_fwd(msfno_sht_plan_s* f, const float* Xt, float* S, int R, hipStream_t s,
+                        const float* rowscale = nullptr, int C = 0) {
   MSFNO_TRY(ensure_desc(f, R, 0, f->spec.ldT));
   GemmEpi e;
+  e.rowscale = rowscale;
+  e.rs_C = C;
   return gemm_desc(TILE_128x64, Xt, f->table, S, f->d_desc, f->ndesc, f->desc_tiles, e, s);
 }
 
@@ -252,12 +307,11 @@ struct BlockBufs {
   float2* Xn; float* Xt; float2* rs0; float* sc0; float* sh0;
   float* Sa; float* Sb; float* Sc; float* Wexp[9];
   float* xt; float* yt;
-  float* Yt; float2* Yn; float* filt; float* x1;
+  float* Yt; float2* Yn; float* x1;
   float2* st1; float* sc1; float* sh1;
   float* W1f; float* b1f; float* h;
 };
 
-static constexpr int kStatTile = 128;  // BN of the 1x1-conv GEMM tile
 
 static void carve_block(Carve& cv, BlockBufs& b, const msfno_block_desc* d,
                         const msfno_sht_plan_s* f, const msfno_sht_plan_s* g, int B,
@@ -289,14 +343,12 @@ static void carve_block(Carve& cv, BlockBufs& b, const msfno_block_desc* d,
   }
   b.Yt = cv.take<float>((int64_t)g->mmax * R * g->ldk);
   b.Yn = cv.take<float2>(BC * g->nlat * g->mmax);
-  b.filt = cv.take<float>(BC * P);
   b.x1 = nullptr;
   b.st1 = nullptr;
   b.sc1 = b.sh1 = b.W1f = b.b1f = b.h = nullptr;
   if (!with_norms) return;
   b.x1 = cv.take<float>(BC * P);
-  const int64_t np = std::max<int64_t>({cdiv(P, kStatTile), (int64_t)g->nlat, cdiv(P, 1024)});
-  b.st1 = cv.take<float2>(BC * np);
+  b.st1 = cv.take<float2>(BC * g->nlat);
   b.sc1 = cv.take<float>(BC);
   b.sh1 = cv.take<float>(BC);
   if (d->has_mlp) {
@@ -375,23 +427,54 @@ static int run_spectral(const msfno_block_desc* d, msfno_sht_plan_s* f, msfno_sh
                         const BlockBufs& b, const float* x, int B, bool norm0, hipStream_t s) {
   const int64_t C = d->C, BC = (int64_t)B * C, R = 2 * BC;
   prof(ST_FFT_FWD, s);
-  MSFNO_TRY(launch_fft_r2c_rows(f->fft, x, b.Xn, norm0 ? b.rs0 : nullptr, BC * f->nlat, f->mmax,
-                                (float)(2.0 * M_PI / f->nlon), s));
-  if (norm0) {
-    prof(ST_NORM0, s);
-    MSFNO_TRY(launch_chan_affine(b.rs0, f->nlat, f->nlon, f->nlon, B, (int)C, d->norm0_w,
-                                 d->norm0_b, d->norm_eps, nullptr, nullptr, 0.f, b.sc0, b.sh0, s));
+  const float scale = (float)(2.0 * M_PI / f->nlon);
+  if (use_fft_tile(f->fft)) {
+    // fused FFT + transpose; norm0 applied afterwards (m = 0 fix-up + GEMM row scale)
+    MSFNO_TRY(launch_fft_r2c_tile(f->fft, x, b.Xt, norm0 ? b.rs0 : nullptr, B, (int)C, f->nlat,
+                                  f->mmax, f->ldk, scale, s));
+    if (norm0) {
+      prof(ST_NORM0, s);
+      MSFNO_TRY(launch_chan_affine(b.rs0, f->nlat, f->nlon, f->nlon, B, (int)C, d->norm0_w,
+                                   d->norm0_b, d->norm_eps, nullptr, nullptr, 0.f, b.sc0, b.sh0,
+                                   s));
+      MSFNO_TRY(launch_dc_fixup(b.Xt, B, (int)C, f->nlat, f->ldk, b.sc0, b.sh0, s));
+    }
+    prof(ST_LEG_FWD, s);
+    MSFNO_TRY(legendre_fwd(f, b.Xt, b.Sa, (int)R, s, norm0 ? b.sc0 : nullptr, (int)C));
+  } else {
+    MSFNO_TRY(launch_fft_r2c_rows(f->fft, x, b.Xn, norm0 ? b.rs0 : nullptr, BC * f->nlat, f->mmax,
+                                  scale, s));
+    if (norm0) {
+      prof(ST_NORM0, s);
+      MSFNO_TRY(launch_chan_affine(b.rs0, f->nlat, f->nlon, f->nlon, B, (int)C, d->norm0_w,
+                                   d->norm0_b, d->norm_eps, nullptr, nullptr, 0.f, b.sc0, b.sh0,
+                                   s));
+    }
+    prof(ST_TRANSPOSE_FWD, s);
+    MSFNO_TRY(launch_transpose_fwd(b.Xn, b.Xt, B, (int)C, f->nlat, f->mmax, f->ldk,
+                                   norm0 ? b.sc0 : nullptr, norm0 ? b.sh0 : nullptr, s));
+    prof(ST_LEG_FWD, s);
+    MSFNO_TRY(legendre_fwd(f, b.Xt, b.Sa, (int)R, s));
   }
-  prof(ST_TRANSPOSE_FWD, s);
-  MSFNO_TRY(launch_transpose_fwd(b.Xn, b.Xt, B, (int)C, f->nlat, f->mmax, f->ldk,
-                                 norm0 ? b.sc0 : nullptr, norm0 ? b.sh0 : nullptr, s));
-  prof(ST_LEG_FWD, s);
-  MSFNO_TRY(legendre_fwd(f, b.Xt, b.Sa, (int)R, s));
   MSFNO_TRY(run_filter(d, f, g, b, B, s));
   prof(ST_LEG_INV, s);
   MSFNO_TRY(legendre_inv(g, b.Sa, b.Yt, (int)R, s));
+  return MSFNO_OK;
+}
+
+// Yt -> spatial rows (fused transpose + irfft when enabled); out = act(addsrc + irfft)
+static int run_inverse_fft(msfno_sht_plan_s* g, const BlockBufs& b, int B, int C, float* out,
+                           const float* addsrc, float2* rowstats, int act, hipStream_t s) {
+  const int64_t BC = (int64_t)B * C;
+  if (use_fft_tile(g->fft) && addsrc == nullptr) {
+    prof(ST_FFT_INV, s);
+    return launch_fft_c2r_tile(g->fft, b.Yt, out, rowstats, B, C, g->nlat, g->mmax,
+                               g->spec.mact, g->ldk, act, s);
+  }
   prof(ST_TRANSPOSE_INV, s);
-  MSFNO_TRY(launch_transpose_inv(b.Yt, b.Yn, B, (int)C, g->nlat, g->mmax, g->spec.mact, g->ldk, s));
+  MSFNO_TRY(launch_transpose_inv(b.Yt, b.Yn, B, C, g->nlat, g->mmax, g->spec.mact, g->ldk, s));
+  prof(ST_FFT_INV, s);
+  return launch_fft_c2r_rows(g->fft, b.Yn, out, addsrc, rowstats, BC * g->nlat, g->mmax, act, s);
   return MSFNO_OK;
 }
 
@@ -493,9 +576,13 @@ int msfno_sht_forward(msfno_sht_plan_t p, const float* x, float* out, int bc, vo
   float2* Xn = cv.take<float2>((int64_t)bc * p->nlat * p->mmax);
   float* Xt = cv.take<float>((int64_t)p->mmax * R * p->ldk);
   float* S = cv.take<float>(R * p->spec.ldT);
-  MSFNO_TRY(launch_fft_r2c_rows(p->fft, x, Xn, nullptr, (int64_t)bc * p->nlat, p->mmax,
-                                (float)(2.0 * M_PI / p->nlon), s));
-  MSFNO_TRY(launch_transpose_fwd(Xn, Xt, 1, bc, p->nlat, p->mmax, p->ldk, nullptr, nullptr, s));
+  const float scale = (float)(2.0 * M_PI / p->nlon);
+  if (use_fft_tile(p->fft)) {
+    MSFNO_TRY(launch_fft_r2c_tile(p->fft, x, Xt, nullptr, 1, bc, p->nlat, p->mmax, p->ldk, scale, s));
+  } else {
+    MSFNO_TRY(launch_fft_r2c_rows(p->fft, x, Xn, nullptr, (int64_t)bc * p->nlat, p->mmax, scale, s));
+    MSFNO_TRY(launch_transpose_fwd(Xn, Xt, 1, bc, p->nlat, p->mmax, p->ldk, nullptr, nullptr, s));
+  }
   MSFNO_TRY(legendre_fwd(p, Xt, S, (int)R, s));
   MSFNO_TRY(launch_spec_to_ref(*p, S, reinterpret_cast<float2*>(out), 1, bc, p->d_off, s));
   return MSFNO_OK;
@@ -515,8 +602,13 @@ int msfno_sht_inverse(msfno_sht_plan_t p, const float* in, float* x, int bc, voi
   float* S = cv.take<float>(R * p->spec.ldT);
   MSFNO_TRY(launch_ref_to_spec(*p, reinterpret_cast<const float2*>(in), S, 1, bc, p->d_off, s));
   MSFNO_TRY(legendre_inv(p, S, Yt, (int)R, s));
-  MSFNO_TRY(launch_transpose_inv(Yt, Yn, 1, bc, p->nlat, p->mmax, p->spec.mact, p->ldk, s));
-  MSFNO_TRY(launch_fft_c2r_rows(p->fft, Yn, x, nullptr, (int64_t)bc * p->nlat, p->mmax, 0, s));
+  if (use_fft_tile(p->fft)) {
+    MSFNO_TRY(launch_fft_c2r_tile(p->fft, Yt, x, nullptr, 1, bc, p->nlat, p->mmax, p->spec.mact,
+                                  p->ldk, 0, s));
+  } else {
+    MSFNO_TRY(launch_transpose_inv(Yt, Yn, 1, bc, p->nlat, p->mmax, p->spec.mact, p->ldk, s));
+    MSFNO_TRY(launch_fft_c2r_rows(p->fft, Yn, x, nullptr, nullptr, (int64_t)bc * p->nlat, p->mmax, 0, s));
+  }
   return MSFNO_OK;
 }
 
@@ -555,8 +647,8 @@ int msfno_filter_forward(const msfno_block_desc* d, msfno_sht_plan_t f, msfno_sh
   BlockBufs b;
   carve_block(cv, b, d, f, g, B, false);
   MSFNO_TRY(run_spectral(d, f, g, b, x, B, false, s));
-  const int64_t BC = (int64_t)B * d->C;
-  MSFNO_TRY(launch_fft_c2r_rows(g->fft, b.Yn, y, nullptr, BC * g->nlat, g->mmax, 0, s));
+  MSFNO_TRY(run_inverse_fft(g, b, B, d->C, y, nullptr, nullptr, 0, s));
+  prof(ST_END, s);
   return MSFNO_OK;
 }
 
@@ -582,35 +674,35 @@ int msfno_block_forward(const msfno_block_desc* d, msfno_sht_plan_t f, msfno_sht
   const int64_t P = (int64_t)g->nlat * g->nlon;
   const int act = d->filter_type == MSFNO_FILTER_LINEAR ? 1 : 0;  // GELU after skip (linear only)
 
-  MSFNO_TRY(run_spectral(d, f, g, b, x, B, true, s));
-
-  // ---- inner skip + activation -> x1 (with norm1 partial statistics) -----------
-  int64_t np = 0, cnt = 0, cnt_last = 0;
+  // ---- inner skip 1x1 conv first (depends only on x): x1 = Ws·x + bs ----------
   float* x1 = b.x1;
-  prof(ST_FFT_INV, s);
-  if (d->inner_skip == MSFNO_SKIP_NONE) {
-    MSFNO_TRY(launch_fft_c2r_rows(g->fft, b.Yn, x1, b.st1, BC * g->nlat, g->mmax, act, s));
-    np = g->nlat; cnt = cnt_last = g->nlon;
-  } else {
-    MSFNO_TRY(launch_fft_c2r_rows(g->fft, b.Yn, b.filt, nullptr, BC * g->nlat, g->mmax, 0, s));
-    prof(ST_SKIP, s);
-    if (d->inner_skip == MSFNO_SKIP_LINEAR) {
-      MSFNO_REQUIRE(d->skip_w, MSFNO_EINVAL, "missing inner_skip weight");
-      np = cdiv(P, kStatTile);
-      GemmEpi e;
-      e.bias = d->skip_b;
-      e.addend = b.filt; e.sD = C * P; e.ldd = (int)P;
-      e.act = act;
-      e.stats = b.st1; e.sStats = C * np; e.stats_ld = (int)np;
-      MSFNO_TRY(gemm_uniform(TILE_128x128, d->skip_w, x, x1, (int)C, (int)P, (int)C, (int)C,
-                             (int)P, (int)P, 0, C * P, C * P, B, e, s));
-      cnt = kStatTile; cnt_last = P - (np - 1) * kStatTile;
-    } else {
-      np = cdiv(P, 1024);
-      MSFNO_TRY(launch_affine_rows(b.filt, nullptr, nullptr, x, x1, BC, P, act, b.st1, (int)np, s));
-      cnt = 1024; cnt_last = P - (np - 1) * 1024;
+  SideCtx* side = nullptr;
+  if (d->inner_skip == MSFNO_SKIP_LINEAR) {
+    MSFNO_REQUIRE(d->skip_w, MSFNO_EINVAL, "missing inner_skip weight");
+    MSFNO_TRY(side_ctx(&side));
+    hipStream_t ss = s;
+    if (side) {  // fork
+      MSFNO_CHECK_HIP(hipEventRecord(side->fork, s));
+      MSFNO_CHECK_HIP(hipStreamWaitEvent(side->side, side->fork, 0));
+      ss = side->side;
+    }
+    prof(ST_SKIP, ss);
+    GemmEpi e;
+    e.bias = d->skip_b;
+    MSFNO_TRY(gemm_uniform(TILE_128x128, d->skip_w, x, x1, (int)C, (int)P, (int)C, (int)C,
+                           (int)P, (int)P, 0, C * P, C * P, B, e, ss));
+    if (side) {
+      prof(ST_END, ss);
+      MSFNO_CHECK_HIP(hipEventRecord(side->join, ss));
     }
   }
+  MSFNO_TRY(run_spectral(d, f, g, b, x, B, true, s));
+  if (side) MSFNO_CHECK_HIP(hipStreamWaitEvent(s, side->join, 0));  // join
+  // ---- filter output + skip (+ GELU for the linear filter) -> x1, norm1 partials ---
+  const float* skip_src = d->inner_skip == MSFNO_SKIP_LINEAR ? x1
+                          : (d->inner_skip == MSFNO_SKIP_IDENTITY ? x : nullptr);
+  MSFNO_TRY(run_inverse_fft(g, b, B, (int)C, x1, skip_src, b.st1, act, s));
+  const int64_t np = g->nlat, cnt = g->nlon, cnt_last = g->nlon;
   // ---- norm1 (+ FiLM) as a per-(b,c) affine --------------------------------------
   prof(ST_NORM1, s);
   MSFNO_TRY(launch_chan_affine(b.st1, np, cnt, cnt_last, B, (int)C, d->norm1_w, d->norm1_b,
@@ -622,15 +714,18 @@ int msfno_block_forward(const msfno_block_desc* d, msfno_sht_plan_t f, msfno_sht
     MSFNO_TRY(launch_fold_affine(d->fc1_w, d->fc1_b, b.sc1, b.sh1, b.W1f, b.b1f, B, (int)Hd,
                                  (int)C, s));
     prof(ST_FC1, s);
-    GemmEpi e1;
-    e1.bias = b.b1f; e1.sBias = Hd; e1.act = 1;
+    GemmEpi e1;  // pre-activation h = W1'·x1 + b1' (GELU is applied when fc2 stages h)
+    e1.bias = b.b1f; e1.sBias = Hd;
     MSFNO_TRY(gemm_uniform(TILE_128x128, b.W1f, x1, b.h, (int)Hd, (int)P, (int)C, (int)C, (int)P,
                            (int)P, Hd * C, C * P, Hd * P, B, e1, s));
     prof(ST_FC2, s);
     GemmEpi e2;
+    e2.act = 2;
     e2.bias = d->fc2_b;
     if (resid) { e2.addend = resid; e2.sD = C * P; e2.ldd = (int)P; }
-    MSFNO_TRY(gemm_uniform(TILE_128x128, d->fc2_w, b.h, out, (int)C, (int)P, (int)Hd, (int)Hd,
+    // one M tile for C <= 256, so every h element is GELU'd exactly once while staged
+    const GemmTile t2 = C <= 256 && C > 128 ? TILE_256x64 : TILE_128x128;
+    MSFNO_TRY(gemm_uniform(t2, d->fc2_w, b.h, out, (int)C, (int)P, (int)Hd, (int)Hd,
                            (int)P, (int)P, 0, Hd * P, C * P, B, e2, s));
   } else {
     prof(ST_OUT_AFFINE, s);
@@ -652,16 +747,18 @@ const char* msfno_profile_stage_name(int stage) {
 
 int msfno_profile_collect(double* total_ms, int* counts) {
   auto& mk = g_prof.marks;
-  if (!mk.empty()) MSFNO_CHECK_HIP(hipEventSynchronize(mk.back().second));
-  for (size_t i = 0; i + 1 < mk.size(); ++i) {
-    const int st = mk[i].first;
-    if (st == ST_END) continue;
+  for (auto& m : mk) MSFNO_CHECK_HIP(hipEventSynchronize(m.ev));
+  for (size_t i = 0; i < mk.size(); ++i) {
+    if (mk[i].stage == ST_END) continue;
+    size_t j = i + 1;
+    while (j < mk.size() && mk[j].stream != mk[i].stream) ++j;
+    if (j == mk.size()) continue;
     float ms = 0.f;
-    MSFNO_CHECK_HIP(hipEventElapsedTime(&ms, mk[i].second, mk[i + 1].second));
-    if (total_ms) total_ms[st] += ms;
-    if (counts) counts[st] += 1;
+    MSFNO_CHECK_HIP(hipEventElapsedTime(&ms, mk[i].ev, mk[j].ev));
+    if (total_ms) total_ms[mk[i].stage] += ms;
+    if (counts) counts[mk[i].stage] += 1;
   }
-  for (auto& p : mk) g_prof.pool.push_back(p.second);
+  for (auto& m : mk) g_prof.pool.push_back(m.ev);
   mk.clear();
   return MSFNO_OK;
 }

@@ -96,7 +96,7 @@ struct GemmDesc {
   int lda, ldb, ldc;
   int tiles_m, tiles_n;
   int tile_start;
-  int pad_;
+  int flags;  // bit 0: apply GemmEpi::rowscale (Legendre-forward m >= 1)
 };
 
 struct GemmEpi {
@@ -105,12 +105,14 @@ struct GemmEpi {
   float2* stats = nullptr;          // per (row, tile_n) partial (mean, M2) (batch stride sStats)
   int64_t sBias = 0, sD = 0, sStats = 0;
   int ldd = 0;
-  int act = 0;                      // 0 none, 1 GELU(erf)
+  int act = 0;                      // 0 none, 1 GELU(erf) on C, 2 GELU(erf) on B while staged
   int relu_period = 0, relu_rows = 0;  // ReLU rows where (row % period) < relu_rows
   int stats_ld = 0;                 // partials per row
+  const float* rowscale = nullptr;  // per-(b,c) factor for rows r=(b,ri,c); C = rs_C
+  int rs_C = 0;
 };
 
-enum GemmTile { TILE_128x128 = 0, TILE_128x64 = 1, TILE_64x64 = 2 };
+enum GemmTile { TILE_128x128 = 0, TILE_128x64 = 1, TILE_64x64 = 2, TILE_256x64 = 3 };
 
 // C[M,N] = A[M,K] · B[K,N] (+ epilogue), row-major, fp32 MFMA.
 // Uniform batched mode: batch index = grid.z, operand batch strides sA/sB/sC.

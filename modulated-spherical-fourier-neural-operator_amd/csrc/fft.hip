@@ -11,6 +11,7 @@
 // pass over HBM; the inverse kernel can apply GELU and emit output-row stats.
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 
 #include "kernels.h"
 
@@ -34,6 +35,36 @@ template <bool INV>
 __device__ __forceinline__ float2 mul_mi(float2 a) {
   return INV ? make_float2(-a.y, a.x) : make_float2(a.y, -a.x);
 }
+
+// e^{∓2πi t/R} for the internal twiddles of the nested radix-16 / radix-9 butterflies
+template <int R, bool INV>
+__device__ __forceinline__ float2 root(int t) {
+  float c = 1.f, sn = 0.f;
+  if constexpr (R == 16) {
+    constexpr float C1 = 0.92387953251128675613f, S1 = 0.38268343236508977173f;
+    constexpr float R2 = 0.70710678118654752440f;
+    switch (t) {
+      case 1: c = C1; sn = S1; break;
+      case 2: c = R2; sn = R2; break;
+      case 3: c = S1; sn = C1; break;
+      case 4: c = 0.f; sn = 1.f; break;
+      case 6: c = -R2; sn = R2; break;
+      case 9: c = -C1; sn = -S1; break;
+      default: break;
+    }
+  } else {  // R == 9
+    switch (t) {
+      case 1: c = 0.76604444311897803520f; sn = 0.64278760968653932632f; break;
+      case 2: c = 0.17364817766693034885f; sn = 0.98480775301220805936f; break;
+      case 4: c = -0.93969262078590838405f; sn = 0.34202014332566873304f; break;
+      default: break;
+    }
+  }
+  return make_float2(c, INV ? sn : -sn);
+}
+
+template <int R, bool INV>
+__device__ __forceinline__ void butterfly(float2 (&v)[R], const float2* twH, int H);
 
 template <int R, bool INV>
 __device__ __forceinline__ void butterfly(float2 (&v)[R], const float2* twH, int H) {
@@ -72,6 +103,29 @@ __device__ __forceinline__ void butterfly(float2 (&v)[R], const float2* twH, int
     v[4] = csub(a1, b1);
     v[2] = cadd(a2, b2);
     v[3] = csub(a2, b2);
+  } else if constexpr (R == 16 || R == 9) {
+    // R = P·P: inner P-point DFTs over a (stride P), internal twiddles W_R^{b·k1},
+    // outer P-point DFTs over b.  Output index k1 + P·k2.
+    constexpr int P = R == 16 ? 4 : 3;
+    float2 y[P][P];  // y[b][k1]
+#pragma unroll
+    for (int b = 0; b < P; ++b) {
+      float2 t[P];
+#pragma unroll
+      for (int a = 0; a < P; ++a) t[a] = v[P * a + b];
+      butterfly<P, INV>(t, twH, H);
+#pragma unroll
+      for (int k1 = 0; k1 < P; ++k1) y[b][k1] = (b * k1 == 0) ? t[k1] : cmul(t[k1], root<R, INV>(b * k1));
+    }
+#pragma unroll
+    for (int k1 = 0; k1 < P; ++k1) {
+      float2 t[P];
+#pragma unroll
+      for (int b = 0; b < P; ++b) t[b] = y[b][k1];
+      butterfly<P, INV>(t, twH, H);
+#pragma unroll
+      for (int k2 = 0; k2 < P; ++k2) v[k1 + P * k2] = t[k2];
+    }
   } else {
     // generic small prime: y_q = Σ_r v_r·w_q^r by Horner's rule (one root per output)
     float2 y[R];
@@ -90,6 +144,44 @@ __device__ __forceinline__ void butterfly(float2 (&v)[R], const float2* twH, int
     }
 #pragma unroll
     for (int q = 0; q < R; ++q) v[q] = y[q];
+  }
+}
+
+// v[r] *= w^r with w = tw[idx]: the powers are built from one table read (two
+// for R = P·P: w and w^P), at most three complex products per factor.
+template <int R, bool INV>
+__device__ __forceinline__ void apply_twiddles(float2 (&v)[R], const float2* tw, int idx) {
+  float2 w1 = tw[idx];
+  if (INV) w1.y = -w1.y;
+  if constexpr (R == 16 || R == 9) {
+    constexpr int P = R == 16 ? 4 : 3;
+    float2 wp = tw[P * idx];
+    if (INV) wp.y = -wp.y;
+    float2 pb[P], pa[P];  // w^b, (w^P)^a
+    pb[0] = make_float2(1.f, 0.f);
+    pa[0] = make_float2(1.f, 0.f);
+    pb[1] = w1;
+    pa[1] = wp;
+#pragma unroll
+    for (int e = 2; e < P; ++e) {
+      pb[e] = cmul(pb[e - 1], w1);
+      pa[e] = cmul(pa[e - 1], wp);
+    }
+#pragma unroll
+    for (int a = 0; a < P; ++a)
+#pragma unroll
+      for (int b = 0; b < P; ++b) {
+        if (a == 0 && b == 0) continue;
+        const float2 wr = a == 0 ? pb[b] : (b == 0 ? pa[a] : cmul(pa[a], pb[b]));
+        v[P * a + b] = cmul(v[P * a + b], wr);
+      }
+  } else {
+    float2 wr = w1;
+#pragma unroll
+    for (int r = 1; r < R; ++r) {
+      if (r > 1) wr = (r == 2) ? cmul(w1, w1) : cmul(wr, w1);
+      v[r] = cmul(v[r], wr);
+    }
   }
 }
 
@@ -117,14 +209,7 @@ __device__ __forceinline__ void stockham_pass_inplace(float2* buf, int H, int Ns
     const int j = lane + 64 * it;
     if (j < nb) {
       const int k = j % Ns;
-      if (Ns > 1) {
-#pragma unroll
-        for (int r = 1; r < R; ++r) {
-          float2 w = tw[r * k * step];
-          if (INV) w.y = -w.y;
-          v[it][r] = cmul(v[it][r], w);
-        }
-      }
+      if (Ns > 1) apply_twiddles<R, INV>(v[it], tw, k * step);
       butterfly<R, INV>(v[it], tw, H);
     }
   }
@@ -179,7 +264,7 @@ struct FixedFFT {
   static constexpr int H = (Rs * ...);
   static constexpr int kBufs = 1;
   template <bool INV>
-  __device__ static void run(float2* buf, float2*, const struct FFTArgs&, const float2* tw,
+  __device__ __forceinline__ static void run(float2* buf, float2*, const struct FFTArgs&, const float2* tw,
                              int lane) {
     int Ns = 1;
     ((stockham_pass_inplace<Rs, pass_iters(H, Rs), INV>(buf, H, Ns, tw, lane), Ns *= Rs), ...);
@@ -190,7 +275,7 @@ struct GenericFFT {
   static constexpr int H = 0;  // runtime
   static constexpr int kBufs = 2;
   template <bool INV>
-  __device__ static void run(float2* buf, float2* buf2, const struct FFTArgs& f, const float2* tw,
+  __device__ __forceinline__ static void run(float2* buf, float2* buf2, const struct FFTArgs& f, const float2* tw,
                              int lane) {
     int Ns = 1;
     float2* a = buf;
@@ -223,6 +308,7 @@ __device__ __forceinline__ float wave_sum(float v) {
 }
 
 constexpr int kWaves = 4;  // rows in flight per workgroup (one per wave)
+constexpr int kStageMax = 512;  // prefetched inverse-FFT input row (complex bins)
 
 // LDS: [twiddles (H)] [per-wave row buffer (H) x kWaves]
 __device__ __forceinline__ void load_twiddles(float2* tw, const FFTArgs& f) {
@@ -246,11 +332,38 @@ __global__ __launch_bounds__(256) void fft_r2c_rows_kernel(const float* __restri
   float2* buf = smem + H + (size_t)w * per;
   float2* buf2 = buf + H;
   load_twiddles(tw, f);
-  for (int64_t row = (int64_t)blockIdx.x * kWaves + w; row < rows;
-       row += (int64_t)gridDim.x * kWaves) {
+  constexpr int NV = CL::H > 0 ? (CL::H / 2 + 63) / 64 : 1;  // float4 per lane per row
+  float4 pf[NV];
+  const int64_t stride = (int64_t)gridDim.x * kWaves;
+  auto fetch = [&](int64_t r) {
+    if constexpr (CL::H > 0) {
+      if (r < rows) {
+        const float4* x4 = reinterpret_cast<const float4*>(x + r * (2 * CL::H));
+#pragma unroll
+        for (int j = 0; j < NV; ++j) {
+          const int n = lane + 64 * j;
+          if (n < CL::H / 2) pf[j] = x4[n];
+        }
+      }
+    }
+  };
+  fetch((int64_t)blockIdx.x * kWaves + w);
+  for (int64_t row = (int64_t)blockIdx.x * kWaves + w; row < rows; row += stride) {
     const float* xr = x + row * N;
     float s = 0.f;
-    if (f.packed) {
+    if constexpr (CL::H > 0) {  // codelet: rows arrive through the register prefetch
+#pragma unroll
+      for (int j = 0; j < NV; ++j) {
+        const int n = lane + 64 * j;
+        if (n < CL::H / 2) {
+          const float4 v = pf[j];
+          buf[2 * n] = make_float2(v.x, v.y);
+          buf[2 * n + 1] = make_float2(v.z, v.w);
+          s += (v.x + v.y) + (v.z + v.w);
+        }
+      }
+      fetch(row + stride);
+    } else if (f.packed) {
       if ((N & 3) == 0) {
         const float4* x4 = reinterpret_cast<const float4*>(xr);
         for (int n = lane; n < N / 4; n += 64) {
@@ -318,7 +431,7 @@ __device__ __forceinline__ float gelu_erf_f(float v) {
 
 template <class CL>
 __global__ __launch_bounds__(256) void fft_c2r_rows_kernel(const float2* __restrict__ in,
-                                                           float* __restrict__ x,
+                                                           float* x, const float* addsrc,
                                                            float2* __restrict__ rowstats,
                                                            int64_t rows, int mmax, int act,
                                                            FFTArgs f) {
@@ -328,13 +441,39 @@ __global__ __launch_bounds__(256) void fft_c2r_rows_kernel(const float2* __restr
   const int H = CL::H > 0 ? CL::H : f.H;
   const int N = f.N;
   float2* tw = smem;
-  const int per = CL::kBufs * H;
+  // per wave: FFT buffer(s) + (codelets) a staging row for the prefetched input
+  const int per = CL::kBufs * H + (CL::H > 0 ? kStageMax : 0);
   float2* buf = smem + H + (size_t)w * per;
   float2* buf2 = buf + H;
+  float2* stage = buf + CL::kBufs * H;
   load_twiddles(tw, f);
-  for (int64_t row = (int64_t)blockIdx.x * kWaves + w; row < rows;
-       row += (int64_t)gridDim.x * kWaves) {
+  constexpr int NVI = kStageMax / 64;
+  float2 pf[NVI];
+  const int64_t stride = (int64_t)gridDim.x * kWaves;
+  const bool use_pf = CL::H > 0 && mmax <= kStageMax;
+  auto fetch = [&](int64_t r) {
+    if (use_pf && r < rows) {
+      const float2* yr = in + r * mmax;
+#pragma unroll
+      for (int j = 0; j < NVI; ++j) {
+        const int k = lane + 64 * j;
+        if (k < mmax) pf[j] = yr[k];
+      }
+    }
+  };
+  fetch((int64_t)blockIdx.x * kWaves + w);
+  for (int64_t row = (int64_t)blockIdx.x * kWaves + w; row < rows; row += stride) {
     const float2* yr = in + row * mmax;
+    if (use_pf) {
+#pragma unroll
+      for (int j = 0; j < NVI; ++j) {
+        const int k = lane + 64 * j;
+        if (k < mmax) stage[k] = pf[j];
+      }
+      fetch(row + stride);
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+      yr = stage;
+    }
     if (f.packed) {
       for (int k = lane; k < H; k += 64) {
         float2 xk = k < mmax ? yr[k] : make_float2(0.f, 0.f);
@@ -363,15 +502,22 @@ __global__ __launch_bounds__(256) void fft_c2r_rows_kernel(const float2* __restr
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
     CL::template run<true>(buf, buf2, f, tw, lane);
     float* xo = x + row * N;
+    const float* ao = addsrc ? addsrc + row * N : nullptr;
     float s = 0.f;
     if (f.packed) {
       if ((N & 3) == 0) {
         float4* x4 = reinterpret_cast<float4*>(xo);
         for (int n = lane; n < N / 4; n += 64) {
           float2 a = buf[2 * n], b = buf[2 * n + 1];
-          if (act == 1) {
-            a.x = gelu_erf_f(a.x); a.y = gelu_erf_f(a.y);
-            b.x = gelu_erf_f(b.x); b.y = gelu_erf_f(b.y);
+          if (ao) {  // skip branch: x1 = act(x1_skip + filter)
+            const float4 r = reinterpret_cast<const float4*>(ao)[n];
+            a.x += r.x; a.y += r.y; b.x += r.z; b.y += r.w;
+          }
+          if (act == 1 || ao) {
+            if (act == 1) {
+              a.x = gelu_erf_f(a.x); a.y = gelu_erf_f(a.y);
+              b.x = gelu_erf_f(b.x); b.y = gelu_erf_f(b.y);
+            }
             buf[2 * n] = a;
             buf[2 * n + 1] = b;
           }
@@ -382,7 +528,9 @@ __global__ __launch_bounds__(256) void fft_c2r_rows_kernel(const float2* __restr
         float2* x2 = reinterpret_cast<float2*>(xo);
         for (int n = lane; n < H; n += 64) {
           float2 v = buf[n];
-          if (act == 1) { v.x = gelu_erf_f(v.x); v.y = gelu_erf_f(v.y); buf[n] = v; }
+          if (ao) { v.x += ao[2 * n]; v.y += ao[2 * n + 1]; }
+          if (act == 1) { v.x = gelu_erf_f(v.x); v.y = gelu_erf_f(v.y); }
+          buf[n] = v;
           x2[n] = v;
           s += v.x + v.y;
         }
@@ -390,7 +538,9 @@ __global__ __launch_bounds__(256) void fft_c2r_rows_kernel(const float2* __restr
     } else {
       for (int n = lane; n < N; n += 64) {
         float v = buf[n].x;
-        if (act == 1) { v = gelu_erf_f(v); buf[n].x = v; }
+        if (ao) v += ao[n];
+        if (act == 1) v = gelu_erf_f(v);
+        buf[n].x = v;
         xo[n] = v;
         s += v;
       }
@@ -412,6 +562,216 @@ __global__ __launch_bounds__(256) void fft_c2r_rows_kernel(const float2* __restr
       }
       q = wave_sum(q);
       if (lane == 0) rowstats[row] = make_float2(mean, q);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Fused FFT + transpose kernels (the block's path).  A workgroup owns TK
+// consecutive latitudes of one (b,c) plane; each wave transforms TK/4 rows with
+// the next row's global loads in flight (register prefetch) while it computes.
+//   forward: x rows -> LDS tile [m][TK] -> Xt[m][(b,ri,c)][k0..k0+TK)   (m-major
+//            GEMM operand of the Legendre stage; spectrum NOT normalised: the
+//            InstanceNorm-0 affine is applied later, see dc_fixup / GEMM rowscale)
+//   inverse: Yt[m][(b,ri,c)][k0..) -> LDS tile [m][TK] -> irfft rows -> output
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ int xcd_remap_1d(int orig, int nwg) {
+  const int xcd = orig & 7;
+  const int q = nwg >> 3, r = nwg & 7;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
+}
+
+// LDS tile: separate real / imaginary planes [mmax][TK + pad] so that four
+// consecutive latitudes move as one float4 between LDS and HBM.
+template <int TK>
+struct TileGeom {
+  static constexpr int TS = TK + 4;  // plane row stride (floats), keeps float4 alignment
+};
+
+template <class CL, int TK>
+__global__ __launch_bounds__(256) void fft_r2c_tile_kernel(const float* __restrict__ x,
+                                                           float* __restrict__ Xt,
+                                                           float2* __restrict__ rowstats, int C,
+                                                           int nlat, int mmax, int ldk, int64_t R,
+                                                           int ntiles, float scale, FFTArgs f) {
+  extern __shared__ float2 smem[];
+  constexpr int H = CL::H;
+  constexpr int N = 2 * H;
+  constexpr int NV = (N / 4 + 63) / 64;
+  constexpr int TS = TileGeom<TK>::TS;
+  const int lane = threadIdx.x & 63;
+  const int w = threadIdx.x >> 6;
+  float2* tw = smem;
+  float* pre = reinterpret_cast<float*>(smem + H);
+  float* pim = pre + (size_t)mmax * TS;
+  float2* buf = reinterpret_cast<float2*>(pim + (size_t)mmax * TS) + (size_t)w * H;
+  load_twiddles(tw, f);
+  const int lin = xcd_remap_1d(blockIdx.x, gridDim.x);
+  const int tile = lin % ntiles;
+  const int bc = lin / ntiles;
+  const int k0 = tile * TK;
+  const float4* plane = reinterpret_cast<const float4*>(x + (int64_t)bc * nlat * N);
+  float4 pf[NV];
+  auto prefetch = [&](int kk) {
+    const int k = k0 + kk;
+    if (kk < TK && k < nlat) {
+      const float4* r4 = plane + (int64_t)k * (N / 4);
+#pragma unroll
+      for (int j = 0; j < NV; ++j) {
+        const int n = lane + 64 * j;
+        if (n < N / 4) pf[j] = r4[n];
+      }
+    }
+  };
+  prefetch(w);
+  for (int kk = w; kk < TK && k0 + kk < nlat; kk += 4) {
+    const int k = k0 + kk;
+    float s = 0.f;
+#pragma unroll
+    for (int j = 0; j < NV; ++j) {
+      const int n = lane + 64 * j;
+      if (n < N / 4) {
+        const float4 v = pf[j];
+        buf[2 * n] = make_float2(v.x, v.y);
+        buf[2 * n + 1] = make_float2(v.z, v.w);
+        s += (v.x + v.y) + (v.z + v.w);
+      }
+    }
+    prefetch(kk + 4);
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    if (rowstats) {
+      const float mean = wave_sum(s) / (float)N;
+      float q = 0.f;
+      for (int n = lane; n < H; n += 64) {
+        const float2 v = buf[n];
+        q += (v.x - mean) * (v.x - mean) + (v.y - mean) * (v.y - mean);
+      }
+      q = wave_sum(q);
+      if (lane == 0) rowstats[(int64_t)bc * nlat + k] = make_float2(mean, q);
+    }
+    CL::template run<false>(buf, nullptr, f, tw, lane);
+    for (int m = lane; m < mmax; m += 64) {
+      const float2 zk = buf[m % H];
+      const float2 zc = cconj(buf[(H - m) % H]);
+      const float2 E = make_float2(0.5f * (zk.x + zc.x), 0.5f * (zk.y + zc.y));
+      const float2 D = csub(zk, zc);
+      const float2 O = make_float2(0.5f * D.y, -0.5f * D.x);
+      const float2 X = cadd(E, cmul(f.twN[m], O));
+      pre[m * TS + kk] = scale * X.x;
+      pim[m * TS + kk] = scale * X.y;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+  }
+  __syncthreads();
+  const int b = bc / C, c = bc - b * C;
+  const int64_t rre = (int64_t)(b * 2) * C + c, rim = rre + C;
+  constexpr int Q = TK / 4;
+  const int total = mmax * 2 * Q;
+  for (int e = threadIdx.x; e < total; e += 256) {
+    const int m = e / (2 * Q);
+    const int rem = e - m * 2 * Q;
+    const int ri = rem / Q, q = rem - ri * Q;
+    const int k = k0 + 4 * q;
+    if (k < nlat) {  // k < nlat <= ldk, ldk % 4 == 0: the float4 stays inside the row
+      const float4 v = *reinterpret_cast<const float4*>((ri ? pim : pre) + m * TS + 4 * q);
+      *reinterpret_cast<float4*>(Xt + ((int64_t)m * R + (ri ? rim : rre)) * ldk + k) = v;
+    }
+  }
+}
+
+template <class CL, int TK>
+__global__ __launch_bounds__(256) void fft_c2r_tile_kernel(const float* __restrict__ Yt,
+                                                           float* __restrict__ out,
+                                                           float2* __restrict__ rowstats, int C,
+                                                           int nlat, int mmax, int mact, int ldk,
+                                                           int64_t R, int ntiles, int act,
+                                                           FFTArgs f) {
+  extern __shared__ float2 smem[];
+  constexpr int H = CL::H;
+  constexpr int N = 2 * H;
+  constexpr int TS = TileGeom<TK>::TS;
+  const int lane = threadIdx.x & 63;
+  const int w = threadIdx.x >> 6;
+  float2* tw = smem;
+  float* pre = reinterpret_cast<float*>(smem + H);
+  float* pim = pre + (size_t)mmax * TS;
+  float2* buf = reinterpret_cast<float2*>(pim + (size_t)mmax * TS) + (size_t)w * H;
+  const int lin = xcd_remap_1d(blockIdx.x, gridDim.x);
+  const int tile = lin % ntiles;
+  const int bc = lin / ntiles;
+  const int k0 = tile * TK;
+  const int b = bc / C, c = bc - b * C;
+  const int64_t rre = (int64_t)(b * 2) * C + c, rim = rre + C;
+  for (int t = threadIdx.x; t < H; t += 256) tw[t] = f.twH[t];
+  constexpr int Q = TK / 4;
+  const int total = mmax * 2 * Q;
+  // all loads of the tile issued before any LDS write (kLoadBatch in flight per lane)
+  constexpr int kLoadBatch = 8;
+  for (int e0 = 0; e0 < total; e0 += 256 * kLoadBatch) {
+    float4 v[kLoadBatch];
+#pragma unroll
+    for (int u = 0; u < kLoadBatch; ++u) {
+      const int e = e0 + u * 256 + threadIdx.x;
+      const int m = e / (2 * Q);
+      const int rem = e - m * 2 * Q;
+      const int ri = rem / Q, q = rem - ri * Q;
+      const int k = k0 + 4 * q;
+      v[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (e < total && k < nlat && m < mact)
+        v[u] = *reinterpret_cast<const float4*>(Yt + ((int64_t)m * R + (ri ? rim : rre)) * ldk + k);
+    }
+#pragma unroll
+    for (int u = 0; u < kLoadBatch; ++u) {
+      const int e = e0 + u * 256 + threadIdx.x;
+      if (e < total) {
+        const int m = e / (2 * Q);
+        const int rem = e - m * 2 * Q;
+        const int ri = rem / Q, q = rem - ri * Q;
+        *reinterpret_cast<float4*>((ri ? pim : pre) + m * TS + 4 * q) = v[u];
+      }
+    }
+  }
+  __syncthreads();
+  for (int kk = w; kk < TK && k0 + kk < nlat; kk += 4) {
+    const int k = k0 + kk;
+    for (int q = lane; q < H; q += 64) {
+      float2 xk = q < mmax ? make_float2(pre[q * TS + kk], pim[q * TS + kk]) : make_float2(0.f, 0.f);
+      if (q == 0) xk.y = 0.f;
+      const int q2 = H - q;
+      float2 xh = q2 < mmax ? make_float2(pre[q2 * TS + kk], pim[q2 * TS + kk]) : make_float2(0.f, 0.f);
+      if (q2 == H || q2 == 0) xh.y = 0.f;
+      const float2 xc = cconj(xh);
+      const float2 A = cadd(xk, xc);
+      const float2 D = csub(xk, xc);
+      const float2 T = cmul(cconj(f.twN[q]), D);
+      buf[q] = make_float2(A.x - T.y, A.y + T.x);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    CL::template run<true>(buf, nullptr, f, tw, lane);
+    float4* o4 = reinterpret_cast<float4*>(out + ((int64_t)bc * nlat + k) * N);
+    float s = 0.f;
+    for (int n = lane; n < N / 4; n += 64) {
+      float2 a = buf[2 * n], bb = buf[2 * n + 1];
+      if (act == 1) {
+        a.x = gelu_erf_f(a.x); a.y = gelu_erf_f(a.y);
+        bb.x = gelu_erf_f(bb.x); bb.y = gelu_erf_f(bb.y);
+        buf[2 * n] = a;
+        buf[2 * n + 1] = bb;
+      }
+      o4[n] = make_float4(a.x, a.y, bb.x, bb.y);
+      s += (a.x + a.y) + (bb.x + bb.y);
+    }
+    if (rowstats) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+      const float mean = wave_sum(s) / (float)N;
+      float q = 0.f;
+      for (int n = lane; n < H; n += 64) {
+        const float2 v = buf[n];
+        q += (v.x - mean) * (v.x - mean) + (v.y - mean) * (v.y - mean);
+      }
+      q = wave_sum(q);
+      if (lane == 0) rowstats[(int64_t)bc * nlat + k] = make_float2(mean, q);
     }
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
   }
@@ -457,12 +817,14 @@ static int launch_r2c(const FFTArgs& a, const float* x, float2* out, float2* row
 }
 
 template <class CL>
-static int launch_c2r(const FFTArgs& a, const float2* in, float* x, float2* rowstats,
-                      int64_t rows, int mmax, int act, hipStream_t s) {
-  const size_t lds = (size_t)(kWaves * CL::kBufs + 1) * a.H * sizeof(float2);
+static int launch_c2r(const FFTArgs& a, const float2* in, float* x, const float* addsrc,
+                      float2* rowstats, int64_t rows, int mmax, int act, hipStream_t s) {
+  const size_t lds =
+      ((size_t)(kWaves * CL::kBufs + 1) * a.H + (CL::H > 0 ? kWaves * kStageMax : 0)) *
+      sizeof(float2);
   MSFNO_REQUIRE(lds <= 64 * 1024, MSFNO_EUNSUPPORTED, "nlon too large for the LDS FFT");
   hipLaunchKernelGGL((fft_c2r_rows_kernel<CL>), dim3((unsigned)fft_grid(rows)), dim3(256), lds, s,
-                     in, x, rowstats, rows, mmax, act, a);
+                     in, x, addsrc, rowstats, rows, mmax, act, a);
   return launch_check("fft_c2r_rows");
 }
 
@@ -479,26 +841,111 @@ int launch_fft_r2c_rows(const FFTPlan& f, const float* x, float2* out, float2* r
   }
 }
 
-int launch_fft_c2r_rows(const FFTPlan& f, const float2* in, float* x, float2* rowstats,
-                        int64_t rows, int mmax, int act, hipStream_t s) {
+int launch_fft_c2r_rows(const FFTPlan& f, const float2* in, float* x, const float* addsrc,
+                        float2* rowstats, int64_t rows, int mmax, int act, hipStream_t s) {
   if (rows <= 0) return MSFNO_OK;
   const FFTArgs a = make_args(f);
   switch (f.codelet) {
 #define X(id, CL) \
-  case id: return launch_c2r<CL>(a, in, x, rowstats, rows, mmax, act, s);
+  case id: return launch_c2r<CL>(a, in, x, addsrc, rowstats, rows, mmax, act, s);
     MSFNO_FFT_CODELETS(X)
 #undef X
-    default: return launch_c2r<GenericFFT>(a, in, x, rowstats, rows, mmax, act, s);
+    default: return launch_c2r<GenericFFT>(a, in, x, addsrc, rowstats, rows, mmax, act, s);
+  }
+}
+
+template <class CL, int TK>
+static size_t tile_lds(int mmax) {
+  return (size_t)CL::H * 5 * sizeof(float2) + (size_t)2 * mmax * TileGeom<TK>::TS * sizeof(float);
+}
+
+static int set_lds_limit(const void* fn, size_t lds) {
+  if (lds > 64 * 1024)
+    MSFNO_CHECK_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  return MSFNO_OK;
+}
+
+static int tile_k() {
+  static int tk = -1;
+  if (tk < 0) {
+    const char* e = getenv("MSFNO_FFT_TK");
+    tk = (e && atoi(e) == 8) ? 8 : 16;
+  }
+  return tk;
+}
+
+template <class CL, int TK>
+static int launch_r2c_tile_t(const FFTArgs& a, const float* x, float* Xt, float2* rowstats, int B,
+                             int C, int nlat, int mmax, int ldk, float scale, hipStream_t s) {
+  const size_t lds = tile_lds<CL, TK>(mmax);
+  MSFNO_REQUIRE(lds <= 160 * 1024, MSFNO_EUNSUPPORTED, "FFT tile exceeds LDS");
+  MSFNO_TRY(set_lds_limit(reinterpret_cast<const void*>(&fft_r2c_tile_kernel<CL, TK>), lds));
+  const int ntiles = (int)cdiv(nlat, TK);
+  hipLaunchKernelGGL((fft_r2c_tile_kernel<CL, TK>), dim3((unsigned)(ntiles * B * C)), dim3(256),
+                     lds, s, x, Xt, rowstats, C, nlat, mmax, ldk, 2LL * B * C, ntiles, scale, a);
+  return launch_check("fft_r2c_tile");
+}
+
+template <class CL, int TK>
+static int launch_c2r_tile_t(const FFTArgs& a, const float* Yt, float* out, float2* rowstats,
+                             int B, int C, int nlat, int mmax, int mact, int ldk, int act,
+                             hipStream_t s) {
+  const size_t lds = tile_lds<CL, TK>(mmax);
+  MSFNO_REQUIRE(lds <= 160 * 1024, MSFNO_EUNSUPPORTED, "FFT tile exceeds LDS");
+  MSFNO_TRY(set_lds_limit(reinterpret_cast<const void*>(&fft_c2r_tile_kernel<CL, TK>), lds));
+  const int ntiles = (int)cdiv(nlat, TK);
+  hipLaunchKernelGGL((fft_c2r_tile_kernel<CL, TK>), dim3((unsigned)(ntiles * B * C)), dim3(256),
+                     lds, s, Yt, out, rowstats, C, nlat, mmax, mact, ldk, 2LL * B * C, ntiles, act,
+                     a);
+  return launch_check("fft_c2r_tile");
+}
+
+template <class CL>
+static int launch_r2c_tile(const FFTArgs& a, const float* x, float* Xt, float2* rowstats, int B,
+                           int C, int nlat, int mmax, int ldk, float scale, hipStream_t s) {
+  return tile_k() == 8
+             ? launch_r2c_tile_t<CL, 8>(a, x, Xt, rowstats, B, C, nlat, mmax, ldk, scale, s)
+             : launch_r2c_tile_t<CL, 16>(a, x, Xt, rowstats, B, C, nlat, mmax, ldk, scale, s);
+}
+
+template <class CL>
+static int launch_c2r_tile(const FFTArgs& a, const float* Yt, float* out, float2* rowstats,
+                           int B, int C, int nlat, int mmax, int mact, int ldk, int act,
+                           hipStream_t s) {
+  return tile_k() == 8
+             ? launch_c2r_tile_t<CL, 8>(a, Yt, out, rowstats, B, C, nlat, mmax, mact, ldk, act, s)
+             : launch_c2r_tile_t<CL, 16>(a, Yt, out, rowstats, B, C, nlat, mmax, mact, ldk, act, s);
+}
+
+bool fft_tile_supported(const FFTPlan& f) { return f.codelet != 0 && (f.N % 4) == 0; }
+
+int launch_fft_r2c_tile(const FFTPlan& f, const float* x, float* Xt, float2* rowstats, int B,
+                        int C, int nlat, int mmax, int ldk, float scale, hipStream_t s) {
+  const FFTArgs a = make_args(f);
+  switch (f.codelet) {
+#define X(id, CL) \
+  case id: return launch_r2c_tile<CL>(a, x, Xt, rowstats, B, C, nlat, mmax, ldk, scale, s);
+    MSFNO_FFT_CODELETS(X)
+#undef X
+    default: set_error("no FFT codelet for this nlon"); return MSFNO_EUNSUPPORTED;
+  }
+}
+
+int launch_fft_c2r_tile(const FFTPlan& f, const float* Yt, float* out, float2* rowstats, int B,
+                        int C, int nlat, int mmax, int mact, int ldk, int act, hipStream_t s) {
+  const FFTArgs a = make_args(f);
+  switch (f.codelet) {
+#define X(id, CL) \
+  case id: return launch_c2r_tile<CL>(a, Yt, out, rowstats, B, C, nlat, mmax, mact, ldk, act, s);
+    MSFNO_FFT_CODELETS(X)
+#undef X
+    default: set_error("no FFT codelet for this nlon"); return MSFNO_EUNSUPPORTED;
   }
 }
 
 template <int... Rs>
 static bool matches(const FFTPlan& p, FixedFFT<Rs...>*) {
-  const int want[] = {Rs...};
-  if (p.nrad != (int)sizeof...(Rs)) return false;
-  for (int i = 0; i < p.nrad; ++i)
-    if (p.radices[i] != want[i]) return false;
-  return true;
+  return p.packed && FixedFFT<Rs...>::H == p.H;  // the codelet brings its own radix plan
 }
 
 // ---------------------------------------------------------------------------

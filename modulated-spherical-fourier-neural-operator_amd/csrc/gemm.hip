@@ -29,6 +29,8 @@ struct GemmParams {
   float2* stats;
   int64_t sBias, sD, sStats;
   int ldd, act, relu_period, relu_rows, stats_ld;
+  const float* rowscale;
+  int rs_C;
 };
 
 __device__ __forceinline__ int xcd_remap(int orig, int nwg) {
@@ -65,7 +67,8 @@ __device__ __forceinline__ float gelu_erf(float v) {
   return 0.5f * v * (1.0f + erf_fast(v * 0.70710678118654752440f));
 }
 
-enum : int { EPI_BIAS = 1, EPI_ADD = 2, EPI_GELU = 4, EPI_RELU = 8, EPI_STATS = 16 };
+// epilogue flags (+ EPI_GELU_B: GELU applied to the B operand while it is staged)
+enum : int { EPI_BIAS = 1, EPI_ADD = 2, EPI_GELU = 4, EPI_RELU = 8, EPI_STATS = 16, EPI_ROWSCALE = 32, EPI_GELU_B = 64 };
 
 template <int BM, int BN, int BK, bool VEC, int EPI>
 __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmParams p) {
@@ -93,6 +96,7 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmParams p) {
   const float* bias = p.bias;
   const float* addend = p.addend;
   float2* stats = p.stats;
+  int dflags = 0;
   if (p.descs) {
     const int lin = xcd_remap(blockIdx.x, gridDim.x);
     int lo = 0, hi = p.ndesc - 1;
@@ -103,6 +107,7 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmParams p) {
     const GemmDesc d = p.descs[lo];
     A += d.offA; B += d.offB; C += d.offC;
     M = d.M; N = d.N; K = d.K; lda = d.lda; ldb = d.ldb; ldc = d.ldc;
+    dflags = d.flags;
     const int local = lin - d.tile_start;
     tm = local % d.tiles_m;
     tn = local / d.tiles_m;
@@ -182,11 +187,11 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmParams p) {
       const int col = (idx % (BN / 4)) * 4;
       const bool kok = k0 + kr < K;
       const int cg = n0 + col;
-      float4 v;
-      v.x = (kok && cg + 0 < N) ? rb[q].x : 0.f;
-      v.y = (kok && cg + 1 < N) ? rb[q].y : 0.f;
-      v.z = (kok && cg + 2 < N) ? rb[q].z : 0.f;
-      v.w = (kok && cg + 3 < N) ? rb[q].w : 0.f;
+      float4 v = rb[q];  // (EPI_GELU_B: already transformed inside the MFMA loop)
+      v.x = (kok && cg + 0 < N) ? v.x : 0.f;
+      v.y = (kok && cg + 1 < N) ? v.y : 0.f;
+      v.z = (kok && cg + 2 < N) ? v.z : 0.f;
+      v.w = (kok && cg + 3 < N) ? v.w : 0.f;
       *reinterpret_cast<float4*>(&Bs[buf][kr * LDB_S + col]) = v;
     }
   };
@@ -201,6 +206,13 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmParams p) {
 
   if (nk > 0) {
     load_tile(0);
+    if constexpr ((EPI & EPI_GELU_B) != 0) {
+#pragma unroll
+      for (int q = 0; q < B_LD; ++q) {
+        rb[q].x = gelu_erf(rb[q].x); rb[q].y = gelu_erf(rb[q].y);
+        rb[q].z = gelu_erf(rb[q].z); rb[q].w = gelu_erf(rb[q].w);
+      }
+    }
     store_tile(0, 0);
   }
   __syncthreads();
@@ -224,6 +236,17 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmParams p) {
 #pragma unroll
         for (int j = 0; j < NT; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i], b[j], acc[i][j], 0, 0, 0);
+      if constexpr ((EPI & EPI_GELU_B) != 0) {
+        // GELU of the next B tile, issued while this tile's MFMAs drain (VALU and
+        // the matrix pipe overlap within the wave)
+        if (kk == BK / 2 - 3 && kt + 1 < nk) {
+#pragma unroll
+          for (int q = 0; q < B_LD; ++q) {
+            rb[q].x = gelu_erf(rb[q].x); rb[q].y = gelu_erf(rb[q].y);
+            rb[q].z = gelu_erf(rb[q].z); rb[q].w = gelu_erf(rb[q].w);
+          }
+        }
+      }
     }
     if (kt + 1 < nk) store_tile(cur ^ 1, kt + 1);
     __syncthreads();
@@ -233,13 +256,18 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmParams p) {
   constexpr bool kStats = (EPI & EPI_STATS) != 0;
 #pragma unroll
   for (int i = 0; i < MT; ++i) {
-    float bv[16];
+    float bv[16], sv[16];
     int rowv[16];
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int lrow = wm * WM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
       rowv[r] = m0 + lrow;
       if constexpr ((EPI & EPI_BIAS) != 0) bv[r] = bias[min(rowv[r], M - 1)];
+      if constexpr ((EPI & EPI_ROWSCALE) != 0) {
+        const int rr = min(rowv[r], M - 1);
+        const int C2 = 2 * p.rs_C;
+        sv[r] = (dflags & 1) ? p.rowscale[(rr / C2) * p.rs_C + rr % p.rs_C] : 1.f;
+      }
     }
     float s[16], sq[16];
     if constexpr (kStats) {
@@ -259,6 +287,7 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmParams p) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         float v = acc[i][j][r];
+        if constexpr ((EPI & EPI_ROWSCALE) != 0) v *= sv[r];
         if constexpr ((EPI & EPI_BIAS) != 0) v += bv[r];
         if constexpr ((EPI & EPI_ADD) != 0) v += add[r];
         if constexpr ((EPI & EPI_GELU) != 0) v = gelu_erf(v);
@@ -310,6 +339,7 @@ void gemm_tile_dims(GemmTile tile, int* bm, int* bn) {
   switch (tile) {
     case TILE_128x128: *bm = 128; *bn = 128; break;
     case TILE_128x64: *bm = 128; *bn = 64; break;
+    case TILE_256x64: *bm = 256; *bn = 64; break;
     default: *bm = 64; *bn = 64; break;
   }
 }
@@ -321,6 +351,8 @@ static GemmParams make_params(const float* A, const float* B, float* C, const Ge
   p.sBias = e.sBias; p.sD = e.sD; p.sStats = e.sStats;
   p.ldd = e.ldd; p.act = e.act; p.relu_period = e.relu_period; p.relu_rows = e.relu_rows;
   p.stats_ld = e.stats_ld;
+  p.rowscale = e.rowscale;
+  p.rs_C = e.rs_C;
   return p;
 }
 
@@ -334,7 +366,8 @@ static void launch_e(const GemmParams& p, dim3 grid, hipStream_t s) {
 
 static int epi_code(const GemmParams& p) {
   return (p.bias ? EPI_BIAS : 0) | (p.addend ? EPI_ADD : 0) | (p.act == 1 ? EPI_GELU : 0) |
-         (p.relu_period ? EPI_RELU : 0) | (p.stats ? EPI_STATS : 0);
+         (p.relu_period ? EPI_RELU : 0) | (p.stats ? EPI_STATS : 0) |
+         (p.rowscale ? EPI_ROWSCALE : 0) | (p.act == 2 ? EPI_GELU_B : 0);
 }
 
 // the epilogue combinations the block uses (anything else is rejected)
@@ -343,9 +376,13 @@ static int launch(const GemmParams& p, dim3 grid, hipStream_t s) {
   switch (epi_code(p)) {
     case 0: launch_e<BM, BN, BK, 0>(p, grid, s); break;
     case EPI_RELU: launch_e<BM, BN, BK, EPI_RELU>(p, grid, s); break;
+    case EPI_ROWSCALE: launch_e<BM, BN, BK, EPI_ROWSCALE>(p, grid, s); break;
     case EPI_BIAS: launch_e<BM, BN, BK, EPI_BIAS>(p, grid, s); break;
     case EPI_BIAS | EPI_GELU: launch_e<BM, BN, BK, EPI_BIAS | EPI_GELU>(p, grid, s); break;
     case EPI_BIAS | EPI_ADD: launch_e<BM, BN, BK, EPI_BIAS | EPI_ADD>(p, grid, s); break;
+    case EPI_GELU_B | EPI_BIAS: launch_e<BM, BN, BK, EPI_GELU_B | EPI_BIAS>(p, grid, s); break;
+    case EPI_GELU_B | EPI_BIAS | EPI_ADD:
+      launch_e<BM, BN, BK, EPI_GELU_B | EPI_BIAS | EPI_ADD>(p, grid, s); break;
     case EPI_ADD: launch_e<BM, BN, BK, EPI_ADD>(p, grid, s); break;
     case EPI_BIAS | EPI_ADD | EPI_STATS:
       launch_e<BM, BN, BK, EPI_BIAS | EPI_ADD | EPI_STATS>(p, grid, s); break;
@@ -370,6 +407,7 @@ static int dispatch(GemmTile tile, const GemmParams& p, dim3 grid, hipStream_t s
   switch (tile) {
     case TILE_128x128: rc = launch<128, 128, MSFNO_GEMM_BK>(p, grid, s); break;
     case TILE_128x64: rc = launch<128, 64, MSFNO_GEMM_BK>(p, grid, s); break;
+    case TILE_256x64: rc = launch<256, 64, MSFNO_GEMM_BK>(p, grid, s); break;
     default: rc = launch<64, 64, MSFNO_GEMM_BK>(p, grid, s); break;
   }
   if (rc != MSFNO_OK) return rc;

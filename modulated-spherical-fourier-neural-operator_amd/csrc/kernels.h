@@ -11,8 +11,21 @@ int launch_fft_r2c_rows(const FFTPlan& f, const float* x, float2* out, float2* r
                         int64_t rows, int mmax, float scale, hipStream_t s);
 // in (rows, mmax) complex (Hermitian half spectrum, zero beyond mmax) -> x (rows, N);
 // act: 0 none, 1 GELU; optional per-row (mean, M2) of the outputs.
-int launch_fft_c2r_rows(const FFTPlan& f, const float2* in, float* x, float2* rowstats,
-                        int64_t rows, int mmax, int act, hipStream_t s);
+// addsrc (may alias x): x = act(addsrc + irfft(in))  (the block's skip branch)
+int launch_fft_c2r_rows(const FFTPlan& f, const float2* in, float* x, const float* addsrc,
+                        float2* rowstats, int64_t rows, int mmax, int act, hipStream_t s);
+
+// fused FFT + transpose (block path); only for plans with a compiled codelet
+bool fft_tile_supported(const FFTPlan& f);
+// x (B*C, nlat, N) -> Xt (mmax, R=2BC, ldk) raw spectrum·scale (+ per-row (mean, M2))
+int launch_fft_r2c_tile(const FFTPlan& f, const float* x, float* Xt, float2* rowstats, int B,
+                        int C, int nlat, int mmax, int ldk, float scale, hipStream_t s);
+// Yt (mmax, R, ldk) -> out (B*C, nlat, N), GELU if act, optional output row stats
+int launch_fft_c2r_tile(const FFTPlan& f, const float* Yt, float* out, float2* rowstats, int B,
+                        int C, int nlat, int mmax, int mact, int ldk, int act, hipStream_t s);
+// m = 0 slice of Xt: v -> scale[bc]·v + 2π·shift[bc] (real rows), scale[bc]·v (imag rows)
+int launch_dc_fixup(float* Xt, int B, int C, int nlat, int ldk, const float* nscale,
+                    const float* nshift, hipStream_t s);
 
 // ---- spectral.hip ------------------------------------------------------------
 // Xn (BC, nlat, mmax) complex -> Xt (mmax, R=2BC, ldk); per-bc affine of the

@@ -53,6 +53,32 @@ __global__ __launch_bounds__(256) void transpose_fwd_kernel(const float2* __rest
   }
 }
 
+__global__ void dc_fixup_kernel(float* __restrict__ Xt, int B, int C, int nlat, int ldk,
+                                const float* __restrict__ nscale,
+                                const float* __restrict__ nshift) {
+  const int64_t R = 2LL * B * C;
+  const int64_t n = R * nlat;
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < n;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = e / nlat;
+    const int k = (int)(e - r * nlat);
+    const int b = (int)(r / (2 * C));
+    const int ri = (int)((r / C) & 1);
+    const int c = (int)(r % C);
+    const int bc = b * C + c;
+    float* p = Xt + r * ldk + k;
+    *p = ri ? nscale[bc] * *p : fmaf(nscale[bc], *p, kTwoPi * nshift[bc]);
+  }
+}
+
+int launch_dc_fixup(float* Xt, int B, int C, int nlat, int ldk, const float* nscale,
+                    const float* nshift, hipStream_t s) {
+  const int64_t n = 2LL * B * C * nlat;
+  hipLaunchKernelGGL(dc_fixup_kernel, dim3((unsigned)std::min<int64_t>(cdiv(n, 256), 4096)),
+                     dim3(256), 0, s, Xt, B, C, nlat, ldk, nscale, nshift);
+  return launch_check("dc_fixup");
+}
+
 int launch_transpose_fwd(const float2* Xn, float* Xt, int B, int C, int nlat, int mmax, int ldk,
                          const float* nscale, const float* nshift, hipStream_t s) {
   dim3 grid((unsigned)cdiv(nlat, TK), (unsigned)cdiv(mmax, TMM), (unsigned)(B * C));

@@ -57,17 +57,21 @@ int main() {
   GemmEpi plain;
   GemmEpi gelu; gelu.bias = bias; gelu.act = 1;
   GemmEpi skipe; skipe.bias = bias; skipe.addend = D; skipe.ldd = P;
+  GemmEpi fc2e; fc2e.bias = bias; fc2e.addend = D; fc2e.ldd = P;
+  GemmEpi fc2g = fc2e; fc2g.act = 2;
+  GemmEpi geluB; geluB.act = 2; geluB.bias = bias;
   float2* st; hipMalloc(&st, 256 * 8200 * 8);
   skipe.stats = st; skipe.stats_ld = 8200;
   const int T = 65536;
   struct S { const char* n; int M, N, K; GemmEpi e; };
   std::vector<S> shapes = {
-      {"fc1", 512, P, 256, gelu}, {"fc1-nogelu", 512, P, 256, plain}, {"fc2", 256, P, 512, plain}, {"skip", 256, P, 256, plain}, {"skip-epi", 256, P, 256, skipe},
-      {"spec_l1", 1024, T, 1024, plain}, {"spec_l0", 1024, T, 512, plain}};
+      {"fc2", 256, P, 512, plain}, {"fc2-badd", 256, P, 512, fc2e},
+      {"fc2-geluB", 256, P, 512, geluB}, {"fc2-full", 256, P, 512, fc2g}};
   for (auto& s : shapes) {
     const double fl = 2.0 * s.M * (double)s.N * s.K;
     run<128, 128, 16>(s.n, s.M, s.N, s.K, A, B, C, s.e, 5, fl);
     run<128, 64, 16>(s.n, s.M, s.N, s.K, A, B, C, s.e, 5, fl);
+    run<256, 64, 16>(s.n, s.M, s.N, s.K, A, B, C, s.e, 5, fl);
   }
   return 0;
 }
