@@ -7,9 +7,14 @@ FiLM on — over one synthetic 721x1440x256 field per GPU (x ~ N(0,1), seed 0),
 lmax=360/mmax=361 equiangular SHT with the reference's ×1e5 rescale, random
 init weights of that architecture (reference init recipe, seed 1).
 
-Multi-GPU (torchrun, one process per GPU): replicas — each rank runs its own
-field through the block; no data-path collective ("scaling": "weak"); the timed
-region is bracketed by barrier + synchronize and the max over ranks is used.
+Multi-GPU (torchrun, one process per GPU), "scaling": "weak" in both modes:
+  --parallel replicas (default): each rank runs its own field batch through the
+      block; no data-path collective.
+  --parallel latband: one batch of batch*N fields is latitude-band sharded over
+      the N ranks: two RCCL all-to-alls and two small
+      all-gathers per block forward (msfno_amd.sfno.LatBandBlock).
+The timed region is bracketed by barrier + synchronize and the max over ranks
+is used.
 
 Prints ONE JSON line (rank 0) with the roofline of the dominant kernel (timed
 with hipEvents on the block's stream over the timed region) and the oracle's
@@ -65,7 +70,7 @@ def pmc_traffic(stage):
     return None, None
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
@@ -79,13 +84,22 @@ def parse():
     ap.add_argument("--cpu-baseline", type=int, default=1, help="time the oracle on CPU (rank 0, N=1)")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--stages", action="store_true", help="print per-stage timings to stderr")
-    return ap.parse_args()
+    ap.add_argument("--parallel", default="replicas", choices=["replicas", "latband"],
+                    help="N>1: independent replicas (one field batch per GPU) or one batch of "
+                         "batch*N fields latitude-band sharded over the N GPUs (RCCL all-to-all)")
+    return ap.parse_args(argv)
 
 
-def stage_work(name, B, C, nlat, nlon, lmax, mmax, hid, shid):
-    """Algorithmic work per launch: ('mfma', flops) or ('hbm', bytes)."""
-    T = sum(max(lmax - m, 0) for m in range(mmax))
-    P = nlat * nlon
+parse_args = parse
+
+
+def stage_work(name, B, C, nlat, nlon, lmax, mmax, hid, shid, rows=None, mset=None):
+    """Algorithmic work per launch: ('mfma', flops) or ('hbm', bytes).  Latitude-band
+    shards: `rows` local latitude rows, `mset` the rank's zonal wavenumbers."""
+    ms = range(mmax) if mset is None else mset
+    T = sum(max(lmax - m, 0) for m in ms)
+    rows = nlat if rows is None else rows
+    P = rows * nlon
     BC = B * C
     tab = {
         "mlp_fc1": ("mfma", 2 * B * P * C * hid),
@@ -98,10 +112,10 @@ def stage_work(name, B, C, nlat, nlon, lmax, mmax, hid, shid):
         "legendre_fwd": ("mfma", 2 * (2 * BC) * nlat * T),
         "legendre_inv": ("mfma", 2 * (2 * BC) * nlat * T),
         # HBM-bound stages: compulsory bytes moved
-        "fft_fwd": ("hbm", BC * nlat * (nlon * 4 + mmax * 8)),
-        "fft_inv": ("hbm", BC * nlat * (nlon * 4 + mmax * 8)),
-        "transpose_fwd": ("hbm", 2 * BC * nlat * mmax * 8),
-        "transpose_inv": ("hbm", 2 * BC * nlat * mmax * 8),
+        "fft_fwd": ("hbm", BC * rows * (nlon * 4 + mmax * 8)),
+        "fft_inv": ("hbm", BC * rows * (nlon * 4 + mmax * 8)),
+        "transpose_fwd": ("hbm", 2 * BC * rows * mmax * 8),
+        "transpose_inv": ("hbm", 2 * BC * rows * mmax * 8),
         "linear_contract": ("hbm", 8 * C * C * T + 2 * 8 * BC * T),
     }
     return tab.get(name)
@@ -171,11 +185,35 @@ def main():
     from msfno_amd import _native as N
 
     blk, p, cfg = build_block(args, dev)
-    B, C = args.batch, args.C
-    g = torch.Generator().manual_seed(1000 * rank)
-    x = torch.randn(B, C, args.nlat, args.nlon, generator=g).to(dev)
-    gamma = (0.1 * torch.randn(B, C, generator=g)).to(dev)
-    beta = (0.1 * torch.randn(B, C, generator=g)).to(dev)
+    C = args.C
+    band = args.parallel == "latband"
+    rows = mset = None
+    if band:
+        # one batch of batch*N fields, each rank holding its latitude band of every field
+        from msfno_amd.sfno import LatBandBlock, TorchComm
+        B = args.batch * world
+        shard = LatBandBlock(blk, rank, world, device=dev)
+        r0, r1 = shard.rows
+        rows, mset = r1 - r0, [m for m, o in enumerate(shard.m_owner) if o == rank]
+        gd = torch.Generator(device=dev).manual_seed(0)
+        x = torch.empty(B, C, rows, args.nlon, device=dev)
+        for b in range(B):  # field b is identical on every rank; keep this rank's rows
+            x[b] = torch.randn(C, args.nlat, args.nlon, generator=gd, device=dev)[:, r0:r1]
+        gamma = 0.1 * torch.randn(B, C, generator=gd, device=dev)
+        beta = 0.1 * torch.randn(B, C, generator=gd, device=dev)
+        comm = TorchComm() if dist else None
+
+        def step():
+            return shard(x, gamma, beta, 1.0, comm=comm)
+    else:
+        B = args.batch
+        g = torch.Generator().manual_seed(1000 * rank)
+        x = torch.randn(B, C, args.nlat, args.nlon, generator=g).to(dev)
+        gamma = (0.1 * torch.randn(B, C, generator=g)).to(dev)
+        beta = (0.1 * torch.randn(B, C, generator=g)).to(dev)
+
+        def step():
+            return blk(x, gamma, beta, 1.0)
 
     def barrier():
         if dist:
@@ -183,7 +221,7 @@ def main():
 
     with torch.no_grad():
         for _ in range(args.warmup):
-            y = blk(x, gamma, beta, 1.0)
+            y = step()
         torch.cuda.synchronize()
         N.profile_collect()  # discard
         N.profile_enable(True)
@@ -191,7 +229,7 @@ def main():
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for _ in range(args.steps):
-            y = blk(x, gamma, beta, 1.0)
+            y = step()
         torch.cuda.synchronize()
         barrier()
         t1 = time.perf_counter()
@@ -204,7 +242,7 @@ def main():
         elapsed = t.item()
     assert torch.isfinite(y).all()
 
-    fields = world * B * args.steps
+    fields = (B if band else world * B) * args.steps
     value = fields / elapsed
     ms_per_step = 1000.0 * elapsed / args.steps
 
@@ -220,8 +258,8 @@ def main():
     if dom is not None:
         name, (tot_ms, cnt) = dom
         avg_s = tot_ms / cnt / 1000.0
-        w = stage_work(name, B, C, args.nlat, args.nlon, args.lmax, mmax, hid, shid)
-        tr, tr_src = pmc_traffic(name) if (B == 1 and C == 256 and args.nlat == 721
+        w = stage_work(name, B, C, args.nlat, args.nlon, args.lmax, mmax, hid, shid, rows, mset)
+        tr, tr_src = pmc_traffic(name) if (B == 1 and C == 256 and args.nlat == 721 and not band
                                             and args.filter == "non-linear") else (None, None)
         if w is not None:
             kind, amount = w
@@ -239,7 +277,7 @@ def main():
                         "kernel": name, "avg_ms": round(avg_s * 1e3, 4)}
     if args.stages and rank == 0:
         for k, (ms, c) in sorted(stages.items(), key=lambda kv: -kv[1][0]):
-            w = stage_work(k, B, C, args.nlat, args.nlon, args.lmax, mmax, hid, shid)
+            w = stage_work(k, B, C, args.nlat, args.nlon, args.lmax, mmax, hid, shid, rows, mset)
             extra = ""
             if w:
                 a = w[1] / (ms / c / 1e3)
@@ -268,8 +306,10 @@ def main():
             "data": "synthetic (x~N(0,1), random-init weights of the reference block)",
             "config": {"workload": f"sfno_block_fwd_{args.nlat}x{args.nlon}_C{C}_lmax{args.lmax}_"
                                    f"{args.filter}_filmed",
-                       "batch_per_gpu": B, "filter": args.filter,
-                       "parallelism": f"replicas{world}" if world > 1 else "single"},
+                       "batch_per_gpu": args.batch, "global_batch": B if band else B * world,
+                       "filter": args.filter,
+                       "parallelism": (f"latband{world}" if band else
+                                       (f"replicas{world}" if world > 1 else "single"))},
             "roofline": roof,
             "cpu_baseline": cpu,
         }

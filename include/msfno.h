@@ -143,6 +143,67 @@ int msfno_filter_forward(const msfno_block_desc* d, msfno_sht_plan_t fwd, msfno_
                          void* stream);
 
 /* ---------------------------------------------------------------------------
+ * Latitude-band sharded SFNO-Block (multi-GPU form of
+ * msfno_block_forward).  The reference runs one block per process on the whole
+ * field (DDP = replicas, MSFNO/main.py:1153); this splits ONE field batch over
+ * `world` ranks: rank r owns latitude rows [row_start[r], row_start[r+1]) for
+ * every pointwise / FFT / 1x1-conv / MLP stage and the zonal wavenumbers
+ * {m : m_owner[m] == r} for the Legendre transforms and the spectral filter.
+ * The caller (Python, torch.distributed over RCCL) performs the collectives
+ * between the stages; the library never communicates:
+ *
+ *   stage 0  x_local -> inner-skip GEMM (side stream), FFT rows    -> stats_local
+ *   [all_gather stats_local -> stats_all]              (norm0, B*C*3 doubles)
+ *   stage 1  norm0 affine, pack spectra by owner of m     -> send
+ *   [all_to_all send -> recv, counts from msfno_band_exchange_counts(phase 0)]
+ *   stage 2  recv -> Legendre fwd -> filter -> Legendre inv -> send
+ *   [all_to_all send -> recv, phase 1]
+ *   stage 3  recv -> inverse FFT rows + skip (+GELU)       -> stats_local
+ *   [all_gather stats_local -> stats_all]              (norm1)
+ *   stage 4  norm1 (+FiLM) -> MLP (+outer skip)            -> out_local
+ *
+ * Same-grid blocks only (inner/outer skips need equal input/output grids);
+ * non-linear filter (the reference default); at most 64 ranks.
+ * ------------------------------------------------------------------------- */
+typedef struct msfno_band_plan_s* msfno_band_plan_t;
+
+/* Default partition (host only, no GPU): balanced contiguous latitude bands and
+ * a zig-zag (snake) assignment of m = 0..mact-1 that balances both the count of
+ * m and the Legendre/filter work sum(lmax - m) per rank; m >= lmax -> -1. */
+int msfno_band_partition(int world, int nlat, int lmax, int mmax, int* row_start, int* m_owner);
+/* all-to-all element counts (floats) per peer for `rank` (host only):
+ * phase 0 (spectra rows->m), phase 1 (m->rows); R = 2*B*C. */
+int msfno_band_exchange_counts(int world, int rank, int nlat, int mmax, const int* row_start,
+                               const int* m_owner, int R, int phase, long long* send_counts,
+                               long long* recv_counts);
+int msfno_band_plan_create(int nlat, int nlon, int lmax, int mmax, int world, int rank,
+                           const int* row_start, const int* m_owner, msfno_band_plan_t* plan);
+int msfno_band_plan_destroy(msfno_band_plan_t plan);
+/* full reference tables (mmax,lmax,nlat) fp32 device buffers (RealSHT.weights,
+ * InverseRealSHT.pct incl. the 1e5 rescale); only this rank's m-set is kept */
+int msfno_band_plan_load_tables(msfno_band_plan_t plan, const float* fwd_table,
+                                const float* inv_table, void* stream);
+
+typedef struct msfno_band_io {
+  const float* x;           /* (B, C, rows_local, nlon)                         */
+  const float* gamma;       /* (B, C) or NULL                                   */
+  const float* beta;        /* (B, C) or NULL                                   */
+  float film_scale;
+  float* out;               /* (B, C, rows_local, nlon)                         */
+  float* send;              /* exchange buffers, >= max over phases of the sum  */
+  float* recv;              /*   of the send / recv counts (floats)             */
+  double* stats_local;      /* (B*C, 3) {n, mean, M2}                           */
+  const double* stats_all;  /* (world, B*C, 3), the all_gather of stats_local   */
+} msfno_band_io;
+
+size_t msfno_band_workspace_size(const msfno_block_desc* d, msfno_band_plan_t plan, int B);
+/* Run one stage (0..4) on `stream`.  ws must be the same buffer for all five
+ * stages of one forward. */
+int msfno_band_block_stage(const msfno_block_desc* d, msfno_band_plan_t plan, int stage,
+                           const msfno_band_io* io, int B, void* ws, size_t ws_bytes,
+                           void* stream);
+
+/* ---------------------------------------------------------------------------
  * Instrumentation (not a reference interface): per-stage device time of the
  * fused block measured with hipEvents recorded on the caller's stream between
  * stages.  Used by bench.py to time the dominant kernel inside the timed region.

@@ -5,14 +5,14 @@
 #include <cstdlib>
 #include <cstring>
 
-#include "kernels.h"
+#include "block.h"
 
 namespace msfno {
 
 static thread_local std::string g_last_error;
 void set_error(const std::string& msg) { g_last_error = msg; }
 
-void SpecLayout::build(int lmax_, int mmax_) {
+void SpecLayout::build(int lmax_, int mmax_, const std::vector<char>* mask) {
   lmax = lmax_;
   mmax = mmax_;
   L.assign(mmax, 0);
@@ -21,7 +21,7 @@ void SpecLayout::build(int lmax_, int mmax_) {
   T = Tp = 0;
   mact = 0;
   for (int m = 0; m < mmax; ++m) {
-    const int l = std::max(lmax - m, 0);
+    const int l = (mask && !(*mask)[m]) ? 0 : std::max(lmax - m, 0);
     L[m] = l;
     Lp[m] = (int)round_up(l, 4);
     off[m] = (int)Tp;
@@ -147,16 +147,12 @@ static int legendre_table(int mmax, int lmax, int nlat, int grid, int inverse, i
 // ---------------------------------------------------------------------------
 // stage profiler (hipEvents on the caller's stream)
 // ---------------------------------------------------------------------------
-enum Stage {
-  ST_FFT_FWD = 0, ST_NORM0, ST_TRANSPOSE_FWD, ST_LEG_FWD, ST_SPEC_PREP, ST_SPEC_L0, ST_SPEC_L1,
-  ST_SPEC_L2, ST_SPEC_L3, ST_SPEC_OUT, ST_LIN_GATHER, ST_LIN_CONTRACT, ST_LIN_SCATTER, ST_LEG_INV,
-  ST_TRANSPOSE_INV, ST_FFT_INV, ST_SKIP, ST_NORM1, ST_FC1, ST_FC2, ST_OUT_AFFINE, ST_END
-};
 static const char* kStageNames[MSFNO_PROF_NSTAGES] = {
     "fft_fwd", "norm0_stats", "transpose_fwd", "legendre_fwd", "spectral_prep", "spectral_l0",
     "spectral_l1", "spectral_l2", "spectral_l3", "spectral_out", "linear_gather",
     "linear_contract", "linear_scatter", "legendre_inv", "transpose_inv", "fft_inv",
-    "inner_skip", "norm1_film_fold", "mlp_fc1", "mlp_fc2", "out_affine", "end"};
+    "inner_skip", "norm1_film_fold", "mlp_fc1", "mlp_fc2", "out_affine", "band_pack",
+    "band_gather", "band_scatter", "end"};
 
 struct Profiler {
   bool on = false;
@@ -185,19 +181,15 @@ struct Profiler {
   }
 };
 static Profiler g_prof;
-static inline void prof(int stage, hipStream_t s) { g_prof.mark(stage, s); }
+void prof(int stage, hipStream_t s) { g_prof.mark(stage, s); }
 
 // ---------------------------------------------------------------------------
 // per-device side stream: the inner-skip 1x1 conv (MFMA-bound, depends only on
 // the block input) runs concurrently with the HBM-bound SHT stages (fork/join
 // through events; capture-safe).  MSFNO_SIDE_STREAM=0 disables it.
 // ---------------------------------------------------------------------------
-struct SideCtx {
-  hipStream_t side = nullptr;
-  hipEvent_t fork = nullptr, join = nullptr;
-};
 
-static int side_ctx(SideCtx** out) {
+int side_ctx(SideCtx** out) {
   static int enabled = -1;
   if (enabled < 0) {
     const char* e = getenv("MSFNO_SIDE_STREAM");
@@ -222,18 +214,8 @@ static int side_ctx(SideCtx** out) {
 // ---------------------------------------------------------------------------
 // workspace carving
 // ---------------------------------------------------------------------------
-struct Carve {
-  size_t off = 0;
-  char* base = nullptr;
-  template <typename T>
-  T* take(size_t count) {
-    const size_t o = off;
-    off = (size_t)round_up((int64_t)(off + count * sizeof(T)), 256);
-    return base ? reinterpret_cast<T*>(base + o) : nullptr;
-  }
-};
 
-static int ensure_desc(msfno_sht_plan_s* p, int R, int other_ld, int64_t ldT) {
+int ensure_desc(msfno_sht_plan_s* p, int R, int other_ld, int64_t ldT) {
   // forward plan: A = Xt (R x nlat, ld ldk), B = table, C = S (ld ldT)
   // inverse plan: A = S (ld ldT), B = table, C = Yt (R x nlat, ld ldk)
   if (p->desc_R == R && p->d_desc) return MSFNO_OK;
@@ -243,16 +225,18 @@ static int ensure_desc(msfno_sht_plan_s* p, int R, int other_ld, int64_t ldT) {
   int tiles = 0;
   const SpecLayout& L = p->spec;
   for (int m = 0; m < L.mact; ++m) {
+    if (L.L[m] == 0) continue;  // m outside a sharded plan's m-set
+    const int64_t sl = p->slab[m];
     GemmDesc g{};
     g.M = R;
     if (!p->inverse) {
       g.N = L.Lp[m]; g.K = p->nlat;
       g.lda = p->ldk; g.ldb = L.Lp[m]; g.ldc = (int)ldT;
-      g.offA = (int64_t)m * R * p->ldk; g.offB = p->tab_off[m]; g.offC = L.off[m];
+      g.offA = sl * R * p->ldk; g.offB = p->tab_off[m]; g.offC = L.off[m];
     } else {
       g.N = p->nlat; g.K = L.L[m];
       g.lda = (int)ldT; g.ldb = p->ldk; g.ldc = p->ldk;
-      g.offA = L.off[m]; g.offB = p->tab_off[m]; g.offC = (int64_t)m * R * p->ldk;
+      g.offA = L.off[m]; g.offB = p->tab_off[m]; g.offC = sl * R * p->ldk;
     }
     g.tiles_m = (int)cdiv(g.M, bm);
     g.tiles_n = (int)cdiv(g.N, bn);
@@ -276,7 +260,7 @@ static int ensure_desc(msfno_sht_plan_s* p, int R, int other_ld, int64_t ldT) {
 // MSFNO_FFT_TILE=1 selects the fused FFT+transpose tile kernels instead of the
 // row FFT + separate transpose kernels (measured slower on MI355X at 721x1440:
 // DESIGN.md §5); kept as an A/B switch.
-static bool use_fft_tile(const FFTPlan& f) {
+bool use_fft_tile(const FFTPlan& f) {
   static int mode = -1;
   if (mode < 0) {
     const char* e = getenv("MSFNO_FFT_TILE");
@@ -285,8 +269,8 @@ static bool use_fft_tile(const FFTPlan& f) {
   return mode == 1 && fft_tile_supported(f);
 }
 
-static int legendre_fwd(msfno_sht_plan_s* f, const float* Xt, float* S, int R, hipStream_t s,
-                        const float* rowscale = nullptr, int C = 0) {
+int legendre_fwd(msfno_sht_plan_s* f, const float* Xt, float* S, int R, hipStream_t s,
+                 const float* rowscale, int C) {
   MSFNO_TRY(ensure_desc(f, R, 0, f->spec.ldT));
   GemmEpi e;
   e.rowscale = rowscale;
@@ -294,7 +278,7 @@ static int legendre_fwd(msfno_sht_plan_s* f, const float* Xt, float* S, int R, h
   return gemm_desc(TILE_128x64, Xt, f->table, S, f->d_desc, f->ndesc, f->desc_tiles, e, s);
 }
 
-static int legendre_inv(msfno_sht_plan_s* g, const float* S, float* Yt, int R, hipStream_t s) {
+int legendre_inv(msfno_sht_plan_s* g, const float* S, float* Yt, int R, hipStream_t s) {
   MSFNO_TRY(ensure_desc(g, R, 0, g->spec.ldT));
   GemmEpi e;
   return gemm_desc(TILE_128x64, S, g->table, Yt, g->d_desc, g->ndesc, g->desc_tiles, e, s);
@@ -303,17 +287,9 @@ static int legendre_inv(msfno_sht_plan_s* g, const float* S, float* Yt, int R, h
 // ---------------------------------------------------------------------------
 // block workspace layout (shared by size query and forward)
 // ---------------------------------------------------------------------------
-struct BlockBufs {
-  float2* Xn; float* Xt; float2* rs0; float* sc0; float* sh0;
-  float* Sa; float* Sb; float* Sc; float* Wexp[9];
-  float* xt; float* yt;
-  float* Yt; float2* Yn; float* x1;
-  float2* st1; float* sc1; float* sh1;
-  float* W1f; float* b1f; float* h;
-};
 
 
-static void carve_block(Carve& cv, BlockBufs& b, const msfno_block_desc* d,
+void carve_block(Carve& cv, BlockBufs& b, const msfno_block_desc* d,
                         const msfno_sht_plan_s* f, const msfno_sht_plan_s* g, int B,
                         bool with_norms) {
   const int64_t C = d->C, BC = (int64_t)B * C, R = 2 * BC;
@@ -359,7 +335,7 @@ static void carve_block(Carve& cv, BlockBufs& b, const msfno_block_desc* d,
   }
 }
 
-static int check_pair(const msfno_block_desc* d, const msfno_sht_plan_s* f,
+int check_pair(const msfno_block_desc* d, const msfno_sht_plan_s* f,
                       const msfno_sht_plan_s* g) {
   MSFNO_REQUIRE(d && f && g, MSFNO_EINVAL, "null descriptor or plan");
   MSFNO_REQUIRE(!f->inverse && g->inverse, MSFNO_EINVAL,
@@ -378,7 +354,7 @@ static int check_pair(const msfno_block_desc* d, const msfno_sht_plan_s* f,
   return MSFNO_OK;
 }
 
-static int run_filter(const msfno_block_desc* d, msfno_sht_plan_s* f, msfno_sht_plan_s* g,
+int run_filter(const msfno_block_desc* d, msfno_sht_plan_s* f, msfno_sht_plan_s* g,
                       const BlockBufs& b, int B, hipStream_t s) {
   const int64_t C = d->C;
   const SpecLayout& L = f->spec;
@@ -423,7 +399,7 @@ static int run_filter(const msfno_block_desc* d, msfno_sht_plan_s* f, msfno_sht_
 }
 
 // x -> (FFT, norm0 folded) -> Legendre -> filter -> inverse Legendre -> Yn
-static int run_spectral(const msfno_block_desc* d, msfno_sht_plan_s* f, msfno_sht_plan_s* g,
+int run_spectral(const msfno_block_desc* d, msfno_sht_plan_s* f, msfno_sht_plan_s* g,
                         const BlockBufs& b, const float* x, int B, bool norm0, hipStream_t s) {
   const int64_t C = d->C, BC = (int64_t)B * C, R = 2 * BC;
   prof(ST_FFT_FWD, s);
@@ -463,7 +439,7 @@ static int run_spectral(const msfno_block_desc* d, msfno_sht_plan_s* f, msfno_sh
 }
 
 // Yt -> spatial rows (fused transpose + irfft when enabled); out = act(addsrc + irfft)
-static int run_inverse_fft(msfno_sht_plan_s* g, const BlockBufs& b, int B, int C, float* out,
+int run_inverse_fft(msfno_sht_plan_s* g, const BlockBufs& b, int B, int C, float* out,
                            const float* addsrc, float2* rowstats, int act, hipStream_t s) {
   const int64_t BC = (int64_t)B * C;
   if (use_fft_tile(g->fft) && addsrc == nullptr) {
@@ -478,6 +454,46 @@ static int run_inverse_fft(msfno_sht_plan_s* g, const BlockBufs& b, int B, int C
   return MSFNO_OK;
 }
 
+
+int plan_create(int nlat, int nlon, int lmax, int mmax, int inverse,
+                const std::vector<char>* mask, msfno_sht_plan_s** plan) {
+  MSFNO_REQUIRE(nlat > 0 && nlon > 1 && lmax > 0 && mmax > 0, MSFNO_EINVAL, "bad SHT dims");
+  MSFNO_REQUIRE(mmax <= nlon / 2 + 1, MSFNO_EINVAL, "mmax must be <= nlon//2 + 1");
+  MSFNO_REQUIRE(!mask || (int)mask->size() == mmax, MSFNO_EINVAL, "m-set mask must have mmax entries");
+  auto* p = new msfno_sht_plan_s();
+  p->nlat = nlat; p->nlon = nlon; p->lmax = lmax; p->mmax = mmax; p->inverse = inverse ? 1 : 0;
+  p->ldk = (int)round_up(nlat, 4);
+  p->spec.build(lmax, mmax, mask);
+  p->slab.assign(mmax, -1);
+  for (int m = 0; m < mmax; ++m) {
+    if (!mask) p->slab[m] = m;
+    else if (p->spec.L[m] > 0) p->slab[m] = p->nslab++;
+  }
+  if (!mask) p->nslab = mmax;
+  int rc = fft_plan_build(p->fft, nlon);
+  if (rc != MSFNO_OK) { delete p; return rc; }
+  p->tab_off.assign(mmax, 0);
+  int64_t acc = 0;
+  for (int m = 0; m < mmax; ++m) {
+    p->tab_off[m] = acc;
+    acc += p->inverse ? (int64_t)p->spec.L[m] * p->ldk : (int64_t)nlat * p->spec.Lp[m];
+  }
+  p->table_elems = acc;
+  hipError_t e = hipMalloc(&p->table, std::max<int64_t>(acc, 4) * sizeof(float));
+  if (e == hipSuccess) e = hipMalloc(&p->d_tab_off, mmax * sizeof(int64_t));
+  if (e == hipSuccess) e = hipMalloc(&p->d_Lp, mmax * sizeof(int));
+  if (e == hipSuccess) e = hipMalloc(&p->d_off, mmax * sizeof(int));
+  if (e == hipSuccess) e = hipMemcpy(p->d_tab_off, p->tab_off.data(), mmax * sizeof(int64_t), hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMemcpy(p->d_Lp, p->spec.Lp.data(), mmax * sizeof(int), hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMemcpy(p->d_off, p->spec.off.data(), mmax * sizeof(int), hipMemcpyHostToDevice);
+  if (e != hipSuccess) {
+    set_error(std::string("plan allocation failed: ") + hipGetErrorString(e));
+    msfno_sht_plan_destroy(p);
+    return MSFNO_EHIP;
+  }
+  *plan = p;
+  return MSFNO_OK;
+}
 }  // namespace msfno
 
 using namespace msfno;
@@ -504,35 +520,7 @@ int msfno_legendre_table(int mmax, int lmax, int nlat, int grid, int inverse, in
 int msfno_sht_plan_create(int nlat, int nlon, int lmax, int mmax, int inverse,
                           msfno_sht_plan_t* plan) {
   MSFNO_REQUIRE(plan, MSFNO_EINVAL, "null plan pointer");
-  MSFNO_REQUIRE(nlat > 0 && nlon > 1 && lmax > 0 && mmax > 0, MSFNO_EINVAL, "bad SHT dims");
-  MSFNO_REQUIRE(mmax <= nlon / 2 + 1, MSFNO_EINVAL, "mmax must be <= nlon//2 + 1");
-  auto* p = new msfno_sht_plan_s();
-  p->nlat = nlat; p->nlon = nlon; p->lmax = lmax; p->mmax = mmax; p->inverse = inverse ? 1 : 0;
-  p->ldk = (int)round_up(nlat, 4);
-  p->spec.build(lmax, mmax);
-  int rc = fft_plan_build(p->fft, nlon);
-  if (rc != MSFNO_OK) { delete p; return rc; }
-  p->tab_off.assign(mmax, 0);
-  int64_t acc = 0;
-  for (int m = 0; m < mmax; ++m) {
-    p->tab_off[m] = acc;
-    acc += p->inverse ? (int64_t)p->spec.L[m] * p->ldk : (int64_t)nlat * p->spec.Lp[m];
-  }
-  p->table_elems = acc;
-  hipError_t e = hipMalloc(&p->table, std::max<int64_t>(acc, 4) * sizeof(float));
-  if (e == hipSuccess) e = hipMalloc(&p->d_tab_off, mmax * sizeof(int64_t));
-  if (e == hipSuccess) e = hipMalloc(&p->d_Lp, mmax * sizeof(int));
-  if (e == hipSuccess) e = hipMalloc(&p->d_off, mmax * sizeof(int));
-  if (e == hipSuccess) e = hipMemcpy(p->d_tab_off, p->tab_off.data(), mmax * sizeof(int64_t), hipMemcpyHostToDevice);
-  if (e == hipSuccess) e = hipMemcpy(p->d_Lp, p->spec.Lp.data(), mmax * sizeof(int), hipMemcpyHostToDevice);
-  if (e == hipSuccess) e = hipMemcpy(p->d_off, p->spec.off.data(), mmax * sizeof(int), hipMemcpyHostToDevice);
-  if (e != hipSuccess) {
-    set_error(std::string("plan allocation failed: ") + hipGetErrorString(e));
-    msfno_sht_plan_destroy(p);
-    return MSFNO_EHIP;
-  }
-  *plan = p;
-  return MSFNO_OK;
+  return plan_create(nlat, nlon, lmax, mmax, inverse, nullptr, plan);
 }
 
 int msfno_sht_plan_destroy(msfno_sht_plan_t p) {

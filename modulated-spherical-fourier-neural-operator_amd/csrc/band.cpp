@@ -1,0 +1,368 @@
+// Latitude-band sharded SFNO-Block: plans, exchange layout and
+// the five per-rank stages between which the caller runs the collectives
+// (include/msfno.h, "Latitude-band sharded SFNO-Block").
+//
+// Exchange layout.  Spectra leave stage 1 as slabs (R = 2BC rows, H_r latitude
+// columns), one slab per owned-elsewhere m, ordered by (owner, m): the
+// all-to-all block for rank q is then contiguous.  perm[m] is that slab index
+// (the same order is used for the return trip in stage 3).  On the owner the
+// received blocks are per source band p: (nm_r * R, H_p) at offset
+// nm_r * R * row0[p]; band_copy re-assembles full-latitude (nm_r, R, ldk) slabs
+// for the Legendre GEMMs and splits them again afterwards.
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+
+#include "block.h"
+
+using namespace msfno;
+
+struct msfno_band_plan_s {
+  int nlat = 0, nlon = 0, lmax = 0, mmax = 0, world = 0, rank = 0;
+  std::vector<int> row0;   // world + 1 band boundaries
+  std::vector<int> owner;  // per m, -1: no coefficients (m >= lmax)
+  std::vector<int> nm_of;  // per rank: number of owned m
+  int rows = 0;            // local latitude rows
+  int nm = 0;              // local m count
+  int mact = 0;            // global count of m with lmax - m > 0
+  msfno_sht_plan_s* fwd = nullptr;
+  msfno_sht_plan_s* inv = nullptr;
+  int* d_row0 = nullptr;
+  int* d_perm = nullptr;
+};
+
+namespace {
+
+int validate_partition(int world, int nlat, int lmax, int mmax, const int* row_start,
+                       const int* m_owner) {
+  MSFNO_REQUIRE(world >= 1 && world <= 64, MSFNO_EUNSUPPORTED, "band sharding needs 1..64 ranks");
+  MSFNO_REQUIRE(row_start && m_owner, MSFNO_EINVAL, "null partition arrays");
+  MSFNO_REQUIRE(row_start[0] == 0 && row_start[world] == nlat, MSFNO_EINVAL,
+                "row_start must run from 0 to nlat");
+  for (int r = 0; r < world; ++r)
+    MSFNO_REQUIRE(row_start[r + 1] > row_start[r], MSFNO_EINVAL,
+                  "every rank needs at least one latitude row");
+  for (int m = 0; m < mmax; ++m) {
+    const bool has = lmax - m > 0;
+    MSFNO_REQUIRE(has ? (m_owner[m] >= 0 && m_owner[m] < world) : m_owner[m] == -1, MSFNO_EINVAL,
+                  "m_owner must assign every m < lmax to a rank and m >= lmax to -1");
+  }
+  return MSFNO_OK;
+}
+
+struct BandBufs {
+  float2* Xn;   // (BC, rows, mmax) spectra of local rows; reused as Yn
+  float2* rs;   // (BC, rows) row (mean, M2), norm0 then norm1
+  float *sc0, *sh0, *sc1, *sh1;
+  float* Xt;    // (nm, R, ldk) full-latitude slabs; reused as Yt
+  BlockBufs fb; // filter buffers (Sa, Sb, Sc, Wexp) in the local spectral layout
+  float* x1;    // (B, C, rows*nlon)
+  float *W1f, *b1f, *h;
+};
+
+void carve_band(Carve& cv, BandBufs& b, const msfno_block_desc* d, const msfno_band_plan_s* p,
+                int B) {
+  const int64_t C = d->C, BC = (int64_t)B * C, R = 2 * BC;
+  const int64_t Pl = (int64_t)p->rows * p->nlon;
+  const SpecLayout& L = p->fwd->spec;
+  b.Xn = cv.take<float2>(BC * p->rows * p->mmax);
+  b.rs = cv.take<float2>(BC * p->rows);
+  b.sc0 = cv.take<float>(BC);
+  b.sh0 = cv.take<float>(BC);
+  b.sc1 = cv.take<float>(BC);
+  b.sh1 = cv.take<float>(BC);
+  b.Xt = cv.take<float>(std::max<int64_t>((int64_t)p->nm * R * p->fwd->ldk, 4));
+  std::memset(&b.fb, 0, sizeof(b.fb));
+  b.fb.Sa = cv.take<float>(R * L.ldT);
+  const int64_t Hs = d->spec_hidden;
+  b.fb.Sb = cv.take<float>((int64_t)B * 2 * Hs * L.ldT);
+  b.fb.Sc = cv.take<float>((int64_t)B * 2 * Hs * L.ldT);
+  for (int l = 0; l <= d->spectral_layers && l < 9; ++l) {
+    const int64_t ci = (l == 0) ? C : Hs;
+    const int64_t co = (l == d->spectral_layers) ? C : Hs;
+    b.fb.Wexp[l] = cv.take<float>(4 * ci * co);
+  }
+  b.x1 = cv.take<float>(BC * Pl);
+  b.W1f = b.b1f = b.h = nullptr;
+  if (d->has_mlp) {
+    const int64_t Hd = d->mlp_hidden;
+    b.W1f = cv.take<float>((int64_t)B * Hd * C);
+    b.b1f = cv.take<float>((int64_t)B * Hd);
+    b.h = cv.take<float>((int64_t)B * Hd * Pl);
+  }
+}
+
+int check_band(const msfno_block_desc* d, const msfno_band_plan_s* p) {
+  MSFNO_REQUIRE(d && p, MSFNO_EINVAL, "null descriptor or band plan");
+  MSFNO_REQUIRE(p->fwd->table_loaded && p->inv->table_loaded, MSFNO_EINVAL,
+                "band plan tables not loaded");
+  MSFNO_REQUIRE(d->C > 0, MSFNO_EINVAL, "C must be > 0");
+  MSFNO_REQUIRE(d->filter_type == MSFNO_FILTER_NONLINEAR, MSFNO_EUNSUPPORTED,
+                "latitude-band sharding supports the non-linear spectral filter only");
+  MSFNO_REQUIRE(d->spectral_layers >= 1 && d->spectral_layers <= 8, MSFNO_EUNSUPPORTED,
+                "spectral_layers must be in [1, 8]");
+  MSFNO_REQUIRE(d->spec_hidden > 0, MSFNO_EINVAL, "spec_hidden must be > 0");
+  MSFNO_REQUIRE(d->outer_skip != MSFNO_SKIP_LINEAR, MSFNO_EUNSUPPORTED,
+                "outer_skip='linear' is not supported by the fused block");
+  return MSFNO_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int msfno_band_partition(int world, int nlat, int lmax, int mmax, int* row_start, int* m_owner) {
+  MSFNO_REQUIRE(world >= 1 && world <= 64, MSFNO_EUNSUPPORTED, "band sharding needs 1..64 ranks");
+  MSFNO_REQUIRE(nlat >= world, MSFNO_EINVAL, "need at least one latitude row per rank");
+  MSFNO_REQUIRE(lmax > 0 && mmax > 0 && row_start && m_owner, MSFNO_EINVAL, "bad partition args");
+  const int q = nlat / world, rem = nlat % world;
+  row_start[0] = 0;
+  for (int r = 0; r < world; ++r) row_start[r + 1] = row_start[r] + q + (r < rem ? 1 : 0);
+  // snake over m ascending (work lmax - m descending): 0..W-1, W-1..0, ...
+  for (int m = 0; m < mmax; ++m) {
+    if (lmax - m <= 0) {
+      m_owner[m] = -1;
+      continue;
+    }
+    const int round = m / world, pos = m % world;
+    m_owner[m] = (round & 1) ? world - 1 - pos : pos;
+  }
+  return MSFNO_OK;
+}
+
+int msfno_band_exchange_counts(int world, int rank, int nlat, int mmax, const int* row_start,
+                               const int* m_owner, int R, int phase, long long* send_counts,
+                               long long* recv_counts) {
+  MSFNO_REQUIRE(rank >= 0 && rank < world && R > 0 && send_counts && recv_counts, MSFNO_EINVAL,
+                "bad exchange-count arguments");
+  int lmax_eff = 0;  // validate against the implied lmax (owners of -1 mark m >= lmax)
+  for (int m = 0; m < mmax; ++m)
+    if (m_owner && m_owner[m] >= 0) lmax_eff = m + 1;
+  MSFNO_TRY(validate_partition(world, nlat, std::max(lmax_eff, 1), mmax, row_start, m_owner));
+  std::vector<long long> nm(world, 0);
+  for (int m = 0; m < mmax; ++m)
+    if (m_owner[m] >= 0) ++nm[m_owner[m]];
+  const long long hr = row_start[rank + 1] - row_start[rank];
+  for (int q = 0; q < world; ++q) {
+    const long long hq = row_start[q + 1] - row_start[q];
+    if (phase == 0) {  // rows -> m: send my rows of q's m-set, receive q's rows of mine
+      send_counts[q] = nm[q] * R * hr;
+      recv_counts[q] = nm[rank] * R * hq;
+    } else {           // m -> rows
+      send_counts[q] = nm[rank] * R * hq;
+      recv_counts[q] = nm[q] * R * hr;
+    }
+  }
+  MSFNO_REQUIRE(phase == 0 || phase == 1, MSFNO_EINVAL, "phase must be 0 or 1");
+  return MSFNO_OK;
+}
+
+int msfno_band_plan_destroy(msfno_band_plan_t p) {
+  if (!p) return MSFNO_OK;
+  msfno_sht_plan_destroy(p->fwd);
+  msfno_sht_plan_destroy(p->inv);
+  if (p->d_row0) (void)hipFree(p->d_row0);
+  if (p->d_perm) (void)hipFree(p->d_perm);
+  delete p;
+  return MSFNO_OK;
+}
+
+int msfno_band_plan_create(int nlat, int nlon, int lmax, int mmax, int world, int rank,
+                           const int* row_start, const int* m_owner, msfno_band_plan_t* plan) {
+  MSFNO_REQUIRE(plan, MSFNO_EINVAL, "null plan pointer");
+  MSFNO_REQUIRE(rank >= 0 && rank < world, MSFNO_EINVAL, "rank out of range");
+  MSFNO_TRY(validate_partition(world, nlat, lmax, mmax, row_start, m_owner));
+  auto* p = new msfno_band_plan_s();
+  p->nlat = nlat; p->nlon = nlon; p->lmax = lmax; p->mmax = mmax;
+  p->world = world; p->rank = rank;
+  p->row0.assign(row_start, row_start + world + 1);
+  p->owner.assign(m_owner, m_owner + mmax);
+  p->rows = row_start[rank + 1] - row_start[rank];
+  p->nm_of.assign(world, 0);
+  std::vector<char> mask(mmax, 0);
+  for (int m = 0; m < mmax; ++m) {
+    if (m_owner[m] < 0) continue;
+    p->mact = m + 1;
+    ++p->nm_of[m_owner[m]];
+    if (m_owner[m] == rank) mask[m] = 1;
+  }
+  p->nm = p->nm_of[rank];
+  // slab order for the exchanges: by (owner, m)
+  std::vector<int> perm(mmax, -1), start(world, 0);
+  for (int q = 1; q < world; ++q) start[q] = start[q - 1] + p->nm_of[q - 1];
+  for (int m = 0; m < mmax; ++m)
+    if (m_owner[m] >= 0) perm[m] = start[m_owner[m]]++;
+  int rc = plan_create(nlat, nlon, lmax, mmax, 0, &mask, &p->fwd);
+  if (rc == MSFNO_OK) rc = plan_create(nlat, nlon, lmax, mmax, 1, &mask, &p->inv);
+  if (rc != MSFNO_OK) {
+    msfno_band_plan_destroy(p);
+    return rc;
+  }
+  hipError_t e = hipMalloc(&p->d_row0, (world + 1) * sizeof(int));
+  if (e == hipSuccess) e = hipMalloc(&p->d_perm, mmax * sizeof(int));
+  if (e == hipSuccess)
+    e = hipMemcpy(p->d_row0, p->row0.data(), (world + 1) * sizeof(int), hipMemcpyHostToDevice);
+  if (e == hipSuccess)
+    e = hipMemcpy(p->d_perm, perm.data(), mmax * sizeof(int), hipMemcpyHostToDevice);
+  if (e != hipSuccess) {
+    set_error(std::string("band plan allocation failed: ") + hipGetErrorString(e));
+    msfno_band_plan_destroy(p);
+    return MSFNO_EHIP;
+  }
+  *plan = p;
+  return MSFNO_OK;
+}
+
+int msfno_band_plan_load_tables(msfno_band_plan_t p, const float* fwd_table,
+                                const float* inv_table, void* stream) {
+  MSFNO_REQUIRE(p && fwd_table && inv_table, MSFNO_EINVAL, "null band plan or table");
+  MSFNO_TRY(msfno_sht_plan_load_table(p->fwd, fwd_table, stream));
+  MSFNO_TRY(msfno_sht_plan_load_table(p->inv, inv_table, stream));
+  return MSFNO_OK;
+}
+
+size_t msfno_band_workspace_size(const msfno_block_desc* d, msfno_band_plan_t p, int B) {
+  if (!d || !p || B <= 0) return 0;
+  Carve cv;
+  BandBufs b;
+  carve_band(cv, b, d, p, B);
+  return cv.off;
+}
+
+int msfno_band_block_stage(const msfno_block_desc* d, msfno_band_plan_t p, int stage,
+                           const msfno_band_io* io, int B, void* ws, size_t ws_bytes,
+                           void* stream) {
+  MSFNO_TRY(check_band(d, p));
+  MSFNO_REQUIRE(io && B > 0, MSFNO_EINVAL, "null io or bad batch");
+  MSFNO_REQUIRE(ws_bytes >= msfno_band_workspace_size(d, p, B), MSFNO_EWORKSPACE,
+                "workspace too small");
+  hipStream_t s = (hipStream_t)stream;
+  Carve cv;
+  cv.base = (char*)ws;
+  BandBufs b;
+  carve_band(cv, b, d, p, B);
+  const int64_t C = d->C, BC = (int64_t)B * C, R = 2 * BC;
+  const int64_t Pl = (int64_t)p->rows * p->nlon;
+  const int64_t slab_rows = (int64_t)p->nm * R;
+  switch (stage) {
+    case 0: {
+      MSFNO_REQUIRE(io->x && io->stats_local, MSFNO_EINVAL, "stage 0 needs x and stats_local");
+      if (d->inner_skip == MSFNO_SKIP_LINEAR) {
+        MSFNO_REQUIRE(d->skip_w, MSFNO_EINVAL, "missing inner_skip weight");
+        SideCtx* side = nullptr;
+        MSFNO_TRY(side_ctx(&side));
+        hipStream_t ss = s;
+        if (side) {
+          MSFNO_CHECK_HIP(hipEventRecord(side->fork, s));
+          MSFNO_CHECK_HIP(hipStreamWaitEvent(side->side, side->fork, 0));
+          ss = side->side;
+        }
+        prof(ST_SKIP, ss);
+        GemmEpi e;
+        e.bias = d->skip_b;
+        MSFNO_TRY(gemm_uniform(TILE_128x128, d->skip_w, io->x, b.x1, (int)C, (int)Pl, (int)C,
+                               (int)C, (int)Pl, (int)Pl, 0, C * Pl, C * Pl, B, e, ss));
+        if (side) {
+          prof(ST_END, ss);
+          MSFNO_CHECK_HIP(hipEventRecord(side->join, ss));
+        }
+      }
+      prof(ST_FFT_FWD, s);
+      const float scale = (float)(2.0 * M_PI / p->nlon);
+      MSFNO_TRY(launch_fft_r2c_rows(p->fwd->fft, io->x, b.Xn, b.rs, BC * p->rows, p->mmax, scale,
+                                    s));
+      prof(ST_NORM0, s);
+      MSFNO_TRY(launch_stats_partial(b.rs, p->rows, p->nlon, BC, io->stats_local, s));
+      break;
+    }
+    case 1: {
+      MSFNO_REQUIRE(io->stats_all && io->send, MSFNO_EINVAL, "stage 1 needs stats_all and send");
+      MSFNO_TRY(launch_chan_affine_parts(io->stats_all, p->world, B, (int)C, d->norm0_w,
+                                         d->norm0_b, d->norm_eps, nullptr, nullptr, 0.f, b.sc0,
+                                         b.sh0, s));
+      prof(ST_BAND_PACK, s);
+      MSFNO_TRY(launch_transpose_fwd(b.Xn, io->send, B, (int)C, p->rows, p->mmax, p->rows, b.sc0,
+                                     b.sh0, s, p->d_perm));
+      break;
+    }
+    case 2: {
+      MSFNO_REQUIRE(io->send && io->recv, MSFNO_EINVAL, "stage 2 needs send and recv");
+      if (p->nm == 0) break;  // this rank owns no zonal wavenumber
+      prof(ST_BAND_GATHER, s);
+      MSFNO_TRY(launch_band_copy(io->recv, b.Xt, slab_rows, p->nlat, p->fwd->ldk, p->d_row0,
+                                 p->world, false, s));
+      prof(ST_LEG_FWD, s);
+      MSFNO_TRY(legendre_fwd(p->fwd, b.Xt, b.fb.Sa, (int)R, s));
+      MSFNO_TRY(run_filter(d, p->fwd, p->inv, b.fb, B, s));
+      prof(ST_LEG_INV, s);
+      MSFNO_TRY(legendre_inv(p->inv, b.fb.Sa, b.Xt, (int)R, s));
+      prof(ST_BAND_SCATTER, s);
+      MSFNO_TRY(launch_band_copy(b.Xt, io->send, slab_rows, p->nlat, p->inv->ldk, p->d_row0,
+                                 p->world, true, s));
+      break;
+    }
+    case 3: {
+      MSFNO_REQUIRE(io->recv && io->x && io->stats_local, MSFNO_EINVAL,
+                    "stage 3 needs recv, x and stats_local");
+      prof(ST_TRANSPOSE_INV, s);
+      MSFNO_TRY(launch_transpose_inv(io->recv, b.Xn, B, (int)C, p->rows, p->mmax, p->mact,
+                                     p->rows, s, p->d_perm));
+      const float* skip_src = nullptr;
+      if (d->inner_skip == MSFNO_SKIP_LINEAR) {
+        SideCtx* side = nullptr;
+        MSFNO_TRY(side_ctx(&side));
+        if (side) MSFNO_CHECK_HIP(hipStreamWaitEvent(s, side->join, 0));
+        skip_src = b.x1;
+      } else if (d->inner_skip == MSFNO_SKIP_IDENTITY) {
+        skip_src = io->x;
+      }
+      prof(ST_FFT_INV, s);
+      MSFNO_TRY(launch_fft_c2r_rows(p->inv->fft, b.Xn, b.x1, skip_src, b.rs, BC * p->rows,
+                                    p->mmax, 0, s));
+      prof(ST_NORM1, s);
+      MSFNO_TRY(launch_stats_partial(b.rs, p->rows, p->nlon, BC, io->stats_local, s));
+      break;
+    }
+    case 4: {
+      MSFNO_REQUIRE(io->stats_all && io->out && io->x, MSFNO_EINVAL,
+                    "stage 4 needs stats_all, x and out");
+      MSFNO_REQUIRE((io->gamma == nullptr) == (io->beta == nullptr), MSFNO_EINVAL,
+                    "gamma and beta must both be given or both be NULL");
+      MSFNO_TRY(launch_chan_affine_parts(io->stats_all, p->world, B, (int)C, d->norm1_w,
+                                         d->norm1_b, d->norm_eps, io->gamma, io->beta,
+                                         io->film_scale, b.sc1, b.sh1, s));
+      const float* resid = d->outer_skip == MSFNO_SKIP_IDENTITY ? io->x : nullptr;
+      if (d->has_mlp) {
+        MSFNO_REQUIRE(d->fc1_w && d->fc2_w, MSFNO_EINVAL, "missing MLP weights");
+        const int64_t Hd = d->mlp_hidden;
+        MSFNO_TRY(launch_fold_affine(d->fc1_w, d->fc1_b, b.sc1, b.sh1, b.W1f, b.b1f, B, (int)Hd,
+                                     (int)C, s));
+        prof(ST_FC1, s);
+        GemmEpi e1;
+        e1.bias = b.b1f;
+        e1.sBias = Hd;
+        MSFNO_TRY(gemm_uniform(TILE_128x128, b.W1f, b.x1, b.h, (int)Hd, (int)Pl, (int)C, (int)C,
+                               (int)Pl, (int)Pl, Hd * C, C * Pl, Hd * Pl, B, e1, s));
+        prof(ST_FC2, s);
+        GemmEpi e2;
+        e2.act = 2;
+        e2.bias = d->fc2_b;
+        if (resid) { e2.addend = resid; e2.sD = C * Pl; e2.ldd = (int)Pl; }
+        const GemmTile t2 = C <= 256 && C > 128 ? TILE_256x64 : TILE_128x128;
+        MSFNO_TRY(gemm_uniform(t2, d->fc2_w, b.h, io->out, (int)C, (int)Pl, (int)Hd, (int)Hd,
+                               (int)Pl, (int)Pl, 0, Hd * Pl, C * Pl, B, e2, s));
+      } else {
+        prof(ST_OUT_AFFINE, s);
+        MSFNO_TRY(launch_affine_rows(b.x1, b.sc1, b.sh1, resid, io->out, BC, Pl, 0, nullptr, 0, s));
+      }
+      prof(ST_END, s);
+      break;
+    }
+    default:
+      set_error("band stage must be 0..4");
+      return MSFNO_EINVAL;
+  }
+  return MSFNO_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,60 @@
+// Internal block-orchestration helpers shared by api.cpp (single-GPU block)
+// and band.cpp (latitude-band sharded block).  Not part of the C-ABI.
+#pragma once
+#include "kernels.h"
+
+namespace msfno {
+
+// stage profiler (hipEvents; msfno_profile_*)
+enum Stage {
+  ST_FFT_FWD = 0, ST_NORM0, ST_TRANSPOSE_FWD, ST_LEG_FWD, ST_SPEC_PREP, ST_SPEC_L0, ST_SPEC_L1,
+  ST_SPEC_L2, ST_SPEC_L3, ST_SPEC_OUT, ST_LIN_GATHER, ST_LIN_CONTRACT, ST_LIN_SCATTER, ST_LEG_INV,
+  ST_TRANSPOSE_INV, ST_FFT_INV, ST_SKIP, ST_NORM1, ST_FC1, ST_FC2, ST_OUT_AFFINE, ST_BAND_PACK,
+  ST_BAND_GATHER, ST_BAND_SCATTER, ST_END
+};
+void prof(int stage, hipStream_t s);
+
+// workspace carving: deterministic 256-B aligned sub-allocations of one buffer
+struct Carve {
+  size_t off = 0;
+  char* base = nullptr;
+  template <typename T>
+  T* take(size_t count) {
+    const size_t o = off;
+    off = (size_t)round_up((int64_t)(off + count * sizeof(T)), 256);
+    return base ? reinterpret_cast<T*>(base + o) : nullptr;
+  }
+};
+
+// per-device side stream for the inner-skip GEMM (fork/join through events)
+struct SideCtx {
+  hipStream_t side = nullptr;
+  hipEvent_t fork = nullptr, join = nullptr;
+};
+int side_ctx(SideCtx** out);
+
+struct BlockBufs {
+  float2* Xn; float* Xt; float2* rs0; float* sc0; float* sh0;
+  float* Sa; float* Sb; float* Sc; float* Wexp[9];
+  float* xt; float* yt;
+  float* Yt; float2* Yn; float* x1;
+  float2* st1; float* sc1; float* sh1;
+  float* W1f; float* b1f; float* h;
+};
+
+void carve_block(Carve& cv, BlockBufs& b, const msfno_block_desc* d, const msfno_sht_plan_s* f,
+                 const msfno_sht_plan_s* g, int B, bool with_norms);
+int check_pair(const msfno_block_desc* d, const msfno_sht_plan_s* f, const msfno_sht_plan_s* g);
+int ensure_desc(msfno_sht_plan_s* p, int R, int other_ld, int64_t ldT);
+int legendre_fwd(msfno_sht_plan_s* f, const float* Xt, float* S, int R, hipStream_t s,
+                 const float* rowscale = nullptr, int C = 0);
+int legendre_inv(msfno_sht_plan_s* g, const float* S, float* Yt, int R, hipStream_t s);
+// spectral filter on S (f->spec layout) in b.Sa (in place)
+int run_filter(const msfno_block_desc* d, msfno_sht_plan_s* f, msfno_sht_plan_s* g,
+               const BlockBufs& b, int B, hipStream_t s);
+bool use_fft_tile(const FFTPlan& f);
+// plan construction (mask: optional m-set, see SpecLayout::build)
+int plan_create(int nlat, int nlon, int lmax, int mmax, int inverse,
+                const std::vector<char>* mask, msfno_sht_plan_s** out);
+
+}  // namespace msfno

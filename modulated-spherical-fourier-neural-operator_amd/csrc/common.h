@@ -66,7 +66,9 @@ struct SpecLayout {
   int64_t T = 0;                // number of (l,m) with l>=m (tril count)
   int64_t Tp = 0;               // total padded columns
   int64_t ldT = 0;              // row stride of S buffers (multiple of 4)
-  void build(int lmax_, int mmax_);
+  // mask (size mmax, optional): keep only the m with mask[m] != 0 (latitude-band
+  // sharding: the m-set owned by one rank); the others get L = Lp = 0
+  void build(int lmax_, int mmax_, const std::vector<char>* mask = nullptr);
 };
 
 // ---------------------------------------------------------------------------
@@ -138,6 +140,9 @@ struct msfno_sht_plan_s {
   int* d_Lp = nullptr;
   int* d_off = nullptr;          // S-layout column offsets off[m]
   int table_loaded = 0;
+  // Xt / Yt slab of each m (-1: m not in this plan's m-set); full plans: slab[m] = m
+  std::vector<int> slab;
+  int nslab = 0;
   // cached Legendre GEMM descriptors for a given row count R
   int desc_R = -1;
   msfno::GemmDesc* d_desc = nullptr;

@@ -30,11 +30,13 @@ int launch_dc_fixup(float* Xt, int B, int C, int nlat, int ldk, const float* nsc
 // ---- spectral.hip ------------------------------------------------------------
 // Xn (BC, nlat, mmax) complex -> Xt (mmax, R=2BC, ldk); per-bc affine of the
 // spatial field folded in: m>0 -> s·X, m=0 -> s·X + 2π·t (real part).
+// slab (device, optional, size mmax): Xt slab of each m (-1 = skip); default slab = m.
 int launch_transpose_fwd(const float2* Xn, float* Xt, int B, int C, int nlat, int mmax, int ldk,
-                         const float* nscale, const float* nshift, hipStream_t s);
+                         const float* nscale, const float* nshift, hipStream_t s,
+                         const int* slab = nullptr);
 // Yt (mmax, R, ldk) -> Yn (BC, nlat, mmax); m >= mact written as 0.
 int launch_transpose_inv(const float* Yt, float2* Yn, int B, int C, int nlat, int mmax, int mact,
-                         int ldk, hipStream_t s);
+                         int ldk, hipStream_t s, const int* slab = nullptr);
 // Combine per-(bc) partial (mean, M2) statistics (np partials, each over `cnt`
 // elements except the last over `cnt_last`) and produce the affine that
 // implements InstanceNorm (+ optional FiLM): y = scale·x + shift.
@@ -42,6 +44,17 @@ int launch_chan_affine(const float2* partials, int64_t np, int64_t cnt, int64_t 
                        int B, int C, const float* w, const float* b, float eps,
                        const float* gamma, const float* beta, float film_scale, float* scale,
                        float* shift, hipStream_t s);
+// latitude-band sharding helpers (band.cpp)
+// rowstats (BC, np) (mean, M2) over cnt each -> out (BC, 3) fp64 {n, mean, M2}
+int launch_stats_partial(const float2* rowstats, int64_t np, int64_t cnt, int64_t BC, double* out,
+                         hipStream_t s);
+// parts (nparts, BC, 3) fp64 -> InstanceNorm (+FiLM) per-(b,c) affine
+int launch_chan_affine_parts(const double* parts, int nparts, int B, int C, const float* w,
+                             const float* b, float eps, const float* gamma, const float* beta,
+                             float film_scale, float* scale, float* shift, hipStream_t s);
+// slabs (rows, ldk) <-> per-band blocks (rows, H_p) at offset rows*row0[p]
+int launch_band_copy(const float* src, float* dst, int64_t rows, int nlat, int ldk,
+                     const int* d_row0, int W, bool to_bands, hipStream_t s);
 // W' [b] = W·diag(scale[b]),  b'[b] = bias + W·shift[b]
 int launch_fold_affine(const float* W, const float* bias, const float* scale, const float* shift,
                        float* Wf, float* bf, int B, int O, int I, hipStream_t s);

@@ -20,7 +20,8 @@ __global__ __launch_bounds__(256) void transpose_fwd_kernel(const float2* __rest
                                                             float* __restrict__ Xt, int B, int C,
                                                             int nlat, int mmax, int ldk,
                                                             const float* __restrict__ nscale,
-                                                            const float* __restrict__ nshift) {
+                                                            const float* __restrict__ nshift,
+                                                            const int* __restrict__ slab) {
   __shared__ float2 tile[TMM][TK + 1];
   const int k0 = blockIdx.x * TK, m0 = blockIdx.y * TMM;
   const int bc = blockIdx.z;
@@ -42,11 +43,12 @@ __global__ __launch_bounds__(256) void transpose_fwd_kernel(const float2* __rest
   for (int i = threadIdx.x; i < TK * TMM; i += 256) {
     const int mm = i / TK, kk = i - mm * TK;
     const int k = k0 + kk, m = m0 + mm;
-    if (k < nlat && m < mmax) {
+    const int sl = (m < mmax) ? (slab ? slab[m] : m) : -1;
+    if (k < nlat && sl >= 0) {
       float2 v = tile[mm][kk];
       v.x = v.x * sc + (m == 0 ? sh : 0.f);
       v.y = v.y * sc;
-      float* dst = Xt + (int64_t)m * R * ldk;
+      float* dst = Xt + (int64_t)sl * R * ldk;
       dst[rre * ldk + k] = v.x;
       dst[rim * ldk + k] = v.y;
     }
@@ -80,17 +82,19 @@ int launch_dc_fixup(float* Xt, int B, int C, int nlat, int ldk, const float* nsc
 }
 
 int launch_transpose_fwd(const float2* Xn, float* Xt, int B, int C, int nlat, int mmax, int ldk,
-                         const float* nscale, const float* nshift, hipStream_t s) {
+                         const float* nscale, const float* nshift, hipStream_t s,
+                         const int* slab) {
   dim3 grid((unsigned)cdiv(nlat, TK), (unsigned)cdiv(mmax, TMM), (unsigned)(B * C));
   hipLaunchKernelGGL(transpose_fwd_kernel, grid, dim3(256), 0, s, Xn, Xt, B, C, nlat, mmax, ldk,
-                     nscale, nshift);
+                     nscale, nshift, slab);
   return launch_check("transpose_fwd");
 }
 
 __global__ __launch_bounds__(256) void transpose_inv_kernel(const float* __restrict__ Yt,
                                                             float2* __restrict__ Yn, int B, int C,
                                                             int nlat, int mmax, int mact,
-                                                            int ldk) {
+                                                            int ldk,
+                                                            const int* __restrict__ slab) {
   __shared__ float2 tile[TMM][TK + 1];
   const int k0 = blockIdx.x * TK, m0 = blockIdx.y * TMM;
   const int bc = blockIdx.z;
@@ -102,8 +106,9 @@ __global__ __launch_bounds__(256) void transpose_inv_kernel(const float* __restr
     const int mm = i / TK, kk = i - mm * TK;
     const int k = k0 + kk, m = m0 + mm;
     float2 v = make_float2(0.f, 0.f);
-    if (k < nlat && m < mact) {
-      const float* src = Yt + (int64_t)m * R * ldk;
+    const int sl = (m < mact) ? (slab ? slab[m] : m) : -1;
+    if (k < nlat && sl >= 0) {
+      const float* src = Yt + (int64_t)sl * R * ldk;
       v = make_float2(src[rre * ldk + k], src[rim * ldk + k]);
     }
     tile[mm][kk] = v;
@@ -118,10 +123,10 @@ __global__ __launch_bounds__(256) void transpose_inv_kernel(const float* __restr
 }
 
 int launch_transpose_inv(const float* Yt, float2* Yn, int B, int C, int nlat, int mmax, int mact,
-                         int ldk, hipStream_t s) {
+                         int ldk, hipStream_t s, const int* slab) {
   dim3 grid((unsigned)cdiv(nlat, TK), (unsigned)cdiv(mmax, TMM), (unsigned)(B * C));
   hipLaunchKernelGGL(transpose_inv_kernel, grid, dim3(256), 0, s, Yt, Yn, B, C, nlat, mmax, mact,
-                     ldk);
+                     ldk, slab);
   return launch_check("transpose_inv");
 }
 
@@ -196,6 +201,133 @@ int launch_chan_affine(const float2* partials, int64_t np, int64_t cnt, int64_t 
   hipLaunchKernelGGL(chan_affine_kernel, dim3(B * C), dim3(256), 0, s, partials, np, cnt,
                      cnt_last, C, w, b, eps, gamma, beta, film_scale, scale, shift);
   return launch_check("chan_affine");
+}
+
+// ---------------------------------------------------------------------------
+// latitude-band sharding: per-rank statistics partials and the
+// band <-> full-latitude re-layout around the all-to-all exchanges
+// ---------------------------------------------------------------------------
+// rowstats (BC, np) (mean, M2) over cnt elements each -> out (BC, 3) fp64 {n, mean, M2}
+__global__ __launch_bounds__(256) void stats_partial_kernel(const float2* __restrict__ part,
+                                                            int64_t np, int64_t cnt,
+                                                            double* __restrict__ out) {
+  __shared__ double sn[256], smean[256], sm2[256];
+  const int bc = blockIdx.x;
+  const float2* p = part + (int64_t)bc * np;
+  Welford acc{0.0, 0.0, 0.0};
+  for (int64_t i = threadIdx.x; i < np; i += 256) {
+    const float2 v = p[i];
+    acc = wcombine(acc, Welford{(double)cnt, (double)v.x, (double)v.y});
+  }
+  sn[threadIdx.x] = acc.n;
+  smean[threadIdx.x] = acc.mean;
+  sm2[threadIdx.x] = acc.m2;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) {
+      Welford a{sn[threadIdx.x], smean[threadIdx.x], sm2[threadIdx.x]};
+      a = wcombine(a, Welford{sn[threadIdx.x + o], smean[threadIdx.x + o], sm2[threadIdx.x + o]});
+      sn[threadIdx.x] = a.n;
+      smean[threadIdx.x] = a.mean;
+      sm2[threadIdx.x] = a.m2;
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    out[3 * (int64_t)bc + 0] = sn[0];
+    out[3 * (int64_t)bc + 1] = smean[0];
+    out[3 * (int64_t)bc + 2] = sm2[0];
+  }
+}
+
+int launch_stats_partial(const float2* rowstats, int64_t np, int64_t cnt, int64_t BC, double* out,
+                         hipStream_t s) {
+  hipLaunchKernelGGL(stats_partial_kernel, dim3((unsigned)BC), dim3(256), 0, s, rowstats, np, cnt,
+                     out);
+  return launch_check("stats_partial");
+}
+
+// parts (nparts, BC, 3) -> InstanceNorm (+FiLM) affine, same math as chan_affine_kernel
+__global__ void chan_affine_parts_kernel(const double* __restrict__ parts, int nparts, int BC,
+                                         int C, const float* __restrict__ w,
+                                         const float* __restrict__ bsh, float eps,
+                                         const float* __restrict__ gamma,
+                                         const float* __restrict__ beta, float film_scale,
+                                         float* __restrict__ scale, float* __restrict__ shift) {
+  const int bc = blockIdx.x * blockDim.x + threadIdx.x;
+  if (bc >= BC) return;
+  const int c = bc % C;
+  Welford acc{0.0, 0.0, 0.0};
+  for (int p = 0; p < nparts; ++p) {
+    const double* q = parts + 3 * ((int64_t)p * BC + bc);
+    acc = wcombine(acc, Welford{q[0], q[1], q[2]});
+  }
+  const double var = acc.m2 / acc.n;
+  const double rstd = 1.0 / sqrt(var + (double)eps);
+  double sc = (w ? (double)w[c] : 1.0) * rstd;
+  double sh = (bsh ? (double)bsh[c] : 0.0) - sc * acc.mean;
+  if (gamma) {
+    const double g = 1.0 + (double)gamma[bc] * (double)film_scale;
+    sc *= g;
+    sh = sh * g + (double)beta[bc] * (double)film_scale;
+  }
+  scale[bc] = (float)sc;
+  shift[bc] = (float)sh;
+}
+
+int launch_chan_affine_parts(const double* parts, int nparts, int B, int C, const float* w,
+                             const float* b, float eps, const float* gamma, const float* beta,
+                             float film_scale, float* scale, float* shift, hipStream_t s) {
+  const int BC = B * C;
+  hipLaunchKernelGGL(chan_affine_parts_kernel, dim3((unsigned)cdiv(BC, 256)), dim3(256), 0, s,
+                     parts, nparts, BC, C, w, b, eps, gamma, beta, film_scale, scale, shift);
+  return launch_check("chan_affine_parts");
+}
+
+// Full-latitude slabs F (rows, ldk) [row = mi*R + r]  <->  band buffer Q laid out
+// per band p as (rows, H_p) at offset rows * row0[p]   (the all-to-all block of p).
+// One wave per row; TO_BANDS: F -> Q (pack), else Q -> F (unpack, pads k >= nlat).
+template <bool TO_BANDS>
+__global__ __launch_bounds__(256) void band_copy_kernel(const float* __restrict__ src,
+                                                        float* __restrict__ dst, int64_t rows,
+                                                        int nlat, int ldk,
+                                                        const int* __restrict__ row0, int W) {
+  __shared__ int r0[65];
+  for (int i = threadIdx.x; i <= W; i += 256) r0[i] = row0[i];
+  __syncthreads();
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const int lane = threadIdx.x & 63;
+  int p = 0;
+  for (int k = lane; k < (TO_BANDS ? nlat : ldk); k += 64) {
+    if (k >= nlat) {  // unpack only: zero the latitude padding
+      dst[row * ldk + k] = 0.f;
+      continue;
+    }
+    while (k >= r0[p + 1]) ++p;
+    const int hp = r0[p + 1] - r0[p];
+    const int64_t q = rows * r0[p] + row * hp + (k - r0[p]);
+    if (TO_BANDS)
+      dst[q] = src[row * ldk + k];
+    else
+      dst[row * ldk + k] = src[q];
+  }
+}
+
+int launch_band_copy(const float* src, float* dst, int64_t rows, int nlat, int ldk,
+                     const int* d_row0, int W, bool to_bands, hipStream_t s) {
+  if (W > 64) {
+    set_error("latitude-band sharding supports at most 64 ranks");
+    return MSFNO_EUNSUPPORTED;
+  }
+  const dim3 grid((unsigned)cdiv(rows, 4));
+  if (to_bands)
+    hipLaunchKernelGGL(band_copy_kernel<true>, grid, dim3(256), 0, s, src, dst, rows, nlat, ldk,
+                       d_row0, W);
+  else
+    hipLaunchKernelGGL(band_copy_kernel<false>, grid, dim3(256), 0, s, src, dst, rows, nlat, ldk,
+                       d_row0, W);
+  return launch_check("band_copy");
 }
 
 // W'[b][o][i] = W[o][i]·scale[b][i];  b'[b][o] = bias[o] + Σ_i W[o][i]·shift[b][i]
@@ -324,8 +456,8 @@ __global__ void relayout_table_kernel(const float* __restrict__ tab, float* __re
                                       int inverse) {
   const int m = blockIdx.y;
   const int L = lmax - m;
-  if (L <= 0) return;
   const int lp = Lp[m];
+  if (L <= 0 || lp == 0) return;  // lp == 0: m outside a sharded plan's m-set
   float* o = out + tab_off[m];
   const int64_t n = inverse ? (int64_t)L * ldk : (int64_t)nlat * lp;
   for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < n;

@@ -48,6 +48,18 @@ class BlockDesc(ctypes.Structure):
     ]
 
 
+class BandIO(ctypes.Structure):
+    """Mirror of ``msfno_band_io`` (include/msfno.h)."""
+
+    _fields_ = [
+        ("x", _vp), ("gamma", _vp), ("beta", _vp), ("film_scale", _f), ("out", _vp),
+        ("send", _vp), ("recv", _vp), ("stats_local", _vp), ("stats_all", _vp),
+    ]
+
+
+_ip = ctypes.POINTER(_i)
+_llp = ctypes.POINTER(ctypes.c_longlong)
+
 # (name, restype, argtypes) — every symbol declared in include/msfno.h
 SIGNATURES = [
     ("msfno_last_error", ctypes.c_char_p, []),
@@ -67,6 +79,14 @@ SIGNATURES = [
                                  _i, _vp, _sz, _vp]),
     ("msfno_filter_forward", _i, [ctypes.POINTER(BlockDesc), _vp, _vp, _vp, _vp, _i, _vp, _sz,
                                   _vp]),
+    ("msfno_band_partition", _i, [_i, _i, _i, _i, _ip, _ip]),
+    ("msfno_band_exchange_counts", _i, [_i, _i, _i, _i, _ip, _ip, _i, _i, _llp, _llp]),
+    ("msfno_band_plan_create", _i, [_i, _i, _i, _i, _i, _i, _ip, _ip, ctypes.POINTER(_vp)]),
+    ("msfno_band_plan_destroy", _i, [_vp]),
+    ("msfno_band_plan_load_tables", _i, [_vp, _vp, _vp, _vp]),
+    ("msfno_band_workspace_size", _sz, [ctypes.POINTER(BlockDesc), _vp, _i]),
+    ("msfno_band_block_stage", _i, [ctypes.POINTER(BlockDesc), _vp, _i, ctypes.POINTER(BandIO),
+                                    _i, _vp, _sz, _vp]),
     ("msfno_profile_enable", _i, [_i]),
     ("msfno_profile_collect", _i, [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_i)]),
     ("msfno_profile_stage_name", ctypes.c_char_p, [_i]),

@@ -8,3 +8,4 @@ from .sfnonet import (  # noqa: F401
     FourierNeuralOperatorBlock_Filmed,
     SpectralFilterLayer,
 )
+from .latband import LatBandBlock, LocalGroup, TorchComm, band_partition, exchange_counts  # noqa: F401,E501

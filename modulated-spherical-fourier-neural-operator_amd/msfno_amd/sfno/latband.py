@@ -1,0 +1,281 @@
+"""Latitude-band sharded SFNO-Block forward.
+
+The reference scales only by data-parallel replicas (one whole field per
+process, MSFNO/main.py:1153).  Here ONE batch of fields is split over the ranks
+of a process group: rank r keeps latitude rows [row_start[r], row_start[r+1])
+of every field for the pointwise / FFT / 1x1-conv / MLP work and the zonal
+wavenumbers {m : m_owner[m] == r} for the Legendre transforms and the spectral
+filter, which couple all latitudes of one m but are independent across m.
+Per block forward (include/msfno.h, "Latitude-band sharded SFNO-Block"):
+
+    stage 0  skip GEMM (side stream) + FFT of local rows      -> norm0 partials
+    all_gather(norm0 partials)                                  2*B*C*3 doubles
+    stage 1  norm0 affine, pack spectra by owner of m
+    all_to_all                                    B*C*nlat*mact*8 bytes in total
+    stage 2  Legendre fwd -> spectral filter -> Legendre inv on the local m-set
+    all_to_all                                                     same volume
+    stage 3  inverse FFT of local rows + skip                   -> norm1 partials
+    all_gather(norm1 partials)
+    stage 4  norm1 (+FiLM) -> MLP (+outer skip)
+
+The result equals ``block(x, gamma, beta, scale)`` on the gathered field up to
+fp32 rounding (Welford statistics are merged in fp64).  Collectives go through
+``torch.distributed`` (backend "nccl" = RCCL over xGMI on MI355X; "gloo" is
+supported by staging through host memory).  ``LocalGroup`` runs several
+virtual ranks of one process in lock step, for tests and single-GPU use.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+
+from .. import _native as N
+
+
+def band_partition(world: int, nlat: int, lmax: int, mmax: int):
+    """Default partition: balanced latitude bands + zig-zag m ownership."""
+    rows = (ctypes.c_int * (world + 1))()
+    own = (ctypes.c_int * mmax)()
+    N.check(N.lib().msfno_band_partition(world, nlat, lmax, mmax, rows, own), "band_partition")
+    return list(rows), list(own)
+
+
+def exchange_counts(world, rank, nlat, mmax, row_start, m_owner, R, phase):
+    """(send_counts, recv_counts) in floats per peer for all-to-all `phase`."""
+    rs = (ctypes.c_int * (world + 1))(*row_start)
+    mo = (ctypes.c_int * mmax)(*m_owner)
+    sc = (ctypes.c_longlong * world)()
+    rc = (ctypes.c_longlong * world)()
+    N.check(N.lib().msfno_band_exchange_counts(world, rank, nlat, mmax, rs, mo, R, phase, sc, rc),
+            "band_exchange_counts")
+    return list(sc), list(rc)
+
+
+class TorchComm:
+    """Collectives of one torch.distributed process group."""
+
+    def __init__(self, group=None):
+        import torch.distributed as dist
+        self.dist = dist
+        self.group = group
+        self.world = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+        self.host = dist.get_backend(group) == "gloo"
+
+    def all_gather(self, t):
+        src = t.cpu() if self.host else t
+        parts = [torch.empty_like(src) for _ in range(self.world)]
+        self.dist.all_gather(parts, src, group=self.group)
+        return torch.stack(parts).to(t.device)
+
+    def all_to_all(self, send, send_counts, recv, recv_counts):
+        ns, nr = sum(send_counts), sum(recv_counts)
+        if self.host:
+            r = torch.empty(nr, dtype=recv.dtype)
+            self.dist.all_to_all_single(r, send[:ns].cpu(), recv_counts, send_counts,
+                                        group=self.group)
+            recv[:nr].copy_(r)
+        else:
+            self.dist.all_to_all_single(recv[:nr], send[:ns], recv_counts, send_counts,
+                                        group=self.group)
+
+
+def _drive(gen, comm):
+    """Run one rank's stage generator against `comm`."""
+    req = next(gen)
+    while True:
+        if req[0] == "all_gather":
+            res = comm.all_gather(req[1])
+        else:
+            _, send, sc, recv, rc = req
+            comm.all_to_all(send, sc, recv, rc)
+            res = None
+        try:
+            req = gen.send(res)
+        except StopIteration as stop:
+            return stop.value
+
+
+class LocalGroup:
+    """Lock-step execution of several virtual ranks in one process (the
+    exchanges become device copies).  Used by the parity tests to run the
+    sharded path on one GPU, and by world-size-1 runs."""
+
+    @staticmethod
+    def run(gens):
+        reqs = [next(g) for g in gens]
+        outs = [None] * len(gens)
+        live = list(range(len(gens)))
+        while live:
+            kind = reqs[live[0]][0]
+            assert all(reqs[i][0] == kind for i in live), "ranks out of step"
+            res = [None] * len(gens)
+            if kind == "all_gather":
+                stacked = torch.stack([reqs[i][1] for i in live])
+                res = [stacked] * len(gens)
+            else:
+                W = len(gens)
+                offs = []
+                for p in range(W):
+                    sc = reqs[p][2]
+                    o, acc = [], 0
+                    for c in sc:
+                        o.append(acc)
+                        acc += c
+                    offs.append(o)
+                for q in range(W):
+                    recv, rc = reqs[q][3], reqs[q][4]
+                    acc = 0
+                    for p in range(W):
+                        n = rc[p]
+                        assert reqs[p][2][q] == n, "send/recv counts disagree"
+                        recv[acc:acc + n].copy_(reqs[p][1][offs[p][q]:offs[p][q] + n])
+                        acc += n
+            nxt = []
+            for i in live:
+                try:
+                    reqs[i] = gens[i].send(res[i])
+                    nxt.append(i)
+                except StopIteration as stop:
+                    outs[i] = stop.value
+            live = nxt
+        return outs
+
+
+class _BandPlan:
+    def __init__(self, nlat, nlon, lmax, mmax, world, rank, row_start, m_owner, device):
+        self.device = device
+        h = ctypes.c_void_p()
+        rs = (ctypes.c_int * (world + 1))(*row_start)
+        mo = (ctypes.c_int * mmax)(*m_owner)
+        with torch.cuda.device(device):
+            N.check(N.lib().msfno_band_plan_create(nlat, nlon, lmax, mmax, world, rank, rs, mo,
+                                                   ctypes.byref(h)), "msfno_band_plan_create")
+        self.handle = h
+        self.key = None
+
+    def load(self, fwd_table, inv_table, key):
+        if key == self.key:
+            return
+        with torch.cuda.device(self.device):
+            N.check(N.lib().msfno_band_plan_load_tables(self.handle, fwd_table.data_ptr(),
+                                                        inv_table.data_ptr(),
+                                                        N.stream_of(self.device)),
+                    "msfno_band_plan_load_tables")
+        self._tables = (fwd_table, inv_table)
+        self.key = key
+
+    def __del__(self):
+        try:
+            if self.handle:
+                N.lib().msfno_band_plan_destroy(self.handle)
+        except Exception:
+            pass
+
+
+class LatBandBlock:
+    """One rank's share of a latitude-band sharded FourierNeuralOperatorBlock[_Filmed].
+
+    ``block`` is the (replicated) block module; ``forward(x_local, gamma, beta,
+    scale)`` takes this rank's rows ``x[:, :, row_start[rank]:row_start[rank+1]]``
+    and returns the same rows of the block output."""
+
+    def __init__(self, block, rank: int, world: int, row_start=None, m_owner=None,
+                 device=None):
+        fwd, inv = block._transforms()
+        if (fwd.nlat, fwd.nlon) != (inv.nlat, inv.nlon):
+            raise NotImplementedError("latitude-band sharding needs equal input/output grids")
+        self.block = block
+        self.rank, self.world = rank, world
+        self.nlat, self.nlon, self.lmax, self.mmax = fwd.nlat, fwd.nlon, fwd.lmax, fwd.mmax
+        if row_start is None or m_owner is None:
+            row_start, m_owner = band_partition(world, self.nlat, self.lmax, self.mmax)
+        self.row_start, self.m_owner = list(row_start), list(m_owner)
+        self.device = device if device is not None else torch.device("cuda",
+                                                                    torch.cuda.current_device())
+        self.plan = _BandPlan(self.nlat, self.nlon, self.lmax, self.mmax, world, rank,
+                              self.row_start, self.m_owner, self.device)
+        self._bufs = {}
+
+    @property
+    def rows(self):
+        return self.row_start[self.rank], self.row_start[self.rank + 1]
+
+    def _tables(self):
+        fwd, inv = self.block._transforms()
+        tabs = []
+        for t in (fwd.weights, inv.pct):
+            if t.device != self.device or t.dtype != torch.float32 or not t.is_contiguous():
+                t = t.to(device=self.device, dtype=torch.float32).contiguous()
+            tabs.append(t)
+        key = tuple((t.data_ptr(), t._version) for t in (fwd.weights, inv.pct))
+        self.plan.load(tabs[0], tabs[1], key)
+
+    def _buffers(self, B, C):
+        key = (B, C)
+        if key not in self._bufs:
+            R = 2 * B * C
+            cnt = [exchange_counts(self.world, self.rank, self.nlat, self.mmax, self.row_start,
+                                   self.m_owner, R, ph) for ph in (0, 1)]
+            n = max(max(sum(s), sum(r)) for s, r in cnt)
+            dev = self.device
+            self._bufs[key] = dict(
+                counts=cnt,
+                send=torch.empty(max(n, 1), dtype=torch.float32, device=dev),
+                recv=torch.empty(max(n, 1), dtype=torch.float32, device=dev),
+                stats=torch.empty(B * C, 3, dtype=torch.float64, device=dev))
+        return self._bufs[key]
+
+    def stages(self, x, gamma=None, beta=None, scale=1.0):
+        """Generator over the five native stages; yields the collective requests
+        ("all_gather", tensor) / ("all_to_all", send, send_counts, recv, recv_counts)."""
+        x = N.require_device_f32(x, "band block input")
+        B, C, H, W = x.shape
+        r0, r1 = self.rows
+        if H != r1 - r0 or W != self.nlon or C != self.block.embed_dim_sfno:
+            raise ValueError(f"x_local must be (B, {self.block.embed_dim_sfno}, {r1 - r0}, "
+                             f"{self.nlon}), got {tuple(x.shape)}")
+        self._tables()
+        d, keep = self.block.native_desc()
+        if gamma is not None:
+            gamma = gamma.detach().float().reshape(B, C).contiguous()
+            beta = beta.detach().float().reshape(B, C).contiguous()
+        L = N.lib()
+        bufs = self._buffers(B, C)
+        nbytes = L.msfno_band_workspace_size(d, self.plan.handle, B)
+        ws = torch.empty(nbytes, dtype=torch.uint8, device=x.device)
+        out = torch.empty_like(x)
+        io = N.BandIO(x=x.data_ptr(), gamma=N.ptr(gamma), beta=N.ptr(beta),
+                      film_scale=float(scale), out=out.data_ptr(), send=bufs["send"].data_ptr(),
+                      recv=bufs["recv"].data_ptr(), stats_local=bufs["stats"].data_ptr(),
+                      stats_all=None)
+        stream = N.stream_of(x.device)
+
+        def stage(i):
+            N.check(L.msfno_band_block_stage(d, self.plan.handle, i, ctypes.byref(io), B,
+                                             ws.data_ptr(), nbytes, stream),
+                    f"band stage {i}")
+
+        (sc0, rc0), (sc1, rc1) = bufs["counts"]
+        stage(0)
+        st = yield ("all_gather", bufs["stats"])
+        io.stats_all = st.data_ptr()
+        stage(1)
+        yield ("all_to_all", bufs["send"], sc0, bufs["recv"], rc0)
+        stage(2)
+        yield ("all_to_all", bufs["send"], sc1, bufs["recv"], rc1)
+        stage(3)
+        st2 = yield ("all_gather", bufs["stats"])
+        io.stats_all = st2.data_ptr()
+        stage(4)
+        del keep, st, st2
+        return out
+
+    def forward(self, x, gamma=None, beta=None, scale=1.0, comm=None):
+        gen = self.stages(x, gamma, beta, scale)
+        if self.world == 1 and comm is None:
+            return LocalGroup.run([gen])[0]
+        return _drive(gen, comm if comm is not None else TorchComm())
+
+    __call__ = forward
