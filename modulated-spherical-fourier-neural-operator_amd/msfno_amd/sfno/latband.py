@@ -204,12 +204,15 @@ class LatBandBlock:
 
     def _tables(self):
         fwd, inv = self.block._transforms()
+        key = tuple((t.data_ptr(), t._version, t.dtype, str(t.device))
+                    for t in (fwd.weights, inv.pct))
+        if key == self.plan.key:  # (re)load only when a table tensor changed
+            return
         tabs = []
         for t in (fwd.weights, inv.pct):
             if t.device != self.device or t.dtype != torch.float32 or not t.is_contiguous():
                 t = t.to(device=self.device, dtype=torch.float32).contiguous()
             tabs.append(t)
-        key = tuple((t.data_ptr(), t._version) for t in (fwd.weights, inv.pct))
         self.plan.load(tabs[0], tabs[1], key)
 
     def _buffers(self, B, C):
