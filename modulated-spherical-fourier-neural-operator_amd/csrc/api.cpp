@@ -17,13 +17,15 @@ void SpecLayout::build(int lmax_, int mmax_, const std::vector<char>* mask) {
   mmax = mmax_;
   L.assign(mmax, 0);
   Lp.assign(mmax, 0);
+  Lpe.assign(mmax, 0);
   off.assign(mmax, 0);
   T = Tp = 0;
   mact = 0;
   for (int m = 0; m < mmax; ++m) {
     const int l = (mask && !(*mask)[m]) ? 0 : std::max(lmax - m, 0);
     L[m] = l;
-    Lp[m] = (int)round_up(l, 4);
+    Lpe[m] = (int)round_up((l + 1) / 2, 4);
+    Lp[m] = Lpe[m] + (int)round_up(l / 2, 4);
     off[m] = (int)Tp;
     T += l;
     Tp += Lp[m];
@@ -216,34 +218,69 @@ int side_ctx(SideCtx** out) {
 // ---------------------------------------------------------------------------
 
 int ensure_desc(msfno_sht_plan_s* p, int R, int other_ld, int64_t ldT) {
-  // forward plan: A = Xt (R x nlat, ld ldk), B = table, C = S (ld ldT)
-  // inverse plan: A = S (ld ldT), B = table, C = Yt (R x nlat, ld ldk)
+  // forward: A = Xt slab (R x K), B = table, C = S (ld ldT)
+  // inverse: A = S (ld ldT), B = table, C = Yt slab (R x N)
+  // symmetric plans: one even-parity and one odd-parity problem per m
   if (p->desc_R == R && p->d_desc) return MSFNO_OK;
   int bm, bn;
   gemm_tile_dims(TILE_128x64, &bm, &bn);
   std::vector<GemmDesc> d;
   int tiles = 0;
   const SpecLayout& L = p->spec;
-  for (int m = 0; m < L.mact; ++m) {
-    if (L.L[m] == 0) continue;  // m outside a sharded plan's m-set
-    const int64_t sl = p->slab[m];
-    GemmDesc g{};
-    g.M = R;
-    if (!p->inverse) {
-      g.N = L.Lp[m]; g.K = p->nlat;
-      g.lda = p->ldk; g.ldb = L.Lp[m]; g.ldc = (int)ldT;
-      g.offA = sl * R * p->ldk; g.offB = p->tab_off[m]; g.offC = L.off[m];
-    } else {
-      g.N = p->nlat; g.K = L.L[m];
-      g.lda = (int)ldT; g.ldb = p->ldk; g.ldc = p->ldk;
-      g.offA = L.off[m]; g.offB = p->tab_off[m]; g.offC = sl * R * p->ldk;
-    }
+  auto push = [&](GemmDesc g) {
     g.tiles_m = (int)cdiv(g.M, bm);
     g.tiles_n = (int)cdiv(g.N, bn);
+    if (g.tiles_m * g.tiles_n == 0) return;
     g.tile_start = tiles;
-    g.flags = (!p->inverse && m > 0) ? 1 : 0;  // m = 0 is normalised by dc_fixup
     tiles += g.tiles_m * g.tiles_n;
     d.push_back(g);
+  };
+  const int ldko = (int)round_up(p->Ko, 4);
+  for (int m = 0; m < L.mact; ++m) {
+    if (L.L[m] == 0) continue;  // m outside a sharded plan's m-set
+    const int64_t slab = (int64_t)p->slab[m] * R * p->ldk;
+    const int lpe = L.Lpe[m], lpo = L.Lp[m] - L.Lpe[m];
+    const int le = (L.L[m] + 1) / 2, lo = L.L[m] / 2;
+    const int flags = (!p->inverse && m > 0) ? 1 : 0;  // m = 0 is normalised by dc_fixup
+    GemmDesc g{};
+    g.M = R;
+    g.flags = flags;
+    if (!p->sym) {
+      if (!p->inverse) {
+        g.N = L.Lp[m]; g.K = p->nlat;
+        g.lda = p->ldk; g.ldb = L.Lp[m]; g.ldc = (int)ldT;
+        g.offA = slab; g.offB = p->tab_off[m]; g.offC = L.off[m];
+      } else {
+        g.N = p->nlat; g.K = L.Lp[m];
+        g.lda = (int)ldT; g.ldb = p->ldk; g.ldc = p->ldk;
+        g.offA = L.off[m]; g.offB = p->tab_off[m]; g.offC = slab;
+      }
+      push(g);
+      continue;
+    }
+    if (!p->inverse) {
+      GemmDesc e = g;  // even: Xs (R x Ke) . We (Ke x Lpe)
+      e.N = lpe; e.K = p->Ke; e.lda = p->ldk; e.ldb = lpe; e.ldc = (int)ldT;
+      e.offA = slab; e.offB = p->tab_off[m]; e.offC = L.off[m];
+      push(e);
+      if (lo > 0) {
+        GemmDesc o = g;  // odd: Xa (R x Ko) . Wo (Ko x Lpo)
+        o.N = lpo; o.K = p->Ko; o.lda = p->ldk; o.ldb = lpo; o.ldc = (int)ldT;
+        o.offA = slab + p->ldke; o.offB = p->tab_off[m] + (int64_t)p->Ke * lpe;
+        o.offC = L.off[m] + lpe;
+        push(o);
+      }
+    } else {
+      GemmDesc e = g;  // even: E (R x Ke) = S_e (R x Le) . Pe (Le x Ke)
+      e.N = p->Ke; e.K = le; e.lda = (int)ldT; e.ldb = p->ldke; e.ldc = p->ldk;
+      e.offA = L.off[m]; e.offB = p->tab_off[m]; e.offC = slab;
+      push(e);
+      GemmDesc o = g;  // odd: O (R x Ko) = S_o (R x Lo) . Po (Lo x Ko)
+      o.N = p->Ko; o.K = lo; o.lda = (int)ldT; o.ldb = ldko; o.ldc = p->ldk;
+      o.offA = L.off[m] + lpe; o.offB = p->tab_off[m] + (int64_t)lpe * p->ldke;
+      o.offC = slab + p->ldke;
+      if (lo > 0) push(o);
+    }
   }
   (void)other_ld;
   if (p->d_desc) MSFNO_CHECK_HIP(hipFree(p->d_desc));
@@ -260,13 +297,27 @@ int ensure_desc(msfno_sht_plan_s* p, int R, int other_ld, int64_t ldT) {
 // MSFNO_FFT_TILE=1 selects the fused FFT+transpose tile kernels instead of the
 // row FFT + separate transpose kernels (measured slower on MI355X at 721x1440:
 // DESIGN.md §5); kept as an A/B switch.
-bool use_fft_tile(const FFTPlan& f) {
+bool use_fft_tile(const msfno_sht_plan_s* p) {
   static int mode = -1;
   if (mode < 0) {
     const char* e = getenv("MSFNO_FFT_TILE");
     mode = (e && e[0] == '1') ? 1 : 0;
   }
-  return mode == 1 && fft_tile_supported(f);
+  return mode == 1 && !p->sym && fft_tile_supported(p->fft);  // tile kernels: general layout
+}
+
+// Xn (BC, nlat, mmax) -> the plan's slab layout (hemispheres folded when symmetric)
+int transpose_fwd_plan(const msfno_sht_plan_s* p, const float2* Xn, float* Xt, int B, int C,
+                       const float* nscale, const float* nshift, hipStream_t s) {
+  if (p->sym)
+    return launch_transpose_fwd_sym(Xn, Xt, B, C, p->geom(), p->mmax, nscale, nshift, s);
+  return launch_transpose_fwd(Xn, Xt, B, C, p->nlat, p->mmax, p->ldk, nscale, nshift, s);
+}
+
+int transpose_inv_plan(const msfno_sht_plan_s* p, const float* Yt, float2* Yn, int B, int C,
+                       hipStream_t s) {
+  if (p->sym) return launch_transpose_inv_sym(Yt, Yn, B, C, p->geom(), p->mmax, p->spec.mact, s);
+  return launch_transpose_inv(Yt, Yn, B, C, p->nlat, p->mmax, p->spec.mact, p->ldk, s);
 }
 
 int legendre_fwd(msfno_sht_plan_s* f, const float* Xt, float* S, int R, hipStream_t s,
@@ -388,11 +439,11 @@ int run_filter(const msfno_block_desc* d, msfno_sht_plan_s* f, msfno_sht_plan_s*
   } else {
     MSFNO_REQUIRE(d->lin_w, MSFNO_EINVAL, "missing linear spectral weight");
     prof(ST_LIN_GATHER, s);
-    MSFNO_TRY(launch_spec_to_tril(L, b.Sa, b.xt, B, (int)C, f->d_off, s));
+    MSFNO_TRY(launch_spec_to_tril(*f, b.Sa, b.xt, B, (int)C, s));
     prof(ST_LIN_CONTRACT, s);
     MSFNO_TRY(launch_compl_contract(b.xt, d->lin_w, b.yt, B, (int)C, (int)C, L.T, s));
     prof(ST_LIN_SCATTER, s);
-    MSFNO_TRY(launch_tril_to_spec(L, b.yt, b.Sa, B, (int)C, f->d_off, s));
+    MSFNO_TRY(launch_tril_to_spec(*f, b.yt, b.Sa, B, (int)C, s));
   }
   (void)g;
   return MSFNO_OK;
@@ -404,7 +455,7 @@ int run_spectral(const msfno_block_desc* d, msfno_sht_plan_s* f, msfno_sht_plan_
   const int64_t C = d->C, BC = (int64_t)B * C, R = 2 * BC;
   prof(ST_FFT_FWD, s);
   const float scale = (float)(2.0 * M_PI / f->nlon);
-  if (use_fft_tile(f->fft)) {
+  if (use_fft_tile(f)) {
     // fused FFT + transpose; norm0 applied afterwards (m = 0 fix-up + GEMM row scale)
     MSFNO_TRY(launch_fft_r2c_tile(f->fft, x, b.Xt, norm0 ? b.rs0 : nullptr, B, (int)C, f->nlat,
                                   f->mmax, f->ldk, scale, s));
@@ -427,8 +478,8 @@ int run_spectral(const msfno_block_desc* d, msfno_sht_plan_s* f, msfno_sht_plan_
                                    s));
     }
     prof(ST_TRANSPOSE_FWD, s);
-    MSFNO_TRY(launch_transpose_fwd(b.Xn, b.Xt, B, (int)C, f->nlat, f->mmax, f->ldk,
-                                   norm0 ? b.sc0 : nullptr, norm0 ? b.sh0 : nullptr, s));
+    MSFNO_TRY(transpose_fwd_plan(f, b.Xn, b.Xt, B, (int)C, norm0 ? b.sc0 : nullptr,
+                                 norm0 ? b.sh0 : nullptr, s));
     prof(ST_LEG_FWD, s);
     MSFNO_TRY(legendre_fwd(f, b.Xt, b.Sa, (int)R, s));
   }
@@ -442,18 +493,38 @@ int run_spectral(const msfno_block_desc* d, msfno_sht_plan_s* f, msfno_sht_plan_
 int run_inverse_fft(msfno_sht_plan_s* g, const BlockBufs& b, int B, int C, float* out,
                            const float* addsrc, float2* rowstats, int act, hipStream_t s) {
   const int64_t BC = (int64_t)B * C;
-  if (use_fft_tile(g->fft) && addsrc == nullptr) {
+  if (use_fft_tile(g) && addsrc == nullptr) {
     prof(ST_FFT_INV, s);
     return launch_fft_c2r_tile(g->fft, b.Yt, out, rowstats, B, C, g->nlat, g->mmax,
                                g->spec.mact, g->ldk, act, s);
   }
   prof(ST_TRANSPOSE_INV, s);
-  MSFNO_TRY(launch_transpose_inv(b.Yt, b.Yn, B, C, g->nlat, g->mmax, g->spec.mact, g->ldk, s));
+  MSFNO_TRY(transpose_inv_plan(g, b.Yt, b.Yn, B, C, s));
   prof(ST_FFT_INV, s);
   return launch_fft_c2r_rows(g->fft, b.Yn, out, addsrc, rowstats, BC * g->nlat, g->mmax, act, s);
   return MSFNO_OK;
 }
 
+
+// per-m table offsets of the plan GEMM layout:
+//   general:   fwd  W (nlat x Lp) columns in S order;  inv  P (Lp x ldk) rows in S order
+//   symmetric: fwd  We (Ke x Lpe), Wo (Ko x Lpo);      inv  Pe (Lpe x ldke), Po (Lpo x ldko)
+void set_table_offsets(msfno_sht_plan_s* p, int sym) {
+  const SpecLayout& L = p->spec;
+  p->tab_off.assign(p->mmax, 0);
+  int64_t acc = 0;
+  for (int m = 0; m < p->mmax; ++m) {
+    p->tab_off[m] = acc;
+    if (L.L[m] == 0) continue;
+    const int64_t lpe = L.Lpe[m], lpo = L.Lp[m] - L.Lpe[m];
+    if (!sym)
+      acc += p->inverse ? (int64_t)L.Lp[m] * p->ldk : (int64_t)p->nlat * L.Lp[m];
+    else
+      acc += p->inverse ? lpe * p->ldke + lpo * round_up(p->Ko, 4)
+                        : (int64_t)p->Ke * lpe + (int64_t)p->Ko * lpo;
+  }
+  if (!sym) p->table_elems = acc;
+}
 
 int plan_create(int nlat, int nlon, int lmax, int mmax, int inverse,
                 const std::vector<char>* mask, msfno_sht_plan_s** plan) {
@@ -462,7 +533,11 @@ int plan_create(int nlat, int nlon, int lmax, int mmax, int inverse,
   MSFNO_REQUIRE(!mask || (int)mask->size() == mmax, MSFNO_EINVAL, "m-set mask must have mmax entries");
   auto* p = new msfno_sht_plan_s();
   p->nlat = nlat; p->nlon = nlon; p->lmax = lmax; p->mmax = mmax; p->inverse = inverse ? 1 : 0;
-  p->ldk = (int)round_up(nlat, 4);
+  p->nh = nlat / 2;
+  p->Ke = nlat - p->nh;
+  p->Ko = p->nh;
+  p->ldke = (int)round_up(p->Ke, 4);
+  p->ldk = (int)std::max<int64_t>(round_up(nlat, 4), p->ldke + round_up(p->Ko, 4));
   p->spec.build(lmax, mmax, mask);
   p->slab.assign(mmax, -1);
   for (int m = 0; m < mmax; ++m) {
@@ -472,17 +547,15 @@ int plan_create(int nlat, int nlon, int lmax, int mmax, int inverse,
   if (!mask) p->nslab = mmax;
   int rc = fft_plan_build(p->fft, nlon);
   if (rc != MSFNO_OK) { delete p; return rc; }
-  p->tab_off.assign(mmax, 0);
-  int64_t acc = 0;
-  for (int m = 0; m < mmax; ++m) {
-    p->tab_off[m] = acc;
-    acc += p->inverse ? (int64_t)p->spec.L[m] * p->ldk : (int64_t)nlat * p->spec.Lp[m];
-  }
-  p->table_elems = acc;
+  // table sized for the general (non-symmetric) layout, the larger of the two
+  set_table_offsets(p, 0);
+  const int64_t acc = p->table_elems;
   hipError_t e = hipMalloc(&p->table, std::max<int64_t>(acc, 4) * sizeof(float));
   if (e == hipSuccess) e = hipMalloc(&p->d_tab_off, mmax * sizeof(int64_t));
   if (e == hipSuccess) e = hipMalloc(&p->d_Lp, mmax * sizeof(int));
   if (e == hipSuccess) e = hipMalloc(&p->d_off, mmax * sizeof(int));
+  if (e == hipSuccess) e = hipMalloc(&p->d_Lpe, mmax * sizeof(int));
+  if (e == hipSuccess) e = hipMemcpy(p->d_Lpe, p->spec.Lpe.data(), mmax * sizeof(int), hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipMemcpy(p->d_tab_off, p->tab_off.data(), mmax * sizeof(int64_t), hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipMemcpy(p->d_Lp, p->spec.Lp.data(), mmax * sizeof(int), hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipMemcpy(p->d_off, p->spec.off.data(), mmax * sizeof(int), hipMemcpyHostToDevice);
@@ -493,6 +566,28 @@ int plan_create(int nlat, int nlon, int lmax, int mmax, int inverse,
   }
   *plan = p;
   return MSFNO_OK;
+}
+
+// channel MLP of the block (layers.py:145-178) on x1 (B, C, P) with norm1/FiLM
+// already folded into (W1f, b1f):  out = W2·GELU(W1f·x1 + b1f) + b2 (+ resid).
+// GELU(erf) in fc1's epilogue on 128x64 tiles, bias + outer skip in fc2's
+// (measured cheapest split: DESIGN.md §8).
+int run_mlp(const msfno_block_desc* d, const float* W1f, const float* b1f, const float* x1,
+            float* h, float* out, const float* resid, int B, int64_t P, hipStream_t s) {
+  const int64_t C = d->C, Hd = d->mlp_hidden;
+  prof(ST_FC1, s);
+  GemmEpi e1;
+  e1.bias = b1f;
+  e1.sBias = Hd;
+  e1.act = 1;
+  MSFNO_TRY(gemm_uniform(TILE_128x64, W1f, x1, h, (int)Hd, (int)P, (int)C, (int)C, (int)P,
+                         (int)P, Hd * C, C * P, Hd * P, B, e1, s));
+  prof(ST_FC2, s);
+  GemmEpi e2;
+  e2.bias = d->fc2_b;
+  if (resid) { e2.addend = resid; e2.sD = C * P; e2.ldd = (int)P; }
+  return gemm_uniform(TILE_128x128, d->fc2_w, h, out, (int)C, (int)P, (int)Hd, (int)Hd, (int)P,
+                      (int)P, 0, Hd * P, C * P, B, e2, s);
 }
 }  // namespace msfno
 
@@ -530,6 +625,7 @@ int msfno_sht_plan_destroy(msfno_sht_plan_t p) {
   if (p->d_tab_off) (void)hipFree(p->d_tab_off);
   if (p->d_Lp) (void)hipFree(p->d_Lp);
   if (p->d_off) (void)hipFree(p->d_off);
+  if (p->d_Lpe) (void)hipFree(p->d_Lpe);
   if (p->d_desc) (void)hipFree(p->d_desc);
   delete p;
   return MSFNO_OK;
@@ -537,7 +633,30 @@ int msfno_sht_plan_destroy(msfno_sht_plan_t p) {
 
 int msfno_sht_plan_load_table(msfno_sht_plan_t p, const float* table, void* stream) {
   MSFNO_REQUIRE(p && table, MSFNO_EINVAL, "null plan or table");
-  MSFNO_TRY(launch_relayout_table(*p, table, (hipStream_t)stream));
+  hipStream_t s = (hipStream_t)stream;
+  // one-time setup: detect the equatorial symmetry of this table (host sync)
+  int sym = 0;
+  if (!getenv("MSFNO_NO_SYM") && p->nlat >= 2) {
+    int* d_flag = nullptr;
+    MSFNO_CHECK_HIP(hipMalloc(&d_flag, sizeof(int)));
+    int h_flag = 0;
+    hipError_t e = hipMemsetAsync(d_flag, 0, sizeof(int), s);
+    int rc = MSFNO_OK;
+    if (e == hipSuccess) rc = launch_check_symmetry(table, p->mmax, p->lmax, p->nlat, d_flag, s);
+    if (e == hipSuccess && rc == MSFNO_OK)
+      e = hipMemcpyAsync(&h_flag, d_flag, sizeof(int), hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    (void)hipFree(d_flag);
+    MSFNO_TRY(rc);
+    MSFNO_CHECK_HIP(e);
+    sym = h_flag == 0;
+  }
+  p->sym = sym;
+  set_table_offsets(p, sym);
+  MSFNO_CHECK_HIP(hipMemcpy(p->d_tab_off, p->tab_off.data(), p->mmax * sizeof(int64_t),
+                            hipMemcpyHostToDevice));
+  p->desc_R = -1;  // descriptors depend on the layout
+  MSFNO_TRY(launch_relayout_table(*p, table, s));
   p->table_loaded = 1;
   return MSFNO_OK;
 }
@@ -565,11 +684,11 @@ int msfno_sht_forward(msfno_sht_plan_t p, const float* x, float* out, int bc, vo
   float* Xt = cv.take<float>((int64_t)p->mmax * R * p->ldk);
   float* S = cv.take<float>(R * p->spec.ldT);
   const float scale = (float)(2.0 * M_PI / p->nlon);
-  if (use_fft_tile(p->fft)) {
+  if (use_fft_tile(p)) {
     MSFNO_TRY(launch_fft_r2c_tile(p->fft, x, Xt, nullptr, 1, bc, p->nlat, p->mmax, p->ldk, scale, s));
   } else {
     MSFNO_TRY(launch_fft_r2c_rows(p->fft, x, Xn, nullptr, (int64_t)bc * p->nlat, p->mmax, scale, s));
-    MSFNO_TRY(launch_transpose_fwd(Xn, Xt, 1, bc, p->nlat, p->mmax, p->ldk, nullptr, nullptr, s));
+    MSFNO_TRY(transpose_fwd_plan(p, Xn, Xt, 1, bc, nullptr, nullptr, s));
   }
   MSFNO_TRY(legendre_fwd(p, Xt, S, (int)R, s));
   MSFNO_TRY(launch_spec_to_ref(*p, S, reinterpret_cast<float2*>(out), 1, bc, p->d_off, s));
@@ -590,11 +709,11 @@ int msfno_sht_inverse(msfno_sht_plan_t p, const float* in, float* x, int bc, voi
   float* S = cv.take<float>(R * p->spec.ldT);
   MSFNO_TRY(launch_ref_to_spec(*p, reinterpret_cast<const float2*>(in), S, 1, bc, p->d_off, s));
   MSFNO_TRY(legendre_inv(p, S, Yt, (int)R, s));
-  if (use_fft_tile(p->fft)) {
+  if (use_fft_tile(p)) {
     MSFNO_TRY(launch_fft_c2r_tile(p->fft, Yt, x, nullptr, 1, bc, p->nlat, p->mmax, p->spec.mact,
                                   p->ldk, 0, s));
   } else {
-    MSFNO_TRY(launch_transpose_inv(Yt, Yn, 1, bc, p->nlat, p->mmax, p->spec.mact, p->ldk, s));
+    MSFNO_TRY(transpose_inv_plan(p, Yt, Yn, 1, bc, s));
     MSFNO_TRY(launch_fft_c2r_rows(p->fft, Yn, x, nullptr, nullptr, (int64_t)bc * p->nlat, p->mmax, 0, s));
   }
   return MSFNO_OK;
@@ -701,20 +820,7 @@ int msfno_block_forward(const msfno_block_desc* d, msfno_sht_plan_t f, msfno_sht
     const int64_t Hd = d->mlp_hidden;
     MSFNO_TRY(launch_fold_affine(d->fc1_w, d->fc1_b, b.sc1, b.sh1, b.W1f, b.b1f, B, (int)Hd,
                                  (int)C, s));
-    prof(ST_FC1, s);
-    GemmEpi e1;  // pre-activation h = W1'·x1 + b1' (GELU is applied when fc2 stages h)
-    e1.bias = b.b1f; e1.sBias = Hd;
-    MSFNO_TRY(gemm_uniform(TILE_128x128, b.W1f, x1, b.h, (int)Hd, (int)P, (int)C, (int)C, (int)P,
-                           (int)P, Hd * C, C * P, Hd * P, B, e1, s));
-    prof(ST_FC2, s);
-    GemmEpi e2;
-    e2.act = 2;
-    e2.bias = d->fc2_b;
-    if (resid) { e2.addend = resid; e2.sD = C * P; e2.ldd = (int)P; }
-    // one M tile for C <= 256, so every h element is GELU'd exactly once while staged
-    const GemmTile t2 = C <= 256 && C > 128 ? TILE_256x64 : TILE_128x128;
-    MSFNO_TRY(gemm_uniform(t2, d->fc2_w, b.h, out, (int)C, (int)P, (int)Hd, (int)Hd,
-                           (int)P, (int)P, 0, Hd * P, C * P, B, e2, s));
+    MSFNO_TRY(run_mlp(d, b.W1f, b.b1f, x1, b.h, out, resid, B, P, s));
   } else {
     prof(ST_OUT_AFFINE, s);
     MSFNO_TRY(launch_affine_rows(x1, b.sc1, b.sh1, resid, out, BC, P, 0, nullptr, 0, s));

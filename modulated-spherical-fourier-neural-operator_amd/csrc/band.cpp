@@ -289,7 +289,7 @@ int msfno_band_block_stage(const msfno_block_desc* d, msfno_band_plan_t p, int s
       MSFNO_REQUIRE(io->send && io->recv, MSFNO_EINVAL, "stage 2 needs send and recv");
       if (p->nm == 0) break;  // this rank owns no zonal wavenumber
       prof(ST_BAND_GATHER, s);
-      MSFNO_TRY(launch_band_copy(io->recv, b.Xt, slab_rows, p->nlat, p->fwd->ldk, p->d_row0,
+      MSFNO_TRY(launch_band_copy(io->recv, b.Xt, slab_rows, p->fwd->geom(), p->d_row0,
                                  p->world, false, s));
       prof(ST_LEG_FWD, s);
       MSFNO_TRY(legendre_fwd(p->fwd, b.Xt, b.fb.Sa, (int)R, s));
@@ -297,7 +297,7 @@ int msfno_band_block_stage(const msfno_block_desc* d, msfno_band_plan_t p, int s
       prof(ST_LEG_INV, s);
       MSFNO_TRY(legendre_inv(p->inv, b.fb.Sa, b.Xt, (int)R, s));
       prof(ST_BAND_SCATTER, s);
-      MSFNO_TRY(launch_band_copy(b.Xt, io->send, slab_rows, p->nlat, p->inv->ldk, p->d_row0,
+      MSFNO_TRY(launch_band_copy(b.Xt, io->send, slab_rows, p->inv->geom(), p->d_row0,
                                  p->world, true, s));
       break;
     }
@@ -337,20 +337,7 @@ int msfno_band_block_stage(const msfno_block_desc* d, msfno_band_plan_t p, int s
         const int64_t Hd = d->mlp_hidden;
         MSFNO_TRY(launch_fold_affine(d->fc1_w, d->fc1_b, b.sc1, b.sh1, b.W1f, b.b1f, B, (int)Hd,
                                      (int)C, s));
-        prof(ST_FC1, s);
-        GemmEpi e1;
-        e1.bias = b.b1f;
-        e1.sBias = Hd;
-        MSFNO_TRY(gemm_uniform(TILE_128x128, b.W1f, b.x1, b.h, (int)Hd, (int)Pl, (int)C, (int)C,
-                               (int)Pl, (int)Pl, Hd * C, C * Pl, Hd * Pl, B, e1, s));
-        prof(ST_FC2, s);
-        GemmEpi e2;
-        e2.act = 2;
-        e2.bias = d->fc2_b;
-        if (resid) { e2.addend = resid; e2.sD = C * Pl; e2.ldd = (int)Pl; }
-        const GemmTile t2 = C <= 256 && C > 128 ? TILE_256x64 : TILE_128x128;
-        MSFNO_TRY(gemm_uniform(t2, d->fc2_w, b.h, io->out, (int)C, (int)Pl, (int)Hd, (int)Hd,
-                               (int)Pl, (int)Pl, 0, Hd * Pl, C * Pl, B, e2, s));
+        MSFNO_TRY(run_mlp(d, b.W1f, b.b1f, b.x1, b.h, io->out, resid, B, Pl, s));
       } else {
         prof(ST_OUT_AFFINE, s);
         MSFNO_TRY(launch_affine_rows(b.x1, b.sc1, b.sh1, resid, io->out, BC, Pl, 0, nullptr, 0, s));

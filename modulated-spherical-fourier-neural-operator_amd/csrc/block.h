@@ -46,13 +46,21 @@ void carve_block(Carve& cv, BlockBufs& b, const msfno_block_desc* d, const msfno
                  const msfno_sht_plan_s* g, int B, bool with_norms);
 int check_pair(const msfno_block_desc* d, const msfno_sht_plan_s* f, const msfno_sht_plan_s* g);
 int ensure_desc(msfno_sht_plan_s* p, int R, int other_ld, int64_t ldT);
+int transpose_fwd_plan(const msfno_sht_plan_s* p, const float2* Xn, float* Xt, int B, int C,
+                       const float* nscale, const float* nshift, hipStream_t s);
+int transpose_inv_plan(const msfno_sht_plan_s* p, const float* Yt, float2* Yn, int B, int C,
+                       hipStream_t s);
 int legendre_fwd(msfno_sht_plan_s* f, const float* Xt, float* S, int R, hipStream_t s,
                  const float* rowscale = nullptr, int C = 0);
 int legendre_inv(msfno_sht_plan_s* g, const float* S, float* Yt, int R, hipStream_t s);
 // spectral filter on S (f->spec layout) in b.Sa (in place)
 int run_filter(const msfno_block_desc* d, msfno_sht_plan_s* f, msfno_sht_plan_s* g,
                const BlockBufs& b, int B, hipStream_t s);
-bool use_fft_tile(const FFTPlan& f);
+bool use_fft_tile(const msfno_sht_plan_s* p);
+void set_table_offsets(msfno_sht_plan_s* p, int sym);
+// channel MLP with norm1/FiLM folded into (W1f, b1f): out = W2·GELU(W1f·x1 + b1f) + b2 (+resid)
+int run_mlp(const msfno_block_desc* d, const float* W1f, const float* b1f, const float* x1,
+            float* h, float* out, const float* resid, int B, int64_t P, hipStream_t s);
 // plan construction (mask: optional m-set, see SpecLayout::build)
 int plan_create(int nlat, int nlon, int lmax, int mmax, int inverse,
                 const std::vector<char>* mask, msfno_sht_plan_s** out);

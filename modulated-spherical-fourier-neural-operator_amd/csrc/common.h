@@ -55,20 +55,31 @@ inline int64_t round_up(int64_t v, int64_t m) { return (v + m - 1) / m * m; }
 inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
 // ---------------------------------------------------------------------------
-// Spectral ("S") layout, m-major packed triangle:
-//   row r = (b*2 + ri)*C + c ;  column t = off[m] + (l - m),  l in [m, lmax)
-//   each m block is padded to Lp_m = round_up(lmax-m, 4) columns (zeros).
+// Spectral ("S") layout, m-major packed triangle, parity split:
+//   row r = (b*2 + ri)*C + c ;  for j = l - m (l in [m, lmax)):
+//     j even -> column off[m] + j/2           (Le_m = ceil(L_m/2) columns)
+//     j odd  -> column off[m] + Lpe_m + j/2   (Lo_m = floor(L_m/2) columns)
+//   with Lpe_m = round_up(Le_m, 4), Lp_m = Lpe_m + round_up(Lo_m, 4); pads are 0.
+// The split matches the equatorial symmetry P_l^m(-x) = (-1)^(l-m) P_l^m(x)
+// that halves the Legendre work on symmetric grids (see msfno_sht_plan_s::sym).
 // ---------------------------------------------------------------------------
+__host__ __device__ inline int64_t spec_col(const int* off, const int* Lpe, int m, int l) {
+  const int j = l - m;
+  return off[m] + ((j & 1) ? Lpe[m] : 0) + (j >> 1);
+}
+
 struct SpecLayout {
   int lmax = 0, mmax = 0;
   int mact = 0;                 // number of m with lmax - m > 0
   std::vector<int> L, Lp, off;  // per m (size mmax)
+  std::vector<int> Lpe;         // per m: padded even-parity block width
   int64_t T = 0;                // number of (l,m) with l>=m (tril count)
   int64_t Tp = 0;               // total padded columns
   int64_t ldT = 0;              // row stride of S buffers (multiple of 4)
   // mask (size mmax, optional): keep only the m with mask[m] != 0 (latitude-band
   // sharding: the m-set owned by one rank); the others get L = Lp = 0
   void build(int lmax_, int mmax_, const std::vector<char>* mask = nullptr);
+  int64_t col(int m, int l) const { return spec_col(off.data(), Lpe.data(), m, l); }
 };
 
 // ---------------------------------------------------------------------------
@@ -87,6 +98,15 @@ struct FFTPlan {
   float2* twN = nullptr;  // e^{-2πi k/N}, k <= N/2   (device)
 };
 int fft_plan_build(FFTPlan& p, int N);
+
+// latitude geometry of a plan passed to kernels by value
+struct LatGeom {
+  int sym;        // equatorially symmetric parity-split slabs
+  int nlat, nh;   // nh = nlat / 2 (pairs k, nlat-1-k for k < nh; centre row if odd)
+  int Ke, Ko;     // nlat - nh, nh
+  int ldke;       // column of Xa in a slab row
+  int ldk;        // slab row stride
+};
 void fft_plan_free(FFTPlan& p);
 
 // ---------------------------------------------------------------------------
@@ -130,7 +150,7 @@ void gemm_tile_dims(GemmTile tile, int* bm, int* bn);
 
 struct msfno_sht_plan_s {
   int nlat, nlon, lmax, mmax, inverse;
-  int ldk;                       // padded latitude stride (multiple of 4)
+  int ldk;                       // slab row stride (>= round_up(nlat,4), fits both layouts)
   msfno::SpecLayout spec;
   msfno::FFTPlan fft;
   float* table = nullptr;        // device, plan GEMM layout
@@ -140,6 +160,14 @@ struct msfno_sht_plan_s {
   int* d_Lp = nullptr;
   int* d_off = nullptr;          // S-layout column offsets off[m]
   int table_loaded = 0;
+  // equatorial symmetry: the grid is symmetric (table[m][l][nlat-1-k] =
+  // (-1)^(l-m) table[m][l][k], checked at load).  Then the Legendre GEMMs run
+  // over the northern half + equator only, on Xs = X_k + X_{n-1-k} (even l-m,
+  // K = Ke) and Xa = X_k - X_{n-1-k} (odd, K = Ko): half the flops.  Slab rows
+  // hold [Xs (Ke) | pad | Xa (Ko) | pad] (Xs at column 0, Xa at column ldke).
+  int sym = 0;
+  int nh = 0, Ke = 0, Ko = 0, ldke = 0;
+  int* d_Lpe = nullptr;
   // Xt / Yt slab of each m (-1: m not in this plan's m-set); full plans: slab[m] = m
   std::vector<int> slab;
   int nslab = 0;
@@ -147,4 +175,5 @@ struct msfno_sht_plan_s {
   int desc_R = -1;
   msfno::GemmDesc* d_desc = nullptr;
   int ndesc = 0, desc_tiles = 0;
+  msfno::LatGeom geom() const { return {sym, nlat, nh, Ke, Ko, ldke, ldk}; }
 };

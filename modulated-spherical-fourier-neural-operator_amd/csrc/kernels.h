@@ -52,8 +52,9 @@ int launch_stats_partial(const float2* rowstats, int64_t np, int64_t cnt, int64_
 int launch_chan_affine_parts(const double* parts, int nparts, int B, int C, const float* w,
                              const float* b, float eps, const float* gamma, const float* beta,
                              float film_scale, float* scale, float* shift, hipStream_t s);
-// slabs (rows, ldk) <-> per-band blocks (rows, H_p) at offset rows*row0[p]
-int launch_band_copy(const float* src, float* dst, int64_t rows, int nlat, int ldk,
+// slabs (rows, g.ldk) <-> per-band blocks (rows, H_p) at offset rows*row0[p];
+// symmetric geometry folds / unfolds the hemispheres on the way
+int launch_band_copy(const float* src, float* dst, int64_t rows, const LatGeom& g,
                      const int* d_row0, int W, bool to_bands, hipStream_t s);
 // W' [b] = W·diag(scale[b]),  b'[b] = bias + W·shift[b]
 int launch_fold_affine(const float* W, const float* bias, const float* scale, const float* shift,
@@ -64,18 +65,26 @@ int launch_affine_rows(const float* x, const float* scale, const float* shift,
                        float2* stats, int stats_ld, hipStream_t s);
 // complex (Ci,Co,2) weight -> real (2Co x 2Ci) block matrix [[Wr^T,-Wi^T],[Wi^T,Wr^T]]
 int launch_expand_complex_weight(const float* w, float* Wexp, int Ci, int Co, hipStream_t s);
-// (mmax,lmax,nlat) reference table -> plan GEMM layout
+// (mmax,lmax,nlat) reference table -> plan GEMM layout (general or symmetric)
 int launch_relayout_table(const msfno_sht_plan_s& p, const float* table, hipStream_t s);
+// *d_flag |= 1 unless table[m][l][nlat-1-k] = (-1)^(l-m) table[m][l][k] (rel. 1e-5)
+int launch_check_symmetry(const float* table, int mmax, int lmax, int nlat, int* d_flag,
+                          hipStream_t s);
+// symmetric plans: transposes that fold / unfold the hemispheres (common.h LatGeom)
+int launch_transpose_fwd_sym(const float2* Xn, float* Xt, int B, int C, const LatGeom& g, int mmax,
+                             const float* nscale, const float* nshift, hipStream_t s);
+int launch_transpose_inv_sym(const float* Yt, float2* Yn, int B, int C, const LatGeom& g, int mmax,
+                             int mact, hipStream_t s);
 // S layout <-> reference (bc, lmax, mmax) complex dense
 int launch_spec_to_ref(const msfno_sht_plan_s& p, const float* S, float2* out, int B, int C,
                        const int* d_off, hipStream_t s);
 int launch_ref_to_spec(const msfno_sht_plan_s& p, const float2* in, float* S, int B, int C,
                        const int* d_off, hipStream_t s);
 // S layout <-> tril (B,C,T,2) (torch.tril_indices(lmax,mmax) order, layers.py:368)
-int launch_spec_to_tril(const SpecLayout& L, const float* S, float* xt, int B, int C,
-                        const int* d_off, hipStream_t s);
-int launch_tril_to_spec(const SpecLayout& L, const float* yt, float* S, int B, int C,
-                        const int* d_off, hipStream_t s);
+int launch_spec_to_tril(const msfno_sht_plan_s& p, const float* S, float* xt, int B, int C,
+                        hipStream_t s);
+int launch_tril_to_spec(const msfno_sht_plan_s& p, const float* yt, float* S, int B, int C,
+                        hipStream_t s);
 // compl_contract_fwd_c: a (B,Ci,T,2), w (Co,Ci,T,2) -> y (B,Co,T,2)
 int launch_compl_contract(const float* a, const float* w, float* y, int B, int Ci, int Co,
                           int64_t T, hipStream_t s);

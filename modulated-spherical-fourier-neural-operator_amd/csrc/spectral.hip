@@ -130,6 +130,109 @@ int launch_transpose_inv(const float* Yt, float2* Yn, int B, int C, int nlat, in
   return launch_check("transpose_inv");
 }
 
+// Equatorially symmetric plans (msfno_sht_plan_s::sym): the forward transpose
+// also folds the hemispheres, Xs_k = X_k + X_{n-1-k} (k < Ke; the centre row of
+// an odd grid once) into slab columns [0, Ke) and Xa_k = X_k - X_{n-1-k} (k < Ko)
+// into [ldke, ldke + Ko); the inverse one unfolds Y_k = E_k + O_k,
+// Y_{n-1-k} = E_k - O_k from the even/odd Legendre outputs.
+__global__ __launch_bounds__(256) void transpose_fwd_sym_kernel(
+    const float2* __restrict__ Xn, float* __restrict__ Xt, int B, int C, LatGeom g, int mmax,
+    const float* __restrict__ nscale, const float* __restrict__ nshift) {
+  __shared__ float2 tn[TMM][TK + 1], ts[TMM][TK + 1];
+  const int k0 = blockIdx.x * TK, m0 = blockIdx.y * TMM;
+  const int bc = blockIdx.z;
+  const int b = bc / C, c = bc - b * C;
+  const float2* src = Xn + (int64_t)bc * g.nlat * mmax;
+  for (int i = threadIdx.x; i < TK * TMM; i += 256) {
+    const int kk = i / TMM, mm = i - kk * TMM;
+    const int k = k0 + kk, m = m0 + mm;
+    float2 vn = make_float2(0.f, 0.f), vs = vn;
+    if (k < g.Ke && m < mmax) {
+      vn = src[(int64_t)k * mmax + m];
+      if (k < g.nh) vs = src[(int64_t)(g.nlat - 1 - k) * mmax + m];
+    }
+    tn[mm][kk] = vn;
+    ts[mm][kk] = vs;
+  }
+  __syncthreads();
+  const float sc = nscale ? nscale[bc] : 1.f;
+  const float sh = nshift ? nshift[bc] * kTwoPi : 0.f;
+  const int64_t R = 2LL * B * C;
+  const int64_t rre = (int64_t)(b * 2 + 0) * C + c;
+  const int64_t rim = (int64_t)(b * 2 + 1) * C + c;
+  for (int i = threadIdx.x; i < TK * TMM; i += 256) {
+    const int mm = i / TK, kk = i - mm * TK;
+    const int k = k0 + kk, m = m0 + mm;
+    if (k >= g.Ke || m >= mmax) continue;
+    const float2 n = tn[mm][kk], q = ts[mm][kk];
+    const float shm = (m == 0) ? sh : 0.f;
+    float* dst = Xt + (int64_t)m * R * g.ldk;
+    const bool pair = k < g.nh;
+    // affine per row, then fold: s(N + S) + 2t  /  s(N - S)
+    dst[rre * g.ldk + k] = pair ? fmaf(sc, n.x + q.x, 2.f * shm) : fmaf(sc, n.x, shm);
+    dst[rim * g.ldk + k] = pair ? sc * (n.y + q.y) : sc * n.y;
+    if (pair) {
+      dst[rre * g.ldk + g.ldke + k] = sc * (n.x - q.x);
+      dst[rim * g.ldk + g.ldke + k] = sc * (n.y - q.y);
+    }
+  }
+}
+
+int launch_transpose_fwd_sym(const float2* Xn, float* Xt, int B, int C, const LatGeom& g, int mmax,
+                             const float* nscale, const float* nshift, hipStream_t s) {
+  dim3 grid((unsigned)cdiv(g.Ke, TK), (unsigned)cdiv(mmax, TMM), (unsigned)(B * C));
+  hipLaunchKernelGGL(transpose_fwd_sym_kernel, grid, dim3(256), 0, s, Xn, Xt, B, C, g, mmax,
+                     nscale, nshift);
+  return launch_check("transpose_fwd_sym");
+}
+
+__global__ __launch_bounds__(256) void transpose_inv_sym_kernel(const float* __restrict__ Yt,
+                                                                float2* __restrict__ Yn, int B,
+                                                                int C, LatGeom g, int mmax,
+                                                                int mact) {
+  __shared__ float2 tn[TMM][TK + 1], ts[TMM][TK + 1];
+  const int k0 = blockIdx.x * TK, m0 = blockIdx.y * TMM;
+  const int bc = blockIdx.z;
+  const int b = bc / C, c = bc - b * C;
+  const int64_t R = 2LL * B * C;
+  const int64_t rre = (int64_t)(b * 2 + 0) * C + c;
+  const int64_t rim = (int64_t)(b * 2 + 1) * C + c;
+  for (int i = threadIdx.x; i < TK * TMM; i += 256) {
+    const int mm = i / TK, kk = i - mm * TK;
+    const int k = k0 + kk, m = m0 + mm;
+    float2 n = make_float2(0.f, 0.f), q = n;
+    if (k < g.Ke && m < mact) {
+      const float* src = Yt + (int64_t)m * R * g.ldk;
+      const float2 e = make_float2(src[rre * g.ldk + k], src[rim * g.ldk + k]);
+      if (k < g.nh) {
+        const float2 o = make_float2(src[rre * g.ldk + g.ldke + k], src[rim * g.ldk + g.ldke + k]);
+        n = make_float2(e.x + o.x, e.y + o.y);
+        q = make_float2(e.x - o.x, e.y - o.y);
+      } else {
+        n = e;
+      }
+    }
+    tn[mm][kk] = n;
+    ts[mm][kk] = q;
+  }
+  __syncthreads();
+  float2* dst = Yn + (int64_t)bc * g.nlat * mmax;
+  for (int i = threadIdx.x; i < TK * TMM; i += 256) {
+    const int kk = i / TMM, mm = i - kk * TMM;
+    const int k = k0 + kk, m = m0 + mm;
+    if (k >= g.Ke || m >= mmax) continue;
+    dst[(int64_t)k * mmax + m] = tn[mm][kk];
+    if (k < g.nh) dst[(int64_t)(g.nlat - 1 - k) * mmax + m] = ts[mm][kk];
+  }
+}
+
+int launch_transpose_inv_sym(const float* Yt, float2* Yn, int B, int C, const LatGeom& g, int mmax,
+                             int mact, hipStream_t s) {
+  dim3 grid((unsigned)cdiv(g.Ke, TK), (unsigned)cdiv(mmax, TMM), (unsigned)(B * C));
+  hipLaunchKernelGGL(transpose_inv_sym_kernel, grid, dim3(256), 0, s, Yt, Yn, B, C, g, mmax, mact);
+  return launch_check("transpose_inv_sym");
+}
+
 // ---------------------------------------------------------------------------
 // statistics: combine (mean, M2) partials per channel, fp64 (Chan et al.)
 // ---------------------------------------------------------------------------
@@ -286,47 +389,77 @@ int launch_chan_affine_parts(const double* parts, int nparts, int B, int C, cons
 
 // Full-latitude slabs F (rows, ldk) [row = mi*R + r]  <->  band buffer Q laid out
 // per band p as (rows, H_p) at offset rows * row0[p]   (the all-to-all block of p).
-// One wave per row; TO_BANDS: F -> Q (pack), else Q -> F (unpack, pads k >= nlat).
+// One wave per row.  TO_BANDS: F -> Q (pack), else Q -> F (unpack, zero pads).
+// Symmetric geometry: F rows are [Xs | Xa] (unpack folds the hemispheres) and
+// [E | O] (pack unfolds them), as transpose_fwd_sym / transpose_inv_sym.
+__device__ __forceinline__ int64_t band_pos(const int* r0, int W, int64_t rows, int64_t row,
+                                           int k) {
+  int lo = 0, hi = W - 1;  // band with r0[p] <= k < r0[p+1]
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (r0[mid] <= k) lo = mid; else hi = mid - 1;
+  }
+  return rows * r0[lo] + row * (r0[lo + 1] - r0[lo]) + (k - r0[lo]);
+}
+
 template <bool TO_BANDS>
 __global__ __launch_bounds__(256) void band_copy_kernel(const float* __restrict__ src,
                                                         float* __restrict__ dst, int64_t rows,
-                                                        int nlat, int ldk,
-                                                        const int* __restrict__ row0, int W) {
+                                                        LatGeom g, const int* __restrict__ row0,
+                                                        int W) {
   __shared__ int r0[65];
   for (int i = threadIdx.x; i <= W; i += 256) r0[i] = row0[i];
   __syncthreads();
   const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= rows) return;
   const int lane = threadIdx.x & 63;
-  int p = 0;
-  for (int k = lane; k < (TO_BANDS ? nlat : ldk); k += 64) {
-    if (k >= nlat) {  // unpack only: zero the latitude padding
-      dst[row * ldk + k] = 0.f;
-      continue;
+  const float* F = TO_BANDS ? src + row * g.ldk : nullptr;
+  if (TO_BANDS) {
+    for (int k = lane; k < g.nlat; k += 64) {
+      float v;
+      if (!g.sym) {
+        v = F[k];
+      } else if (k < g.nh) {
+        v = F[k] + F[g.ldke + k];
+      } else if (k >= g.nlat - g.nh) {
+        const int kn = g.nlat - 1 - k;
+        v = F[kn] - F[g.ldke + kn];
+      } else {
+        v = F[k];  // equator row of an odd grid
+      }
+      dst[band_pos(r0, W, rows, row, k)] = v;
     }
-    while (k >= r0[p + 1]) ++p;
-    const int hp = r0[p + 1] - r0[p];
-    const int64_t q = rows * r0[p] + row * hp + (k - r0[p]);
-    if (TO_BANDS)
-      dst[q] = src[row * ldk + k];
-    else
-      dst[row * ldk + k] = src[q];
+  } else {
+    float* D = dst + row * g.ldk;
+    for (int c = lane; c < g.ldk; c += 64) {
+      float v = 0.f;
+      if (!g.sym) {
+        if (c < g.nlat) v = src[band_pos(r0, W, rows, row, c)];
+      } else if (c < g.Ke) {
+        v = src[band_pos(r0, W, rows, row, c)];
+        if (c < g.nh) v += src[band_pos(r0, W, rows, row, g.nlat - 1 - c)];
+      } else if (c >= g.ldke && c < g.ldke + g.Ko) {
+        const int k = c - g.ldke;
+        v = src[band_pos(r0, W, rows, row, k)] - src[band_pos(r0, W, rows, row, g.nlat - 1 - k)];
+      }
+      D[c] = v;
+    }
   }
 }
 
-int launch_band_copy(const float* src, float* dst, int64_t rows, int nlat, int ldk,
+int launch_band_copy(const float* src, float* dst, int64_t rows, const LatGeom& g,
                      const int* d_row0, int W, bool to_bands, hipStream_t s) {
   if (W > 64) {
     set_error("latitude-band sharding supports at most 64 ranks");
     return MSFNO_EUNSUPPORTED;
   }
+  if (rows == 0) return MSFNO_OK;
   const dim3 grid((unsigned)cdiv(rows, 4));
   if (to_bands)
-    hipLaunchKernelGGL(band_copy_kernel<true>, grid, dim3(256), 0, s, src, dst, rows, nlat, ldk,
-                       d_row0, W);
+    hipLaunchKernelGGL(band_copy_kernel<true>, grid, dim3(256), 0, s, src, dst, rows, g, d_row0, W);
   else
-    hipLaunchKernelGGL(band_copy_kernel<false>, grid, dim3(256), 0, s, src, dst, rows, nlat, ldk,
-                       d_row0, W);
+    hipLaunchKernelGGL(band_copy_kernel<false>, grid, dim3(256), 0, s, src, dst, rows, g, d_row0,
+                       W);
   return launch_check("band_copy");
 }
 
@@ -450,25 +583,59 @@ int launch_expand_complex_weight(const float* w, float* Wexp, int Ci, int Co, hi
 
 // forward table:  Wf[m][k][j] = weights[m][m+j][k]   (ld Lp_m, zero pad j >= L_m)
 // inverse table:  Pi[m][j][k] = pct[m][m+j][k]       (ld ldk,  zero pad k >= nlat)
+// (mmax, lmax, nlat) reference table -> per-m plan GEMM blocks (common.h:
+// set_table_offsets); columns / rows in the parity-split S order, pads zero.
 __global__ void relayout_table_kernel(const float* __restrict__ tab, float* __restrict__ out,
                                       const int64_t* __restrict__ tab_off,
-                                      const int* __restrict__ Lp, int lmax, int nlat, int ldk,
-                                      int inverse) {
+                                      const int* __restrict__ Lp, const int* __restrict__ Lpe,
+                                      int lmax, LatGeom g, int inverse) {
   const int m = blockIdx.y;
   const int L = lmax - m;
-  const int lp = Lp[m];
+  const int lp = Lp[m], lpe = Lpe[m], lpo = lp - lpe;
   if (L <= 0 || lp == 0) return;  // lp == 0: m outside a sharded plan's m-set
   float* o = out + tab_off[m];
-  const int64_t n = inverse ? (int64_t)L * ldk : (int64_t)nlat * lp;
+  const float* t = tab + (int64_t)m * lmax * g.nlat;
+  // value of row j (= l - m) at latitude k, 0 outside the triangle
+  auto at = [&](int j, int k) -> float {
+    return (j < L) ? t[(int64_t)(m + j) * g.nlat + k] : 0.f;
+  };
+  auto jcol = [&](int c) { return c < lpe ? 2 * c : 2 * (c - lpe) + 1; };
+  const int ldko = (g.Ko + 3) & ~3;
+  int64_t n;
+  if (!g.sym) n = inverse ? (int64_t)lp * g.ldk : (int64_t)g.nlat * lp;
+  else n = inverse ? (int64_t)lpe * g.ldke + (int64_t)lpo * ldko
+                   : (int64_t)g.Ke * lpe + (int64_t)g.Ko * lpo;
   for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < n;
        e += (int64_t)gridDim.x * blockDim.x) {
     float v = 0.f;
-    if (inverse) {
-      const int j = (int)(e / ldk), k = (int)(e - (int64_t)j * ldk);
-      if (k < nlat) v = tab[((int64_t)m * lmax + (m + j)) * nlat + k];
+    if (!g.sym) {
+      if (inverse) {  // (lp x ldk)
+        const int c = (int)(e / g.ldk), k = (int)(e - (int64_t)c * g.ldk);
+        if (k < g.nlat) v = at(jcol(c), k);
+      } else {        // (nlat x lp)
+        const int k = (int)(e / lp), c = (int)(e - (int64_t)k * lp);
+        v = at(jcol(c), k);
+      }
+    } else if (inverse) {
+      const int64_t ne = (int64_t)lpe * g.ldke;
+      if (e < ne) {   // Pe (lpe x ldke)
+        const int c = (int)(e / g.ldke), k = (int)(e - (int64_t)c * g.ldke);
+        if (k < g.Ke) v = at(2 * c, k);
+      } else {        // Po (lpo x ldko)
+        const int64_t f = e - ne;
+        const int c = (int)(f / ldko), k = (int)(f - (int64_t)c * ldko);
+        if (k < g.Ko) v = at(2 * c + 1, k);
+      }
     } else {
-      const int k = (int)(e / lp), j = (int)(e - (int64_t)k * lp);
-      if (j < L) v = tab[((int64_t)m * lmax + (m + j)) * nlat + k];
+      const int64_t ne = (int64_t)g.Ke * lpe;
+      if (e < ne) {   // We (Ke x lpe)
+        const int k = (int)(e / lpe), c = (int)(e - (int64_t)k * lpe);
+        v = at(2 * c, k);
+      } else {        // Wo (Ko x lpo)
+        const int64_t f = e - ne;
+        const int k = (int)(f / lpo), c = (int)(f - (int64_t)k * lpo);
+        v = at(2 * c + 1, k);
+      }
     }
     o[e] = v;
   }
@@ -477,8 +644,39 @@ __global__ void relayout_table_kernel(const float* __restrict__ tab, float* __re
 int launch_relayout_table(const msfno_sht_plan_s& p, const float* table, hipStream_t s) {
   dim3 grid(256, (unsigned)p.mmax);
   hipLaunchKernelGGL(relayout_table_kernel, grid, dim3(256), 0, s, table, p.table, p.d_tab_off,
-                     p.d_Lp, p.lmax, p.nlat, p.ldk, p.inverse);
+                     p.d_Lp, p.d_Lpe, p.lmax, p.geom(), p.inverse);
   return launch_check("relayout_table");
+}
+
+// flag |= 1 when some row (m, l) of the table breaks
+// t[nlat-1-k] = (-1)^(l-m) t[k] beyond 1e-5 of the row's max magnitude
+__global__ __launch_bounds__(256) void check_symmetry_kernel(const float* __restrict__ tab,
+                                                             int lmax, int nlat,
+                                                             int* __restrict__ flag) {
+  __shared__ float red[256];
+  const int m = blockIdx.y, l = blockIdx.x;
+  const float* t = tab + ((int64_t)m * lmax + l) * nlat;
+  float mx = 0.f;
+  for (int k = threadIdx.x; k < nlat; k += 256) mx = fmaxf(mx, fabsf(t[k]));
+  red[threadIdx.x] = mx;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) red[threadIdx.x] = fmaxf(red[threadIdx.x], red[threadIdx.x + o]);
+    __syncthreads();
+  }
+  const float tol = 1e-5f * red[0];
+  const float sgn = ((l - m) & 1) ? -1.f : 1.f;
+  bool bad = false;
+  for (int k = threadIdx.x; k < nlat / 2; k += 256)
+    bad |= !(fabsf(t[nlat - 1 - k] - sgn * t[k]) <= tol);  // NaN-safe
+  if (bad) atomicOr(flag, 1);
+}
+
+int launch_check_symmetry(const float* table, int mmax, int lmax, int nlat, int* d_flag,
+                          hipStream_t s) {
+  hipLaunchKernelGGL(check_symmetry_kernel, dim3((unsigned)lmax, (unsigned)mmax), dim3(256), 0, s,
+                     table, lmax, nlat, d_flag);
+  return launch_check("check_symmetry");
 }
 
 // ---------------------------------------------------------------------------
@@ -493,10 +691,20 @@ __device__ __forceinline__ int find_m(const int* off, int mact, int64_t t) {
   return lo;
 }
 
+// column t of an S row -> (m, j = l - m); j < 0 for padding
+__device__ __forceinline__ void spec_col_inv(const int* off, const int* Lpe, const int* Lp,
+                                             int mact, int64_t t, int lmax, int& m, int& j) {
+  m = find_m(off, mact, t);
+  const int u = (int)(t - off[m]);
+  const int lpe = Lpe[m];
+  j = u < lpe ? 2 * u : 2 * (u - lpe) + 1;
+  if (u >= Lp[m] || m + j >= lmax) j = -1;
+}
+
 // out (bc, lmax, mmax) complex dense (zeros where l < m)
 __global__ void spec_to_ref_kernel(const float* __restrict__ S, float2* __restrict__ out, int B,
                                    int C, int lmax, int mmax, int mact, int64_t ldT,
-                                   const int* __restrict__ off) {
+                                   const int* __restrict__ off, const int* __restrict__ Lpe) {
   const int64_t n = (int64_t)B * C * lmax * mmax;
   for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < n;
        e += (int64_t)gridDim.x * blockDim.x) {
@@ -506,7 +714,7 @@ __global__ void spec_to_ref_kernel(const float* __restrict__ S, float2* __restri
     const int b = (int)(bc / C), c = (int)(bc % C);
     float2 v = make_float2(0.f, 0.f);
     if (l >= m && m < mact) {
-      const int64_t t = off[m] + (l - m);
+      const int64_t t = spec_col(off, Lpe, m, l);
       v.x = S[((int64_t)(b * 2 + 0) * C + c) * ldT + t];
       v.y = S[((int64_t)(b * 2 + 1) * C + c) * ldT + t];
     }
@@ -519,23 +727,24 @@ int launch_spec_to_ref(const msfno_sht_plan_s& p, const float* S, float2* out, i
   const int64_t n = (int64_t)B * C * p.lmax * p.mmax;
   hipLaunchKernelGGL(spec_to_ref_kernel, dim3((unsigned)std::min<int64_t>(cdiv(n, 256), 65535)),
                      dim3(256), 0, s, S, out, B, C, p.lmax, p.mmax, p.spec.mact, p.spec.ldT,
-                     d_off);
+                     d_off, p.d_Lpe);
   return launch_check("spec_to_ref");
 }
 
 __global__ void ref_to_spec_kernel(const float2* __restrict__ in, float* __restrict__ S, int B,
                                    int C, int lmax, int mmax, int mact, int64_t Tp, int64_t ldT,
-                                   const int* __restrict__ off) {
+                                   const int* __restrict__ off, const int* __restrict__ Lpe,
+                                   const int* __restrict__ Lp) {
   const int64_t n = (int64_t)B * C * Tp;
   for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < n;
        e += (int64_t)gridDim.x * blockDim.x) {
     const int64_t t = e % Tp;
     const int64_t bc = e / Tp;
     const int b = (int)(bc / C), c = (int)(bc % C);
-    const int m = find_m(off, mact, t);
-    const int l = m + (int)(t - off[m]);
+    int m, j;
+    spec_col_inv(off, Lpe, Lp, mact, t, lmax, m, j);
     float2 v = make_float2(0.f, 0.f);
-    if (l < lmax) v = in[(bc * lmax + l) * mmax + m];
+    if (j >= 0) v = in[(bc * lmax + m + j) * mmax + m];
     S[((int64_t)(b * 2 + 0) * C + c) * ldT + t] = v.x;
     S[((int64_t)(b * 2 + 1) * C + c) * ldT + t] = v.y;
   }
@@ -546,7 +755,7 @@ int launch_ref_to_spec(const msfno_sht_plan_s& p, const float2* in, float* S, in
   const int64_t n = (int64_t)B * C * p.spec.Tp;
   hipLaunchKernelGGL(ref_to_spec_kernel, dim3((unsigned)std::min<int64_t>(cdiv(n, 256), 65535)),
                      dim3(256), 0, s, in, S, B, C, p.lmax, p.mmax, p.spec.mact, p.spec.Tp,
-                     p.spec.ldT, d_off);
+                     p.spec.ldT, d_off, p.d_Lpe, p.d_Lp);
   return launch_check("ref_to_spec");
 }
 
@@ -559,17 +768,18 @@ __device__ __forceinline__ int64_t tril_row_off(int l, int mmax) {
 // S -> xt (B, C, T, 2);  one thread per (bc, t) of the S row (coalesced reads)
 __global__ void spec_to_tril_kernel(const float* __restrict__ S, float* __restrict__ xt, int B,
                                     int C, int lmax, int mmax, int mact, int64_t Tp, int64_t T,
-                                    int64_t ldT, const int* __restrict__ off) {
+                                    int64_t ldT, const int* __restrict__ off,
+                                    const int* __restrict__ Lpe, const int* __restrict__ Lp) {
   const int64_t n = (int64_t)B * C * Tp;
   for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < n;
        e += (int64_t)gridDim.x * blockDim.x) {
     const int64_t t = e % Tp;
     const int64_t bc = e / Tp;
     const int b = (int)(bc / C), c = (int)(bc % C);
-    const int m = find_m(off, mact, t);
-    const int l = m + (int)(t - off[m]);
-    if (l >= lmax) continue;
-    const int64_t nn = tril_row_off(l, mmax) + m;
+    int m, j;
+    spec_col_inv(off, Lpe, Lp, mact, t, lmax, m, j);
+    if (j < 0) continue;
+    const int64_t nn = tril_row_off(m + j, mmax) + m;
     const float re = S[((int64_t)(b * 2 + 0) * C + c) * ldT + t];
     const float im = S[((int64_t)(b * 2 + 1) * C + c) * ldT + t];
     reinterpret_cast<float2*>(xt)[bc * T + nn] = make_float2(re, im);
@@ -578,37 +788,40 @@ __global__ void spec_to_tril_kernel(const float* __restrict__ S, float* __restri
 
 __global__ void tril_to_spec_kernel(const float* __restrict__ yt, float* __restrict__ S, int B,
                                     int C, int lmax, int mmax, int mact, int64_t Tp, int64_t T,
-                                    int64_t ldT, const int* __restrict__ off) {
+                                    int64_t ldT, const int* __restrict__ off,
+                                    const int* __restrict__ Lpe, const int* __restrict__ Lp) {
   const int64_t n = (int64_t)B * C * Tp;
   for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < n;
        e += (int64_t)gridDim.x * blockDim.x) {
     const int64_t t = e % Tp;
     const int64_t bc = e / Tp;
     const int b = (int)(bc / C), c = (int)(bc % C);
-    const int m = find_m(off, mact, t);
-    const int l = m + (int)(t - off[m]);
+    int m, j;
+    spec_col_inv(off, Lpe, Lp, mact, t, lmax, m, j);
     float2 v = make_float2(0.f, 0.f);
-    if (l < lmax) v = reinterpret_cast<const float2*>(yt)[bc * T + tril_row_off(l, mmax) + m];
+    if (j >= 0) v = reinterpret_cast<const float2*>(yt)[bc * T + tril_row_off(m + j, mmax) + m];
     S[((int64_t)(b * 2 + 0) * C + c) * ldT + t] = v.x;
     S[((int64_t)(b * 2 + 1) * C + c) * ldT + t] = v.y;
   }
 }
 
-int launch_spec_to_tril(const SpecLayout& L, const float* S, float* xt, int B, int C,
-                        const int* d_off, hipStream_t s) {
+int launch_spec_to_tril(const msfno_sht_plan_s& p, const float* S, float* xt, int B, int C,
+                        hipStream_t s) {
+  const SpecLayout& L = p.spec;
   const int64_t n = (int64_t)B * C * L.Tp;
   hipLaunchKernelGGL(spec_to_tril_kernel, dim3((unsigned)std::min<int64_t>(cdiv(n, 256), 65535)),
                      dim3(256), 0, s, S, xt, B, C, L.lmax, L.mmax, L.mact, L.Tp, L.T, L.ldT,
-                     d_off);
+                     p.d_off, p.d_Lpe, p.d_Lp);
   return launch_check("spec_to_tril");
 }
 
-int launch_tril_to_spec(const SpecLayout& L, const float* yt, float* S, int B, int C,
-                        const int* d_off, hipStream_t s) {
+int launch_tril_to_spec(const msfno_sht_plan_s& p, const float* yt, float* S, int B, int C,
+                        hipStream_t s) {
+  const SpecLayout& L = p.spec;
   const int64_t n = (int64_t)B * C * L.Tp;
   hipLaunchKernelGGL(tril_to_spec_kernel, dim3((unsigned)std::min<int64_t>(cdiv(n, 256), 65535)),
                      dim3(256), 0, s, yt, S, B, C, L.lmax, L.mmax, L.mact, L.Tp, L.T, L.ldT,
-                     d_off);
+                     p.d_off, p.d_Lpe, p.d_Lp);
   return launch_check("tril_to_spec");
 }
 

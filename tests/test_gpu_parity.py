@@ -75,6 +75,47 @@ def test_sht_round_trip_full_resolution():
     assert (back - a).abs().max().item() < 2e-4 * a.abs().max().item()
 
 
+@pytest.mark.parametrize("grid,nlat,nlon,lmax,mmax", SHT_CASES[:5])
+def test_sht_general_layout_matches_oracle(grid, nlat, nlon, lmax, mmax, monkeypatch):
+    """MSFNO_NO_SYM=1 forces the general (non-folded) Legendre layout that
+    non-symmetric tables use; it must agree with the oracle as well."""
+    from msfno_amd.harmonics import InverseRealSHT, RealSHT
+    monkeypatch.setenv("MSFNO_NO_SYM", "1")
+    g = torch.Generator().manual_seed(11 + nlat)
+    x = torch.randn(2, 3, nlat, nlon, generator=g)
+    want = S.RealSHT(nlat, nlon, lmax=lmax, mmax=mmax, grid=grid)(x.double())
+    got = RealSHT(nlat, nlon, lmax=lmax, mmax=mmax, grid=grid).float().to(DEV)(x.to(DEV)).cpu()
+    assert _rel(got.to(torch.complex128), want) < 2e-6
+    a = torch.view_as_complex(torch.randn(2, 3, lmax, mmax, 2, generator=g))
+    want = S.InverseRealSHT(nlat, nlon, lmax=lmax, mmax=mmax, grid=grid)(a.to(torch.complex128))
+    got = InverseRealSHT(nlat, nlon, lmax=lmax, mmax=mmax, grid=grid).float().to(DEV)(a.to(DEV)).cpu()
+    assert _rel(got.double(), want) < 2e-6
+
+
+def test_asymmetric_table_uses_general_layout():
+    """A table without the equatorial symmetry (here: one latitude perturbed)
+    must not be folded: the transform follows the table exactly."""
+    from msfno_amd.harmonics import InverseRealSHT, RealSHT
+    nlat, nlon, lmax, mmax = 33, 64, 16, 17
+    f = RealSHT(nlat, nlon, lmax=lmax, mmax=mmax, grid="equiangular").float()
+    f.weights = f.weights.clone()
+    f.weights[:, :, 3] *= 1.5
+    gi = InverseRealSHT(nlat, nlon, lmax=lmax, mmax=mmax, grid="equiangular").float()
+    gi.pct = gi.pct.clone()
+    gi.pct[:, :, 30] *= 0.5
+    g = torch.Generator().manual_seed(5)
+    x = torch.randn(2, nlat, nlon, generator=g, dtype=torch.float64)
+    X = 2.0 * torch.pi * torch.fft.rfft(x, norm="forward")[..., :mmax]
+    want = torch.einsum("...km,mlk->...lm", X, f.weights.double().to(torch.complex128))
+    got = f.to(DEV)(x.float().to(DEV)).cpu()
+    assert _rel(got.to(torch.complex128), want) < 2e-6
+    a = torch.view_as_complex(torch.randn(2, lmax, mmax, 2, generator=g, dtype=torch.float64))
+    Y = torch.einsum("...lm,mlk->...km", a, gi.pct.double().to(torch.complex128))
+    want = torch.fft.irfft(Y, n=nlon, norm="forward")
+    got = gi.to(DEV)(a.to(torch.complex64).to(DEV)).cpu()
+    assert _rel(got.double(), want) < 2e-6
+
+
 def test_compl_contract_matches_einsum():
     from msfno_amd.sfno import compl_contract_fwd_c
     for (B, Ci, Co, T) in [(1, 8, 8, 528), (2, 16, 12, 1035), (3, 4, 20, 7), (8, 8, 8, 100)]:

@@ -1,8 +1,9 @@
 // Microbenchmark of the fp32 MFMA GEMM variants on the block's shapes.
-// Build: hipcc -O3 --offload-arch=gfx950 -std=c++17 tools/gemm_bench.hip -o tools/gemm_bench
+// Build: hipcc -O3 --offload-arch=gfx950 -std=c++17 tools/gemm_bench.hip -lrocblas -o tools/bin/gemm_bench
 #include <chrono>
 #include <cstdio>
 #include <vector>
+#include <rocblas/rocblas.h>
 
 #include "../modulated-spherical-fourier-neural-operator_amd/csrc/gemm.hip"
 
@@ -65,13 +66,38 @@ int main() {
   const int T = 65536;
   struct S { const char* n; int M, N, K; GemmEpi e; };
   std::vector<S> shapes = {
-      {"fc2", 256, P, 512, plain}, {"fc2-badd", 256, P, 512, fc2e},
-      {"fc2-geluB", 256, P, 512, geluB}, {"fc2-full", 256, P, 512, fc2g}};
+      {"fc2", 256, P, 512, plain}, {"fc2-geluB", 256, P, 512, geluB}, {"fc1", 512, P, 256, plain}, {"fc1-gelu", 512, P, 256, gelu},
+      {"fc2-full", 256, P, 512, fc2g}};
   for (auto& s : shapes) {
     const double fl = 2.0 * s.M * (double)s.N * s.K;
     run<128, 128, 16>(s.n, s.M, s.N, s.K, A, B, C, s.e, 5, fl);
     run<128, 64, 16>(s.n, s.M, s.N, s.K, A, B, C, s.e, 5, fl);
     run<256, 64, 16>(s.n, s.M, s.N, s.K, A, B, C, s.e, 5, fl);
+    // run<256, 64, 32>(s.n, s.M, s.N, s.K, A, B, C, s.e, 5, fl);
+  }
+  // rocBLAS sgemm on the same row-major problem: C^T = B^T A^T (column-major)
+  rocblas_handle rh;
+  rocblas_create_handle(&rh);
+  const float one = 1.f, zero = 0.f;
+  struct G { int M, N, K; };
+  for (G g : {G{256, P, 512}, G{512, P, 256}, G{256, P, 256}, G{1024, 65536, 1024}}) {
+    for (int i = 0; i < 2; ++i)
+      rocblas_sgemm(rh, rocblas_operation_none, rocblas_operation_none, g.N, g.M, g.K, &one, B, g.N,
+                    A, g.K, &zero, C, g.N);
+    hipEvent_t a, b;
+    hipEventCreate(&a);
+    hipEventCreate(&b);
+    hipEventRecord(a, 0);
+    for (int i = 0; i < 5; ++i)
+      rocblas_sgemm(rh, rocblas_operation_none, rocblas_operation_none, g.N, g.M, g.K, &one, B, g.N,
+                    A, g.K, &zero, C, g.N);
+    hipEventRecord(b, 0);
+    hipEventSynchronize(b);
+    float ms = 0;
+    hipEventElapsedTime(&ms, a, b);
+    ms /= 5;
+    printf("rocblas M=%d N=%d K=%d: %.3f ms %.1f TF/s\n", g.M, g.N, g.K, ms,
+           2.0 * g.M * (double)g.N * g.K / ms / 1e9);
   }
   return 0;
 }
