@@ -279,7 +279,7 @@ int ensure_desc(msfno_sht_plan_s* p, int R, int other_ld, int64_t ldT) {
       o.N = p->Ko; o.K = lo; o.lda = (int)ldT; o.ldb = ldko; o.ldc = p->ldk;
       o.offA = L.off[m] + lpe; o.offB = p->tab_off[m] + (int64_t)lpe * p->ldke;
       o.offC = slab + p->ldke;
-      if (lo > 0) push(o);
+      push(o);  // also for lo == 0 (K = 0 writes zeros): transpose_inv_sym reads O
     }
   }
   (void)other_ld;
