@@ -223,7 +223,7 @@ int ensure_desc(msfno_sht_plan_s* p, int R, int other_ld, int64_t ldT) {
   // symmetric plans: one even-parity and one odd-parity problem per m
   if (p->desc_R == R && p->d_desc) return MSFNO_OK;
   int bm, bn;
-  gemm_tile_dims(TILE_128x64, &bm, &bn);
+  gemm_tile_dims(role_tile(ROLE_LEG, TILE_128x64), &bm, &bn);
   std::vector<GemmDesc> d;
   int tiles = 0;
   const SpecLayout& L = p->spec;
@@ -326,13 +326,15 @@ int legendre_fwd(msfno_sht_plan_s* f, const float* Xt, float* S, int R, hipStrea
   GemmEpi e;
   e.rowscale = rowscale;
   e.rs_C = C;
-  return gemm_desc(TILE_128x64, Xt, f->table, S, f->d_desc, f->ndesc, f->desc_tiles, e, s);
+  return gemm_desc(role_tile(ROLE_LEG, TILE_128x64), Xt, f->table, S, f->d_desc, f->ndesc,
+                   f->desc_tiles, e, s);
 }
 
 int legendre_inv(msfno_sht_plan_s* g, const float* S, float* Yt, int R, hipStream_t s) {
   MSFNO_TRY(ensure_desc(g, R, 0, g->spec.ldT));
   GemmEpi e;
-  return gemm_desc(TILE_128x64, S, g->table, Yt, g->d_desc, g->ndesc, g->desc_tiles, e, s);
+  return gemm_desc(role_tile(ROLE_LEG, TILE_128x64), S, g->table, Yt, g->d_desc, g->ndesc,
+                   g->desc_tiles, e, s);
 }
 
 // ---------------------------------------------------------------------------
@@ -431,7 +433,7 @@ int run_filter(const msfno_block_desc* d, msfno_sht_plan_s* f, msfno_sht_plan_s*
         e.relu_period = 2 * co;
         e.relu_rows = co;
       }
-      MSFNO_TRY(gemm_uniform(TILE_128x128, b.Wexp[l], in, out, 2 * co, (int)L.Tp, 2 * ci, 2 * ci,
+      MSFNO_TRY(gemm_uniform(role_tile(ROLE_SPEC, TILE_256x128), b.Wexp[l], in, out, 2 * co, (int)L.Tp, 2 * ci, 2 * ci,
                              (int)L.ldT, (int)L.ldT, 0, 2LL * ci * L.ldT, 2LL * co * L.ldT, B, e,
                              s));
       in = out;
@@ -580,13 +582,13 @@ int run_mlp(const msfno_block_desc* d, const float* W1f, const float* b1f, const
   e1.bias = b1f;
   e1.sBias = Hd;
   e1.act = 1;
-  MSFNO_TRY(gemm_uniform(TILE_128x64, W1f, x1, h, (int)Hd, (int)P, (int)C, (int)C, (int)P,
+  MSFNO_TRY(gemm_uniform(role_tile(ROLE_FC1, TILE_128x64), W1f, x1, h, (int)Hd, (int)P, (int)C, (int)C, (int)P,
                          (int)P, Hd * C, C * P, Hd * P, B, e1, s));
   prof(ST_FC2, s);
   GemmEpi e2;
   e2.bias = d->fc2_b;
   if (resid) { e2.addend = resid; e2.sD = C * P; e2.ldd = (int)P; }
-  return gemm_uniform(TILE_128x128, d->fc2_w, h, out, (int)C, (int)P, (int)Hd, (int)Hd, (int)P,
+  return gemm_uniform(role_tile(ROLE_FC2, TILE_128x128), d->fc2_w, h, out, (int)C, (int)P, (int)Hd, (int)Hd, (int)P,
                       (int)P, 0, Hd * P, C * P, B, e2, s);
 }
 }  // namespace msfno
@@ -796,7 +798,7 @@ int msfno_block_forward(const msfno_block_desc* d, msfno_sht_plan_t f, msfno_sht
     prof(ST_SKIP, ss);
     GemmEpi e;
     e.bias = d->skip_b;
-    MSFNO_TRY(gemm_uniform(TILE_128x128, d->skip_w, x, x1, (int)C, (int)P, (int)C, (int)C,
+    MSFNO_TRY(gemm_uniform(role_tile(ROLE_SKIP, TILE_128x128), d->skip_w, x, x1, (int)C, (int)P, (int)C, (int)C,
                            (int)P, (int)P, 0, C * P, C * P, B, e, ss));
     if (side) {
       prof(ST_END, ss);

@@ -124,17 +124,22 @@ struct GemmDesc {
 struct GemmEpi {
   const float* bias = nullptr;      // per row (batch stride sBias)
   const float* addend = nullptr;    // matrix, ld = ldd (batch stride sD)
-  float2* stats = nullptr;          // per (row, tile_n) partial (mean, M2) (batch stride sStats)
-  int64_t sBias = 0, sD = 0, sStats = 0;
+  int64_t sBias = 0, sD = 0;
   int ldd = 0;
   int act = 0;                      // 0 none, 1 GELU(erf) on C, 2 GELU(erf) on B while staged
   int relu_period = 0, relu_rows = 0;  // ReLU rows where (row % period) < relu_rows
-  int stats_ld = 0;                 // partials per row
   const float* rowscale = nullptr;  // per-(b,c) factor for rows r=(b,ri,c); C = rs_C
   int rs_C = 0;
 };
 
-enum GemmTile { TILE_128x128 = 0, TILE_128x64 = 1, TILE_64x64 = 2, TILE_256x64 = 3 };
+enum GemmTile {
+  TILE_128x128 = 0, TILE_128x64 = 1, TILE_64x64 = 2, TILE_256x64 = 3, TILE_256x128 = 4,
+  TILE_128x256 = 5
+};
+// GEMM role -> tile (defaults chosen by measurement); MSFNO_TILES
+// ("skip=4,fc1=1,...", values = GemmTile) overrides them for A/B experiments
+enum GemmRole { ROLE_SKIP = 0, ROLE_FC1, ROLE_FC2, ROLE_SPEC, ROLE_LEG, ROLE_COUNT };
+GemmTile role_tile(GemmRole r, GemmTile dflt);
 
 // C[M,N] = A[M,K] · B[K,N] (+ epilogue), row-major, fp32 MFMA.
 // Uniform batched mode: batch index = grid.z, operand batch strides sA/sB/sC.

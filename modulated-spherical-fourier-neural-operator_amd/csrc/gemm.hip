@@ -7,6 +7,9 @@
 // a 2×2 arrangement, each wave owning (BM/2)×(BN/2) as 32×32 MFMA tiles.
 // LDS is double buffered with one barrier per K-tile; A is staged k-major
 // (transposed) so both MFMA operands are read as conflict-free ds_read_b32.
+#include <cstdlib>
+#include <string>
+
 #include "common.h"
 
 namespace msfno {
@@ -26,9 +29,9 @@ struct GemmParams {
   // epilogue
   const float* bias;
   const float* addend;
-  float2* stats;
-  int64_t sBias, sD, sStats;
-  int ldd, act, relu_period, relu_rows, stats_ld;
+  int64_t sBias, sD;
+  int ldd, act, relu_period, relu_rows;
+  int vecC;  // C (and addend) rows 16-B aligned: float4 epilogue loads/stores
   const float* rowscale;
   int rs_C;
 };
@@ -89,7 +92,7 @@ __device__ __forceinline__ float gelu_erf(float v) {
 }
 
 // epilogue flags (+ EPI_GELU_B: GELU applied to the B operand while it is staged)
-enum : int { EPI_BIAS = 1, EPI_ADD = 2, EPI_GELU = 4, EPI_RELU = 8, EPI_STATS = 16, EPI_ROWSCALE = 32, EPI_GELU_B = 64 };
+enum : int { EPI_BIAS = 1, EPI_ADD = 2, EPI_GELU = 4, EPI_RELU = 8, EPI_ROWSCALE = 32, EPI_GELU_B = 64 };
 
 template <int BM, int BN, int BK, bool VEC, int EPI>
 __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmParams p) {
@@ -99,9 +102,14 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmParams p) {
   constexpr int LDB_S = BN;
   constexpr int A_LD = BM * BK / 1024;  // float4 staging loads per thread
   constexpr int B_LD = BN * BK / 1024;
-  __shared__ float As[2][BK * LDA_S];
-  __shared__ float Bs[2][BK * LDB_S];
-  __shared__ float red[2 * BM];
+  // one LDS array: the double-buffered A/B staging, reused by the epilogue as a
+  // 64-row x (BN + 8) row-major image of the accumulators
+  constexpr int CS_LD = BN + 8;
+  constexpr int STAGE = 2 * BK * LDA_S + 2 * BK * LDB_S;
+  constexpr int LDS_FLOATS = STAGE > 64 * CS_LD ? STAGE : 64 * CS_LD;
+  __shared__ __attribute__((aligned(16))) float lds[LDS_FLOATS];
+  auto As = [&](int buf) { return lds + buf * (BK * LDA_S); };
+  auto Bs = [&](int buf) { return lds + 2 * BK * LDA_S + buf * (BK * LDB_S); };
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -116,7 +124,6 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmParams p) {
   int tm, tn;
   const float* bias = p.bias;
   const float* addend = p.addend;
-  float2* stats = p.stats;
   int dflags = 0;
   if (p.descs) {
     const int lin = xcd_remap(blockIdx.x, gridDim.x);
@@ -140,14 +147,10 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmParams p) {
     A += z * p.sA; B += z * p.sB; C += z * p.sC;
     if (bias) bias += z * p.sBias;
     if (addend) addend += z * p.sD;
-    if (stats) stats += z * p.sStats;
   }
   const int m0 = tm * BM, n0 = tn * BN;
   const int nk = (K + BK - 1) / BK;
 
-  if constexpr ((EPI & EPI_STATS) != 0) {
-    if (tid < BM) { red[tid] = 0.f; red[BM + tid] = 0.f; }
-  }
 
   float4 ra[A_LD], rb[B_LD];
 
@@ -198,7 +201,7 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmParams p) {
       const int k = (idx % (BK / 4)) * 4;
       const bool rok = m0 + row < M;
       const int kg = k0 + k;
-      float* dst = &As[buf][k * LDA_S + row];
+      float* dst = As(buf) + k * LDA_S + row;
       dst[0] = (rok && kg + 0 < K) ? ra[q].x : 0.f;
       dst[LDA_S] = (rok && kg + 1 < K) ? ra[q].y : 0.f;
       dst[2 * LDA_S] = (rok && kg + 2 < K) ? ra[q].z : 0.f;
@@ -219,10 +222,11 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmParams p) {
       v.y = (kok && cg + 1 < N) ? v.y : 0.f;
       v.z = (kok && cg + 2 < N) ? v.z : 0.f;
       v.w = (kok && cg + 3 < N) ? v.w : 0.f;
-      *reinterpret_cast<float4*>(&Bs[buf][kr * LDB_S + col]) = v;
+      *reinterpret_cast<float4*>(Bs(buf) + kr * LDB_S + col) = v;
     }
   };
 
+  const int half = lane >> 5;
   floatx16 acc[MT][NT];
 #pragma unroll
   for (int i = 0; i < MT; ++i)
@@ -231,12 +235,11 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmParams p) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-  const int half = lane >> 5;
   const int l32 = lane & 31;
   // the MFMAs of one staged k-tile; per_kk(kk) runs after each MFMA group
   auto mfma_tile = [&](int buf, auto&& per_kk) {
-    const float* as = &As[buf][0];
-    const float* bs = &Bs[buf][0];
+    const float* as = As(buf);
+    const float* bs = Bs(buf);
 #pragma unroll
     for (int kk = 0; kk < BK / 2; ++kk) {
       const int k = 2 * kk + half;
@@ -315,87 +318,110 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmParams p) {
     }
   }
 
-  // ---- epilogue (compile-time specialised; one 32x32 tile at a time) ---------
-  constexpr bool kStats = (EPI & EPI_STATS) != 0;
+  // ---- epilogue through LDS ---------------------------------------------------
+  // Per MFMA row-tile i the four waves write their 32-row slices into a 64 x BN
+  // row-major LDS image; then all 256 threads walk it with 16-B vectors: bias,
+  // addend (all loads of a thread issued before any use), activation, and
+  // coalesced float4 stores.  Keeps the accumulators in AGPRs until here, the
+  // epilogue VGPR-light, and the global traffic in full lines.
+  float* Cs = lds;  // the main loop ended with a barrier: staging memory is free
+  constexpr int QPT = (64 * BN / 4) / 256;  // float4 per thread per row-tile
+  const bool vecC = p.vecC;
 #pragma unroll
   for (int i = 0; i < MT; ++i) {
-    float bv[16], sv[16];
-    int rowv[16];
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int lrow = wm * WM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
-      rowv[r] = m0 + lrow;
-      if constexpr ((EPI & EPI_BIAS) != 0) bv[r] = bias[min(rowv[r], M - 1)];
-      if constexpr ((EPI & EPI_ROWSCALE) != 0) {
-        const int rr = min(rowv[r], M - 1);
-        const int C2 = 2 * p.rs_C;
-        sv[r] = (dflags & 1) ? p.rowscale[(rr / C2) * p.rs_C + rr % p.rs_C] : 1.f;
-      }
-    }
-    float s[16], sq[16];
-    if constexpr (kStats) {
+    for (int j = 0; j < NT; ++j)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) s[r] = sq[r] = 0.f;
-    }
-#pragma unroll
-    for (int j = 0; j < NT; ++j) {
-      const int col = n0 + wn * WN + j * 32 + l32;
-      const bool cok = col < N;
-      float add[16];
-      if constexpr ((EPI & EPI_ADD) != 0) {
-#pragma unroll
-        for (int r = 0; r < 16; ++r)
-          add[r] = addend[(int64_t)min(rowv[r], M - 1) * p.ldd + min(col, N - 1)];
-      }
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        float v = acc[i][j][r];
-        if constexpr ((EPI & EPI_ROWSCALE) != 0) v *= sv[r];
-        if constexpr ((EPI & EPI_BIAS) != 0) v += bv[r];
-        if constexpr ((EPI & EPI_ADD) != 0) v += add[r];
-        if constexpr ((EPI & EPI_GELU) != 0) v = gelu_erf(v);
-        if constexpr ((EPI & EPI_RELU) != 0) {
-          if ((unsigned)rowv[r] % (unsigned)p.relu_period < (unsigned)p.relu_rows) v = fmaxf(v, 0.f);
-        }
-        const bool ok = cok && rowv[r] < M;
-        if (ok) C[(int64_t)rowv[r] * ldc + col] = v;
-        if constexpr (kStats) {
-          const float vz = ok ? v : 0.f;
-          s[r] += vz;
-          sq[r] += vz * vz;
-        }
-      }
-    }
-    if constexpr (kStats) {
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        float a = s[r], q = sq[r];
-#pragma unroll
-        for (int o = 1; o < 32; o <<= 1) {
-          a += __shfl_xor(a, o);
-          q += __shfl_xor(q, o);
-        }
-        if (l32 == 0) {
-          const int lrow = rowv[r] - m0;
-          atomicAdd(&red[lrow], a);
-          atomicAdd(&red[BM + lrow], q);
-        }
-      }
-    }
-  }
-  if constexpr (kStats) {
+      for (int r = 0; r < 16; ++r)
+        Cs[(wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * half) * CS_LD + wn * WN + j * 32 + l32] =
+            acc[i][j][r];
     __syncthreads();
-    if (tid < BM) {
-      const int row = m0 + tid;
-      if (row < M) {
-        const float n = (float)min(BN, N - n0);
-        const float sm = red[tid];
-        const float mean = sm / n;
-        const float m2 = fmaxf(red[BM + tid] - sm * mean, 0.f);
-        stats[(int64_t)row * p.stats_ld + tn] = make_float2(mean, m2);
+    float4 add4[QPT];
+    if constexpr ((EPI & EPI_ADD) != 0) {
+#pragma unroll
+      for (int q = 0; q < QPT; ++q) {
+        const int idx = tid + 256 * q;
+        const int lr = idx / (BN / 4);
+        const int row = min(m0 + (lr >> 5) * WM + i * 32 + (lr & 31), M - 1);
+        const int col = n0 + 4 * (idx % (BN / 4));
+        const float* src = addend + (int64_t)row * p.ldd;
+        if (vecC) {
+          add4[q] = *reinterpret_cast<const float4*>(src + min(col, (N - 1) & ~3));
+        } else {
+          add4[q] = make_float4(src[min(col, N - 1)], src[min(col + 1, N - 1)],
+                                src[min(col + 2, N - 1)], src[min(col + 3, N - 1)]);
+        }
       }
     }
+#pragma unroll
+    for (int q = 0; q < QPT; ++q) {
+      const int idx = tid + 256 * q;
+      const int lr = idx / (BN / 4);
+      const int c4 = idx % (BN / 4);
+      const int row = m0 + (lr >> 5) * WM + i * 32 + (lr & 31);
+      const int col = n0 + 4 * c4;
+      float4 v = *reinterpret_cast<const float4*>(Cs + lr * CS_LD + 4 * c4);
+      const int rr = min(row, M - 1);
+      if constexpr ((EPI & EPI_ROWSCALE) != 0) {
+        const int C2 = 2 * p.rs_C;
+        const float sv = (dflags & 1) ? p.rowscale[(rr / C2) * p.rs_C + rr % p.rs_C] : 1.f;
+        v.x *= sv; v.y *= sv; v.z *= sv; v.w *= sv;
+      }
+      if constexpr ((EPI & EPI_BIAS) != 0) {
+        const float bv = bias[rr];
+        v.x += bv; v.y += bv; v.z += bv; v.w += bv;
+      }
+      if constexpr ((EPI & EPI_ADD) != 0) {
+        v.x += add4[q].x; v.y += add4[q].y; v.z += add4[q].z; v.w += add4[q].w;
+      }
+      if constexpr ((EPI & EPI_GELU) != 0) {
+        v.x = gelu_erf(v.x); v.y = gelu_erf(v.y); v.z = gelu_erf(v.z); v.w = gelu_erf(v.w);
+      }
+      if constexpr ((EPI & EPI_RELU) != 0) {
+        if ((unsigned)row % (unsigned)p.relu_period < (unsigned)p.relu_rows) {
+          v.x = fmaxf(v.x, 0.f); v.y = fmaxf(v.y, 0.f); v.z = fmaxf(v.z, 0.f); v.w = fmaxf(v.w, 0.f);
+        }
+      }
+      if (row < M) {
+        float* dst = C + (int64_t)row * ldc + col;
+        if (vecC && col + 3 < N) {
+          *reinterpret_cast<float4*>(dst) = v;
+        } else {
+          if (col < N) dst[0] = v.x;
+          if (col + 1 < N) dst[1] = v.y;
+          if (col + 2 < N) dst[2] = v.z;
+          if (col + 3 < N) dst[3] = v.w;
+        }
+      }
+    }
+    if (i + 1 < MT) __syncthreads();
   }
+}
+
+GemmTile role_tile(GemmRole r, GemmTile dflt) {
+  static int table[ROLE_COUNT];
+  static bool init = false;
+  if (!init) {
+    for (int& t : table) t = -1;
+    if (const char* e = getenv("MSFNO_TILES")) {
+      static const char* names[ROLE_COUNT] = {"skip", "fc1", "fc2", "spec", "leg"};
+      std::string spec(e);
+      size_t pos = 0;
+      while (pos < spec.size()) {
+        size_t end = spec.find(',', pos);
+        if (end == std::string::npos) end = spec.size();
+        const std::string kv = spec.substr(pos, end - pos);
+        const size_t eq = kv.find('=');
+        if (eq != std::string::npos)
+          for (int i = 0; i < ROLE_COUNT; ++i)
+            if (kv.substr(0, eq) == names[i]) table[i] = atoi(kv.c_str() + eq + 1);
+        pos = end + 1;
+      }
+    }
+    init = true;
+  }
+  const int t = table[r];
+  return (t >= 0 && t <= TILE_128x256) ? (GemmTile)t : dflt;
 }
 
 void gemm_tile_dims(GemmTile tile, int* bm, int* bn) {
@@ -403,6 +429,8 @@ void gemm_tile_dims(GemmTile tile, int* bm, int* bn) {
     case TILE_128x128: *bm = 128; *bn = 128; break;
     case TILE_128x64: *bm = 128; *bn = 64; break;
     case TILE_256x64: *bm = 256; *bn = 64; break;
+    case TILE_256x128: *bm = 256; *bn = 128; break;
+    case TILE_128x256: *bm = 128; *bn = 256; break;
     default: *bm = 64; *bn = 64; break;
   }
 }
@@ -410,10 +438,9 @@ void gemm_tile_dims(GemmTile tile, int* bm, int* bn) {
 static GemmParams make_params(const float* A, const float* B, float* C, const GemmEpi& e) {
   GemmParams p{};
   p.A = A; p.B = B; p.C = C;
-  p.bias = e.bias; p.addend = e.addend; p.stats = e.stats;
-  p.sBias = e.sBias; p.sD = e.sD; p.sStats = e.sStats;
+  p.bias = e.bias; p.addend = e.addend;
+  p.sBias = e.sBias; p.sD = e.sD;
   p.ldd = e.ldd; p.act = e.act; p.relu_period = e.relu_period; p.relu_rows = e.relu_rows;
-  p.stats_ld = e.stats_ld;
   p.rowscale = e.rowscale;
   p.rs_C = e.rs_C;
   return p;
@@ -429,7 +456,7 @@ static void launch_e(const GemmParams& p, dim3 grid, hipStream_t s) {
 
 static int epi_code(const GemmParams& p) {
   return (p.bias ? EPI_BIAS : 0) | (p.addend ? EPI_ADD : 0) | (p.act == 1 ? EPI_GELU : 0) |
-         (p.relu_period ? EPI_RELU : 0) | (p.stats ? EPI_STATS : 0) |
+         (p.relu_period ? EPI_RELU : 0) |
          (p.rowscale ? EPI_ROWSCALE : 0) | (p.act == 2 ? EPI_GELU_B : 0);
 }
 
@@ -447,13 +474,6 @@ static int launch(const GemmParams& p, dim3 grid, hipStream_t s) {
     case EPI_GELU_B | EPI_BIAS | EPI_ADD:
       launch_e<BM, BN, BK, EPI_GELU_B | EPI_BIAS | EPI_ADD>(p, grid, s); break;
     case EPI_ADD: launch_e<BM, BN, BK, EPI_ADD>(p, grid, s); break;
-    case EPI_BIAS | EPI_ADD | EPI_STATS:
-      launch_e<BM, BN, BK, EPI_BIAS | EPI_ADD | EPI_STATS>(p, grid, s); break;
-    case EPI_BIAS | EPI_ADD | EPI_GELU | EPI_STATS:
-      launch_e<BM, BN, BK, EPI_BIAS | EPI_ADD | EPI_GELU | EPI_STATS>(p, grid, s); break;
-    case EPI_ADD | EPI_STATS: launch_e<BM, BN, BK, EPI_ADD | EPI_STATS>(p, grid, s); break;
-    case EPI_ADD | EPI_GELU | EPI_STATS:
-      launch_e<BM, BN, BK, EPI_ADD | EPI_GELU | EPI_STATS>(p, grid, s); break;
     default:
       set_error("gemm: unsupported epilogue combination");
       return MSFNO_EUNSUPPORTED;
@@ -471,6 +491,8 @@ static int dispatch(GemmTile tile, const GemmParams& p, dim3 grid, hipStream_t s
     case TILE_128x128: rc = launch<128, 128, MSFNO_GEMM_BK>(p, grid, s); break;
     case TILE_128x64: rc = launch<128, 64, MSFNO_GEMM_BK>(p, grid, s); break;
     case TILE_256x64: rc = launch<256, 64, MSFNO_GEMM_BK>(p, grid, s); break;
+    case TILE_256x128: rc = launch<256, 128, MSFNO_GEMM_BK>(p, grid, s); break;
+    case TILE_128x256: rc = launch<128, 256, MSFNO_GEMM_BK>(p, grid, s); break;
     default: rc = launch<64, 64, MSFNO_GEMM_BK>(p, grid, s); break;
   }
   if (rc != MSFNO_OK) return rc;
@@ -492,6 +514,8 @@ int gemm_uniform(GemmTile tile, const float* A, const float* B, float* C, int M,
   p.tiles_n = (int)cdiv(N, bn);
   p.vecA = (lda % 4 == 0) && (sA % 4 == 0) && aligned16(A);
   p.vecB = (ldb % 4 == 0) && (sB % 4 == 0) && aligned16(B);
+  p.vecC = (ldc % 4 == 0) && (sC % 4 == 0) && aligned16(C) &&
+           (!epi.addend || ((epi.ldd % 4 == 0) && (epi.sD % 4 == 0) && aligned16(epi.addend)));
   MSFNO_REQUIRE(batch <= 65535, MSFNO_EINVAL, "gemm: batch too large");
   dim3 grid(p.tiles_m * p.tiles_n, 1, batch);
   return dispatch(tile, p, grid, s);
@@ -506,6 +530,7 @@ int gemm_desc(GemmTile tile, const float* A, const float* B, float* C, const Gem
   // descriptor problems are laid out with lda/ldb/offsets that are multiples of 4
   p.vecA = aligned16(A);
   p.vecB = aligned16(B);
+  p.vecC = aligned16(C) && !epi.addend;
   return dispatch(tile, p, dim3(total_tiles), s);
 }
 

@@ -2,6 +2,7 @@
 // Build: hipcc -O3 --offload-arch=gfx950 -std=c++17 tools/gemm_bench.hip -lrocblas -o tools/bin/gemm_bench
 #include <chrono>
 #include <cstdio>
+#include <string>
 #include <vector>
 #include <rocblas/rocblas.h>
 
@@ -36,7 +37,8 @@ float run(const char* name, int M, int N, int K, float* A, float* B, float* C, c
   return ms;
 }
 
-int main() {
+int main(int argc, char** argv) {
+  const char* only = argc > 1 ? argv[1] : nullptr;
   const int P = 721 * 1440;
   size_t maxA = 1024 * 1024, maxB = (size_t)512 * P, maxC = (size_t)512 * P;
   float *A, *B, *C, *D, *bias;
@@ -58,24 +60,29 @@ int main() {
   GemmEpi plain;
   GemmEpi gelu; gelu.bias = bias; gelu.act = 1;
   GemmEpi skipe; skipe.bias = bias; skipe.addend = D; skipe.ldd = P;
+  GemmEpi skipb; skipb.bias = bias;
+  GemmEpi relu; relu.relu_period = 1024; relu.relu_rows = 512;
   GemmEpi fc2e; fc2e.bias = bias; fc2e.addend = D; fc2e.ldd = P;
   GemmEpi fc2g = fc2e; fc2g.act = 2;
   GemmEpi geluB; geluB.act = 2; geluB.bias = bias;
-  float2* st; hipMalloc(&st, 256 * 8200 * 8);
-  skipe.stats = st; skipe.stats_ld = 8200;
   const int T = 65536;
   struct S { const char* n; int M, N, K; GemmEpi e; };
   std::vector<S> shapes = {
-      {"fc2", 256, P, 512, plain}, {"fc2-geluB", 256, P, 512, geluB}, {"fc1", 512, P, 256, plain}, {"fc1-gelu", 512, P, 256, gelu},
+      {"fc2", 256, P, 512, plain}, {"fc2-geluB", 256, P, 512, geluB}, {"spec-relu", 1024, 65536, 1024, relu}, {"fc1", 512, P, 256, plain}, {"fc1-gelu", 512, P, 256, gelu},
+      {"fc2-badd", 256, P, 512, fc2e}, {"skip", 256, P, 256, skipb}, {"spec", 1024, 65536, 1024, plain},
       {"fc2-full", 256, P, 512, fc2g}};
   for (auto& s : shapes) {
+    if (only && std::string(s.n) != only) continue;
     const double fl = 2.0 * s.M * (double)s.N * s.K;
     run<128, 128, 16>(s.n, s.M, s.N, s.K, A, B, C, s.e, 5, fl);
     run<128, 64, 16>(s.n, s.M, s.N, s.K, A, B, C, s.e, 5, fl);
     run<256, 64, 16>(s.n, s.M, s.N, s.K, A, B, C, s.e, 5, fl);
-    // run<256, 64, 32>(s.n, s.M, s.N, s.K, A, B, C, s.e, 5, fl);
+    run<256, 128, 16>(s.n, s.M, s.N, s.K, A, B, C, s.e, 5, fl);
+    run<128, 256, 16>(s.n, s.M, s.N, s.K, A, B, C, s.e, 5, fl);
+    run<128, 128, 32>(s.n, s.M, s.N, s.K, A, B, C, s.e, 5, fl);
   }
   // rocBLAS sgemm on the same row-major problem: C^T = B^T A^T (column-major)
+  if (only) return 0;
   rocblas_handle rh;
   rocblas_create_handle(&rh);
   const float one = 1.f, zero = 0.f;
