@@ -44,9 +44,11 @@ PEAK_HBM_GBS = 8000.0           # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 # stages that run on the block's side stream (concurrent with the SHT)
 SIDE_STAGES = {"inner_skip"}
 # stage -> kernel symbol in the rocprofv3 summaries (profiles/<tag>/kernel_stats.csv);
-# the fc2 GEMM is the only instantiation with this tile/epilogue (bias + residual + GELU-on-B)
+# fc1 (bias + GELU epilogue, 128x64) and fc2 (bias + residual, 128x128) are the only
+# launches of their template instantiations in the block
 STAGE_KERNEL = {
-    "mlp_fc2": "void msfno::gemm_f32_kernel<256, 64, 16, true, 67>(msfno::GemmParams)",
+    "mlp_fc1": "void msfno::gemm_f32_kernel<128, 64, 16, true, 5>(msfno::GemmParams)",
+    "mlp_fc2": "void msfno::gemm_f32_kernel<128, 128, 16, true, 3>(msfno::GemmParams)",
 }
 
 

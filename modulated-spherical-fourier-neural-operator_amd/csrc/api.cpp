@@ -433,7 +433,8 @@ int run_filter(const msfno_block_desc* d, msfno_sht_plan_s* f, msfno_sht_plan_s*
         e.relu_period = 2 * co;
         e.relu_rows = co;
       }
-      MSFNO_TRY(gemm_uniform(role_tile(ROLE_SPEC, TILE_256x128), b.Wexp[l], in, out, 2 * co, (int)L.Tp, 2 * ci, 2 * ci,
+      MSFNO_TRY(gemm_uniform(role_tile(ROLE_SPEC, TILE_128x128), b.Wexp[l], in, out, 2 * co,
+                             (int)L.Tp, 2 * ci, 2 * ci,
                              (int)L.ldT, (int)L.ldT, 0, 2LL * ci * L.ldT, 2LL * co * L.ldT, B, e,
                              s));
       in = out;
