@@ -47,8 +47,8 @@ SIDE_STAGES = {"inner_skip"}
 # fc1 (bias + GELU epilogue, 128x64) and fc2 (bias + residual, 128x128) are the only
 # launches of their template instantiations in the block
 STAGE_KERNEL = {
-    "mlp_fc1": "void msfno::gemm_f32_kernel<128, 64, 16, true, 5>(msfno::GemmParams)",
-    "mlp_fc2": "void msfno::gemm_f32_kernel<128, 128, 16, true, 3>(msfno::GemmParams)",
+    "mlp_fc1": "void msfno::gemm_f32_kernel<128, 256, 16, true, 5>(msfno::GemmParams)",
+    "mlp_fc2": "void msfno::gemm_f32_kernel<256, 128, 16, true, 3>(msfno::GemmParams)",
 }
 
 

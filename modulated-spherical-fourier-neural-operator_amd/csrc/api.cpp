@@ -583,13 +583,13 @@ int run_mlp(const msfno_block_desc* d, const float* W1f, const float* b1f, const
   e1.bias = b1f;
   e1.sBias = Hd;
   e1.act = 1;
-  MSFNO_TRY(gemm_uniform(role_tile(ROLE_FC1, TILE_128x64), W1f, x1, h, (int)Hd, (int)P, (int)C, (int)C, (int)P,
+  MSFNO_TRY(gemm_uniform(role_tile(ROLE_FC1, TILE_128x256), W1f, x1, h, (int)Hd, (int)P, (int)C, (int)C, (int)P,
                          (int)P, Hd * C, C * P, Hd * P, B, e1, s));
   prof(ST_FC2, s);
   GemmEpi e2;
   e2.bias = d->fc2_b;
   if (resid) { e2.addend = resid; e2.sD = C * P; e2.ldd = (int)P; }
-  return gemm_uniform(role_tile(ROLE_FC2, TILE_128x128), d->fc2_w, h, out, (int)C, (int)P, (int)Hd, (int)Hd, (int)P,
+  return gemm_uniform(role_tile(ROLE_FC2, TILE_256x128), d->fc2_w, h, out, (int)C, (int)P, (int)Hd, (int)Hd, (int)P,
                       (int)P, 0, Hd * P, C * P, B, e2, s);
 }
 }  // namespace msfno
@@ -799,7 +799,7 @@ int msfno_block_forward(const msfno_block_desc* d, msfno_sht_plan_t f, msfno_sht
     prof(ST_SKIP, ss);
     GemmEpi e;
     e.bias = d->skip_b;
-    MSFNO_TRY(gemm_uniform(role_tile(ROLE_SKIP, TILE_128x128), d->skip_w, x, x1, (int)C, (int)P, (int)C, (int)C,
+    MSFNO_TRY(gemm_uniform(role_tile(ROLE_SKIP, TILE_128x256), d->skip_w, x, x1, (int)C, (int)P, (int)C, (int)C,
                            (int)P, (int)P, 0, C * P, C * P, B, e, ss));
     if (side) {
       prof(ST_END, ss);

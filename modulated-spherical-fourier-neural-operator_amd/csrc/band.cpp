@@ -260,7 +260,7 @@ int msfno_band_block_stage(const msfno_block_desc* d, msfno_band_plan_t p, int s
         prof(ST_SKIP, ss);
         GemmEpi e;
         e.bias = d->skip_b;
-        MSFNO_TRY(gemm_uniform(role_tile(ROLE_SKIP, TILE_128x128), d->skip_w, io->x, b.x1, (int)C, (int)Pl, (int)C,
+        MSFNO_TRY(gemm_uniform(role_tile(ROLE_SKIP, TILE_128x256), d->skip_w, io->x, b.x1, (int)C, (int)Pl, (int)C,
                                (int)C, (int)Pl, (int)Pl, 0, C * Pl, C * Pl, B, e, ss));
         if (side) {
           prof(ST_END, ss);
