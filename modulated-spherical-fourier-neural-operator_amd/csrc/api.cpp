@@ -294,6 +294,26 @@ int ensure_desc(msfno_sht_plan_s* p, int R, int other_ld, int64_t ldT) {
   return MSFNO_OK;
 }
 
+// spectral MLP: Gauss 3M complex GEMM by default (MSFNO_SPEC_4M=1: the real-ified
+// 4-multiplication GEMM, kept as an A/B switch); MSFNO_C3M_TILE picks its tile
+bool use_c3m() {
+  static int mode = -1;
+  if (mode < 0) {
+    const char* e = getenv("MSFNO_SPEC_4M");
+    mode = (e && e[0] == '1') ? 0 : 1;
+  }
+  return mode == 1;
+}
+
+int c3m_tile() {
+  static int t = -1;
+  if (t < 0) {
+    const char* e = getenv("MSFNO_C3M_TILE");
+    t = e ? atoi(e) : 1;  // 64x128 measured best (in-block A/B)
+  }
+  return t;
+}
+
 // MSFNO_FFT_TILE=1 selects the fused FFT+transpose tile kernels instead of the
 // row FFT + separate transpose kernels (measured slower on MI355X at 721x1440:
 // DESIGN.md §5); kept as an A/B switch.
@@ -415,12 +435,16 @@ int run_filter(const msfno_block_desc* d, msfno_sht_plan_s* f, msfno_sht_plan_s*
     const int nl = d->spectral_layers;
     const int64_t Hs = d->spec_hidden;
     prof(ST_SPEC_PREP, s);
+    const bool c3m = use_c3m();
     for (int l = 0; l <= nl; ++l) {
       const int ci = (l == 0) ? (int)C : (int)Hs;
       const int co = (l == nl) ? (int)C : (int)Hs;
       const float* w = (l == nl) ? d->spec_wout : d->spec_w[l];
       MSFNO_REQUIRE(w, MSFNO_EINVAL, "missing spectral weight");
-      MSFNO_TRY(launch_expand_complex_weight(w, b.Wexp[l], ci, co, s));
+      if (c3m)
+        MSFNO_TRY(launch_split_complex_weight(w, b.Wexp[l], b.Wexp[l] + (int64_t)ci * co, ci, co, s));
+      else
+        MSFNO_TRY(launch_expand_complex_weight(w, b.Wexp[l], ci, co, s));
     }
     const float* in = b.Sa;
     for (int l = 0; l <= nl; ++l) {
@@ -428,15 +452,21 @@ int run_filter(const msfno_block_desc* d, msfno_sht_plan_s* f, msfno_sht_plan_s*
       const int co = (l == nl) ? (int)C : (int)Hs;
       float* out = (l == nl) ? b.Sa : ((l & 1) ? b.Sc : b.Sb);
       prof(l == nl ? ST_SPEC_OUT : ST_SPEC_L0 + std::min(l, 3), s);
-      GemmEpi e;
-      if (l < nl) {  // ComplexReLU(mode="real") on the real rows of each batch block
-        e.relu_period = 2 * co;
-        e.relu_rows = co;
+      if (c3m) {
+        // Gauss 3-multiplication complex GEMM (cgemm.hip), ComplexReLU(real) fused
+        MSFNO_TRY(gemm_c3m(b.Wexp[l], b.Wexp[l] + (int64_t)ci * co, in, out, co, ci, (int)L.Tp,
+                           (int)L.ldT, (int)L.ldT, 2LL * ci * L.ldT, 2LL * co * L.ldT, B, l < nl,
+                           c3m_tile(), s));
+      } else {
+        GemmEpi e;
+        if (l < nl) {  // ComplexReLU(mode="real") on the real rows of each batch block
+          e.relu_period = 2 * co;
+          e.relu_rows = co;
+        }
+        MSFNO_TRY(gemm_uniform(role_tile(ROLE_SPEC, TILE_128x128), b.Wexp[l], in, out, 2 * co,
+                               (int)L.Tp, 2 * ci, 2 * ci, (int)L.ldT, (int)L.ldT, 0,
+                               2LL * ci * L.ldT, 2LL * co * L.ldT, B, e, s));
       }
-      MSFNO_TRY(gemm_uniform(role_tile(ROLE_SPEC, TILE_128x128), b.Wexp[l], in, out, 2 * co,
-                             (int)L.Tp, 2 * ci, 2 * ci,
-                             (int)L.ldT, (int)L.ldT, 0, 2LL * ci * L.ldT, 2LL * co * L.ldT, B, e,
-                             s));
       in = out;
     }
   } else {

@@ -57,6 +57,8 @@ int legendre_inv(msfno_sht_plan_s* g, const float* S, float* Yt, int R, hipStrea
 int run_filter(const msfno_block_desc* d, msfno_sht_plan_s* f, msfno_sht_plan_s* g,
                const BlockBufs& b, int B, hipStream_t s);
 bool use_fft_tile(const msfno_sht_plan_s* p);
+bool use_c3m();
+int c3m_tile();
 void set_table_offsets(msfno_sht_plan_s* p, int sym);
 // channel MLP with norm1/FiLM folded into (W1f, b1f): out = W2·GELU(W1f·x1 + b1f) + b2 (+resid)
 int run_mlp(const msfno_block_desc* d, const float* W1f, const float* b1f, const float* x1,

@@ -63,6 +63,14 @@ int launch_fold_affine(const float* W, const float* bias, const float* scale, co
 int launch_affine_rows(const float* x, const float* scale, const float* shift,
                        const float* addend, float* out, int64_t BC, int64_t P, int act,
                        float2* stats, int stats_ld, hipStream_t s);
+// ---- cgemm.hip -----------------------------------------------------------------
+// complex (Ci,Co,2) weight -> Ar, Ai (Co x Ci) row-major (Ar[o][i] = Re w[i][o])
+int launch_split_complex_weight(const float* w, float* Ar, float* Ai, int Ci, int Co,
+                                hipStream_t s);
+// Y = W.X complex per column (3M scheme), X/Y rows [b][re|im][ci|co] in the S layout;
+// relu: ComplexReLU(real) on the output; tile 0: 128x64, 1: 64x128, 2: 128x128
+int gemm_c3m(const float* Ar, const float* Ai, const float* X, float* Y, int co, int ci, int N,
+             int ldx, int ldy, int64_t sX, int64_t sY, int B, bool relu, int tile, hipStream_t s);
 // complex (Ci,Co,2) weight -> real (2Co x 2Ci) block matrix [[Wr^T,-Wi^T],[Wi^T,Wr^T]]
 int launch_expand_complex_weight(const float* w, float* Wexp, int Ci, int Co, hipStream_t s);
 // (mmax,lmax,nlat) reference table -> plan GEMM layout (general or symmetric)
