@@ -119,6 +119,10 @@ def stage_work(name, B, C, nlat, nlon, lmax, mmax, hid, shid, rows=None, mset=No
         "transpose_fwd": ("hbm", 2 * BC * rows * mmax * 8),
         "transpose_inv": ("hbm", 2 * BC * rows * mmax * 8),
         "linear_contract": ("hbm", 8 * C * C * T + 2 * 8 * BC * T),
+        # latitude-band exchange re-layouts (this rank's rows / m-set)
+        "band_pack": ("hbm", 2 * BC * rows * mmax * 8),
+        "band_gather": ("hbm", 2 * 2 * BC * nlat * len(ms) * 4),
+        "band_scatter": ("hbm", 2 * 2 * BC * nlat * len(ms) * 4),
     }
     return tab.get(name)
 
@@ -194,12 +198,19 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = world > 1
+    # rehearsal knobs for a one-GPU box (never used by the driver's runs):
+    # MSFNO_BENCH_BACKEND=gloo and MSFNO_BENCH_SHARE_GPU=1 put every rank on cuda:0
+    backend = os.environ.get("MSFNO_BENCH_BACKEND", "nccl")
+    gpu = 0 if os.environ.get("MSFNO_BENCH_SHARE_GPU") == "1" else local
     if dist:
         import torch.distributed as td
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(local)
-        td.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local)
+        torch.cuda.set_device(gpu)
+        if backend == "nccl":
+            td.init_process_group("nccl", device_id=torch.device("cuda", gpu))
+        else:
+            td.init_process_group(backend)
+    dev = torch.device("cuda", gpu)
     torch.cuda.set_device(dev)
 
     from msfno_amd import _native as N
@@ -257,7 +268,8 @@ def main():
         stages = N.profile_collect()
     elapsed = t1 - t0
     if dist:
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        t = torch.tensor([elapsed], device=dev if backend == "nccl" else "cpu",
+                         dtype=torch.float64)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         elapsed = t.item()
     assert torch.isfinite(y).all()
