@@ -143,6 +143,27 @@ int msfno_filter_forward(const msfno_block_desc* d, msfno_sht_plan_t fwd, msfno_
                          void* stream);
 
 /* ---------------------------------------------------------------------------
+ * Channel MLP (MSFNO/Models/sfno/layers.py:145-178, MLP.forward) as used by the
+ * network encoder and decoder (sfnonet.py:513-523, 617-629, forward :667-686):
+ *   out = W2 · GELU(W1 · [x ; x2] + b1) (+ b2) (+ addend)
+ * x (B, Cin, P) and the optional second input x2 (B, Cin2, P) are the two halves
+ * of the channel concatenation torch.cat((x, residual), dim=1) of the big skip
+ * (sfnonet.py:680-681), consumed without materialising it; fc1_w is
+ * (Hid, Cin + Cin2).  addend (optional) is added to the output with batch
+ * stride add_bstride (0 broadcasts it: the encoder's pos_embed, :674).
+ * ------------------------------------------------------------------------- */
+typedef struct msfno_mlp_desc {
+  int Cin, Cin2, Hid, Cout;
+  const float* fc1_w; const float* fc1_b;   /* (Hid, Cin+Cin2, 1, 1), (Hid)  */
+  const float* fc2_w; const float* fc2_b;   /* (Cout, Hid, 1, 1), (Cout) or NULL */
+} msfno_mlp_desc;
+
+size_t msfno_mlp_workspace_size(const msfno_mlp_desc* d, int B, long long P);
+int msfno_mlp_forward(const msfno_mlp_desc* d, const float* x, const float* x2,
+                      const float* addend, long long add_bstride, float* out, int B,
+                      long long P, void* ws, size_t ws_bytes, void* stream);
+
+/* ---------------------------------------------------------------------------
  * Latitude-band sharded SFNO-Block (multi-GPU form of
  * msfno_block_forward).  The reference runs one block per process on the whole
  * field (DDP = replicas, MSFNO/main.py:1153); this splits ONE field batch over

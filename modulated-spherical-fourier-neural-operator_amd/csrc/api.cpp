@@ -891,3 +891,67 @@ int msfno_profile_collect(double* total_ms, int* counts) {
 }
 
 }  // extern "C"
+
+// ---------------------------------------------------------------------------
+// channel MLP (encoder / decoder of the network)
+// ---------------------------------------------------------------------------
+extern "C" {
+
+size_t msfno_mlp_workspace_size(const msfno_mlp_desc* d, int B, long long P) {
+  if (!d || B <= 0 || P <= 0) return 0;
+  Carve cv;
+  cv.take<float>((int64_t)B * d->Hid * P);                // h
+  if (d->Cin2 > 0) cv.take<float>((int64_t)B * d->Hid * P);  // first half of fc1
+  return cv.off;
+}
+
+int msfno_mlp_forward(const msfno_mlp_desc* d, const float* x, const float* x2,
+                      const float* addend, long long add_bstride, float* out, int B,
+                      long long P, void* ws, size_t ws_bytes, void* stream) {
+  MSFNO_REQUIRE(d && x && out && d->fc1_w && d->fc2_w && d->fc1_b, MSFNO_EINVAL,
+                "mlp: missing tensors");
+  MSFNO_REQUIRE(d->Cin > 0 && d->Hid > 0 && d->Cout > 0 && d->Cin2 >= 0 && B > 0 && P > 0,
+                MSFNO_EINVAL, "mlp: bad sizes");
+  MSFNO_REQUIRE((d->Cin2 > 0) == (x2 != nullptr), MSFNO_EINVAL,
+                "mlp: x2 must be given exactly when Cin2 > 0");
+  MSFNO_REQUIRE(P <= 0x7fffffff, MSFNO_EINVAL, "mlp: too many pixels");
+  MSFNO_REQUIRE(ws_bytes >= msfno_mlp_workspace_size(d, B, P), MSFNO_EWORKSPACE,
+                "workspace too small");
+  hipStream_t s = (hipStream_t)stream;
+  Carve cv;
+  cv.base = (char*)ws;
+  const int64_t Hd = d->Hid, Ct = d->Cin + d->Cin2;
+  float* h = cv.take<float>((int64_t)B * Hd * P);
+  const int Pi = (int)P;
+  prof(ST_FC1, s);
+  if (d->Cin2 > 0) {
+    // fc1 over the concatenation [x ; x2]: t = W1[:, :Cin]·x, then h = GELU(W1[:, Cin:]·x2 + b1 + t)
+    float* t = cv.take<float>((int64_t)B * Hd * P);
+    GemmEpi e0;
+    MSFNO_TRY(gemm_uniform(role_tile(ROLE_FC1, TILE_128x256), d->fc1_w, x, t, (int)Hd, Pi, d->Cin,
+                           (int)Ct, Pi, Pi, 0, (int64_t)d->Cin * P, Hd * P, B, e0, s));
+    GemmEpi e1;
+    e1.bias = d->fc1_b;
+    e1.addend = t; e1.sD = Hd * P; e1.ldd = Pi;
+    e1.act = 1;
+    MSFNO_TRY(gemm_uniform(role_tile(ROLE_FC1, TILE_128x256), d->fc1_w + d->Cin, x2, h, (int)Hd,
+                           Pi, d->Cin2, (int)Ct, Pi, Pi, 0, (int64_t)d->Cin2 * P, Hd * P, B, e1, s));
+  } else {
+    GemmEpi e1;
+    e1.bias = d->fc1_b;
+    e1.act = 1;
+    MSFNO_TRY(gemm_uniform(role_tile(ROLE_FC1, TILE_128x256), d->fc1_w, x, h, (int)Hd, Pi, d->Cin,
+                           d->Cin, Pi, Pi, 0, (int64_t)d->Cin * P, Hd * P, B, e1, s));
+  }
+  prof(ST_FC2, s);
+  GemmEpi e2;
+  e2.bias = d->fc2_b;
+  if (addend) { e2.addend = addend; e2.sD = add_bstride; e2.ldd = Pi; }
+  const GemmTile t2 = d->Cout <= 128 ? TILE_128x128 : role_tile(ROLE_FC2, TILE_256x128);
+  MSFNO_TRY(gemm_uniform(t2, d->fc2_w, h, out, d->Cout, Pi, (int)Hd, (int)Hd, Pi, Pi, 0, Hd * P,
+                         (int64_t)d->Cout * P, B, e2, s));
+  prof(ST_END, s);
+  return MSFNO_OK;
+}
+
+}  // extern "C"

@@ -48,6 +48,15 @@ class BlockDesc(ctypes.Structure):
     ]
 
 
+class MlpDesc(ctypes.Structure):
+    """Mirror of ``msfno_mlp_desc`` (include/msfno.h)."""
+
+    _fields_ = [
+        ("Cin", _i), ("Cin2", _i), ("Hid", _i), ("Cout", _i),
+        ("fc1_w", _vp), ("fc1_b", _vp), ("fc2_w", _vp), ("fc2_b", _vp),
+    ]
+
+
 class BandIO(ctypes.Structure):
     """Mirror of ``msfno_band_io`` (include/msfno.h)."""
 
@@ -79,6 +88,9 @@ SIGNATURES = [
                                  _i, _vp, _sz, _vp]),
     ("msfno_filter_forward", _i, [ctypes.POINTER(BlockDesc), _vp, _vp, _vp, _vp, _i, _vp, _sz,
                                   _vp]),
+    ("msfno_mlp_workspace_size", _sz, [ctypes.POINTER(MlpDesc), _i, ctypes.c_longlong]),
+    ("msfno_mlp_forward", _i, [ctypes.POINTER(MlpDesc), _vp, _vp, _vp, ctypes.c_longlong, _vp, _i,
+                               ctypes.c_longlong, _vp, _sz, _vp]),
     ("msfno_band_partition", _i, [_i, _i, _i, _i, _ip, _ip]),
     ("msfno_band_exchange_counts", _i, [_i, _i, _i, _i, _ip, _ip, _i, _i, _llp, _llp]),
     ("msfno_band_plan_create", _i, [_i, _i, _i, _i, _i, _i, _ip, _ip, ctypes.POINTER(_vp)]),

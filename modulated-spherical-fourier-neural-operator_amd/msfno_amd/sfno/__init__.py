@@ -6,6 +6,8 @@ from .sfnonet import (  # noqa: F401
     FiLM,
     FourierNeuralOperatorBlock,
     FourierNeuralOperatorBlock_Filmed,
+    FourierNeuralOperatorNet,
+    FourierNeuralOperatorNet_Filmed,
     SpectralFilterLayer,
 )
 from .latband import LatBandBlock, LocalGroup, TorchComm, band_partition, exchange_counts  # noqa: F401,E501

@@ -60,7 +60,8 @@ class DropPath(nn.Module):
 class MLP(nn.Module):
     """Conv1x1 → act → Conv1x1 (state-dict keys fwd.0.*, fwd.2.*).  Inside a
     block it is executed by the fused native block (two MFMA GEMMs with the
-    norm1/FiLM affine folded into fc1 and GELU / bias / residual in epilogues)."""
+    norm1/FiLM affine folded into fc1 and GELU / bias / residual in epilogues);
+    standalone (the network encoder / decoder) by msfno_mlp_forward."""
 
     def __init__(self, in_features, hidden_features=None, out_features=None, act_layer=nn.GELU,
                  output_bias=True, drop_rate=0.0, checkpointing_mlp=False):
@@ -77,8 +78,63 @@ class MLP(nn.Module):
         else:
             self.fwd = nn.Sequential(fc1, act, fc2)
 
+    def native_desc(self, cin2=0):
+        fc1, act, fc2 = self.fwd[0], self.fwd[1], self.fwd[-1]
+        if not (isinstance(act, nn.GELU) and getattr(act, "approximate", "none") == "none"):
+            raise NotImplementedError("the native MLP fuses GELU(approximate='none') only")
+        if self.training and len(self.fwd) > 3:
+            raise NotImplementedError("MLP dropout in training mode is not fused")
+        keep = []
+
+        def f32(t):
+            t = t.detach().float().contiguous()
+            keep.append(t)
+            return t
+
+        w1, w2 = f32(fc1.weight), f32(fc2.weight)
+        b1 = f32(fc1.bias)
+        b2 = f32(fc2.bias) if fc2.bias is not None else None
+        d = N.MlpDesc()
+        d.Cin = w1.shape[1] - cin2
+        d.Cin2 = cin2
+        d.Hid = w1.shape[0]
+        d.Cout = w2.shape[0]
+        d.fc1_w, d.fc1_b, d.fc2_w, d.fc2_b = w1.data_ptr(), b1.data_ptr(), w2.data_ptr(), N.ptr(b2)
+        return d, keep
+
+    def native_forward(self, x, x2=None, addend=None):
+        """out = fc2(GELU(fc1(cat(x, x2)))) (+ addend, broadcast over the batch when its
+        leading dimension is 1) in two MFMA GEMMs (msfno_mlp_forward); the channel
+        concatenation is consumed in place (sfnonet.py:680-686)."""
+        dtype = x.dtype
+        x = N.require_device_f32(x, "MLP input")
+        B, Cin, H, W = x.shape
+        cin2 = 0
+        if x2 is not None:
+            x2 = N.require_device_f32(x2, "MLP second input")
+            assert x2.shape[0] == B and x2.shape[2:] == x.shape[2:]
+            cin2 = x2.shape[1]
+        d, keep = self.native_desc(cin2)
+        if d.Cin != Cin:
+            raise ValueError(f"MLP expects {d.Cin} (+{cin2}) input channels, got {Cin}")
+        bstride = 0
+        if addend is not None:
+            addend = N.require_device_f32(addend, "MLP addend")
+            assert addend.shape[1:] == (d.Cout, H, W)
+            bstride = 0 if addend.shape[0] == 1 else d.Cout * H * W
+        L = N.lib()
+        P = H * W
+        nbytes = L.msfno_mlp_workspace_size(d, B, P)
+        ws = torch.empty(nbytes, dtype=torch.uint8, device=x.device)
+        out = torch.empty(B, d.Cout, H, W, dtype=torch.float32, device=x.device)
+        N.check(L.msfno_mlp_forward(d, x.data_ptr(), N.ptr(x2), N.ptr(addend), bstride,
+                                    out.data_ptr(), B, P, ws.data_ptr(), nbytes,
+                                    N.stream_of(x.device)), "MLP.forward")
+        del keep
+        return out.to(dtype)
+
     def forward(self, x):
-        return self.fwd(x)
+        return self.native_forward(x)
 
 
 def _check_transforms(fwd, inv):

@@ -1,6 +1,7 @@
-"""SFNO-Block — mirror of MSFNO/Models/sfno/sfnonet.py (SpectralFilterLayer
-:56-133, FourierNeuralOperatorBlock :136-251, FourierNeuralOperatorBlock_Filmed
-:254-393, FiLM :689-697).
+"""SFNO-Block and network — mirror of MSFNO/Models/sfno/sfnonet.py
+(SpectralFilterLayer :56-133, FourierNeuralOperatorBlock :136-251,
+FourierNeuralOperatorBlock_Filmed :254-393, FourierNeuralOperatorNet :406-686,
+FiLM :689-697, FourierNeuralOperatorNet_Filmed :699-860).
 
 Same constructor signatures, submodule names and state-dict keys as the
 reference.  ``forward`` executes the whole block — norm0, SHT, spectral filter,
@@ -200,3 +201,203 @@ class FourierNeuralOperatorBlock_Filmed(FourierNeuralOperatorBlock):
 
     def forward(self, x, gamma, beta, scale=1):
         return self._native_forward(x, gamma, beta, scale)
+
+
+def _trunc_normal_init(m):
+    """FourierNeuralOperatorNet._init_weights (sfnonet.py:632-640)."""
+    from .layers import trunc_normal_
+    if isinstance(m, (nn.Linear, nn.Conv2d)):
+        trunc_normal_(m.weight, std=0.02)
+        if m.bias is not None:
+            nn.init.constant_(m.bias, 0)
+    elif isinstance(m, nn.LayerNorm):
+        nn.init.constant_(m.bias, 0)
+        nn.init.constant_(m.weight, 1.0)
+
+
+class FourierNeuralOperatorNet(nn.Module):
+    """Mirror of MSFNO/Models/sfno/sfnonet.py:406-686 (the network around the
+    block): encoder MLP → + pos_embed → num_layers blocks (block 0 maps the
+    img_size equiangular grid to the (h, w) Legendre-Gauss grid, the last one
+    maps back) → big-skip concat → decoder MLP.  Same constructor arguments,
+    submodule names and state-dict keys; every stage runs natively (the encoder
+    adds pos_embed in its fc2 epilogue, the decoder consumes the concatenation
+    in place).  ``spectral_transform="fft"`` is out of scope."""
+
+    def __init__(self, device, cfg, spectral_transform="sht", filter_type="non-linear",
+                 img_size=(721, 1440), scale_factor=6, in_chans=73, out_chans=73,
+                 embed_dim_sfno=256, num_layers=12, mlp_mode="distributed", mlp_ratio=2.0,
+                 drop_rate=0.0, drop_path_rate=0.0, num_blocks=8, sparsity_threshold=0.0,
+                 normalization_layer="instance_norm", hard_thresholding_fraction=1.0,
+                 use_complex_kernels=True, big_skip=True, compression=None, rank=128,
+                 complex_network=True, complex_activation="real", spectral_layers=3,
+                 laplace_weighting=False, checkpointing_mlp=False, checkpointing_block=False,
+                 checkpointing_encoder=False, checkpointing_decoder=False, batch_size=1,
+                 **overflow):
+        super().__init__()
+        from functools import partial
+
+        from ..harmonics import InverseRealSHT
+        from .layers import trunc_normal_
+        self.cfg, self.device = cfg, device
+        self.spectral_transform = spectral_transform
+        self.filter_type = filter_type
+        self.img_size = img_size
+        self.scale_factor = scale_factor
+        self.in_chans, self.out_chans = in_chans, out_chans
+        self.embed_dim_sfno = self.num_features = embed_dim_sfno
+        self.num_layers, self.num_blocks = num_layers, num_blocks
+        self.hard_thresholding_fraction = hard_thresholding_fraction
+        self.normalization_layer = normalization_layer
+        self.mlp_mode = mlp_mode
+        self.big_skip = big_skip
+        self.compression, self.rank = compression, rank
+        self.complex_network, self.complex_activation = complex_network, complex_activation
+        self.spectral_layers = spectral_layers
+        self.laplace_weighting = laplace_weighting
+        self.checkpointing_mlp = checkpointing_mlp
+        self.checkpointing_block = checkpointing_block
+        self.checkpointing_encoder = checkpointing_encoder
+        self.checkpointing_decoder = checkpointing_decoder
+        self.batch_size = batch_size
+        self.h = self.img_size[0] // self.scale_factor
+        self.w = self.img_size[1] // self.scale_factor
+        self.pos_drop = nn.Dropout(p=drop_rate) if drop_rate > 0.0 else nn.Identity()
+        self.dpr = [x.item() for x in torch.linspace(0, drop_path_rate, self.num_layers)]
+        if self.normalization_layer == "layer_norm":
+            self.norm_layer0 = partial(nn.LayerNorm, normalized_shape=(img_size[0], img_size[1]),
+                                       eps=1e-6)
+            self.norm_layer1 = partial(nn.LayerNorm, normalized_shape=(self.h, self.w), eps=1e-6)
+        elif self.normalization_layer == "instance_norm":
+            self.norm_layer0 = partial(nn.InstanceNorm2d, num_features=embed_dim_sfno, eps=1e-6,
+                                       affine=True, track_running_stats=False)
+            self.norm_layer1 = self.norm_layer0
+        else:
+            raise NotImplementedError(
+                f"Error, normalization {self.normalization_layer} not implemented.")
+        self.encoder = MLP(in_features=in_chans, hidden_features=embed_dim_sfno,
+                           out_features=embed_dim_sfno, output_bias=False, act_layer=nn.GELU,
+                           drop_rate=0.0, checkpointing_mlp=checkpointing_mlp)
+        self.pos_embed = nn.Parameter(torch.zeros(1, embed_dim_sfno, img_size[0], img_size[1]))
+        modes_lat = int(self.h * self.hard_thresholding_fraction)
+        modes_lon = int((self.w // 2 + 1) * self.hard_thresholding_fraction)
+        if self.spectral_transform == "sht":
+            self.trans_down = RealSHT(*self.img_size, lmax=modes_lat, mmax=modes_lon,
+                                      grid="equiangular").float()
+            self.itrans_up = InverseRealSHT(*self.img_size, lmax=modes_lat, mmax=modes_lon,
+                                            grid="equiangular").float()
+            self.trans = RealSHT(self.h, self.w, lmax=modes_lat, mmax=modes_lon,
+                                 grid="legendre-gauss").float()
+            self.itrans = InverseRealSHT(self.h, self.w, lmax=modes_lat, mmax=modes_lon,
+                                         grid="legendre-gauss").float()
+            sht_rescaling_factor = 1e5  # sfnonet.py:550-555
+            self.trans_down.weights = self.trans_down.weights * sht_rescaling_factor
+            self.itrans_up.pct = self.itrans_up.pct / sht_rescaling_factor
+            self.trans.weights = self.trans.weights * sht_rescaling_factor
+            self.itrans.pct = self.itrans.pct / sht_rescaling_factor
+        elif self.spectral_transform == "fft":
+            raise NotImplementedError("spectral_transform='fft' (RealFFT2) is not on the MI355X path")
+        else:
+            raise ValueError("Unknown spectral transform")
+        self.blocks = nn.ModuleList([self._make_block(i, drop_rate, sparsity_threshold,
+                                                      use_complex_kernels, mlp_ratio)
+                                     for i in range(self.num_layers)])
+        self.decoder = MLP(in_features=embed_dim_sfno + self.big_skip * in_chans,
+                           hidden_features=embed_dim_sfno, out_features=out_chans,
+                           output_bias=False, act_layer=nn.GELU, drop_rate=0.0,
+                           checkpointing_mlp=checkpointing_mlp)
+        trunc_normal_(self.pos_embed, std=0.02)
+        self.apply(_trunc_normal_init)
+
+    def _block_class(self, i):
+        return FourierNeuralOperatorBlock
+
+    def _make_block(self, i, drop_rate, sparsity_threshold, use_complex_kernels, mlp_ratio):
+        first_layer, last_layer = i == 0, i == self.num_layers - 1
+        forward_transform = self.trans_down if first_layer else self.trans
+        inverse_transform = self.itrans_up if last_layer else self.itrans
+        inner_skip = "linear" if 0 < i < self.num_layers - 1 else None
+        outer_skip = "identity" if 0 < i < self.num_layers - 1 else None
+        mlp_mode = self.mlp_mode if not last_layer else "none"
+        if first_layer:
+            norm_layer = (self.norm_layer0, self.norm_layer1)
+        elif last_layer:
+            norm_layer = (self.norm_layer1, self.norm_layer0)
+        else:
+            norm_layer = (self.norm_layer1, self.norm_layer1)
+        return self._block_class(i)(
+            forward_transform, inverse_transform, self.embed_dim_sfno,
+            filter_type=self.filter_type, mlp_ratio=mlp_ratio, drop_rate=drop_rate,
+            drop_path=self.dpr[i], norm_layer=norm_layer, sparsity_threshold=sparsity_threshold,
+            use_complex_kernels=use_complex_kernels, inner_skip=inner_skip,
+            outer_skip=outer_skip, mlp_mode=mlp_mode, compression=self.compression,
+            rank=self.rank, complex_network=self.complex_network,
+            complex_activation=self.complex_activation, spectral_layers=self.spectral_layers,
+            checkpointing_mlp=self.checkpointing_mlp)
+
+    @torch.jit.ignore
+    def no_weight_decay(self):
+        return {"pos_embed", "cls_token"}
+
+    def encode(self, x):
+        """encoder(x) + pos_embed (sfnonet.py:667-674), pos_embed added in fc2's epilogue."""
+        return self.encoder.native_forward(x, addend=self.pos_embed)
+
+    def decode(self, x, residual):
+        """decoder(cat(x, residual)) (sfnonet.py:679-686) without materialising the concat."""
+        if self.big_skip:
+            return self.decoder.native_forward(x, x2=residual)
+        return self.decoder.native_forward(x)
+
+    def forward_features(self, x):
+        x = self.pos_drop(x)
+        for blk in self.blocks:
+            x = blk(x)
+        return x
+
+    def forward(self, x):
+        residual = x
+        x = self.encode(x)
+        x = self.forward_features(x)
+        return self.decode(x, residual)
+
+
+class FourierNeuralOperatorNet_Filmed(FourierNeuralOperatorNet):
+    """Mirror of sfnonet.py:699-860: the last ``film_layers`` blocks (every block
+    with cfg.repeat_film) are FourierNeuralOperatorBlock_Filmed.  The FiLM
+    generator (Film_wrapper: GCN / ViT / MAE over SST fields, :862-) is outside
+    the MI355X hot path: pass ``film_gen`` (any module mapping sst to
+    (B, 2, film_layers, C)) or call forward with the modulation tensor itself as
+    ``sst`` (film_mod[:, 0] = gamma, film_mod[:, 1] = beta, :812)."""
+
+    def __init__(self, device, cfg, mlp_ratio=2.0, drop_rate=0.0, sparsity_threshold=0.0,
+                 use_complex_kernels=True, film_gen=None, **kwargs):
+        self.advanced_logging = kwargs.get("advanced_logging", False)
+        self.film_layers = kwargs["film_layers"]
+        self.depth = kwargs.get("model_depth")
+        self._repeat_film = bool(getattr(cfg, "repeat_film", False))
+        super().__init__(device, cfg, mlp_ratio=mlp_ratio, drop_rate=drop_rate,
+                         sparsity_threshold=sparsity_threshold,
+                         use_complex_kernels=use_complex_kernels, **kwargs)
+        self.film_gen = film_gen
+
+    def _filmed(self, i):
+        return self._repeat_film or i >= self.num_layers - self.film_layers
+
+    def _block_class(self, i):
+        return FourierNeuralOperatorBlock_Filmed if self._filmed(i) else FourierNeuralOperatorBlock
+
+    def forward(self, x, sst, scale=1):
+        film_mod = self.film_gen(sst) if self.film_gen is not None else sst
+        gamma, beta = film_mod[:, 0], film_mod[:, 1]
+        if self.advanced_logging:
+            self.gamma, self.beta = gamma, beta
+        residual = x
+        x = self.pos_drop(self.encode(x))
+        for i, blk in enumerate(self.blocks):
+            if self._filmed(i):
+                film_idx = i - (self.num_layers - self.film_layers)
+                x = blk(x, gamma[:, film_idx], beta[:, film_idx], scale)
+            else:
+                x = blk(x)
+        return self.decode(x, residual)

@@ -212,3 +212,58 @@ def algorithmic_flops(B, C, nlat, nlon, lmax, mmax, cfg: BlockCfg, hidden_factor
     skip = 2 * B * C * C * P if cfg.inner_skip == "linear" else 0
     mlpf = 2 * B * P * (2 * C * hid) if cfg.has_mlp else 0
     return fft + leg + spec + skip + mlpf
+
+
+# --- the network around the block (sfnonet.py:406-686) ----------------------------
+@dataclass
+class NetCfg:
+    img_size: tuple = (721, 1440)
+    scale_factor: int = 6
+    num_layers: int = 12
+    filter_type: str = "non-linear"
+    big_skip: bool = True
+    spectral_layers: int = 3
+    hard_thresholding_fraction: float = 1.0
+
+
+def make_net_transforms(cfg: NetCfg, dtype=torch.float32):
+    """trans_down / itrans_up on the image grid, trans / itrans on the (h, w)
+    Legendre-Gauss grid, all with the x1e5 rescale (sfnonet.py:532-555)."""
+    h, w = cfg.img_size[0] // cfg.scale_factor, cfg.img_size[1] // cfg.scale_factor
+    lmax = int(h * cfg.hard_thresholding_fraction)
+    mmax = int((w // 2 + 1) * cfg.hard_thresholding_fraction)
+    down = RealSHT(*cfg.img_size, lmax=lmax, mmax=mmax, grid="equiangular").to(dtype)
+    up = InverseRealSHT(*cfg.img_size, lmax=lmax, mmax=mmax, grid="equiangular").to(dtype)
+    tr = RealSHT(h, w, lmax=lmax, mmax=mmax, grid="legendre-gauss").to(dtype)
+    itr = InverseRealSHT(h, w, lmax=lmax, mmax=mmax, grid="legendre-gauss").to(dtype)
+    for f in (down, tr):
+        f.weights = f.weights * 1e5
+    for g in (up, itr):
+        g.pct = g.pct / 1e5
+    return down, up, tr, itr
+
+
+def net_forward(p, x, cfg: NetCfg, transforms=None, film=None, scale=1.0):
+    """FourierNeuralOperatorNet.forward (sfnonet.py:662-686); with ``film`` =
+    (gamma, beta) of shape (B, film_layers, C) the last film_layers blocks are
+    FiLM-modulated as in FourierNeuralOperatorNet_Filmed.forward (:837-844)."""
+    down, up, tr, itr = transforms if transforms is not None else make_net_transforms(cfg)
+    residual = x
+    x = mlp(x, p, prefix="encoder.fwd.")
+    x = x + p["pos_embed"]
+    n = cfg.num_layers
+    film_layers = film[0].shape[1] if film is not None else 0
+    for i in range(n):
+        first, last = i == 0, i == n - 1
+        bcfg = BlockCfg(filter_type=cfg.filter_type,
+                        inner_skip="linear" if 0 < i < n - 1 else None,
+                        outer_skip="identity" if 0 < i < n - 1 else None,
+                        has_mlp=not last, spectral_layers=cfg.spectral_layers)
+        bp = {k[len(f"blocks.{i}."):]: v for k, v in p.items() if k.startswith(f"blocks.{i}.")}
+        g = b = None
+        if film is not None and i >= n - film_layers:
+            g, b = film[0][:, i - (n - film_layers)], film[1][:, i - (n - film_layers)]
+        x = block_forward(bp, x, down if first else tr, up if last else itr, bcfg, g, b, scale)
+    if cfg.big_skip:
+        x = torch.cat((x, residual), dim=1)
+    return mlp(x, p, prefix="decoder.fwd.")

@@ -20,7 +20,7 @@ Every other line executed (SpectralFilterLayer, SpectralAttentionS2,
 SpectralConvS2, contractions, ComplexReLU, MLP, InstanceNorm, FiLM, block
 wiring, the ×1e5 rescale recipe) is the reference's own code.
 
-Usage:  python tests/golden/make_golden.py
+Usage:  python tests/golden/make_golden.py [--net]   (--net: only the network fixtures)
 """
 from __future__ import annotations
 
@@ -179,5 +179,48 @@ def main():
                     print("wrote", path, y.shape, float(y.abs().max()))
 
 
+def main_net():
+    """The network around the block (sfnonet.py:406-686): encoder, pos_embed, a
+    4-block stack (block 0 equiangular 33x64 -> Gauss 8x16, block 3 back), big
+    skip, decoder — the reference's own FourierNeuralOperatorNet."""
+    mods = load_reference()
+    sfnonet = mods["sfnonet"]
+    for filter_type in ("non-linear", "linear"):
+        seed = 4321
+        torch.manual_seed(seed)
+        kw = dict(spectral_transform="sht", filter_type=filter_type, img_size=(33, 64),
+                  scale_factor=4, in_chans=5, out_chans=5, embed_dim_sfno=16, num_layers=4,
+                  spectral_layers=3)
+        net = sfnonet.FourierNeuralOperatorNet("cpu", None, **kw)
+        gen = torch.Generator().manual_seed(seed + 1)
+        randomize_(net, gen)
+        with torch.no_grad():  # O(1) outputs: non-trivial pos_embed, unit-gain encoder/decoder
+            net.pos_embed.copy_(0.1 * torch.randn(net.pos_embed.shape, generator=gen))
+            for name, p in net.named_parameters():
+                if name.startswith(("encoder", "decoder")) and name.endswith("weight"):
+                    p.copy_(torch.randn(p.shape, generator=gen) / p.shape[1] ** 0.5)
+        net.eval()
+        x = torch.randn(2, 5, 33, 64, generator=gen)
+        with torch.no_grad():
+            y = net(x)
+        full_sd = net.state_dict()
+        ft = "nl" if filter_type == "non-linear" else "lin"
+        out = {"meta_kind": "net", "meta_filter": filter_type, "meta_nlat": 33, "meta_nlon": 64,
+               "meta_scale_factor": 4, "meta_in_chans": 5, "meta_out_chans": 5, "meta_C": 16,
+               "meta_num_layers": 4, "x": x.numpy(), "y": y.numpy(),
+               "state_dict_keys": np.array(sorted(full_sd.keys()))}
+        for k, v in full_sd.items():
+            if not k.endswith((".weights", ".pct")):
+                out["p__" + k] = v.numpy()
+        path = os.path.join(HERE, "net", f"net_{ft}.npz")
+        os.makedirs(os.path.dirname(path), exist_ok=True)
+        np.savez_compressed(path, **out)
+        print("wrote", path, tuple(y.shape), float(y.abs().max()))
+
+
 if __name__ == "__main__":
-    main()
+    if "--net" in sys.argv:
+        main_net()
+    else:
+        main()
+        main_net()
