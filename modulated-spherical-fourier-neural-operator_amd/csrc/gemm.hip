@@ -503,6 +503,8 @@ static int launch(const GemmParams& p, dim3 grid, hipStream_t s) {
     case EPI_GELU_B | EPI_BIAS | EPI_ADD:
       launch_e<BM, BN, BK, EPI_GELU_B | EPI_BIAS | EPI_ADD>(p, grid, s); break;
     case EPI_ADD: launch_e<BM, BN, BK, EPI_ADD>(p, grid, s); break;
+    case EPI_BIAS | EPI_ADD | EPI_GELU:  // decoder fc1 over the big-skip concatenation
+      launch_e<BM, BN, BK, EPI_BIAS | EPI_ADD | EPI_GELU>(p, grid, s); break;
     default:
       set_error("gemm: unsupported epilogue combination");
       return MSFNO_EUNSUPPORTED;
