@@ -86,6 +86,10 @@ def parse(argv=None):
     ap.add_argument("--cpu-baseline", type=int, default=1, help="time the oracle on CPU (rank 0, N=1)")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--stages", action="store_true", help="print per-stage timings to stderr")
+    ap.add_argument("--workload", default="block", choices=["block", "net"],
+                    help="block: one SFNO-Block forward per field (config 2, the headline); "
+                         "net: one 6 h step of the 12-block FourierNeuralOperatorNet_Filmed "
+                         "(config 3: encoder, blocks on the 120x240 Gauss grid, decoder; 73 ch)")
     ap.add_argument("--parallel", default="replicas", choices=["replicas", "latband"],
                     help="N>1: independent replicas (one field batch per GPU) or one batch of "
                          "batch*N fields latitude-band sharded over the N GPUs (RCCL all-to-all)")
@@ -192,6 +196,61 @@ def cpu_baseline(args, p, cfg):
                       f"{dt:.2f} s/field{note}"}
 
 
+def run_net(args, rank, world, dev, dist, backend):
+    """Config 3: one autoregressive 6 h step of the reference-default network
+    (FourierNeuralOperatorNet_Filmed, sfnonet.py:699-860): 73 -> 256 channels,
+    12 blocks (block 0 721x1440 -> 120x240 Gauss, blocks 1-10 at 120x240 lmax 120,
+    block 11 back to 721x1440), FiLM on the last block, big skip, decoder.
+    Synthetic input and FiLM modulation (the FiLM generator is out of scope)."""
+    from msfno_amd.sfno import FourierNeuralOperatorNet_Filmed
+    torch.manual_seed(1)
+    net = FourierNeuralOperatorNet_Filmed("cpu", None, film_layers=1, advanced_logging=False,
+                                          model_depth=None, img_size=(args.nlat, args.nlon),
+                                          in_chans=73, out_chans=73, embed_dim_sfno=args.C,
+                                          num_layers=12, filter_type=args.filter,
+                                          spectral_layers=3).eval().to(dev)
+    B = args.batch
+    g = torch.Generator(device=dev).manual_seed(1000 * rank)
+    x = torch.randn(B, 73, args.nlat, args.nlon, generator=g, device=dev)
+    film = 0.1 * torch.randn(B, 2, 1, args.C, generator=g, device=dev)
+
+    def barrier():
+        if dist:
+            torch.distributed.barrier()
+
+    with torch.no_grad():
+        for _ in range(args.warmup):
+            y = net(x, film, 1.0)
+        barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            y = net(x, film, 1.0)
+        torch.cuda.synchronize()
+        barrier()
+        elapsed = time.perf_counter() - t0
+    if dist:
+        t = torch.tensor([elapsed], device=dev if backend == "nccl" else "cpu",
+                         dtype=torch.float64)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        elapsed = t.item()
+    assert torch.isfinite(y).all()
+    if rank == 0:
+        print(json.dumps({
+            "metric": "FourierNeuralOperatorNet_Filmed 6h steps/sec (12 blocks, 73 ch, 721x1440)",
+            "value": round(world * B * args.steps / elapsed, 3), "unit": "steps/s",
+            "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(1000.0 * elapsed / args.steps, 3), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+            "data": "synthetic (x~N(0,1), FiLM modulation ~0.1 N(0,1), random-init weights)",
+            "config": {"workload": f"sfno_net12_filmed_{args.nlat}x{args.nlon}_C{args.C}_73ch",
+                       "batch_per_gpu": B, "filter": args.filter,
+                       "parallelism": f"replicas{world}" if world > 1 else "single"}}),
+              flush=True)
+    if dist:
+        torch.distributed.destroy_process_group()
+
+
 def main():
     args = parse()
     rank = int(os.environ.get("RANK", "0"))
@@ -215,6 +274,8 @@ def main():
 
     from msfno_amd import _native as N
 
+    if args.workload == "net":
+        return run_net(args, rank, world, dev, dist, backend)
     blk, p, cfg = build_block(args, dev)
     C = args.C
     band = args.parallel == "latband"
