@@ -220,8 +220,17 @@ __device__ __forceinline__ void stockham_pass_inplace(float2* buf, int H, int Ns
     if (j < nb) {
       const int k = j % Ns;
       const int base = (j / Ns) * Ns * R + k;
+      if ((R % 2) == 0 && Ns == 1) {
+        // first pass: a lane's R outputs are contiguous; 16-B stores halve the
+        // bank conflicts of R strided 8-B stores
 #pragma unroll
-      for (int r = 0; r < R; ++r) buf[base + r * Ns] = v[it][r];
+        for (int r = 0; r < R; r += 2)
+          *reinterpret_cast<float4*>(buf + base + r) =
+              make_float4(v[it][r].x, v[it][r].y, v[it][r + 1].x, v[it][r + 1].y);
+      } else {
+#pragma unroll
+        for (int r = 0; r < R; ++r) buf[base + r * Ns] = v[it][r];
+      }
     }
   }
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
