@@ -90,6 +90,9 @@ def parse(argv=None):
                     help="block: one SFNO-Block forward per field (config 2, the headline); "
                          "net: one 6 h step of the 12-block FourierNeuralOperatorNet_Filmed "
                          "(config 3: encoder, blocks on the 120x240 Gauss grid, decoder; 73 ch)")
+    ap.add_argument("--graph", type=int, default=-1,
+                    help="capture one step in a HIP graph and replay it (default: on for "
+                         "--workload net, off for block)")
     ap.add_argument("--parallel", default="replicas", choices=["replicas", "latband"],
                     help="N>1: independent replicas (one field batch per GPU) or one batch of "
                          "batch*N fields latitude-band sharded over the N GPUs (RCCL all-to-all)")
@@ -218,17 +221,42 @@ def run_net(args, rank, world, dev, dist, backend):
         if dist:
             torch.distributed.barrier()
 
+    use_graph = args.graph != 0
     with torch.no_grad():
-        for _ in range(args.warmup):
+        for _ in range(max(args.warmup, 1)):
             y = net(x, film, 1.0)
+        torch.cuda.synchronize()
+        if use_graph:
+            # one 6 h step as a HIP graph: removes the host cost of ~300 launches and
+            # the per-call module bookkeeping (the 120x240 blocks are launch-bound)
+            graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(graph):
+                y = net(x, film, 1.0)
+            graph.replay()
+            torch.cuda.synchronize()
+
+            def step():
+                graph.replay()
+        else:
+            def step():
+                return net(x, film, 1.0)
+        from msfno_amd import _native as N
+        if args.stages and not use_graph:
+            N.profile_collect()
+            N.profile_enable(True)
         barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for _ in range(args.steps):
-            y = net(x, film, 1.0)
+            step()
         torch.cuda.synchronize()
         barrier()
         elapsed = time.perf_counter() - t0
+        if args.stages and not use_graph and rank == 0:
+            N.profile_enable(False)
+            for k, (ms, c) in sorted(N.profile_collect().items(), key=lambda kv: -kv[1][0]):
+                print(f"  stage {k:18s} {ms / args.steps:8.3f} ms/step x{c // args.steps}",
+                      file=sys.stderr)
     if dist:
         t = torch.tensor([elapsed], device=dev if backend == "nccl" else "cpu",
                          dtype=torch.float64)
@@ -244,7 +272,7 @@ def run_net(args, rank, world, dev, dist, backend):
             "scaling": "weak", "vs_baseline": None, "dtype": "f32",
             "data": "synthetic (x~N(0,1), FiLM modulation ~0.1 N(0,1), random-init weights)",
             "config": {"workload": f"sfno_net12_filmed_{args.nlat}x{args.nlon}_C{args.C}_73ch",
-                       "batch_per_gpu": B, "filter": args.filter,
+                       "batch_per_gpu": B, "filter": args.filter, "hip_graph": use_graph,
                        "parallelism": f"replicas{world}" if world > 1 else "single"}}),
               flush=True)
     if dist:
