@@ -8,5 +8,6 @@ for tensor storage and streams only.
 from . import _native  # noqa: F401
 from . import harmonics  # noqa: F401
 from . import sfno  # noqa: F401
+from . import rollout  # noqa: F401
 
 __version__ = "0.1.0"
