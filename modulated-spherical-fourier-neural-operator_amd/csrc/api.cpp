@@ -217,13 +217,18 @@ int side_ctx(SideCtx** out) {
 // workspace carving
 // ---------------------------------------------------------------------------
 
+// Legendre GEMM tiles (descriptor layout and launch must agree)
+static GemmTile leg_tile(int inverse) {
+  return inverse ? role_tile(ROLE_LEGI, TILE_128x128) : role_tile(ROLE_LEG, TILE_128x64);
+}
+
 int ensure_desc(msfno_sht_plan_s* p, int R, int other_ld, int64_t ldT) {
   // forward: A = Xt slab (R x K), B = table, C = S (ld ldT)
   // inverse: A = S (ld ldT), B = table, C = Yt slab (R x N)
   // symmetric plans: one even-parity and one odd-parity problem per m
   if (p->desc_R == R && p->d_desc) return MSFNO_OK;
   int bm, bn;
-  gemm_tile_dims(role_tile(ROLE_LEG, TILE_128x64), &bm, &bn);
+  gemm_tile_dims(leg_tile(p->inverse), &bm, &bn);
   std::vector<GemmDesc> d;
   int tiles = 0;
   const SpecLayout& L = p->spec;
@@ -346,14 +351,14 @@ int legendre_fwd(msfno_sht_plan_s* f, const float* Xt, float* S, int R, hipStrea
   GemmEpi e;
   e.rowscale = rowscale;
   e.rs_C = C;
-  return gemm_desc(role_tile(ROLE_LEG, TILE_128x64), Xt, f->table, S, f->d_desc, f->ndesc,
+  return gemm_desc(leg_tile(0), Xt, f->table, S, f->d_desc, f->ndesc,
                    f->desc_tiles, e, s);
 }
 
 int legendre_inv(msfno_sht_plan_s* g, const float* S, float* Yt, int R, hipStream_t s) {
   MSFNO_TRY(ensure_desc(g, R, 0, g->spec.ldT));
   GemmEpi e;
-  return gemm_desc(role_tile(ROLE_LEG, TILE_128x64), S, g->table, Yt, g->d_desc, g->ndesc,
+  return gemm_desc(leg_tile(1), S, g->table, Yt, g->d_desc, g->ndesc,
                    g->desc_tiles, e, s);
 }
 

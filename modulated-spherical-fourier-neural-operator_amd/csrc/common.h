@@ -138,7 +138,7 @@ enum GemmTile {
 };
 // GEMM role -> tile (defaults chosen by measurement); MSFNO_TILES
 // ("skip=4,fc1=1,...", values = GemmTile) overrides them for A/B experiments
-enum GemmRole { ROLE_SKIP = 0, ROLE_FC1, ROLE_FC2, ROLE_SPEC, ROLE_LEG, ROLE_COUNT };
+enum GemmRole { ROLE_SKIP = 0, ROLE_FC1, ROLE_FC2, ROLE_SPEC, ROLE_LEG, ROLE_LEGI, ROLE_COUNT };
 GemmTile role_tile(GemmRole r, GemmTile dflt);
 
 // C[M,N] = A[M,K] · B[K,N] (+ epilogue), row-major, fp32 MFMA.

@@ -433,7 +433,7 @@ GemmTile role_tile(GemmRole r, GemmTile dflt) {
   if (!init) {
     for (int& t : table) t = -1;
     if (const char* e = getenv("MSFNO_TILES")) {
-      static const char* names[ROLE_COUNT] = {"skip", "fc1", "fc2", "spec", "leg"};
+      static const char* names[ROLE_COUNT] = {"skip", "fc1", "fc2", "spec", "leg", "legi"};
       std::string spec(e);
       size_t pos = 0;
       while (pos < spec.size()) {
