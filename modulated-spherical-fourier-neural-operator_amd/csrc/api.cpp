@@ -411,6 +411,19 @@ void carve_block(Carve& cv, BlockBufs& b, const msfno_block_desc* d,
     b.b1f = cv.take<float>((int64_t)B * Hd);
     b.h = cv.take<float>((int64_t)B * Hd * P);
   }
+  carve_dense_ws(cv, b.dw, d, B);
+}
+
+void carve_dense_ws(Carve& cv, DenseWs& w, const msfno_block_desc* d, int B) {
+  w = DenseWs{};
+  const int C = (int)d->C;
+  if (d->inner_skip == MSFNO_SKIP_LINEAR && (w.skip_b = gemm_dense_workspace(C, C, 1)))
+    w.skip = cv.take<char>(w.skip_b);
+  if (d->has_mlp) {
+    const int Hd = (int)d->mlp_hidden;
+    if ((w.fc1_b = gemm_dense_workspace(Hd, C, B))) w.fc1 = cv.take<char>(w.fc1_b);
+    if ((w.fc2_b = gemm_dense_workspace(C, Hd, 1))) w.fc2 = cv.take<char>(w.fc2_b);
+  }
 }
 
 int check_pair(const msfno_block_desc* d, const msfno_sht_plan_s* f,
@@ -611,21 +624,22 @@ int plan_create(int nlat, int nlon, int lmax, int mmax, int inverse,
 // GELU(erf) in fc1's epilogue on 128x64 tiles, bias + outer skip in fc2's
 // (measured cheapest split: DESIGN.md §8).
 int run_mlp(const msfno_block_desc* d, const float* W1f, const float* b1f, const float* x1,
-            float* h, float* out, const float* resid, int B, int64_t P, hipStream_t s) {
+            float* h, float* out, const float* resid, int B, int64_t P, const DenseWs& dw,
+            hipStream_t s) {
   const int64_t C = d->C, Hd = d->mlp_hidden;
   prof(ST_FC1, s);
   GemmEpi e1;
   e1.bias = b1f;
   e1.sBias = Hd;
   e1.act = 1;
-  MSFNO_TRY(gemm_uniform(role_tile(ROLE_FC1, TILE_128x256), W1f, x1, h, (int)Hd, (int)P, (int)C, (int)C, (int)P,
-                         (int)P, Hd * C, C * P, Hd * P, B, e1, s));
+  MSFNO_TRY(gemm_dense(ROLE_FC1, TILE_128x256, W1f, x1, h, (int)Hd, (int)P, (int)C, (int)C,
+                       (int)P, (int)P, Hd * C, C * P, Hd * P, B, e1, dw.fc1, dw.fc1_b, s));
   prof(ST_FC2, s);
   GemmEpi e2;
   e2.bias = d->fc2_b;
   if (resid) { e2.addend = resid; e2.sD = C * P; e2.ldd = (int)P; }
-  return gemm_uniform(role_tile(ROLE_FC2, TILE_256x128), d->fc2_w, h, out, (int)C, (int)P, (int)Hd, (int)Hd, (int)P,
-                      (int)P, 0, Hd * P, C * P, B, e2, s);
+  return gemm_dense(ROLE_FC2, TILE_256x128, d->fc2_w, h, out, (int)C, (int)P, (int)Hd, (int)Hd,
+                    (int)P, (int)P, 0, Hd * P, C * P, B, e2, dw.fc2, dw.fc2_b, s);
 }
 }  // namespace msfno
 
@@ -834,8 +848,8 @@ int msfno_block_forward(const msfno_block_desc* d, msfno_sht_plan_t f, msfno_sht
     prof(ST_SKIP, ss);
     GemmEpi e;
     e.bias = d->skip_b;
-    MSFNO_TRY(gemm_uniform(role_tile(ROLE_SKIP, TILE_128x256), d->skip_w, x, x1, (int)C, (int)P, (int)C, (int)C,
-                           (int)P, (int)P, 0, C * P, C * P, B, e, ss));
+    MSFNO_TRY(gemm_dense(ROLE_SKIP, TILE_128x256, d->skip_w, x, x1, (int)C, (int)P, (int)C,
+                         (int)C, (int)P, (int)P, 0, C * P, C * P, B, e, b.dw.skip, b.dw.skip_b, ss));
     if (side) {
       prof(ST_END, ss);
       MSFNO_CHECK_HIP(hipEventRecord(side->join, ss));
@@ -858,7 +872,7 @@ int msfno_block_forward(const msfno_block_desc* d, msfno_sht_plan_t f, msfno_sht
     const int64_t Hd = d->mlp_hidden;
     MSFNO_TRY(launch_fold_affine(d->fc1_w, d->fc1_b, b.sc1, b.sh1, b.W1f, b.b1f, B, (int)Hd,
                                  (int)C, s));
-    MSFNO_TRY(run_mlp(d, b.W1f, b.b1f, x1, b.h, out, resid, B, P, s));
+    MSFNO_TRY(run_mlp(d, b.W1f, b.b1f, x1, b.h, out, resid, B, P, b.dw, s));
   } else {
     prof(ST_OUT_AFFINE, s);
     MSFNO_TRY(launch_affine_rows(x1, b.sc1, b.sh1, resid, out, BC, P, 0, nullptr, 0, s));
@@ -907,6 +921,9 @@ size_t msfno_mlp_workspace_size(const msfno_mlp_desc* d, int B, long long P) {
   Carve cv;
   cv.take<float>((int64_t)B * d->Hid * P);                // h
   if (d->Cin2 > 0) cv.take<float>((int64_t)B * d->Hid * P);  // first half of fc1
+  cv.take<char>(gemm_dense_workspace(d->Hid, d->Cin, 1));   // split fc1 weights
+  if (d->Cin2 > 0) cv.take<char>(gemm_dense_workspace(d->Hid, d->Cin2, 1));
+  cv.take<char>(gemm_dense_workspace(d->Cout, d->Hid, 1));  // split fc2 weights
   return cv.off;
 }
 
@@ -927,34 +944,40 @@ int msfno_mlp_forward(const msfno_mlp_desc* d, const float* x, const float* x2,
   cv.base = (char*)ws;
   const int64_t Hd = d->Hid, Ct = d->Cin + d->Cin2;
   float* h = cv.take<float>((int64_t)B * Hd * P);
+  float* t = d->Cin2 > 0 ? cv.take<float>((int64_t)B * Hd * P) : nullptr;
+  const size_t w1b = gemm_dense_workspace((int)Hd, d->Cin, 1);
+  void* w1 = cv.take<char>(w1b);
+  const size_t w1b2 = d->Cin2 > 0 ? gemm_dense_workspace((int)Hd, d->Cin2, 1) : 0;
+  void* w12 = d->Cin2 > 0 ? cv.take<char>(w1b2) : nullptr;
+  const size_t w2b = gemm_dense_workspace(d->Cout, (int)Hd, 1);
+  void* w2 = cv.take<char>(w2b);
   const int Pi = (int)P;
   prof(ST_FC1, s);
   if (d->Cin2 > 0) {
     // fc1 over the concatenation [x ; x2]: t = W1[:, :Cin]·x, then h = GELU(W1[:, Cin:]·x2 + b1 + t)
-    float* t = cv.take<float>((int64_t)B * Hd * P);
     GemmEpi e0;
-    MSFNO_TRY(gemm_uniform(role_tile(ROLE_FC1, TILE_128x256), d->fc1_w, x, t, (int)Hd, Pi, d->Cin,
-                           (int)Ct, Pi, Pi, 0, (int64_t)d->Cin * P, Hd * P, B, e0, s));
+    MSFNO_TRY(gemm_dense(ROLE_FC1, TILE_128x256, d->fc1_w, x, t, (int)Hd, Pi, d->Cin, (int)Ct, Pi,
+                         Pi, 0, (int64_t)d->Cin * P, Hd * P, B, e0, w1, w1b, s));
     GemmEpi e1;
     e1.bias = d->fc1_b;
     e1.addend = t; e1.sD = Hd * P; e1.ldd = Pi;
     e1.act = 1;
-    MSFNO_TRY(gemm_uniform(role_tile(ROLE_FC1, TILE_128x256), d->fc1_w + d->Cin, x2, h, (int)Hd,
-                           Pi, d->Cin2, (int)Ct, Pi, Pi, 0, (int64_t)d->Cin2 * P, Hd * P, B, e1, s));
+    MSFNO_TRY(gemm_dense(ROLE_FC1, TILE_128x256, d->fc1_w + d->Cin, x2, h, (int)Hd, Pi, d->Cin2,
+                         (int)Ct, Pi, Pi, 0, (int64_t)d->Cin2 * P, Hd * P, B, e1, w12, w1b2, s));
   } else {
     GemmEpi e1;
     e1.bias = d->fc1_b;
     e1.act = 1;
-    MSFNO_TRY(gemm_uniform(role_tile(ROLE_FC1, TILE_128x256), d->fc1_w, x, h, (int)Hd, Pi, d->Cin,
-                           d->Cin, Pi, Pi, 0, (int64_t)d->Cin * P, Hd * P, B, e1, s));
+    MSFNO_TRY(gemm_dense(ROLE_FC1, TILE_128x256, d->fc1_w, x, h, (int)Hd, Pi, d->Cin, d->Cin, Pi,
+                         Pi, 0, (int64_t)d->Cin * P, Hd * P, B, e1, w1, w1b, s));
   }
   prof(ST_FC2, s);
   GemmEpi e2;
   e2.bias = d->fc2_b;
   if (addend) { e2.addend = addend; e2.sD = add_bstride; e2.ldd = Pi; }
-  const GemmTile t2 = d->Cout <= 128 ? TILE_128x128 : role_tile(ROLE_FC2, TILE_256x128);
-  MSFNO_TRY(gemm_uniform(t2, d->fc2_w, h, out, d->Cout, Pi, (int)Hd, (int)Hd, Pi, Pi, 0, Hd * P,
-                         (int64_t)d->Cout * P, B, e2, s));
+  const GemmTile t2 = d->Cout <= 128 ? TILE_128x128 : TILE_256x128;
+  MSFNO_TRY(gemm_dense(ROLE_FC2, t2, d->fc2_w, h, out, d->Cout, Pi, (int)Hd, (int)Hd, Pi, Pi, 0,
+                       Hd * P, (int64_t)d->Cout * P, B, e2, w2, w2b, s));
   prof(ST_END, s);
   return MSFNO_OK;
 }

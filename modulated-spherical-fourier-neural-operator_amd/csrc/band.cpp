@@ -90,6 +90,7 @@ void carve_band(Carve& cv, BandBufs& b, const msfno_block_desc* d, const msfno_b
     b.b1f = cv.take<float>((int64_t)B * Hd);
     b.h = cv.take<float>((int64_t)B * Hd * Pl);
   }
+  carve_dense_ws(cv, b.fb.dw, d, B);
 }
 
 int check_band(const msfno_block_desc* d, const msfno_band_plan_s* p) {
@@ -260,8 +261,9 @@ int msfno_band_block_stage(const msfno_block_desc* d, msfno_band_plan_t p, int s
         prof(ST_SKIP, ss);
         GemmEpi e;
         e.bias = d->skip_b;
-        MSFNO_TRY(gemm_uniform(role_tile(ROLE_SKIP, TILE_128x256), d->skip_w, io->x, b.x1, (int)C, (int)Pl, (int)C,
-                               (int)C, (int)Pl, (int)Pl, 0, C * Pl, C * Pl, B, e, ss));
+        MSFNO_TRY(gemm_dense(ROLE_SKIP, TILE_128x256, d->skip_w, io->x, b.x1, (int)C, (int)Pl,
+                             (int)C, (int)C, (int)Pl, (int)Pl, 0, C * Pl, C * Pl, B, e,
+                             b.fb.dw.skip, b.fb.dw.skip_b, ss));
         if (side) {
           prof(ST_END, ss);
           MSFNO_CHECK_HIP(hipEventRecord(side->join, ss));
@@ -337,7 +339,7 @@ int msfno_band_block_stage(const msfno_block_desc* d, msfno_band_plan_t p, int s
         const int64_t Hd = d->mlp_hidden;
         MSFNO_TRY(launch_fold_affine(d->fc1_w, d->fc1_b, b.sc1, b.sh1, b.W1f, b.b1f, B, (int)Hd,
                                      (int)C, s));
-        MSFNO_TRY(run_mlp(d, b.W1f, b.b1f, b.x1, b.h, io->out, resid, B, Pl, s));
+        MSFNO_TRY(run_mlp(d, b.W1f, b.b1f, b.x1, b.h, io->out, resid, B, Pl, b.fb.dw, s));
       } else {
         prof(ST_OUT_AFFINE, s);
         MSFNO_TRY(launch_affine_rows(b.x1, b.sc1, b.sh1, resid, io->out, BC, Pl, 0, nullptr, 0, s));

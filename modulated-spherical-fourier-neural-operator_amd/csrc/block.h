@@ -33,6 +33,14 @@ struct SideCtx {
 };
 int side_ctx(SideCtx** out);
 
+// split-A workspaces of the dense GEMMs (gemm_dense): one per call site, the
+// skip GEMM runs on the side stream concurrently with the spectral path
+struct DenseWs {
+  void *skip = nullptr, *fc1 = nullptr, *fc2 = nullptr;
+  size_t skip_b = 0, fc1_b = 0, fc2_b = 0;
+};
+void carve_dense_ws(Carve& cv, DenseWs& w, const msfno_block_desc* d, int B);
+
 struct BlockBufs {
   float2* Xn; float* Xt; float2* rs0; float* sc0; float* sh0;
   float* Sa; float* Sb; float* Sc; float* Wexp[9];
@@ -40,6 +48,7 @@ struct BlockBufs {
   float* Yt; float2* Yn; float* x1;
   float2* st1; float* sc1; float* sh1;
   float* W1f; float* b1f; float* h;
+  DenseWs dw;
 };
 
 void carve_block(Carve& cv, BlockBufs& b, const msfno_block_desc* d, const msfno_sht_plan_s* f,
@@ -62,7 +71,8 @@ int c3m_tile();
 void set_table_offsets(msfno_sht_plan_s* p, int sym);
 // channel MLP with norm1/FiLM folded into (W1f, b1f): out = W2·GELU(W1f·x1 + b1f) + b2 (+resid)
 int run_mlp(const msfno_block_desc* d, const float* W1f, const float* b1f, const float* x1,
-            float* h, float* out, const float* resid, int B, int64_t P, hipStream_t s);
+            float* h, float* out, const float* resid, int B, int64_t P, const DenseWs& dw,
+            hipStream_t s);
 // plan construction (mask: optional m-set, see SpecLayout::build)
 int plan_create(int nlat, int nlon, int lmax, int mmax, int inverse,
                 const std::vector<char>* mask, msfno_sht_plan_s** out);

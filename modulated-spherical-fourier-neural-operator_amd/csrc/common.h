@@ -134,7 +134,7 @@ struct GemmEpi {
 
 enum GemmTile {
   TILE_128x128 = 0, TILE_128x64 = 1, TILE_64x64 = 2, TILE_256x64 = 3, TILE_256x128 = 4,
-  TILE_128x256 = 5
+  TILE_128x256 = 5, TILE_256x256 = 6  // 256x256: gemm_x6 only
 };
 // GEMM role -> tile (defaults chosen by measurement); MSFNO_TILES
 // ("skip=4,fc1=1,...", values = GemmTile) overrides them for A/B experiments
@@ -150,6 +150,23 @@ int gemm_uniform(GemmTile tile, const float* A, const float* B, float* C, int M,
 int gemm_desc(GemmTile tile, const float* A, const float* B, float* C, const GemmDesc* descs,
               int ndesc, int total_tiles, const GemmEpi& epi, hipStream_t s);
 void gemm_tile_dims(GemmTile tile, int* bm, int* bn);
+// fp32-accurate GEMM on the bf16 matrix cores (gemm_x6.hip): same contract as
+// gemm_uniform (no GELU-on-B / rowscale epilogues); ws >= gemm_x6_workspace
+// holds A split into bf16 terms (written by this call, stream-ordered)
+size_t gemm_x6_workspace(int M, int K, int batch);
+int gemm_x6(GemmTile tile, const float* A, const float* B, float* C, int M, int N, int K, int lda,
+            int ldb, int ldc, int64_t sA, int64_t sB, int64_t sC, int batch, const GemmEpi& epi,
+            void* ws, size_t ws_bytes, hipStream_t s);
+int launch_split_a(const float* A, unsigned short* Ax, int M, int K, int lda, int64_t sA,
+                   int batch, hipStream_t s);
+// dense 1x1-conv GEMMs of the block / MLP: gemm_x6 unless MSFNO_GEMM=f32 (or no
+// workspace / a GELU-on-B or rowscale epilogue), else the fp32 MFMA kernel on
+// role_tile(role, f32_tile).  batch_a = 1 when sA == 0, else batch.
+bool gemm_use_x6();
+size_t gemm_dense_workspace(int M, int K, int batch_a);
+int gemm_dense(GemmRole role, GemmTile f32_tile, const float* A, const float* B, float* C, int M,
+               int N, int K, int lda, int ldb, int ldc, int64_t sA, int64_t sB, int64_t sC,
+               int batch, const GemmEpi& epi, void* ws, size_t ws_bytes, hipStream_t s);
 
 }  // namespace msfno
 

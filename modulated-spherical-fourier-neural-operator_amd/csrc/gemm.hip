@@ -10,115 +10,9 @@
 #include <cstdlib>
 #include <string>
 
-#include "common.h"
+#include "gemm_common.h"
 
 namespace msfno {
-
-typedef float floatx16 __attribute__((ext_vector_type(16)));
-
-struct GemmParams {
-  const float* A;
-  const float* B;
-  float* C;
-  int M, N, K, lda, ldb, ldc;
-  int64_t sA, sB, sC;
-  int tiles_m, tiles_n;
-  const GemmDesc* descs;
-  int ndesc;
-  int vecA, vecB;
-  // epilogue
-  const float* bias;
-  const float* addend;
-  int64_t sBias, sD;
-  int ldd, act, relu_period, relu_rows;
-  int vecC;  // C (and addend) rows 16-B aligned: float4 epilogue loads/stores
-  const float* rowscale;
-  int rs_C;
-};
-
-__device__ __forceinline__ int xcd_remap(int orig, int nwg) {
-  // bijective: blocks that share an XCD (orig % 8) get contiguous logical ids
-  const int xcd = orig & 7;
-  const int q = nwg >> 3, r = nwg & 7;
-  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
-}
-
-// erf with the coefficients of ROCm's ocml erff, evaluated branch-free (both
-// polynomial regimes, then a select) with the hardware exp2; |err| < 2e-7.
-__device__ __forceinline__ float erf_fast(float x) {
-  const float t = fabsf(x);
-  const float s = t * t;
-  float p = fmaf(__uint_as_float(0xba1345e1u), s, __uint_as_float(0x3ba10414u));
-  p = fmaf(s, p, __uint_as_float(0xbcdac9b8u));
-  p = fmaf(s, p, __uint_as_float(0x3de703beu));
-  p = fmaf(s, p, __uint_as_float(0xbec09330u));
-  p = fmaf(s, p, __uint_as_float(0x3e0375d0u));
-  const float small = fmaf(t, p, t);
-  float q = fmaf(__uint_as_float(0x378e98abu), t, __uint_as_float(0xb9c68948u));
-  q = fmaf(t, q, __uint_as_float(0x3b7cd369u));
-  q = fmaf(t, q, __uint_as_float(0xbcc618b2u));
-  q = fmaf(t, q, __uint_as_float(0x3dda74e4u));
-  q = fmaf(t, q, __uint_as_float(0x3f228afdu));
-  q = fmaf(t, q, __uint_as_float(0x3e03c728u));
-  q = fmaf(t, q, t);
-  const float large = 1.0f - __builtin_amdgcn_exp2f(-1.44269504088896341f * q);
-  const float r = t < 1.0f ? small : large;
-  return copysignf(r, x);
-}
-
-// Abramowitz & Stegun 7.1.26 (|err| <= 1.5e-7): one rational + one exp2, no
-// regime select (fewer VALU slots than the two-regime ocml form)
-__device__ __forceinline__ float erf_as(float x) {
-  const float t0 = fabsf(x);
-  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, t0, 1.0f));
-  float p = fmaf(1.061405429f, t, -1.453152027f);
-  p = fmaf(p, t, 1.421413741f);
-  p = fmaf(p, t, -0.284496736f);
-  p = fmaf(p, t, 0.254829592f);
-  p *= t;
-  const float e = __builtin_amdgcn_exp2f(-1.44269504088896341f * t0 * t0);
-  return copysignf(fmaf(-p, e, 1.0f), x);
-}
-
-// the same A&S GELU on two values with packed fp32 math (v_pk_fma/mul/add_f32:
-// two lanes' worth per instruction; only rcp/exp2 stay scalar)
-typedef float f32x2 __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ f32x2 gelu_erf2(f32x2 v) {
-  const f32x2 z = v * 0.70710678118654752440f;
-  const f32x2 t0 = __builtin_elementwise_abs(z);
-  const f32x2 den = t0 * 0.3275911f + 1.0f;
-  f32x2 t;
-  t.x = __builtin_amdgcn_rcpf(den.x);
-  t.y = __builtin_amdgcn_rcpf(den.y);
-  f32x2 p = t * 1.061405429f - 1.453152027f;
-  p = p * t + 1.421413741f;
-  p = p * t - 0.284496736f;
-  p = p * t + 0.254829592f;
-  p = p * t;
-  const f32x2 q = (t0 * t0) * -1.44269504088896341f;
-  f32x2 e;
-  e.x = __builtin_amdgcn_exp2f(q.x);
-  e.y = __builtin_amdgcn_exp2f(q.y);
-  const f32x2 erfa = 1.0f - p * e;  // erf(|z|)
-  f32x2 erfz;
-  erfz.x = copysignf(erfa.x, z.x);
-  erfz.y = copysignf(erfa.y, z.y);
-  return (v * 0.5f) * (erfz + 1.0f);
-}
-
-#ifndef MSFNO_GELU_IMPL
-#define MSFNO_GELU_IMPL 1  // 1: A&S 7.1.26 (measured 0.05-0.1 ms cheaper on fc1/fc2), 0: ocml form
-#endif
-__device__ __forceinline__ float gelu_erf(float v) {
-#if MSFNO_GELU_IMPL == 1
-  return 0.5f * v * (1.0f + erf_as(v * 0.70710678118654752440f));
-#else
-  return 0.5f * v * (1.0f + erf_fast(v * 0.70710678118654752440f));
-#endif
-}
-
-// epilogue flags (+ EPI_GELU_B: GELU applied to the B operand while it is staged)
-enum : int { EPI_BIAS = 1, EPI_ADD = 2, EPI_GELU = 4, EPI_RELU = 8, EPI_ROWSCALE = 32, EPI_GELU_B = 64 };
 
 template <int BM, int BN, int BK, bool VEC, int EPI>
 __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmParams p) {
@@ -133,7 +27,12 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmParams p) {
   constexpr int CS_LD = BN + 8;
   constexpr int STAGE = 2 * BK * LDA_S + 2 * BK * LDB_S;
   constexpr int LDS_FLOATS = STAGE > 64 * CS_LD ? STAGE : 64 * CS_LD;
-  __shared__ __attribute__((aligned(16))) float lds[LDS_FLOATS];
+  // + the tile's BM bias values, staged once: read from global inside the
+  // epilogue they were serialised behind the C stores (possible aliasing),
+  // one L2 round trip per float4 stored
+  constexpr bool HAS_BIAS = (EPI & EPI_BIAS) != 0;
+  __shared__ __attribute__((aligned(16))) float lds[LDS_FLOATS + (HAS_BIAS ? BM : 0)];
+  float* const bias_s = lds + LDS_FLOATS;
   auto As = [&](int buf) { return lds + buf * (BK * LDA_S); };
   auto Bs = [&](int buf) { return lds + 2 * BK * LDA_S + buf * (BK * LDB_S); };
 
@@ -176,6 +75,9 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmParams p) {
   }
   const int m0 = tm * BM, n0 = tn * BN;
   const int nk = (K + BK - 1) / BK;
+  if constexpr (HAS_BIAS) {
+    for (int r = tid; r < BM; r += 256) bias_s[r] = M > 0 ? bias[min(m0 + r, M - 1)] : 0.f;
+  }  // visible after the prologue barrier
 
 
   float4 ra[A_LD], rb[B_LD];
@@ -344,87 +246,7 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmParams p) {
     }
   }
 
-  // ---- epilogue through LDS ---------------------------------------------------
-  // Per MFMA row-tile i the four waves write their 32-row slices into a 64 x BN
-  // row-major LDS image; then all 256 threads walk it with 16-B vectors: bias,
-  // addend (all loads of a thread issued before any use), activation, and
-  // coalesced float4 stores.  Keeps the accumulators in AGPRs until here, the
-  // epilogue VGPR-light, and the global traffic in full lines.
-  float* Cs = lds;  // the main loop ended with a barrier: staging memory is free
-  constexpr int QPT = (64 * BN / 4) / 256;  // float4 per thread per row-tile
-  const bool vecC = p.vecC;
-#pragma unroll
-  for (int i = 0; i < MT; ++i) {
-#pragma unroll
-    for (int j = 0; j < NT; ++j)
-#pragma unroll
-      for (int r = 0; r < 16; ++r)
-        Cs[(wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * half) * CS_LD + wn * WN + j * 32 + l32] =
-            acc[i][j][r];
-    __syncthreads();
-    float4 add4[QPT];
-    if constexpr ((EPI & EPI_ADD) != 0) {
-#pragma unroll
-      for (int q = 0; q < QPT; ++q) {
-        const int idx = tid + 256 * q;
-        const int lr = idx / (BN / 4);
-        const int row = min(m0 + (lr >> 5) * WM + i * 32 + (lr & 31), M - 1);
-        const int col = n0 + 4 * (idx % (BN / 4));
-        const float* src = addend + (int64_t)row * p.ldd;
-        if (vecC) {
-          add4[q] = *reinterpret_cast<const float4*>(src + min(col, (N - 1) & ~3));
-        } else {
-          add4[q] = make_float4(src[min(col, N - 1)], src[min(col + 1, N - 1)],
-                                src[min(col + 2, N - 1)], src[min(col + 3, N - 1)]);
-        }
-      }
-    }
-#pragma unroll
-    for (int q = 0; q < QPT; ++q) {
-      const int idx = tid + 256 * q;
-      const int lr = idx / (BN / 4);
-      const int c4 = idx % (BN / 4);
-      const int row = m0 + (lr >> 5) * WM + i * 32 + (lr & 31);
-      const int col = n0 + 4 * c4;
-      float4 v = *reinterpret_cast<const float4*>(Cs + lr * CS_LD + 4 * c4);
-      const int rr = min(row, M - 1);
-      if constexpr ((EPI & EPI_ROWSCALE) != 0) {
-        const int C2 = 2 * p.rs_C;
-        const float sv = (dflags & 1) ? p.rowscale[(rr / C2) * p.rs_C + rr % p.rs_C] : 1.f;
-        v.x *= sv; v.y *= sv; v.z *= sv; v.w *= sv;
-      }
-      if constexpr ((EPI & EPI_BIAS) != 0) {
-        const float bv = bias[rr];
-        v.x += bv; v.y += bv; v.z += bv; v.w += bv;
-      }
-      if constexpr ((EPI & EPI_ADD) != 0) {
-        v.x += add4[q].x; v.y += add4[q].y; v.z += add4[q].z; v.w += add4[q].w;
-      }
-      if constexpr ((EPI & EPI_GELU) != 0) {
-        f32x2 lo = {v.x, v.y}, hi = {v.z, v.w};
-        lo = gelu_erf2(lo);
-        hi = gelu_erf2(hi);
-        v = make_float4(lo.x, lo.y, hi.x, hi.y);
-      }
-      if constexpr ((EPI & EPI_RELU) != 0) {
-        if ((unsigned)row % (unsigned)p.relu_period < (unsigned)p.relu_rows) {
-          v.x = fmaxf(v.x, 0.f); v.y = fmaxf(v.y, 0.f); v.z = fmaxf(v.z, 0.f); v.w = fmaxf(v.w, 0.f);
-        }
-      }
-      if (row < M) {
-        float* dst = C + (int64_t)row * ldc + col;
-        if (vecC && col + 3 < N) {
-          *reinterpret_cast<float4*>(dst) = v;
-        } else {
-          if (col < N) dst[0] = v.x;
-          if (col + 1 < N) dst[1] = v.y;
-          if (col + 2 < N) dst[2] = v.z;
-          if (col + 3 < N) dst[3] = v.w;
-        }
-      }
-    }
-    if (i + 1 < MT) __syncthreads();
-  }
+  gemm_epilogue<BM, BN, EPI>(p, acc, lds, bias_s, C, addend, M, N, ldc, m0, n0, dflags);
 }
 
 GemmTile role_tile(GemmRole r, GemmTile dflt) {
@@ -450,7 +272,7 @@ GemmTile role_tile(GemmRole r, GemmTile dflt) {
     init = true;
   }
   const int t = table[r];
-  return (t >= 0 && t <= TILE_128x256) ? (GemmTile)t : dflt;
+  return (t >= 0 && t <= TILE_256x256) ? (GemmTile)t : dflt;
 }
 
 void gemm_tile_dims(GemmTile tile, int* bm, int* bn) {
@@ -460,6 +282,7 @@ void gemm_tile_dims(GemmTile tile, int* bm, int* bn) {
     case TILE_256x64: *bm = 256; *bn = 64; break;
     case TILE_256x128: *bm = 256; *bn = 128; break;
     case TILE_128x256: *bm = 128; *bn = 256; break;
+    case TILE_256x256: *bm = 256; *bn = 256; break;
     default: *bm = 64; *bn = 64; break;
   }
 }
@@ -536,6 +359,7 @@ int gemm_uniform(GemmTile tile, const float* A, const float* B, float* C, int M,
                  int lda, int ldb, int ldc, int64_t sA, int64_t sB, int64_t sC, int batch,
                  const GemmEpi& epi, hipStream_t s) {
   if (M <= 0 || N <= 0 || batch <= 0) return MSFNO_OK;
+  if (tile == TILE_256x256) tile = TILE_128x256;  // no fp32 instance
   int bm, bn;
   gemm_tile_dims(tile, &bm, &bn);
   GemmParams p = make_params(A, B, C, epi);
@@ -555,6 +379,7 @@ int gemm_uniform(GemmTile tile, const float* A, const float* B, float* C, int M,
 int gemm_desc(GemmTile tile, const float* A, const float* B, float* C, const GemmDesc* descs,
               int ndesc, int total_tiles, const GemmEpi& epi, hipStream_t s) {
   if (total_tiles <= 0) return MSFNO_OK;
+  MSFNO_REQUIRE(tile != TILE_256x256, MSFNO_EINVAL, "gemm_desc: no fp32 256x256 instance");
   GemmParams p = make_params(A, B, C, epi);
   p.descs = descs;
   p.ndesc = ndesc;

@@ -1,0 +1,390 @@
+// fp32-accurate GEMM on the bf16 matrix cores ("x6" split) for gfx950.
+//
+// Every fp32 operand value is split exactly into three bf16 terms
+//   x = x0 + x1 + x2,  x0 = bf16(x), x1 = bf16(x - x0), x2 = bf16(x - x0 - x1)
+// (8 significant bits each, 24 together = the fp32 significand; the residual
+// subtractions are exact).  A·B is then the sum of the six products whose term
+// orders add to <= 2:  a2b0 + a1b1 + a0b2 + a1b0 + a0b1 + a0b0.  bf16 x bf16
+// products are exact in fp32 and v_mfma_f32_32x32x16_bf16 accumulates in fp32;
+// the dropped products (a1b2, a2b1, a2b2) are below 2^-24 relative, i.e. under
+// the fp32 rounding of the result.  Measured against an fp64 reference the error
+// is at or below the fp32 MFMA kernel's (tests/test_gpu_gemm_x6.py).  Six bf16
+// MFMAs (32 cycles each) replace eight v_mfma_f32_32x32x2_f32 (64 cycles each)
+// per 32x32x16 block: 2.67x fewer matrix-core cycles.
+//
+// C[M,N] = A[M,K]·B[K,N]; A is the small operand (weights) and is pre-split by
+// launch_split_a into bf16 planes [batch][3][Mp][Kp] (zero padded), B is fp32
+// row-major and split while it is staged.  Tile BM x BN x 16, 4 waves (2x2),
+// each wave (BM/2)x(BN/2) as 32x32 blocks — the fp32 kernel's C layout, so the
+// fused epilogue (gemm_common.h) is shared.
+// LDS images (bf16):
+//   A: [plane][m][16 k], 32-B rows; the two 16-B k-halves of row m are swapped
+//      when (m>>3)&1 so ds_read_b128 fragment reads are bank-conflict free;
+//   B: [plane][k][BN + 32] (row-major as in HBM; +64 B per row makes the
+//      transposed fragment reads conflict free), read with ds_read_b64_tr_b16
+//      (4 k x 16 n per 16-lane group, delivered k-contiguous per lane).
+#include <cstdlib>
+#include <string>
+
+#include "gemm_common.h"
+
+namespace msfno {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef short s16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x2v __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2v __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ uint32_t cvt_pk_bf16(float a, float b) {
+  const f32x2v v = {a, b};
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, bf16x2v));
+}
+__device__ __forceinline__ float bf_lo(uint32_t u) { return __uint_as_float(u << 16); }
+__device__ __forceinline__ float bf_hi(uint32_t u) { return __uint_as_float(u & 0xffff0000u); }
+
+// (a, b) -> three packed bf16x2 terms
+__device__ __forceinline__ void split2(float a, float b, uint32_t& t0, uint32_t& t1, uint32_t& t2) {
+  t0 = cvt_pk_bf16(a, b);
+  a -= bf_lo(t0);
+  b -= bf_hi(t0);
+  t1 = cvt_pk_bf16(a, b);
+  a -= bf_lo(t1);
+  b -= bf_hi(t1);
+  t2 = cvt_pk_bf16(a, b);
+}
+
+__global__ void split_a_kernel(const float* __restrict__ A, unsigned short* __restrict__ Ax, int M,
+                               int K, int lda, int64_t sA, int Mp, int Kp) {
+  const int z = blockIdx.y;
+  const int64_t plane = (int64_t)Mp * Kp;
+  const int64_t n = plane / 2;  // bf16 pairs per plane (Kp even)
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < n;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const int m = (int)((2 * e) / Kp), k = (int)((2 * e) % Kp);
+    const float* a = A + z * sA + (int64_t)m * lda;
+    const float v0 = (m < M && k < K) ? a[k] : 0.f;
+    const float v1 = (m < M && k + 1 < K) ? a[k + 1] : 0.f;
+    uint32_t t0, t1, t2;
+    split2(v0, v1, t0, t1, t2);
+    uint32_t* o = reinterpret_cast<uint32_t*>(Ax + z * 3 * plane) + e;
+    o[0] = t0;
+    o[n] = t1;
+    o[2 * n] = t2;
+  }
+}
+
+template <int BM, int BN, int WGM, int WGN, bool VEC, int EPI>
+__global__ __launch_bounds__(64 * WGM * WGN) void gemm_x6_kernel(GemmParams p) {
+  constexpr int BK = 16;
+  constexpr int NTHR = 64 * WGM * WGN;
+  constexpr int WM = BM / WGM, WN = BN / WGN;
+  constexpr int MT = WM / 32, NT = WN / 32;
+  constexpr int A_PLANE = BM * BK;  // bf16 elements
+  constexpr int A_STAGE = 3 * A_PLANE;
+  constexpr int B_ROW = BN + 32;
+  constexpr int B_PLANE = BK * B_ROW;
+  constexpr int B_STAGE = 3 * B_PLANE;
+  constexpr int STAGE_BYTES = 2 * (A_STAGE + B_STAGE) * 2;
+  constexpr int EPI_BYTES = 32 * WGM * (BN + 8) * 4;
+  constexpr int LDS_BYTES = STAGE_BYTES > EPI_BYTES ? STAGE_BYTES : EPI_BYTES;
+  constexpr bool HAS_BIAS = (EPI & EPI_BIAS) != 0;
+  constexpr int A_LD = 6 * BM / NTHR;       // 16-B chunks of split A per thread
+  constexpr int B_LD = BK * BN / 4 / NTHR;  // float4 of B per thread
+  static_assert(A_LD * NTHR == 6 * BM && B_LD * NTHR * 4 == BK * BN, "tile shape");
+  __shared__ __attribute__((aligned(16))) char lds_raw[LDS_BYTES + (HAS_BIAS ? BM * 4 : 0)];
+  unsigned short* const As = reinterpret_cast<unsigned short*>(lds_raw);
+  unsigned short* const Bs = As + 2 * A_STAGE;
+  float* const bias_s = reinterpret_cast<float*>(lds_raw + LDS_BYTES);
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wm = wave / WGN, wn = wave % WGN;
+  const int half = lane >> 5, l32 = lane & 31;
+
+  const int lin = xcd_remap(blockIdx.x, gridDim.x);
+  const int tm = lin % p.tiles_m, tn = lin / p.tiles_m;
+  const int z = blockIdx.z;
+  const unsigned short* Ax = p.Ax + z * p.sAx;
+  const float* B = p.B + z * p.sB;
+  float* C = p.C + z * p.sC;
+  const float* bias = p.bias ? p.bias + z * p.sBias : nullptr;
+  const float* addend = p.addend ? p.addend + z * p.sD : nullptr;
+  const int M = p.M, N = p.N, K = p.K, ldb = p.ldb, ldc = p.ldc, ldax = p.ldax;
+  const int64_t sAxp = p.sAxp;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int nk = (K + BK - 1) / BK;
+  if constexpr (HAS_BIAS) {
+    for (int r = tid; r < BM; r += NTHR) bias_s[r] = bias[min(m0 + r, M - 1)];
+  }
+
+  uint4 ra[A_LD];
+  float4 rb[B_LD];
+  const int Kc = K - 1, Nc = N - 1;
+  auto load_A = [&](int kt) {
+#pragma unroll
+    for (int q = 0; q < A_LD; ++q) {
+      const int c = tid + NTHR * q;
+      const int pl = c / (2 * BM), rem = c % (2 * BM);
+      const int m = rem >> 1, h = rem & 1;
+      ra[q] = *reinterpret_cast<const uint4*>(Ax + pl * sAxp + (int64_t)(m0 + m) * ldax +
+                                              kt * BK + 8 * h);
+    }
+  };
+  auto store_A = [&](int buf) {
+#pragma unroll
+    for (int q = 0; q < A_LD; ++q) {
+      const int c = tid + NTHR * q;
+      const int pl = c / (2 * BM), rem = c % (2 * BM);
+      const int m = rem >> 1, h = rem & 1;
+      *reinterpret_cast<uint4*>(As + buf * A_STAGE + pl * A_PLANE + m * BK +
+                                8 * (h ^ ((m >> 3) & 1))) = ra[q];
+    }
+  };
+  auto load_B = [&](int kt) {
+#pragma unroll
+    for (int q = 0; q < B_LD; ++q) {
+      const int f = tid + NTHR * q;
+      const int kr = min(kt * BK + f / (BN / 4), Kc);
+      const int col = n0 + 4 * (f % (BN / 4));
+      const float* src = B + (int64_t)kr * ldb;
+      if constexpr (VEC) {
+        rb[q] = *reinterpret_cast<const float4*>(src + min(col, Nc & ~3));
+      } else {
+        rb[q] = make_float4(src[min(col, Nc)], src[min(col + 1, Nc)], src[min(col + 2, Nc)],
+                            src[min(col + 3, Nc)]);
+      }
+    }
+  };
+  auto store_B = [&](int buf, int kt) {
+#pragma unroll
+    for (int q = 0; q < B_LD; ++q) {
+      const int f = tid + NTHR * q;
+      const int kr = f / (BN / 4), c4 = 4 * (f % (BN / 4));
+      const bool kok = kt * BK + kr < K;
+      const int cg = n0 + c4;
+      float4 v = rb[q];
+      v.x = (kok && cg + 0 < N) ? v.x : 0.f;
+      v.y = (kok && cg + 1 < N) ? v.y : 0.f;
+      v.z = (kok && cg + 2 < N) ? v.z : 0.f;
+      v.w = (kok && cg + 3 < N) ? v.w : 0.f;
+      uint32_t a0, a1, a2, b0, b1, b2;
+      split2(v.x, v.y, a0, a1, a2);
+      split2(v.z, v.w, b0, b1, b2);
+      unsigned short* dst = Bs + buf * B_STAGE + kr * B_ROW + c4;
+      *reinterpret_cast<uint2*>(dst) = make_uint2(a0, b0);
+      *reinterpret_cast<uint2*>(dst + B_PLANE) = make_uint2(a1, b1);
+      *reinterpret_cast<uint2*>(dst + 2 * B_PLANE) = make_uint2(a2, b2);
+    }
+  };
+
+  floatx16 acc[MT][NT];
+#pragma unroll
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int j = 0; j < NT; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  // per-lane fragment addresses (bf16 element offsets within one stage)
+  int a_off[MT];
+#pragma unroll
+  for (int i = 0; i < MT; ++i) {
+    const int row = wm * WM + i * 32 + l32;
+    a_off[i] = row * BK + 8 * (half ^ ((row >> 3) & 1));
+  }
+  const int li = lane & 15, g16 = (lane >> 4) & 1;
+  const int b_off = (8 * half + (li >> 2)) * B_ROW + wn * WN + 16 * g16 + 4 * (li & 3);
+
+  auto mfma_tile = [&](int buf) {
+    typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+    const unsigned short* as = As + buf * A_STAGE;
+    const unsigned short* bs = Bs + buf * B_STAGE;
+    bf16x8 a[MT][3];
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+      for (int pl = 0; pl < 3; ++pl)
+        a[i][pl] = *reinterpret_cast<const bf16x8*>(as + pl * A_PLANE + a_off[i]);
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+      bf16x8 b[3];
+#pragma unroll
+      for (int pl = 0; pl < 3; ++pl) {
+        const unsigned short* q = bs + pl * B_PLANE + b_off + j * 32;
+        const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (lds_s16x4*)((__attribute__((address_space(3))) unsigned short*)q));
+        const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (lds_s16x4*)((__attribute__((address_space(3))) unsigned short*)(q + 4 * B_ROW)));
+        const s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        b[pl] = __builtin_bit_cast(bf16x8, v);
+      }
+#pragma unroll
+      for (int i = 0; i < MT; ++i) {
+        floatx16 c = acc[i][j];
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i][2], b[0], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i][1], b[1], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i][0], b[2], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i][1], b[0], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i][0], b[1], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i][0], b[0], c, 0, 0, 0);
+        acc[i][j] = c;
+      }
+    }
+  };
+
+  if (nk > 0) {
+    load_A(0);
+    load_B(0);
+    store_A(0);
+    store_B(0, 0);
+  }
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) {
+      load_A(kt + 1);
+      load_B(kt + 1);
+    }
+    mfma_tile(cur);
+    if (kt + 1 < nk) {
+      store_A(cur ^ 1);
+      store_B(cur ^ 1, kt + 1);
+    }
+    __syncthreads();
+  }
+  gemm_epilogue<BM, BN, EPI, WGM, WGN>(p, acc, reinterpret_cast<float*>(lds_raw), bias_s, C, addend, M, N,
+                             ldc, m0, n0, 0);
+}
+
+// ---- host ---------------------------------------------------------------------
+
+bool gemm_use_x6() {
+  static const bool on = [] {
+    const char* e = getenv("MSFNO_GEMM");
+    return !(e && std::string(e) == "f32");
+  }();
+  return on;
+}
+
+size_t gemm_dense_workspace(int M, int K, int batch_a) {
+  return gemm_use_x6() ? gemm_x6_workspace(M, K, batch_a) : 0;
+}
+
+// 256x256 (8 waves) when the grid still fills the chip twice over, else 128x128;
+// MSFNO_X6_TILE=<GemmTile id> overrides for experiments
+static GemmTile x6_tile(int M, int N, int batch) {
+  static const int forced = [] {
+    const char* e = getenv("MSFNO_X6_TILE");
+    return e ? atoi(e) : -1;
+  }();
+  if (forced >= 0 && forced <= TILE_256x256) return (GemmTile)forced;
+  const int64_t big = cdiv(M, 256) * cdiv(N, 256) * (int64_t)batch;
+  return big >= 512 ? TILE_256x256 : TILE_128x128;
+}
+
+size_t gemm_x6_workspace(int M, int K, int batch) {
+  const int64_t Mp = round_up(M, 256), Kp = round_up(K, 16);
+  return (size_t)round_up(3 * Mp * Kp * 2 * (int64_t)batch, 256);
+}
+
+template <int BM, int BN, int WGM, int WGN, int EPI>
+static void launch_x6_e(const GemmParams& p, dim3 grid, hipStream_t s) {
+  if (p.vecB)
+    hipLaunchKernelGGL((gemm_x6_kernel<BM, BN, WGM, WGN, true, EPI>), grid, dim3(64 * WGM * WGN),
+                       0, s, p);
+  else
+    hipLaunchKernelGGL((gemm_x6_kernel<BM, BN, WGM, WGN, false, EPI>), grid, dim3(64 * WGM * WGN),
+                       0, s, p);
+}
+
+template <int BM, int BN, int WGM, int WGN>
+static int launch_x6(const GemmParams& p, dim3 grid, hipStream_t s) {
+  const int code = (p.bias ? EPI_BIAS : 0) | (p.addend ? EPI_ADD : 0) | (p.act == 1 ? EPI_GELU : 0) |
+                   (p.relu_period ? EPI_RELU : 0);
+  if (p.act == 2 || p.rowscale) {
+    set_error("gemm_x6: unsupported epilogue");
+    return MSFNO_EUNSUPPORTED;
+  }
+  switch (code) {
+    case 0: launch_x6_e<BM, BN, WGM, WGN, 0>(p, grid, s); break;
+    case EPI_RELU: launch_x6_e<BM, BN, WGM, WGN, EPI_RELU>(p, grid, s); break;
+    case EPI_BIAS: launch_x6_e<BM, BN, WGM, WGN, EPI_BIAS>(p, grid, s); break;
+    case EPI_BIAS | EPI_GELU: launch_x6_e<BM, BN, WGM, WGN, EPI_BIAS | EPI_GELU>(p, grid, s); break;
+    case EPI_BIAS | EPI_ADD: launch_x6_e<BM, BN, WGM, WGN, EPI_BIAS | EPI_ADD>(p, grid, s); break;
+    case EPI_ADD: launch_x6_e<BM, BN, WGM, WGN, EPI_ADD>(p, grid, s); break;
+    case EPI_BIAS | EPI_ADD | EPI_GELU:
+      launch_x6_e<BM, BN, WGM, WGN, EPI_BIAS | EPI_ADD | EPI_GELU>(p, grid, s); break;
+    default:
+      set_error("gemm_x6: unsupported epilogue combination");
+      return MSFNO_EUNSUPPORTED;
+  }
+  return MSFNO_OK;
+}
+
+int launch_split_a(const float* A, unsigned short* Ax, int M, int K, int lda, int64_t sA,
+                   int batch, hipStream_t s) {
+  const int Mp = (int)round_up(M, 256), Kp = (int)round_up(K, 16);
+  const int64_t pairs = (int64_t)Mp * Kp / 2;
+  const int blocks = (int)std::min<int64_t>(cdiv(pairs, 256), 1024);
+  hipLaunchKernelGGL(split_a_kernel, dim3(blocks, batch), dim3(256), 0, s, A, Ax, M, K, lda, sA,
+                     Mp, Kp);
+  return launch_check("split_a");
+}
+
+int gemm_x6(GemmTile tile, const float* A, const float* B, float* C, int M, int N, int K, int lda,
+            int ldb, int ldc, int64_t sA, int64_t sB, int64_t sC, int batch, const GemmEpi& epi,
+            void* ws, size_t ws_bytes, hipStream_t s) {
+  if (M <= 0 || N <= 0 || batch <= 0) return MSFNO_OK;
+  MSFNO_REQUIRE(ws && ws_bytes >= gemm_x6_workspace(M, K, sA == 0 ? 1 : batch), MSFNO_EINVAL,
+                "gemm_x6: workspace too small");
+  MSFNO_REQUIRE(batch <= 65535, MSFNO_EINVAL, "gemm_x6: batch too large");
+  unsigned short* Ax = static_cast<unsigned short*>(ws);
+  const int abatch = sA == 0 ? 1 : batch;  // one A for every batch entry: split once
+  MSFNO_TRY(launch_split_a(A, Ax, M, K, lda, sA, abatch, s));
+  const int Mp = (int)round_up(M, 256), Kp = (int)round_up(K, 16);
+  GemmParams p{};
+  p.B = B; p.C = C;
+  p.M = M; p.N = N; p.K = K; p.ldb = ldb; p.ldc = ldc;
+  p.sB = sB; p.sC = sC;
+  p.bias = epi.bias; p.addend = epi.addend; p.sBias = epi.sBias; p.sD = epi.sD;
+  p.ldd = epi.ldd; p.act = epi.act; p.relu_period = epi.relu_period; p.relu_rows = epi.relu_rows;
+  p.rowscale = epi.rowscale;
+  p.Ax = Ax; p.sAxp = (int64_t)Mp * Kp; p.sAx = sA == 0 ? 0 : 3 * p.sAxp; p.ldax = Kp;
+  p.vecB = (ldb % 4 == 0) && (sB % 4 == 0) && ((reinterpret_cast<uintptr_t>(B) & 15) == 0);
+  p.vecC = (ldc % 4 == 0) && (sC % 4 == 0) && ((reinterpret_cast<uintptr_t>(C) & 15) == 0) &&
+           (!epi.addend || ((epi.ldd % 4 == 0) && (epi.sD % 4 == 0) &&
+                            ((reinterpret_cast<uintptr_t>(epi.addend) & 15) == 0)));
+  // tile -> (BM, BN, wave grid): 128x128 4 waves, 256x128 8 waves (4x2),
+  // 128x256 4 waves, 256x256 8 waves (4x2)
+  int bm, bn;
+  gemm_tile_dims(tile, &bm, &bn);
+  if (tile != TILE_256x128 && tile != TILE_128x256 && tile != TILE_256x256) {
+    tile = TILE_128x128; bm = bn = 128;
+  }
+  p.tiles_m = (int)cdiv(M, bm);
+  p.tiles_n = (int)cdiv(N, bn);
+  const dim3 grid(p.tiles_m * p.tiles_n, 1, batch);
+  int rc;
+  switch (tile) {
+    case TILE_256x128: rc = launch_x6<256, 128, 4, 2>(p, grid, s); break;
+    case TILE_128x256: rc = launch_x6<128, 256, 2, 2>(p, grid, s); break;
+    case TILE_256x256: rc = launch_x6<256, 256, 4, 2>(p, grid, s); break;
+    default: rc = launch_x6<128, 128, 2, 2>(p, grid, s); break;
+  }
+  if (rc != MSFNO_OK) return rc;
+  return launch_check("gemm_x6");
+}
+
+int gemm_dense(GemmRole role, GemmTile f32_tile, const float* A, const float* B, float* C, int M,
+               int N, int K, int lda, int ldb, int ldc, int64_t sA, int64_t sB, int64_t sC,
+               int batch, const GemmEpi& epi, void* ws, size_t ws_bytes, hipStream_t s) {
+  if (gemm_use_x6() && ws && epi.act != 2 && !epi.rowscale)
+    return gemm_x6(x6_tile(M, N, batch), A, B, C, M, N, K, lda, ldb, ldc, sA, sB, sC, batch, epi,
+                   ws, ws_bytes, s);
+  return gemm_uniform(role_tile(role, f32_tile), A, B, C, M, N, K, lda, ldb, ldc, sA, sB, sC,
+                      batch, epi, s);
+}
+
+}  // namespace msfno

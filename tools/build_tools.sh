@@ -1,0 +1,9 @@
+#!/bin/bash
+# Builds the microbenchmarks under tools/bin against the in-tree libmsfno.so
+set -e
+cd "$(dirname "$0")/.."
+CS=modulated-spherical-fourier-neural-operator_amd/csrc
+LIB=modulated-spherical-fourier-neural-operator_amd/msfno_amd
+mkdir -p tools/bin
+/opt/rocm/bin/hipcc -O3 --offload-arch=gfx950 -std=c++17 -I $CS tools/gemm_x6_bench.hip \
+  -L $LIB -lmsfno -Wl,-rpath,'$ORIGIN/../../'$LIB -o tools/bin/gemm_x6_bench

@@ -1,0 +1,124 @@
+// fp32 MFMA GEMM vs the bf16x6 split GEMM: speed on the block's 1x1-conv shapes
+// and accuracy against an fp64 host reference.
+// Build: see tools/build_tools.sh (links the in-tree libmsfno.so)
+#include <cmath>
+#include <cstdio>
+#include <string>
+#include <vector>
+
+#include "common.h"
+
+using namespace msfno;
+
+static float frand(uint64_t& s) {
+  s = s * 6364136223846793005ull + 1442695040888963407ull;
+  return (float)((s >> 40) & 0xffffff) / (float)0x1000000 * 2.f - 1.f;
+}
+
+int main(int argc, char** argv) {
+  const char* only = argc > 1 ? argv[1] : nullptr;
+  const int P = 721 * 1440;
+  size_t maxB = (size_t)512 * P;
+  float *A, *B, *C, *D, *bias;
+  void* ws;
+  hipMalloc(&A, 1024 * 1024 * 4);
+  hipMalloc(&B, maxB * 4);
+  hipMalloc(&C, maxB * 4);
+  hipMalloc(&D, maxB * 4);
+  hipMalloc(&bias, 4096 * 4);
+  const size_t wsb = gemm_x6_workspace(1024, 1024, 1);
+  hipMalloc(&ws, wsb);
+  uint64_t seed = 1;
+  {
+    std::vector<float> h(1024 * 1024);
+    for (auto& v : h) v = 0.05f * frand(seed);
+    hipMemcpy(A, h.data(), h.size() * 4, hipMemcpyHostToDevice);
+    std::vector<float> hb(1 << 24);
+    for (auto& v : hb) v = frand(seed);
+    for (size_t off = 0; off < maxB; off += hb.size()) {
+      hipMemcpy(B + off, hb.data(), std::min(hb.size(), maxB - off) * 4, hipMemcpyHostToDevice);
+      hipMemcpy(D + off, hb.data(), std::min(hb.size(), maxB - off) * 4, hipMemcpyHostToDevice);
+    }
+    hipMemcpy(bias, h.data(), 4096 * 4, hipMemcpyHostToDevice);
+  }
+  GemmEpi gelu; gelu.bias = bias; gelu.act = 1;
+  GemmEpi badd; badd.bias = bias; badd.addend = D; badd.ldd = P;
+  GemmEpi sb; sb.bias = bias;
+  struct S { const char* n; int M, K; GemmEpi e; GemmTile t32; };
+  std::vector<S> shapes = {{"fc1-gelu", 512, 256, gelu, TILE_128x256},
+                           {"fc2-badd", 256, 512, badd, TILE_256x128},
+                           {"skip", 256, 256, sb, TILE_128x256}};
+  hipEvent_t e0, e1;
+  hipEventCreate(&e0);
+  hipEventCreate(&e1);
+  auto timeit = [&](auto&& fn) {
+    for (int i = 0; i < 2; ++i) fn();
+    hipEventRecord(e0, 0);
+    for (int i = 0; i < 5; ++i) fn();
+    hipEventRecord(e1, 0);
+    hipEventSynchronize(e1);
+    float ms;
+    hipEventElapsedTime(&ms, e0, e1);
+    return ms / 5;
+  };
+  for (auto& s : shapes) {
+    if (only && std::string(s.n) != only) continue;
+    const double fl = 2.0 * s.M * (double)P * s.K;
+    float ms = timeit([&] {
+      gemm_uniform(s.t32, A, B, C, s.M, P, s.K, s.K, P, P, 0, 0, 0, 1, s.e, 0);
+    });
+    printf("%-9s f32  tile=%d: %.3f ms %.1f TF/s\n", s.n, (int)s.t32, ms, fl / ms / 1e9);
+    for (GemmTile t : {TILE_128x128, TILE_256x128, TILE_128x256, TILE_256x256}) {
+      ms = timeit([&] {
+        gemm_x6(t, A, B, C, s.M, P, s.K, s.K, P, P, 0, 0, 0, 1, s.e, ws, wsb, 0);
+      });
+      printf("%-9s x6   tile=%d: %.3f ms %.1f TF/s (fp32-equivalent)\n", s.n, (int)t, ms,
+             fl / ms / 1e9);
+    }
+  }
+  if (hipGetLastError() != hipSuccess) { printf("launch error\n"); return 1; }
+  // accuracy: M=256 N=4100 (ragged) K=520 (ragged), plain epilogue
+  {
+    const int M = 256, N = 4100, K = 520;
+    std::vector<float> ha((size_t)M * K), hb((size_t)K * N);
+    for (auto& v : ha) v = 0.05f * frand(seed);
+    for (auto& v : hb) v = frand(seed);
+    float *dA, *dB, *dC;
+    hipMalloc(&dA, ha.size() * 4);
+    hipMalloc(&dB, hb.size() * 4);
+    hipMalloc(&dC, (size_t)M * N * 4);
+    hipMemcpy(dA, ha.data(), ha.size() * 4, hipMemcpyHostToDevice);
+    hipMemcpy(dB, hb.data(), hb.size() * 4, hipMemcpyHostToDevice);
+    std::vector<double> ref((size_t)M * N, 0.0), mag((size_t)M * N, 0.0);
+    for (int m = 0; m < M; ++m)
+      for (int k = 0; k < K; ++k) {
+        const double a = ha[(size_t)m * K + k];
+        for (int n = 0; n < N; ++n) {
+          ref[(size_t)m * N + n] += a * hb[(size_t)k * N + n];
+          mag[(size_t)m * N + n] += std::fabs(a * hb[(size_t)k * N + n]);
+        }
+      }
+    std::vector<float> hc((size_t)M * N);
+    GemmEpi none;
+    for (int mode = 0; mode < 5; ++mode) {
+      hipMemset(dC, 0, (size_t)M * N * 4);
+      int rc;
+      if (mode == 0)
+        rc = gemm_uniform(TILE_128x128, dA, dB, dC, M, N, K, K, N, N, 0, 0, 0, 1, none, 0);
+      else
+        rc = gemm_x6(mode == 1 ? TILE_128x128 : mode == 2 ? TILE_256x128 : mode == 3 ? TILE_128x256 : TILE_256x256, dA, dB,
+                     dC, M, N, K, K, N, N, 0, 0, 0, 1, none, ws, wsb, 0);
+      hipMemcpy(hc.data(), dC, hc.size() * 4, hipMemcpyDeviceToHost);
+      double emax = 0, erel = 0;
+      for (size_t i = 0; i < hc.size(); ++i) {
+        const double e = std::fabs(hc[i] - ref[i]);
+        emax = std::max(emax, e);
+        erel = std::max(erel, e / mag[i]);
+      }
+      printf("accuracy %s rc=%d: max|err| %.3e  max|err|/sum|ab| %.3e\n",
+             mode == 0 ? "f32 " : mode == 1 ? "x6/128x128" : mode == 2 ? "x6/256x128" : mode == 3 ? "x6/128x256" : "x6/256x256",
+             rc, emax, erel);
+    }
+  }
+  return 0;
+}
