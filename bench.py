@@ -38,25 +38,52 @@ for _p in (REPO, PKG_DIR):
 import torch  # noqa: E402
 
 PEAK_FP32_MFMA_TFLOPS = 157.3   # MI355X_MICROARCH.md: f32 MFMA 157.3 TF (spec)
+PEAK_BF16_MFMA_TFLOPS = 2500.0  # MI355X_MICROARCH.md: bf16 MFMA ~2.5 PF dense (spec)
+# fp32 GEMMs on the "x6" engine (csrc/gemm_x6.hip): six bf16 MFMAs per fp32 product
+# block (exact three-term operand split), so their roof is the bf16 peak / 6
+PEAK_X6_TFLOPS = PEAK_BF16_MFMA_TFLOPS / 6.0
 PEAK_HBM_GBS = 8000.0           # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 
 
 # stages that run on the block's side stream (concurrent with the SHT)
 SIDE_STAGES = {"inner_skip"}
 # stage -> kernel symbol in the rocprofv3 summaries (profiles/<tag>/kernel_stats.csv);
-# fc1 (bias + GELU epilogue, 128x64) and fc2 (bias + residual, 128x128) are the only
-# launches of their template instantiations in the block
-STAGE_KERNEL = {
+# fc1 (bias + GELU epilogue) and fc2 (bias + residual) are the only launches of their
+# template instantiations in the block (x6 engine, 256x256 tiles; f32 engine kept
+# for MSFNO_GEMM=f32)
+STAGE_KERNEL_X6 = {
+    "mlp_fc1": "void msfno::gemm_x6_kernel<256, 256, 4, 2, true, 5>(msfno::GemmParams)",
+    "mlp_fc2": "void msfno::gemm_x6_kernel<256, 256, 4, 2, true, 3>(msfno::GemmParams)",
+    "inner_skip": "void msfno::gemm_x6_kernel<256, 256, 4, 2, true, 1>(msfno::GemmParams)",
+}
+STAGE_KERNEL_F32 = {
     "mlp_fc1": "void msfno::gemm_f32_kernel<128, 256, 16, true, 5>(msfno::GemmParams)",
     "mlp_fc2": "void msfno::gemm_f32_kernel<256, 128, 16, true, 3>(msfno::GemmParams)",
 }
+X6_STAGES = {"mlp_fc1", "mlp_fc2", "inner_skip"}
+X6_SPEC_STAGES = {"spectral_l0", "spectral_l1", "spectral_l2", "spectral_out"}
+
+
+def x6_engine():
+    """Dense-GEMM engine the library uses (csrc/gemm_x6.hip gemm_use_x6 /
+    api.cpp spec_use_x6 read the same switches)."""
+    dense = os.environ.get("MSFNO_GEMM", "") != "f32"
+    spec = dense and not os.environ.get("MSFNO_SPEC_X6", "").startswith("0")
+    return dense, spec
+
+
+def mfma_peak(stage):
+    dense, spec = x6_engine()
+    if (dense and stage in X6_STAGES) or (spec and stage in X6_SPEC_STAGES):
+        return PEAK_X6_TFLOPS, "x6 (fp32 via 3-term bf16 split, bf16 MFMA / 6)"
+    return PEAK_FP32_MFMA_TFLOPS, "f32 MFMA"
 
 
 def pmc_traffic(stage):
     """HBM bytes per launch of the stage's kernel from the newest committed PMC
     summary (profiles/*/pmc_traffic.json, written by tools/rocpd_summary.py from
     separate FETCH_SIZE / WRITE_SIZE passes, gfx950-corrected), or None."""
-    sym = STAGE_KERNEL.get(stage)
+    sym = (STAGE_KERNEL_X6 if x6_engine()[0] else STAGE_KERNEL_F32).get(stage)
     if sym is None:
         return None, None
     import glob
@@ -386,10 +413,11 @@ def main():
             kind, amount = w
             if kind == "mfma":
                 ach = amount / avg_s / 1e12
-                roof = {"bound": "mfma", "achieved": round(ach, 2), "peak": PEAK_FP32_MFMA_TFLOPS,
-                        "unit": "TFLOP/s", "frac": round(ach / PEAK_FP32_MFMA_TFLOPS, 4),
+                peak, engine = mfma_peak(name)
+                roof = {"bound": "mfma", "achieved": round(ach, 2), "peak": round(peak, 1),
+                        "unit": "TFLOP/s", "frac": round(ach / peak, 4),
                         "traffic": tr, "traffic_source": tr_src, "kernel": name,
-                        "avg_ms": round(avg_s * 1e3, 4)}
+                        "engine": engine, "avg_ms": round(avg_s * 1e3, 4)}
             else:
                 ach = amount / avg_s / 1e9
                 roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": PEAK_HBM_GBS,
@@ -402,7 +430,11 @@ def main():
             extra = ""
             if w:
                 a = w[1] / (ms / c / 1e3)
-                extra = f" {a / 1e12:.1f} TFLOP/s" if w[0] == "mfma" else f" {a / 1e9:.0f} GB/s"
+                if w[0] == "mfma":
+                    pk = mfma_peak(k)[0]
+                    extra = f" {a / 1e12:.1f} TFLOP/s ({100 * a / 1e12 / pk:.0f}% of {pk:.0f})"
+                else:
+                    extra = f" {a / 1e9:.0f} GB/s ({100 * a / 1e9 / PEAK_HBM_GBS:.0f}%)"
             print(f"  stage {k:18s} {ms / c:8.3f} ms x{c}{extra}", file=sys.stderr)
 
     cpu = None

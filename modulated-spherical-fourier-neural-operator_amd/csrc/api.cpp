@@ -310,6 +310,17 @@ bool use_c3m() {
   return mode == 1;
 }
 
+// spectral MLP on the x6 engine (real-ified 4-multiplication GEMM on the bf16
+// matrix cores, fp32-accurate split) whenever the dense GEMMs use it;
+// MSFNO_SPEC_X6=0 keeps the fp32 3M kernel for A/B
+bool spec_use_x6() {
+  static const bool on = [] {
+    const char* e = getenv("MSFNO_SPEC_X6");
+    return gemm_use_x6() && !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 int c3m_tile() {
   static int t = -1;
   if (t < 0) {
@@ -381,16 +392,18 @@ void carve_block(Carve& cv, BlockBufs& b, const msfno_block_desc* d,
   b.Sa = cv.take<float>(R * L.ldT);
   b.Sb = b.Sc = nullptr;
   for (auto& w : b.Wexp) w = nullptr;
+  b.dw = DenseWs{};
   b.xt = b.yt = nullptr;
   if (d->filter_type == MSFNO_FILTER_NONLINEAR) {
     const int64_t Hs = d->spec_hidden;
-    b.Sb = cv.take<float>((int64_t)B * 2 * Hs * L.ldT);
-    b.Sc = cv.take<float>((int64_t)B * 2 * Hs * L.ldT);
+    b.Sb = cv.take<float>(spec_hidden_floats(B, Hs, L));
+    b.Sc = cv.take<float>(spec_hidden_floats(B, Hs, L));
     for (int l = 0; l <= d->spectral_layers; ++l) {
       const int64_t ci = (l == 0) ? C : Hs;
       const int64_t co = (l == d->spectral_layers) ? C : Hs;
       b.Wexp[l] = cv.take<float>(4 * ci * co);
     }
+    carve_spec_ws(cv, b.dw, d);
   } else {
     b.xt = cv.take<float>(BC * L.T * 2);
     b.yt = cv.take<float>(BC * L.T * 2);
@@ -409,13 +422,14 @@ void carve_block(Carve& cv, BlockBufs& b, const msfno_block_desc* d,
     const int64_t Hd = d->mlp_hidden;
     b.W1f = cv.take<float>((int64_t)B * Hd * C);
     b.b1f = cv.take<float>((int64_t)B * Hd);
-    b.h = cv.take<float>((int64_t)B * Hd * P);
+    b.h = cv.take<float>(mlp_h_floats(B, Hd, P));
   }
   carve_dense_ws(cv, b.dw, d, B);
 }
 
 void carve_dense_ws(Carve& cv, DenseWs& w, const msfno_block_desc* d, int B) {
-  w = DenseWs{};
+  w.skip = w.fc1 = w.fc2 = nullptr;
+  w.skip_b = w.fc1_b = w.fc2_b = 0;
   const int C = (int)d->C;
   if (d->inner_skip == MSFNO_SKIP_LINEAR && (w.skip_b = gemm_dense_workspace(C, C, 1)))
     w.skip = cv.take<char>(w.skip_b);
@@ -423,6 +437,27 @@ void carve_dense_ws(Carve& cv, DenseWs& w, const msfno_block_desc* d, int B) {
     const int Hd = (int)d->mlp_hidden;
     if ((w.fc1_b = gemm_dense_workspace(Hd, C, B))) w.fc1 = cv.take<char>(w.fc1_b);
     if ((w.fc2_b = gemm_dense_workspace(C, Hd, 1))) w.fc2 = cv.take<char>(w.fc2_b);
+  }
+}
+
+// floats to reserve for one spectral-MLP hidden buffer (B, 2 Hs, T): fp32, or
+// bf16x3 planes with a row stride padded to 8 on the x6 engine
+int64_t spec_hidden_floats(int B, int64_t Hs, const SpecLayout& L) {
+  if (!spec_use_x6()) return (int64_t)B * 2 * Hs * L.ldT;
+  return std::max<int64_t>((int64_t)B * 2 * Hs * L.ldT,
+                           cdiv((int64_t)B * 3 * 2 * Hs * round_up(L.Tp, 8) * 2, 4));
+}
+
+// split-A planes of the real-ified spectral MLP weights (x6 engine)
+void carve_spec_ws(Carve& cv, DenseWs& w, const msfno_block_desc* d) {
+  for (auto& p : w.spec) p = nullptr;
+  for (auto& n : w.spec_b) n = 0;
+  if (!spec_use_x6() || d->filter_type != MSFNO_FILTER_NONLINEAR) return;
+  for (int l = 0; l <= d->spectral_layers && l < 9; ++l) {
+    const int ci = (l == 0) ? (int)d->C : (int)d->spec_hidden;
+    const int co = (l == d->spectral_layers) ? (int)d->C : (int)d->spec_hidden;
+    w.spec_b[l] = gemm_dense_workspace(2 * co, 2 * ci, 1);
+    if (w.spec_b[l]) w.spec[l] = cv.take<char>(w.spec_b[l]);
   }
 }
 
@@ -453,7 +488,8 @@ int run_filter(const msfno_block_desc* d, msfno_sht_plan_s* f, msfno_sht_plan_s*
     const int nl = d->spectral_layers;
     const int64_t Hs = d->spec_hidden;
     prof(ST_SPEC_PREP, s);
-    const bool c3m = use_c3m();
+    const bool x6 = spec_use_x6() && b.dw.spec[0];
+    const bool c3m = !x6 && use_c3m();
     for (int l = 0; l <= nl; ++l) {
       const int ci = (l == 0) ? (int)C : (int)Hs;
       const int co = (l == nl) ? (int)C : (int)Hs;
@@ -470,7 +506,33 @@ int run_filter(const msfno_block_desc* d, msfno_sht_plan_s* f, msfno_sht_plan_s*
       const int co = (l == nl) ? (int)C : (int)Hs;
       float* out = (l == nl) ? b.Sa : ((l & 1) ? b.Sc : b.Sb);
       prof(l == nl ? ST_SPEC_OUT : ST_SPEC_L0 + std::min(l, 3), s);
-      if (c3m) {
+      if (x6) {
+        // real-ified [[Wr, -Wi], [Wi, Wr]] GEMM on the x6 engine, ComplexReLU(real)
+        // = ReLU on the real rows of each batch block, in the epilogue.  Hidden
+        // activations travel as bf16x3 planes [b][plane][2 Hs][ldTx]: layer 0
+        // splits its fp32 input in-kernel, later layers stage planes by LDS-DMA
+        // (gemm_x6p), the output layer writes fp32 S for the inverse Legendre.
+        const int64_t ldTx = round_up(L.Tp, 8);
+        GemmEpi e;
+        if (l < nl) {
+          e.relu_period = 2 * co;
+          e.relu_rows = co;
+          e.c_planes = reinterpret_cast<unsigned short*>(out);
+          e.c_plane_stride = 2LL * co * ldTx;
+        }
+        const int ldc = l < nl ? (int)ldTx : (int)L.ldT;
+        const int64_t sC = l < nl ? 3 * 2LL * co * ldTx : 2LL * co * L.ldT;
+        if (l == 0) {
+          MSFNO_TRY(gemm_dense(ROLE_SPEC, TILE_128x128, b.Wexp[l], in, out, 2 * co, (int)L.Tp,
+                               2 * ci, 2 * ci, (int)L.ldT, ldc, 0, 2LL * ci * L.ldT, sC, B, e,
+                               b.dw.spec[l], b.dw.spec_b[l], s));
+        } else {
+          e.b_planes = reinterpret_cast<const unsigned short*>(in);
+          e.b_plane_stride = 2LL * ci * ldTx;
+          MSFNO_TRY(gemm_x6p(b.Wexp[l], out, 2 * co, (int)L.Tp, 2 * ci, 2 * ci, (int)ldTx, ldc, 0,
+                             3 * 2LL * ci * ldTx, sC, B, e, b.dw.spec[l], b.dw.spec_b[l], s));
+        }
+      } else if (c3m) {
         // Gauss 3-multiplication complex GEMM (cgemm.hip), ComplexReLU(real) fused
         MSFNO_TRY(gemm_c3m(b.Wexp[l], b.Wexp[l] + (int64_t)ci * co, in, out, co, ci, (int)L.Tp,
                            (int)L.ldT, (int)L.ldT, 2LL * ci * L.ldT, 2LL * co * L.ldT, B, l < nl,
@@ -627,19 +689,49 @@ int run_mlp(const msfno_block_desc* d, const float* W1f, const float* b1f, const
             float* h, float* out, const float* resid, int B, int64_t P, const DenseWs& dw,
             hipStream_t s) {
   const int64_t C = d->C, Hd = d->mlp_hidden;
+  // x6 engine: h travels as bf16x3 planes [B][3][Hd][ldh] (fc1 splits it once in its
+  // epilogue, fc2 stages it without conversion)
+  const bool planes = mlp_h_planes(dw.fc1 != nullptr && dw.fc2 != nullptr);
+  const int64_t ldh = planes ? round_up(P, 8) : P;
+  unsigned short* hx = planes ? reinterpret_cast<unsigned short*>(h) : nullptr;
   prof(ST_FC1, s);
   GemmEpi e1;
   e1.bias = b1f;
   e1.sBias = Hd;
   e1.act = 1;
+  if (planes) { e1.c_planes = hx; e1.c_plane_stride = Hd * ldh; }
   MSFNO_TRY(gemm_dense(ROLE_FC1, TILE_128x256, W1f, x1, h, (int)Hd, (int)P, (int)C, (int)C,
-                       (int)P, (int)P, Hd * C, C * P, Hd * P, B, e1, dw.fc1, dw.fc1_b, s));
+                       (int)P, (int)ldh, Hd * C, C * P, (planes ? 3 : 1) * Hd * ldh, B, e1,
+                       dw.fc1, dw.fc1_b, s));
   prof(ST_FC2, s);
   GemmEpi e2;
   e2.bias = d->fc2_b;
   if (resid) { e2.addend = resid; e2.sD = C * P; e2.ldd = (int)P; }
+  if (planes) {
+    e2.b_planes = hx;
+    e2.b_plane_stride = Hd * ldh;
+    return gemm_x6p(d->fc2_w, out, (int)C, (int)P, (int)Hd, (int)Hd, (int)ldh, (int)P, 0,
+                    3 * Hd * ldh, C * P, B, e2, dw.fc2, dw.fc2_b, s);
+  }
   return gemm_dense(ROLE_FC2, TILE_256x128, d->fc2_w, h, out, (int)C, (int)P, (int)Hd, (int)Hd,
-                    (int)P, (int)P, 0, Hd * P, C * P, B, e2, dw.fc2, dw.fc2_b, s);
+                    (int)ldh, (int)P, 0, (planes ? 3 : 1) * Hd * ldh, C * P, B, e2, dw.fc2,
+                    dw.fc2_b, s);
+}
+
+// MLP hidden activation in the bf16x3 plane format (x6 engine; MSFNO_H_PLANES=0
+// keeps it fp32 for A/B)
+bool mlp_h_planes(bool have_ws) {
+  static const bool on = [] {
+    const char* e = getenv("MSFNO_H_PLANES");
+    return gemm_use_x6() && !(e && e[0] == '0');
+  }();
+  return on && have_ws;
+}
+
+// floats to reserve for the MLP hidden activation h (B, Hd, P) in either format
+int64_t mlp_h_floats(int B, int64_t Hd, int64_t P) {
+  if (!mlp_h_planes(true)) return (int64_t)B * Hd * P;
+  return cdiv((int64_t)B * 3 * Hd * round_up(P, 8) * 2, 4);
 }
 }  // namespace msfno
 

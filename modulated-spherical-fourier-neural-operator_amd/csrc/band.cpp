@@ -75,20 +75,21 @@ void carve_band(Carve& cv, BandBufs& b, const msfno_block_desc* d, const msfno_b
   std::memset(&b.fb, 0, sizeof(b.fb));
   b.fb.Sa = cv.take<float>(R * L.ldT);
   const int64_t Hs = d->spec_hidden;
-  b.fb.Sb = cv.take<float>((int64_t)B * 2 * Hs * L.ldT);
-  b.fb.Sc = cv.take<float>((int64_t)B * 2 * Hs * L.ldT);
+  b.fb.Sb = cv.take<float>(spec_hidden_floats(B, Hs, L));
+  b.fb.Sc = cv.take<float>(spec_hidden_floats(B, Hs, L));
   for (int l = 0; l <= d->spectral_layers && l < 9; ++l) {
     const int64_t ci = (l == 0) ? C : Hs;
     const int64_t co = (l == d->spectral_layers) ? C : Hs;
     b.fb.Wexp[l] = cv.take<float>(4 * ci * co);
   }
+  carve_spec_ws(cv, b.fb.dw, d);
   b.x1 = cv.take<float>(BC * Pl);
   b.W1f = b.b1f = b.h = nullptr;
   if (d->has_mlp) {
     const int64_t Hd = d->mlp_hidden;
     b.W1f = cv.take<float>((int64_t)B * Hd * C);
     b.b1f = cv.take<float>((int64_t)B * Hd);
-    b.h = cv.take<float>((int64_t)B * Hd * Pl);
+    b.h = cv.take<float>(mlp_h_floats(B, Hd, Pl));
   }
   carve_dense_ws(cv, b.fb.dw, d, B);
 }

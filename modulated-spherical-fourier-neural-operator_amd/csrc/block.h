@@ -38,8 +38,13 @@ int side_ctx(SideCtx** out);
 struct DenseWs {
   void *skip = nullptr, *fc1 = nullptr, *fc2 = nullptr;
   size_t skip_b = 0, fc1_b = 0, fc2_b = 0;
+  void* spec[9] = {};     // real-ified spectral MLP layers (x6 engine only)
+  size_t spec_b[9] = {};
 };
 void carve_dense_ws(Carve& cv, DenseWs& w, const msfno_block_desc* d, int B);
+void carve_spec_ws(Carve& cv, DenseWs& w, const msfno_block_desc* d);
+bool spec_use_x6();
+int64_t spec_hidden_floats(int B, int64_t Hs, const SpecLayout& L);
 
 struct BlockBufs {
   float2* Xn; float* Xt; float2* rs0; float* sc0; float* sh0;
@@ -73,6 +78,8 @@ void set_table_offsets(msfno_sht_plan_s* p, int sym);
 int run_mlp(const msfno_block_desc* d, const float* W1f, const float* b1f, const float* x1,
             float* h, float* out, const float* resid, int B, int64_t P, const DenseWs& dw,
             hipStream_t s);
+bool mlp_h_planes(bool have_ws);
+int64_t mlp_h_floats(int B, int64_t Hd, int64_t P);
 // plan construction (mask: optional m-set, see SpecLayout::build)
 int plan_create(int nlat, int nlon, int lmax, int mmax, int inverse,
                 const std::vector<char>* mask, msfno_sht_plan_s** out);

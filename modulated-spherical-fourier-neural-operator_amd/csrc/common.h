@@ -130,6 +130,13 @@ struct GemmEpi {
   int relu_period = 0, relu_rows = 0;  // ReLU rows where (row % period) < relu_rows
   const float* rowscale = nullptr;  // per-(b,c) factor for rows r=(b,ri,c); C = rs_C
   int rs_C = 0;
+  // x6 engine only: operands in the bf16x3 plane format (three exact bf16 terms
+  // per fp32 value, plane stride in elements; batch stride / ld as for fp32).
+  // b_planes replaces B; c_planes receives C (the fp32 C pointer is unused)
+  const unsigned short* b_planes = nullptr;
+  int64_t b_plane_stride = 0;
+  unsigned short* c_planes = nullptr;
+  int64_t c_plane_stride = 0;
 };
 
 enum GemmTile {
@@ -159,6 +166,17 @@ int gemm_x6(GemmTile tile, const float* A, const float* B, float* C, int M, int 
             void* ws, size_t ws_bytes, hipStream_t s);
 int launch_split_a(const float* A, unsigned short* Ax, int M, int K, int lda, int64_t sA,
                    int batch, hipStream_t s);
+// x6 GEMM with B (and optionally C) in the bf16x3 plane format (gemm_x6p.hip):
+// epi.b_planes required (ldb, sB, b_plane_stride % 8 == 0, 16-B aligned); A fp32
+// is split per call into ws (>= gemm_x6p_workspace(M, K, sA == 0 ? 1 : batch))
+size_t gemm_x6p_workspace(int M, int K, int batch_a);
+int gemm_x6p(const float* A, float* C, int M, int N, int K, int lda, int ldb, int ldc,
+             int64_t sA, int64_t sB, int64_t sC, int batch, const GemmEpi& epi, void* ws,
+             size_t ws_bytes, hipStream_t s);
+// fp32 x[z][r][c] (ld ldx, batch stride sx) -> bf16x3 planes xp[z][plane][r][c]
+int launch_split_planes(const float* x, unsigned short* xp, int rows, int cols, int ldx,
+                        int64_t sx, int ldp, int64_t pstride, int64_t sxp, int batch,
+                        hipStream_t s);
 // dense 1x1-conv GEMMs of the block / MLP: gemm_x6 unless MSFNO_GEMM=f32 (or no
 // workspace / a GELU-on-B or rowscale epilogue), else the fp32 MFMA kernel on
 // role_tile(role, f32_tile).  batch_a = 1 when sA == 0, else batch.

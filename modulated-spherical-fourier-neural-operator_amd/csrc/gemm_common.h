@@ -29,6 +29,13 @@ struct GemmParams {
   const unsigned short* Ax;
   int64_t sAx, sAxp;  // batch stride, plane stride (elements)
   int ldax;           // Kp
+  // bf16x3 "plane" operands (gemm_x6.hip): B given as 3 exact bf16 terms
+  // [batch sB][plane sBxp][K][ldb] instead of fp32; C written as planes
+  // [batch sC][plane sCxp][M][ldc] (EPI_PLANES) instead of fp32
+  const unsigned short* Bx;
+  int64_t sBxp;
+  unsigned short* Cx;
+  int64_t sCxp;
 };
 
 __device__ __forceinline__ int xcd_remap(int orig, int nwg) {
@@ -113,7 +120,30 @@ __device__ __forceinline__ float gelu_erf(float v) {
 }
 
 // epilogue flags (+ EPI_GELU_B: GELU applied to the B operand while it is staged)
-enum : int { EPI_BIAS = 1, EPI_ADD = 2, EPI_GELU = 4, EPI_RELU = 8, EPI_ROWSCALE = 32, EPI_GELU_B = 64 };
+enum : int {
+  EPI_BIAS = 1, EPI_ADD = 2, EPI_GELU = 4, EPI_RELU = 8, EPI_ROWSCALE = 32, EPI_GELU_B = 64,
+  EPI_PLANES = 128  // store C as three exact bf16 terms (the x6 operand format)
+};
+
+// (a, b) -> packed bf16x2 terms t0 + t1 + t2 == (a, b) exactly (24 significant
+// bits = the fp32 significand; round-to-nearest cvt, exact residuals)
+typedef float f32x2v_ __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2v_ __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t cvt_pk_bf16(float a, float b) {
+  const f32x2v_ v = {a, b};
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, bf16x2v_));
+}
+__device__ __forceinline__ float bf_lo(uint32_t u) { return __uint_as_float(u << 16); }
+__device__ __forceinline__ float bf_hi(uint32_t u) { return __uint_as_float(u & 0xffff0000u); }
+__device__ __forceinline__ void split2(float a, float b, uint32_t& t0, uint32_t& t1, uint32_t& t2) {
+  t0 = cvt_pk_bf16(a, b);
+  a -= bf_lo(t0);
+  b -= bf_hi(t0);
+  t1 = cvt_pk_bf16(a, b);
+  a -= bf_lo(t1);
+  b -= bf_hi(t1);
+  t2 = cvt_pk_bf16(a, b);
+}
 
 // C tile epilogue.  acc holds each wave's (BM/WGM)x(BN/WGN) part of the tile
 // (waves WGM x WGN, wave w at (w / WGN, w % WGN)) as 32x32 MFMA blocks (row
@@ -141,7 +171,8 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, floatx16 (&ac
   // epilogue VGPR-light, and the global traffic in full lines.
   float* Cs = lds;  // the main loop ended with a barrier: staging memory is free
   constexpr int QPT = (32 * WGM * BN / 4) / NTHR;  // float4 per thread per row-tile
-  static_assert(QPT * NTHR * 4 == 32 * WGM * BN, "epilogue mapping");
+  constexpr int QC = QPT < 8 ? QPT : 8;
+  static_assert(QPT * NTHR * 4 == 32 * WGM * BN && QPT % QC == 0, "epilogue mapping");
   const bool vecC = p.vecC;
 #pragma unroll
   for (int i = 0; i < MT; ++i) {
@@ -152,82 +183,102 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, floatx16 (&ac
         Cs[(wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * half) * CS_LD + wn * WN + j * 32 + l32] =
             acc[i][j][r];
     __syncthreads();
-    float4 add4[QPT];
-    if constexpr ((EPI & EPI_ADD) != 0) {
-#pragma unroll
-      for (int q = 0; q < QPT; ++q) {
-        const int idx = tid + NTHR * q;
-        const int lr = idx / (BN / 4);
-        const int row = min(m0 + (lr >> 5) * WM + i * 32 + (lr & 31), M - 1);
-        const int col = n0 + 4 * (idx % (BN / 4));
-        const float* src = addend + (int64_t)row * p.ldd;
-        if (vecC) {
-          add4[q] = *reinterpret_cast<const float4*>(src + min(col, (N - 1) & ~3));
-        } else {
-          add4[q] = make_float4(src[min(col, N - 1)], src[min(col + 1, N - 1)],
-                                src[min(col + 2, N - 1)], src[min(col + 3, N - 1)]);
-        }
-      }
-    }
-    // all LDS reads of the row-tile first (one lgkmcnt wait), then the math and
-    // the stores: per-q read->use chains serialised ~100 cycles each behind the
-    // stores of the previous q
-    float4 cv[QPT];
-#pragma unroll
-    for (int q = 0; q < QPT; ++q) {
-      const int idx = tid + NTHR * q;
-      cv[q] = *reinterpret_cast<const float4*>(Cs + (idx / (BN / 4)) * CS_LD + 4 * (idx % (BN / 4)));
-    }
-    float bvq[QPT];
-    if constexpr ((EPI & EPI_BIAS) != 0) {
-#pragma unroll
-      for (int q = 0; q < QPT; ++q) {
-        const int lr = (tid + NTHR * q) / (BN / 4);
-        const int row = m0 + (lr >> 5) * WM + i * 32 + (lr & 31);
-        bvq[q] = bias_s[min(row, M - 1) - m0];
-      }
-    }
-#pragma unroll
-    for (int q = 0; q < QPT; ++q) {
-      const int idx = tid + NTHR * q;
-      const int lr = idx / (BN / 4);
-      const int c4 = idx % (BN / 4);
-      const int row = m0 + (lr >> 5) * WM + i * 32 + (lr & 31);
-      const int col = n0 + 4 * c4;
-      float4 v = cv[q];
-      const int rr = min(row, M - 1);
-      if constexpr ((EPI & EPI_ROWSCALE) != 0) {
-        const int C2 = 2 * p.rs_C;
-        const float sv = (dflags & 1) ? p.rowscale[(rr / C2) * p.rs_C + rr % p.rs_C] : 1.f;
-        v.x *= sv; v.y *= sv; v.z *= sv; v.w *= sv;
-      }
-      if constexpr ((EPI & EPI_BIAS) != 0) {
-        const float bv = bvq[q];
-        v.x += bv; v.y += bv; v.z += bv; v.w += bv;
-      }
+    // in chunks of QC float4 per thread (<= 8: bounds the epilogue's VGPRs)
+    for (int qc = 0; qc < QPT; qc += QC) {
+      float4 add4[QC];
       if constexpr ((EPI & EPI_ADD) != 0) {
-        v.x += add4[q].x; v.y += add4[q].y; v.z += add4[q].z; v.w += add4[q].w;
-      }
-      if constexpr ((EPI & EPI_GELU) != 0) {
-        f32x2 lo = {v.x, v.y}, hi = {v.z, v.w};
-        lo = gelu_erf2(lo);
-        hi = gelu_erf2(hi);
-        v = make_float4(lo.x, lo.y, hi.x, hi.y);
-      }
-      if constexpr ((EPI & EPI_RELU) != 0) {
-        if ((unsigned)row % (unsigned)p.relu_period < (unsigned)p.relu_rows) {
-          v.x = fmaxf(v.x, 0.f); v.y = fmaxf(v.y, 0.f); v.z = fmaxf(v.z, 0.f); v.w = fmaxf(v.w, 0.f);
+#pragma unroll
+        for (int q = 0; q < QC; ++q) {
+          const int idx = tid + NTHR * (qc + q);
+          const int lr = idx / (BN / 4);
+          const int row = min(m0 + (lr >> 5) * WM + i * 32 + (lr & 31), M - 1);
+          const int col = n0 + 4 * (idx % (BN / 4));
+          const float* src = addend + (int64_t)row * p.ldd;
+          if (vecC) {
+            add4[q] = *reinterpret_cast<const float4*>(src + min(col, (N - 1) & ~3));
+          } else {
+            add4[q] = make_float4(src[min(col, N - 1)], src[min(col + 1, N - 1)],
+                                  src[min(col + 2, N - 1)], src[min(col + 3, N - 1)]);
+          }
         }
       }
-      if (row < M) {
-        float* dst = C + (int64_t)row * ldc + col;
-        if (vecC && col + 3 < N) {
-          *reinterpret_cast<float4*>(dst) = v;
-        } else {
-          if (col < N) dst[0] = v.x;
-          if (col + 1 < N) dst[1] = v.y;
-          if (col + 2 < N) dst[2] = v.z;
-          if (col + 3 < N) dst[3] = v.w;
+      // all LDS reads of the row-tile first (one lgkmcnt wait), then the math and
+      // the stores: per-q read->use chains serialised ~100 cycles each behind the
+      // stores of the previous q
+      float4 cv[QC];
+#pragma unroll
+      for (int q = 0; q < QC; ++q) {
+        const int idx = tid + NTHR * (qc + q);
+        cv[q] = *reinterpret_cast<const float4*>(Cs + (idx / (BN / 4)) * CS_LD + 4 * (idx % (BN / 4)));
+      }
+      float bvq[QC];
+      if constexpr ((EPI & EPI_BIAS) != 0) {
+#pragma unroll
+        for (int q = 0; q < QC; ++q) {
+          const int lr = (tid + NTHR * (qc + q)) / (BN / 4);
+          const int row = m0 + (lr >> 5) * WM + i * 32 + (lr & 31);
+          bvq[q] = bias_s[min(row, M - 1) - m0];
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < QC; ++q) {
+        const int idx = tid + NTHR * (qc + q);
+        const int lr = idx / (BN / 4);
+        const int c4 = idx % (BN / 4);
+        const int row = m0 + (lr >> 5) * WM + i * 32 + (lr & 31);
+        const int col = n0 + 4 * c4;
+        float4 v = cv[q];
+        const int rr = min(row, M - 1);
+        if constexpr ((EPI & EPI_ROWSCALE) != 0) {
+          const int C2 = 2 * p.rs_C;
+          const float sv = (dflags & 1) ? p.rowscale[(rr / C2) * p.rs_C + rr % p.rs_C] : 1.f;
+          v.x *= sv; v.y *= sv; v.z *= sv; v.w *= sv;
+        }
+        if constexpr ((EPI & EPI_BIAS) != 0) {
+          const float bv = bvq[q];
+          v.x += bv; v.y += bv; v.z += bv; v.w += bv;
+        }
+        if constexpr ((EPI & EPI_ADD) != 0) {
+          v.x += add4[q].x; v.y += add4[q].y; v.z += add4[q].z; v.w += add4[q].w;
+        }
+        if constexpr ((EPI & EPI_GELU) != 0) {
+          f32x2 lo = {v.x, v.y}, hi = {v.z, v.w};
+          lo = gelu_erf2(lo);
+          hi = gelu_erf2(hi);
+          v = make_float4(lo.x, lo.y, hi.x, hi.y);
+        }
+        if constexpr ((EPI & EPI_RELU) != 0) {
+          if ((unsigned)row % (unsigned)p.relu_period < (unsigned)p.relu_rows) {
+            v.x = fmaxf(v.x, 0.f); v.y = fmaxf(v.y, 0.f); v.z = fmaxf(v.z, 0.f); v.w = fmaxf(v.w, 0.f);
+          }
+        }
+        if constexpr ((EPI & EPI_PLANES) != 0) {
+          if (row < M) {
+            unsigned short* dst = p.Cx + blockIdx.z * p.sC + (int64_t)row * ldc + col;
+            uint32_t a0, a1, a2, b0, b1, b2;
+            split2(v.x, v.y, a0, a1, a2);
+            split2(v.z, v.w, b0, b1, b2);
+            if (col + 3 < N) {  // ldc % 4 == 0 (checked on the host): 8-B aligned
+              *reinterpret_cast<uint2*>(dst) = make_uint2(a0, b0);
+              *reinterpret_cast<uint2*>(dst + p.sCxp) = make_uint2(a1, b1);
+              *reinterpret_cast<uint2*>(dst + 2 * p.sCxp) = make_uint2(a2, b2);
+            } else {
+              const uint32_t t[3][2] = {{a0, b0}, {a1, b1}, {a2, b2}};
+              for (int e = 0; e < 4 && col + e < N; ++e)
+                for (int pl = 0; pl < 3; ++pl)
+                  dst[pl * p.sCxp + e] = (unsigned short)(t[pl][e >> 1] >> (16 * (e & 1)));
+            }
+          }
+        } else if (row < M) {
+          float* dst = C + (int64_t)row * ldc + col;
+          if (vecC && col + 3 < N) {
+            *reinterpret_cast<float4*>(dst) = v;
+          } else {
+            if (col < N) dst[0] = v.x;
+            if (col + 1 < N) dst[1] = v.y;
+            if (col + 2 < N) dst[2] = v.z;
+            if (col + 3 < N) dst[3] = v.w;
+          }
         }
       }
     }

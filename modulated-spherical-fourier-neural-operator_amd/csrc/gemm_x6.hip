@@ -24,6 +24,7 @@
 //      transposed fragment reads conflict free), read with ds_read_b64_tr_b16
 //      (4 k x 16 n per 16-lane group, delivered k-contiguous per lane).
 #include <cstdlib>
+#include <type_traits>
 #include <string>
 
 #include "gemm_common.h"
@@ -33,27 +34,6 @@ namespace msfno {
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef short s16x4 __attribute__((ext_vector_type(4)));
 typedef short s16x8 __attribute__((ext_vector_type(8)));
-typedef float f32x2v __attribute__((ext_vector_type(2)));
-typedef __bf16 bf16x2v __attribute__((ext_vector_type(2)));
-
-__device__ __forceinline__ uint32_t cvt_pk_bf16(float a, float b) {
-  const f32x2v v = {a, b};
-  return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, bf16x2v));
-}
-__device__ __forceinline__ float bf_lo(uint32_t u) { return __uint_as_float(u << 16); }
-__device__ __forceinline__ float bf_hi(uint32_t u) { return __uint_as_float(u & 0xffff0000u); }
-
-// (a, b) -> three packed bf16x2 terms
-__device__ __forceinline__ void split2(float a, float b, uint32_t& t0, uint32_t& t1, uint32_t& t2) {
-  t0 = cvt_pk_bf16(a, b);
-  a -= bf_lo(t0);
-  b -= bf_hi(t0);
-  t1 = cvt_pk_bf16(a, b);
-  a -= bf_lo(t1);
-  b -= bf_hi(t1);
-  t2 = cvt_pk_bf16(a, b);
-}
-
 __global__ void split_a_kernel(const float* __restrict__ A, unsigned short* __restrict__ Ax, int M,
                                int K, int lda, int64_t sA, int Mp, int Kp) {
   const int z = blockIdx.y;
@@ -74,7 +54,8 @@ __global__ void split_a_kernel(const float* __restrict__ A, unsigned short* __re
   }
 }
 
-template <int BM, int BN, int WGM, int WGN, bool VEC, int EPI>
+// BPL: B arrives pre-split as bf16 planes (p.Bx), staged without conversion
+template <int BM, int BN, int WGM, int WGN, bool VEC, int EPI, bool BPL>
 __global__ __launch_bounds__(64 * WGM * WGN) void gemm_x6_kernel(GemmParams p) {
   constexpr int BK = 16;
   constexpr int NTHR = 64 * WGM * WGN;
@@ -92,6 +73,11 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_x6_kernel(GemmParams p) {
   constexpr int A_LD = 6 * BM / NTHR;       // 16-B chunks of split A per thread
   constexpr int B_LD = BK * BN / 4 / NTHR;  // float4 of B per thread
   static_assert(A_LD * NTHR == 6 * BM && B_LD * NTHR * 4 == BK * BN, "tile shape");
+  // pre-split B: chunks of BCH bf16 (16 or 8 bytes), BPQ per thread
+  constexpr int BCH = ((3 * BK * BN / 8) % NTHR == 0) ? 8 : 4;
+  constexpr int BPQ = 3 * BK * BN / BCH / NTHR;
+  static_assert(BPQ * NTHR * BCH == 3 * BK * BN, "plane tile shape");
+  typedef typename std::conditional<BCH == 8, uint4, uint2>::type bchunk_t;
   __shared__ __attribute__((aligned(16))) char lds_raw[LDS_BYTES + (HAS_BIAS ? BM * 4 : 0)];
   unsigned short* const As = reinterpret_cast<unsigned short*>(lds_raw);
   unsigned short* const Bs = As + 2 * A_STAGE;
@@ -120,7 +106,9 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_x6_kernel(GemmParams p) {
   }
 
   uint4 ra[A_LD];
-  float4 rb[B_LD];
+  float4 rb[BPL ? 1 : B_LD];
+  bchunk_t rbp[BPL ? BPQ : 1];
+  const unsigned short* Bx = BPL ? p.Bx + z * p.sB : nullptr;
   const int Kc = K - 1, Nc = N - 1;
   auto load_A = [&](int kt) {
 #pragma unroll
@@ -143,6 +131,17 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_x6_kernel(GemmParams p) {
     }
   };
   auto load_B = [&](int kt) {
+    if constexpr (BPL) {
+#pragma unroll
+      for (int q = 0; q < BPQ; ++q) {
+        const int c = tid + NTHR * q;
+        const int pl = c / (BK * BN / BCH), rem = c % (BK * BN / BCH);
+        const int kr = min(kt * BK + rem / (BN / BCH), Kc);
+        const int col = min(n0 + BCH * (rem % (BN / BCH)), Nc & ~(BCH - 1));
+        rbp[q] = *reinterpret_cast<const bchunk_t*>(Bx + pl * p.sBxp + (int64_t)kr * ldb + col);
+      }
+      return;
+    }
 #pragma unroll
     for (int q = 0; q < B_LD; ++q) {
       const int f = tid + NTHR * q;
@@ -158,6 +157,29 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_x6_kernel(GemmParams p) {
     }
   };
   auto store_B = [&](int buf, int kt) {
+    if constexpr (BPL) {
+#pragma unroll
+      for (int q = 0; q < BPQ; ++q) {
+        const int c = tid + NTHR * q;
+        const int pl = c / (BK * BN / BCH), rem = c % (BK * BN / BCH);
+        const int kr = rem / (BN / BCH), cl = BCH * (rem % (BN / BCH));
+        bchunk_t v = rbp[q];
+        const bool kok = kt * BK + kr < K;
+        if (!kok || n0 + cl + BCH > N) {  // K tail / ragged N: zero what is out of range
+          unsigned short e[BCH];
+          __builtin_memcpy(e, &v, sizeof(v));
+          // the load was clamped to the last aligned chunk: re-read exact elements
+          const int kr_g = min(kt * BK + kr, Kc);
+          for (int t = 0; t < BCH; ++t) {
+            const int cg = n0 + cl + t;
+            e[t] = (kok && cg < N) ? Bx[pl * p.sBxp + (int64_t)kr_g * ldb + cg] : 0;
+          }
+          __builtin_memcpy(&v, e, sizeof(v));
+        }
+        *reinterpret_cast<bchunk_t*>(Bs + buf * B_STAGE + pl * B_PLANE + kr * B_ROW + cl) = v;
+      }
+      return;
+    }
 #pragma unroll
     for (int q = 0; q < B_LD; ++q) {
       const int f = tid + NTHR * q;
@@ -291,18 +313,21 @@ size_t gemm_x6_workspace(int M, int K, int batch) {
 
 template <int BM, int BN, int WGM, int WGN, int EPI>
 static void launch_x6_e(const GemmParams& p, dim3 grid, hipStream_t s) {
-  if (p.vecB)
-    hipLaunchKernelGGL((gemm_x6_kernel<BM, BN, WGM, WGN, true, EPI>), grid, dim3(64 * WGM * WGN),
-                       0, s, p);
+  if (p.Bx)
+    hipLaunchKernelGGL((gemm_x6_kernel<BM, BN, WGM, WGN, true, EPI, true>), grid,
+                       dim3(64 * WGM * WGN), 0, s, p);
+  else if (p.vecB)
+    hipLaunchKernelGGL((gemm_x6_kernel<BM, BN, WGM, WGN, true, EPI, false>), grid,
+                       dim3(64 * WGM * WGN), 0, s, p);
   else
-    hipLaunchKernelGGL((gemm_x6_kernel<BM, BN, WGM, WGN, false, EPI>), grid, dim3(64 * WGM * WGN),
-                       0, s, p);
+    hipLaunchKernelGGL((gemm_x6_kernel<BM, BN, WGM, WGN, false, EPI, false>), grid,
+                       dim3(64 * WGM * WGN), 0, s, p);
 }
 
 template <int BM, int BN, int WGM, int WGN>
 static int launch_x6(const GemmParams& p, dim3 grid, hipStream_t s) {
   const int code = (p.bias ? EPI_BIAS : 0) | (p.addend ? EPI_ADD : 0) | (p.act == 1 ? EPI_GELU : 0) |
-                   (p.relu_period ? EPI_RELU : 0);
+                   (p.relu_period ? EPI_RELU : 0) | (p.Cx ? EPI_PLANES : 0);
   if (p.act == 2 || p.rowscale) {
     set_error("gemm_x6: unsupported epilogue");
     return MSFNO_EUNSUPPORTED;
@@ -316,6 +341,12 @@ static int launch_x6(const GemmParams& p, dim3 grid, hipStream_t s) {
     case EPI_ADD: launch_x6_e<BM, BN, WGM, WGN, EPI_ADD>(p, grid, s); break;
     case EPI_BIAS | EPI_ADD | EPI_GELU:
       launch_x6_e<BM, BN, WGM, WGN, EPI_BIAS | EPI_ADD | EPI_GELU>(p, grid, s); break;
+    case EPI_PLANES: launch_x6_e<BM, BN, WGM, WGN, EPI_PLANES>(p, grid, s); break;
+    case EPI_RELU | EPI_PLANES: launch_x6_e<BM, BN, WGM, WGN, EPI_RELU | EPI_PLANES>(p, grid, s); break;
+    case EPI_BIAS | EPI_GELU | EPI_PLANES:
+      launch_x6_e<BM, BN, WGM, WGN, EPI_BIAS | EPI_GELU | EPI_PLANES>(p, grid, s); break;
+    case EPI_BIAS | EPI_ADD | EPI_GELU | EPI_PLANES:
+      launch_x6_e<BM, BN, WGM, WGN, EPI_BIAS | EPI_ADD | EPI_GELU | EPI_PLANES>(p, grid, s); break;
     default:
       set_error("gemm_x6: unsupported epilogue combination");
       return MSFNO_EUNSUPPORTED;
@@ -353,6 +384,16 @@ int gemm_x6(GemmTile tile, const float* A, const float* B, float* C, int M, int 
   p.rowscale = epi.rowscale;
   p.Ax = Ax; p.sAxp = (int64_t)Mp * Kp; p.sAx = sA == 0 ? 0 : 3 * p.sAxp; p.ldax = Kp;
   p.vecB = (ldb % 4 == 0) && (sB % 4 == 0) && ((reinterpret_cast<uintptr_t>(B) & 15) == 0);
+  p.Bx = epi.b_planes; p.sBxp = epi.b_plane_stride;
+  p.Cx = epi.c_planes; p.sCxp = epi.c_plane_stride;
+  if (p.Bx)
+    MSFNO_REQUIRE(ldb % 8 == 0 && sB % 8 == 0 && p.sBxp % 8 == 0 &&
+                      (reinterpret_cast<uintptr_t>(p.Bx) & 15) == 0,
+                  MSFNO_EINVAL, "gemm_x6: B planes need ld, strides % 8 == 0 and 16-B alignment");
+  if (p.Cx)
+    MSFNO_REQUIRE(ldc % 4 == 0 && sC % 4 == 0 && p.sCxp % 4 == 0 &&
+                      (reinterpret_cast<uintptr_t>(p.Cx) & 7) == 0,
+                  MSFNO_EINVAL, "gemm_x6: C planes need ld, strides % 4 == 0 and 8-B alignment");
   p.vecC = (ldc % 4 == 0) && (sC % 4 == 0) && ((reinterpret_cast<uintptr_t>(C) & 15) == 0) &&
            (!epi.addend || ((epi.ldd % 4 == 0) && (epi.sD % 4 == 0) &&
                             ((reinterpret_cast<uintptr_t>(epi.addend) & 15) == 0)));
@@ -380,6 +421,8 @@ int gemm_x6(GemmTile tile, const float* A, const float* B, float* C, int M, int 
 int gemm_dense(GemmRole role, GemmTile f32_tile, const float* A, const float* B, float* C, int M,
                int N, int K, int lda, int ldb, int ldc, int64_t sA, int64_t sB, int64_t sC,
                int batch, const GemmEpi& epi, void* ws, size_t ws_bytes, hipStream_t s) {
+  MSFNO_REQUIRE(!(epi.b_planes || epi.c_planes) || (gemm_use_x6() && ws), MSFNO_EINVAL,
+                "gemm_dense: plane operands need the x6 engine");
   if (gemm_use_x6() && ws && epi.act != 2 && !epi.rowscale)
     return gemm_x6(x6_tile(M, N, batch), A, B, C, M, N, K, lda, ldb, ldc, sA, sB, sC, batch, epi,
                    ws, ws_bytes, s);

@@ -5,5 +5,5 @@ cd "$(dirname "$0")/.."
 CS=modulated-spherical-fourier-neural-operator_amd/csrc
 LIB=modulated-spherical-fourier-neural-operator_amd/msfno_amd
 mkdir -p tools/bin
-/opt/rocm/bin/hipcc -O3 --offload-arch=gfx950 -std=c++17 -I $CS tools/gemm_x6_bench.hip \
+/opt/rocm/bin/hipcc -O3 --offload-arch=gfx950 -std=c++17 -Wno-unused-value -Wno-unused-result -I $CS tools/gemm_x6_bench.hip \
   -L $LIB -lmsfno -Wl,-rpath,'$ORIGIN/../../'$LIB -o tools/bin/gemm_x6_bench

@@ -16,7 +16,9 @@ static float frand(uint64_t& s) {
 }
 
 int main(int argc, char** argv) {
+  // usage: gemm_x6_bench [shape [x6 tile id]]  (tile only: run just that x6 config)
   const char* only = argc > 1 ? argv[1] : nullptr;
+  const int only_tile = argc > 2 ? atoi(argv[2]) : -1;
   const int P = 721 * 1440;
   size_t maxB = (size_t)512 * P;
   float *A, *B, *C, *D, *bias;
@@ -26,7 +28,7 @@ int main(int argc, char** argv) {
   hipMalloc(&C, maxB * 4);
   hipMalloc(&D, maxB * 4);
   hipMalloc(&bias, 4096 * 4);
-  const size_t wsb = gemm_x6_workspace(1024, 1024, 1);
+  const size_t wsb = gemm_x6_workspace(1024, 4096, 1);
   hipMalloc(&ws, wsb);
   uint64_t seed = 1;
   {
@@ -64,11 +66,15 @@ int main(int argc, char** argv) {
   for (auto& s : shapes) {
     if (only && std::string(s.n) != only) continue;
     const double fl = 2.0 * s.M * (double)P * s.K;
-    float ms = timeit([&] {
-      gemm_uniform(s.t32, A, B, C, s.M, P, s.K, s.K, P, P, 0, 0, 0, 1, s.e, 0);
-    });
-    printf("%-9s f32  tile=%d: %.3f ms %.1f TF/s\n", s.n, (int)s.t32, ms, fl / ms / 1e9);
+    float ms;
+    if (only_tile < 0) {
+      ms = timeit([&] {
+        gemm_uniform(s.t32, A, B, C, s.M, P, s.K, s.K, P, P, 0, 0, 0, 1, s.e, 0);
+      });
+      printf("%-9s f32  tile=%d: %.3f ms %.1f TF/s\n", s.n, (int)s.t32, ms, fl / ms / 1e9);
+    }
     for (GemmTile t : {TILE_128x128, TILE_256x128, TILE_128x256, TILE_256x256}) {
+      if (only_tile >= 0 && (int)t != only_tile) continue;
       ms = timeit([&] {
         gemm_x6(t, A, B, C, s.M, P, s.K, s.K, P, P, 0, 0, 0, 1, s.e, ws, wsb, 0);
       });
@@ -76,7 +82,54 @@ int main(int argc, char** argv) {
              fl / ms / 1e9);
     }
   }
+  // custom x6p shape: gemm_x6_bench x6p M N K [epi: 0 none, 1 bias, 3 bias+add]
+  if (only && std::string(only) == "x6p" && argc >= 6) {
+    const int M = atoi(argv[2]), N = atoi(argv[3]), K = atoi(argv[4]), ep = argc > 5 ? atoi(argv[5]) : 0;
+    const int ldp = (N + 7) / 8 * 8;
+    unsigned short* Bp;
+    hipMalloc(&Bp, (size_t)3 * K * ldp * 2);
+    launch_split_planes(B, Bp, K, N, N, 0, ldp, (int64_t)K * ldp, 0, 1, 0);
+    GemmEpi e;
+    if (ep & 1) e.bias = bias;
+    if (ep & 2) { e.addend = D; e.ldd = N; }
+    e.b_planes = Bp;
+    e.b_plane_stride = (int64_t)K * ldp;
+    const double fl = 2.0 * M * (double)N * K;
+    float ms = timeit([&] { gemm_x6p(A, C, M, N, K, K, ldp, N, 0, 0, 0, 1, e, ws, wsb, 0); });
+    printf("x6p M=%d N=%d K=%d epi=%d: %.3f ms %.1f TF/s (fp32-equivalent)\n", M, N, K, ep, ms,
+           fl / ms / 1e9);
+    return 0;
+  }
+  // x6p (both operands as bf16x3 planes, LDS-DMA ring): fc2 shape, B = h planes
+  if (!only || std::string(only) == "fc2p" || std::string(only) == "fc1p") {
+    const bool f1 = only && std::string(only) == "fc1p";
+    const int M = f1 ? 512 : 256, K = f1 ? 256 : 512;
+    const int ldp = (P + 7) / 8 * 8;
+    unsigned short* Bp;
+    hipMalloc(&Bp, (size_t)3 * K * ldp * 2);
+    launch_split_planes(B, Bp, K, P, P, 0, ldp, (int64_t)K * ldp, 0, 1, 0);
+    GemmEpi e = f1 ? gelu : badd;
+    e.b_planes = Bp;
+    e.b_plane_stride = (int64_t)K * ldp;
+    const double fl = 2.0 * M * (double)P * K;
+    float ms = timeit([&] { gemm_x6p(A, C, M, P, K, K, ldp, P, 0, 0, 0, 1, e, ws, wsb, 0); });
+    printf("%-9s x6p  256x256: %.3f ms %.1f TF/s (fp32-equivalent)\n", f1 ? "fc1p" : "fc2p", ms,
+           fl / ms / 1e9);
+    GemmEpi e0 = f1 ? gelu : badd;
+    gemm_x6(TILE_256x256, A, B, D, M, P, K, K, P, P, 0, 0, 0, 1, e0, ws, wsb, 0);
+    std::vector<float> h1((size_t)M * P), h2((size_t)M * P);
+    hipMemcpy(h1.data(), C, h1.size() * 4, hipMemcpyDeviceToHost);
+    hipMemcpy(h2.data(), D, h2.size() * 4, hipMemcpyDeviceToHost);
+    double dmax = 0, vmax = 0;
+    for (size_t i = 0; i < h1.size(); ++i) {
+      dmax = std::max(dmax, (double)std::fabs(h1[i] - h2[i]));
+      vmax = std::max(vmax, (double)std::fabs(h2[i]));
+    }
+    printf("x6p vs x6: max|diff| %.3e (max|C| %.3e)\n", dmax, vmax);
+    hipFree(Bp);
+  }
   if (hipGetLastError() != hipSuccess) { printf("launch error\n"); return 1; }
+  if (only_tile >= 0) return 0;
   // accuracy: M=256 N=4100 (ragged) K=520 (ragged), plain epilogue
   {
     const int M = 256, N = 4100, K = 520;
