@@ -490,11 +490,27 @@ int run_filter(const msfno_block_desc* d, msfno_sht_plan_s* f, msfno_sht_plan_s*
     prof(ST_SPEC_PREP, s);
     const bool x6 = spec_use_x6() && b.dw.spec[0];
     const bool c3m = !x6 && use_c3m();
+    const bool split_l0 = x6 && C <= Hs;  // layer 0 input split into Sc (below)
+    if (x6) {
+      // every layer's real-ified weight straight into its x6p A image, one launch
+      SpecWeightsX6p sw{};
+      sw.nlayers = nl + 1;
+      for (int l = 0; l <= nl; ++l) {
+        sw.w[l] = (l == nl) ? d->spec_wout : d->spec_w[l];
+        MSFNO_REQUIRE(sw.w[l], MSFNO_EINVAL, "missing spectral weight");
+        sw.ci[l] = (l == 0) ? (int)C : (int)Hs;
+        sw.co[l] = (l == nl) ? (int)C : (int)Hs;
+        sw.out[l] = static_cast<unsigned short*>(b.dw.spec[l]);
+      }
+      spec_weights_x6p_layout(sw);
+      MSFNO_TRY(launch_spec_weights_x6p(sw, s));
+    }
     for (int l = 0; l <= nl; ++l) {
       const int ci = (l == 0) ? (int)C : (int)Hs;
       const int co = (l == nl) ? (int)C : (int)Hs;
       const float* w = (l == nl) ? d->spec_wout : d->spec_w[l];
       MSFNO_REQUIRE(w, MSFNO_EINVAL, "missing spectral weight");
+      if (x6 && (l > 0 || split_l0)) continue;  // prepared above
       if (c3m)
         MSFNO_TRY(launch_split_complex_weight(w, b.Wexp[l], b.Wexp[l] + (int64_t)ci * co, ci, co, s));
       else
@@ -522,7 +538,19 @@ int run_filter(const msfno_block_desc* d, msfno_sht_plan_s* f, msfno_sht_plan_s*
         }
         const int ldc = l < nl ? (int)ldTx : (int)L.ldT;
         const int64_t sC = l < nl ? 3 * 2LL * co * ldTx : 2LL * co * L.ldT;
-        if (l == 0) {
+        if (l > 0 || split_l0) e.a_planes = static_cast<const unsigned short*>(b.dw.spec[l]);
+        if (l == 0 && split_l0) {  // Sc is free during layer 0
+          // layer 0's fp32 input (the forward Legendre output) -> planes in Sc: one
+          // streaming pass, then the LDS-DMA kernel (cheaper than splitting the
+          // 2C x T operand once per M-tile inside the GEMM)
+          unsigned short* inx = reinterpret_cast<unsigned short*>(b.Sc);
+          MSFNO_TRY(launch_split_planes(in, inx, 2 * ci, (int)L.Tp, (int)L.ldT, 2LL * ci * L.ldT,
+                                        (int)ldTx, 2LL * ci * ldTx, 3 * 2LL * ci * ldTx, B, s));
+          e.b_planes = inx;
+          e.b_plane_stride = 2LL * ci * ldTx;
+          MSFNO_TRY(gemm_x6p(b.Wexp[l], out, 2 * co, (int)L.Tp, 2 * ci, 2 * ci, (int)ldTx, ldc, 0,
+                             3 * 2LL * ci * ldTx, sC, B, e, b.dw.spec[l], b.dw.spec_b[l], s));
+        } else if (l == 0) {
           MSFNO_TRY(gemm_dense(ROLE_SPEC, TILE_128x128, b.Wexp[l], in, out, 2 * co, (int)L.Tp,
                                2 * ci, 2 * ci, (int)L.ldT, ldc, 0, 2LL * ci * L.ldT, sC, B, e,
                                b.dw.spec[l], b.dw.spec_b[l], s));

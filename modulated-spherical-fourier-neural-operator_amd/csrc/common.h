@@ -137,6 +137,9 @@ struct GemmEpi {
   int64_t b_plane_stride = 0;
   unsigned short* c_planes = nullptr;
   int64_t c_plane_stride = 0;
+  // gemm_x6p only: A already split into its image ([3][KT][Mp][16], e.g. by
+  // launch_spec_weights_x6p); the fp32 A pointer and the workspace are unused
+  const unsigned short* a_planes = nullptr;
 };
 
 enum GemmTile {
@@ -173,6 +176,18 @@ size_t gemm_x6p_workspace(int M, int K, int batch_a);
 int gemm_x6p(const float* A, float* C, int M, int N, int K, int lda, int ldb, int ldc,
              int64_t sA, int64_t sB, int64_t sC, int batch, const GemmEpi& epi, void* ws,
              size_t ws_bytes, hipStream_t s);
+// all spectral-MLP weights of a block -> x6p A images in one launch: fill w, ci,
+// co, out (each >= gemm_x6p_workspace(2 co, 2 ci, 1) bytes) and nlayers, then
+// spec_weights_x6p_layout (fills start[], returns the bytes the images need)
+struct SpecWeightsX6p {
+  const float* w[9];
+  unsigned short* out[9];
+  int ci[9], co[9];
+  int64_t start[10];  // pair offsets of each layer in the flattened index space
+  int nlayers;
+};
+size_t spec_weights_x6p_layout(SpecWeightsX6p& a);
+int launch_spec_weights_x6p(const SpecWeightsX6p& a, hipStream_t s);
 // fp32 x[z][r][c] (ld ldx, batch stride sx) -> bf16x3 planes xp[z][plane][r][c]
 int launch_split_planes(const float* x, unsigned short* xp, int rows, int cols, int ldx,
                         int64_t sx, int ldp, int64_t pstride, int64_t sxp, int batch,

@@ -72,6 +72,45 @@ __global__ void split_a_tiles_kernel(const float* __restrict__ A, unsigned short
   }
 }
 
+// All spectral-MLP weights of a block in one launch: layer l's complex weight
+// w (ci, co, 2) (SpectralAttentionS2 w.l / wout, layers.py:580-596) real-ified to
+// [[Wr, -Wi], [Wi, Wr]] (2 co x 2 ci) and split straight into the x6p A image.
+__global__ void spec_weights_x6p_kernel(SpecWeightsX6p a) {
+  const int64_t total = a.start[a.nlayers];
+  for (int64_t g = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; g < total;
+       g += (int64_t)gridDim.x * blockDim.x) {
+    int l = 0;
+    while (l + 1 < a.nlayers && g >= a.start[l + 1]) ++l;
+    const int ci = a.ci[l], co = a.co[l];
+    const int M = 2 * co, K = 2 * ci;
+    const int Mp = (M + X6P_BM - 1) / X6P_BM * X6P_BM, KT = (K + X6P_BK - 1) / X6P_BK;
+    const int64_t n = (int64_t)Mp * KT * 8;  // pairs per plane
+    const int64_t e = g - a.start[l];
+    const int64_t idx = 2 * e;
+    const int kt = (int)(idx / ((int64_t)Mp * 16));
+    const int rem = (int)(idx - (int64_t)kt * Mp * 16);
+    const int m = rem >> 4, k0 = kt * 16 + (rem & 15);
+    float v[2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const int k = k0 + t;
+      float x = 0.f;
+      if (m < M && k < K) {
+        const int ro = m / co, o = m - ro * co, ri = k / ci, i = k - ri * ci;
+        const float wr = a.w[l][((int64_t)i * co + o) * 2], wi = a.w[l][((int64_t)i * co + o) * 2 + 1];
+        x = ro == 0 ? (ri == 0 ? wr : -wi) : (ri == 0 ? wi : wr);
+      }
+      v[t] = x;
+    }
+    uint32_t t0, t1, t2;
+    split2(v[0], v[1], t0, t1, t2);
+    uint32_t* o = reinterpret_cast<uint32_t*>(a.out[l]) + e;
+    o[0] = t0;
+    o[n] = t1;
+    o[2 * n] = t2;
+  }
+}
+
 // fp32 rows -> bf16x3 planes: x[z][r][c] (ld ldx, batch stride sx) ->
 // xp[z][plane][r][c] (ld ldp, plane stride pstride, batch stride sxp)
 __global__ void split_planes_kernel(const float* __restrict__ x, unsigned short* __restrict__ xp,
@@ -275,6 +314,25 @@ size_t gemm_x6p_workspace(int M, int K, int batch_a) {
   return (size_t)round_up(3 * Mp * Kp * 2 * (int64_t)batch_a, 256);
 }
 
+int launch_spec_weights_x6p(const SpecWeightsX6p& a, hipStream_t s) {
+  if (a.nlayers <= 0) return MSFNO_OK;
+  const int blocks = (int)std::min<int64_t>(cdiv(a.start[a.nlayers], 256), 4096);
+  hipLaunchKernelGGL(spec_weights_x6p_kernel, dim3(blocks), dim3(256), 0, s, a);
+  return launch_check("spec_weights_x6p");
+}
+
+size_t spec_weights_x6p_layout(SpecWeightsX6p& a) {
+  size_t bytes = 0;
+  a.start[0] = 0;
+  for (int l = 0; l < a.nlayers; ++l) {
+    const size_t b = gemm_x6p_workspace(2 * a.co[l], 2 * a.ci[l], 1);
+    a.start[l + 1] = a.start[l] + (int64_t)round_up(2 * a.co[l], X6P_BM) *
+                                      cdiv(2 * a.ci[l], X6P_BK) * 8;
+    bytes += b;
+  }
+  return bytes;
+}
+
 int launch_split_planes(const float* x, unsigned short* xp, int rows, int cols, int ldx,
                         int64_t sx, int ldp, int64_t pstride, int64_t sxp, int batch,
                         hipStream_t s) {
@@ -298,8 +356,9 @@ int gemm_x6p(const float* A, float* C, int M, int N, int K, int lda, int ldb, in
              size_t ws_bytes, hipStream_t s) {
   if (M <= 0 || N <= 0 || batch <= 0) return MSFNO_OK;
   const int abatch = sA == 0 ? 1 : batch;
-  MSFNO_REQUIRE(ws && ws_bytes >= gemm_x6p_workspace(M, K, abatch), MSFNO_EINVAL,
-                "gemm_x6p: workspace too small");
+  MSFNO_REQUIRE(epi.a_planes || (ws && ws_bytes >= gemm_x6p_workspace(M, K, abatch)),
+                MSFNO_EINVAL, "gemm_x6p: workspace too small");
+  MSFNO_REQUIRE(!epi.a_planes || sA == 0, MSFNO_EINVAL, "gemm_x6p: pre-split A is not batched");
   MSFNO_REQUIRE(epi.b_planes, MSFNO_EINVAL, "gemm_x6p: B must be in the plane format");
   MSFNO_REQUIRE(batch <= 65535 && K > 0, MSFNO_EINVAL, "gemm_x6p: bad batch / K");
   MSFNO_REQUIRE(ldb % 8 == 0 && ldb >= 8 && sB % 8 == 0 && epi.b_plane_stride % 8 == 0 &&
@@ -309,7 +368,9 @@ int gemm_x6p(const float* A, float* C, int M, int N, int K, int lda, int ldb, in
                 "gemm_x6p: unsupported epilogue");
   const int Mp = (int)round_up(M, X6P_BM), KT = (int)cdiv(K, X6P_BK);
   unsigned short* Ax = static_cast<unsigned short*>(ws);
-  {
+  if (epi.a_planes) {
+    Ax = const_cast<unsigned short*>(epi.a_planes);  // already in the A image layout
+  } else {
     const int64_t pairs = (int64_t)Mp * KT * 8;
     const int blocks = (int)std::min<int64_t>(cdiv(pairs, 256), 1024);
     hipLaunchKernelGGL(split_a_tiles_kernel, dim3(blocks, abatch), dim3(256), 0, s, A, Ax, M, K,
