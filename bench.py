@@ -52,9 +52,11 @@ SIDE_STAGES = {"inner_skip"}
 # template instantiations in the block (x6 engine, 256x256 tiles; f32 engine kept
 # for MSFNO_GEMM=f32)
 STAGE_KERNEL_X6 = {
-    "mlp_fc1": "void msfno::gemm_x6_kernel<256, 256, 4, 2, true, 5>(msfno::GemmParams)",
-    "mlp_fc2": "void msfno::gemm_x6_kernel<256, 256, 4, 2, true, 3>(msfno::GemmParams)",
-    "inner_skip": "void msfno::gemm_x6_kernel<256, 256, 4, 2, true, 1>(msfno::GemmParams)",
+    # fc1: fp32 B split in-kernel, bias + GELU, h written as bf16x3 planes (EPI 133)
+    "mlp_fc1": "void msfno::gemm_x6_kernel<256, 256, 4, 2, true, 133, false>(msfno::GemmParams)",
+    # fc2: h planes staged by LDS-DMA (x6p), bias + outer skip (EPI 3)
+    "mlp_fc2": "void msfno::gemm_x6p_kernel<3>(msfno::GemmParams)",
+    "inner_skip": "void msfno::gemm_x6_kernel<256, 256, 4, 2, true, 1, false>(msfno::GemmParams)",
 }
 STAGE_KERNEL_F32 = {
     "mlp_fc1": "void msfno::gemm_f32_kernel<128, 256, 16, true, 5>(msfno::GemmParams)",

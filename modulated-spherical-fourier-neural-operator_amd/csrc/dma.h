@@ -1,0 +1,48 @@
+// LDS-DMA helpers (global_load_lds) as inline asm, for gfx950.
+//
+// hipcc counts a __builtin_amdgcn_global_load_lds as a pending write of the
+// whole LDS array and drains it (vmcnt(0)) before later ds_reads it cannot
+// prove disjoint; in a ring / double-buffered structure that serialises the
+// prefetch.  As inline asm the DMA is invisible to hipcc's waitcnt pass, so the
+// kernel owns its completion: a counted `s_waitcnt vmcnt(N)` (N = vector-memory
+// instructions the wave issued after the DMA), plus a barrier when other waves
+// read the data (cdna_hip_programming.md §5.7).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+namespace msfno {
+
+typedef __attribute__((address_space(3))) void lds_void_t;
+
+// LDS byte address of a pointer into __shared__ memory
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {
+  return (uint32_t)(uintptr_t)(lds_void_t*)p;
+}
+
+// one wave-instruction: lane l copies 16 B from gsrc to LDS byte (lds + 16 l);
+// lds must be wave-uniform
+__device__ __forceinline__ void glds16(const void* gsrc, uint32_t lds) {
+  unsigned keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(gsrc), "s"(__builtin_amdgcn_readfirstlane(lds))
+      : "memory");
+}
+
+// s_waitcnt vmcnt(n) for a run-time n, rounded down to a supported immediate
+// (waiting for more than needed is safe)
+__device__ __forceinline__ void wait_vmcnt(int n) {
+  if (n >= 12) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+  else if (n >= 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else if (n >= 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  else if (n >= 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  else if (n >= 3) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+  else if (n >= 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+  else if (n >= 1) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+}  // namespace msfno

@@ -13,6 +13,7 @@
 #include <cmath>
 #include <cstdlib>
 
+#include "dma.h"
 #include "kernels.h"
 
 namespace msfno {
@@ -577,6 +578,213 @@ __global__ __launch_bounds__(256) void fft_c2r_rows_kernel(const float2* __restr
 }
 
 // ---------------------------------------------------------------------------
+// LDS-DMA row kernels (compiled codelets, N % 8 == 0; the block's path).  Each
+// wave keeps its next row in flight as an asynchronous global->LDS copy
+// (dma.h) while it transforms the current one, so the HBM latency is covered
+// without parking rows in VGPRs: the register-prefetch kernels above hold ~3
+// workgroups per CU and their waves wait on memory most of the time (the
+// inverse one also reads its skip-branch row synchronously).  The FFT runs in
+// place in the LDS row the DMA filled; both twiddle tables live in LDS (a
+// global twiddle read would make hipcc drain the copies in flight).
+// ---------------------------------------------------------------------------
+template <class CL, int WV>
+__global__ __launch_bounds__(64 * WV) void fft_r2c_dma_kernel(const float* __restrict__ x,
+                                                              float2* __restrict__ out,
+                                                              float2* __restrict__ rowstats,
+                                                              int64_t rows, int mmax, float scale,
+                                                              FFTArgs f) {
+  constexpr int H = CL::H, N = 2 * H, RB = N * 4;
+  constexpr int NCH = (RB + 1023) / 1024;  // DMA wave-instructions per row
+  constexpr int SLOT = NCH * 1024;
+  constexpr int NS = 3;                    // row slots per wave: 2 rows in flight
+  extern __shared__ float2 smem[];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  float2* tw = smem;
+  float2* twN = smem + H;
+  char* slots = reinterpret_cast<char*>(smem + 2 * H + 2) + (size_t)w * NS * SLOT;
+  for (int t = threadIdx.x; t < H; t += blockDim.x) tw[t] = f.twH[t];
+  for (int t = threadIdx.x; t <= H; t += blockDim.x) twN[t] = f.twN[t];
+  __syncthreads();
+  const int64_t stride = (int64_t)gridDim.x * WV;
+  const int64_t row0 = (int64_t)blockIdx.x * WV + w;
+  auto issue = [&](int64_t r, int sl) {
+    const char* src = reinterpret_cast<const char*>(x + r * N);
+    const uint32_t dst = lds_addr(slots + sl * SLOT);
+#pragma unroll
+    for (int c = 0; c < NCH; ++c)
+      glds16(src + min(c * 1024 + lane * 16, RB - 16), dst + c * 1024);
+  };
+  if (row0 < rows) issue(row0, 0);
+  if (row0 + stride < rows) issue(row0 + stride, 1);
+  const int nst = (mmax + 63) / 64 + (rowstats ? 1 : 0);  // vector stores per row
+  int sl = 0;
+  int i = 0;
+  for (int64_t row = row0; row < rows; row += stride, ++i) {
+    // this row's copy has landed: count what this wave issued after it (the next
+    // row's copy, if any, and the stores of the previous one or two rows)
+    const bool next = row + stride < rows;
+    wait_vmcnt((i >= 2 ? nst : 0) + (next ? NCH : 0) + (i >= 1 ? nst : 0));
+    if (row + 2 * stride < rows) issue(row + 2 * stride, sl == 0 ? 2 : sl - 1);
+    float2* buf = reinterpret_cast<float2*>(slots + sl * SLOT);
+    if (rowstats) {
+      float s = 0.f;
+      for (int n = lane; n < H; n += 64) s += buf[n].x + buf[n].y;
+      const float mean = wave_sum(s) / (float)N;
+      float q = 0.f;
+      for (int n = lane; n < H; n += 64) {
+        const float2 v = buf[n];
+        q += (v.x - mean) * (v.x - mean) + (v.y - mean) * (v.y - mean);
+      }
+      q = wave_sum(q);
+      if (lane == 0) rowstats[row] = make_float2(mean, q);
+    }
+    CL::template run<false>(buf, nullptr, f, tw, lane);
+    float2* o = out + row * mmax;
+    for (int k = lane; k < mmax; k += 64) {
+      const float2 zk = buf[k % H];
+      const float2 zc = cconj(buf[(H - k) % H]);
+      const float2 E = make_float2(0.5f * (zk.x + zc.x), 0.5f * (zk.y + zc.y));
+      const float2 D = csub(zk, zc);
+      const float2 O = make_float2(0.5f * D.y, -0.5f * D.x);  // D / (2i)
+      const float2 X = cadd(E, cmul(twN[k], O));
+      o[k] = make_float2(scale * X.x, scale * X.y);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    sl = sl == 2 ? 0 : sl + 1;
+  }
+}
+
+// inverse: Yn row (mmax bins, DMA from the 16-B aligned address below the row
+// start) and, with ADD, the skip-branch row x1 (x = act(x1 + irfft)); output
+// rows stored from registers, row stats for InstanceNorm-1.  AH (1 or 2) rows in
+// flight per wave (AH Yn and AH skip slots).  Measured at 721x1440: one row ahead
+// with two 4-wave workgroups per CU beats two rows ahead with one 6-wave one
+// (0.81 vs 0.98 ms): the row FFT itself is VALU/LDS-latency bound, so waves per
+// CU matter more than bytes in flight.
+template <class CL, bool ADD, int WV, int AH>
+__global__ __launch_bounds__(64 * WV) void fft_c2r_dma_kernel(const float2* __restrict__ in,
+                                                              float* x, const float* addsrc,
+                                                              float2* __restrict__ rowstats,
+                                                              int64_t rows, int mmax, int act,
+                                                              int ncy, FFTArgs f) {
+  constexpr int H = CL::H, N = 2 * H, RB = N * 4;
+  constexpr int NCA = (RB + 1023) / 1024;  // DMA instructions per skip row
+  constexpr int NST = (N / 4 + 63) / 64;   // float4 store instructions per row
+  extern __shared__ float2 smem[];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  float2* tw = smem;
+  float2* twN = smem + H;
+  const int YS = ncy * 1024;
+  const int per = RB + AH * YS + (ADD ? AH * NCA * 1024 : 0);
+  char* wb = reinterpret_cast<char*>(smem + 2 * H + 2) + (size_t)w * per;
+  float2* buf = reinterpret_cast<float2*>(wb);
+  char* yst = wb + RB;                  // AH slots of YS
+  char* ast = wb + RB + AH * YS;        // AH slots of NCA KB
+  for (int t = threadIdx.x; t < H; t += blockDim.x) tw[t] = f.twH[t];
+  for (int t = threadIdx.x; t <= H; t += blockDim.x) twN[t] = f.twN[t];
+  __syncthreads();
+  const int64_t stride = (int64_t)gridDim.x * WV;
+  const int YB = mmax * 8;
+  const int64_t yend = (((int64_t)rows * YB) & ~(int64_t)15) - 16;  // last chunk inside Yn
+  auto issue_y = [&](int64_t r, int sl) {
+    const int64_t a0 = ((int64_t)r * YB) & ~(int64_t)15;
+    const char* src = reinterpret_cast<const char*>(in);
+    const uint32_t dst = lds_addr(yst + sl * YS);
+    for (int c = 0; c < ncy; ++c)
+      glds16(src + min(a0 + c * 1024 + lane * 16, yend), dst + c * 1024);
+  };
+  auto issue_a = [&](int64_t r, int sl) {
+    const char* src = reinterpret_cast<const char*>(addsrc + r * N);
+    const uint32_t dst = lds_addr(ast + sl * NCA * 1024);
+#pragma unroll
+    for (int c = 0; c < NCA; ++c)
+      glds16(src + min(c * 1024 + lane * 16, RB - 16), dst + c * 1024);
+  };
+  const int64_t row0 = (int64_t)blockIdx.x * WV + w;
+  if (row0 < rows) {
+    issue_y(row0, 0);
+    if constexpr (ADD) issue_a(row0, 0);
+  }
+  if (AH == 2 && row0 + stride < rows) {
+    issue_y(row0 + stride, 1);
+    if constexpr (ADD) issue_a(row0 + stride, 1);
+  }
+  const int nst = NST + (rowstats ? 1 : 0);
+  const int na = ADD ? NCA : 0;
+  int i = 0;
+  for (int64_t row = row0; row < rows; row += stride, ++i) {
+    const int sl = AH == 2 ? (i & 1) : 0;
+    const bool e1 = row + stride < rows, e2 = row + 2 * stride < rows;
+    // Yn(row) landed: count what this wave issued after it (dma.h)
+    if (AH == 2)
+      wait_vmcnt((i >= 2 ? nst : 0) + na + (i >= 1 ? nst : 0) + (e1 ? ncy + na : 0));
+    else
+      wait_vmcnt(na + (i >= 1 ? nst : 0));
+    const float2* yr = reinterpret_cast<const float2*>(yst + sl * YS) + (((int64_t)row * YB) & 15) / 8;
+    for (int k = lane; k < H; k += 64) {
+      float2 xk = k < mmax ? yr[k] : make_float2(0.f, 0.f);
+      if (k == 0) xk.y = 0.f;
+      const int k2 = H - k;
+      float2 xh = k2 < mmax ? yr[k2] : make_float2(0.f, 0.f);
+      if (k2 == H || k2 == 0) xh.y = 0.f;  // DC / Nyquist imaginary parts are ignored
+      const float2 xc = cconj(xh);
+      const float2 A = cadd(xk, xc);
+      const float2 D = csub(xk, xc);
+      const float2 T = cmul(cconj(twN[k]), D);
+      buf[k] = make_float2(A.x - T.y, A.y + T.x);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    if (AH == 2 ? e2 : e1) issue_y(row + AH * stride, sl);  // this Yn slot was consumed above
+    CL::template run<true>(buf, nullptr, f, tw, lane);
+    if constexpr (ADD) {  // skip row landed
+      if (AH == 2)
+        wait_vmcnt((e1 ? ncy + na : 0) + (i >= 1 ? nst : 0) + (e2 ? ncy : 0));
+      else
+        wait_vmcnt(e1 ? ncy : 0);
+    }
+    const float4* a4 = reinterpret_cast<const float4*>(ast + sl * NCA * 1024);
+    float4* x4 = reinterpret_cast<float4*>(x + row * N);
+    float s = 0.f;
+#pragma unroll
+    for (int j = 0; j < NST; ++j) {
+      const int n = lane + 64 * j;
+      if (n < N / 4) {
+        float2 a = buf[2 * n], b = buf[2 * n + 1];
+        if constexpr (ADD) {
+          const float4 r = a4[n];
+          a.x += r.x; a.y += r.y; b.x += r.z; b.y += r.w;
+        }
+        if (act == 1) {
+          a.x = gelu_erf_f(a.x); a.y = gelu_erf_f(a.y);
+          b.x = gelu_erf_f(b.x); b.y = gelu_erf_f(b.y);
+        }
+        if (ADD || act == 1) {
+          buf[2 * n] = a;
+          buf[2 * n + 1] = b;
+        }
+        x4[n] = make_float4(a.x, a.y, b.x, b.y);
+        s += (a.x + a.y) + (b.x + b.y);
+      }
+    }
+    if (rowstats) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+      const float mean = wave_sum(s) / (float)N;
+      float q = 0.f;
+      for (int n = lane; n < H; n += 64) {
+        const float2 v = buf[n];
+        q += (v.x - mean) * (v.x - mean) + (v.y - mean) * (v.y - mean);
+      }
+      q = wave_sum(q);
+      if (lane == 0) rowstats[row] = make_float2(mean, q);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    if constexpr (ADD) {
+      if (AH == 2 ? e2 : e1) issue_a(row + AH * stride, sl);  // this skip slot was consumed
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Fused FFT + transpose kernels (the block's path).  A workgroup owns TK
 // consecutive latitudes of one (b,c) plane; each wave transforms TK/4 rows with
 // the next row's global loads in flight (register prefetch) while it computes.
@@ -815,9 +1023,47 @@ using FFT32 = FixedFFT<4, 4>;             // nlon 32
   X(5, FFT180)                \
   X(6, FFT32)
 
+// LDS-DMA row kernels for compiled codelets (MSFNO_FFT_DMA=0: register-prefetch
+// kernels, kept for A/B)
+static bool use_fft_dma() {
+  static const bool on = [] {
+    const char* e = getenv("MSFNO_FFT_DMA");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
+static int set_lds_limit(const void* fn, size_t lds);
+
+// persistent grid of the DMA row kernels: one workgroup per CU
+static int64_t dma_grid() {
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        cus <= 0)
+      cus = 256;
+  }
+  return cus;
+}
+
 template <class CL>
 static int launch_r2c(const FFTArgs& a, const float* x, float2* out, float2* rowstats,
                       int64_t rows, int mmax, float scale, hipStream_t s) {
+  if constexpr (CL::H > 0) {
+    if (use_fft_dma() && (2 * CL::H) % 8 == 0 && mmax <= CL::H + 1) {
+      constexpr int WV = 8;  // one 8-wave workgroup per CU, 3 row slots per wave
+      const size_t slot = (size_t)((2 * CL::H * 4 + 1023) / 1024) * 1024;
+      const size_t lds = (size_t)(2 * CL::H + 2) * sizeof(float2) + WV * 3 * slot;
+      MSFNO_REQUIRE(lds <= 160 * 1024, MSFNO_EUNSUPPORTED, "nlon too large for the LDS FFT");
+      MSFNO_TRY(set_lds_limit(reinterpret_cast<const void*>(&fft_r2c_dma_kernel<CL, WV>), lds));
+      const int64_t grid = std::min<int64_t>(cdiv(rows, WV), dma_grid());
+      hipLaunchKernelGGL((fft_r2c_dma_kernel<CL, WV>), dim3((unsigned)grid), dim3(64 * WV), lds,
+                         s, x, out, rowstats, rows, mmax, scale, a);
+      return launch_check("fft_r2c_dma");
+    }
+  }
   const size_t lds = (size_t)(kWaves * CL::kBufs + 1) * a.H * sizeof(float2);
   MSFNO_REQUIRE(lds <= 64 * 1024, MSFNO_EUNSUPPORTED, "nlon too large for the LDS FFT");
   hipLaunchKernelGGL((fft_r2c_rows_kernel<CL>), dim3((unsigned)fft_grid(rows)), dim3(256), lds, s,
@@ -828,6 +1074,30 @@ static int launch_r2c(const FFTArgs& a, const float* x, float2* out, float2* row
 template <class CL>
 static int launch_c2r(const FFTArgs& a, const float2* in, float* x, const float* addsrc,
                       float2* rowstats, int64_t rows, int mmax, int act, hipStream_t s) {
+  if constexpr (CL::H > 0) {
+    const int ncy = (mmax * 8 + 16 + 1023) / 1024;
+    if (use_fft_dma() && (2 * CL::H) % 8 == 0 && mmax <= CL::H + 1 && ncy <= 5) {
+      const int rb = 2 * CL::H * 4, nca = (rb + 1023) / 1024;
+      // one row ahead, 4-wave workgroups, as many per CU as the LDS holds
+      const size_t per = (size_t)rb + ncy * 1024 + (addsrc ? nca * 1024 : 0);
+      const size_t tw = (size_t)(2 * CL::H + 2) * sizeof(float2);
+      const int wg_cu = (int)std::max<size_t>(1, (160 * 1024) / (tw + 4 * per));
+      MSFNO_REQUIRE(tw + 4 * per <= 160 * 1024, MSFNO_EUNSUPPORTED, "nlon too large for the LDS FFT");
+      auto go = [&](auto kern, int WV) -> int {
+        const size_t lds = tw + WV * per;
+        MSFNO_TRY(set_lds_limit(reinterpret_cast<const void*>(kern), lds));
+        const int64_t grid = std::min<int64_t>(cdiv(rows, WV), dma_grid() * wg_cu);
+        hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(64 * WV), lds, s, in, x, addsrc,
+                           rowstats, rows, mmax, act, ncy, a);
+        return MSFNO_OK;
+      };
+      if (addsrc)
+        MSFNO_TRY(go(fft_c2r_dma_kernel<CL, true, 4, 1>, 4));
+      else
+        MSFNO_TRY(go(fft_c2r_dma_kernel<CL, false, 4, 1>, 4));
+      return launch_check("fft_c2r_dma");
+    }
+  }
   const size_t lds =
       ((size_t)(kWaves * CL::kBufs + 1) * a.H + (CL::H > 0 ? kWaves * kStageMax : 0)) *
       sizeof(float2);
