@@ -413,6 +413,7 @@ void carve_block(Carve& cv, BlockBufs& b, const msfno_block_desc* d,
   b.x1 = nullptr;
   b.st1 = nullptr;
   b.sc1 = b.sh1 = b.W1f = b.b1f = b.h = nullptr;
+  b.x1p = nullptr;
   if (!with_norms) return;
   b.x1 = cv.take<float>(BC * P);
   b.st1 = cv.take<float2>(BC * g->nlat);
@@ -424,6 +425,7 @@ void carve_block(Carve& cv, BlockBufs& b, const msfno_block_desc* d,
     b.b1f = cv.take<float>((int64_t)B * Hd);
     b.h = cv.take<float>(mlp_h_floats(B, Hd, P));
   }
+  b.x1p = x1_planes(d, g) ? cv.take<unsigned short>(BC * 3 * P) : nullptr;
   carve_dense_ws(cv, b.dw, d, B);
 }
 
@@ -632,7 +634,8 @@ int run_spectral(const msfno_block_desc* d, msfno_sht_plan_s* f, msfno_sht_plan_
 
 // Yt -> spatial rows (fused transpose + irfft when enabled); out = act(addsrc + irfft)
 int run_inverse_fft(msfno_sht_plan_s* g, const BlockBufs& b, int B, int C, float* out,
-                           const float* addsrc, float2* rowstats, int act, hipStream_t s) {
+                           const float* addsrc, float2* rowstats, int act, hipStream_t s,
+                           unsigned short* planes = nullptr) {
   const int64_t BC = (int64_t)B * C;
   if (use_fft_tile(g) && addsrc == nullptr) {
     prof(ST_FFT_INV, s);
@@ -642,8 +645,12 @@ int run_inverse_fft(msfno_sht_plan_s* g, const BlockBufs& b, int B, int C, float
   prof(ST_TRANSPOSE_INV, s);
   MSFNO_TRY(transpose_inv_plan(g, b.Yt, b.Yn, B, C, s));
   prof(ST_FFT_INV, s);
+  if (planes) {
+    const C2RPlanes pl{planes, C, g->nlat};
+    return launch_fft_c2r_rows(g->fft, b.Yn, out, addsrc, rowstats, BC * g->nlat, g->mmax, act,
+                               s, &pl);
+  }
   return launch_fft_c2r_rows(g->fft, b.Yn, out, addsrc, rowstats, BC * g->nlat, g->mmax, act, s);
-  return MSFNO_OK;
 }
 
 
@@ -715,7 +722,7 @@ int plan_create(int nlat, int nlon, int lmax, int mmax, int inverse,
 // (measured cheapest split: DESIGN.md §8).
 int run_mlp(const msfno_block_desc* d, const float* W1f, const float* b1f, const float* x1,
             float* h, float* out, const float* resid, int B, int64_t P, const DenseWs& dw,
-            hipStream_t s) {
+            hipStream_t s, const unsigned short* x1p) {
   const int64_t C = d->C, Hd = d->mlp_hidden;
   // x6 engine: h travels as bf16x3 planes [B][3][Hd][ldh] (fc1 splits it once in its
   // epilogue, fc2 stages it without conversion)
@@ -728,6 +735,13 @@ int run_mlp(const msfno_block_desc* d, const float* W1f, const float* b1f, const
   e1.sBias = Hd;
   e1.act = 1;
   if (planes) { e1.c_planes = hx; e1.c_plane_stride = Hd * ldh; }
+  if (planes && x1p) {
+    // x1 arrives as planes from the inverse FFT: LDS-DMA GEMM (per-field folded W1)
+    e1.b_planes = x1p;
+    e1.b_plane_stride = C * P;
+    MSFNO_TRY(gemm_x6p(W1f, h, (int)Hd, (int)P, (int)C, (int)C, (int)P, (int)ldh, Hd * C,
+                       3 * C * P, 3 * Hd * ldh, B, e1, dw.fc1, dw.fc1_b, s));
+  } else
   MSFNO_TRY(gemm_dense(ROLE_FC1, TILE_128x256, W1f, x1, h, (int)Hd, (int)P, (int)C, (int)C,
                        (int)P, (int)ldh, Hd * C, C * P, (planes ? 3 : 1) * Hd * ldh, B, e1,
                        dw.fc1, dw.fc1_b, s));
@@ -744,6 +758,18 @@ int run_mlp(const msfno_block_desc* d, const float* W1f, const float* b1f, const
   return gemm_dense(ROLE_FC2, TILE_256x128, d->fc2_w, h, out, (int)C, (int)P, (int)Hd, (int)Hd,
                     (int)ldh, (int)P, 0, (planes ? 3 : 1) * Hd * ldh, C * P, B, e2, dw.fc2,
                     dw.fc2_b, s);
+}
+
+// x1 (the MLP input) written by the inverse FFT as bf16x3 planes: x6 engine, an
+// MLP, and an LDS-DMA inverse FFT whose rows tile the plane rows (P % 8 == 0);
+// MSFNO_X1_PLANES=0 keeps fp32 x1 for A/B
+bool x1_planes(const msfno_block_desc* d, const msfno_sht_plan_s* g) {
+  static const bool on = [] {
+    const char* e = getenv("MSFNO_X1_PLANES");
+    return !(e && e[0] == '0');
+  }();
+  return on && d->has_mlp && mlp_h_planes(true) &&
+         ((int64_t)g->nlat * g->nlon) % 8 == 0 && fft_c2r_planes_supported(g->fft, g->mmax);
 }
 
 // MLP hidden activation in the bf16x3 plane format (x6 engine; MSFNO_H_PLANES=0
@@ -980,7 +1006,7 @@ int msfno_block_forward(const msfno_block_desc* d, msfno_sht_plan_t f, msfno_sht
   // ---- filter output + skip (+ GELU for the linear filter) -> x1, norm1 partials ---
   const float* skip_src = d->inner_skip == MSFNO_SKIP_LINEAR ? x1
                           : (d->inner_skip == MSFNO_SKIP_IDENTITY ? x : nullptr);
-  MSFNO_TRY(run_inverse_fft(g, b, B, (int)C, x1, skip_src, b.st1, act, s));
+  MSFNO_TRY(run_inverse_fft(g, b, B, (int)C, x1, skip_src, b.st1, act, s, b.x1p));
   const int64_t np = g->nlat, cnt = g->nlon, cnt_last = g->nlon;
   // ---- norm1 (+ FiLM) as a per-(b,c) affine --------------------------------------
   prof(ST_NORM1, s);
@@ -992,7 +1018,7 @@ int msfno_block_forward(const msfno_block_desc* d, msfno_sht_plan_t f, msfno_sht
     const int64_t Hd = d->mlp_hidden;
     MSFNO_TRY(launch_fold_affine(d->fc1_w, d->fc1_b, b.sc1, b.sh1, b.W1f, b.b1f, B, (int)Hd,
                                  (int)C, s));
-    MSFNO_TRY(run_mlp(d, b.W1f, b.b1f, x1, b.h, out, resid, B, P, b.dw, s));
+    MSFNO_TRY(run_mlp(d, b.W1f, b.b1f, x1, b.h, out, resid, B, P, b.dw, s, b.x1p));
   } else {
     prof(ST_OUT_AFFINE, s);
     MSFNO_TRY(launch_affine_rows(x1, b.sc1, b.sh1, resid, out, BC, P, 0, nullptr, 0, s));

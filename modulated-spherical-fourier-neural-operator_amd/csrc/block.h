@@ -53,6 +53,7 @@ struct BlockBufs {
   float* Yt; float2* Yn; float* x1;
   float2* st1; float* sc1; float* sh1;
   float* W1f; float* b1f; float* h;
+  unsigned short* x1p;  // x1 as bf16x3 planes for fc1 (x6 engine), else null
   DenseWs dw;
 };
 
@@ -77,9 +78,10 @@ void set_table_offsets(msfno_sht_plan_s* p, int sym);
 // channel MLP with norm1/FiLM folded into (W1f, b1f): out = W2·GELU(W1f·x1 + b1f) + b2 (+resid)
 int run_mlp(const msfno_block_desc* d, const float* W1f, const float* b1f, const float* x1,
             float* h, float* out, const float* resid, int B, int64_t P, const DenseWs& dw,
-            hipStream_t s);
+            hipStream_t s, const unsigned short* x1p = nullptr);
 bool mlp_h_planes(bool have_ws);
 int64_t mlp_h_floats(int B, int64_t Hd, int64_t P);
+bool x1_planes(const msfno_block_desc* d, const msfno_sht_plan_s* g);
 // plan construction (mask: optional m-set, see SpecLayout::build)
 int plan_create(int nlat, int nlon, int lmax, int mmax, int inverse,
                 const std::vector<char>* mask, msfno_sht_plan_s** out);

@@ -13,6 +13,7 @@
 #include <cmath>
 #include <cstdlib>
 
+#include "bf16x3.h"
 #include "dma.h"
 #include "kernels.h"
 
@@ -661,15 +662,15 @@ __global__ __launch_bounds__(64 * WV) void fft_r2c_dma_kernel(const float* __res
 // with two 4-wave workgroups per CU beats two rows ahead with one 6-wave one
 // (0.81 vs 0.98 ms): the row FFT itself is VALU/LDS-latency bound, so waves per
 // CU matter more than bytes in flight.
-template <class CL, bool ADD, int WV, int AH>
+template <class CL, bool ADD, int WV, int AH, bool PL>
 __global__ __launch_bounds__(64 * WV) void fft_c2r_dma_kernel(const float2* __restrict__ in,
                                                               float* x, const float* addsrc,
                                                               float2* __restrict__ rowstats,
                                                               int64_t rows, int mmax, int act,
-                                                              int ncy, FFTArgs f) {
+                                                              int ncy, FFTArgs f, C2RPlanes pp) {
   constexpr int H = CL::H, N = 2 * H, RB = N * 4;
   constexpr int NCA = (RB + 1023) / 1024;  // DMA instructions per skip row
-  constexpr int NST = (N / 4 + 63) / 64;   // float4 store instructions per row
+  constexpr int NST = (PL ? 3 : 1) * ((N / 4 + 63) / 64);  // store instructions per row
   extern __shared__ float2 smem[];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   float2* tw = smem;
@@ -744,6 +745,15 @@ __global__ __launch_bounds__(64 * WV) void fft_c2r_dma_kernel(const float2* __re
     }
     const float4* a4 = reinterpret_cast<const float4*>(ast + sl * NCA * 1024);
     float4* x4 = reinterpret_cast<float4*>(x + row * N);
+    unsigned short* xq = nullptr;
+    int64_t ps = 0;
+    if constexpr (PL) {  // plane row: (b, c, lat) of row = (b*C + c)*nlat + lat
+      const int64_t bc = row / pp.nlat, lat = row - bc * pp.nlat;
+      const int64_t b = bc / pp.C, c = bc - b * pp.C;
+      const int64_t P = (int64_t)pp.nlat * N;
+      ps = (int64_t)pp.C * P;
+      xq = pp.xp + b * 3 * ps + c * P + lat * N;
+    }
     float s = 0.f;
 #pragma unroll
     for (int j = 0; j < NST; ++j) {
@@ -762,7 +772,17 @@ __global__ __launch_bounds__(64 * WV) void fft_c2r_dma_kernel(const float2* __re
           buf[2 * n] = a;
           buf[2 * n + 1] = b;
         }
-        x4[n] = make_float4(a.x, a.y, b.x, b.y);
+        if constexpr (PL) {
+          uint32_t a0, a1, a2, b0, b1, b2;
+          split2(a.x, a.y, a0, a1, a2);
+          split2(b.x, b.y, b0, b1, b2);
+          uint2* q = reinterpret_cast<uint2*>(xq + 4 * n);
+          q[0] = make_uint2(a0, b0);
+          *reinterpret_cast<uint2*>(xq + ps + 4 * n) = make_uint2(a1, b1);
+          *reinterpret_cast<uint2*>(xq + 2 * ps + 4 * n) = make_uint2(a2, b2);
+        } else {
+          x4[n] = make_float4(a.x, a.y, b.x, b.y);
+        }
         s += (a.x + a.y) + (b.x + b.y);
       }
     }
@@ -1073,9 +1093,12 @@ static int launch_r2c(const FFTArgs& a, const float* x, float2* out, float2* row
 
 template <class CL>
 static int launch_c2r(const FFTArgs& a, const float2* in, float* x, const float* addsrc,
-                      float2* rowstats, int64_t rows, int mmax, int act, hipStream_t s) {
+                      float2* rowstats, int64_t rows, int mmax, int act, hipStream_t s,
+                      const C2RPlanes* planes) {
   if constexpr (CL::H > 0) {
     const int ncy = (mmax * 8 + 16 + 1023) / 1024;
+    C2RPlanes pp{};
+    if (planes) pp = *planes;
     if (use_fft_dma() && (2 * CL::H) % 8 == 0 && mmax <= CL::H + 1 && ncy <= 5) {
       const int rb = 2 * CL::H * 4, nca = (rb + 1023) / 1024;
       // one row ahead, 4-wave workgroups, as many per CU as the LDS holds
@@ -1088,16 +1111,21 @@ static int launch_c2r(const FFTArgs& a, const float2* in, float* x, const float*
         MSFNO_TRY(set_lds_limit(reinterpret_cast<const void*>(kern), lds));
         const int64_t grid = std::min<int64_t>(cdiv(rows, WV), dma_grid() * wg_cu);
         hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(64 * WV), lds, s, in, x, addsrc,
-                           rowstats, rows, mmax, act, ncy, a);
+                           rowstats, rows, mmax, act, ncy, a, pp);
         return MSFNO_OK;
       };
-      if (addsrc)
-        MSFNO_TRY(go(fft_c2r_dma_kernel<CL, true, 4, 1>, 4));
+      if (planes && addsrc)
+        MSFNO_TRY(go(fft_c2r_dma_kernel<CL, true, 4, 1, true>, 4));
+      else if (planes)
+        MSFNO_TRY(go(fft_c2r_dma_kernel<CL, false, 4, 1, true>, 4));
+      else if (addsrc)
+        MSFNO_TRY(go(fft_c2r_dma_kernel<CL, true, 4, 1, false>, 4));
       else
-        MSFNO_TRY(go(fft_c2r_dma_kernel<CL, false, 4, 1>, 4));
+        MSFNO_TRY(go(fft_c2r_dma_kernel<CL, false, 4, 1, false>, 4));
       return launch_check("fft_c2r_dma");
     }
   }
+  MSFNO_REQUIRE(!planes, MSFNO_EUNSUPPORTED, "plane output needs the LDS-DMA inverse FFT");
   const size_t lds =
       ((size_t)(kWaves * CL::kBufs + 1) * a.H + (CL::H > 0 ? kWaves * kStageMax : 0)) *
       sizeof(float2);
@@ -1121,16 +1149,23 @@ int launch_fft_r2c_rows(const FFTPlan& f, const float* x, float2* out, float2* r
 }
 
 int launch_fft_c2r_rows(const FFTPlan& f, const float2* in, float* x, const float* addsrc,
-                        float2* rowstats, int64_t rows, int mmax, int act, hipStream_t s) {
+                        float2* rowstats, int64_t rows, int mmax, int act, hipStream_t s,
+                        const C2RPlanes* planes) {
   if (rows <= 0) return MSFNO_OK;
   const FFTArgs a = make_args(f);
   switch (f.codelet) {
 #define X(id, CL) \
-  case id: return launch_c2r<CL>(a, in, x, addsrc, rowstats, rows, mmax, act, s);
+  case id: return launch_c2r<CL>(a, in, x, addsrc, rowstats, rows, mmax, act, s, planes);
     MSFNO_FFT_CODELETS(X)
 #undef X
-    default: return launch_c2r<GenericFFT>(a, in, x, addsrc, rowstats, rows, mmax, act, s);
+    default: return launch_c2r<GenericFFT>(a, in, x, addsrc, rowstats, rows, mmax, act, s, planes);
   }
+}
+
+bool fft_c2r_planes_supported(const FFTPlan& f, int mmax) {
+  const int ncy = (mmax * 8 + 16 + 1023) / 1024;
+  return use_fft_dma() && f.codelet != 0 && f.packed && f.N % 8 == 0 && mmax <= f.H + 1 &&
+         ncy <= 5;
 }
 
 template <class CL, int TK>

@@ -2,6 +2,7 @@
 // fp32-accurate 6-term bf16 split): kernel parameters, the XCD-aware tile
 // remap, GELU(erf) and the LDS-staged fused epilogue.
 #pragma once
+#include "bf16x3.h"
 #include "common.h"
 
 namespace msfno {
@@ -125,25 +126,7 @@ enum : int {
   EPI_PLANES = 128  // store C as three exact bf16 terms (the x6 operand format)
 };
 
-// (a, b) -> packed bf16x2 terms t0 + t1 + t2 == (a, b) exactly (24 significant
-// bits = the fp32 significand; round-to-nearest cvt, exact residuals)
-typedef float f32x2v_ __attribute__((ext_vector_type(2)));
-typedef __bf16 bf16x2v_ __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ uint32_t cvt_pk_bf16(float a, float b) {
-  const f32x2v_ v = {a, b};
-  return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, bf16x2v_));
-}
-__device__ __forceinline__ float bf_lo(uint32_t u) { return __uint_as_float(u << 16); }
-__device__ __forceinline__ float bf_hi(uint32_t u) { return __uint_as_float(u & 0xffff0000u); }
-__device__ __forceinline__ void split2(float a, float b, uint32_t& t0, uint32_t& t1, uint32_t& t2) {
-  t0 = cvt_pk_bf16(a, b);
-  a -= bf_lo(t0);
-  b -= bf_hi(t0);
-  t1 = cvt_pk_bf16(a, b);
-  a -= bf_lo(t1);
-  b -= bf_hi(t1);
-  t2 = cvt_pk_bf16(a, b);
-}
+
 
 // C tile epilogue.  acc holds each wave's (BM/WGM)x(BN/WGN) part of the tile
 // (waves WGM x WGN, wave w at (w / WGN, w % WGN)) as 32x32 MFMA blocks (row
