@@ -24,14 +24,14 @@ void SpecLayout::build(int lmax_, int mmax_, const std::vector<char>* mask) {
   for (int m = 0; m < mmax; ++m) {
     const int l = (mask && !(*mask)[m]) ? 0 : std::max(lmax - m, 0);
     L[m] = l;
-    Lpe[m] = (int)round_up((l + 1) / 2, 4);
-    Lp[m] = Lpe[m] + (int)round_up(l / 2, 4);
+    Lpe[m] = (int)round_up((l + 1) / 2, 8);  // 8: 16-B bf16 chunks of the x6 Legendre GEMM
+    Lp[m] = Lpe[m] + (int)round_up(l / 2, 8);
     off[m] = (int)Tp;
     T += l;
     Tp += Lp[m];
     if (l > 0) mact = m + 1;
   }
-  ldT = round_up(std::max<int64_t>(Tp, 4), 4);
+  ldT = round_up(std::max<int64_t>(Tp, 8), 8);
 }
 
 // ---------------------------------------------------------------------------
@@ -356,6 +356,128 @@ int transpose_inv_plan(const msfno_sht_plan_s* p, const float* Yt, float2* Yn, i
   return launch_transpose_inv(Yt, Yn, B, C, p->nlat, p->mmax, p->spec.mact, p->ldk, s);
 }
 
+// ---- x6 Legendre (symmetric plans) -----------------------------------------------
+// The per-(m, parity) problems of DESIGN.md §3 on the x6 engine: the plan's table
+// image in bf16x3 planes (rows zero-padded to 16) is built once at load; A is the
+// slab (forward, written as planes by transpose_fwd_sym_planes) or the S
+// coefficients (inverse, written as planes by the spectral MLP's output layer).
+// Off by default: measured slower than the fp32-MFMA descriptor GEMM at 721x1440
+// (forward 0.44 vs 0.38 ms, inverse 0.68 vs 0.54 ms, side stream off): the
+// per-(m, parity) problems are narrow (N ~ 90, or K <= 180), so the six-MFMA
+// k-steps of a 128 x 64 tile are too short to amortise the per-k-tile barrier
+// and DMA waits.  MSFNO_LEG_X6=1 enables it.
+bool leg_x6_enabled() {
+  static const bool on = [] {
+    const char* e = getenv("MSFNO_LEG_X6");
+    return e && e[0] == '1';
+  }();
+  return on && spec_use_x6();
+}
+
+int build_table_x6(msfno_sht_plan_s* p, const float* table, hipStream_t s) {
+  const SpecLayout& L = p->spec;
+  const int64_t ke16 = round_up(p->Ke, 16), ko16 = round_up(p->Ko, 16);
+  p->tabx_offe.assign(p->mmax, 0);
+  p->tabx_offo.assign(p->mmax, 0);
+  int64_t acc = 0;
+  for (int m = 0; m < p->mmax; ++m) {
+    const int64_t lpe = L.Lpe[m], lpo = L.Lp[m] - L.Lpe[m];
+    p->tabx_offe[m] = acc;
+    if (L.L[m] == 0) { p->tabx_offo[m] = acc; continue; }
+    acc += p->inverse ? round_up(lpe, 16) * p->ldke : ke16 * lpe;
+    p->tabx_offo[m] = acc;
+    acc += p->inverse ? round_up(lpo, 16) * ko16 : ko16 * lpo;
+  }
+  p->tabx_plane = round_up(std::max<int64_t>(acc, 8), 8);
+  if (p->tabx) (void)hipFree(p->tabx);
+  if (!p->d_tabx_offe) MSFNO_CHECK_HIP(hipMalloc(&p->d_tabx_offe, p->mmax * sizeof(int64_t)));
+  if (!p->d_tabx_offo) MSFNO_CHECK_HIP(hipMalloc(&p->d_tabx_offo, p->mmax * sizeof(int64_t)));
+  MSFNO_CHECK_HIP(hipMalloc(&p->tabx, 3 * p->tabx_plane * sizeof(unsigned short)));
+  MSFNO_CHECK_HIP(hipMemsetAsync(p->tabx, 0, 3 * p->tabx_plane * sizeof(unsigned short), s));
+  MSFNO_CHECK_HIP(hipMemcpy(p->d_tabx_offe, p->tabx_offe.data(), p->mmax * sizeof(int64_t),
+                            hipMemcpyHostToDevice));
+  MSFNO_CHECK_HIP(hipMemcpy(p->d_tabx_offo, p->tabx_offo.data(), p->mmax * sizeof(int64_t),
+                            hipMemcpyHostToDevice));
+  return launch_relayout_table_x6(*p, table, s);
+}
+
+// descriptors of the x6 problems (offsets per plane; A and C layouts as in
+// ensure_desc, B = the table image)
+int ensure_descx(msfno_sht_plan_s* p, int R, int64_t ldT) {
+  if (p->descx_R == R && p->d_descx) return MSFNO_OK;
+  MSFNO_REQUIRE(p->sym && p->tabx, MSFNO_EINVAL, "x6 Legendre needs a symmetric plan");
+  const SpecLayout& L = p->spec;
+  const int ke16 = (int)round_up(p->Ke, 16), ko16 = (int)round_up(p->Ko, 16);
+  std::vector<GemmDesc> d;
+  int tiles = 0;
+  auto push = [&](GemmDesc g) {
+    g.tiles_m = (int)cdiv(g.M, X6D_TILE_M);
+    g.tiles_n = (int)cdiv(g.N, X6D_TILE_N);
+    if (g.tiles_m * g.tiles_n == 0) return;
+    g.tile_start = tiles;
+    tiles += g.tiles_m * g.tiles_n;
+    d.push_back(g);
+  };
+  for (int m = 0; m < L.mact; ++m) {
+    if (L.L[m] == 0) continue;
+    const int64_t slab = (int64_t)p->slab[m] * R * p->ldk;
+    const int lpe = L.Lpe[m], lpo = L.Lp[m] - L.Lpe[m];
+    const int le = (L.L[m] + 1) / 2, lo = L.L[m] / 2;
+    GemmDesc g{};
+    g.M = R;
+    if (!p->inverse) {
+      GemmDesc e = g;  // even: Xs (R x Ke) . We (Ke x Lpe) -> S[:, off]
+      e.N = lpe; e.K = p->Ke; e.lda = p->ldk; e.ldb = lpe; e.ldc = (int)ldT;
+      e.offA = slab; e.offB = p->tabx_offe[m]; e.offC = L.off[m];
+      push(e);
+      if (lo > 0) {
+        GemmDesc o = g;  // odd: Xa (R x Ko) . Wo (Ko x Lpo) -> S[:, off + Lpe]
+        o.N = lpo; o.K = p->Ko; o.lda = p->ldk; o.ldb = lpo; o.ldc = (int)ldT;
+        o.offA = slab + p->ldke; o.offB = p->tabx_offo[m]; o.offC = L.off[m] + lpe;
+        push(o);
+      }
+    } else {
+      GemmDesc e = g;  // even: E (R x Ke) = S_e (R x Le) . Pe (Le x Ke)
+      e.N = p->Ke; e.K = le; e.lda = (int)ldT; e.ldb = ke16; e.ldc = p->ldk;
+      e.offA = L.off[m]; e.offB = p->tabx_offe[m]; e.offC = slab;
+      push(e);
+      GemmDesc o = g;  // odd: O (R x Ko) = S_o (R x Lo) . Po (Lo x Ko); K = 0 writes zeros
+      o.N = p->Ko; o.K = lo; o.lda = (int)ldT; o.ldb = ko16; o.ldc = p->ldk;
+      o.offA = L.off[m] + lpe; o.offB = p->tabx_offo[m]; o.offC = slab + p->ldke;
+      push(o);
+    }
+  }
+  for (const GemmDesc& g : d)
+    MSFNO_REQUIRE(g.lda % 8 == 0 && g.ldb % 8 == 0 && g.ldc % 4 == 0 && g.offA % 8 == 0 &&
+                      g.offB % 8 == 0 && g.offC % 4 == 0,
+                  MSFNO_EINVAL, "x6 Legendre: misaligned problem layout");
+  if (p->d_descx) MSFNO_CHECK_HIP(hipFree(p->d_descx));
+  p->d_descx = nullptr;
+  MSFNO_CHECK_HIP(hipMalloc(&p->d_descx, std::max<size_t>(1, d.size()) * sizeof(GemmDesc)));
+  if (!d.empty())
+    MSFNO_CHECK_HIP(hipMemcpy(p->d_descx, d.data(), d.size() * sizeof(GemmDesc), hipMemcpyHostToDevice));
+  p->ndescx = (int)d.size();
+  p->descx_tiles = tiles;
+  p->descx_R = R;
+  return MSFNO_OK;
+}
+
+// forward: Xtp (slab planes, plane stride xstride) -> S fp32 (ld ldT)
+int legendre_fwd_x6(msfno_sht_plan_s* f, const unsigned short* Xtp, int64_t xstride, float* S,
+                    int R, hipStream_t s) {
+  MSFNO_TRY(ensure_descx(f, R, f->spec.ldT));
+  return gemm_x6d(Xtp, xstride, f->tabx, f->tabx_plane, S, f->d_descx, f->ndescx,
+                  f->descx_tiles, s);
+}
+
+// inverse: Sp (coefficient planes [plane][R][ldT]) -> Yt fp32 slabs
+int legendre_inv_x6(msfno_sht_plan_s* g, const unsigned short* Sp, float* Yt, int R,
+                    hipStream_t s) {
+  MSFNO_TRY(ensure_descx(g, R, g->spec.ldT));
+  return gemm_x6d(Sp, (int64_t)R * g->spec.ldT, g->tabx, g->tabx_plane, Yt, g->d_descx,
+                  g->ndescx, g->descx_tiles, s);
+}
+
 int legendre_fwd(msfno_sht_plan_s* f, const float* Xt, float* S, int R, hipStream_t s,
                  const float* rowscale, int C) {
   MSFNO_TRY(ensure_desc(f, R, 0, f->spec.ldT));
@@ -407,6 +529,12 @@ void carve_block(Carve& cv, BlockBufs& b, const msfno_block_desc* d,
   } else {
     b.xt = cv.take<float>(BC * L.T * 2);
     b.yt = cv.take<float>(BC * L.T * 2);
+  }
+  b.Xtp = b.Sp = nullptr;
+  if (d->filter_type == MSFNO_FILTER_NONLINEAR && leg_x6_enabled()) {
+    // used when both plans turn out symmetric (known once their tables are loaded)
+    b.Xtp = cv.take<unsigned short>(3LL * f->nslab * R * f->ldk);
+    b.Sp = cv.take<unsigned short>(3LL * R * L.ldT);
   }
   b.Yt = cv.take<float>((int64_t)g->mmax * R * g->ldk);
   b.Yn = cv.take<float2>(BC * g->nlat * g->mmax);
@@ -483,7 +611,7 @@ int check_pair(const msfno_block_desc* d, const msfno_sht_plan_s* f,
 }
 
 int run_filter(const msfno_block_desc* d, msfno_sht_plan_s* f, msfno_sht_plan_s* g,
-                      const BlockBufs& b, int B, hipStream_t s) {
+                      const BlockBufs& b, int B, hipStream_t s, unsigned short* Sp) {
   const int64_t C = d->C;
   const SpecLayout& L = f->spec;
   if (d->filter_type == MSFNO_FILTER_NONLINEAR) {
@@ -540,6 +668,10 @@ int run_filter(const msfno_block_desc* d, msfno_sht_plan_s* f, msfno_sht_plan_s*
         }
         const int ldc = l < nl ? (int)ldTx : (int)L.ldT;
         const int64_t sC = l < nl ? 3 * 2LL * co * ldTx : 2LL * co * L.ldT;
+        if (l == nl && Sp) {  // S for the x6 inverse Legendre: planes [plane][R][ldT]
+          e.c_planes = Sp;
+          e.c_plane_stride = 2LL * B * co * L.ldT;
+        }
         if (l > 0 || split_l0) e.a_planes = static_cast<const unsigned short*>(b.dw.spec[l]);
         if (l == 0 && split_l0) {  // Sc is free during layer 0
           // layer 0's fp32 input (the forward Legendre output) -> planes in Sc: one
@@ -596,6 +728,9 @@ int run_filter(const msfno_block_desc* d, msfno_sht_plan_s* f, msfno_sht_plan_s*
 int run_spectral(const msfno_block_desc* d, msfno_sht_plan_s* f, msfno_sht_plan_s* g,
                         const BlockBufs& b, const float* x, int B, bool norm0, hipStream_t s) {
   const int64_t C = d->C, BC = (int64_t)B * C, R = 2 * BC;
+  // x6 Legendre: symmetric plans, slab / coefficient planes carved, row path
+  const bool lx6 = b.Xtp && b.Sp && f->sym && g->sym && !use_fft_tile(f) &&
+                   f->spec.ldT == g->spec.ldT;
   prof(ST_FFT_FWD, s);
   const float scale = (float)(2.0 * M_PI / f->nlon);
   if (use_fft_tile(f)) {
@@ -621,14 +756,26 @@ int run_spectral(const msfno_block_desc* d, msfno_sht_plan_s* f, msfno_sht_plan_
                                    s));
     }
     prof(ST_TRANSPOSE_FWD, s);
-    MSFNO_TRY(transpose_fwd_plan(f, b.Xn, b.Xt, B, (int)C, norm0 ? b.sc0 : nullptr,
-                                 norm0 ? b.sh0 : nullptr, s));
-    prof(ST_LEG_FWD, s);
-    MSFNO_TRY(legendre_fwd(f, b.Xt, b.Sa, (int)R, s));
+    if (lx6) {
+      const int64_t xstride = (int64_t)f->nslab * R * f->ldk;
+      MSFNO_TRY(launch_transpose_fwd_sym_planes(b.Xn, b.Xtp, xstride, B, (int)C, f->geom(),
+                                                f->mmax, norm0 ? b.sc0 : nullptr,
+                                                norm0 ? b.sh0 : nullptr, s));
+      prof(ST_LEG_FWD, s);
+      MSFNO_TRY(legendre_fwd_x6(f, b.Xtp, xstride, b.Sa, (int)R, s));
+    } else {
+      MSFNO_TRY(transpose_fwd_plan(f, b.Xn, b.Xt, B, (int)C, norm0 ? b.sc0 : nullptr,
+                                   norm0 ? b.sh0 : nullptr, s));
+      prof(ST_LEG_FWD, s);
+      MSFNO_TRY(legendre_fwd(f, b.Xt, b.Sa, (int)R, s));
+    }
   }
-  MSFNO_TRY(run_filter(d, f, g, b, B, s));
+  MSFNO_TRY(run_filter(d, f, g, b, B, s, lx6 ? b.Sp : nullptr));
   prof(ST_LEG_INV, s);
-  MSFNO_TRY(legendre_inv(g, b.Sa, b.Yt, (int)R, s));
+  if (lx6)
+    MSFNO_TRY(legendre_inv_x6(g, b.Sp, b.Yt, (int)R, s));
+  else
+    MSFNO_TRY(legendre_inv(g, b.Sa, b.Yt, (int)R, s));
   return MSFNO_OK;
 }
 
@@ -684,8 +831,9 @@ int plan_create(int nlat, int nlon, int lmax, int mmax, int inverse,
   p->nh = nlat / 2;
   p->Ke = nlat - p->nh;
   p->Ko = p->nh;
-  p->ldke = (int)round_up(p->Ke, 4);
-  p->ldk = (int)std::max<int64_t>(round_up(nlat, 4), p->ldke + round_up(p->Ko, 4));
+  // slab columns padded to 16: whole k-tiles of the x6 Legendre GEMM stay in a row
+  p->ldke = (int)round_up(p->Ke, 16);
+  p->ldk = (int)std::max<int64_t>(round_up(nlat, 16), p->ldke + round_up(p->Ko, 16));
   p->spec.build(lmax, mmax, mask);
   p->slab.assign(mmax, -1);
   for (int m = 0; m < mmax; ++m) {
@@ -825,6 +973,10 @@ int msfno_sht_plan_destroy(msfno_sht_plan_t p) {
   if (p->d_off) (void)hipFree(p->d_off);
   if (p->d_Lpe) (void)hipFree(p->d_Lpe);
   if (p->d_desc) (void)hipFree(p->d_desc);
+  if (p->tabx) (void)hipFree(p->tabx);
+  if (p->d_tabx_offe) (void)hipFree(p->d_tabx_offe);
+  if (p->d_tabx_offo) (void)hipFree(p->d_tabx_offo);
+  if (p->d_descx) (void)hipFree(p->d_descx);
   delete p;
   return MSFNO_OK;
 }
@@ -855,6 +1007,8 @@ int msfno_sht_plan_load_table(msfno_sht_plan_t p, const float* table, void* stre
                             hipMemcpyHostToDevice));
   p->desc_R = -1;  // descriptors depend on the layout
   MSFNO_TRY(launch_relayout_table(*p, table, s));
+  p->descx_R = -1;
+  if (sym) MSFNO_TRY(build_table_x6(p, table, s));
   p->table_loaded = 1;
   return MSFNO_OK;
 }

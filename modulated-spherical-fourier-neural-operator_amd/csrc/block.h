@@ -54,6 +54,8 @@ struct BlockBufs {
   float2* st1; float* sc1; float* sh1;
   float* W1f; float* b1f; float* h;
   unsigned short* x1p;  // x1 as bf16x3 planes for fc1 (x6 engine), else null
+  unsigned short* Xtp;  // x6 Legendre: forward slabs as bf16x3 planes, else null
+  unsigned short* Sp;   // x6 Legendre: filter output S as planes [plane][R][ldT]
   DenseWs dw;
 };
 
@@ -70,7 +72,7 @@ int legendre_fwd(msfno_sht_plan_s* f, const float* Xt, float* S, int R, hipStrea
 int legendre_inv(msfno_sht_plan_s* g, const float* S, float* Yt, int R, hipStream_t s);
 // spectral filter on S (f->spec layout) in b.Sa (in place)
 int run_filter(const msfno_block_desc* d, msfno_sht_plan_s* f, msfno_sht_plan_s* g,
-               const BlockBufs& b, int B, hipStream_t s);
+               const BlockBufs& b, int B, hipStream_t s, unsigned short* Sp = nullptr);
 bool use_fft_tile(const msfno_sht_plan_s* p);
 bool use_c3m();
 int c3m_tile();
@@ -82,6 +84,7 @@ int run_mlp(const msfno_block_desc* d, const float* W1f, const float* b1f, const
 bool mlp_h_planes(bool have_ws);
 int64_t mlp_h_floats(int B, int64_t Hd, int64_t P);
 bool x1_planes(const msfno_block_desc* d, const msfno_sht_plan_s* g);
+bool leg_x6_enabled();
 // plan construction (mask: optional m-set, see SpecLayout::build)
 int plan_create(int nlat, int nlon, int lmax, int mmax, int inverse,
                 const std::vector<char>* mask, msfno_sht_plan_s** out);

@@ -188,6 +188,12 @@ struct SpecWeightsX6p {
 };
 size_t spec_weights_x6p_layout(SpecWeightsX6p& a);
 int launch_spec_weights_x6p(const SpecWeightsX6p& a, hipStream_t s);
+// descriptor-mode x6 GEMM (gemm_x6p.hip): every problem's A (M x K, lda) and B
+// (K x N, ldb; rows zero-padded to a multiple of 16) in bf16x3 planes (plane
+// strides sAxp, sBxp; descriptor offsets per plane), fp32 C; tiles 128 x 64
+constexpr int X6D_TILE_M = 128, X6D_TILE_N = 64;
+int gemm_x6d(const unsigned short* Ax, int64_t sAxp, const unsigned short* Bx, int64_t sBxp,
+             float* C, const GemmDesc* descs, int ndesc, int total_tiles, hipStream_t s);
 // fp32 x[z][r][c] (ld ldx, batch stride sx) -> bf16x3 planes xp[z][plane][r][c]
 int launch_split_planes(const float* x, unsigned short* xp, int rows, int cols, int ldx,
                         int64_t sx, int ldp, int64_t pstride, int64_t sxp, int batch,
@@ -230,5 +236,15 @@ struct msfno_sht_plan_s {
   int desc_R = -1;
   msfno::GemmDesc* d_desc = nullptr;
   int ndesc = 0, desc_tiles = 0;
+  // x6 Legendre (symmetric plans): table image in bf16x3 planes (gemm_x6d's B),
+  // per-m even / odd block offsets within a plane, and its descriptor cache
+  unsigned short* tabx = nullptr;
+  int64_t tabx_plane = 0;
+  std::vector<int64_t> tabx_offe, tabx_offo;
+  int64_t* d_tabx_offe = nullptr;
+  int64_t* d_tabx_offo = nullptr;
+  int descx_R = -1;
+  msfno::GemmDesc* d_descx = nullptr;
+  int ndescx = 0, descx_tiles = 0;
   msfno::LatGeom geom() const { return {sym, nlat, nh, Ke, Ko, ldke, ldk}; }
 };

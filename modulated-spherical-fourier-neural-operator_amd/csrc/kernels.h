@@ -84,6 +84,13 @@ int gemm_c3m(const float* Ar, const float* Ai, const float* X, float* Y, int co,
 int launch_expand_complex_weight(const float* w, float* Wexp, int Ci, int Co, hipStream_t s);
 // (mmax,lmax,nlat) reference table -> plan GEMM layout (general or symmetric)
 int launch_relayout_table(const msfno_sht_plan_s& p, const float* table, hipStream_t s);
+// x6 Legendre table image (bf16x3 planes, rows padded to 16; gemm_x6d's B)
+int launch_relayout_table_x6(const msfno_sht_plan_s& p, const float* table, hipStream_t s);
+// symmetric forward transpose writing Xt as bf16x3 planes (plane stride pstride),
+// zero pads (gemm_x6d's A)
+int launch_transpose_fwd_sym_planes(const float2* Xn, unsigned short* Xtp, int64_t pstride, int B,
+                                    int C, const LatGeom& g, int mmax, const float* nscale,
+                                    const float* nshift, hipStream_t s);
 // *d_flag |= 1 unless table[m][l][nlat-1-k] = (-1)^(l-m) table[m][l][k] (rel. 1e-5)
 int launch_check_symmetry(const float* table, int mmax, int lmax, int nlat, int* d_flag,
                           hipStream_t s);
