@@ -52,8 +52,9 @@ SIDE_STAGES = {"inner_skip"}
 # template instantiations in the block (x6 engine, 256x256 tiles; f32 engine kept
 # for MSFNO_GEMM=f32)
 STAGE_KERNEL_X6 = {
-    # fc1: fp32 B split in-kernel, bias + GELU, h written as bf16x3 planes (EPI 133)
-    "mlp_fc1": "void msfno::gemm_x6_kernel<256, 256, 4, 2, true, 133, false>(msfno::GemmParams)",
+    # fc1: x1 planes (from the inverse FFT) by LDS-DMA, bias + GELU, h written as
+    # bf16x3 planes (EPI 133)
+    "mlp_fc1": "void msfno::gemm_x6p_kernel<133>(msfno::GemmParams)",
     # fc2: h planes staged by LDS-DMA (x6p), bias + outer skip (EPI 3)
     "mlp_fc2": "void msfno::gemm_x6p_kernel<3>(msfno::GemmParams)",
     "inner_skip": "void msfno::gemm_x6_kernel<256, 256, 4, 2, true, 1, false>(msfno::GemmParams)",
@@ -151,7 +152,9 @@ def stage_work(name, B, C, nlat, nlon, lmax, mmax, hid, shid, rows=None, mset=No
         "legendre_inv": ("mfma", 2 * (2 * BC) * nlat * T),
         # HBM-bound stages: compulsory bytes moved
         "fft_fwd": ("hbm", BC * rows * (nlon * 4 + mmax * 8)),
-        "fft_inv": ("hbm", BC * rows * (nlon * 4 + mmax * 8)),
+        # irfft: Yn read + skip-branch row read + x1 written (bf16x3 planes, 6 B per
+        # value, on the x6 engine with an MLP)
+        "fft_inv": ("hbm", BC * rows * (mmax * 8 + nlon * 4 + nlon * (6 if x6_engine()[0] else 4))),
         "transpose_fwd": ("hbm", 2 * BC * rows * mmax * 8),
         "transpose_inv": ("hbm", 2 * BC * rows * mmax * 8),
         "linear_contract": ("hbm", 8 * C * C * T + 2 * 8 * BC * T),
