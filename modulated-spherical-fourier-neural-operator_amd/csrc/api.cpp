@@ -570,12 +570,23 @@ void carve_dense_ws(Carve& cv, DenseWs& w, const msfno_block_desc* d, int B) {
   }
 }
 
+// spectral MLP as Gauss 3M complex GEMMs on the x6 engine (gemm_x6c.hip);
+// MSFNO_SPEC_3M=0 keeps the real-ified 4M x6p GEMMs for A/B
+bool spec_use_3m() {
+  static const bool on = [] {
+    const char* e = getenv("MSFNO_SPEC_3M");
+    return !(e && e[0] == '0');
+  }();
+  return on && spec_use_x6();
+}
+
 // floats to reserve for one spectral-MLP hidden buffer (B, 2 Hs, T): fp32, or
 // bf16x3 planes with a row stride padded to 8 on the x6 engine
 int64_t spec_hidden_floats(int B, int64_t Hs, const SpecLayout& L) {
   if (!spec_use_x6()) return (int64_t)B * 2 * Hs * L.ldT;
+  const int64_t planes = spec_use_3m() ? 9 : 6;  // 3M: re, im, re+im; 4M: re/im rows
   return std::max<int64_t>((int64_t)B * 2 * Hs * L.ldT,
-                           cdiv((int64_t)B * 3 * 2 * Hs * round_up(L.Tp, 8) * 2, 4));
+                           cdiv((int64_t)B * planes * Hs * round_up(L.Tp, 8) * 2, 4));
 }
 
 // split-A planes of the real-ified spectral MLP weights (x6 engine)
@@ -586,7 +597,7 @@ void carve_spec_ws(Carve& cv, DenseWs& w, const msfno_block_desc* d) {
   for (int l = 0; l <= d->spectral_layers && l < 9; ++l) {
     const int ci = (l == 0) ? (int)d->C : (int)d->spec_hidden;
     const int co = (l == d->spectral_layers) ? (int)d->C : (int)d->spec_hidden;
-    w.spec_b[l] = gemm_dense_workspace(2 * co, 2 * ci, 1);
+    w.spec_b[l] = std::max(gemm_dense_workspace(2 * co, 2 * ci, 1), gemm_x6c_weight_bytes(co, ci));
     if (w.spec_b[l]) w.spec[l] = cv.take<char>(w.spec_b[l]);
   }
 }
@@ -620,6 +631,33 @@ int run_filter(const msfno_block_desc* d, msfno_sht_plan_s* f, msfno_sht_plan_s*
     prof(ST_SPEC_PREP, s);
     const bool x6 = spec_use_x6() && b.dw.spec[0];
     const bool c3m = !x6 && use_c3m();
+    if (x6 && spec_use_3m() && !Sp && C <= Hs) {
+      // Gauss 3M complex GEMMs (gemm_x6c.hip): weights Wr, Wi, Wr+Wi of all layers in
+      // one launch; layer 0's input split into 3M planes in Sc (free until layer 1)
+      SpecWeightsX6p sw{};
+      sw.nlayers = nl + 1;
+      for (int l = 0; l <= nl; ++l) {
+        sw.w[l] = (l == nl) ? d->spec_wout : d->spec_w[l];
+        MSFNO_REQUIRE(sw.w[l], MSFNO_EINVAL, "missing spectral weight");
+        sw.ci[l] = (l == 0) ? (int)C : (int)Hs;
+        sw.co[l] = (l == nl) ? (int)C : (int)Hs;
+        sw.out[l] = static_cast<unsigned short*>(b.dw.spec[l]);
+      }
+      spec_weights_3m_layout(sw);
+      MSFNO_TRY(launch_spec_weights_3m(sw, s));
+      const int ldTx = (int)round_up(L.Tp, 8);
+      unsigned short* cur = reinterpret_cast<unsigned short*>(b.Sc);
+      MSFNO_TRY(launch_split3m(b.Sa, cur, B, (int)C, (int)L.Tp, (int)L.ldT, ldTx, s));
+      for (int l = 0; l <= nl; ++l) {
+        prof(l == nl ? ST_SPEC_OUT : ST_SPEC_L0 + std::min(l, 3), s);
+        unsigned short* out = l == nl ? nullptr
+                                      : reinterpret_cast<unsigned short*>((l & 1) ? b.Sc : b.Sb);
+        MSFNO_TRY(gemm_x6c(sw.out[l], sw.co[l], sw.ci[l], cur, (int)L.Tp, ldTx, out,
+                           l == nl ? b.Sa : nullptr, (int)L.ldT, l < nl, B, s));
+        cur = out;
+      }
+      return MSFNO_OK;
+    }
     const bool split_l0 = x6 && C <= Hs;  // layer 0 input split into Sc (below)
     if (x6) {
       // every layer's real-ified weight straight into its x6p A image, one launch

@@ -194,6 +194,15 @@ int launch_spec_weights_x6p(const SpecWeightsX6p& a, hipStream_t s);
 constexpr int X6D_TILE_M = 128, X6D_TILE_N = 64;
 int gemm_x6d(const unsigned short* Ax, int64_t sAxp, const unsigned short* Bx, int64_t sBxp,
              float* C, const GemmDesc* descs, int ndesc, int total_tiles, hipStream_t s);
+// spectral-MLP layer as a Gauss 3M complex GEMM on the x6 engine (gemm_x6c.hip);
+// activations in "3M planes" [b][re, im, re+im][plane][rows][ld]
+size_t gemm_x6c_weight_bytes(int co, int ci);
+size_t spec_weights_3m_layout(SpecWeightsX6p& a);
+int launch_spec_weights_3m(const SpecWeightsX6p& a, hipStream_t s);
+int launch_split3m(const float* S, unsigned short* X, int B, int C, int N, int ldS, int ldx,
+                   hipStream_t s);
+int gemm_x6c(const unsigned short* Aw, int co, int ci, const unsigned short* X, int N, int ldx,
+             unsigned short* Y, float* S, int ldS, bool relu, int B, hipStream_t s);
 // fp32 x[z][r][c] (ld ldx, batch stride sx) -> bf16x3 planes xp[z][plane][r][c]
 int launch_split_planes(const float* x, unsigned short* xp, int rows, int cols, int ldx,
                         int64_t sx, int ldp, int64_t pstride, int64_t sxp, int batch,

@@ -1,0 +1,386 @@
+// Spectral-MLP layer as a Gauss three-multiplication complex GEMM on the x6
+// engine ("x6c"), for gfx950.
+//
+// One layer of SpectralAttentionS2.forward_mlp (layers.py:604-620; the
+// contraction compl_mul2d_fwd_c, contractions.py:132-137) is Y = W · X over the
+// channels of every (l, m) column, W (co x ci) and X (ci x T) complex.  With
+//   P1 = Wr·Xr,  P2 = Wi·Xi,  P3 = (Wr + Wi)·(Xr + Xi)
+// Re Y = P1 - P2 and Im Y = P3 - P1 - P2: three real products instead of the four
+// of the real-ified [[Wr, -Wi], [Wi, Wr]] GEMM, 25 % fewer matrix-core cycles.
+// Each product is an x6 product (gemm_x6p.hip) of bf16x3 planes, so both
+// operands carry a third "matrix": Ws = Wr + Wi (weight prep) and Xs = Xr + Xi,
+// which the producer of X writes next to Xr and Xi (the previous layer's
+// epilogue, or split3m for layer 0).  ComplexReLU(real) (activations.py:42-46)
+// is applied to Re in the epilogue, before Ys = Re + Im is formed.
+//
+// Activation layout ("3M planes"): X[b][mat][plane][c][ld], mat 0 = real,
+// 1 = imaginary, 2 = real + imaginary.
+// Tile 128 complex rows x 128 columns x 16 (k), 8 waves as 4 (M) x 2 (N), each
+// wave 32 x 64 with three accumulator sets (P1, P2, P3).  Stage (72 KB) = A: 3
+// matrices x 3 planes x [128][16] + B: 3 x 3 x [16][128]; two stages, one k-tile
+// in flight (LDS-DMA, dma.h).  LDS swizzles as in gemm_x6p_kernel.
+#include "dma.h"
+#include "gemm_common.h"
+
+namespace msfno {
+
+typedef __bf16 bf16x8c __attribute__((ext_vector_type(8)));
+typedef short s16x4c __attribute__((ext_vector_type(4)));
+typedef short s16x8c __attribute__((ext_vector_type(8)));
+
+constexpr int X6C_BM = 128, X6C_BN = 128, X6C_BK = 16;
+
+struct X6CParams {
+  const unsigned short* Aw;  // [mat][plane][kt][Mp][16]
+  int64_t a_mat, a_plane;
+  int Mp;
+  const unsigned short* X;   // [b][mat][plane][ci][ldx]
+  int64_t x_b, x_mat, x_plane;
+  int ldx;
+  unsigned short* Y;         // planes out [b][mat][plane][co][ldy] (hidden layers)
+  int64_t y_b, y_mat, y_plane;
+  int ldy;
+  float* S;                  // fp32 out (output layer): Re rows at S + b*s_b, Im at + s_im
+  int64_t s_b, s_im;
+  int ldS;
+  int co, ci, N;
+  int tiles_m, tiles_n;
+  int relu;
+};
+
+// A image of one layer: Wr, Wi, Ws = Wr + Wi (co x ci each) from the reference
+// weight w (ci, co, 2), each split into [plane][kt][Mp][16]
+__global__ void spec_weights_3m_kernel(SpecWeightsX6p a) {
+  const int64_t total = a.start[a.nlayers];
+  for (int64_t g = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; g < total;
+       g += (int64_t)gridDim.x * blockDim.x) {
+    int l = 0;
+    while (l + 1 < a.nlayers && g >= a.start[l + 1]) ++l;
+    const int ci = a.ci[l], co = a.co[l];
+    const int Mp = (co + X6C_BM - 1) / X6C_BM * X6C_BM, KT = (ci + X6C_BK - 1) / X6C_BK;
+    const int64_t n = (int64_t)Mp * KT * 8;  // pairs per plane
+    const int64_t e = g - a.start[l];
+    const int mat = (int)(e / n);
+    const int64_t f = e - mat * n;
+    const int64_t idx = 2 * f;
+    const int kt = (int)(idx / ((int64_t)Mp * 16));
+    const int rem = (int)(idx - (int64_t)kt * Mp * 16);
+    const int o = rem >> 4, k0 = kt * 16 + (rem & 15);
+    float v[2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const int i = k0 + t;
+      float x = 0.f;
+      if (o < co && i < ci) {
+        const float wr = a.w[l][((int64_t)i * co + o) * 2], wi = a.w[l][((int64_t)i * co + o) * 2 + 1];
+        x = mat == 0 ? wr : (mat == 1 ? wi : wr + wi);
+      }
+      v[t] = x;
+    }
+    uint32_t t0, t1, t2;
+    split2(v[0], v[1], t0, t1, t2);
+    uint32_t* out = reinterpret_cast<uint32_t*>(a.out[l]) + mat * 3 * n + f;
+    out[0] = t0;
+    out[n] = t1;
+    out[2 * n] = t2;
+  }
+}
+
+// S fp32 rows [b][ri][c] (ld ldS) -> 3M planes [b][mat][plane][c][ldx]
+__global__ void split3m_kernel(const float* __restrict__ S, unsigned short* __restrict__ X, int C,
+                               int N, int ldS, int ldx, int64_t x_b, int64_t x_mat,
+                               int64_t x_plane) {
+  const int b = blockIdx.y;
+  const int cp = (N + 1) / 2;
+  const int64_t n = (int64_t)C * cp;
+  const float* Sb = S + (int64_t)b * 2 * C * ldS;
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < n;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const int c = (int)(e / cp), col = 2 * (int)(e - (int64_t)c * cp);
+    const float* re = Sb + (int64_t)c * ldS + col;
+    const float* im = Sb + (int64_t)(C + c) * ldS + col;
+    const bool two = col + 1 < N;
+    const float r0 = re[0], r1 = two ? re[1] : 0.f;
+    const float i0 = im[0], i1 = two ? im[1] : 0.f;
+    const float v[3][2] = {{r0, r1}, {i0, i1}, {r0 + i0, r1 + i1}};
+    unsigned short* d = X + b * x_b + (int64_t)c * ldx + col;
+#pragma unroll
+    for (int mat = 0; mat < 3; ++mat) {
+      uint32_t t0, t1, t2;
+      split2(v[mat][0], v[mat][1], t0, t1, t2);
+      unsigned short* q = d + mat * x_mat;
+      if (two) {
+        *reinterpret_cast<uint32_t*>(q) = t0;
+        *reinterpret_cast<uint32_t*>(q + x_plane) = t1;
+        *reinterpret_cast<uint32_t*>(q + 2 * x_plane) = t2;
+      } else {
+        q[0] = (unsigned short)t0;
+        q[x_plane] = (unsigned short)t1;
+        q[2 * x_plane] = (unsigned short)t2;
+      }
+    }
+  }
+}
+
+template <bool PLANES_OUT>
+__global__ __launch_bounds__(512) void gemm_x6c_kernel(X6CParams p) {
+  constexpr int BM = X6C_BM, BN = X6C_BN, BK = X6C_BK;
+  constexpr int WGM = 4, WGN = 2;
+  constexpr int WM = BM / WGM, WN = BN / WGN;  // 32 x 64
+  constexpr int MT = WM / 32, NT = WN / 32;
+  constexpr int A_PLANE = BM * BK, B_PLANE = BK * BN;  // bf16 elements per matrix plane
+  constexpr int A_ALL = 9 * A_PLANE;
+  constexpr int STAGE = 9 * (A_PLANE + B_PLANE);        // 72 KB
+  constexpr int NSTAGE = 2;
+  constexpr int RING_BYTES = NSTAGE * STAGE * 2;
+  constexpr int EPI_BYTES = 32 * WGM * (BN + 8) * 4;
+  constexpr int LDS_BYTES = RING_BYTES > EPI_BYTES ? RING_BYTES : EPI_BYTES;
+  static_assert(STAGE * 2 == 72 * 1024, "stage = 72 pieces of 1 KB");
+  __shared__ __attribute__((aligned(16))) char lds_raw[LDS_BYTES];
+  unsigned short* const ring = reinterpret_cast<unsigned short*>(lds_raw);
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wm = wave / WGN, wn = wave % WGN;
+  const int half = lane >> 5, l32 = lane & 31;
+
+  const int lin = xcd_remap(blockIdx.x, gridDim.x);
+  const int tm = lin % p.tiles_m, tn = lin / p.tiles_m;
+  const int z = blockIdx.z;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int K = p.ci, N = p.N, ldx = p.ldx;
+  const int nk = (K + BK - 1) / BK;
+  const unsigned short* X = p.X + z * p.x_b;
+
+  // LDS-DMA pieces c = wave + 8 q (q < 9): c < 36 -> A (matrix-plane c / 4, rows
+  // 32 (c % 4) ..), else B (matrix-plane (c - 36) / 4, k rows 4 ((c - 36) % 4) ..)
+  const unsigned short* src[9];
+  int dst[9];
+  int brow[9];  // B: k row of this lane within the k-tile (-1 for A pieces)
+#pragma unroll
+  for (int q = 0; q < 9; ++q) {
+    const int c = wave + 8 * q;
+    if (c < 36) {
+      const int mp = c >> 2, mb = c & 3;
+      const int mat = mp / 3, pl = mp - 3 * mat;
+      const int m = 32 * mb + (lane >> 1);
+      const int h = (lane & 1) ^ ((m >> 3) & 1);
+      src[q] = p.Aw + mat * p.a_mat + pl * p.a_plane + (int64_t)(m0 + m) * 16 + 8 * h;
+      dst[q] = mp * A_PLANE + mb * 32 * BK;
+      brow[q] = -1;
+    } else {
+      const int cb = c - 36;
+      const int mp = cb >> 2, rq = cb & 3;
+      const int mat = mp / 3, pl = mp - 3 * mat;
+      const int row = 4 * rq + (lane >> 4);
+      const int gu = (lane & 15) ^ (4 * (row & 3));
+      src[q] = X + mat * p.x_mat + pl * p.x_plane + min(n0 + 8 * gu, ldx - 8);
+      dst[q] = A_ALL + mp * B_PLANE + rq * 4 * BN;
+      brow[q] = row;
+    }
+  }
+  const int64_t a_kstride = (int64_t)p.Mp * 16;
+  const uint32_t ring_lds = lds_addr(ring);
+  auto issue = [&](int kt, int st) {
+    const uint32_t base = ring_lds + (uint32_t)(st * STAGE * 2);
+#pragma unroll
+    for (int q = 0; q < 9; ++q) {
+      const unsigned short* g = brow[q] < 0
+                                    ? src[q] + kt * a_kstride
+                                    : src[q] + (int64_t)min(kt * BK + brow[q], K - 1) * ldx;
+      glds16(g, base + (uint32_t)(dst[q] * 2));
+    }
+  };
+
+  floatx16 acc[3][MT][NT];
+#pragma unroll
+  for (int t = 0; t < 3; ++t)
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+      for (int j = 0; j < NT; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[t][i][j][r] = 0.f;
+  int a_off[MT];
+#pragma unroll
+  for (int i = 0; i < MT; ++i) {
+    const int row = wm * WM + i * 32 + l32;
+    a_off[i] = row * BK + 8 * (half ^ ((row >> 3) & 1));
+  }
+  const int li = lane & 15, g16 = (lane >> 4) & 1;
+  const int br = 8 * half + (li >> 2);
+  int b_off[NT];
+#pragma unroll
+  for (int j = 0; j < NT; ++j) {
+    const int c = wn * WN + j * 32 + 16 * g16 + 4 * (li & 3);
+    b_off[j] = A_ALL + br * BN + (((c >> 3) ^ (4 * (br & 3))) << 3) + (c & 7);
+  }
+  auto mfma_tile = [&](int st) {
+    typedef __attribute__((address_space(3))) s16x4c lds_s16x4;
+    const unsigned short* base = ring + st * STAGE;
+#pragma unroll
+    for (int mat = 0; mat < 3; ++mat) {
+      bf16x8c a[MT][3];
+#pragma unroll
+      for (int i = 0; i < MT; ++i)
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl)
+          a[i][pl] = *reinterpret_cast<const bf16x8c*>(base + (mat * 3 + pl) * A_PLANE + a_off[i]);
+#pragma unroll
+      for (int j = 0; j < NT; ++j) {
+        bf16x8c b[3];
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl) {
+          const unsigned short* q = base + (mat * 3 + pl) * B_PLANE + b_off[j];
+          const s16x4c lo4 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+              (lds_s16x4*)((__attribute__((address_space(3))) unsigned short*)q));
+          const s16x4c hi4 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+              (lds_s16x4*)((__attribute__((address_space(3))) unsigned short*)(q + 4 * BN)));
+          const s16x8c v = {lo4[0], lo4[1], lo4[2], lo4[3], hi4[0], hi4[1], hi4[2], hi4[3]};
+          b[pl] = __builtin_bit_cast(bf16x8c, v);
+        }
+#pragma unroll
+        for (int i = 0; i < MT; ++i) {
+          floatx16 c = acc[mat][i][j];
+          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i][2], b[0], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i][1], b[1], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i][0], b[2], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i][1], b[0], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i][0], b[1], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i][0], b[0], c, 0, 0, 0);
+          acc[mat][i][j] = c;
+        }
+      }
+    }
+  };
+
+  issue(0, 0);
+  for (int kt = 0; kt < nk; ++kt) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // my DMA of k-tile kt landed
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // everyone's landed; stage (kt + 1) & 1 is free
+    if (kt + 1 < nk) issue(kt + 1, (kt + 1) & 1);
+    __builtin_amdgcn_s_setprio(1);
+    mfma_tile(kt & 1);
+    __builtin_amdgcn_s_setprio(0);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  // Re = P1 - P2 (ComplexReLU on hidden layers), Im = P3 - P1 - P2, Ys = Re + Im
+#pragma unroll
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int j = 0; j < NT; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float p1 = acc[0][i][j][r], p2 = acc[1][i][j][r], p3 = acc[2][i][j][r];
+        float re = p1 - p2;
+        const float im = p3 - p1 - p2;
+        if (p.relu) re = fmaxf(re, 0.f);
+        acc[0][i][j][r] = re;
+        acc[1][i][j][r] = im;
+        acc[2][i][j][r] = re + im;
+      }
+  float* lds = reinterpret_cast<float*>(lds_raw);
+  GemmParams q{};
+  q.vecC = 1;
+  if constexpr (PLANES_OUT) {
+#pragma unroll
+    for (int mat = 0; mat < 3; ++mat) {
+      q.Cx = p.Y + mat * p.y_mat;
+      q.sC = p.y_b;
+      q.sCxp = p.y_plane;
+      gemm_epilogue<BM, BN, EPI_PLANES, WGM, WGN>(q, acc[mat], lds, nullptr, nullptr, nullptr,
+                                                  p.co, N, p.ldy, m0, n0, 0);
+      __syncthreads();
+    }
+  } else {
+#pragma unroll
+    for (int mat = 0; mat < 2; ++mat) {
+      float* C = p.S + z * p.s_b + (mat ? p.s_im : 0);
+      q.vecC = (p.ldS % 4 == 0) && ((reinterpret_cast<uintptr_t>(C) & 15) == 0);
+      gemm_epilogue<BM, BN, 0, WGM, WGN>(q, acc[mat], lds, nullptr, C, nullptr, p.co, N, p.ldS,
+                                         m0, n0, 0);
+      __syncthreads();
+    }
+  }
+}
+
+// ---- host ---------------------------------------------------------------------
+
+size_t gemm_x6c_weight_bytes(int co, int ci) {
+  const int64_t Mp = round_up(co, X6C_BM), Kp = round_up(ci, X6C_BK);
+  return (size_t)round_up(3 * 3 * Mp * Kp * 2, 256);
+}
+
+size_t spec_weights_3m_layout(SpecWeightsX6p& a) {
+  size_t bytes = 0;
+  a.start[0] = 0;
+  for (int l = 0; l < a.nlayers; ++l) {
+    a.start[l + 1] = a.start[l] + 3 * round_up(a.co[l], X6C_BM) * cdiv(a.ci[l], X6C_BK) * 8;
+    bytes += gemm_x6c_weight_bytes(a.co[l], a.ci[l]);
+  }
+  return bytes;
+}
+
+int launch_spec_weights_3m(const SpecWeightsX6p& a, hipStream_t s) {
+  if (a.nlayers <= 0) return MSFNO_OK;
+  const int blocks = (int)std::min<int64_t>(cdiv(a.start[a.nlayers], 256), 4096);
+  hipLaunchKernelGGL(spec_weights_3m_kernel, dim3(blocks), dim3(256), 0, s, a);
+  return launch_check("spec_weights_3m");
+}
+
+int launch_split3m(const float* S, unsigned short* X, int B, int C, int N, int ldS, int ldx,
+                   hipStream_t s) {
+  MSFNO_REQUIRE(ldx % 8 == 0, MSFNO_EINVAL, "split3m: ld must be a multiple of 8");
+  const int64_t x_plane = (int64_t)C * ldx;
+  const int64_t n = (int64_t)C * ((N + 1) / 2);
+  const int blocks = (int)std::min<int64_t>(cdiv(n, 256), 2048);
+  hipLaunchKernelGGL(split3m_kernel, dim3(blocks, B), dim3(256), 0, s, S, X, C, N, ldS, ldx,
+                     9 * x_plane, 3 * x_plane, x_plane);
+  return launch_check("split3m");
+}
+
+// one spectral-MLP layer: X (3M planes, ci rows, ld ldx) -> Y (3M planes, co rows,
+// ld ldx; relu) or, with S given, fp32 rows [b][re/im][co] of S (ld ldS)
+int gemm_x6c(const unsigned short* Aw, int co, int ci, const unsigned short* X, int N, int ldx,
+             unsigned short* Y, float* S, int ldS, bool relu, int B, hipStream_t s) {
+  if (co <= 0 || N <= 0 || B <= 0) return MSFNO_OK;
+  MSFNO_REQUIRE(ldx % 8 == 0 && ldx >= 8 && (reinterpret_cast<uintptr_t>(X) & 15) == 0,
+                MSFNO_EINVAL, "gemm_x6c: X planes need ld % 8 == 0 and 16-B alignment");
+  MSFNO_REQUIRE((Y != nullptr) != (S != nullptr), MSFNO_EINVAL, "gemm_x6c: one output");
+  X6CParams p{};
+  p.Mp = (int)round_up(co, X6C_BM);
+  const int KT = (int)cdiv(ci, X6C_BK);
+  p.Aw = Aw;
+  p.a_plane = (int64_t)p.Mp * KT * 16;
+  p.a_mat = 3 * p.a_plane;
+  p.X = X;
+  p.x_plane = (int64_t)ci * ldx;
+  p.x_mat = 3 * p.x_plane;
+  p.x_b = 3 * p.x_mat;
+  p.ldx = ldx;
+  p.Y = Y;
+  p.y_plane = (int64_t)co * ldx;
+  p.y_mat = 3 * p.y_plane;
+  p.y_b = 3 * p.y_mat;
+  p.ldy = ldx;
+  p.S = S;
+  p.s_b = 2LL * co * ldS;
+  p.s_im = (int64_t)co * ldS;
+  p.ldS = ldS;
+  p.co = co; p.ci = ci; p.N = N;
+  p.tiles_m = p.Mp / X6C_BM;
+  p.tiles_n = (int)cdiv(N, X6C_BN);
+  p.relu = relu ? 1 : 0;
+  const dim3 grid(p.tiles_m * p.tiles_n, 1, B);
+  if (Y)
+    hipLaunchKernelGGL(gemm_x6c_kernel<true>, grid, dim3(512), 0, s, p);
+  else
+    hipLaunchKernelGGL(gemm_x6c_kernel<false>, grid, dim3(512), 0, s, p);
+  return launch_check("gemm_x6c");
+}
+
+}  // namespace msfno
