@@ -205,7 +205,16 @@ int side_ctx(SideCtx** out) {
   MSFNO_REQUIRE(dev >= 0 && dev < 64, MSFNO_EINVAL, "device index out of range");
   SideCtx& c = ctx[dev];
   if (!c.side) {
-    MSFNO_CHECK_HIP(hipStreamCreateWithFlags(&c.side, hipStreamNonBlocking));
+    // side stream at the lowest priority: the skip GEMM fills what the spectral path
+    // leaves (+1 % over equal priority, measured); MSFNO_SIDE_PRIO=normal|high for A/B
+    const char* pe = getenv("MSFNO_SIDE_PRIO");
+    int least = 0, greatest = 0;
+    MSFNO_CHECK_HIP(hipDeviceGetStreamPriorityRange(&least, &greatest));
+    if (pe && std::string(pe) == "normal")
+      MSFNO_CHECK_HIP(hipStreamCreateWithFlags(&c.side, hipStreamNonBlocking));
+    else
+      MSFNO_CHECK_HIP(hipStreamCreateWithPriority(
+          &c.side, hipStreamNonBlocking, (pe && std::string(pe) == "high") ? greatest : least));
     MSFNO_CHECK_HIP(hipEventCreateWithFlags(&c.fork, hipEventDisableTiming));
     MSFNO_CHECK_HIP(hipEventCreateWithFlags(&c.join, hipEventDisableTiming));
   }
