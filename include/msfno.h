@@ -164,6 +164,43 @@ int msfno_mlp_forward(const msfno_mlp_desc* d, const float* x, const float* x2,
                       long long P, void* ws, size_t ws_bytes, void* stream);
 
 /* ---------------------------------------------------------------------------
+ * FiLM backward.  MSFNO fine-tunes only its FiLM
+ * generator: the filmed blocks and the decoder run with autograd, every SFNO
+ * weight is frozen (MSFNO/Models/sfno/sfnonet.py:787-860, the training loop of
+ * MSFNO/main.py).  These entry points give the gradients autograd would
+ * compute there.
+ *
+ * msfno_block_film_backward replaces the backward of
+ * FourierNeuralOperatorBlock_Filmed.forward(x, gamma, beta, scale)
+ * (sfnonet.py:359-393) with respect to gamma and beta: given dout = dL/d(out),
+ *   dgamma[b,c] = scale * sum_p du[b,c,p] * xhat[b,c,p],
+ *   dbeta[b,c]  = scale * sum_p du[b,c,p],
+ * with xhat = norm1(x1) (InstanceNorm-1 output), u = (1 + gamma scale) xhat +
+ * beta scale, du = dL/du (through the channel MLP when the block has one; the
+ * identity outer skip does not depend on u).  The forward up to x1 is recomputed
+ * (as the reference's checkpoint(blk, ...)).  dL/dx is not produced: with the
+ * reference default film_layers = 1 the filmed block is the last one and
+ * nothing before it takes gradients.
+ * ------------------------------------------------------------------------- */
+size_t msfno_block_film_backward_workspace_size(const msfno_block_desc* d, msfno_sht_plan_t fwd,
+                                                msfno_sht_plan_t inv, int B);
+int msfno_block_film_backward(const msfno_block_desc* d, msfno_sht_plan_t fwd,
+                              msfno_sht_plan_t inv, const float* x, const float* gamma,
+                              const float* beta, float film_scale, const float* dout,
+                              float* dgamma, float* dbeta, int B, void* ws, size_t ws_bytes,
+                              void* stream);
+
+/* Backward of the channel MLP (layers.py:145-178) to its first input, weights
+ * frozen: the decoder over cat(x, residual) (sfnonet.py:679-686) when the loss
+ * gradient dy = dL/dy reaches it.
+ *   dx = W1[:, :Cin]^T (GELU'(W1 [x ; x2] + b1) * (W2^T dy))
+ * (dL/dx2 is not produced: x2 is the network input.) */
+size_t msfno_mlp_backward_input_workspace_size(const msfno_mlp_desc* d, int B, long long P);
+int msfno_mlp_backward_input(const msfno_mlp_desc* d, const float* x, const float* x2,
+                             const float* dy, float* dx, int B, long long P, void* ws,
+                             size_t ws_bytes, void* stream);
+
+/* ---------------------------------------------------------------------------
  * Latitude-band sharded SFNO-Block (multi-GPU form of
  * msfno_block_forward).  The reference runs one block per process on the whole
  * field (DDP = replicas, MSFNO/main.py:1153); this splits ONE field batch over

@@ -1330,3 +1330,194 @@ int msfno_mlp_forward(const msfno_mlp_desc* d, const float* x, const float* x2,
 }
 
 }  // extern "C"
+
+// ---------------------------------------------------------------------------
+// FiLM backward: gradients of a loss with respect to the
+// FiLM modulation (gamma, beta) of a filmed block and through the decoder, with
+// every SFNO weight frozen, as MSFNO fine-tunes its FiLM generator
+// (MSFNO/Models/sfno/sfnonet.py:787-860: blocks before the filmed ones run under
+// no_grad; the filmed block and the decoder run with autograd).
+// ---------------------------------------------------------------------------
+namespace msfno {
+
+struct FilmBwdBufs {
+  BlockBufs b;
+  float *an, *tn, *du, *pre, *dh, *W2T, *W1T;
+  void *wsa, *wsb;
+  size_t wsa_b, wsb_b;
+};
+
+static void carve_film_bwd(Carve& cv, FilmBwdBufs& r, const msfno_block_desc* d,
+                           const msfno_sht_plan_s* f, const msfno_sht_plan_s* g, int B) {
+  carve_block(cv, r.b, d, f, g, B, true);
+  const int64_t C = d->C, BC = (int64_t)B * C, P = (int64_t)g->nlat * g->nlon;
+  r.an = cv.take<float>(BC);
+  r.tn = cv.take<float>(BC);
+  r.du = r.pre = r.dh = r.W2T = r.W1T = nullptr;
+  r.wsa = r.wsb = nullptr;
+  r.wsa_b = r.wsb_b = 0;
+  if (!d->has_mlp) return;
+  const int64_t Hd = d->mlp_hidden;
+  r.du = cv.take<float>(BC * P);
+  r.pre = cv.take<float>((int64_t)B * Hd * P);
+  r.dh = cv.take<float>((int64_t)B * Hd * P);
+  r.W2T = cv.take<float>(Hd * C);
+  r.W1T = cv.take<float>(C * Hd);
+  if ((r.wsa_b = gemm_dense_workspace((int)Hd, (int)C, 1))) r.wsa = cv.take<char>(r.wsa_b);
+  if ((r.wsb_b = gemm_dense_workspace((int)C, (int)Hd, 1))) r.wsb = cv.take<char>(r.wsb_b);
+}
+
+}  // namespace msfno
+
+extern "C" {
+
+size_t msfno_block_film_backward_workspace_size(const msfno_block_desc* d, msfno_sht_plan_t f,
+                                                msfno_sht_plan_t g, int B) {
+  if (check_pair(d, f, g) != MSFNO_OK || B <= 0) return 0;
+  Carve cv;
+  FilmBwdBufs r;
+  carve_film_bwd(cv, r, d, f, g, B);
+  return cv.off;
+}
+
+int msfno_block_film_backward(const msfno_block_desc* d, msfno_sht_plan_t f, msfno_sht_plan_t g,
+                              const float* x, const float* gamma, const float* beta,
+                              float film_scale, const float* dout, float* dgamma, float* dbeta,
+                              int B, void* ws, size_t ws_bytes, void* stream) {
+  MSFNO_TRY(check_pair(d, f, g));
+  MSFNO_REQUIRE(x && gamma && beta && dout && dgamma && dbeta && B > 0, MSFNO_EINVAL,
+                "film backward: missing tensors");
+  MSFNO_REQUIRE(ws_bytes >= msfno_block_film_backward_workspace_size(d, f, g, B),
+                MSFNO_EWORKSPACE, "workspace too small");
+  MSFNO_REQUIRE(d->outer_skip != MSFNO_SKIP_LINEAR, MSFNO_EUNSUPPORTED,
+                "outer_skip='linear' is not supported by the fused block");
+  MSFNO_REQUIRE(f->nlat == g->nlat && f->nlon == g->nlon || d->inner_skip == MSFNO_SKIP_NONE,
+                MSFNO_EINVAL, "skips require equal input and output grids");
+  hipStream_t s = (hipStream_t)stream;
+  Carve cv;
+  cv.base = (char*)ws;
+  FilmBwdBufs r;
+  carve_film_bwd(cv, r, d, f, g, B);
+  BlockBufs& b = r.b;
+  const int64_t C = d->C, BC = (int64_t)B * C;
+  const int64_t P = (int64_t)g->nlat * g->nlon;
+  const int act = d->filter_type == MSFNO_FILTER_LINEAR ? 1 : 0;
+  // ---- recompute x1 (fp32) and its InstanceNorm-1 statistics (the forward's
+  // checkpoint, as the reference's checkpoint(blk, ...) does) ----------------------
+  float* x1 = b.x1;
+  if (d->inner_skip == MSFNO_SKIP_LINEAR) {
+    MSFNO_REQUIRE(d->skip_w, MSFNO_EINVAL, "missing inner_skip weight");
+    GemmEpi e;
+    e.bias = d->skip_b;
+    MSFNO_TRY(gemm_dense(ROLE_SKIP, TILE_128x256, d->skip_w, x, x1, (int)C, (int)P, (int)C,
+                         (int)C, (int)P, (int)P, 0, C * P, C * P, B, e, b.dw.skip, b.dw.skip_b, s));
+  }
+  MSFNO_TRY(run_spectral(d, f, g, b, x, B, true, s));
+  const float* skip_src = d->inner_skip == MSFNO_SKIP_LINEAR ? x1
+                          : (d->inner_skip == MSFNO_SKIP_IDENTITY ? x : nullptr);
+  MSFNO_TRY(run_inverse_fft(g, b, B, (int)C, x1, skip_src, b.st1, act, s, nullptr));
+  const int64_t np = g->nlat, cnt = g->nlon;
+  // norm1 alone: xhat = an * x1 + tn; norm1 + FiLM: u = sc1 * x1 + sh1
+  MSFNO_TRY(launch_chan_affine(b.st1, np, cnt, cnt, B, (int)C, d->norm1_w, d->norm1_b,
+                               d->norm_eps, nullptr, nullptr, 0.f, r.an, r.tn, s));
+  const float* du = dout;
+  if (d->has_mlp) {
+    // out = W2 GELU(W1 u + b1) + b2 (+ x):  du = W1^T (GELU'(pre) * W2^T dout)
+    MSFNO_REQUIRE(d->fc1_w && d->fc2_w, MSFNO_EINVAL, "missing MLP weights");
+    MSFNO_TRY(launch_chan_affine(b.st1, np, cnt, cnt, B, (int)C, d->norm1_w, d->norm1_b,
+                                 d->norm_eps, gamma, beta, film_scale, b.sc1, b.sh1, s));
+    const int64_t Hd = d->mlp_hidden;
+    const int Pi = (int)P;
+    MSFNO_TRY(launch_fold_affine(d->fc1_w, d->fc1_b, b.sc1, b.sh1, b.W1f, b.b1f, B, (int)Hd,
+                                 (int)C, s));
+    GemmEpi e1;  // pre-activation of fc1 (no GELU)
+    e1.bias = b.b1f;
+    e1.sBias = Hd;
+    MSFNO_TRY(gemm_dense(ROLE_FC1, TILE_128x256, b.W1f, x1, r.pre, (int)Hd, Pi, (int)C, (int)C,
+                         Pi, Pi, Hd * C, C * P, Hd * P, B, e1, b.dw.fc1, b.dw.fc1_b, s));
+    MSFNO_TRY(launch_transpose_mat(d->fc2_w, (int)C, (int)Hd, (int)Hd, r.W2T, s));
+    GemmEpi e0;
+    MSFNO_TRY(gemm_dense(ROLE_FC2, TILE_256x128, r.W2T, dout, r.dh, (int)Hd, Pi, (int)C, (int)C,
+                         Pi, Pi, 0, C * P, Hd * P, B, e0, r.wsa, r.wsa_b, s));
+    MSFNO_TRY(launch_gelu_grad_mul(r.dh, r.pre, (int64_t)B * Hd * P, s));
+    MSFNO_TRY(launch_transpose_mat(d->fc1_w, (int)Hd, (int)C, (int)C, r.W1T, s));
+    MSFNO_TRY(gemm_dense(ROLE_FC2, TILE_256x128, r.W1T, r.dh, r.du, (int)C, Pi, (int)Hd, (int)Hd,
+                         Pi, Pi, 0, Hd * P, C * P, B, e0, r.wsb, r.wsb_b, s));
+    du = r.du;
+  }
+  // dgamma = s sum_p du xhat, dbeta = s sum_p du  (FiLM: (1 + gamma s) xhat + beta s)
+  return launch_film_grad_reduce(du, x1, r.an, r.tn, film_scale, (int)BC, P, dgamma, dbeta, s);
+}
+
+size_t msfno_mlp_backward_input_workspace_size(const msfno_mlp_desc* d, int B, long long P) {
+  if (!d || B <= 0 || P <= 0) return 0;
+  Carve cv;
+  cv.take<float>((int64_t)B * d->Hid * P);  // pre
+  cv.take<float>((int64_t)B * d->Hid * P);  // t, then dh
+  cv.take<float>((int64_t)d->Hid * d->Cout);  // W2^T
+  cv.take<float>((int64_t)d->Cin * d->Hid);   // W1[:, :Cin]^T
+  cv.take<char>(gemm_dense_workspace(d->Hid, d->Cin, 1));
+  if (d->Cin2 > 0) cv.take<char>(gemm_dense_workspace(d->Hid, d->Cin2, 1));
+  cv.take<char>(gemm_dense_workspace(d->Hid, d->Cout, 1));
+  cv.take<char>(gemm_dense_workspace(d->Cin, d->Hid, 1));
+  return cv.off;
+}
+
+int msfno_mlp_backward_input(const msfno_mlp_desc* d, const float* x, const float* x2,
+                             const float* dy, float* dx, int B, long long P, void* ws,
+                             size_t ws_bytes, void* stream) {
+  MSFNO_REQUIRE(d && x && dy && dx && d->fc1_w && d->fc2_w && d->fc1_b, MSFNO_EINVAL,
+                "mlp backward: missing tensors");
+  MSFNO_REQUIRE(d->Cin > 0 && d->Hid > 0 && d->Cout > 0 && d->Cin2 >= 0 && B > 0 && P > 0 &&
+                    P <= 0x7fffffff,
+                MSFNO_EINVAL, "mlp backward: bad sizes");
+  MSFNO_REQUIRE((d->Cin2 > 0) == (x2 != nullptr), MSFNO_EINVAL,
+                "mlp backward: x2 must be given exactly when Cin2 > 0");
+  MSFNO_REQUIRE(ws_bytes >= msfno_mlp_backward_input_workspace_size(d, B, P), MSFNO_EWORKSPACE,
+                "workspace too small");
+  hipStream_t s = (hipStream_t)stream;
+  Carve cv;
+  cv.base = (char*)ws;
+  const int64_t Hd = d->Hid, Ct = d->Cin + d->Cin2;
+  const int Pi = (int)P;
+  float* pre = cv.take<float>((int64_t)B * Hd * P);
+  float* t = cv.take<float>((int64_t)B * Hd * P);
+  float* W2T = cv.take<float>(Hd * d->Cout);
+  float* W1T = cv.take<float>((int64_t)d->Cin * Hd);
+  const size_t w1b = gemm_dense_workspace((int)Hd, d->Cin, 1);
+  void* w1 = cv.take<char>(w1b);
+  const size_t w1b2 = d->Cin2 > 0 ? gemm_dense_workspace((int)Hd, d->Cin2, 1) : 0;
+  void* w12 = d->Cin2 > 0 ? cv.take<char>(w1b2) : nullptr;
+  const size_t w2b = gemm_dense_workspace((int)Hd, d->Cout, 1);
+  void* w2 = cv.take<char>(w2b);
+  const size_t w3b = gemm_dense_workspace(d->Cin, (int)Hd, 1);
+  void* w3 = cv.take<char>(w3b);
+  // pre = W1 [x ; x2] + b1 (fc1 without its GELU)
+  if (d->Cin2 > 0) {
+    GemmEpi e0;
+    MSFNO_TRY(gemm_dense(ROLE_FC1, TILE_128x256, d->fc1_w, x, t, (int)Hd, Pi, d->Cin, (int)Ct, Pi,
+                         Pi, 0, (int64_t)d->Cin * P, Hd * P, B, e0, w1, w1b, s));
+    GemmEpi e1;
+    e1.bias = d->fc1_b;
+    e1.addend = t; e1.sD = Hd * P; e1.ldd = Pi;
+    MSFNO_TRY(gemm_dense(ROLE_FC1, TILE_128x256, d->fc1_w + d->Cin, x2, pre, (int)Hd, Pi, d->Cin2,
+                         (int)Ct, Pi, Pi, 0, (int64_t)d->Cin2 * P, Hd * P, B, e1, w12, w1b2, s));
+  } else {
+    GemmEpi e1;
+    e1.bias = d->fc1_b;
+    MSFNO_TRY(gemm_dense(ROLE_FC1, TILE_128x256, d->fc1_w, x, pre, (int)Hd, Pi, d->Cin, d->Cin, Pi,
+                         Pi, 0, (int64_t)d->Cin * P, Hd * P, B, e1, w1, w1b, s));
+  }
+  // dh = GELU'(pre) * W2^T dy ;  dx = W1[:, :Cin]^T dh
+  MSFNO_TRY(launch_transpose_mat(d->fc2_w, d->Cout, (int)Hd, (int)Hd, W2T, s));
+  GemmEpi e0;
+  float* dh = t;
+  MSFNO_TRY(gemm_dense(ROLE_FC2, TILE_256x128, W2T, dy, dh, (int)Hd, Pi, d->Cout, d->Cout, Pi, Pi,
+                       0, (int64_t)d->Cout * P, Hd * P, B, e0, w2, w2b, s));
+  MSFNO_TRY(launch_gelu_grad_mul(dh, pre, (int64_t)B * Hd * P, s));
+  MSFNO_TRY(launch_transpose_mat(d->fc1_w, (int)Hd, d->Cin, (int)Ct, W1T, s));
+  return gemm_dense(ROLE_FC2, TILE_256x128, W1T, dh, dx, d->Cin, Pi, (int)Hd, (int)Hd, Pi, Pi, 0,
+                    Hd * P, (int64_t)d->Cin * P, B, e0, w3, w3b, s);
+}
+
+}  // extern "C"

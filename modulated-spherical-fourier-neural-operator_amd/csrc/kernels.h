@@ -84,6 +84,12 @@ int gemm_c3m(const float* Ar, const float* Ai, const float* X, float* Y, int co,
 int launch_expand_complex_weight(const float* w, float* Wexp, int Ci, int Co, hipStream_t s);
 // (mmax,lmax,nlat) reference table -> plan GEMM layout (general or symmetric)
 int launch_relayout_table(const msfno_sht_plan_s& p, const float* table, hipStream_t s);
+// FiLM backward (film_bwd.hip)
+int launch_transpose_mat(const float* A, int rows, int cols, int lda, float* AT, hipStream_t s);
+int launch_gelu_grad_mul(float* dh, const float* pre, int64_t n, hipStream_t s);
+int launch_film_grad_reduce(const float* du, const float* x1, const float* an, const float* tn,
+                            float scale, int BC, int64_t P, float* dgamma, float* dbeta,
+                            hipStream_t s);
 // x6 Legendre table image (bf16x3 planes, rows padded to 16; gemm_x6d's B)
 int launch_relayout_table_x6(const msfno_sht_plan_s& p, const float* table, hipStream_t s);
 // symmetric forward transpose writing Xt as bf16x3 planes (plane stride pstride),

@@ -91,6 +91,13 @@ SIGNATURES = [
     ("msfno_mlp_workspace_size", _sz, [ctypes.POINTER(MlpDesc), _i, ctypes.c_longlong]),
     ("msfno_mlp_forward", _i, [ctypes.POINTER(MlpDesc), _vp, _vp, _vp, ctypes.c_longlong, _vp, _i,
                                ctypes.c_longlong, _vp, _sz, _vp]),
+    ("msfno_block_film_backward_workspace_size", _sz, [ctypes.POINTER(BlockDesc), _vp, _vp, _i]),
+    ("msfno_block_film_backward", _i, [ctypes.POINTER(BlockDesc), _vp, _vp, _vp, _vp, _vp, _f,
+                                       _vp, _vp, _vp, _i, _vp, _sz, _vp]),
+    ("msfno_mlp_backward_input_workspace_size", _sz, [ctypes.POINTER(MlpDesc), _i,
+                                                       ctypes.c_longlong]),
+    ("msfno_mlp_backward_input", _i, [ctypes.POINTER(MlpDesc), _vp, _vp, _vp, _vp, _i,
+                                      ctypes.c_longlong, _vp, _sz, _vp]),
     ("msfno_band_partition", _i, [_i, _i, _i, _i, _ip, _ip]),
     ("msfno_band_exchange_counts", _i, [_i, _i, _i, _i, _ip, _ip, _i, _i, _llp, _llp]),
     ("msfno_band_plan_create", _i, [_i, _i, _i, _i, _i, _i, _ip, _ip, ctypes.POINTER(_vp)]),

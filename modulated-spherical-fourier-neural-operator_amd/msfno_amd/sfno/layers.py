@@ -133,8 +133,51 @@ class MLP(nn.Module):
         del keep
         return out.to(dtype)
 
+    def native_backward_input(self, x, dy, x2=None):
+        """dL/dx of fc2(GELU(fc1(cat(x, x2)))) for frozen weights
+        (msfno_mlp_backward_input): the decoder's backward in FiLM fine-tuning."""
+        x = N.require_device_f32(x, "MLP input")
+        dy = N.require_device_f32(dy, "MLP output gradient")
+        B, Cin, H, W = x.shape
+        cin2 = 0
+        if x2 is not None:
+            x2 = N.require_device_f32(x2, "MLP second input")
+            cin2 = x2.shape[1]
+        d, keep = self.native_desc(cin2)
+        L = N.lib()
+        P = H * W
+        nbytes = L.msfno_mlp_backward_input_workspace_size(d, B, P)
+        ws = torch.empty(nbytes, dtype=torch.uint8, device=x.device)
+        dx = torch.empty(B, Cin, H, W, dtype=torch.float32, device=x.device)
+        N.check(L.msfno_mlp_backward_input(d, x.data_ptr(), N.ptr(x2), dy.data_ptr(),
+                                           dx.data_ptr(), B, P, ws.data_ptr(), nbytes,
+                                           N.stream_of(x.device)), "MLP.backward")
+        del keep
+        return dx
+
     def forward(self, x):
+        if torch.is_grad_enabled() and x.requires_grad:
+            return _MLPFn.apply(x, None, None, self)
         return self.native_forward(x)
+
+
+class _MLPFn(torch.autograd.Function):
+    """Native MLP forward; backward to the first input only (weights frozen, as in
+    MSFNO's FiLM fine-tuning, sfnonet.py:787-860)."""
+
+    @staticmethod
+    def forward(ctx, x, x2, addend, mlp):
+        ctx.mlp = mlp
+        ctx.save_for_backward(x, x2)
+        return mlp.native_forward(x, x2=x2, addend=addend)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, x2 = ctx.saved_tensors
+        if ctx.needs_input_grad[1] or ctx.needs_input_grad[2]:
+            raise NotImplementedError("MLP backward: gradients only to the first input")
+        dx = ctx.mlp.native_backward_input(x, dy, x2=x2)
+        return dx.to(x.dtype), None, None, None
 
 
 def _check_transforms(fwd, inv):

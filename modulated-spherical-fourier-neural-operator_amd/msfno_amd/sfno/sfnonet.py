@@ -200,7 +200,57 @@ class FourierNeuralOperatorBlock_Filmed(FourierNeuralOperatorBlock):
     _filmed = True
 
     def forward(self, x, gamma, beta, scale=1):
+        if torch.is_grad_enabled() and (gamma.requires_grad or beta.requires_grad
+                                        or x.requires_grad):
+            return _FilmedBlockFn.apply(x, gamma, beta, float(scale), self)
         return self._native_forward(x, gamma, beta, scale)
+
+    def native_film_backward(self, x, gamma, beta, scale, dout):
+        """(dL/dgamma, dL/dbeta) of this block for dout = dL/d(out), SFNO weights frozen
+        (msfno_block_film_backward; the forward up to x1 is recomputed)."""
+        x = N.require_device_f32(x, "block input")
+        dout = N.require_device_f32(dout, "block output gradient")
+        B, C, H, W = x.shape
+        fwd, inv = self._transforms()
+        pf = fwd._plan(x.device)
+        pi = inv._plan(x.device)
+        d, keep = self.native_desc()
+        g = gamma.detach().float().reshape(B, C).contiguous()
+        b = beta.detach().float().reshape(B, C).contiguous()
+        L = N.lib()
+        nbytes = L.msfno_block_film_backward_workspace_size(d, pf.handle, pi.handle, B)
+        ws = torch.empty(nbytes, dtype=torch.uint8, device=x.device)
+        dg = torch.empty(B, C, dtype=torch.float32, device=x.device)
+        db = torch.empty(B, C, dtype=torch.float32, device=x.device)
+        N.check(L.msfno_block_film_backward(d, pf.handle, pi.handle, x.data_ptr(), g.data_ptr(),
+                                            b.data_ptr(), float(scale), dout.data_ptr(),
+                                            dg.data_ptr(), db.data_ptr(), B, ws.data_ptr(),
+                                            nbytes, N.stream_of(x.device)),
+                "FourierNeuralOperatorBlock_Filmed.backward")
+        del keep
+        return dg, db
+
+
+class _FilmedBlockFn(torch.autograd.Function):
+    """Native filmed-block forward; backward to (gamma, beta) with the SFNO weights
+    frozen (sfnonet.py:787-860 runs the filmed blocks with autograd and every
+    earlier block under no_grad)."""
+
+    @staticmethod
+    def forward(ctx, x, gamma, beta, scale, blk):
+        ctx.blk, ctx.scale = blk, scale
+        ctx.save_for_backward(x, gamma, beta)
+        return blk._native_forward(x, gamma, beta, scale)
+
+    @staticmethod
+    def backward(ctx, dout):
+        x, gamma, beta = ctx.saved_tensors
+        if ctx.needs_input_grad[0]:
+            raise NotImplementedError(
+                "dL/dx through a filmed block is not on the MI355X path (film_layers > 1)")
+        dg, db = ctx.blk.native_film_backward(x, gamma, beta, ctx.scale, dout)
+        return None, dg.reshape(gamma.shape).to(gamma.dtype), \
+            db.reshape(beta.shape).to(beta.dtype), None, None
 
 
 def _trunc_normal_init(m):
@@ -344,10 +394,13 @@ class FourierNeuralOperatorNet(nn.Module):
         return self.encoder.native_forward(x, addend=self.pos_embed)
 
     def decode(self, x, residual):
-        """decoder(cat(x, residual)) (sfnonet.py:679-686) without materialising the concat."""
-        if self.big_skip:
-            return self.decoder.native_forward(x, x2=residual)
-        return self.decoder.native_forward(x)
+        """decoder(cat(x, residual)) (sfnonet.py:679-686) without materialising the concat;
+        with autograd (FiLM fine-tuning) the gradient reaches x through the frozen decoder."""
+        x2 = residual if self.big_skip else None
+        if torch.is_grad_enabled() and x.requires_grad:
+            from .layers import _MLPFn
+            return _MLPFn.apply(x, x2, None, self.decoder)
+        return self.decoder.native_forward(x, x2=x2)
 
     def forward_features(self, x):
         x = self.pos_drop(x)
