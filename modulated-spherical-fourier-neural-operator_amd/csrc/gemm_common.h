@@ -132,20 +132,23 @@ enum : int {
 // (waves WGM x WGN, wave w at (w / WGN, w % WGN)) as 32x32 MFMA blocks (row
 // (r&3)+8(r>>2)+4(lane>>5), col lane&31).  lds: at least 32*WGM*(BN+8) floats,
 // free (the caller's main loop ended with a barrier).
-template <int BM, int BN, int EPI, int WGM = 2, int WGN = 2, int MT, int NT>
-__device__ __forceinline__ void gemm_epilogue(const GemmParams& p, floatx16 (&acc)[MT][NT],
+// RB = 32: accumulators in the 32x32 MFMA block layout (floatx16 per block);
+// RB = 16: the 16x16 layout (floatx4: row 4 (lane >> 4) + r, col lane & 15)
+template <int BM, int BN, int EPI, int WGM = 2, int WGN = 2, int MT, int NT, int RB = 32,
+          class AccV = floatx16>
+__device__ __forceinline__ void gemm_epilogue(const GemmParams& p, AccV (&acc)[MT][NT],
                                               float* lds, const float* bias_s, float* C,
                                               const float* addend, int M, int N, int ldc,
                                               int m0, int n0, int dflags) {
   constexpr int NTHR = 64 * WGM * WGN;
   constexpr int WM = BM / WGM, WN = BN / WGN;
-  static_assert(MT == WM / 32 && NT == WN / 32, "accumulator shape");
+  static_assert(MT == WM / RB && NT == WN / RB, "accumulator shape");
   constexpr int CS_LD = BN + 8;
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WGN, wn = wave % WGN;
   const int half = lane >> 5, l32 = lane & 31;
-  (void)bias_s; (void)addend; (void)dflags;
+  (void)bias_s; (void)addend; (void)dflags; (void)half; (void)l32;
   // ---- epilogue through LDS ---------------------------------------------------
   // Per MFMA row-tile i the waves write their 32-row slices into a (32 WGM) x BN
   // row-major LDS image; then all threads walk it with 16-B vectors: bias,
@@ -153,18 +156,26 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, floatx16 (&ac
   // coalesced float4 stores.  Keeps the accumulators in AGPRs until here, the
   // epilogue VGPR-light, and the global traffic in full lines.
   float* Cs = lds;  // the main loop ended with a barrier: staging memory is free
-  constexpr int QPT = (32 * WGM * BN / 4) / NTHR;  // float4 per thread per row-tile
+  constexpr int QPT = (RB * WGM * BN / 4) / NTHR;  // float4 per thread per row-tile
   constexpr int QC = QPT < 8 ? QPT : 8;
-  static_assert(QPT * NTHR * 4 == 32 * WGM * BN && QPT % QC == 0, "epilogue mapping");
+  static_assert(QPT * NTHR * 4 == RB * WGM * BN && QPT % QC == 0, "epilogue mapping");
   const bool vecC = p.vecC;
 #pragma unroll
   for (int i = 0; i < MT; ++i) {
 #pragma unroll
-    for (int j = 0; j < NT; ++j)
+    for (int j = 0; j < NT; ++j) {
+      if constexpr (RB == 32) {
 #pragma unroll
-      for (int r = 0; r < 16; ++r)
-        Cs[(wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * half) * CS_LD + wn * WN + j * 32 + l32] =
-            acc[i][j][r];
+        for (int r = 0; r < 16; ++r)
+          Cs[(wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * half) * CS_LD + wn * WN + j * 32 + l32] =
+              acc[i][j][r];
+      } else {
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          Cs[(wm * 16 + 4 * (lane >> 4) + r) * CS_LD + wn * WN + j * 16 + (lane & 15)] =
+              acc[i][j][r];
+      }
+    }
     __syncthreads();
     // in chunks of QC float4 per thread (<= 8: bounds the epilogue's VGPRs)
     for (int qc = 0; qc < QPT; qc += QC) {
@@ -174,7 +185,7 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, floatx16 (&ac
         for (int q = 0; q < QC; ++q) {
           const int idx = tid + NTHR * (qc + q);
           const int lr = idx / (BN / 4);
-          const int row = min(m0 + (lr >> 5) * WM + i * 32 + (lr & 31), M - 1);
+          const int row = min(m0 + (lr / RB) * WM + i * RB + (lr % RB), M - 1);
           const int col = n0 + 4 * (idx % (BN / 4));
           const float* src = addend + (int64_t)row * p.ldd;
           if (vecC) {
@@ -199,7 +210,7 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, floatx16 (&ac
 #pragma unroll
         for (int q = 0; q < QC; ++q) {
           const int lr = (tid + NTHR * (qc + q)) / (BN / 4);
-          const int row = m0 + (lr >> 5) * WM + i * 32 + (lr & 31);
+          const int row = m0 + (lr / RB) * WM + i * RB + (lr % RB);
           bvq[q] = bias_s[min(row, M - 1) - m0];
         }
       }
@@ -208,7 +219,7 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, floatx16 (&ac
         const int idx = tid + NTHR * (qc + q);
         const int lr = idx / (BN / 4);
         const int c4 = idx % (BN / 4);
-        const int row = m0 + (lr >> 5) * WM + i * 32 + (lr & 31);
+        const int row = m0 + (lr / RB) * WM + i * RB + (lr % RB);
         const int col = n0 + 4 * c4;
         float4 v = cv[q];
         const int rr = min(row, M - 1);

@@ -6,10 +6,11 @@
 // MFMA), but B is not converted in the kernel: its producer already wrote the
 // three bf16 terms (EPI_PLANES epilogue, or launch_split_planes).  With no
 // conversion work left, the operands go HBM/L2 -> LDS by LDS-DMA
-// (global_load_lds_dwordx4, no VGPR staging) into a ring of three stages, so two
-// k-tiles are in flight while the third is multiplied: one raw s_barrier and one
-// counted vmcnt per k-tile (cdna_hip_programming.md §5, "Pipelining across
-// barriers").
+// (global_load_lds_dwordx4, no VGPR staging) into a ring of NSTAGE stages, so
+// NSTAGE - 1 k-tiles are in flight while one is multiplied: one raw s_barrier and
+// one counted vmcnt per k-tile (cdna_hip_programming.md §5, "Pipelining across
+// barriers").  Two stages (one tile ahead) measured 1-3 % faster than three: the
+// GEMM is clock (power) bound, not latency bound, at this size.
 //
 // Tile 256 x 256 x 16 (k), 8 waves as 4 (M) x 2 (N), each wave 64 x 128 as 2 x 4
 // blocks of v_mfma_f32_32x32x16_bf16 (the C layout of the fp32 kernel, so the
@@ -38,17 +39,18 @@ constexpr int X6P_BM = 256, X6P_BN = 256, X6P_BK = 16;
 
 // A (M x K fp32, row stride lda, batch stride sA) -> bf16x3 k-tiles
 // Ax[z][plane][kt][Mp][16], zero padded to Mp x (KT * 16)
+template <int TK>
 __global__ void split_a_tiles_kernel(const float* __restrict__ A, unsigned short* __restrict__ Ax,
                                      int M, int K, int lda, int64_t sA, int Mp, int KT) {
   const int z = blockIdx.y;
-  const int64_t plane = (int64_t)Mp * KT * 16;
+  const int64_t plane = (int64_t)Mp * KT * TK;
   const int64_t n = plane / 2;
   for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < n;
        e += (int64_t)gridDim.x * blockDim.x) {
     const int64_t idx = 2 * e;
-    const int kt = (int)(idx / ((int64_t)Mp * 16));
-    const int rem = (int)(idx - (int64_t)kt * Mp * 16);
-    const int m = rem >> 4, k = kt * 16 + (rem & 15);
+    const int kt = (int)(idx / ((int64_t)Mp * TK));
+    const int rem = (int)(idx - (int64_t)kt * Mp * TK);
+    const int m = rem / TK, k = kt * TK + (rem % TK);
     const float* a = A + z * sA + (int64_t)m * lda;
     const float v0 = (m < M && k < K) ? a[k] : 0.f;
     const float v1 = (m < M && k + 1 < K) ? a[k + 1] : 0.f;
@@ -129,7 +131,7 @@ __global__ void split_planes_kernel(const float* __restrict__ x, unsigned short*
   }
 }
 
-template <int EPI>
+template <int EPI, int NSTAGE = 3>
 __global__ __launch_bounds__(512) void gemm_x6p_kernel(GemmParams p) {
   constexpr int BM = X6P_BM, BN = X6P_BN, BK = X6P_BK;
   constexpr int WGM = 4, WGN = 2, NTHR = 512;
@@ -138,7 +140,6 @@ __global__ __launch_bounds__(512) void gemm_x6p_kernel(GemmParams p) {
   constexpr int A_PLANE = BM * BK;             // bf16 elements
   constexpr int B_PLANE = BK * BN;
   constexpr int STAGE = 3 * (A_PLANE + B_PLANE);
-  constexpr int NSTAGE = 3;
   constexpr int RING_BYTES = NSTAGE * STAGE * 2;
   constexpr int EPI_BYTES = 32 * WGM * (BN + 8) * 4;
   constexpr int LDS_BYTES = RING_BYTES > EPI_BYTES ? RING_BYTES : EPI_BYTES;
@@ -273,11 +274,11 @@ __global__ __launch_bounds__(512) void gemm_x6p_kernel(GemmParams p) {
 
   if constexpr (HAS_BIAS) __syncthreads();  // bias_s visible; no DMA in flight yet
   issue(0, 0);
-  if (nk > 1) issue(1, 1);
+  if (NSTAGE == 3 && nk > 1) issue(1, 1);
   int st = 0;
   for (int kt = 0; kt < nk; ++kt) {
     // my DMA of k-tile kt has landed (k-tile kt + 1 may stay in flight) ...
-    if (kt + 1 < nk)
+    if (NSTAGE == 3 && kt + 1 < nk)
       asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
     else
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -285,15 +286,183 @@ __global__ __launch_bounds__(512) void gemm_x6p_kernel(GemmParams p) {
     // wave has finished reading stage (kt - 1) % 3, which the next issue refills
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
-    if (kt + 2 < nk) issue(kt + 2, st == 0 ? 2 : st - 1);
+    if (NSTAGE == 3) {
+      if (kt + 2 < nk) issue(kt + 2, st == 0 ? 2 : st - 1);
+    } else {
+      if (kt + 1 < nk) issue(kt + 1, st ^ 1);
+    }
     __builtin_amdgcn_s_setprio(1);
     mfma_tile(st);
     __builtin_amdgcn_s_setprio(0);
-    st = st == 2 ? 0 : st + 1;
+    st = NSTAGE == 3 ? (st == 2 ? 0 : st + 1) : (st ^ 1);
   }
   __syncthreads();  // all DMA retired (vmcnt(0) above); the ring is free for the epilogue
   gemm_epilogue<BM, BN, EPI, WGM, WGN>(p, acc, reinterpret_cast<float*>(lds_raw), bias_s, C,
                                        addend, M, N, ldc, m0, n0, 0);
+}
+
+
+// ---- 16x16x32 variant ("x6q") ---------------------------------------------------
+// Same operands and arithmetic as gemm_x6p_kernel, on v_mfma_f32_16x16x32_bf16:
+// at equal FLOPs the 16x16x32 stream holds a higher clock than the 32x32x16 one on
+// random data (tools/mfma_shape_bench.hip: 1.26x; MI355X_MICROARCH.md "DVFS
+// give-back" item 7).  Tile 256 x 128 x 32 (k), 8 waves as 4 x 2, each wave 64 x 64
+// as 4 x 4 blocks of 16 x 16; two 72-KB stages (one k-tile in flight measured as
+// fast as two for gemm_x6p).  A image [plane][k-tile of 32][Mp][32]; LDS: A rows of
+// 64 B with the 16-B slots XORed by (m >> 2) & 3, B rows of 256 B with the 16-B
+// units XORed by 2 (r & 3) + 8 ((r >> 3) & 1): both conflict-free for the
+// ds_read_b128 / ds_read_b64_tr_b16 fragments of the 16x16x32 shape.
+typedef float floatx4q __attribute__((ext_vector_type(4)));
+constexpr int X6Q_BM = 256, X6Q_BN = 128, X6Q_BK = 32;
+
+template <int EPI>
+__global__ __launch_bounds__(512) void gemm_x6q_kernel(GemmParams p) {
+  constexpr int BM = X6Q_BM, BN = X6Q_BN, BK = X6Q_BK;
+  constexpr int WGM = 4, WGN = 2;
+  constexpr int WM = BM / WGM, WN = BN / WGN;  // 64 x 64
+  constexpr int MT = WM / 16, NT = WN / 16;
+  constexpr int A_PLANE = BM * BK, B_PLANE = BK * BN;
+  constexpr int STAGE = 3 * (A_PLANE + B_PLANE);  // 72 KB
+  constexpr int NSTAGE = 2;
+  constexpr int RING_BYTES = NSTAGE * STAGE * 2;
+  constexpr int EPI_BYTES = 16 * WGM * (BN + 8) * 4;
+  constexpr int LDS_BYTES = RING_BYTES > EPI_BYTES ? RING_BYTES : EPI_BYTES;
+  constexpr bool HAS_BIAS = (EPI & EPI_BIAS) != 0;
+  static_assert(STAGE * 2 == 72 * 1024, "stage = 48 A + 24 B pieces of 1 KB");
+  __shared__ __attribute__((aligned(16))) char lds_raw[LDS_BYTES + (HAS_BIAS ? BM * 4 : 0)];
+  unsigned short* const ring = reinterpret_cast<unsigned short*>(lds_raw);
+  float* const bias_s = reinterpret_cast<float*>(lds_raw + LDS_BYTES);
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wm = wave / WGN, wn = wave % WGN;
+  const int lin = xcd_remap(blockIdx.x, gridDim.x);
+  const int tm = lin % p.tiles_m, tn = lin / p.tiles_m;
+  const int z = blockIdx.z;
+  const unsigned short* Ax = p.Ax + z * p.sAx;
+  const unsigned short* Bx = p.Bx + z * p.sB;
+  float* C = p.C + z * p.sC;
+  const float* bias = p.bias ? p.bias + z * p.sBias : nullptr;
+  const float* addend = p.addend ? p.addend + z * p.sD : nullptr;
+  const int M = p.M, N = p.N, K = p.K, ldb = p.ldb, ldc = p.ldc;
+  const int Mp = p.ldax;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int nk = (K + BK - 1) / BK;
+  if constexpr (HAS_BIAS) {
+    for (int r = tid; r < BM; r += 512) bias_s[r] = bias[min(m0 + r, M - 1)];
+  }
+  // LDS-DMA pieces c = wave + 8 q (q < 9): c < 48 -> A (plane c / 16, rows 16 (c % 16)),
+  // else B (plane (c - 48) / 8, k rows 4 ((c - 48) % 8))
+  const unsigned short* src[9];
+  int dst[9], brow[9];
+#pragma unroll
+  for (int q = 0; q < 9; ++q) {
+    const int c = wave + 8 * q;
+    if (c < 48) {
+      const int pl = c >> 4, rb = c & 15;
+      const int m = 16 * rb + (lane >> 2);
+      const int g = (lane & 3) ^ ((m >> 2) & 3);
+      src[q] = Ax + (int64_t)pl * p.sAxp + (int64_t)(m0 + m) * BK + 8 * g;
+      dst[q] = pl * A_PLANE + rb * 16 * BK;
+      brow[q] = -1;
+    } else {
+      const int cb = c - 48;
+      const int pl = cb >> 3, rq = cb & 7;
+      const int row = 4 * rq + (lane >> 4);
+      const int gu = (lane & 15) ^ (2 * (row & 3) + 8 * ((row >> 3) & 1));
+      src[q] = Bx + (int64_t)pl * p.sBxp + min(n0 + 8 * gu, ldb - 8);
+      dst[q] = 3 * A_PLANE + pl * B_PLANE + rq * 4 * BN;
+      brow[q] = row;
+    }
+  }
+  const int64_t a_kstride = (int64_t)Mp * BK;
+  const uint32_t ring_lds = lds_addr(ring);
+  auto issue = [&](int kt, int st) {
+    const uint32_t base = ring_lds + (uint32_t)(st * STAGE * 2);
+#pragma unroll
+    for (int q = 0; q < 9; ++q) {
+      const unsigned short* gp = brow[q] < 0
+                                     ? src[q] + kt * a_kstride
+                                     : src[q] + (int64_t)min(kt * BK + brow[q], K - 1) * ldb;
+      glds16(gp, base + (uint32_t)(dst[q] * 2));
+    }
+  };
+
+  floatx4q acc[MT][NT];
+#pragma unroll
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int j = 0; j < NT; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) acc[i][j][r] = 0.f;
+  int a_off[MT];
+#pragma unroll
+  for (int i = 0; i < MT; ++i) {
+    const int row = wm * WM + i * 16 + (lane & 15);
+    a_off[i] = row * BK + 8 * ((lane >> 4) ^ ((row >> 2) & 3));
+  }
+  const int li = lane & 15, G = lane >> 4;
+  const int r1 = 8 * G + (li >> 2);  // k row of the first tr read (second: + 4)
+  const int fr = 2 * (r1 & 3) + 8 * ((r1 >> 3) & 1);
+  int b_off[NT];
+#pragma unroll
+  for (int j = 0; j < NT; ++j) {
+    const int c = wn * WN + j * 16 + 4 * (li & 3);
+    b_off[j] = 3 * A_PLANE + r1 * BN + (((c >> 3) ^ fr) << 3) + (c & 7);
+  }
+  auto mfma_tile = [&](int st) {
+    typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+    const unsigned short* base = ring + st * STAGE;
+    bf16x8 a[MT][3];
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+      for (int pl = 0; pl < 3; ++pl)
+        a[i][pl] = *reinterpret_cast<const bf16x8*>(base + pl * A_PLANE + a_off[i]);
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+      bf16x8 b[3];
+#pragma unroll
+      for (int pl = 0; pl < 3; ++pl) {
+        const unsigned short* qq = base + pl * B_PLANE + b_off[j];
+        const s16x4 lo4 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (lds_s16x4*)((__attribute__((address_space(3))) unsigned short*)qq));
+        const s16x4 hi4 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (lds_s16x4*)((__attribute__((address_space(3))) unsigned short*)(qq + 4 * BN)));
+        const s16x8 v = {lo4[0], lo4[1], lo4[2], lo4[3], hi4[0], hi4[1], hi4[2], hi4[3]};
+        b[pl] = __builtin_bit_cast(bf16x8, v);
+      }
+#pragma unroll
+      for (int i = 0; i < MT; ++i) {
+        floatx4q c = acc[i][j];
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][2], b[0], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][1], b[1], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][0], b[2], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][1], b[0], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][0], b[1], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][0], b[0], c, 0, 0, 0);
+        acc[i][j] = c;
+      }
+    }
+  };
+
+  if constexpr (HAS_BIAS) __syncthreads();
+  issue(0, 0);
+  int st = 0;
+  for (int kt = 0; kt < nk; ++kt) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // my DMA of k-tile kt landed
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // everyone's; the other stage is free
+    if (kt + 1 < nk) issue(kt + 1, st ^ 1);
+    __builtin_amdgcn_s_setprio(1);
+    mfma_tile(st);
+    __builtin_amdgcn_s_setprio(0);
+    st ^= 1;
+  }
+  __syncthreads();
+  gemm_epilogue<BM, BN, EPI, WGM, WGN, MT, NT, 16, floatx4q>(
+      p, acc, reinterpret_cast<float*>(lds_raw), bias_s, C, addend, M, N, ldc, m0, n0, 0);
 }
 
 // ---- descriptor mode: the per-(m, parity) Legendre GEMMs --------------------------
@@ -476,7 +645,8 @@ int gemm_x6d(const unsigned short* Ax, int64_t sAxp, const unsigned short* Bx, i
 }
 
 size_t gemm_x6p_workspace(int M, int K, int batch_a) {
-  const int64_t Mp = round_up(M, X6P_BM), Kp = round_up(K, X6P_BK);
+  // k padded to 32: covers the 16-deep (x6p) and 32-deep (x6q) A images
+  const int64_t Mp = round_up(M, X6P_BM), Kp = round_up(K, 32);
   return (size_t)round_up(3 * Mp * Kp * 2 * (int64_t)batch_a, 256);
 }
 
@@ -512,9 +682,29 @@ int launch_split_planes(const float* x, unsigned short* xp, int rows, int cols, 
   return launch_check("split_planes");
 }
 
+// MFMA shape of the plane GEMM: 32x32x16 (x6p) unless MSFNO_X6P_MFMA=16 (x6q,
+// measured 2 % slower on the fc2 shape); ring depth MSFNO_X6P_STAGES=2|3 (x6p; 2
+// k-tiles measured 1-3 % faster than 3 on fc1/fc2)
+static bool use_x6q() {
+  static const bool on = [] {
+    const char* e = getenv("MSFNO_X6P_MFMA");
+    return e && std::string(e) == "16";
+  }();
+  return on;
+}
+
 template <int EPI>
-static void launch_x6p_e(const GemmParams& p, dim3 grid, hipStream_t s) {
-  hipLaunchKernelGGL((gemm_x6p_kernel<EPI>), grid, dim3(512), 0, s, p);
+static void launch_x6p_e(const GemmParams& p, dim3 grid, hipStream_t s, bool q) {
+  static const int stages = [] {
+    const char* e = getenv("MSFNO_X6P_STAGES");
+    return (e && e[0] == '3') ? 3 : 2;
+  }();
+  if (q)
+    hipLaunchKernelGGL((gemm_x6q_kernel<EPI>), grid, dim3(512), 0, s, p);
+  else if (stages == 2)
+    hipLaunchKernelGGL((gemm_x6p_kernel<EPI, 2>), grid, dim3(512), 0, s, p);
+  else
+    hipLaunchKernelGGL((gemm_x6p_kernel<EPI, 3>), grid, dim3(512), 0, s, p);
 }
 
 int gemm_x6p(const float* A, float* C, int M, int N, int K, int lda, int ldb, int ldc,
@@ -522,8 +712,12 @@ int gemm_x6p(const float* A, float* C, int M, int N, int K, int lda, int ldb, in
              size_t ws_bytes, hipStream_t s) {
   if (M <= 0 || N <= 0 || batch <= 0) return MSFNO_OK;
   const int abatch = sA == 0 ? 1 : batch;
-  MSFNO_REQUIRE(epi.a_planes || (ws && ws_bytes >= gemm_x6p_workspace(M, K, abatch)),
-                MSFNO_EINVAL, "gemm_x6p: workspace too small");
+  // the pre-split images of launch_spec_weights_x6p are 16-deep: x6p kernel for them
+  const bool q = use_x6q() && !epi.a_planes;
+  const int TKd = q ? X6Q_BK : X6P_BK;
+  const size_t need = (size_t)round_up(3 * round_up(M, X6P_BM) * round_up(K, TKd) * 2 * (int64_t)abatch, 256);
+  MSFNO_REQUIRE(epi.a_planes || (ws && ws_bytes >= need), MSFNO_EINVAL,
+                "gemm_x6p: workspace too small");
   MSFNO_REQUIRE(!epi.a_planes || sA == 0, MSFNO_EINVAL, "gemm_x6p: pre-split A is not batched");
   MSFNO_REQUIRE(epi.b_planes, MSFNO_EINVAL, "gemm_x6p: B must be in the plane format");
   MSFNO_REQUIRE(batch <= 65535 && K > 0, MSFNO_EINVAL, "gemm_x6p: bad batch / K");
@@ -532,15 +726,19 @@ int gemm_x6p(const float* A, float* C, int M, int N, int K, int lda, int ldb, in
                 MSFNO_EINVAL, "gemm_x6p: B planes need ld, strides % 8 == 0 and 16-B alignment");
   MSFNO_REQUIRE(epi.act != 2 && !epi.rowscale, MSFNO_EUNSUPPORTED,
                 "gemm_x6p: unsupported epilogue");
-  const int Mp = (int)round_up(M, X6P_BM), KT = (int)cdiv(K, X6P_BK);
+  const int Mp = (int)round_up(M, X6P_BM), KT = (int)cdiv(K, TKd);
   unsigned short* Ax = static_cast<unsigned short*>(ws);
   if (epi.a_planes) {
     Ax = const_cast<unsigned short*>(epi.a_planes);  // already in the A image layout
   } else {
-    const int64_t pairs = (int64_t)Mp * KT * 8;
+    const int64_t pairs = (int64_t)Mp * KT * TKd / 2;
     const int blocks = (int)std::min<int64_t>(cdiv(pairs, 256), 1024);
-    hipLaunchKernelGGL(split_a_tiles_kernel, dim3(blocks, abatch), dim3(256), 0, s, A, Ax, M, K,
-                       lda, sA, Mp, KT);
+    if (q)
+      hipLaunchKernelGGL(split_a_tiles_kernel<X6Q_BK>, dim3(blocks, abatch), dim3(256), 0, s, A,
+                         Ax, M, K, lda, sA, Mp, KT);
+    else
+      hipLaunchKernelGGL(split_a_tiles_kernel<X6P_BK>, dim3(blocks, abatch), dim3(256), 0, s, A,
+                         Ax, M, K, lda, sA, Mp, KT);
     MSFNO_TRY(launch_check("split_a_tiles"));
   }
   GemmParams p{};
@@ -549,7 +747,7 @@ int gemm_x6p(const float* A, float* C, int M, int N, int K, int lda, int ldb, in
   p.sB = sB; p.sC = sC;
   p.bias = epi.bias; p.addend = epi.addend; p.sBias = epi.sBias; p.sD = epi.sD;
   p.ldd = epi.ldd; p.act = epi.act; p.relu_period = epi.relu_period; p.relu_rows = epi.relu_rows;
-  p.Ax = Ax; p.sAxp = (int64_t)Mp * KT * 16; p.sAx = sA == 0 ? 0 : 3 * p.sAxp; p.ldax = Mp;
+  p.Ax = Ax; p.sAxp = (int64_t)Mp * KT * TKd; p.sAx = sA == 0 ? 0 : 3 * p.sAxp; p.ldax = Mp;
   p.Bx = epi.b_planes; p.sBxp = epi.b_plane_stride;
   p.Cx = epi.c_planes; p.sCxp = epi.c_plane_stride;
   p.vecC = (ldc % 4 == 0) && (sC % 4 == 0) && ((reinterpret_cast<uintptr_t>(C) & 15) == 0) &&
@@ -560,19 +758,19 @@ int gemm_x6p(const float* A, float* C, int M, int N, int K, int lda, int ldb, in
                       (reinterpret_cast<uintptr_t>(p.Cx) & 7) == 0,
                   MSFNO_EINVAL, "gemm_x6p: C planes need ld, strides % 4 == 0 and 8-B alignment");
   p.tiles_m = Mp / X6P_BM;
-  p.tiles_n = (int)cdiv(N, X6P_BN);
+  p.tiles_n = (int)cdiv(N, q ? X6Q_BN : X6P_BN);
   const dim3 grid(p.tiles_m * p.tiles_n, 1, batch);
   const int code = (p.bias ? EPI_BIAS : 0) | (p.addend ? EPI_ADD : 0) | (p.act == 1 ? EPI_GELU : 0) |
                    (p.relu_period ? EPI_RELU : 0) | (p.Cx ? EPI_PLANES : 0);
   switch (code) {
-    case 0: launch_x6p_e<0>(p, grid, s); break;
-    case EPI_RELU: launch_x6p_e<EPI_RELU>(p, grid, s); break;
-    case EPI_RELU | EPI_PLANES: launch_x6p_e<EPI_RELU | EPI_PLANES>(p, grid, s); break;
-    case EPI_PLANES: launch_x6p_e<EPI_PLANES>(p, grid, s); break;
-    case EPI_BIAS: launch_x6p_e<EPI_BIAS>(p, grid, s); break;
-    case EPI_BIAS | EPI_ADD: launch_x6p_e<EPI_BIAS | EPI_ADD>(p, grid, s); break;
+    case 0: launch_x6p_e<0>(p, grid, s, q); break;
+    case EPI_RELU: launch_x6p_e<EPI_RELU>(p, grid, s, q); break;
+    case EPI_RELU | EPI_PLANES: launch_x6p_e<EPI_RELU | EPI_PLANES>(p, grid, s, q); break;
+    case EPI_PLANES: launch_x6p_e<EPI_PLANES>(p, grid, s, q); break;
+    case EPI_BIAS: launch_x6p_e<EPI_BIAS>(p, grid, s, q); break;
+    case EPI_BIAS | EPI_ADD: launch_x6p_e<EPI_BIAS | EPI_ADD>(p, grid, s, q); break;
     case EPI_BIAS | EPI_GELU | EPI_PLANES:
-      launch_x6p_e<EPI_BIAS | EPI_GELU | EPI_PLANES>(p, grid, s); break;
+      launch_x6p_e<EPI_BIAS | EPI_GELU | EPI_PLANES>(p, grid, s, q); break;
     default:
       set_error("gemm_x6p: unsupported epilogue combination");
       return MSFNO_EUNSUPPORTED;
