@@ -4,6 +4,7 @@
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
 
 #include "block.h"
 
@@ -772,8 +773,12 @@ int run_filter(const msfno_block_desc* d, msfno_sht_plan_s* f, msfno_sht_plan_s*
 }
 
 // x -> (FFT, norm0 folded) -> Legendre -> filter -> inverse Legendre -> Yn
+// xplanes: the forward FFT also writes x as bf16x3 planes; after_fft runs once the
+// forward FFT is enqueued (the block forks its inner-skip GEMM there)
 int run_spectral(const msfno_block_desc* d, msfno_sht_plan_s* f, msfno_sht_plan_s* g,
-                        const BlockBufs& b, const float* x, int B, bool norm0, hipStream_t s) {
+                 const BlockBufs& b, const float* x, int B, bool norm0, hipStream_t s,
+                 const C2RPlanes* xplanes = nullptr,
+                 const std::function<int()>& after_fft = std::function<int()>()) {
   const int64_t C = d->C, BC = (int64_t)B * C, R = 2 * BC;
   // x6 Legendre: symmetric plans, slab / coefficient planes carved, row path
   const bool lx6 = b.Xtp && b.Sp && f->sym && g->sym && !use_fft_tile(f) &&
@@ -795,7 +800,8 @@ int run_spectral(const msfno_block_desc* d, msfno_sht_plan_s* f, msfno_sht_plan_
     MSFNO_TRY(legendre_fwd(f, b.Xt, b.Sa, (int)R, s, norm0 ? b.sc0 : nullptr, (int)C));
   } else {
     MSFNO_TRY(launch_fft_r2c_rows(f->fft, x, b.Xn, norm0 ? b.rs0 : nullptr, BC * f->nlat, f->mmax,
-                                  scale, s));
+                                  scale, s, xplanes));
+    if (after_fft) MSFNO_TRY(after_fft());
     if (norm0) {
       prof(ST_NORM0, s);
       MSFNO_TRY(launch_chan_affine(b.rs0, f->nlat, f->nlon, f->nlon, B, (int)C, d->norm0_w,
@@ -953,6 +959,17 @@ int run_mlp(const msfno_block_desc* d, const float* W1f, const float* b1f, const
   return gemm_dense(ROLE_FC2, TILE_256x128, d->fc2_w, h, out, (int)C, (int)P, (int)Hd, (int)Hd,
                     (int)ldh, (int)P, 0, (planes ? 3 : 1) * Hd * ldh, C * P, B, e2, dw.fc2,
                     dw.fc2_b, s);
+}
+
+// the inner-skip GEMM reads x as bf16x3 planes written by the forward FFT (into the
+// x1 plane buffer); MSFNO_SKIP_PLANES=0 keeps the in-kernel split (gemm_x6) for A/B
+bool skip_planes(const msfno_block_desc* d, const msfno_sht_plan_s* f, const BlockBufs& b) {
+  static const bool on = [] {
+    const char* e = getenv("MSFNO_SKIP_PLANES");
+    return !(e && e[0] == '0');
+  }();
+  return on && b.x1p && b.dw.skip && d->inner_skip == MSFNO_SKIP_LINEAR && !use_fft_tile(f) &&
+         fft_r2c_planes_supported(f->fft, f->mmax);
 }
 
 // x1 (the MLP input) written by the inverse FFT as bf16x3 planes: x6 engine, an
@@ -1180,12 +1197,16 @@ int msfno_block_forward(const msfno_block_desc* d, msfno_sht_plan_t f, msfno_sht
   const int64_t P = (int64_t)g->nlat * g->nlon;
   const int act = d->filter_type == MSFNO_FILTER_LINEAR ? 1 : 0;  // GELU after skip (linear only)
 
-  // ---- inner skip 1x1 conv first (depends only on x): x1 = Ws·x + bs ----------
+  // ---- inner skip 1x1 conv (depends only on x): x1 = Ws·x + bs, on the side stream ----
+  // With x6 planes the forward FFT also writes x as bf16x3 planes into the x1 plane
+  // buffer (dead until the inverse FFT, which runs after the skip GEMM): the skip
+  // GEMM is forked after the forward FFT and stages B by LDS-DMA (gemm_x6p) instead
+  // of splitting fp32 x in-kernel.
   float* x1 = b.x1;
   SideCtx* side = nullptr;
-  if (d->inner_skip == MSFNO_SKIP_LINEAR) {
-    MSFNO_REQUIRE(d->skip_w, MSFNO_EINVAL, "missing inner_skip weight");
-    MSFNO_TRY(side_ctx(&side));
+  const bool xpl = skip_planes(d, f, b);
+  const C2RPlanes xp{b.x1p, (int)C, f->nlat};
+  auto launch_skip = [&]() -> int {
     hipStream_t ss = s;
     if (side) {  // fork
       MSFNO_CHECK_HIP(hipEventRecord(side->fork, s));
@@ -1195,14 +1216,31 @@ int msfno_block_forward(const msfno_block_desc* d, msfno_sht_plan_t f, msfno_sht
     prof(ST_SKIP, ss);
     GemmEpi e;
     e.bias = d->skip_b;
-    MSFNO_TRY(gemm_dense(ROLE_SKIP, TILE_128x256, d->skip_w, x, x1, (int)C, (int)P, (int)C,
-                         (int)C, (int)P, (int)P, 0, C * P, C * P, B, e, b.dw.skip, b.dw.skip_b, ss));
+    if (xpl) {
+      e.b_planes = b.x1p;
+      e.b_plane_stride = C * P;
+      MSFNO_TRY(gemm_x6p(d->skip_w, x1, (int)C, (int)P, (int)C, (int)C, (int)P, (int)P, 0,
+                         3 * C * P, C * P, B, e, b.dw.skip, b.dw.skip_b, ss));
+    } else {
+      MSFNO_TRY(gemm_dense(ROLE_SKIP, TILE_128x256, d->skip_w, x, x1, (int)C, (int)P, (int)C,
+                           (int)C, (int)P, (int)P, 0, C * P, C * P, B, e, b.dw.skip, b.dw.skip_b,
+                           ss));
+    }
     if (side) {
       prof(ST_END, ss);
       MSFNO_CHECK_HIP(hipEventRecord(side->join, ss));
     }
+    return MSFNO_OK;
+  };
+  if (d->inner_skip == MSFNO_SKIP_LINEAR) {
+    MSFNO_REQUIRE(d->skip_w, MSFNO_EINVAL, "missing inner_skip weight");
+    MSFNO_TRY(side_ctx(&side));
+    if (!xpl) MSFNO_TRY(launch_skip());
   }
-  MSFNO_TRY(run_spectral(d, f, g, b, x, B, true, s));
+  if (xpl)
+    MSFNO_TRY(run_spectral(d, f, g, b, x, B, true, s, &xp, launch_skip));
+  else
+    MSFNO_TRY(run_spectral(d, f, g, b, x, B, true, s));
   if (side) MSFNO_CHECK_HIP(hipStreamWaitEvent(s, side->join, 0));  // join
   // ---- filter output + skip (+ GELU for the linear filter) -> x1, norm1 partials ---
   const float* skip_src = d->inner_skip == MSFNO_SKIP_LINEAR ? x1

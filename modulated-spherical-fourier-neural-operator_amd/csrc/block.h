@@ -84,6 +84,7 @@ int run_mlp(const msfno_block_desc* d, const float* W1f, const float* b1f, const
 bool mlp_h_planes(bool have_ws);
 int64_t mlp_h_floats(int B, int64_t Hd, int64_t P);
 bool x1_planes(const msfno_block_desc* d, const msfno_sht_plan_s* g);
+bool skip_planes(const msfno_block_desc* d, const msfno_sht_plan_s* f, const BlockBufs& b);
 bool leg_x6_enabled();
 // plan construction (mask: optional m-set, see SpecLayout::build)
 int plan_create(int nlat, int nlon, int lmax, int mmax, int inverse,

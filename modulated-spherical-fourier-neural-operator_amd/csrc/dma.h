@@ -35,7 +35,12 @@ __device__ __forceinline__ void glds16(const void* gsrc, uint32_t lds) {
 // s_waitcnt vmcnt(n) for a run-time n, rounded down to a supported immediate
 // (waiting for more than needed is safe)
 __device__ __forceinline__ void wait_vmcnt(int n) {
-  if (n >= 12) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+  if (n >= 48) asm volatile("s_waitcnt vmcnt(48)" ::: "memory");
+  else if (n >= 40) asm volatile("s_waitcnt vmcnt(40)" ::: "memory");
+  else if (n >= 32) asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
+  else if (n >= 24) asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
+  else if (n >= 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+  else if (n >= 12) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
   else if (n >= 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
   else if (n >= 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
   else if (n >= 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");

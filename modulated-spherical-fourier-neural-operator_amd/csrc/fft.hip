@@ -588,12 +588,12 @@ __global__ __launch_bounds__(256) void fft_c2r_rows_kernel(const float2* __restr
 // place in the LDS row the DMA filled; both twiddle tables live in LDS (a
 // global twiddle read would make hipcc drain the copies in flight).
 // ---------------------------------------------------------------------------
-template <class CL, int WV>
+template <class CL, int WV, bool PL>
 __global__ __launch_bounds__(64 * WV) void fft_r2c_dma_kernel(const float* __restrict__ x,
                                                               float2* __restrict__ out,
                                                               float2* __restrict__ rowstats,
                                                               int64_t rows, int mmax, float scale,
-                                                              FFTArgs f) {
+                                                              FFTArgs f, C2RPlanes pp) {
   constexpr int H = CL::H, N = 2 * H, RB = N * 4;
   constexpr int NCH = (RB + 1023) / 1024;  // DMA wave-instructions per row
   constexpr int SLOT = NCH * 1024;
@@ -617,7 +617,8 @@ __global__ __launch_bounds__(64 * WV) void fft_r2c_dma_kernel(const float* __res
   };
   if (row0 < rows) issue(row0, 0);
   if (row0 + stride < rows) issue(row0 + stride, 1);
-  const int nst = (mmax + 63) / 64 + (rowstats ? 1 : 0);  // vector stores per row
+  constexpr int NSP = PL ? 3 * ((N / 4 + 63) / 64) : 0;  // plane stores per row
+  const int nst = (mmax + 63) / 64 + (rowstats ? 1 : 0) + NSP;  // vector stores per row
   int sl = 0;
   int i = 0;
   for (int64_t row = row0; row < rows; row += stride, ++i) {
@@ -627,6 +628,26 @@ __global__ __launch_bounds__(64 * WV) void fft_r2c_dma_kernel(const float* __res
     wait_vmcnt((i >= 2 ? nst : 0) + (next ? NCH : 0) + (i >= 1 ? nst : 0));
     if (row + 2 * stride < rows) issue(row + 2 * stride, sl == 0 ? 2 : sl - 1);
     float2* buf = reinterpret_cast<float2*>(slots + sl * SLOT);
+    if constexpr (PL) {  // the raw row as bf16x3 planes, (b, c, lat) of row = (b*C + c)*nlat + lat
+      const int64_t bc = row / pp.nlat, lat = row - bc * pp.nlat;
+      const int64_t b = bc / pp.C, c = bc - b * pp.C;
+      const int64_t P = (int64_t)pp.nlat * N, ps = (int64_t)pp.C * P;
+      unsigned short* xq = pp.xp + b * 3 * ps + c * P + lat * N;
+      const float4* b4 = reinterpret_cast<const float4*>(buf);
+#pragma unroll
+      for (int j = 0; j < NSP / 3; ++j) {
+        const int n = lane + 64 * j;
+        if (n < N / 4) {
+          const float4 v = b4[n];
+          uint32_t a0, a1, a2, c0, c1, c2;
+          split2(v.x, v.y, a0, a1, a2);
+          split2(v.z, v.w, c0, c1, c2);
+          *reinterpret_cast<uint2*>(xq + 4 * n) = make_uint2(a0, c0);
+          *reinterpret_cast<uint2*>(xq + ps + 4 * n) = make_uint2(a1, c1);
+          *reinterpret_cast<uint2*>(xq + 2 * ps + 4 * n) = make_uint2(a2, c2);
+        }
+      }
+    }
     if (rowstats) {
       float s = 0.f;
       for (int n = lane; n < H; n += 64) s += buf[n].x + buf[n].y;
@@ -1070,20 +1091,27 @@ static int64_t dma_grid() {
 
 template <class CL>
 static int launch_r2c(const FFTArgs& a, const float* x, float2* out, float2* rowstats,
-                      int64_t rows, int mmax, float scale, hipStream_t s) {
+                      int64_t rows, int mmax, float scale, hipStream_t s,
+                      const C2RPlanes* planes) {
   if constexpr (CL::H > 0) {
     if (use_fft_dma() && (2 * CL::H) % 8 == 0 && mmax <= CL::H + 1) {
       constexpr int WV = 8;  // one 8-wave workgroup per CU, 3 row slots per wave
       const size_t slot = (size_t)((2 * CL::H * 4 + 1023) / 1024) * 1024;
       const size_t lds = (size_t)(2 * CL::H + 2) * sizeof(float2) + WV * 3 * slot;
       MSFNO_REQUIRE(lds <= 160 * 1024, MSFNO_EUNSUPPORTED, "nlon too large for the LDS FFT");
-      MSFNO_TRY(set_lds_limit(reinterpret_cast<const void*>(&fft_r2c_dma_kernel<CL, WV>), lds));
       const int64_t grid = std::min<int64_t>(cdiv(rows, WV), dma_grid());
-      hipLaunchKernelGGL((fft_r2c_dma_kernel<CL, WV>), dim3((unsigned)grid), dim3(64 * WV), lds,
-                         s, x, out, rowstats, rows, mmax, scale, a);
-      return launch_check("fft_r2c_dma");
+      auto go = [&](auto kern) -> int {
+        MSFNO_TRY(set_lds_limit(reinterpret_cast<const void*>(kern), lds));
+        C2RPlanes pp{};
+        if (planes) pp = *planes;
+        hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(64 * WV), lds, s, x, out, rowstats,
+                           rows, mmax, scale, a, pp);
+        return launch_check("fft_r2c_dma");
+      };
+      return planes ? go(fft_r2c_dma_kernel<CL, WV, true>) : go(fft_r2c_dma_kernel<CL, WV, false>);
     }
   }
+  MSFNO_REQUIRE(!planes, MSFNO_EUNSUPPORTED, "r2c plane output needs the LDS-DMA row FFT");
   const size_t lds = (size_t)(kWaves * CL::kBufs + 1) * a.H * sizeof(float2);
   MSFNO_REQUIRE(lds <= 64 * 1024, MSFNO_EUNSUPPORTED, "nlon too large for the LDS FFT");
   hipLaunchKernelGGL((fft_r2c_rows_kernel<CL>), dim3((unsigned)fft_grid(rows)), dim3(256), lds, s,
@@ -1136,15 +1164,16 @@ static int launch_c2r(const FFTArgs& a, const float2* in, float* x, const float*
 }
 
 int launch_fft_r2c_rows(const FFTPlan& f, const float* x, float2* out, float2* rowstats,
-                        int64_t rows, int mmax, float scale, hipStream_t s) {
+                        int64_t rows, int mmax, float scale, hipStream_t s,
+                        const C2RPlanes* planes) {
   if (rows <= 0) return MSFNO_OK;
   const FFTArgs a = make_args(f);
   switch (f.codelet) {
 #define X(id, CL) \
-  case id: return launch_r2c<CL>(a, x, out, rowstats, rows, mmax, scale, s);
+  case id: return launch_r2c<CL>(a, x, out, rowstats, rows, mmax, scale, s, planes);
     MSFNO_FFT_CODELETS(X)
 #undef X
-    default: return launch_r2c<GenericFFT>(a, x, out, rowstats, rows, mmax, scale, s);
+    default: return launch_r2c<GenericFFT>(a, x, out, rowstats, rows, mmax, scale, s, planes);
   }
 }
 
@@ -1160,6 +1189,10 @@ int launch_fft_c2r_rows(const FFTPlan& f, const float2* in, float* x, const floa
 #undef X
     default: return launch_c2r<GenericFFT>(a, in, x, addsrc, rowstats, rows, mmax, act, s, planes);
   }
+}
+
+bool fft_r2c_planes_supported(const FFTPlan& f, int mmax) {
+  return use_fft_dma() && f.codelet != 0 && f.packed && f.N % 8 == 0 && mmax <= f.H + 1;
 }
 
 bool fft_c2r_planes_supported(const FFTPlan& f, int mmax) {

@@ -7,22 +7,26 @@ namespace msfno {
 // ---- fft.hip ----------------------------------------------------------------
 // x (rows, N) fp32 -> out (rows, mmax) complex, scaled by `scale`; optional
 // per-row (mean, M2) over the N inputs.
+// planes (optional, LDS-DMA path only): the input rows are also written as bf16x3
+// planes in the C2RPlanes layout below (the inner-skip GEMM's B operand)
 int launch_fft_r2c_rows(const FFTPlan& f, const float* x, float2* out, float2* rowstats,
-                        int64_t rows, int mmax, float scale, hipStream_t s);
+                        int64_t rows, int mmax, float scale, hipStream_t s,
+                        const struct C2RPlanes* planes = nullptr);
 // in (rows, mmax) complex (Hermitian half spectrum, zero beyond mmax) -> x (rows, N);
 // act: 0 none, 1 GELU; optional per-row (mean, M2) of the outputs.
 // addsrc (may alias x): x = act(addsrc + irfft(in))  (the block's skip branch)
 int launch_fft_c2r_rows(const FFTPlan& f, const float2* in, float* x, const float* addsrc,
                         float2* rowstats, int64_t rows, int mmax, int act, hipStream_t s,
                         const struct C2RPlanes* planes = nullptr);
-// optional bf16x3 plane output of launch_fft_c2r_rows (the next GEMM's B operand,
-// gemm_x6p): rows are (b*C + c)*nlat + lat, written to
+// optional bf16x3 plane output of launch_fft_c2r_rows / _r2c_rows (the next GEMM's B
+// operand, gemm_x6p): rows are (b*C + c)*nlat + lat, written to
 // xp[b][plane][c][lat*N + n] with plane stride C*nlat*N; x (fp32) is not written
 struct C2RPlanes {
   unsigned short* xp;
   int C, nlat;
 };
 bool fft_c2r_planes_supported(const FFTPlan& f, int mmax);
+bool fft_r2c_planes_supported(const FFTPlan& f, int mmax);
 
 // fused FFT + transpose (block path); only for plans with a compiled codelet
 bool fft_tile_supported(const FFTPlan& f);
