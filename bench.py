@@ -151,7 +151,10 @@ def stage_work(name, B, C, nlat, nlon, lmax, mmax, hid, shid, rows=None, mset=No
         "legendre_fwd": ("mfma", 2 * (2 * BC) * nlat * T),
         "legendre_inv": ("mfma", 2 * (2 * BC) * nlat * T),
         # HBM-bound stages: compulsory bytes moved
-        "fft_fwd": ("hbm", BC * rows * (nlon * 4 + mmax * 8)),
+        # rfft: x read + spectrum written (+ x as bf16x3 planes for the inner-skip GEMM on
+        # the x6 engine, whole-field block only)
+        "fft_fwd": ("hbm", BC * rows * (nlon * 4 + mmax * 8 +
+                                        (nlon * 6 if x6_engine()[0] and mset is None else 0))),
         # irfft: Yn read + skip-branch row read + x1 written (bf16x3 planes, 6 B per
         # value, on the x6 engine with an MLP)
         "fft_inv": ("hbm", BC * rows * (mmax * 8 + nlon * 4 + nlon * (6 if x6_engine()[0] else 4))),

@@ -588,7 +588,7 @@ __global__ __launch_bounds__(256) void fft_c2r_rows_kernel(const float2* __restr
 // place in the LDS row the DMA filled; both twiddle tables live in LDS (a
 // global twiddle read would make hipcc drain the copies in flight).
 // ---------------------------------------------------------------------------
-template <class CL, int WV, bool PL>
+template <class CL, int WV, bool PL, int NS = 3>
 __global__ __launch_bounds__(64 * WV) void fft_r2c_dma_kernel(const float* __restrict__ x,
                                                               float2* __restrict__ out,
                                                               float2* __restrict__ rowstats,
@@ -597,7 +597,7 @@ __global__ __launch_bounds__(64 * WV) void fft_r2c_dma_kernel(const float* __res
   constexpr int H = CL::H, N = 2 * H, RB = N * 4;
   constexpr int NCH = (RB + 1023) / 1024;  // DMA wave-instructions per row
   constexpr int SLOT = NCH * 1024;
-  constexpr int NS = 3;                    // row slots per wave: 2 rows in flight
+  // NS row slots per wave: NS - 1 rows in flight while one is transformed
   extern __shared__ float2 smem[];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   float2* tw = smem;
@@ -625,8 +625,12 @@ __global__ __launch_bounds__(64 * WV) void fft_r2c_dma_kernel(const float* __res
     // this row's copy has landed: count what this wave issued after it (the next
     // row's copy, if any, and the stores of the previous one or two rows)
     const bool next = row + stride < rows;
-    wait_vmcnt((i >= 2 ? nst : 0) + (next ? NCH : 0) + (i >= 1 ? nst : 0));
-    if (row + 2 * stride < rows) issue(row + 2 * stride, sl == 0 ? 2 : sl - 1);
+    if constexpr (NS == 3) {
+      wait_vmcnt((i >= 2 ? nst : 0) + (next ? NCH : 0) + (i >= 1 ? nst : 0));
+      if (row + 2 * stride < rows) issue(row + 2 * stride, sl == 0 ? 2 : sl - 1);
+    } else {  // the next row was issued after the previous row's stores
+      wait_vmcnt((i >= 1 ? nst : 0) + (next ? NCH : 0));
+    }
     float2* buf = reinterpret_cast<float2*>(slots + sl * SLOT);
     if constexpr (PL) {  // the raw row as bf16x3 planes, (b, c, lat) of row = (b*C + c)*nlat + lat
       const int64_t bc = row / pp.nlat, lat = row - bc * pp.nlat;
@@ -672,7 +676,14 @@ __global__ __launch_bounds__(64 * WV) void fft_r2c_dma_kernel(const float* __res
       o[k] = make_float2(scale * X.x, scale * X.y);
     }
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-    sl = sl == 2 ? 0 : sl + 1;
+    if constexpr (NS == 3) {
+      sl = sl == 2 ? 0 : sl + 1;
+    } else {
+      // every read of this slot has returned: refill it with the row after next
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      if (row + 2 * stride < rows) issue(row + 2 * stride, sl);
+      sl ^= 1;
+    }
   }
 }
 
@@ -1095,12 +1106,22 @@ static int launch_r2c(const FFTArgs& a, const float* x, float2* out, float2* row
                       const C2RPlanes* planes) {
   if constexpr (CL::H > 0) {
     if (use_fft_dma() && (2 * CL::H) % 8 == 0 && mmax <= CL::H + 1) {
-      constexpr int WV = 8;  // one 8-wave workgroup per CU, 3 row slots per wave
+      // waves x row slots per workgroup, one workgroup per CU: 12 x 2 (one row in
+      // flight, 12 waves) measured 4 % faster than 8 x 3 (two rows in flight, 8
+      // waves) at 721 x 1440 and 5 x 2 (two workgroups) slower; the row FFT is
+      // latency bound, waves per CU beat rows in flight.  MSFNO_R2C_CFG=8x3|5x2 (A/B)
+      static const int cfg = [] {
+        const char* e = getenv("MSFNO_R2C_CFG");
+        if (e && std::string(e) == "8x3") return 0;
+        if (e && std::string(e) == "5x2") return 2;
+        return 1;
+      }();
       const size_t slot = (size_t)((2 * CL::H * 4 + 1023) / 1024) * 1024;
-      const size_t lds = (size_t)(2 * CL::H + 2) * sizeof(float2) + WV * 3 * slot;
-      MSFNO_REQUIRE(lds <= 160 * 1024, MSFNO_EUNSUPPORTED, "nlon too large for the LDS FFT");
-      const int64_t grid = std::min<int64_t>(cdiv(rows, WV), dma_grid());
-      auto go = [&](auto kern) -> int {
+      auto go = [&](auto kern, int WV, int NS) -> int {
+        const size_t lds = (size_t)(2 * CL::H + 2) * sizeof(float2) + WV * NS * slot;
+        MSFNO_REQUIRE(lds <= 160 * 1024, MSFNO_EUNSUPPORTED, "nlon too large for the LDS FFT");
+        const int64_t grid =
+            std::min<int64_t>(cdiv(rows, WV), dma_grid() * (WV == 5 ? 2 : 1));  // WGs per CU
         MSFNO_TRY(set_lds_limit(reinterpret_cast<const void*>(kern), lds));
         C2RPlanes pp{};
         if (planes) pp = *planes;
@@ -1108,7 +1129,14 @@ static int launch_r2c(const FFTArgs& a, const float* x, float2* out, float2* row
                            rows, mmax, scale, a, pp);
         return launch_check("fft_r2c_dma");
       };
-      return planes ? go(fft_r2c_dma_kernel<CL, WV, true>) : go(fft_r2c_dma_kernel<CL, WV, false>);
+      if (cfg == 1)
+        return planes ? go(fft_r2c_dma_kernel<CL, 12, true, 2>, 12, 2)
+                      : go(fft_r2c_dma_kernel<CL, 12, false, 2>, 12, 2);
+      if (cfg == 2)
+        return planes ? go(fft_r2c_dma_kernel<CL, 5, true, 2>, 5, 2)
+                      : go(fft_r2c_dma_kernel<CL, 5, false, 2>, 5, 2);
+      return planes ? go(fft_r2c_dma_kernel<CL, 8, true>, 8, 3)
+                    : go(fft_r2c_dma_kernel<CL, 8, false>, 8, 3);
     }
   }
   MSFNO_REQUIRE(!planes, MSFNO_EUNSUPPORTED, "r2c plane output needs the LDS-DMA row FFT");
