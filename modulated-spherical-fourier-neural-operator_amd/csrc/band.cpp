@@ -58,6 +58,8 @@ struct BandBufs {
   BlockBufs fb; // filter buffers (Sa, Sb, Sc, Wexp) in the local spectral layout
   float* x1;    // (B, C, rows*nlon)
   float *W1f, *b1f, *h;
+  // fb.x1p: (B, 3, C, rows*nlon) bf16x3 planes (x6 engine with an MLP): x for the
+  // skip GEMM (written by the rfft), then x1 for fc1 (written by the irfft)
 };
 
 void carve_band(Carve& cv, BandBufs& b, const msfno_block_desc* d, const msfno_band_plan_s* p,
@@ -91,6 +93,8 @@ void carve_band(Carve& cv, BandBufs& b, const msfno_block_desc* d, const msfno_b
     b.b1f = cv.take<float>((int64_t)B * Hd);
     b.h = cv.take<float>(mlp_h_floats(B, Hd, Pl));
   }
+  b.fb.x1p = (x1_planes(d, p->inv) && Pl % 8 == 0) ? cv.take<unsigned short>(BC * 3 * Pl)
+                                                   : nullptr;
   carve_dense_ws(cv, b.fb.dw, d, B);
 }
 
@@ -249,8 +253,10 @@ int msfno_band_block_stage(const msfno_block_desc* d, msfno_band_plan_t p, int s
   switch (stage) {
     case 0: {
       MSFNO_REQUIRE(io->x && io->stats_local, MSFNO_EINVAL, "stage 0 needs x and stats_local");
-      if (d->inner_skip == MSFNO_SKIP_LINEAR) {
-        MSFNO_REQUIRE(d->skip_w, MSFNO_EINVAL, "missing inner_skip weight");
+      // the skip GEMM as in msfno_block_forward: on x planes written by the rfft (forked
+      // after it) when the plane buffer exists, else on fp32 x (forked first)
+      const bool xpl = skip_planes(d, p->fwd, b.fb);
+      auto launch_skip = [&]() -> int {
         SideCtx* side = nullptr;
         MSFNO_TRY(side_ctx(&side));
         hipStream_t ss = s;
@@ -262,18 +268,32 @@ int msfno_band_block_stage(const msfno_block_desc* d, msfno_band_plan_t p, int s
         prof(ST_SKIP, ss);
         GemmEpi e;
         e.bias = d->skip_b;
-        MSFNO_TRY(gemm_dense(ROLE_SKIP, TILE_128x256, d->skip_w, io->x, b.x1, (int)C, (int)Pl,
-                             (int)C, (int)C, (int)Pl, (int)Pl, 0, C * Pl, C * Pl, B, e,
-                             b.fb.dw.skip, b.fb.dw.skip_b, ss));
+        if (xpl) {
+          e.b_planes = b.fb.x1p;
+          e.b_plane_stride = C * Pl;
+          MSFNO_TRY(gemm_x6p(d->skip_w, b.x1, (int)C, (int)Pl, (int)C, (int)C, (int)Pl, (int)Pl,
+                             0, 3 * C * Pl, C * Pl, B, e, b.fb.dw.skip, b.fb.dw.skip_b, ss));
+        } else {
+          MSFNO_TRY(gemm_dense(ROLE_SKIP, TILE_128x256, d->skip_w, io->x, b.x1, (int)C, (int)Pl,
+                               (int)C, (int)C, (int)Pl, (int)Pl, 0, C * Pl, C * Pl, B, e,
+                               b.fb.dw.skip, b.fb.dw.skip_b, ss));
+        }
         if (side) {
           prof(ST_END, ss);
           MSFNO_CHECK_HIP(hipEventRecord(side->join, ss));
         }
+        return MSFNO_OK;
+      };
+      if (d->inner_skip == MSFNO_SKIP_LINEAR) {
+        MSFNO_REQUIRE(d->skip_w, MSFNO_EINVAL, "missing inner_skip weight");
+        if (!xpl) MSFNO_TRY(launch_skip());
       }
       prof(ST_FFT_FWD, s);
       const float scale = (float)(2.0 * M_PI / p->nlon);
+      const C2RPlanes xp{b.fb.x1p, (int)C, p->rows};
       MSFNO_TRY(launch_fft_r2c_rows(p->fwd->fft, io->x, b.Xn, b.rs, BC * p->rows, p->mmax, scale,
-                                    s));
+                                    s, xpl ? &xp : nullptr));
+      if (xpl) MSFNO_TRY(launch_skip());
       prof(ST_NORM0, s);
       MSFNO_TRY(launch_stats_partial(b.rs, p->rows, p->nlon, BC, io->stats_local, s));
       break;
@@ -320,8 +340,10 @@ int msfno_band_block_stage(const msfno_block_desc* d, msfno_band_plan_t p, int s
         skip_src = io->x;
       }
       prof(ST_FFT_INV, s);
+      // with an MLP on the x6 engine the irfft writes x1 as planes (fc1's B operand)
+      const C2RPlanes x1p{b.fb.x1p, (int)C, p->rows};
       MSFNO_TRY(launch_fft_c2r_rows(p->inv->fft, b.Xn, b.x1, skip_src, b.rs, BC * p->rows,
-                                    p->mmax, 0, s));
+                                    p->mmax, 0, s, b.fb.x1p ? &x1p : nullptr));
       prof(ST_NORM1, s);
       MSFNO_TRY(launch_stats_partial(b.rs, p->rows, p->nlon, BC, io->stats_local, s));
       break;
@@ -340,7 +362,8 @@ int msfno_band_block_stage(const msfno_block_desc* d, msfno_band_plan_t p, int s
         const int64_t Hd = d->mlp_hidden;
         MSFNO_TRY(launch_fold_affine(d->fc1_w, d->fc1_b, b.sc1, b.sh1, b.W1f, b.b1f, B, (int)Hd,
                                      (int)C, s));
-        MSFNO_TRY(run_mlp(d, b.W1f, b.b1f, b.x1, b.h, io->out, resid, B, Pl, b.fb.dw, s));
+        MSFNO_TRY(run_mlp(d, b.W1f, b.b1f, b.x1, b.h, io->out, resid, B, Pl, b.fb.dw, s,
+                          b.fb.x1p));
       } else {
         prof(ST_OUT_AFFINE, s);
         MSFNO_TRY(launch_affine_rows(b.x1, b.sc1, b.sh1, resid, io->out, BC, Pl, 0, nullptr, 0, s));
