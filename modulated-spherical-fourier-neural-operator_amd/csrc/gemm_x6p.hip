@@ -131,11 +131,13 @@ __global__ void split_planes_kernel(const float* __restrict__ x, unsigned short*
   }
 }
 
-template <int EPI, int NSTAGE = 3>
-__global__ __launch_bounds__(512) void gemm_x6p_kernel(GemmParams p) {
+template <int EPI, int NSTAGE = 3, int WAVES = 8>
+__global__ __launch_bounds__(64 * WAVES) void gemm_x6p_kernel(GemmParams p) {
   constexpr int BM = X6P_BM, BN = X6P_BN, BK = X6P_BK;
-  constexpr int WGM = 4, WGN = 2, NTHR = 512;
-  constexpr int WM = BM / WGM, WN = BN / WGN;  // 64 x 128
+  // 8 waves as 4 x 2 (wave 64 x 128), or 4 waves as 2 x 2 (wave 128 x 128, 256
+  // accumulator registers: one wave per SIMD)
+  constexpr int WGM = WAVES == 8 ? 4 : 2, WGN = 2, NTHR = 64 * WAVES;
+  constexpr int WM = BM / WGM, WN = BN / WGN;
   constexpr int MT = WM / 32, NT = WN / 32;
   constexpr int A_PLANE = BM * BK;             // bf16 elements
   constexpr int B_PLANE = BK * BN;
@@ -144,8 +146,9 @@ __global__ __launch_bounds__(512) void gemm_x6p_kernel(GemmParams p) {
   constexpr int EPI_BYTES = 32 * WGM * (BN + 8) * 4;
   constexpr int LDS_BYTES = RING_BYTES > EPI_BYTES ? RING_BYTES : EPI_BYTES;
   constexpr bool HAS_BIAS = (EPI & EPI_BIAS) != 0;
-  constexpr int LOADS = 6;  // LDS-DMA wave-instructions per wave per k-tile
-  static_assert(STAGE * 2 == 48 * 1024 && LOADS * 8 * 1024 == STAGE * 2, "stage = 48 x 1 KB");
+  constexpr int LOADS = 48 / WAVES;  // LDS-DMA wave-instructions per wave per k-tile
+  constexpr int QA = LOADS / 2;       // A (and B) pieces per wave
+  static_assert(STAGE * 2 == 48 * 1024 && LOADS * WAVES * 1024 == STAGE * 2, "stage = 48 x 1 KB");
   // one LDS object only: a second __shared__ array makes hipcc drain the DMA
   // (vmcnt(0)) before the first ds_read of every k-tile
   __shared__ __attribute__((aligned(16))) char lds_raw[LDS_BYTES + (HAS_BIAS ? BM * 4 : 0)];
@@ -174,16 +177,16 @@ __global__ __launch_bounds__(512) void gemm_x6p_kernel(GemmParams p) {
     for (int r = tid; r < BM; r += NTHR) bias_s[r] = bias[min(m0 + r, M - 1)];
   }
 
-  // ---- LDS-DMA sources: per wave 3 A pieces and 3 B pieces of 1 KB per k-tile
-  // A piece a = wave + 8 q (q < 3): plane a / 8, rows 32 (a % 8) .. + 31
-  // B piece b = wave + 8 q (q < 3): plane b / 8, rows 2 (b % 8), 2 (b % 8) + 1
-  const unsigned short* a_src[3];
-  int a_dst[3], b_dst[3];
-  int64_t b_row_off[3];
-  int b_col[3], b_row[3];
+  // ---- LDS-DMA sources: per wave QA A pieces and QA B pieces of 1 KB per k-tile
+  // A piece a = wave + WAVES q (q < QA): plane a / 8, rows 32 (a % 8) .. + 31
+  // B piece b = wave + WAVES q (q < QA): plane b / 8, rows 2 (b % 8), 2 (b % 8) + 1
+  const unsigned short* a_src[QA];
+  int a_dst[QA], b_dst[QA];
+  int64_t b_row_off[QA];
+  int b_col[QA], b_row[QA];
 #pragma unroll
-  for (int q = 0; q < 3; ++q) {
-    const int a = wave + 8 * q;
+  for (int q = 0; q < QA; ++q) {
+    const int a = wave + WAVES * q;
     const int pl = a >> 3, mb = a & 7;
     const int m = 32 * mb + (lane >> 1);
     const int h = (lane & 1) ^ ((m >> 3) & 1);
@@ -201,11 +204,11 @@ __global__ __launch_bounds__(512) void gemm_x6p_kernel(GemmParams p) {
   auto issue = [&](int kt, int st) {
     const uint32_t base = ring_lds + (uint32_t)(st * STAGE * 2);
 #pragma unroll
-    for (int q = 0; q < 3; ++q)
+    for (int q = 0; q < QA; ++q)
       glds16(a_src[q] + kt * a_kstride,
              __builtin_amdgcn_readfirstlane(base + (uint32_t)(a_dst[q] * 2)));
 #pragma unroll
-    for (int q = 0; q < 3; ++q) {
+    for (int q = 0; q < QA; ++q) {
       const int kr = min(kt * BK + b_row[q], K - 1);
       glds16(Bx + b_row_off[q] + (int64_t)kr * ldb + b_col[q],
              __builtin_amdgcn_readfirstlane(base + (uint32_t)(b_dst[q] * 2)));
@@ -279,7 +282,7 @@ __global__ __launch_bounds__(512) void gemm_x6p_kernel(GemmParams p) {
   for (int kt = 0; kt < nk; ++kt) {
     // my DMA of k-tile kt has landed (k-tile kt + 1 may stay in flight) ...
     if (NSTAGE == 3 && kt + 1 < nk)
-      asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+      wait_vmcnt(LOADS);
     else
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     // ... and everyone's: after this barrier stage kt % 3 is complete and every
@@ -693,6 +696,15 @@ static bool use_x6q() {
   return on;
 }
 
+// workgroup of the plane GEMM: 8 waves (default) or 4 (MSFNO_X6P_WAVES=4)
+static int x6p_waves() {
+  static const int w = [] {
+    const char* e = getenv("MSFNO_X6P_WAVES");
+    return (e && e[0] == '4') ? 4 : 8;
+  }();
+  return w;
+}
+
 template <int EPI>
 static void launch_x6p_e(const GemmParams& p, dim3 grid, hipStream_t s, bool q) {
   static const int stages = [] {
@@ -701,6 +713,8 @@ static void launch_x6p_e(const GemmParams& p, dim3 grid, hipStream_t s, bool q) 
   }();
   if (q)
     hipLaunchKernelGGL((gemm_x6q_kernel<EPI>), grid, dim3(512), 0, s, p);
+  else if (stages == 2 && x6p_waves() == 4)
+    hipLaunchKernelGGL((gemm_x6p_kernel<EPI, 2, 4>), grid, dim3(256), 0, s, p);
   else if (stages == 2)
     hipLaunchKernelGGL((gemm_x6p_kernel<EPI, 2>), grid, dim3(512), 0, s, p);
   else
