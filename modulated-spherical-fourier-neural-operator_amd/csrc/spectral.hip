@@ -16,6 +16,9 @@ constexpr float kTwoPi = 6.28318530717958647692f;
 // transposes
 // ---------------------------------------------------------------------------
 constexpr int TK = 64, TMM = 32;
+// symmetric transposes, tiles (latitudes x m) measured at 721 x 1440 among 64x32,
+// 32x64, 64x64 and 32x32: forward 64 x 32 (0.31 ms), inverse 32 x 64 (0.27 vs 0.30 ms)
+constexpr int TK_FWD = 64, TM_FWD = 32, TK_INV = 32, TM_INV = 64;
 
 __global__ __launch_bounds__(256) void transpose_fwd_kernel(const float2* __restrict__ Xn,
                                                             float* __restrict__ Xt, int B, int C,
@@ -136,16 +139,17 @@ int launch_transpose_inv(const float* Yt, float2* Yn, int B, int C, int nlat, in
 // an odd grid once) into slab columns [0, Ke) and Xa_k = X_k - X_{n-1-k} (k < Ko)
 // into [ldke, ldke + Ko); the inverse one unfolds Y_k = E_k + O_k,
 // Y_{n-1-k} = E_k - O_k from the even/odd Legendre outputs.
+template <int TKx, int TMx>
 __global__ __launch_bounds__(256) void transpose_fwd_sym_kernel(
     const float2* __restrict__ Xn, float* __restrict__ Xt, int B, int C, LatGeom g, int mmax,
     const float* __restrict__ nscale, const float* __restrict__ nshift) {
-  __shared__ float2 tn[TMM][TK + 1], ts[TMM][TK + 1];
-  const int k0 = blockIdx.x * TK, m0 = blockIdx.y * TMM;
+  __shared__ float2 tn[TMx][TKx + 1], ts[TMx][TKx + 1];
+  const int k0 = blockIdx.x * TKx, m0 = blockIdx.y * TMx;
   const int bc = blockIdx.z;
   const int b = bc / C, c = bc - b * C;
   const float2* src = Xn + (int64_t)bc * g.nlat * mmax;
-  for (int i = threadIdx.x; i < TK * TMM; i += 256) {
-    const int kk = i / TMM, mm = i - kk * TMM;
+  for (int i = threadIdx.x; i < TKx * TMx; i += 256) {
+    const int kk = i / TMx, mm = i - kk * TMx;
     const int k = k0 + kk, m = m0 + mm;
     float2 vn = make_float2(0.f, 0.f), vs = vn;
     if (k < g.Ke && m < mmax) {
@@ -161,8 +165,8 @@ __global__ __launch_bounds__(256) void transpose_fwd_sym_kernel(
   const int64_t R = 2LL * B * C;
   const int64_t rre = (int64_t)(b * 2 + 0) * C + c;
   const int64_t rim = (int64_t)(b * 2 + 1) * C + c;
-  for (int i = threadIdx.x; i < TK * TMM; i += 256) {
-    const int mm = i / TK, kk = i - mm * TK;
+  for (int i = threadIdx.x; i < TKx * TMx; i += 256) {
+    const int mm = i / TKx, kk = i - mm * TKx;
     const int k = k0 + kk, m = m0 + mm;
     if (k >= g.Ke || m >= mmax) continue;
     const float2 n = tn[mm][kk], q = ts[mm][kk];
@@ -181,9 +185,9 @@ __global__ __launch_bounds__(256) void transpose_fwd_sym_kernel(
 
 int launch_transpose_fwd_sym(const float2* Xn, float* Xt, int B, int C, const LatGeom& g, int mmax,
                              const float* nscale, const float* nshift, hipStream_t s) {
-  dim3 grid((unsigned)cdiv(g.Ke, TK), (unsigned)cdiv(mmax, TMM), (unsigned)(B * C));
-  hipLaunchKernelGGL(transpose_fwd_sym_kernel, grid, dim3(256), 0, s, Xn, Xt, B, C, g, mmax,
-                     nscale, nshift);
+  dim3 grid((unsigned)cdiv(g.Ke, TK_FWD), (unsigned)cdiv(mmax, TM_FWD), (unsigned)(B * C));
+  hipLaunchKernelGGL((transpose_fwd_sym_kernel<TK_FWD, TM_FWD>), grid, dim3(256), 0, s, Xn, Xt, B,
+                     C, g, mmax, nscale, nshift);
   return launch_check("transpose_fwd_sym");
 }
 
@@ -325,19 +329,20 @@ int launch_relayout_table_x6(const msfno_sht_plan_s& p, const float* table, hipS
   return launch_check("relayout_table_x6");
 }
 
+template <int TKx, int TMx>
 __global__ __launch_bounds__(256) void transpose_inv_sym_kernel(const float* __restrict__ Yt,
                                                                 float2* __restrict__ Yn, int B,
                                                                 int C, LatGeom g, int mmax,
                                                                 int mact) {
-  __shared__ float2 tn[TMM][TK + 1], ts[TMM][TK + 1];
-  const int k0 = blockIdx.x * TK, m0 = blockIdx.y * TMM;
+  __shared__ float2 tn[TMx][TKx + 1], ts[TMx][TKx + 1];
+  const int k0 = blockIdx.x * TKx, m0 = blockIdx.y * TMx;
   const int bc = blockIdx.z;
   const int b = bc / C, c = bc - b * C;
   const int64_t R = 2LL * B * C;
   const int64_t rre = (int64_t)(b * 2 + 0) * C + c;
   const int64_t rim = (int64_t)(b * 2 + 1) * C + c;
-  for (int i = threadIdx.x; i < TK * TMM; i += 256) {
-    const int mm = i / TK, kk = i - mm * TK;
+  for (int i = threadIdx.x; i < TKx * TMx; i += 256) {
+    const int mm = i / TKx, kk = i - mm * TKx;
     const int k = k0 + kk, m = m0 + mm;
     float2 n = make_float2(0.f, 0.f), q = n;
     if (k < g.Ke && m < mact) {
@@ -356,8 +361,8 @@ __global__ __launch_bounds__(256) void transpose_inv_sym_kernel(const float* __r
   }
   __syncthreads();
   float2* dst = Yn + (int64_t)bc * g.nlat * mmax;
-  for (int i = threadIdx.x; i < TK * TMM; i += 256) {
-    const int kk = i / TMM, mm = i - kk * TMM;
+  for (int i = threadIdx.x; i < TKx * TMx; i += 256) {
+    const int kk = i / TMx, mm = i - kk * TMx;
     const int k = k0 + kk, m = m0 + mm;
     if (k >= g.Ke || m >= mmax) continue;
     dst[(int64_t)k * mmax + m] = tn[mm][kk];
@@ -367,8 +372,9 @@ __global__ __launch_bounds__(256) void transpose_inv_sym_kernel(const float* __r
 
 int launch_transpose_inv_sym(const float* Yt, float2* Yn, int B, int C, const LatGeom& g, int mmax,
                              int mact, hipStream_t s) {
-  dim3 grid((unsigned)cdiv(g.Ke, TK), (unsigned)cdiv(mmax, TMM), (unsigned)(B * C));
-  hipLaunchKernelGGL(transpose_inv_sym_kernel, grid, dim3(256), 0, s, Yt, Yn, B, C, g, mmax, mact);
+  dim3 grid((unsigned)cdiv(g.Ke, TK_INV), (unsigned)cdiv(mmax, TM_INV), (unsigned)(B * C));
+  hipLaunchKernelGGL((transpose_inv_sym_kernel<TK_INV, TM_INV>), grid, dim3(256), 0, s, Yt, Yn, B,
+                     C, g, mmax, mact);
   return launch_check("transpose_inv_sym");
 }
 
