@@ -1072,7 +1072,8 @@ int msfno_sht_plan_load_table(msfno_sht_plan_t p, const float* table, void* stre
   p->desc_R = -1;  // descriptors depend on the layout
   MSFNO_TRY(launch_relayout_table(*p, table, s));
   p->descx_R = -1;
-  if (sym) MSFNO_TRY(build_table_x6(p, table, s));
+  // the bf16x3 table image only feeds the x6 Legendre GEMMs (MSFNO_LEG_X6=1)
+  if (sym && leg_x6_enabled()) MSFNO_TRY(build_table_x6(p, table, s));
   p->table_loaded = 1;
   return MSFNO_OK;
 }

@@ -82,6 +82,21 @@ int main(int argc, char** argv) {
              fl / ms / 1e9);
     }
   }
+  // custom x6 shape (fp32 B split in-kernel): gemm_x6_bench x6 M N K [epi bits: 1 bias,
+  // 2 add, 4 gelu] [tile id]
+  if (only && std::string(only) == "x6" && argc >= 5) {
+    const int M = atoi(argv[2]), N = atoi(argv[3]), K = atoi(argv[4]), ep = argc > 5 ? atoi(argv[5]) : 0;
+    const GemmTile t = argc > 6 ? (GemmTile)atoi(argv[6]) : TILE_256x256;
+    GemmEpi e;
+    if (ep & 1) e.bias = bias;
+    if (ep & 2) { e.addend = D; e.ldd = N; }
+    if (ep & 4) e.act = 1;
+    const double fl = 2.0 * M * (double)N * K;
+    float ms = timeit([&] { gemm_x6(t, A, B, C, M, N, K, K, N, N, 0, 0, 0, 1, e, ws, wsb, 0); });
+    printf("x6 M=%d N=%d K=%d epi=%d tile=%d: %.3f ms %.1f TF/s (fp32-equivalent)\n", M, N, K, ep,
+           (int)t, ms, fl / ms / 1e9);
+    return 0;
+  }
   // custom x6p shape: gemm_x6_bench x6p M N K [epi: 0 none, 1 bias, 3 bias+add]
   if (only && std::string(only) == "x6p" && argc >= 6) {
     const int M = atoi(argv[2]), N = atoi(argv[3]), K = atoi(argv[4]), ep = argc > 5 ? atoi(argv[5]) : 0;
