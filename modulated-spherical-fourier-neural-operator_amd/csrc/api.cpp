@@ -1305,7 +1305,7 @@ extern "C" {
 size_t msfno_mlp_workspace_size(const msfno_mlp_desc* d, int B, long long P) {
   if (!d || B <= 0 || P <= 0) return 0;
   Carve cv;
-  cv.take<float>((int64_t)B * d->Hid * P);                // h
+  cv.take<float>(std::max<int64_t>((int64_t)B * d->Hid * P, mlp_h_floats(B, d->Hid, P)));  // h
   if (d->Cin2 > 0) cv.take<float>((int64_t)B * d->Hid * P);  // first half of fc1
   cv.take<char>(gemm_dense_workspace(d->Hid, d->Cin, 1));   // split fc1 weights
   if (d->Cin2 > 0) cv.take<char>(gemm_dense_workspace(d->Hid, d->Cin2, 1));
@@ -1329,7 +1329,7 @@ int msfno_mlp_forward(const msfno_mlp_desc* d, const float* x, const float* x2,
   Carve cv;
   cv.base = (char*)ws;
   const int64_t Hd = d->Hid, Ct = d->Cin + d->Cin2;
-  float* h = cv.take<float>((int64_t)B * Hd * P);
+  float* h = cv.take<float>(std::max<int64_t>((int64_t)B * Hd * P, mlp_h_floats(B, Hd, P)));
   float* t = d->Cin2 > 0 ? cv.take<float>((int64_t)B * Hd * P) : nullptr;
   const size_t w1b = gemm_dense_workspace((int)Hd, d->Cin, 1);
   void* w1 = cv.take<char>(w1b);
@@ -1338,6 +1338,12 @@ int msfno_mlp_forward(const msfno_mlp_desc* d, const float* x, const float* x2,
   const size_t w2b = gemm_dense_workspace(d->Cout, (int)Hd, 1);
   void* w2 = cv.take<char>(w2b);
   const int Pi = (int)P;
+  // x6 engine: h travels as bf16x3 planes [B][3][Hd][ldh] (fc1's epilogue splits it
+  // once); fc2 stages it by LDS-DMA (gemm_x6p) or, for Cout <= 128 (the decoder's
+  // 256 -> 73), on the 128-row x6 tile with plane B
+  const bool planes = mlp_h_planes(w1 != nullptr && w2 != nullptr);
+  const int64_t ldh = planes ? round_up(P, 8) : P;
+  unsigned short* hx = planes ? reinterpret_cast<unsigned short*>(h) : nullptr;
   prof(ST_FC1, s);
   if (d->Cin2 > 0) {
     // fc1 over the concatenation [x ; x2]: t = W1[:, :Cin]·x, then h = GELU(W1[:, Cin:]·x2 + b1 + t)
@@ -1348,22 +1354,36 @@ int msfno_mlp_forward(const msfno_mlp_desc* d, const float* x, const float* x2,
     e1.bias = d->fc1_b;
     e1.addend = t; e1.sD = Hd * P; e1.ldd = Pi;
     e1.act = 1;
+    if (planes) { e1.c_planes = hx; e1.c_plane_stride = Hd * ldh; }
     MSFNO_TRY(gemm_dense(ROLE_FC1, TILE_128x256, d->fc1_w + d->Cin, x2, h, (int)Hd, Pi, d->Cin2,
-                         (int)Ct, Pi, Pi, 0, (int64_t)d->Cin2 * P, Hd * P, B, e1, w12, w1b2, s));
+                         (int)Ct, Pi, (int)ldh, 0, (int64_t)d->Cin2 * P,
+                         (planes ? 3 : 1) * Hd * ldh, B, e1, w12, w1b2, s));
   } else {
     GemmEpi e1;
     e1.bias = d->fc1_b;
     e1.act = 1;
+    if (planes) { e1.c_planes = hx; e1.c_plane_stride = Hd * ldh; }
     MSFNO_TRY(gemm_dense(ROLE_FC1, TILE_128x256, d->fc1_w, x, h, (int)Hd, Pi, d->Cin, d->Cin, Pi,
-                         Pi, 0, (int64_t)d->Cin * P, Hd * P, B, e1, w1, w1b, s));
+                         (int)ldh, 0, (int64_t)d->Cin * P, (planes ? 3 : 1) * Hd * ldh, B, e1, w1,
+                         w1b, s));
   }
   prof(ST_FC2, s);
   GemmEpi e2;
   e2.bias = d->fc2_b;
   if (addend) { e2.addend = addend; e2.sD = add_bstride; e2.ldd = Pi; }
+  if (planes) {
+    e2.b_planes = hx;
+    e2.b_plane_stride = Hd * ldh;
+    if (d->Cout > 128) {
+      MSFNO_TRY(gemm_x6p(d->fc2_w, out, d->Cout, Pi, (int)Hd, (int)Hd, (int)ldh, Pi, 0,
+                         3 * Hd * ldh, (int64_t)d->Cout * P, B, e2, w2, w2b, s));
+      prof(ST_END, s);
+      return MSFNO_OK;
+    }
+  }
   const GemmTile t2 = d->Cout <= 128 ? TILE_128x128 : TILE_256x128;
-  MSFNO_TRY(gemm_dense(ROLE_FC2, t2, d->fc2_w, h, out, d->Cout, Pi, (int)Hd, (int)Hd, Pi, Pi, 0,
-                       Hd * P, (int64_t)d->Cout * P, B, e2, w2, w2b, s));
+  MSFNO_TRY(gemm_dense(ROLE_FC2, t2, d->fc2_w, h, out, d->Cout, Pi, (int)Hd, (int)Hd, (int)ldh, Pi,
+                       0, (planes ? 3 : 1) * Hd * ldh, (int64_t)d->Cout * P, B, e2, w2, w2b, s));
   prof(ST_END, s);
   return MSFNO_OK;
 }

@@ -783,6 +783,7 @@ int gemm_x6p(const float* A, float* C, int M, int N, int K, int lda, int ldb, in
     case EPI_PLANES: launch_x6p_e<EPI_PLANES>(p, grid, s, q); break;
     case EPI_BIAS: launch_x6p_e<EPI_BIAS>(p, grid, s, q); break;
     case EPI_BIAS | EPI_ADD: launch_x6p_e<EPI_BIAS | EPI_ADD>(p, grid, s, q); break;
+    case EPI_ADD: launch_x6p_e<EPI_ADD>(p, grid, s, q); break;
     case EPI_BIAS | EPI_GELU | EPI_PLANES:
       launch_x6p_e<EPI_BIAS | EPI_GELU | EPI_PLANES>(p, grid, s, q); break;
     default:
