@@ -931,6 +931,37 @@ int run_mlp(const msfno_block_desc* d, const float* W1f, const float* b1f, const
   const int64_t ldh = planes ? round_up(P, 8) : P;
   unsigned short* hx = planes ? reinterpret_cast<unsigned short*>(h) : nullptr;
   prof(ST_FC1, s);
+  const int64_t chunk = mlp_chunk(P);
+  if (planes && x1p && chunk > 0 && chunk < P) {
+    // pixel chunks: fc1 writes a chunk of h (planes) that fc2 reads back while it is
+    // still in the Infinity Cache; both weight images are split once
+    MSFNO_TRY(gemm_x6p_split_a(W1f, (int)Hd, (int)C, (int)C, Hd * C, B, dw.fc1, dw.fc1_b, s));
+    MSFNO_TRY(gemm_x6p_split_a(d->fc2_w, (int)C, (int)Hd, (int)Hd, 0, 1, dw.fc2, dw.fc2_b, s));
+    const int64_t ldc = round_up(chunk, 8);
+    for (int64_t p0 = 0; p0 < P; p0 += chunk) {
+      const int pc = (int)std::min<int64_t>(chunk, P - p0);
+      GemmEpi e1;
+      e1.bias = b1f;
+      e1.sBias = Hd;
+      e1.act = 1;
+      e1.a_planes = static_cast<const unsigned short*>(dw.fc1);
+      e1.b_planes = x1p + p0;
+      e1.b_plane_stride = C * P;
+      e1.c_planes = hx;
+      e1.c_plane_stride = Hd * ldc;
+      MSFNO_TRY(gemm_x6p(W1f, h, (int)Hd, pc, (int)C, (int)C, (int)P, (int)ldc, Hd * C, 3 * C * P,
+                         3 * Hd * ldc, B, e1, dw.fc1, dw.fc1_b, s));
+      GemmEpi e2;
+      e2.bias = d->fc2_b;
+      if (resid) { e2.addend = resid + p0; e2.sD = C * P; e2.ldd = (int)P; }
+      e2.a_planes = static_cast<const unsigned short*>(dw.fc2);
+      e2.b_planes = hx;
+      e2.b_plane_stride = Hd * ldc;
+      MSFNO_TRY(gemm_x6p(d->fc2_w, out + p0, (int)C, pc, (int)Hd, (int)Hd, (int)ldc, (int)P, 0,
+                         3 * Hd * ldc, C * P, B, e2, dw.fc2, dw.fc2_b, s));
+    }
+    return MSFNO_OK;
+  }
   GemmEpi e1;
   e1.bias = b1f;
   e1.sBias = Hd;
@@ -970,6 +1001,17 @@ bool skip_planes(const msfno_block_desc* d, const msfno_sht_plan_s* f, const Blo
   }();
   return on && b.x1p && b.dw.skip && d->inner_skip == MSFNO_SKIP_LINEAR && !use_fft_tile(f) &&
          fft_r2c_planes_supported(f->fft, f->mmax);
+}
+
+// pixels per fc1 -> fc2 chunk of the block MLP (MSFNO_MLP_CHUNK, multiple of 256;
+// 0 = one pass over the field)
+int64_t mlp_chunk(int64_t P) {
+  static const int64_t c = [] {
+    const char* e = getenv("MSFNO_MLP_CHUNK");
+    return e ? (int64_t)atoll(e) / 256 * 256 : (int64_t)0;
+  }();
+  (void)P;
+  return c;
 }
 
 // x1 (the MLP input) written by the inverse FFT as bf16x3 planes: x6 engine, an

@@ -82,6 +82,7 @@ int run_mlp(const msfno_block_desc* d, const float* W1f, const float* b1f, const
             float* h, float* out, const float* resid, int B, int64_t P, const DenseWs& dw,
             hipStream_t s, const unsigned short* x1p = nullptr);
 bool mlp_h_planes(bool have_ws);
+int64_t mlp_chunk(int64_t P);
 int64_t mlp_h_floats(int B, int64_t Hd, int64_t P);
 bool x1_planes(const msfno_block_desc* d, const msfno_sht_plan_s* g);
 bool skip_planes(const msfno_block_desc* d, const msfno_sht_plan_s* f, const BlockBufs& b);

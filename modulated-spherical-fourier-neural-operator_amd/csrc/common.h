@@ -173,6 +173,10 @@ int launch_split_a(const float* A, unsigned short* Ax, int M, int K, int lda, in
 // epi.b_planes required (ldb, sB, b_plane_stride % 8 == 0, 16-B aligned); A fp32
 // is split per call into ws (>= gemm_x6p_workspace(M, K, sA == 0 ? 1 : batch))
 size_t gemm_x6p_workspace(int M, int K, int batch_a);
+// the A image of gemm_x6p (16-deep k-tiles) split once into ws, for a sequence of
+// gemm_x6p calls that pass it as epi.a_planes (e.g. pixel-chunked MLPs)
+int gemm_x6p_split_a(const float* A, int M, int K, int lda, int64_t sA, int batch, void* ws,
+                     size_t ws_bytes, hipStream_t s);
 int gemm_x6p(const float* A, float* C, int M, int N, int K, int lda, int ldb, int ldc,
              int64_t sA, int64_t sB, int64_t sC, int batch, const GemmEpi& epi, void* ws,
              size_t ws_bytes, hipStream_t s);

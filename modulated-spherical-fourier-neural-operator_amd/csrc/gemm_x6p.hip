@@ -195,7 +195,9 @@ __global__ __launch_bounds__(64 * WAVES) void gemm_x6p_kernel(GemmParams p) {
     const int row = 2 * mb + (lane >> 5);
     const int gu = (lane & 31) ^ (4 * (row & 3));
     b_row[q] = row;
-    b_col[q] = min(n0 + 8 * gu, ldb - 8);
+    // clamp to the last full 16-B unit of the N columns (not of the row: B may start
+    // mid-row, e.g. a pixel chunk of a wider plane)
+    b_col[q] = min(n0 + 8 * gu, ((N + 7) & ~7) - 8);
     b_row_off[q] = (int64_t)pl * p.sBxp;
     b_dst[q] = 3 * A_PLANE + pl * B_PLANE + mb * 2 * BN;
   }
@@ -653,6 +655,19 @@ size_t gemm_x6p_workspace(int M, int K, int batch_a) {
   return (size_t)round_up(3 * Mp * Kp * 2 * (int64_t)batch_a, 256);
 }
 
+int gemm_x6p_split_a(const float* A, int M, int K, int lda, int64_t sA, int batch, void* ws,
+                     size_t ws_bytes, hipStream_t s) {
+  const int abatch = sA == 0 ? 1 : batch;
+  const int Mp = (int)round_up(M, X6P_BM), KT = (int)cdiv(K, X6P_BK);
+  MSFNO_REQUIRE(ws && ws_bytes >= gemm_x6p_workspace(M, K, abatch), MSFNO_EINVAL,
+                "gemm_x6p_split_a: workspace too small");
+  const int64_t pairs = (int64_t)Mp * KT * X6P_BK / 2;
+  const int blocks = (int)std::min<int64_t>(cdiv(pairs, 256), 1024);
+  hipLaunchKernelGGL(split_a_tiles_kernel<X6P_BK>, dim3(blocks, abatch), dim3(256), 0, s, A,
+                     static_cast<unsigned short*>(ws), M, K, lda, sA, Mp, KT);
+  return launch_check("split_a_tiles");
+}
+
 int launch_spec_weights_x6p(const SpecWeightsX6p& a, hipStream_t s) {
   if (a.nlayers <= 0) return MSFNO_OK;
   const int blocks = (int)std::min<int64_t>(cdiv(a.start[a.nlayers], 256), 4096);
@@ -732,7 +747,7 @@ int gemm_x6p(const float* A, float* C, int M, int N, int K, int lda, int ldb, in
   const size_t need = (size_t)round_up(3 * round_up(M, X6P_BM) * round_up(K, TKd) * 2 * (int64_t)abatch, 256);
   MSFNO_REQUIRE(epi.a_planes || (ws && ws_bytes >= need), MSFNO_EINVAL,
                 "gemm_x6p: workspace too small");
-  MSFNO_REQUIRE(!epi.a_planes || sA == 0, MSFNO_EINVAL, "gemm_x6p: pre-split A is not batched");
+  // a batched pre-split A (sA != 0) has gemm_x6p_split_a's layout: batch stride 3 planes
   MSFNO_REQUIRE(epi.b_planes, MSFNO_EINVAL, "gemm_x6p: B must be in the plane format");
   MSFNO_REQUIRE(batch <= 65535 && K > 0, MSFNO_EINVAL, "gemm_x6p: bad batch / K");
   MSFNO_REQUIRE(ldb % 8 == 0 && ldb >= 8 && sB % 8 == 0 && epi.b_plane_stride % 8 == 0 &&
