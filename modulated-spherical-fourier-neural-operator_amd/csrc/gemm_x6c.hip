@@ -87,6 +87,52 @@ __global__ void spec_weights_3m_kernel(SpecWeightsX6p a) {
 }
 
 // S fp32 rows [b][ri][c] (ld ldS) -> 3M planes [b][mat][plane][c][ldx]
+// 8 columns per thread: 16-B loads of re and im, 16-B stores of the 9 planes
+// (ldS % 4 == 0, ldx % 8 == 0, 16-B aligned bases); the ragged row tail per column
+__global__ void split3m_x8_kernel(const float* __restrict__ S, unsigned short* __restrict__ X,
+                                  int C, int N, int ldS, int ldx, int64_t x_b, int64_t x_mat,
+                                  int64_t x_plane) {
+  const int b = blockIdx.y;
+  const int c8 = (N + 7) / 8;
+  const int64_t n = (int64_t)C * c8;
+  const float* Sb = S + (int64_t)b * 2 * C * ldS;
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < n;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const int c = (int)(e / c8), col = 8 * (int)(e - (int64_t)c * c8);
+    const float* re = Sb + (int64_t)c * ldS + col;
+    const float* im = Sb + (int64_t)(C + c) * ldS + col;
+    float r[8], i[8];
+    if (col + 8 <= N) {
+      const float4 r0 = *reinterpret_cast<const float4*>(re), r1 = *reinterpret_cast<const float4*>(re + 4);
+      const float4 i0 = *reinterpret_cast<const float4*>(im), i1 = *reinterpret_cast<const float4*>(im + 4);
+      r[0] = r0.x; r[1] = r0.y; r[2] = r0.z; r[3] = r0.w; r[4] = r1.x; r[5] = r1.y; r[6] = r1.z; r[7] = r1.w;
+      i[0] = i0.x; i[1] = i0.y; i[2] = i0.z; i[3] = i0.w; i[4] = i1.x; i[5] = i1.y; i[6] = i1.z; i[7] = i1.w;
+    } else {
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        r[q] = col + q < N ? re[q] : 0.f;
+        i[q] = col + q < N ? im[q] : 0.f;
+      }
+    }
+    unsigned short* d = X + b * x_b + (int64_t)c * ldx + col;
+#pragma unroll
+    for (int mat = 0; mat < 3; ++mat) {
+      uint32_t t[3][4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float a0 = mat == 0 ? r[2 * q] : (mat == 1 ? i[2 * q] : r[2 * q] + i[2 * q]);
+        const float a1 = mat == 0 ? r[2 * q + 1] : (mat == 1 ? i[2 * q + 1] : r[2 * q + 1] + i[2 * q + 1]);
+        split2(a0, a1, t[0][q], t[1][q], t[2][q]);
+      }
+      unsigned short* q0 = d + mat * x_mat;
+      // columns past N are written as the split of 0 (the planes' pad columns)
+#pragma unroll
+      for (int pl = 0; pl < 3; ++pl)
+        *reinterpret_cast<uint4*>(q0 + pl * x_plane) = make_uint4(t[pl][0], t[pl][1], t[pl][2], t[pl][3]);
+    }
+  }
+}
+
 __global__ void split3m_kernel(const float* __restrict__ S, unsigned short* __restrict__ X, int C,
                                int N, int ldS, int ldx, int64_t x_b, int64_t x_mat,
                                int64_t x_plane) {
@@ -336,6 +382,13 @@ int launch_split3m(const float* S, unsigned short* X, int B, int C, int N, int l
                    hipStream_t s) {
   MSFNO_REQUIRE(ldx % 8 == 0, MSFNO_EINVAL, "split3m: ld must be a multiple of 8");
   const int64_t x_plane = (int64_t)C * ldx;
+  if (ldS % 4 == 0 && ldx >= (N + 7) / 8 * 8 && ((reinterpret_cast<uintptr_t>(S) | reinterpret_cast<uintptr_t>(X)) & 15) == 0) {
+    const int64_t n8 = (int64_t)C * ((N + 7) / 8);
+    const int blocks = (int)std::min<int64_t>(cdiv(n8, 256), 4096);
+    hipLaunchKernelGGL(split3m_x8_kernel, dim3(blocks, B), dim3(256), 0, s, S, X, C, N, ldS, ldx,
+                       9 * x_plane, 3 * x_plane, x_plane);
+    return launch_check("split3m");
+  }
   const int64_t n = (int64_t)C * ((N + 1) / 2);
   const int blocks = (int)std::min<int64_t>(cdiv(n, 256), 2048);
   hipLaunchKernelGGL(split3m_kernel, dim3(blocks, B), dim3(256), 0, s, S, X, C, N, ldS, ldx,
