@@ -310,7 +310,8 @@ static GemmTile x6_tile(int M, int N, int batch) {
 }
 
 size_t gemm_x6_workspace(int M, int K, int batch) {
-  const int64_t Mp = round_up(M, 256), Kp = round_up(K, 16);
+  // k padded to 32: the same buffers also hold gemm_x6p's 32-deep x6q A image
+  const int64_t Mp = round_up(M, 256), Kp = round_up(K, 32);
   return (size_t)round_up(3 * Mp * Kp * 2 * (int64_t)batch, 256);
 }
 
