@@ -6,6 +6,7 @@
 //   * the linear filter's per-mode complex contraction (HBM weight stream),
 //   * S-layout conversions (reference dense (l,m) / torch.tril_indices order).
 #include "bf16x3.h"
+#include "dma.h"
 #include "kernels.h"
 
 namespace msfno {
@@ -1071,8 +1072,113 @@ static int launch_contract_t(const float* a, const float* w, float* y, int B, in
   return launch_check("compl_contract");
 }
 
+// Batch 1 (the weight is read exactly once): the weight stream goes HBM -> LDS by
+// LDS-DMA (dma.h), NS - 1 channel steps ahead (MSFNO_CONTRACT_NS, default 2; 2 % faster
+// than the register-load kernel below, which batches > 1 use).  A workgroup owns 256 modes (one per
+// thread) and 16 output channels; a stage holds, for one input channel i, the 16
+// weight rows w[k0 + s, i, n0 .. n0 + 255] and the activation row a[i, n0 ..] (17
+// segments of 2 KB, 34 DMA pieces of 1 KB).
+constexpr int CDMA_KC = 16, CDMA_NT = 256, CDMA_SEG = CDMA_KC + 1, CDMA_PIECES = 2 * CDMA_SEG;
+
+template <int NS>
+__global__ __launch_bounds__(256) void compl_contract_dma_kernel(const float* __restrict__ a,
+                                                                 const float* __restrict__ w,
+                                                                 float* __restrict__ y, int Ci,
+                                                                 int Co, int64_t T, int nkc) {
+  constexpr int STAGE = CDMA_SEG * CDMA_NT * 8;  // bytes
+  __shared__ __attribute__((aligned(16))) char lds[NS * STAGE];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int kc = blockIdx.x % nkc, mt = blockIdx.x / nkc;
+  const int k0 = kc * CDMA_KC;
+  const int64_t n0 = (int64_t)mt * CDMA_NT;
+  const int64_t rowb = T * 8;  // bytes per (k, i) weight row / per activation row
+  // this wave's pieces p = wave + 4 q (p < 34): segment p / 2 (16 = activation), half p % 2
+  constexpr int QMAX = (CDMA_PIECES + 3) / 4;
+  const int nq = (CDMA_PIECES - wave + 3) / 4;
+  const char* src[QMAX];
+  int64_t istep[QMAX];
+  uint32_t dst[QMAX];
+#pragma unroll
+  for (int q = 0; q < QMAX; ++q) {
+    const int pc = min(wave + 4 * q, CDMA_PIECES - 1);
+    const int seg = pc >> 1, half = pc & 1;
+    const int64_t off = min(n0 * 8 + half * 1024 + lane * 16, rowb - 16);
+    const int k = min(k0 + seg, Co - 1);
+    src[q] = seg < CDMA_KC ? reinterpret_cast<const char*>(w) + (int64_t)k * Ci * rowb + off
+                           : reinterpret_cast<const char*>(a) + off;
+    istep[q] = rowb;  // next input channel: next row of the same (k) block / of a
+    dst[q] = (uint32_t)(seg * CDMA_NT * 8 + half * 1024);
+  }
+  const uint32_t lds0 = lds_addr(lds);
+  auto issue = [&](int i, int slot) {
+#pragma unroll
+    for (int q = 0; q < QMAX; ++q)
+      if (q < nq) glds16(src[q] + i * istep[q], lds0 + (uint32_t)(slot * STAGE) + dst[q]);
+  };
+#pragma unroll
+  for (int j = 0; j < NS - 1; ++j)
+    if (j < Ci) issue(j, j);
+  float2 acc[CDMA_KC];
+#pragma unroll
+  for (int k = 0; k < CDMA_KC; ++k) acc[k] = make_float2(0.f, 0.f);
+  for (int i = 0; i < Ci; ++i) {
+    // stage i landed (stages i + 1 .. i + NS - 2 may stay in flight)
+    const int ahead = min(NS - 2, Ci - 1 - i);
+    wait_vmcnt(ahead * nq);
+    // raw barrier (a __syncthreads fence could drain the DMA still in flight): every
+    // wave's pieces landed, and every wave's reads of slot (i - 1) % NS have returned
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (i + NS - 1 < Ci) issue(i + NS - 1, (i + NS - 1) % NS);
+    const float2* st = reinterpret_cast<const float2*>(lds + (i % NS) * STAGE);
+    const float2 av = st[CDMA_KC * CDMA_NT + tid];
+#pragma unroll
+    for (int k = 0; k < CDMA_KC; ++k) {
+      const float2 wv = st[k * CDMA_NT + tid];
+      acc[k].x = fmaf(av.x, wv.x, fmaf(-av.y, wv.y, acc[k].x));
+      acc[k].y = fmaf(av.x, wv.y, fmaf(av.y, wv.x, acc[k].y));
+    }
+  }
+  const int64_t n = n0 + tid;
+  if (n < T) {
+    float2* y2 = reinterpret_cast<float2*>(y);
+#pragma unroll
+    for (int k = 0; k < CDMA_KC; ++k)
+      if (k0 + k < Co) y2[(int64_t)(k0 + k) * T + n] = acc[k];
+  }
+}
+
+// MSFNO_CONTRACT_DMA=0 keeps the register-load kernel at batch 1 (A/B)
+static bool contract_dma() {
+  static const bool on = [] {
+    const char* e = getenv("MSFNO_CONTRACT_DMA");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 int launch_compl_contract(const float* a, const float* w, float* y, int B, int Ci, int Co,
                           int64_t T, hipStream_t s) {
+  if (B == 1 && contract_dma() && T % 2 == 0 && T >= 8 && Ci > 0 &&
+      ((reinterpret_cast<uintptr_t>(a) | reinterpret_cast<uintptr_t>(w)) & 15) == 0) {
+    const int nkc = (int)cdiv(Co, CDMA_KC);
+    const int64_t nmt = cdiv(T, CDMA_NT);
+    MSFNO_REQUIRE(nmt * nkc < (1LL << 31), MSFNO_EINVAL, "contract grid too large");
+    static const int ns = [] {
+      const char* e = getenv("MSFNO_CONTRACT_NS");
+      return e ? atoi(e) : 2;  // two 68-KB workgroups per CU: 5.88 ms vs 6.16 (3) / 6.19 (4)
+    }();
+    if (ns == 2)
+      hipLaunchKernelGGL(compl_contract_dma_kernel<2>, dim3((unsigned)(nmt * nkc)), dim3(256), 0,
+                         s, a, w, y, Ci, Co, T, nkc);
+    else if (ns == 4)
+      hipLaunchKernelGGL(compl_contract_dma_kernel<4>, dim3((unsigned)(nmt * nkc)), dim3(256), 0,
+                         s, a, w, y, Ci, Co, T, nkc);
+    else
+      hipLaunchKernelGGL(compl_contract_dma_kernel<3>, dim3((unsigned)(nmt * nkc)), dim3(256), 0,
+                         s, a, w, y, Ci, Co, T, nkc);
+    return launch_check("compl_contract_dma");
+  }
   const bool even = (T % 2 == 0) && ((reinterpret_cast<uintptr_t>(a) | reinterpret_cast<uintptr_t>(w) |
                                       reinterpret_cast<uintptr_t>(y)) & 15) == 0;
   if (B >= 8) {

@@ -29,6 +29,8 @@ VARIANTS = [
     {"MSFNO_SPEC_3M": "0"},
     {"MSFNO_SIDE_STREAM": "0"},
     {"MSFNO_GEMM": "f32"},
+    {"MSFNO_CONTRACT_DMA": "0"},
+    {"MSFNO_CONTRACT_NS": "3"},
 ]
 
 
