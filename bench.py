@@ -90,8 +90,14 @@ def pmc_traffic(stage):
     if sym is None:
         return None, None
     import glob
+    import re
+
+    def newest_first(path):  # r01_v10 after r01_v9: compare the numbers, not the text
+        tag = os.path.basename(os.path.dirname(path))
+        return [int(t) if t.isdigit() else t for t in re.split(r"(\d+)", tag)]
+
     for f in sorted(glob.glob(os.path.join(REPO, "profiles", "*", "pmc_traffic.json")),
-                    reverse=True):
+                    key=newest_first, reverse=True):
         try:
             with open(f) as fh:
                 k = json.load(fh)["kernels"].get(sym)
