@@ -2,6 +2,7 @@
 // fp32-accurate 6-term bf16 split): kernel parameters, the XCD-aware tile
 // remap, GELU(erf) and the LDS-staged fused epilogue.
 #pragma once
+#include <cstdlib>
 #include "bf16x3.h"
 #include "common.h"
 
@@ -37,6 +38,7 @@ struct GemmParams {
   int64_t sBxp;
   unsigned short* Cx;
   int64_t sCxp;
+  int cx16;  // plane rows 16-B aligned (ldc, sC, sCxp % 8 == 0, Cx 16-B aligned): uint4 stores
 };
 
 __device__ __forceinline__ int xcd_remap(int orig, int nwg) {
@@ -120,6 +122,15 @@ __device__ __forceinline__ float gelu_erf(float v) {
 #endif
 }
 
+// 16-B plane stores in the epilogue (MSFNO_CX16=0: 8-B stores, for A/B)
+inline bool cx16_enabled() {
+  static const bool on = [] {
+    const char* e = getenv("MSFNO_CX16");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 // epilogue flags (+ EPI_GELU_B: GELU applied to the B operand while it is staged)
 enum : int {
   EPI_BIAS = 1, EPI_ADD = 2, EPI_GELU = 4, EPI_RELU = 8, EPI_ROWSCALE = 32, EPI_GELU_B = 64,
@@ -135,7 +146,7 @@ enum : int {
 // RB = 32: accumulators in the 32x32 MFMA block layout (floatx16 per block);
 // RB = 16: the 16x16 layout (floatx4: row 4 (lane >> 4) + r, col lane & 15)
 template <int BM, int BN, int EPI, int WGM = 2, int WGN = 2, int MT, int NT, int RB = 32,
-          class AccV = floatx16>
+          class AccV = floatx16, bool PAIRS = true>
 __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, AccV (&acc)[MT][NT],
                                               float* lds, const float* bias_s, float* C,
                                               const float* addend, int M, int N, int ldc,
@@ -160,6 +171,12 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, AccV (&acc)[M
   constexpr int QC = QPT < 8 ? QPT : 8;
   static_assert(QPT * NTHR * 4 == RB * WGM * BN && QPT % QC == 0, "epilogue mapping");
   const bool vecC = p.vecC;
+  // plane output: a thread takes two adjacent float4 (8 columns) so each plane is
+  // stored as one 16-B vector (half the store instructions of 8-B stores): fc1 1-3 %
+  // faster; the spectral x6c epilogues were 5 % slower with it (PAIRS = false there)
+  constexpr bool PAIR = PAIRS && (EPI & EPI_PLANES) != 0;
+  static_assert(!PAIR || QC % 2 == 0, "pairs of float4");
+  auto eidx = [&](int qq) { return PAIR ? (tid + NTHR * (qq >> 1)) * 2 + (qq & 1) : tid + NTHR * qq; };
 #pragma unroll
   for (int i = 0; i < MT; ++i) {
 #pragma unroll
@@ -183,7 +200,7 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, AccV (&acc)[M
       if constexpr ((EPI & EPI_ADD) != 0) {
 #pragma unroll
         for (int q = 0; q < QC; ++q) {
-          const int idx = tid + NTHR * (qc + q);
+          const int idx = eidx(qc + q);
           const int lr = idx / (BN / 4);
           const int row = min(m0 + (lr / RB) * WM + i * RB + (lr % RB), M - 1);
           const int col = n0 + 4 * (idx % (BN / 4));
@@ -202,21 +219,22 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, AccV (&acc)[M
       float4 cv[QC];
 #pragma unroll
       for (int q = 0; q < QC; ++q) {
-        const int idx = tid + NTHR * (qc + q);
+        const int idx = eidx(qc + q);
         cv[q] = *reinterpret_cast<const float4*>(Cs + (idx / (BN / 4)) * CS_LD + 4 * (idx % (BN / 4)));
       }
       float bvq[QC];
       if constexpr ((EPI & EPI_BIAS) != 0) {
 #pragma unroll
         for (int q = 0; q < QC; ++q) {
-          const int lr = (tid + NTHR * (qc + q)) / (BN / 4);
+          const int lr = eidx(qc + q) / (BN / 4);
           const int row = m0 + (lr / RB) * WM + i * RB + (lr % RB);
           bvq[q] = bias_s[min(row, M - 1) - m0];
         }
       }
+      uint2 held[3];  // PAIR: the planes of the even float4, stored with the odd one
 #pragma unroll
       for (int q = 0; q < QC; ++q) {
-        const int idx = tid + NTHR * (qc + q);
+        const int idx = eidx(qc + q);
         const int lr = idx / (BN / 4);
         const int c4 = idx % (BN / 4);
         const int row = m0 + (lr / RB) * WM + i * RB + (lr % RB);
@@ -247,11 +265,23 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, AccV (&acc)[M
           }
         }
         if constexpr ((EPI & EPI_PLANES) != 0) {
-          if (row < M) {
+          uint32_t a0, a1, a2, b0, b1, b2;
+          split2(v.x, v.y, a0, a1, a2);
+          split2(v.z, v.w, b0, b1, b2);
+          const bool full8 = PAIR && p.cx16 && col - 4 * (q & 1) + 7 < N;  // the pair's 8 columns
+          if ((q & 1) == 0 && full8) {
+            held[0] = make_uint2(a0, b0);
+            held[1] = make_uint2(a1, b1);
+            held[2] = make_uint2(a2, b2);
+          } else if (full8) {
+            if (row < M) {
+              unsigned short* dst = p.Cx + blockIdx.z * p.sC + (int64_t)row * ldc + col - 4;
+              *reinterpret_cast<uint4*>(dst) = make_uint4(held[0].x, held[0].y, a0, b0);
+              *reinterpret_cast<uint4*>(dst + p.sCxp) = make_uint4(held[1].x, held[1].y, a1, b1);
+              *reinterpret_cast<uint4*>(dst + 2 * p.sCxp) = make_uint4(held[2].x, held[2].y, a2, b2);
+            }
+          } else if (row < M) {
             unsigned short* dst = p.Cx + blockIdx.z * p.sC + (int64_t)row * ldc + col;
-            uint32_t a0, a1, a2, b0, b1, b2;
-            split2(v.x, v.y, a0, a1, a2);
-            split2(v.z, v.w, b0, b1, b2);
             if (col + 3 < N) {  // ldc % 4 == 0 (checked on the host): 8-B aligned
               *reinterpret_cast<uint2*>(dst) = make_uint2(a0, b0);
               *reinterpret_cast<uint2*>(dst + p.sCxp) = make_uint2(a1, b1);

@@ -390,6 +390,8 @@ int gemm_x6(GemmTile tile, const float* A, const float* B, float* C, int M, int 
   p.vecB = (ldb % 4 == 0) && (sB % 4 == 0) && ((reinterpret_cast<uintptr_t>(B) & 15) == 0);
   p.Bx = epi.b_planes; p.sBxp = epi.b_plane_stride;
   p.Cx = epi.c_planes; p.sCxp = epi.c_plane_stride;
+  p.cx16 = cx16_enabled() && p.Cx && ldc % 8 == 0 && sC % 8 == 0 && p.sCxp % 8 == 0 &&
+           (reinterpret_cast<uintptr_t>(p.Cx) & 15) == 0;
   if (p.Bx)
     MSFNO_REQUIRE(ldb % 8 == 0 && sB % 8 == 0 && p.sBxp % 8 == 0 &&
                       (reinterpret_cast<uintptr_t>(p.Bx) & 15) == 0,

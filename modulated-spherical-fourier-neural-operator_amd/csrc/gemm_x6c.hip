@@ -338,8 +338,8 @@ __global__ __launch_bounds__(512) void gemm_x6c_kernel(X6CParams p) {
       q.Cx = p.Y + mat * p.y_mat;
       q.sC = p.y_b;
       q.sCxp = p.y_plane;
-      gemm_epilogue<BM, BN, EPI_PLANES, WGM, WGN>(q, acc[mat], lds, nullptr, nullptr, nullptr,
-                                                  p.co, N, p.ldy, m0, n0, 0);
+      gemm_epilogue<BM, BN, EPI_PLANES, WGM, WGN, MT, NT, 32, floatx16, false>(
+          q, acc[mat], lds, nullptr, nullptr, nullptr, p.co, N, p.ldy, m0, n0, 0);
       __syncthreads();
     }
   } else {

@@ -779,6 +779,8 @@ int gemm_x6p(const float* A, float* C, int M, int N, int K, int lda, int ldb, in
   p.Ax = Ax; p.sAxp = (int64_t)Mp * KT * TKd; p.sAx = sA == 0 ? 0 : 3 * p.sAxp; p.ldax = Mp;
   p.Bx = epi.b_planes; p.sBxp = epi.b_plane_stride;
   p.Cx = epi.c_planes; p.sCxp = epi.c_plane_stride;
+  p.cx16 = cx16_enabled() && p.Cx && ldc % 8 == 0 && sC % 8 == 0 && p.sCxp % 8 == 0 &&
+           (reinterpret_cast<uintptr_t>(p.Cx) & 15) == 0;
   p.vecC = (ldc % 4 == 0) && (sC % 4 == 0) && ((reinterpret_cast<uintptr_t>(C) & 15) == 0) &&
            (!epi.addend || ((epi.ldd % 4 == 0) && (epi.sD % 4 == 0) &&
                             ((reinterpret_cast<uintptr_t>(epi.addend) & 15) == 0)));

@@ -31,6 +31,7 @@ VARIANTS = [
     {"MSFNO_GEMM": "f32"},
     {"MSFNO_CONTRACT_DMA": "0"},
     {"MSFNO_CONTRACT_NS": "3"},
+    {"MSFNO_CX16": "0"},
 ]
 
 
