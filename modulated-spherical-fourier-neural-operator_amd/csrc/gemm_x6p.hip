@@ -131,12 +131,15 @@ __global__ void split_planes_kernel(const float* __restrict__ x, unsigned short*
   }
 }
 
-template <int EPI, int NSTAGE = 3, int WAVES = 8>
+template <int EPI, int NSTAGE = 3, int WAVES = 8, int BNT = 256>
 __global__ __launch_bounds__(64 * WAVES) void gemm_x6p_kernel(GemmParams p) {
-  constexpr int BM = X6P_BM, BN = X6P_BN, BK = X6P_BK;
-  // 8 waves as 4 x 2 (wave 64 x 128), or 4 waves as 2 x 2 (wave 128 x 128, 256
-  // accumulator registers: one wave per SIMD)
-  constexpr int WGM = WAVES == 8 ? 4 : 2, WGN = 2, NTHR = 64 * WAVES;
+  constexpr int BM = X6P_BM, BN = BNT, BK = X6P_BK;
+  // 256 x 256 tiles: 8 waves as 4 x 2 (wave 64 x 128), or 4 waves as 2 x 2 (wave
+  // 128 x 128, 256 accumulator registers: one wave per SIMD);
+  // 256 x 128 tiles: 4 waves as 4 x 1 (wave 64 x 128), 72-KB ring: two workgroups per
+  // CU, so one's epilogue stores overlap the other's main loop
+  static_assert(BNT == 256 || (BNT == 128 && WAVES == 4), "tile / waves");
+  constexpr int WGM = (BNT == 128 || WAVES == 8) ? 4 : 2, WGN = WAVES / WGM, NTHR = 64 * WAVES;
   constexpr int WM = BM / WGM, WN = BN / WGN;
   constexpr int MT = WM / 32, NT = WN / 32;
   constexpr int A_PLANE = BM * BK;             // bf16 elements
@@ -146,9 +149,12 @@ __global__ __launch_bounds__(64 * WAVES) void gemm_x6p_kernel(GemmParams p) {
   constexpr int EPI_BYTES = 32 * WGM * (BN + 8) * 4;
   constexpr int LDS_BYTES = RING_BYTES > EPI_BYTES ? RING_BYTES : EPI_BYTES;
   constexpr bool HAS_BIAS = (EPI & EPI_BIAS) != 0;
-  constexpr int LOADS = 48 / WAVES;  // LDS-DMA wave-instructions per wave per k-tile
-  constexpr int QA = LOADS / 2;       // A (and B) pieces per wave
-  static_assert(STAGE * 2 == 48 * 1024 && LOADS * WAVES * 1024 == STAGE * 2, "stage = 48 x 1 KB");
+  constexpr int BPIECES = 3 * BK * BN * 2 / 1024;  // 1-KB B pieces per stage (24 or 12)
+  constexpr int QA = 24 / WAVES;                    // A pieces per wave
+  constexpr int QB = BPIECES / WAVES;               // B pieces per wave
+  constexpr int LOADS = QA + QB;  // LDS-DMA wave-instructions per wave per k-tile
+  constexpr int RPP = 1024 / (BN * 2);              // B rows per piece (2 or 4)
+  static_assert(LOADS * WAVES * 1024 == STAGE * 2 && QB * WAVES == BPIECES, "stage pieces");
   // one LDS object only: a second __shared__ array makes hipcc drain the DMA
   // (vmcnt(0)) before the first ds_read of every k-tile
   __shared__ __attribute__((aligned(16))) char lds_raw[LDS_BYTES + (HAS_BIAS ? BM * 4 : 0)];
@@ -177,13 +183,13 @@ __global__ __launch_bounds__(64 * WAVES) void gemm_x6p_kernel(GemmParams p) {
     for (int r = tid; r < BM; r += NTHR) bias_s[r] = bias[min(m0 + r, M - 1)];
   }
 
-  // ---- LDS-DMA sources: per wave QA A pieces and QA B pieces of 1 KB per k-tile
+  // ---- LDS-DMA sources: per wave QA A pieces and QB B pieces of 1 KB per k-tile
   // A piece a = wave + WAVES q (q < QA): plane a / 8, rows 32 (a % 8) .. + 31
-  // B piece b = wave + WAVES q (q < QA): plane b / 8, rows 2 (b % 8), 2 (b % 8) + 1
+  // B piece b = wave + WAVES q (q < QB): plane b / (16 / RPP), k rows RPP (b % (16 / RPP)) ..
   const unsigned short* a_src[QA];
-  int a_dst[QA], b_dst[QA];
-  int64_t b_row_off[QA];
-  int b_col[QA], b_row[QA];
+  int a_dst[QA], b_dst[QB];
+  int64_t b_row_off[QB];
+  int b_col[QB], b_row[QB];
 #pragma unroll
   for (int q = 0; q < QA; ++q) {
     const int a = wave + WAVES * q;
@@ -192,14 +198,19 @@ __global__ __launch_bounds__(64 * WAVES) void gemm_x6p_kernel(GemmParams p) {
     const int h = (lane & 1) ^ ((m >> 3) & 1);
     a_src[q] = Ax + (int64_t)pl * p.sAxp + (int64_t)(m0 + m) * 16 + 8 * h;
     a_dst[q] = pl * A_PLANE + mb * 32 * BK;
-    const int row = 2 * mb + (lane >> 5);
-    const int gu = (lane & 31) ^ (4 * (row & 3));
+  }
+#pragma unroll
+  for (int q = 0; q < QB; ++q) {
+    const int b = wave + WAVES * q;
+    const int pl = b / (16 / RPP), rb = b % (16 / RPP);
+    const int row = RPP * rb + lane / (64 / RPP);
+    const int gu = (lane % (64 / RPP)) ^ (4 * (row & 3));
     b_row[q] = row;
     // clamp to the last full 16-B unit of the N columns (not of the row: B may start
     // mid-row, e.g. a pixel chunk of a wider plane)
     b_col[q] = min(n0 + 8 * gu, ((N + 7) & ~7) - 8);
     b_row_off[q] = (int64_t)pl * p.sBxp;
-    b_dst[q] = 3 * A_PLANE + pl * B_PLANE + mb * 2 * BN;
+    b_dst[q] = 3 * A_PLANE + pl * B_PLANE + rb * RPP * BN;
   }
   const int64_t a_kstride = (int64_t)Mp * 16;  // elements per k-tile of one A plane
   const uint32_t ring_lds = (uint32_t)(uintptr_t)(lds_void*)ring;
@@ -210,7 +221,7 @@ __global__ __launch_bounds__(64 * WAVES) void gemm_x6p_kernel(GemmParams p) {
       glds16(a_src[q] + kt * a_kstride,
              __builtin_amdgcn_readfirstlane(base + (uint32_t)(a_dst[q] * 2)));
 #pragma unroll
-    for (int q = 0; q < QA; ++q) {
+    for (int q = 0; q < QB; ++q) {
       const int kr = min(kt * BK + b_row[q], K - 1);
       glds16(Bx + b_row_off[q] + (int64_t)kr * ldb + b_col[q],
              __builtin_amdgcn_readfirstlane(base + (uint32_t)(b_dst[q] * 2)));
@@ -715,6 +726,7 @@ static bool use_x6q() {
 static int x6p_waves() {
   static const int w = [] {
     const char* e = getenv("MSFNO_X6P_WAVES");
+    if (e && std::string(e) == "4x128") return 128;  // 256 x 128 tiles, 4 waves
     return (e && e[0] == '4') ? 4 : 8;
   }();
   return w;
@@ -730,6 +742,8 @@ static void launch_x6p_e(const GemmParams& p, dim3 grid, hipStream_t s, bool q) 
     hipLaunchKernelGGL((gemm_x6q_kernel<EPI>), grid, dim3(512), 0, s, p);
   else if (stages == 2 && x6p_waves() == 4)
     hipLaunchKernelGGL((gemm_x6p_kernel<EPI, 2, 4>), grid, dim3(256), 0, s, p);
+  else if (stages == 2 && x6p_waves() == 128)
+    hipLaunchKernelGGL((gemm_x6p_kernel<EPI, 2, 4, 128>), grid, dim3(256), 0, s, p);
   else if (stages == 2)
     hipLaunchKernelGGL((gemm_x6p_kernel<EPI, 2>), grid, dim3(512), 0, s, p);
   else
@@ -789,7 +803,7 @@ int gemm_x6p(const float* A, float* C, int M, int N, int K, int lda, int ldb, in
                       (reinterpret_cast<uintptr_t>(p.Cx) & 7) == 0,
                   MSFNO_EINVAL, "gemm_x6p: C planes need ld, strides % 4 == 0 and 8-B alignment");
   p.tiles_m = Mp / X6P_BM;
-  p.tiles_n = (int)cdiv(N, q ? X6Q_BN : X6P_BN);
+  p.tiles_n = (int)cdiv(N, q ? X6Q_BN : (x6p_waves() == 128 ? 128 : X6P_BN));
   const dim3 grid(p.tiles_m * p.tiles_n, 1, batch);
   const int code = (p.bias ? EPI_BIAS : 0) | (p.addend ? EPI_ADD : 0) | (p.act == 1 ? EPI_GELU : 0) |
                    (p.relu_period ? EPI_RELU : 0) | (p.Cx ? EPI_PLANES : 0);

@@ -23,6 +23,7 @@ VARIANTS = [
     {"MSFNO_X1_PLANES": "0", "MSFNO_H_PLANES": "0"},
     {"MSFNO_X6P_STAGES": "3"},
     {"MSFNO_X6P_WAVES": "4"},
+    {"MSFNO_X6P_WAVES": "4x128"},
     {"MSFNO_X6P_MFMA": "16"},
     {"MSFNO_MLP_CHUNK": "256"},
     {"MSFNO_R2C_CFG": "8x3", "MSFNO_C2R_WV": "4"},
