@@ -54,10 +54,10 @@ SIDE_STAGES = {"inner_skip"}
 STAGE_KERNEL_X6 = {
     # fc1: x1 planes (from the inverse FFT) by LDS-DMA, bias + GELU, h written as
     # bf16x3 planes (EPI 133; two-stage DMA ring)
-    "mlp_fc1": "void msfno::gemm_x6p_kernel<133, 2, 8>(msfno::GemmParams)",
+    "mlp_fc1": "void msfno::gemm_x6p_kernel<133, 2, 8, 256>(msfno::GemmParams)",
     # fc2: h planes staged by LDS-DMA (x6p), bias + outer skip (EPI 3)
-    "mlp_fc2": "void msfno::gemm_x6p_kernel<3, 2, 8>(msfno::GemmParams)",
-    "inner_skip": "void msfno::gemm_x6p_kernel<1, 2, 8>(msfno::GemmParams)",
+    "mlp_fc2": "void msfno::gemm_x6p_kernel<3, 2, 8, 256>(msfno::GemmParams)",
+    "inner_skip": "void msfno::gemm_x6p_kernel<1, 2, 8, 256>(msfno::GemmParams)",
 }
 STAGE_KERNEL_F32 = {
     "mlp_fc1": "void msfno::gemm_f32_kernel<128, 256, 16, true, 5>(msfno::GemmParams)",
