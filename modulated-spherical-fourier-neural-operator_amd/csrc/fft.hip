@@ -711,7 +711,9 @@ __global__ __launch_bounds__(64 * WV) void fft_r2c_dma_kernel(const float* __res
 // with two 4-wave workgroups per CU beats two rows ahead with one 6-wave one
 // (0.81 vs 0.98 ms): the row FFT itself is VALU/LDS-latency bound, so waves per
 // CU matter more than bytes in flight.
-template <class CL, bool ADD, int WV, int AH, bool PL>
+// AR: the skip row is read into registers after the FFT instead of an LDS slot
+// (8.8 instead of 14.8 KB of LDS per wave: more waves per CU)
+template <class CL, bool ADD, int WV, int AH, bool PL, bool AR = false>
 __global__ __launch_bounds__(64 * WV) void fft_c2r_dma_kernel(const float2* __restrict__ in,
                                                               float* x, const float* addsrc,
                                                               float2* __restrict__ rowstats,
@@ -727,7 +729,9 @@ __global__ __launch_bounds__(64 * WV) void fft_c2r_dma_kernel(const float2* __re
   float2* tw = smem;
   float2* twN = smem + H;
   const int YS = ncy * 1024;
-  const int per = RB + AH * YS + (ADD ? AH * NCA * 1024 : 0);
+  static_assert(!AR || (ADD && AH == 1), "register skip rows: one row ahead");
+  constexpr bool ADMA = ADD && !AR;  // skip row staged by LDS-DMA
+  const int per = RB + AH * YS + (ADMA ? AH * NCA * 1024 : 0);
   char* wb = reinterpret_cast<char*>(smem + 2 * H + 2) + (size_t)w * per;
   float2* buf = reinterpret_cast<float2*>(wb);
   char* yst = wb + RB;                  // AH slots of YS
@@ -755,14 +759,14 @@ __global__ __launch_bounds__(64 * WV) void fft_c2r_dma_kernel(const float2* __re
   const int64_t row0 = (int64_t)blockIdx.x * WV + w;
   if (row0 < rows) {
     issue_y(row0, 0);
-    if constexpr (ADD) issue_a(row0, 0);
+    if constexpr (ADMA) issue_a(row0, 0);
   }
   if (AH == 2 && row0 + stride < rows) {
     issue_y(row0 + stride, 1);
-    if constexpr (ADD) issue_a(row0 + stride, 1);
+    if constexpr (ADMA) issue_a(row0 + stride, 1);
   }
   const int nst = NST + (rowstats ? 1 : 0);
-  const int na = ADD ? NCA : 0;
+  const int na = ADMA ? NCA : 0;
   int i = 0;
   for (int64_t row = row0; row < rows; row += stride, ++i) {
     const int sl = AH == 2 ? (i & 1) : 0;
@@ -788,7 +792,17 @@ __global__ __launch_bounds__(64 * WV) void fft_c2r_dma_kernel(const float2* __re
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
     if (AH == 2 ? e2 : e1) issue_y(row + AH * stride, sl);  // this Yn slot was consumed above
     CL::template run<true>(buf, nullptr, f, tw, lane);
-    if constexpr (ADD) {  // skip row landed
+    constexpr int NA4 = (N / 4 + 63) / 64;  // skip-row float4 per lane
+    float4 areg[AR ? NA4 : 1];
+    if constexpr (AR) {  // all of this lane's skip values in flight at once
+      const float4* g4 = reinterpret_cast<const float4*>(addsrc + row * N);
+#pragma unroll
+      for (int j = 0; j < NA4; ++j) {
+        const int n = lane + 64 * j;
+        areg[j] = n < N / 4 ? g4[n] : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+    }
+    if constexpr (ADMA) {  // skip row landed
       if (AH == 2)
         wait_vmcnt((e1 ? ncy + na : 0) + (i >= 1 ? nst : 0) + (e2 ? ncy : 0));
       else
@@ -812,7 +826,7 @@ __global__ __launch_bounds__(64 * WV) void fft_c2r_dma_kernel(const float2* __re
       if (n < N / 4) {
         float2 a = buf[2 * n], b = buf[2 * n + 1];
         if constexpr (ADD) {
-          const float4 r = a4[n];
+          const float4 r = AR ? areg[j < NA4 ? j : 0] : a4[n];
           a.x += r.x; a.y += r.y; b.x += r.z; b.y += r.w;
         }
         if (act == 1) {
@@ -849,7 +863,7 @@ __global__ __launch_bounds__(64 * WV) void fft_c2r_dma_kernel(const float2* __re
       if (lane == 0) rowstats[row] = make_float2(mean, q);
     }
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-    if constexpr (ADD) {
+    if constexpr (ADMA) {
       if (AH == 2 ? e2 : e1) issue_a(row + AH * stride, sl);  // this skip slot was consumed
     }
   }
@@ -1177,12 +1191,20 @@ static int launch_c2r(const FFTArgs& a, const float2* in, float* x, const float*
     if (use_fft_dma() && (2 * CL::H) % 8 == 0 && mmax <= CL::H + 1 && ncy <= 5) {
       const int rb = 2 * CL::H * 4, nca = (rb + 1023) / 1024;
       // one row ahead, 4-wave workgroups, as many per CU as the LDS holds
-      const size_t per = (size_t)rb + ncy * 1024 + (addsrc ? nca * 1024 : 0);
+      // skip rows through registers (no LDS slot): 16 waves per CU instead of 10,
+      // irfft 0.86 -> 0.74 ms at 721 x 1440.  MSFNO_C2R_AREG=0 stages them by LDS-DMA
+      static const bool areg = [] {
+        const char* e = getenv("MSFNO_C2R_AREG");
+        return !(e && e[0] == '0');
+      }();
+      // LDS per wave: row + Yn slot (+ the skip-row slot of the LDS-DMA variants)
+      const size_t per_reg = (size_t)rb + ncy * 1024;
+      const size_t per = per_reg + (addsrc ? nca * 1024 : 0);
       const size_t tw = (size_t)(2 * CL::H + 2) * sizeof(float2);
       const int wg_cu = (int)std::max<size_t>(1, (160 * 1024) / (tw + 4 * per));
       MSFNO_REQUIRE(tw + 4 * per <= 160 * 1024, MSFNO_EUNSUPPORTED, "nlon too large for the LDS FFT");
-      auto go = [&](auto kern, int WV) -> int {
-        const size_t lds = tw + WV * per;
+      auto go = [&](auto kern, int WV, size_t pw) -> int {
+        const size_t lds = tw + WV * pw;
         MSFNO_TRY(set_lds_limit(reinterpret_cast<const void*>(kern), lds));
         const int wgs = WV == 4 ? wg_cu : (int)std::max<size_t>(1, (160 * 1024) / lds);
         const int64_t grid = std::min<int64_t>(cdiv(rows, WV), dma_grid() * wgs);
@@ -1197,16 +1219,18 @@ static int launch_c2r(const FFTArgs& a, const float2* in, float* x, const float*
         const char* e = getenv("MSFNO_C2R_WV");
         return !(e && atoi(e) == 4);
       }();
-      if (planes && addsrc && wide && tw + 10 * per <= 160 * 1024)
-        MSFNO_TRY(go(fft_c2r_dma_kernel<CL, true, 10, 1, true>, 10));
+      if (planes && addsrc && areg && tw + 16 * per_reg <= 160 * 1024)
+        MSFNO_TRY(go(fft_c2r_dma_kernel<CL, true, 16, 1, true, true>, 16, per_reg));
+      else if (planes && addsrc && wide && tw + 10 * per <= 160 * 1024)
+        MSFNO_TRY(go(fft_c2r_dma_kernel<CL, true, 10, 1, true>, 10, per));
       else if (planes && addsrc)
-        MSFNO_TRY(go(fft_c2r_dma_kernel<CL, true, 4, 1, true>, 4));
+        MSFNO_TRY(go(fft_c2r_dma_kernel<CL, true, 4, 1, true>, 4, per));
       else if (planes)
-        MSFNO_TRY(go(fft_c2r_dma_kernel<CL, false, 4, 1, true>, 4));
+        MSFNO_TRY(go(fft_c2r_dma_kernel<CL, false, 4, 1, true>, 4, per));
       else if (addsrc)
-        MSFNO_TRY(go(fft_c2r_dma_kernel<CL, true, 4, 1, false>, 4));
+        MSFNO_TRY(go(fft_c2r_dma_kernel<CL, true, 4, 1, false>, 4, per));
       else
-        MSFNO_TRY(go(fft_c2r_dma_kernel<CL, false, 4, 1, false>, 4));
+        MSFNO_TRY(go(fft_c2r_dma_kernel<CL, false, 4, 1, false>, 4, per));
       return launch_check("fft_c2r_dma");
     }
   }
