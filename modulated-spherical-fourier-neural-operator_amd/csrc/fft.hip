@@ -616,7 +616,7 @@ __global__ __launch_bounds__(64 * WV) void fft_r2c_dma_kernel(const float* __res
       glds16(src + min(c * 1024 + lane * 16, RB - 16), dst + c * 1024);
   };
   if (row0 < rows) issue(row0, 0);
-  if (row0 + stride < rows) issue(row0 + stride, 1);
+  if (NS > 1 && row0 + stride < rows) issue(row0 + stride, 1);
   constexpr bool PL8 = PL && N % 8 == 0;  // 16-B plane stores (8 values per lane)
   constexpr int NSP = PL8 ? 3 * ((N / 8 + 63) / 64) : (PL ? 3 * ((N / 4 + 63) / 64) : 0);
   const int nst = (mmax + 63) / 64 + (rowstats ? 1 : 0) + NSP;  // vector stores per row
@@ -626,7 +626,9 @@ __global__ __launch_bounds__(64 * WV) void fft_r2c_dma_kernel(const float* __res
     // this row's copy has landed: count what this wave issued after it (the next
     // row's copy, if any, and the stores of the previous one or two rows)
     const bool next = row + stride < rows;
-    if constexpr (NS == 3) {
+    if constexpr (NS == 1) {  // the only slot: this row was issued after the last stores
+      wait_vmcnt(0);
+    } else if constexpr (NS == 3) {
       wait_vmcnt((i >= 2 ? nst : 0) + (next ? NCH : 0) + (i >= 1 ? nst : 0));
       if (row + 2 * stride < rows) issue(row + 2 * stride, sl == 0 ? 2 : sl - 1);
     } else {  // the next row was issued after the previous row's stores
@@ -693,7 +695,11 @@ __global__ __launch_bounds__(64 * WV) void fft_r2c_dma_kernel(const float* __res
       o[k] = make_float2(scale * X.x, scale * X.y);
     }
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-    if constexpr (NS == 3) {
+    if constexpr (NS == 1) {
+      // every read of the slot has returned: refill it with the next row
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      if (next) issue(row + stride, 0);
+    } else if constexpr (NS == 3) {
       sl = sl == 2 ? 0 : sl + 1;
     } else {
       // every read of this slot has returned: refill it with the row after next
@@ -1147,6 +1153,7 @@ static int launch_r2c(const FFTArgs& a, const float* x, float2* out, float2* row
         const char* e = getenv("MSFNO_R2C_CFG");
         if (e && std::string(e) == "8x3") return 0;
         if (e && std::string(e) == "5x2") return 2;
+        if (e && std::string(e) == "16x1") return 3;
         return 1;
       }();
       const size_t slot = (size_t)((2 * CL::H * 4 + 1023) / 1024) * 1024;
@@ -1168,6 +1175,9 @@ static int launch_r2c(const FFTArgs& a, const float* x, float2* out, float2* row
       if (cfg == 2)
         return planes ? go(fft_r2c_dma_kernel<CL, 5, true, 2>, 5, 2)
                       : go(fft_r2c_dma_kernel<CL, 5, false, 2>, 5, 2);
+      if (cfg == 3)
+        return planes ? go(fft_r2c_dma_kernel<CL, 16, true, 1>, 16, 1)
+                      : go(fft_r2c_dma_kernel<CL, 16, false, 1>, 16, 1);
       return planes ? go(fft_r2c_dma_kernel<CL, 8, true>, 8, 3)
                     : go(fft_r2c_dma_kernel<CL, 8, false>, 8, 3);
     }

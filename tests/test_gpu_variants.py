@@ -28,6 +28,7 @@ VARIANTS = [
     {"MSFNO_MLP_CHUNK": "256"},
     {"MSFNO_R2C_CFG": "8x3", "MSFNO_C2R_WV": "4", "MSFNO_C2R_AREG": "0"},
     {"MSFNO_C2R_AREG": "0"},
+    {"MSFNO_R2C_CFG": "16x1"},
     {"MSFNO_SPEC_3M": "0"},
     {"MSFNO_SIDE_STREAM": "0"},
     {"MSFNO_GEMM": "f32"},
