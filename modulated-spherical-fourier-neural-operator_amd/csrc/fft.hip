@@ -596,7 +596,11 @@ __global__ __launch_bounds__(64 * WV) void fft_r2c_dma_kernel(const float* __res
                                                               FFTArgs f, C2RPlanes pp) {
   constexpr int H = CL::H, N = 2 * H, RB = N * 4;
   constexpr int NCH = (RB + 1023) / 1024;  // DMA wave-instructions per row
-  constexpr int SLOT = NCH * 1024;
+  // slots are exactly one row (16-B multiple): the last 1-KB piece is issued by the
+  // lanes that cover the row only (a masked LDS-DMA still counts once in vmcnt).
+  // Measured 0.69-0.71 -> 0.67-0.68 ms against 1-KB-rounded slots at 721 x 1440
+  // (13 waves, which the smaller slots would allow, were slower: 0.71 ms)
+  constexpr int SLOT = (RB + 15) / 16 * 16;
   // NS row slots per wave: NS - 1 rows in flight while one is transformed
   extern __shared__ float2 smem[];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -613,7 +617,8 @@ __global__ __launch_bounds__(64 * WV) void fft_r2c_dma_kernel(const float* __res
     const uint32_t dst = lds_addr(slots + sl * SLOT);
 #pragma unroll
     for (int c = 0; c < NCH; ++c)
-      glds16(src + min(c * 1024 + lane * 16, RB - 16), dst + c * 1024);
+      if (c + 1 < NCH || c * 1024 + lane * 16 < RB)
+        glds16(src + min(c * 1024 + lane * 16, RB - 16), dst + c * 1024);
   };
   if (row0 < rows) issue(row0, 0);
   if (NS > 1 && row0 + stride < rows) issue(row0 + stride, 1);
@@ -1156,7 +1161,7 @@ static int launch_r2c(const FFTArgs& a, const float* x, float2* out, float2* row
         if (e && std::string(e) == "16x1") return 3;
         return 1;
       }();
-      const size_t slot = (size_t)((2 * CL::H * 4 + 1023) / 1024) * 1024;
+      const size_t slot = (size_t)(2 * CL::H * 4 + 15) / 16 * 16;  // = the kernel's SLOT
       auto go = [&](auto kern, int WV, int NS) -> int {
         const size_t lds = (size_t)(2 * CL::H + 2) * sizeof(float2) + WV * NS * slot;
         MSFNO_REQUIRE(lds <= 160 * 1024, MSFNO_EUNSUPPORTED, "nlon too large for the LDS FFT");
