@@ -598,8 +598,8 @@ __global__ __launch_bounds__(64 * WV) void fft_r2c_dma_kernel(const float* __res
   constexpr int NCH = (RB + 1023) / 1024;  // DMA wave-instructions per row
   // slots are exactly one row (16-B multiple): the last 1-KB piece is issued by the
   // lanes that cover the row only (a masked LDS-DMA still counts once in vmcnt).
-  // Measured 0.69-0.71 -> 0.67-0.68 ms against 1-KB-rounded slots at 721 x 1440
-  // (13 waves, which the smaller slots would allow, were slower: 0.71 ms)
+  // Same time as 1-KB-rounded slots at 721 x 1440 (0.718 vs 0.719 ms, same box); 13
+  // waves, which the smaller slots would allow, were slower
   constexpr int SLOT = (RB + 15) / 16 * 16;
   // NS row slots per wave: NS - 1 rows in flight while one is transformed
   extern __shared__ float2 smem[];
