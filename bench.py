@@ -7,12 +7,19 @@ FiLM on — over one synthetic 721x1440x256 field per GPU (x ~ N(0,1), seed 0),
 lmax=360/mmax=361 equiangular SHT with the reference's ×1e5 rescale, random
 init weights of that architecture (reference init recipe, seed 1).
 
-Multi-GPU (torchrun, one process per GPU), "scaling": "weak" in both modes:
-  --parallel replicas (default): each rank runs its own field batch through the
-      block; no data-path collective.
-  --parallel latband: one batch of batch*N fields is latitude-band sharded over
-      the N ranks: two RCCL all-to-alls and two small
-      all-gathers per block forward (msfno_amd.sfno.LatBandBlock).
+Multi-GPU: one process per GPU.  ``python bench.py --gpus N`` (N > 1, no
+WORLD_SIZE in the environment) starts the N rank processes itself before any
+GPU call (children, never exec; the reference's own launch is mp.spawn,
+MSFNO/main.py:1149-1156); under torchrun the ranks come from the environment and
+--gpus must equal WORLD_SIZE.  "scaling": "weak" (batch fields per GPU):
+  --parallel latband (the N>1 default): ONE batch of batch*N fields (N=8: the
+      config-4 batch of 8) is latitude-band sharded over the N ranks
+      (SURVEY.md §8e): two RCCL all-to-alls and two small all-gathers per block
+      forward (msfno_amd.sfno.LatBandBlock), pipelined over --band-chunks
+      sub-batches so one sub-batch's exchange overlaps another's compute.  The
+      replica number (below) is printed beside it as the comm-free upper bound.
+  --parallel replicas: each rank runs its own field batch through the
+      whole-field block; no data-path collective.
 The timed region is bracketed by barrier + synchronize and the max over ranks
 is used.
 
@@ -110,7 +117,7 @@ def pmc_traffic(stage):
 
 def parse(argv=None):
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=1, help="GPUs = rank processes (one per GPU)")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=1, help="fields per GPU per step")
@@ -120,7 +127,9 @@ def parse(argv=None):
     ap.add_argument("--nlon", type=int, default=1440)
     ap.add_argument("--lmax", type=int, default=360)
     ap.add_argument("--cpu-baseline", type=int, default=1, help="time the oracle on CPU (rank 0, N=1)")
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="oracle threads (0: the physical cores this job may use, see host_cores)")
+    ap.add_argument("--cpu-reps", type=int, default=3, help="timed oracle reps after 1 warm-up (median)")
     ap.add_argument("--stages", action="store_true", help="print per-stage timings to stderr")
     ap.add_argument("--workload", default="block", choices=["block", "net"],
                     help="block: one SFNO-Block forward per field (config 2, the headline); "
@@ -129,9 +138,16 @@ def parse(argv=None):
     ap.add_argument("--graph", type=int, default=-1,
                     help="capture one step in a HIP graph and replay it (default: on for "
                          "--workload net, off for block)")
-    ap.add_argument("--parallel", default="replicas", choices=["replicas", "latband"],
-                    help="N>1: independent replicas (one field batch per GPU) or one batch of "
-                         "batch*N fields latitude-band sharded over the N GPUs (RCCL all-to-all)")
+    ap.add_argument("--parallel", default="auto", choices=["auto", "replicas", "latband"],
+                    help="N>1: one batch of batch*N fields latitude-band sharded over the N GPUs "
+                         "(RCCL all-to-all; the auto default) or independent replicas")
+    ap.add_argument("--band-chunks", type=int, default=0,
+                    help="latband: sub-batches pipelined so exchanges overlap compute "
+                         "(0: one sub-batch per field pair, at most 4)")
+    ap.add_argument("--replicas-check", type=int, default=1,
+                    help="latband, N>1: also time the replica mode (comm-free upper bound)")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launcher / process-group check only (gloo, no GPU): ranks report in")
     return ap.parse_args(argv)
 
 
@@ -211,12 +227,56 @@ def build_block(args, dev):
     return blk.eval().to(dev), p, cfg
 
 
+def host_cores():
+    """(threads to use, description) for the CPU baseline: the physical cores this
+    process may run on (affinity mask ÷ SMT, cgroup quota) — capped by the job's CPU
+    share when the launcher sets one (OMP_NUM_THREADS; 16 per GPU on the GPU box)."""
+    import subprocess
+    info = {}
+    try:
+        out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
+        for line in out.splitlines():
+            k, _, v = line.partition(":")
+            info[k.strip()] = v.strip()
+    except (OSError, subprocess.SubprocessError):
+        pass
+
+    def num(key, default):
+        try:
+            return int(info.get(key, default))
+        except ValueError:
+            return default
+    logical = len(os.sched_getaffinity(0))
+    tpc = max(1, num("Thread(s) per core", 1))
+    physical = num("Core(s) per socket", 0) * num("Socket(s)", 1) or logical // tpc
+    usable = max(1, min(physical, logical // tpc))
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()
+        if q != "max":
+            quota = max(1, int(int(q) / int(per)))
+            usable = min(usable, quota)
+    except (OSError, ValueError):
+        pass
+    share = os.environ.get("OMP_NUM_THREADS")
+    threads = usable
+    if share and share.isdigit() and int(share) > 0:
+        threads = min(usable, int(share))
+    desc = (f"{info.get('Model name', 'unknown CPU')}; host {physical} physical cores "
+            f"({logical} logical CPUs in the affinity mask, {tpc} threads/core"
+            + (f", cgroup quota {quota} CPUs" if quota else "")
+            + (f", job CPU share OMP_NUM_THREADS={share}" if share else "") + ")")
+    return threads, desc
+
+
 def cpu_baseline(args, p, cfg):
-    """Oracle (torch-CPU restatement of the reference block) on a bounded sample.
-    The linear filter at C > 64 is timed at C = 32 (its 34 GB weight at C = 256 does
-    not fit the sample budget)."""
+    """Oracle (torch-CPU restatement of the reference block) on a bounded sample:
+    1 warm-up + --cpu-reps timed fields, median.  The linear filter
+    at C > 64 is timed at C = 32 (its 34 GB weight at C = 256 does not fit the
+    sample budget)."""
     from oracle import sfno_ref
-    threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
+    auto, desc = host_cores()
+    threads = args.cpu_threads if args.cpu_threads > 0 else auto
     torch.set_num_threads(threads)
     C, nlat, nlon, lmax = args.C, args.nlat, args.nlon, args.lmax
     note = ""
@@ -229,15 +289,21 @@ def cpu_baseline(args, p, cfg):
     x = torch.randn(1, C, nlat, nlon, generator=g)
     gamma = 0.1 * torch.randn(1, C, generator=g)
     beta = 0.1 * torch.randn(1, C, generator=g)
+    times = []
     with torch.no_grad():
         sfno_ref.block_forward(p, x, sht, isht, cfg, gamma, beta, 1.0)   # warm-up
-        t0 = time.perf_counter()
-        sfno_ref.block_forward(p, x, sht, isht, cfg, gamma, beta, 1.0)
-        dt = time.perf_counter() - t0
+        for _ in range(max(1, args.cpu_reps)):
+            t0 = time.perf_counter()
+            sfno_ref.block_forward(p, x, sht, isht, cfg, gamma, beta, 1.0)
+            times.append(time.perf_counter() - t0)
+    times.sort()
+    dt = times[len(times) // 2]
     return {"value": 1.0 / dt, "unit": "fields/s", "cores": threads, "kind": "port",
-            "sample": f"1 field ({nlat}x{nlon}x{C}, lmax={lmax}, {args.filter} filter) after 1 "
-                      f"warm-up; oracle/sfno_ref.py torch-CPU restatement, {threads} threads; "
-                      f"{dt:.2f} s/field{note}"}
+            "cpu": desc,
+            "sample": f"median of {len(times)} fields ({nlat}x{nlon}x{C}, lmax={lmax}, "
+                      f"{args.filter} filter) after 1 warm-up; oracle/sfno_ref.py torch-CPU "
+                      f"restatement, {threads} threads; s/field "
+                      f"{', '.join(f'{t:.2f}' for t in times)}{note}"}
 
 
 def run_net(args, rank, world, dev, dist, backend):
@@ -320,12 +386,159 @@ def run_net(args, rank, world, dev, dist, backend):
         torch.distributed.destroy_process_group()
 
 
+def launch(args):
+    """``--gpus N`` (N > 1) without WORLD_SIZE: start the N rank processes (one per
+    GPU, RANK/LOCAL_RANK/WORLD_SIZE/MASTER_* in their environment) as children of
+    this process, which never touches the GPU.  Returns the first failing exit code
+    (the other ranks are then terminated) or 0."""
+    import socket
+    import subprocess
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    procs = []
+    for r in range(args.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus),
+                   LOCAL_WORLD_SIZE=str(args.gpus), GROUP_RANK="0",
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:],
+                                      env=env))
+    rc = 0
+    alive = list(procs)
+    while alive:
+        for pr in list(alive):
+            r = pr.poll()
+            if r is None:
+                continue
+            alive.remove(pr)
+            if r != 0 and rc == 0:
+                rc = r if r > 0 else 128 - r
+                for q in alive:
+                    q.terminate()
+        time.sleep(0.1)
+    return rc
+
+
+def _max_over_ranks(v, dist, dev, backend):
+    if not dist:
+        return v
+    t = torch.tensor([v], device=dev if backend == "nccl" else "cpu", dtype=torch.float64)
+    torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+    return t.item()
+
+
+def timed(step, args, dist, dev, backend):
+    """W untimed warm-up steps, then exactly K steps between barrier + synchronize
+    on both sides; returns (last output, max-over-ranks seconds, stage profile)."""
+    from msfno_amd import _native as N
+
+    def barrier():
+        if dist:
+            torch.distributed.barrier()
+    y = None
+    for _ in range(args.warmup):
+        y = step()
+    torch.cuda.synchronize()
+    N.profile_collect()  # discard
+    N.profile_enable(True)
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        y = step()
+    torch.cuda.synchronize()
+    barrier()
+    t1 = time.perf_counter()
+    N.profile_enable(False)
+    stages = N.profile_collect()
+    return y, _max_over_ranks(t1 - t0, dist, dev, backend), stages
+
+
+# stage spans that are not kernels: waits on a collective (latitude-band exchange)
+NON_KERNEL_STAGES = {"band_exchange"}
+
+
+def roofline(stages, args, B, C, rows, mset):
+    """Roofline of the dominant kernel: the main-stream stage with the largest device
+    time (the inner-skip GEMM overlaps the SHT on a side stream: its event span is not
+    a kernel duration, so it is not eligible)."""
+    mmax = args.lmax + 1
+    hid = shid = 2 * C
+    side = os.environ.get("MSFNO_SIDE_STREAM", "1") != "0"
+    elig = {k: v for k, v in stages.items()
+            if not (side and k in SIDE_STAGES) and k not in NON_KERNEL_STAGES
+            and stage_work(k, B, C, args.nlat, args.nlon, args.lmax, mmax, hid, shid,
+                           rows, mset) is not None}
+    if not elig:
+        return None
+    name, (tot_ms, cnt) = max(elig.items(), key=lambda kv: kv[1][0])
+    avg_s = tot_ms / cnt / 1000.0
+    kind, amount = stage_work(name, B, C, args.nlat, args.nlon, args.lmax, mmax, hid, shid,
+                              rows, mset)
+    whole = rows is None and mset is None
+    tr, tr_src = pmc_traffic(name) if (B == 1 and C == 256 and args.nlat == 721 and whole
+                                        and args.filter == "non-linear") else (None, None)
+    if kind == "mfma":
+        ach = amount / avg_s / 1e12
+        peak, engine = mfma_peak(name)
+        return {"bound": "mfma", "achieved": round(ach, 2), "peak": round(peak, 1),
+                "unit": "TFLOP/s", "frac": round(ach / peak, 4), "traffic": tr,
+                "traffic_source": (f"stored PMC profile {tr_src} (same kernel and shape; not "
+                                   "measured in this run)") if tr_src else None,
+                "kernel": name, "engine": engine, "avg_ms": round(avg_s * 1e3, 4),
+                "work_per_launch": f"{amount / 1e9:.2f} GFLOP"}
+    ach = amount / avg_s / 1e9
+    return {"bound": "hbm", "achieved": round(ach, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+            "frac": round(ach / PEAK_HBM_GBS, 4), "traffic": tr,
+            "traffic_source": (f"stored PMC profile {tr_src}" if tr_src else None),
+            "kernel": name, "avg_ms": round(avg_s * 1e3, 4),
+            "work_per_launch": f"{amount / 1e9:.3f} GB"}
+
+
+def print_stages(stages, args, B, C, rows, mset, tag=""):
+    mmax = args.lmax + 1
+    for k, (ms, c) in sorted(stages.items(), key=lambda kv: -kv[1][0]):
+        w = stage_work(k, B, C, args.nlat, args.nlon, args.lmax, mmax, 2 * C, 2 * C, rows, mset)
+        extra = ""
+        if w:
+            a = w[1] / (ms / c / 1e3)
+            if w[0] == "mfma":
+                pk = mfma_peak(k)[0]
+                extra = f" {a / 1e12:.1f} TFLOP/s ({100 * a / 1e12 / pk:.0f}% of {pk:.0f})"
+            else:
+                extra = f" {a / 1e9:.0f} GB/s ({100 * a / 1e9 / PEAK_HBM_GBS:.0f}%)"
+        print(f"  {tag}stage {k:18s} {ms / c:8.3f} ms x{c}{extra}", file=sys.stderr)
+
+
+def dry_run(rank, world):
+    """Process-group check without a GPU (tests/test_bench_launch.py): gloo."""
+    import socket
+    import torch.distributed as td
+    td.init_process_group("gloo")
+    seen = [None] * world
+    td.all_gather_object(seen, (rank, socket.gethostname(), os.getpid()))
+    if rank == 0:
+        print(json.dumps({"dry_run": True, "n_gpus": world, "world_size": td.get_world_size(),
+                          "ranks_seen": len({r for r, _, _ in seen}),
+                          "pids": sorted({p for _, _, p in seen})}), flush=True)
+    td.destroy_process_group()
+
+
 def main():
     args = parse()
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        # one process per GPU, started here before anything touches the GPU
+        sys.exit(launch(args))
     rank = int(os.environ.get("RANK", "0"))
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    world = int(env_world or "1")
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gpus != world:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
     dist = world > 1
+    if args.dry_run:
+        return dry_run(rank, world) if dist else print(json.dumps(
+            {"dry_run": True, "n_gpus": 1, "world_size": 1, "ranks_seen": 1}))
     # rehearsal knobs for a one-GPU box (never used by the driver's runs):
     # MSFNO_BENCH_BACKEND=gloo and MSFNO_BENCH_SHARE_GPU=1 put every rank on cuda:0
     backend = os.environ.get("MSFNO_BENCH_BACKEND", "nccl")
@@ -338,17 +551,30 @@ def main():
             td.init_process_group("nccl", device_id=torch.device("cuda", gpu))
         else:
             td.init_process_group(backend)
+        assert td.get_world_size() == world == args.gpus
     dev = torch.device("cuda", gpu)
     torch.cuda.set_device(dev)
 
-    from msfno_amd import _native as N
+    ranks_seen, gpus_seen = 1, 1
+    if dist:
+        import socket
+        props = torch.cuda.get_device_properties(dev)
+        ident = (rank, socket.gethostname(), str(getattr(props, "uuid", gpu)))
+        seen = [None] * world
+        torch.distributed.all_gather_object(seen, ident)
+        ranks_seen = len({r for r, _, _ in seen})
+        gpus_seen = len({(h, u) for _, h, u in seen})
 
     if args.workload == "net":
         return run_net(args, rank, world, dev, dist, backend)
     blk, p, cfg = build_block(args, dev)
     C = args.C
-    band = args.parallel == "latband"
+    parallel = args.parallel
+    if parallel == "auto":
+        parallel = "latband" if dist else "replicas"
+    band = parallel == "latband"
     rows = mset = None
+    chunks = 1
     if band:
         # one batch of batch*N fields, each rank holding its latitude band of every field
         from msfno_amd.sfno import LatBandBlock, TorchComm
@@ -363,9 +589,10 @@ def main():
         gamma = 0.1 * torch.randn(B, C, generator=gd, device=dev)
         beta = 0.1 * torch.randn(B, C, generator=gd, device=dev)
         comm = TorchComm() if dist else None
+        chunks = args.band_chunks if args.band_chunks > 0 else max(1, min(4, B // 2))
 
         def step():
-            return shard(x, gamma, beta, 1.0, comm=comm)
+            return shard(x, gamma, beta, 1.0, comm=comm, chunks=chunks)
     else:
         B = args.batch
         g = torch.Generator().manual_seed(1000 * rank)
@@ -376,80 +603,50 @@ def main():
         def step():
             return blk(x, gamma, beta, 1.0)
 
-    def barrier():
-        if dist:
-            torch.distributed.barrier()
-
     with torch.no_grad():
-        for _ in range(args.warmup):
-            y = step()
-        torch.cuda.synchronize()
-        N.profile_collect()  # discard
-        N.profile_enable(True)
-        barrier()
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        for _ in range(args.steps):
-            y = step()
-        torch.cuda.synchronize()
-        barrier()
-        t1 = time.perf_counter()
-        N.profile_enable(False)
-        stages = N.profile_collect()
-    elapsed = t1 - t0
-    if dist:
-        t = torch.tensor([elapsed], device=dev if backend == "nccl" else "cpu",
-                         dtype=torch.float64)
-        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
-        elapsed = t.item()
+        y, elapsed, stages = timed(step, args, dist, dev, backend)
     assert torch.isfinite(y).all()
-
     fields = (B if band else world * B) * args.steps
     value = fields / elapsed
     ms_per_step = 1000.0 * elapsed / args.steps
+    # work per launch: a latitude-band step launches every kernel once per sub-batch
+    B_launch = B / chunks if band else B
+    roof = roofline(stages, args, B_launch, C, rows, mset)
+    if args.stages:
+        print_stages(stages, args, B_launch, C, rows, mset, tag=f"rank{rank} ")
 
-    mmax = args.lmax + 1
-    hid = shid = 2 * C
-    # dominant kernel = main-stream stage with the largest device time in the timed region
-    # (the inner-skip GEMM overlaps the SHT on a side stream: its event span is not a
-    # kernel duration, so it is not eligible)
-    side = os.environ.get("MSFNO_SIDE_STREAM", "1") != "0"
-    elig = {k: v for k, v in stages.items() if not (side and k in SIDE_STAGES)}
-    dom = max(elig.items(), key=lambda kv: kv[1][0]) if elig else None
-    roof = None
-    if dom is not None:
-        name, (tot_ms, cnt) = dom
-        avg_s = tot_ms / cnt / 1000.0
-        w = stage_work(name, B, C, args.nlat, args.nlon, args.lmax, mmax, hid, shid, rows, mset)
-        tr, tr_src = pmc_traffic(name) if (B == 1 and C == 256 and args.nlat == 721 and not band
-                                            and args.filter == "non-linear") else (None, None)
-        if w is not None:
-            kind, amount = w
-            if kind == "mfma":
-                ach = amount / avg_s / 1e12
-                peak, engine = mfma_peak(name)
-                roof = {"bound": "mfma", "achieved": round(ach, 2), "peak": round(peak, 1),
-                        "unit": "TFLOP/s", "frac": round(ach / peak, 4),
-                        "traffic": tr, "traffic_source": tr_src, "kernel": name,
-                        "engine": engine, "avg_ms": round(avg_s * 1e3, 4)}
-            else:
-                ach = amount / avg_s / 1e9
-                roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": PEAK_HBM_GBS,
-                        "unit": "GB/s", "frac": round(ach / PEAK_HBM_GBS, 4), "traffic": tr,
-                        "traffic_source": tr_src,
-                        "kernel": name, "avg_ms": round(avg_s * 1e3, 4)}
-    if args.stages and rank == 0:
-        for k, (ms, c) in sorted(stages.items(), key=lambda kv: -kv[1][0]):
-            w = stage_work(k, B, C, args.nlat, args.nlon, args.lmax, mmax, hid, shid, rows, mset)
-            extra = ""
-            if w:
-                a = w[1] / (ms / c / 1e3)
-                if w[0] == "mfma":
-                    pk = mfma_peak(k)[0]
-                    extra = f" {a / 1e12:.1f} TFLOP/s ({100 * a / 1e12 / pk:.0f}% of {pk:.0f})"
-                else:
-                    extra = f" {a / 1e9:.0f} GB/s ({100 * a / 1e9 / PEAK_HBM_GBS:.0f}%)"
-            print(f"  stage {k:18s} {ms / c:8.3f} ms x{c}{extra}", file=sys.stderr)
+    replicas = None
+    if band and dist and args.replicas_check:
+        # the comm-free upper bound: every rank runs its own batch fields whole
+        del x, shard
+        torch.cuda.empty_cache()
+        Br = args.batch
+        gr = torch.Generator(device=dev).manual_seed(1000 * rank)
+        xr = torch.randn(Br, C, args.nlat, args.nlon, generator=gr, device=dev)
+        gr_, br_ = gamma[:Br].contiguous(), beta[:Br].contiguous()
+
+        def rstep():
+            return blk(xr, gr_, br_, 1.0)
+        with torch.no_grad():
+            _, rel, rstages = timed(rstep, args, dist, dev, backend)
+        replicas = {"value": round(world * Br * args.steps / rel, 3), "unit": "fields/s",
+                    "ms_per_step": round(1000.0 * rel / args.steps, 3),
+                    "parallelism": f"replicas{world}", "global_batch": world * Br}
+        del xr
+
+    per_rank = None
+    band_info = None
+    if dist:
+        ex = stages.get("band_exchange")
+        mine = {"rank": rank, "kernel": roof and roof["kernel"], "avg_ms": roof and roof["avg_ms"],
+                "frac": roof and roof["frac"],
+                "exchange_wait_ms_per_step": round(ex[0] / args.steps, 3) if ex else None,
+                "rows": rows, "m_count": len(mset) if mset is not None else None}
+        per_rank = [None] * world
+        torch.distributed.all_gather_object(per_rank, mine)
+        if band:
+            band_info = {"chunks": chunks, "rows_per_rank": [q["rows"] for q in per_rank],
+                         "m_per_rank": [q["m_count"] for q in per_rank]}
 
     cpu = None
     if rank == 0 and world == 1 and args.cpu_baseline:
@@ -477,9 +674,17 @@ def main():
                        "filter": args.filter,
                        "parallelism": (f"latband{world}" if band else
                                        (f"replicas{world}" if world > 1 else "single"))},
+            "ranks_seen": ranks_seen,
+            "gpus_seen": gpus_seen,
             "roofline": roof,
             "cpu_baseline": cpu,
         }
+        if band_info:
+            out["latband"] = band_info
+        if per_rank:
+            out["per_rank"] = per_rank
+        if replicas:
+            out["replicas_upper_bound"] = replicas
         print(json.dumps(out), flush=True)
     if dist:
         torch.distributed.destroy_process_group()

@@ -220,8 +220,16 @@ int msfno_mlp_backward_input(const msfno_mlp_desc* d, const float* x, const floa
  *   [all_gather stats_local -> stats_all]              (norm1)
  *   stage 4  norm1 (+FiLM) -> MLP (+outer skip)            -> out_local
  *
- * Same-grid blocks only (inner/outer skips need equal input/output grids);
- * non-linear filter (the reference default); at most 64 ranks.
+ * Resampling blocks (different input and output grids, sfnonet.py:573-614: the
+ * first block 721x1440 -> 120x240 and the last one back) take a second row
+ * partition for the output grid (msfno_band_plan_create2); skips then must be
+ * absent, as in the reference.  Both filters: the linear filter's per-mode
+ * weight is sharded with the m-set (msfno_band_linear_modes), so each rank
+ * streams only its modes' slice.  At most 64 ranks.
+ *
+ * Several sub-batches of one forward may be in flight between stage 0 and
+ * stage 3 at once (their exchanges overlapping each other's compute): give each
+ * a distinct io.slot (0..63), its own workspace and its own exchange buffers.
  * ------------------------------------------------------------------------- */
 typedef struct msfno_band_plan_s* msfno_band_plan_t;
 
@@ -236,6 +244,20 @@ int msfno_band_exchange_counts(int world, int rank, int nlat, int mmax, const in
                                long long* recv_counts);
 int msfno_band_plan_create(int nlat, int nlon, int lmax, int mmax, int world, int rank,
                            const int* row_start, const int* m_owner, msfno_band_plan_t* plan);
+/* Resampling form: rows of the input grid (nlat_in x nlon_in, the forward
+ * transform's) in row_in, of the output grid (the inverse transform's) in row_out. */
+int msfno_band_plan_create2(int nlat_in, int nlon_in, int nlat_out, int nlon_out, int lmax,
+                            int mmax, int world, int rank, const int* row_in, const int* row_out,
+                            const int* m_owner, msfno_band_plan_t* plan);
+/* all-to-all counts (floats per peer) of this plan's rank, phase 0 / 1, R = 2*B*C */
+int msfno_band_plan_exchange_counts(msfno_band_plan_t plan, int R, int phase,
+                                    long long* send_counts, long long* recv_counts);
+/* Linear filter (SpectralConvS2, layers.py:336-427): the global tril indices
+ * (torch.tril_indices(lmax, mmax) order, layers.py:368) of this rank's modes, in
+ * ascending order; *count = their number T_r (modes may be NULL to query it).
+ * The descriptor's lin_w for msfno_band_block_stage is then w[:, :, modes, :],
+ * i.e. (C, C, T_r, 2) — the rank's share of the 34 GB weight at lmax 360. */
+int msfno_band_linear_modes(msfno_band_plan_t plan, long long* modes, long long* count);
 int msfno_band_plan_destroy(msfno_band_plan_t plan);
 /* full reference tables (mmax,lmax,nlat) fp32 device buffers (RealSHT.weights,
  * InverseRealSHT.pct incl. the 1e5 rescale); only this rank's m-set is kept */
@@ -252,6 +274,7 @@ typedef struct msfno_band_io {
   float* recv;              /*   of the send / recv counts (floats)             */
   double* stats_local;      /* (B*C, 3) {n, mean, M2}                           */
   const double* stats_all;  /* (world, B*C, 3), the all_gather of stats_local   */
+  int slot;                 /* in-flight sub-batch index 0..63 (inner-skip join) */
 } msfno_band_io;
 
 size_t msfno_band_workspace_size(const msfno_block_desc* d, msfno_band_plan_t plan, int B);
@@ -268,6 +291,8 @@ int msfno_band_block_stage(const msfno_block_desc* d, msfno_band_plan_t plan, in
  * ------------------------------------------------------------------------- */
 #define MSFNO_PROF_NSTAGES 32
 int msfno_profile_enable(int on);
+/* mark the start of `stage` on `stream` (bench: the wait on a collective) */
+int msfno_profile_mark(int stage, void* stream);
 /* synchronises on the recorded events, adds per-stage milliseconds / launch
  * counts since the last collect into total_ms[stage] / counts[stage] (arrays of
  * MSFNO_PROF_NSTAGES), and clears the recorded marks */

@@ -5,6 +5,8 @@
 #include <cstdlib>
 #include <cstring>
 #include <functional>
+#include <map>
+#include <mutex>
 
 #include "block.h"
 
@@ -155,7 +157,7 @@ static const char* kStageNames[MSFNO_PROF_NSTAGES] = {
     "spectral_l1", "spectral_l2", "spectral_l3", "spectral_out", "linear_gather",
     "linear_contract", "linear_scatter", "legendre_inv", "transpose_inv", "fft_inv",
     "inner_skip", "norm1_film_fold", "mlp_fc1", "mlp_fc2", "out_affine", "band_pack",
-    "band_gather", "band_scatter", "end"};
+    "band_gather", "band_scatter", "band_exchange", "end"};
 
 struct Profiler {
   bool on = false;
@@ -192,7 +194,7 @@ void prof(int stage, hipStream_t s) { g_prof.mark(stage, s); }
 // through events; capture-safe).  MSFNO_SIDE_STREAM=0 disables it.
 // ---------------------------------------------------------------------------
 
-int side_ctx(SideCtx** out) {
+int side_ctx(SideCtx** out, hipStream_t caller) {
   static int enabled = -1;
   if (enabled < 0) {
     const char* e = getenv("MSFNO_SIDE_STREAM");
@@ -200,24 +202,39 @@ int side_ctx(SideCtx** out) {
   }
   *out = nullptr;
   if (!enabled) return MSFNO_OK;
-  static std::vector<SideCtx> ctx(64);
+  // one side stream + fork/join pair per (device, caller stream): the device comes
+  // from the caller's stream (not the thread's current device), and two caller
+  // streams never share fork/join events
+  static std::mutex mu;
+  static std::map<std::pair<int, hipStream_t>, SideCtx> ctx;
   int dev = 0;
-  MSFNO_CHECK_HIP(hipGetDevice(&dev));
-  MSFNO_REQUIRE(dev >= 0 && dev < 64, MSFNO_EINVAL, "device index out of range");
-  SideCtx& c = ctx[dev];
+  if (caller) MSFNO_CHECK_HIP(hipStreamGetDevice(caller, &dev));
+  else MSFNO_CHECK_HIP(hipGetDevice(&dev));
+  std::lock_guard<std::mutex> lk(mu);
+  SideCtx& c = ctx[{dev, caller}];
   if (!c.side) {
+    int cur = 0;
+    MSFNO_CHECK_HIP(hipGetDevice(&cur));
+    if (cur != dev) MSFNO_CHECK_HIP(hipSetDevice(dev));
     // side stream at the lowest priority: the skip GEMM fills what the spectral path
     // leaves (+1 % over equal priority, measured); MSFNO_SIDE_PRIO=normal|high for A/B
     const char* pe = getenv("MSFNO_SIDE_PRIO");
     int least = 0, greatest = 0;
-    MSFNO_CHECK_HIP(hipDeviceGetStreamPriorityRange(&least, &greatest));
-    if (pe && std::string(pe) == "normal")
-      MSFNO_CHECK_HIP(hipStreamCreateWithFlags(&c.side, hipStreamNonBlocking));
-    else
-      MSFNO_CHECK_HIP(hipStreamCreateWithPriority(
-          &c.side, hipStreamNonBlocking, (pe && std::string(pe) == "high") ? greatest : least));
-    MSFNO_CHECK_HIP(hipEventCreateWithFlags(&c.fork, hipEventDisableTiming));
-    MSFNO_CHECK_HIP(hipEventCreateWithFlags(&c.join, hipEventDisableTiming));
+    hipError_t e = hipDeviceGetStreamPriorityRange(&least, &greatest);
+    if (e == hipSuccess) {
+      if (pe && std::string(pe) == "normal")
+        e = hipStreamCreateWithFlags(&c.side, hipStreamNonBlocking);
+      else
+        e = hipStreamCreateWithPriority(&c.side, hipStreamNonBlocking,
+                                        (pe && std::string(pe) == "high") ? greatest : least);
+    }
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&c.fork, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&c.join, hipEventDisableTiming);
+    if (cur != dev) (void)hipSetDevice(cur);
+    if (e != hipSuccess) {
+      set_error(std::string("side stream creation failed: ") + hipGetErrorString(e));
+      return MSFNO_EHIP;
+    }
   }
   *out = &c;
   return MSFNO_OK;
@@ -908,6 +925,24 @@ int plan_create(int nlat, int nlon, int lmax, int mmax, int inverse,
   if (e == hipSuccess) e = hipMemcpy(p->d_tab_off, p->tab_off.data(), mmax * sizeof(int64_t), hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipMemcpy(p->d_Lp, p->spec.Lp.data(), mmax * sizeof(int), hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipMemcpy(p->d_off, p->spec.off.data(), mmax * sizeof(int), hipMemcpyHostToDevice);
+  if (e == hipSuccess && mask) {
+    // tril order: row l holds m = 0..min(l, mmax-1) (torch.tril_indices(lmax, mmax),
+    // layers.py:368); keep the plan's own modes in ascending global order
+    std::vector<int> loc;
+    loc.reserve((size_t)lmax * std::min(lmax, mmax));
+    for (int l = 0; l < lmax; ++l)
+      for (int m = 0; m <= std::min(l, mmax - 1); ++m) {
+        if ((*mask)[m]) {
+          loc.push_back((int)p->lin_modes.size());
+          p->lin_modes.push_back((long long)loc.size() - 1);
+        } else {
+          loc.push_back(-1);
+        }
+      }
+    e = hipMalloc(&p->d_tril_local, std::max<size_t>(loc.size(), 1) * sizeof(int));
+    if (e == hipSuccess)
+      e = hipMemcpy(p->d_tril_local, loc.data(), loc.size() * sizeof(int), hipMemcpyHostToDevice);
+  }
   if (e != hipSuccess) {
     set_error(std::string("plan allocation failed: ") + hipGetErrorString(e));
     msfno_sht_plan_destroy(p);
@@ -1048,7 +1083,7 @@ using namespace msfno;
 extern "C" {
 
 const char* msfno_last_error(void) { return g_last_error.c_str(); }
-int msfno_abi_version(void) { return 1; }
+int msfno_abi_version(void) { return 2; }
 
 int msfno_quadrature(int nlat, int grid, double* nodes, double* weights) {
   std::vector<double> x, w;
@@ -1077,6 +1112,7 @@ int msfno_sht_plan_destroy(msfno_sht_plan_t p) {
   if (p->d_tab_off) (void)hipFree(p->d_tab_off);
   if (p->d_Lp) (void)hipFree(p->d_Lp);
   if (p->d_off) (void)hipFree(p->d_off);
+  if (p->d_tril_local) (void)hipFree(p->d_tril_local);
   if (p->d_Lpe) (void)hipFree(p->d_Lpe);
   if (p->d_desc) (void)hipFree(p->d_desc);
   if (p->tabx) (void)hipFree(p->tabx);
@@ -1277,7 +1313,7 @@ int msfno_block_forward(const msfno_block_desc* d, msfno_sht_plan_t f, msfno_sht
   };
   if (d->inner_skip == MSFNO_SKIP_LINEAR) {
     MSFNO_REQUIRE(d->skip_w, MSFNO_EINVAL, "missing inner_skip weight");
-    MSFNO_TRY(side_ctx(&side));
+    MSFNO_TRY(side_ctx(&side, s));
     if (!xpl) MSFNO_TRY(launch_skip());
   }
   if (xpl)
@@ -1306,6 +1342,12 @@ int msfno_block_forward(const msfno_block_desc* d, msfno_sht_plan_t f, msfno_sht
     MSFNO_TRY(launch_affine_rows(x1, b.sc1, b.sh1, resid, out, BC, P, 0, nullptr, 0, s));
   }
   prof(ST_END, s);
+  return MSFNO_OK;
+}
+
+int msfno_profile_mark(int stage, void* stream) {
+  MSFNO_REQUIRE(stage >= 0 && stage <= ST_END, MSFNO_EINVAL, "profile stage out of range");
+  prof(stage, (hipStream_t)stream);
   return MSFNO_OK;
 }
 

@@ -18,30 +18,45 @@
 using namespace msfno;
 
 struct msfno_band_plan_s {
-  int nlat = 0, nlon = 0, lmax = 0, mmax = 0, world = 0, rank = 0;
-  std::vector<int> row0;   // world + 1 band boundaries
-  std::vector<int> owner;  // per m, -1: no coefficients (m >= lmax)
-  std::vector<int> nm_of;  // per rank: number of owned m
-  int rows = 0;            // local latitude rows
-  int nm = 0;              // local m count
-  int mact = 0;            // global count of m with lmax - m > 0
+  // input grid (stages 0-1) and output grid (stages 3-4); equal except for the
+  // resampling blocks of a network (sfnonet.py:573-614: block 0 721x1440 -> 120x240,
+  // the last block back)
+  int nlat_in = 0, nlon_in = 0, nlat_out = 0, nlon_out = 0;
+  int lmax = 0, mmax = 0, world = 0, rank = 0;
+  std::vector<int> row_in, row_out;  // world + 1 band boundaries on each grid
+  std::vector<int> owner;            // per m, -1: no coefficients (m >= lmax)
+  std::vector<int> nm_of;            // per rank: number of owned m
+  int rows_in = 0, rows_out = 0;     // local latitude rows
+  int nm = 0;                        // local m count
+  int mact = 0;                      // global count of m with lmax - m > 0
   msfno_sht_plan_s* fwd = nullptr;
   msfno_sht_plan_s* inv = nullptr;
-  int* d_row0 = nullptr;
+  int* d_row_in = nullptr;
+  int* d_row_out = nullptr;
   int* d_perm = nullptr;
+  // inner-skip join events, one per in-flight sub-batch slot (msfno_band_io.slot):
+  // several sub-batches of one forward can be between stage 0 and stage 3 at once
+  std::vector<hipEvent_t> join;
+  bool same_grid() const { return nlat_in == nlat_out && nlon_in == nlon_out; }
 };
 
 namespace {
 
-int validate_partition(int world, int nlat, int lmax, int mmax, const int* row_start,
-                       const int* m_owner) {
-  MSFNO_REQUIRE(world >= 1 && world <= 64, MSFNO_EUNSUPPORTED, "band sharding needs 1..64 ranks");
-  MSFNO_REQUIRE(row_start && m_owner, MSFNO_EINVAL, "null partition arrays");
+int validate_rows(int world, int nlat, const int* row_start) {
+  MSFNO_REQUIRE(row_start, MSFNO_EINVAL, "null row partition");
   MSFNO_REQUIRE(row_start[0] == 0 && row_start[world] == nlat, MSFNO_EINVAL,
                 "row_start must run from 0 to nlat");
   for (int r = 0; r < world; ++r)
     MSFNO_REQUIRE(row_start[r + 1] > row_start[r], MSFNO_EINVAL,
                   "every rank needs at least one latitude row");
+  return MSFNO_OK;
+}
+
+int validate_partition(int world, int nlat, int lmax, int mmax, const int* row_start,
+                       const int* m_owner) {
+  MSFNO_REQUIRE(world >= 1 && world <= 64, MSFNO_EUNSUPPORTED, "band sharding needs 1..64 ranks");
+  MSFNO_REQUIRE(row_start && m_owner, MSFNO_EINVAL, "null partition arrays");
+  MSFNO_TRY(validate_rows(world, nlat, row_start));
   for (int m = 0; m < mmax; ++m) {
     const bool has = lmax - m > 0;
     MSFNO_REQUIRE(has ? (m_owner[m] >= 0 && m_owner[m] < world) : m_owner[m] == -1, MSFNO_EINVAL,
@@ -50,51 +65,77 @@ int validate_partition(int world, int nlat, int lmax, int mmax, const int* row_s
   return MSFNO_OK;
 }
 
+// counts (floats) per peer: phase 0 sends my input rows of q's m-set, phase 1 my
+// m-set's slabs of q's output rows
+void exchange_counts(int world, int rank, const std::vector<int>& nm, const int* row_in,
+                     const int* row_out, long long R, int phase, long long* sc, long long* rc) {
+  for (int q = 0; q < world; ++q) {
+    if (phase == 0) {
+      const long long hr = row_in[rank + 1] - row_in[rank], hq = row_in[q + 1] - row_in[q];
+      sc[q] = nm[q] * R * hr;
+      rc[q] = nm[rank] * R * hq;
+    } else {
+      const long long hr = row_out[rank + 1] - row_out[rank], hq = row_out[q + 1] - row_out[q];
+      sc[q] = nm[rank] * R * hq;
+      rc[q] = nm[q] * R * hr;
+    }
+  }
+}
+
 struct BandBufs {
-  float2* Xn;   // (BC, rows, mmax) spectra of local rows; reused as Yn
-  float2* rs;   // (BC, rows) row (mean, M2), norm0 then norm1
+  float2* Xn;   // (BC, max(rows_in, rows_out), mmax) spectra of local rows; reused as Yn
+  float2* rs;   // (BC, max rows) row (mean, M2), norm0 then norm1
   float *sc0, *sh0, *sc1, *sh1;
-  float* Xt;    // (nm, R, ldk) full-latitude slabs; reused as Yt
-  BlockBufs fb; // filter buffers (Sa, Sb, Sc, Wexp) in the local spectral layout
-  float* x1;    // (B, C, rows*nlon)
+  float* Xt;    // (nm, R, max ldk) full-latitude slabs; reused as Yt
+  BlockBufs fb; // filter buffers (Sa, Sb, Sc, Wexp / xt, yt) in the local spectral layout
+  float* x1;    // (B, C, rows_out*nlon_out)
   float *W1f, *b1f, *h;
-  // fb.x1p: (B, 3, C, rows*nlon) bf16x3 planes (x6 engine with an MLP): x for the
-  // skip GEMM (written by the rfft), then x1 for fc1 (written by the irfft)
+  // fb.x1p: (B, 3, C, P) bf16x3 planes (x6 engine with an MLP): x for the skip GEMM
+  // (written by the rfft, same-grid blocks), then x1 for fc1 (written by the irfft)
 };
 
 void carve_band(Carve& cv, BandBufs& b, const msfno_block_desc* d, const msfno_band_plan_s* p,
                 int B) {
   const int64_t C = d->C, BC = (int64_t)B * C, R = 2 * BC;
-  const int64_t Pl = (int64_t)p->rows * p->nlon;
+  const int64_t Pin = (int64_t)p->rows_in * p->nlon_in;
+  const int64_t Pout = (int64_t)p->rows_out * p->nlon_out;
+  const int64_t rmax = std::max(p->rows_in, p->rows_out);
   const SpecLayout& L = p->fwd->spec;
-  b.Xn = cv.take<float2>(BC * p->rows * p->mmax);
-  b.rs = cv.take<float2>(BC * p->rows);
+  b.Xn = cv.take<float2>(BC * rmax * p->mmax);
+  b.rs = cv.take<float2>(BC * rmax);
   b.sc0 = cv.take<float>(BC);
   b.sh0 = cv.take<float>(BC);
   b.sc1 = cv.take<float>(BC);
   b.sh1 = cv.take<float>(BC);
-  b.Xt = cv.take<float>(std::max<int64_t>((int64_t)p->nm * R * p->fwd->ldk, 4));
+  b.Xt = cv.take<float>(std::max<int64_t>((int64_t)p->nm * R * std::max(p->fwd->ldk, p->inv->ldk),
+                                          4));
   std::memset(&b.fb, 0, sizeof(b.fb));
   b.fb.Sa = cv.take<float>(R * L.ldT);
-  const int64_t Hs = d->spec_hidden;
-  b.fb.Sb = cv.take<float>(spec_hidden_floats(B, Hs, L));
-  b.fb.Sc = cv.take<float>(spec_hidden_floats(B, Hs, L));
-  for (int l = 0; l <= d->spectral_layers && l < 9; ++l) {
-    const int64_t ci = (l == 0) ? C : Hs;
-    const int64_t co = (l == d->spectral_layers) ? C : Hs;
-    b.fb.Wexp[l] = cv.take<float>(4 * ci * co);
+  if (d->filter_type == MSFNO_FILTER_NONLINEAR) {
+    const int64_t Hs = d->spec_hidden;
+    b.fb.Sb = cv.take<float>(spec_hidden_floats(B, Hs, L));
+    b.fb.Sc = cv.take<float>(spec_hidden_floats(B, Hs, L));
+    for (int l = 0; l <= d->spectral_layers && l < 9; ++l) {
+      const int64_t ci = (l == 0) ? C : Hs;
+      const int64_t co = (l == d->spectral_layers) ? C : Hs;
+      b.fb.Wexp[l] = cv.take<float>(4 * ci * co);
+    }
+    carve_spec_ws(cv, b.fb.dw, d);
+  } else {
+    b.fb.xt = cv.take<float>(std::max<int64_t>(BC * L.T * 2, 4));
+    b.fb.yt = cv.take<float>(std::max<int64_t>(BC * L.T * 2, 4));
   }
-  carve_spec_ws(cv, b.fb.dw, d);
-  b.x1 = cv.take<float>(BC * Pl);
+  b.x1 = cv.take<float>(BC * Pout);
   b.W1f = b.b1f = b.h = nullptr;
   if (d->has_mlp) {
     const int64_t Hd = d->mlp_hidden;
     b.W1f = cv.take<float>((int64_t)B * Hd * C);
     b.b1f = cv.take<float>((int64_t)B * Hd);
-    b.h = cv.take<float>(mlp_h_floats(B, Hd, Pl));
+    b.h = cv.take<float>(mlp_h_floats(B, Hd, Pout));
   }
-  b.fb.x1p = (x1_planes(d, p->inv) && Pl % 8 == 0) ? cv.take<unsigned short>(BC * 3 * Pl)
-                                                   : nullptr;
+  b.fb.x1p = (x1_planes(d, p->inv) && Pout % 8 == 0)
+                 ? cv.take<unsigned short>(BC * 3 * std::max(Pin, Pout))
+                 : nullptr;
   carve_dense_ws(cv, b.fb.dw, d, B);
 }
 
@@ -103,14 +144,28 @@ int check_band(const msfno_block_desc* d, const msfno_band_plan_s* p) {
   MSFNO_REQUIRE(p->fwd->table_loaded && p->inv->table_loaded, MSFNO_EINVAL,
                 "band plan tables not loaded");
   MSFNO_REQUIRE(d->C > 0, MSFNO_EINVAL, "C must be > 0");
-  MSFNO_REQUIRE(d->filter_type == MSFNO_FILTER_NONLINEAR, MSFNO_EUNSUPPORTED,
-                "latitude-band sharding supports the non-linear spectral filter only");
-  MSFNO_REQUIRE(d->spectral_layers >= 1 && d->spectral_layers <= 8, MSFNO_EUNSUPPORTED,
-                "spectral_layers must be in [1, 8]");
-  MSFNO_REQUIRE(d->spec_hidden > 0, MSFNO_EINVAL, "spec_hidden must be > 0");
+  if (d->filter_type == MSFNO_FILTER_NONLINEAR) {
+    MSFNO_REQUIRE(d->spectral_layers >= 1 && d->spectral_layers <= 8, MSFNO_EUNSUPPORTED,
+                  "spectral_layers must be in [1, 8]");
+    MSFNO_REQUIRE(d->spec_hidden > 0, MSFNO_EINVAL, "spec_hidden must be > 0");
+  } else {
+    MSFNO_REQUIRE(d->filter_type == MSFNO_FILTER_LINEAR, MSFNO_EUNSUPPORTED, "unknown filter_type");
+  }
   MSFNO_REQUIRE(d->outer_skip != MSFNO_SKIP_LINEAR, MSFNO_EUNSUPPORTED,
                 "outer_skip='linear' is not supported by the fused block");
+  MSFNO_REQUIRE(p->same_grid() || (d->inner_skip == MSFNO_SKIP_NONE &&
+                                   d->outer_skip == MSFNO_SKIP_NONE),
+                MSFNO_EINVAL, "skip connections need equal input and output grids");
   return MSFNO_OK;
+}
+
+hipEvent_t slot_event(msfno_band_plan_s* p, int slot) {
+  if (slot < 0 || slot >= 64) return nullptr;
+  if ((int)p->join.size() <= slot) p->join.resize(slot + 1, nullptr);
+  if (!p->join[slot] &&
+      hipEventCreateWithFlags(&p->join[slot], hipEventDisableTiming) != hipSuccess)
+    p->join[slot] = nullptr;
+  return p->join[slot];
 }
 
 }  // namespace
@@ -141,25 +196,25 @@ int msfno_band_exchange_counts(int world, int rank, int nlat, int mmax, const in
                                long long* recv_counts) {
   MSFNO_REQUIRE(rank >= 0 && rank < world && R > 0 && send_counts && recv_counts, MSFNO_EINVAL,
                 "bad exchange-count arguments");
+  MSFNO_REQUIRE(phase == 0 || phase == 1, MSFNO_EINVAL, "phase must be 0 or 1");
   int lmax_eff = 0;  // validate against the implied lmax (owners of -1 mark m >= lmax)
   for (int m = 0; m < mmax; ++m)
     if (m_owner && m_owner[m] >= 0) lmax_eff = m + 1;
   MSFNO_TRY(validate_partition(world, nlat, std::max(lmax_eff, 1), mmax, row_start, m_owner));
-  std::vector<long long> nm(world, 0);
+  std::vector<int> nm(world, 0);
   for (int m = 0; m < mmax; ++m)
     if (m_owner[m] >= 0) ++nm[m_owner[m]];
-  const long long hr = row_start[rank + 1] - row_start[rank];
-  for (int q = 0; q < world; ++q) {
-    const long long hq = row_start[q + 1] - row_start[q];
-    if (phase == 0) {  // rows -> m: send my rows of q's m-set, receive q's rows of mine
-      send_counts[q] = nm[q] * R * hr;
-      recv_counts[q] = nm[rank] * R * hq;
-    } else {           // m -> rows
-      send_counts[q] = nm[rank] * R * hq;
-      recv_counts[q] = nm[q] * R * hr;
-    }
-  }
+  exchange_counts(world, rank, nm, row_start, row_start, R, phase, send_counts, recv_counts);
+  return MSFNO_OK;
+}
+
+int msfno_band_plan_exchange_counts(msfno_band_plan_t p, int R, int phase, long long* send_counts,
+                                    long long* recv_counts) {
+  MSFNO_REQUIRE(p && R > 0 && send_counts && recv_counts, MSFNO_EINVAL,
+                "bad exchange-count arguments");
   MSFNO_REQUIRE(phase == 0 || phase == 1, MSFNO_EINVAL, "phase must be 0 or 1");
+  exchange_counts(p->world, p->rank, p->nm_of, p->row_in.data(), p->row_out.data(), R, phase,
+                  send_counts, recv_counts);
   return MSFNO_OK;
 }
 
@@ -167,23 +222,31 @@ int msfno_band_plan_destroy(msfno_band_plan_t p) {
   if (!p) return MSFNO_OK;
   msfno_sht_plan_destroy(p->fwd);
   msfno_sht_plan_destroy(p->inv);
-  if (p->d_row0) (void)hipFree(p->d_row0);
+  if (p->d_row_in) (void)hipFree(p->d_row_in);
+  if (p->d_row_out) (void)hipFree(p->d_row_out);
   if (p->d_perm) (void)hipFree(p->d_perm);
+  for (hipEvent_t e : p->join)
+    if (e) (void)hipEventDestroy(e);
   delete p;
   return MSFNO_OK;
 }
 
-int msfno_band_plan_create(int nlat, int nlon, int lmax, int mmax, int world, int rank,
-                           const int* row_start, const int* m_owner, msfno_band_plan_t* plan) {
+int msfno_band_plan_create2(int nlat_in, int nlon_in, int nlat_out, int nlon_out, int lmax,
+                            int mmax, int world, int rank, const int* row_in, const int* row_out,
+                            const int* m_owner, msfno_band_plan_t* plan) {
   MSFNO_REQUIRE(plan, MSFNO_EINVAL, "null plan pointer");
   MSFNO_REQUIRE(rank >= 0 && rank < world, MSFNO_EINVAL, "rank out of range");
-  MSFNO_TRY(validate_partition(world, nlat, lmax, mmax, row_start, m_owner));
+  MSFNO_TRY(validate_partition(world, nlat_in, lmax, mmax, row_in, m_owner));
+  MSFNO_TRY(validate_rows(world, nlat_out, row_out));
   auto* p = new msfno_band_plan_s();
-  p->nlat = nlat; p->nlon = nlon; p->lmax = lmax; p->mmax = mmax;
+  p->nlat_in = nlat_in; p->nlon_in = nlon_in; p->nlat_out = nlat_out; p->nlon_out = nlon_out;
+  p->lmax = lmax; p->mmax = mmax;
   p->world = world; p->rank = rank;
-  p->row0.assign(row_start, row_start + world + 1);
+  p->row_in.assign(row_in, row_in + world + 1);
+  p->row_out.assign(row_out, row_out + world + 1);
   p->owner.assign(m_owner, m_owner + mmax);
-  p->rows = row_start[rank + 1] - row_start[rank];
+  p->rows_in = row_in[rank + 1] - row_in[rank];
+  p->rows_out = row_out[rank + 1] - row_out[rank];
   p->nm_of.assign(world, 0);
   std::vector<char> mask(mmax, 0);
   for (int m = 0; m < mmax; ++m) {
@@ -198,16 +261,20 @@ int msfno_band_plan_create(int nlat, int nlon, int lmax, int mmax, int world, in
   for (int q = 1; q < world; ++q) start[q] = start[q - 1] + p->nm_of[q - 1];
   for (int m = 0; m < mmax; ++m)
     if (m_owner[m] >= 0) perm[m] = start[m_owner[m]]++;
-  int rc = plan_create(nlat, nlon, lmax, mmax, 0, &mask, &p->fwd);
-  if (rc == MSFNO_OK) rc = plan_create(nlat, nlon, lmax, mmax, 1, &mask, &p->inv);
+  int rc = plan_create(nlat_in, nlon_in, lmax, mmax, 0, &mask, &p->fwd);
+  if (rc == MSFNO_OK) rc = plan_create(nlat_out, nlon_out, lmax, mmax, 1, &mask, &p->inv);
   if (rc != MSFNO_OK) {
     msfno_band_plan_destroy(p);
     return rc;
   }
-  hipError_t e = hipMalloc(&p->d_row0, (world + 1) * sizeof(int));
+  hipError_t e = hipMalloc(&p->d_row_in, (world + 1) * sizeof(int));
+  if (e == hipSuccess) e = hipMalloc(&p->d_row_out, (world + 1) * sizeof(int));
   if (e == hipSuccess) e = hipMalloc(&p->d_perm, mmax * sizeof(int));
   if (e == hipSuccess)
-    e = hipMemcpy(p->d_row0, p->row0.data(), (world + 1) * sizeof(int), hipMemcpyHostToDevice);
+    e = hipMemcpy(p->d_row_in, p->row_in.data(), (world + 1) * sizeof(int), hipMemcpyHostToDevice);
+  if (e == hipSuccess)
+    e = hipMemcpy(p->d_row_out, p->row_out.data(), (world + 1) * sizeof(int),
+                  hipMemcpyHostToDevice);
   if (e == hipSuccess)
     e = hipMemcpy(p->d_perm, perm.data(), mmax * sizeof(int), hipMemcpyHostToDevice);
   if (e != hipSuccess) {
@@ -219,11 +286,25 @@ int msfno_band_plan_create(int nlat, int nlon, int lmax, int mmax, int world, in
   return MSFNO_OK;
 }
 
+int msfno_band_plan_create(int nlat, int nlon, int lmax, int mmax, int world, int rank,
+                           const int* row_start, const int* m_owner, msfno_band_plan_t* plan) {
+  return msfno_band_plan_create2(nlat, nlon, nlat, nlon, lmax, mmax, world, rank, row_start,
+                                 row_start, m_owner, plan);
+}
+
 int msfno_band_plan_load_tables(msfno_band_plan_t p, const float* fwd_table,
                                 const float* inv_table, void* stream) {
   MSFNO_REQUIRE(p && fwd_table && inv_table, MSFNO_EINVAL, "null band plan or table");
   MSFNO_TRY(msfno_sht_plan_load_table(p->fwd, fwd_table, stream));
   MSFNO_TRY(msfno_sht_plan_load_table(p->inv, inv_table, stream));
+  return MSFNO_OK;
+}
+
+int msfno_band_linear_modes(msfno_band_plan_t p, long long* modes, long long* count) {
+  MSFNO_REQUIRE(p && count, MSFNO_EINVAL, "null band plan or count");
+  const auto& v = p->fwd->lin_modes;
+  *count = (long long)v.size();
+  if (modes && !v.empty()) std::memcpy(modes, v.data(), v.size() * sizeof(long long));
   return MSFNO_OK;
 }
 
@@ -248,7 +329,7 @@ int msfno_band_block_stage(const msfno_block_desc* d, msfno_band_plan_t p, int s
   BandBufs b;
   carve_band(cv, b, d, p, B);
   const int64_t C = d->C, BC = (int64_t)B * C, R = 2 * BC;
-  const int64_t Pl = (int64_t)p->rows * p->nlon;
+  const int64_t Pout = (int64_t)p->rows_out * p->nlon_out;
   const int64_t slab_rows = (int64_t)p->nm * R;
   switch (stage) {
     case 0: {
@@ -256,10 +337,13 @@ int msfno_band_block_stage(const msfno_block_desc* d, msfno_band_plan_t p, int s
       // the skip GEMM as in msfno_block_forward: on x planes written by the rfft (forked
       // after it) when the plane buffer exists, else on fp32 x (forked first)
       const bool xpl = skip_planes(d, p->fwd, b.fb);
+      const int64_t Pl = (int64_t)p->rows_in * p->nlon_in;
       auto launch_skip = [&]() -> int {
         SideCtx* side = nullptr;
-        MSFNO_TRY(side_ctx(&side));
+        MSFNO_TRY(side_ctx(&side, s));
         hipStream_t ss = s;
+        hipEvent_t join = side ? slot_event(p, io->slot) : nullptr;
+        MSFNO_REQUIRE(!side || join, MSFNO_EHIP, "band slot event unavailable (slot must be 0..63)");
         if (side) {
           MSFNO_CHECK_HIP(hipEventRecord(side->fork, s));
           MSFNO_CHECK_HIP(hipStreamWaitEvent(side->side, side->fork, 0));
@@ -280,7 +364,7 @@ int msfno_band_block_stage(const msfno_block_desc* d, msfno_band_plan_t p, int s
         }
         if (side) {
           prof(ST_END, ss);
-          MSFNO_CHECK_HIP(hipEventRecord(side->join, ss));
+          MSFNO_CHECK_HIP(hipEventRecord(join, ss));
         }
         return MSFNO_OK;
       };
@@ -289,30 +373,33 @@ int msfno_band_block_stage(const msfno_block_desc* d, msfno_band_plan_t p, int s
         if (!xpl) MSFNO_TRY(launch_skip());
       }
       prof(ST_FFT_FWD, s);
-      const float scale = (float)(2.0 * M_PI / p->nlon);
-      const C2RPlanes xp{b.fb.x1p, (int)C, p->rows};
-      MSFNO_TRY(launch_fft_r2c_rows(p->fwd->fft, io->x, b.Xn, b.rs, BC * p->rows, p->mmax, scale,
-                                    s, xpl ? &xp : nullptr));
+      const float scale = (float)(2.0 * M_PI / p->nlon_in);
+      const C2RPlanes xp{b.fb.x1p, (int)C, p->rows_in};
+      MSFNO_TRY(launch_fft_r2c_rows(p->fwd->fft, io->x, b.Xn, b.rs, BC * p->rows_in, p->mmax,
+                                    scale, s, xpl ? &xp : nullptr));
       if (xpl) MSFNO_TRY(launch_skip());
       prof(ST_NORM0, s);
-      MSFNO_TRY(launch_stats_partial(b.rs, p->rows, p->nlon, BC, io->stats_local, s));
+      MSFNO_TRY(launch_stats_partial(b.rs, p->rows_in, p->nlon_in, BC, io->stats_local, s));
+      prof(ST_END, s);
       break;
     }
     case 1: {
       MSFNO_REQUIRE(io->stats_all && io->send, MSFNO_EINVAL, "stage 1 needs stats_all and send");
+      prof(ST_NORM0, s);
       MSFNO_TRY(launch_chan_affine_parts(io->stats_all, p->world, B, (int)C, d->norm0_w,
                                          d->norm0_b, d->norm_eps, nullptr, nullptr, 0.f, b.sc0,
                                          b.sh0, s));
       prof(ST_BAND_PACK, s);
-      MSFNO_TRY(launch_transpose_fwd(b.Xn, io->send, B, (int)C, p->rows, p->mmax, p->rows, b.sc0,
-                                     b.sh0, s, p->d_perm));
+      MSFNO_TRY(launch_transpose_fwd(b.Xn, io->send, B, (int)C, p->rows_in, p->mmax, p->rows_in,
+                                     b.sc0, b.sh0, s, p->d_perm));
+      prof(ST_END, s);
       break;
     }
     case 2: {
       MSFNO_REQUIRE(io->send && io->recv, MSFNO_EINVAL, "stage 2 needs send and recv");
       if (p->nm == 0) break;  // this rank owns no zonal wavenumber
       prof(ST_BAND_GATHER, s);
-      MSFNO_TRY(launch_band_copy(io->recv, b.Xt, slab_rows, p->fwd->geom(), p->d_row0,
+      MSFNO_TRY(launch_band_copy(io->recv, b.Xt, slab_rows, p->fwd->geom(), p->d_row_in,
                                  p->world, false, s));
       prof(ST_LEG_FWD, s);
       MSFNO_TRY(legendre_fwd(p->fwd, b.Xt, b.fb.Sa, (int)R, s));
@@ -320,53 +407,63 @@ int msfno_band_block_stage(const msfno_block_desc* d, msfno_band_plan_t p, int s
       prof(ST_LEG_INV, s);
       MSFNO_TRY(legendre_inv(p->inv, b.fb.Sa, b.Xt, (int)R, s));
       prof(ST_BAND_SCATTER, s);
-      MSFNO_TRY(launch_band_copy(b.Xt, io->send, slab_rows, p->inv->geom(), p->d_row0,
+      MSFNO_TRY(launch_band_copy(b.Xt, io->send, slab_rows, p->inv->geom(), p->d_row_out,
                                  p->world, true, s));
+      prof(ST_END, s);
       break;
     }
     case 3: {
-      MSFNO_REQUIRE(io->recv && io->x && io->stats_local, MSFNO_EINVAL,
-                    "stage 3 needs recv, x and stats_local");
+      MSFNO_REQUIRE(io->recv && io->stats_local, MSFNO_EINVAL, "stage 3 needs recv and stats_local");
       prof(ST_TRANSPOSE_INV, s);
-      MSFNO_TRY(launch_transpose_inv(io->recv, b.Xn, B, (int)C, p->rows, p->mmax, p->mact,
-                                     p->rows, s, p->d_perm));
+      MSFNO_TRY(launch_transpose_inv(io->recv, b.Xn, B, (int)C, p->rows_out, p->mmax, p->mact,
+                                     p->rows_out, s, p->d_perm));
       const float* skip_src = nullptr;
       if (d->inner_skip == MSFNO_SKIP_LINEAR) {
         SideCtx* side = nullptr;
-        MSFNO_TRY(side_ctx(&side));
-        if (side) MSFNO_CHECK_HIP(hipStreamWaitEvent(s, side->join, 0));
+        MSFNO_TRY(side_ctx(&side, s));
+        if (side) {
+          hipEvent_t join = slot_event(p, io->slot);
+          MSFNO_REQUIRE(join, MSFNO_EHIP, "band slot event unavailable (slot must be 0..63)");
+          MSFNO_CHECK_HIP(hipStreamWaitEvent(s, join, 0));
+        }
         skip_src = b.x1;
       } else if (d->inner_skip == MSFNO_SKIP_IDENTITY) {
+        MSFNO_REQUIRE(io->x, MSFNO_EINVAL, "stage 3 needs x for the identity skip");
         skip_src = io->x;
       }
       prof(ST_FFT_INV, s);
       // with an MLP on the x6 engine the irfft writes x1 as planes (fc1's B operand)
-      const C2RPlanes x1p{b.fb.x1p, (int)C, p->rows};
-      MSFNO_TRY(launch_fft_c2r_rows(p->inv->fft, b.Xn, b.x1, skip_src, b.rs, BC * p->rows,
-                                    p->mmax, 0, s, b.fb.x1p ? &x1p : nullptr));
+      const C2RPlanes x1p{b.fb.x1p, (int)C, p->rows_out};
+      MSFNO_TRY(launch_fft_c2r_rows(p->inv->fft, b.Xn, b.x1, skip_src, b.rs, BC * p->rows_out,
+                                    p->mmax, d->filter_type == MSFNO_FILTER_LINEAR ? 1 : 0, s,
+                                    b.fb.x1p ? &x1p : nullptr));
       prof(ST_NORM1, s);
-      MSFNO_TRY(launch_stats_partial(b.rs, p->rows, p->nlon, BC, io->stats_local, s));
+      MSFNO_TRY(launch_stats_partial(b.rs, p->rows_out, p->nlon_out, BC, io->stats_local, s));
+      prof(ST_END, s);
       break;
     }
     case 4: {
-      MSFNO_REQUIRE(io->stats_all && io->out && io->x, MSFNO_EINVAL,
-                    "stage 4 needs stats_all, x and out");
+      MSFNO_REQUIRE(io->stats_all && io->out, MSFNO_EINVAL, "stage 4 needs stats_all and out");
       MSFNO_REQUIRE((io->gamma == nullptr) == (io->beta == nullptr), MSFNO_EINVAL,
                     "gamma and beta must both be given or both be NULL");
+      prof(ST_NORM1, s);
       MSFNO_TRY(launch_chan_affine_parts(io->stats_all, p->world, B, (int)C, d->norm1_w,
                                          d->norm1_b, d->norm_eps, io->gamma, io->beta,
                                          io->film_scale, b.sc1, b.sh1, s));
       const float* resid = d->outer_skip == MSFNO_SKIP_IDENTITY ? io->x : nullptr;
+      MSFNO_REQUIRE(d->outer_skip != MSFNO_SKIP_IDENTITY || io->x, MSFNO_EINVAL,
+                    "stage 4 needs x for the outer skip");
       if (d->has_mlp) {
         MSFNO_REQUIRE(d->fc1_w && d->fc2_w, MSFNO_EINVAL, "missing MLP weights");
         const int64_t Hd = d->mlp_hidden;
         MSFNO_TRY(launch_fold_affine(d->fc1_w, d->fc1_b, b.sc1, b.sh1, b.W1f, b.b1f, B, (int)Hd,
                                      (int)C, s));
-        MSFNO_TRY(run_mlp(d, b.W1f, b.b1f, b.x1, b.h, io->out, resid, B, Pl, b.fb.dw, s,
+        MSFNO_TRY(run_mlp(d, b.W1f, b.b1f, b.x1, b.h, io->out, resid, B, Pout, b.fb.dw, s,
                           b.fb.x1p));
       } else {
         prof(ST_OUT_AFFINE, s);
-        MSFNO_TRY(launch_affine_rows(b.x1, b.sc1, b.sh1, resid, io->out, BC, Pl, 0, nullptr, 0, s));
+        MSFNO_TRY(launch_affine_rows(b.x1, b.sc1, b.sh1, resid, io->out, BC, Pout, 0, nullptr, 0,
+                                     s));
       }
       prof(ST_END, s);
       break;

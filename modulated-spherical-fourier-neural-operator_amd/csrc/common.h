@@ -233,6 +233,11 @@ struct msfno_sht_plan_s {
   int64_t* d_tab_off = nullptr;  // device copies of the per-m metadata
   int* d_Lp = nullptr;
   int* d_off = nullptr;          // S-layout column offsets off[m]
+  // m-set plans (latitude-band sharding): global tril index (torch.tril_indices(lmax,
+  // mmax) order) -> position among the plan's own modes (ascending global order),
+  // -1 for modes of other ranks; null for full plans.  lin_modes: the inverse map.
+  int* d_tril_local = nullptr;
+  std::vector<long long> lin_modes;
   int table_loaded = 0;
   // equatorial symmetry: the grid is symmetric (table[m][l][nlat-1-k] =
   // (-1)^(l-m) table[m][l][k], checked at load).  Then the Legendre GEMMs run

@@ -915,7 +915,8 @@ __device__ __forceinline__ int64_t tril_row_off(int l, int mmax) {
 __global__ void spec_to_tril_kernel(const float* __restrict__ S, float* __restrict__ xt, int B,
                                     int C, int lmax, int mmax, int mact, int64_t Tp, int64_t T,
                                     int64_t ldT, const int* __restrict__ off,
-                                    const int* __restrict__ Lpe, const int* __restrict__ Lp) {
+                                    const int* __restrict__ Lpe, const int* __restrict__ Lp,
+                                    const int* __restrict__ tmap) {
   const int64_t n = (int64_t)B * C * Tp;
   for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < n;
        e += (int64_t)gridDim.x * blockDim.x) {
@@ -925,7 +926,8 @@ __global__ void spec_to_tril_kernel(const float* __restrict__ S, float* __restri
     int m, j;
     spec_col_inv(off, Lpe, Lp, mact, t, lmax, m, j);
     if (j < 0) continue;
-    const int64_t nn = tril_row_off(m + j, mmax) + m;
+    int64_t nn = tril_row_off(m + j, mmax) + m;
+    if (tmap) nn = tmap[nn];  // m-set plan: position among this rank's modes
     const float re = S[((int64_t)(b * 2 + 0) * C + c) * ldT + t];
     const float im = S[((int64_t)(b * 2 + 1) * C + c) * ldT + t];
     reinterpret_cast<float2*>(xt)[bc * T + nn] = make_float2(re, im);
@@ -935,7 +937,8 @@ __global__ void spec_to_tril_kernel(const float* __restrict__ S, float* __restri
 __global__ void tril_to_spec_kernel(const float* __restrict__ yt, float* __restrict__ S, int B,
                                     int C, int lmax, int mmax, int mact, int64_t Tp, int64_t T,
                                     int64_t ldT, const int* __restrict__ off,
-                                    const int* __restrict__ Lpe, const int* __restrict__ Lp) {
+                                    const int* __restrict__ Lpe, const int* __restrict__ Lp,
+                                    const int* __restrict__ tmap) {
   const int64_t n = (int64_t)B * C * Tp;
   for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < n;
        e += (int64_t)gridDim.x * blockDim.x) {
@@ -945,7 +948,11 @@ __global__ void tril_to_spec_kernel(const float* __restrict__ yt, float* __restr
     int m, j;
     spec_col_inv(off, Lpe, Lp, mact, t, lmax, m, j);
     float2 v = make_float2(0.f, 0.f);
-    if (j >= 0) v = reinterpret_cast<const float2*>(yt)[bc * T + tril_row_off(m + j, mmax) + m];
+    if (j >= 0) {
+      int64_t nn = tril_row_off(m + j, mmax) + m;
+      if (tmap) nn = tmap[nn];
+      v = reinterpret_cast<const float2*>(yt)[bc * T + nn];
+    }
     S[((int64_t)(b * 2 + 0) * C + c) * ldT + t] = v.x;
     S[((int64_t)(b * 2 + 1) * C + c) * ldT + t] = v.y;
   }
@@ -957,7 +964,7 @@ int launch_spec_to_tril(const msfno_sht_plan_s& p, const float* S, float* xt, in
   const int64_t n = (int64_t)B * C * L.Tp;
   hipLaunchKernelGGL(spec_to_tril_kernel, dim3((unsigned)std::min<int64_t>(cdiv(n, 256), 65535)),
                      dim3(256), 0, s, S, xt, B, C, L.lmax, L.mmax, L.mact, L.Tp, L.T, L.ldT,
-                     p.d_off, p.d_Lpe, p.d_Lp);
+                     p.d_off, p.d_Lpe, p.d_Lp, p.d_tril_local);
   return launch_check("spec_to_tril");
 }
 
@@ -967,7 +974,7 @@ int launch_tril_to_spec(const msfno_sht_plan_s& p, const float* yt, float* S, in
   const int64_t n = (int64_t)B * C * L.Tp;
   hipLaunchKernelGGL(tril_to_spec_kernel, dim3((unsigned)std::min<int64_t>(cdiv(n, 256), 65535)),
                      dim3(256), 0, s, yt, S, B, C, L.lmax, L.mmax, L.mact, L.Tp, L.T, L.ldT,
-                     p.d_off, p.d_Lpe, p.d_Lp);
+                     p.d_off, p.d_Lpe, p.d_Lp, p.d_tril_local);
   return launch_check("tril_to_spec");
 }
 

@@ -63,6 +63,7 @@ class BandIO(ctypes.Structure):
     _fields_ = [
         ("x", _vp), ("gamma", _vp), ("beta", _vp), ("film_scale", _f), ("out", _vp),
         ("send", _vp), ("recv", _vp), ("stats_local", _vp), ("stats_all", _vp),
+        ("slot", _i),
     ]
 
 
@@ -101,17 +102,31 @@ SIGNATURES = [
     ("msfno_band_partition", _i, [_i, _i, _i, _i, _ip, _ip]),
     ("msfno_band_exchange_counts", _i, [_i, _i, _i, _i, _ip, _ip, _i, _i, _llp, _llp]),
     ("msfno_band_plan_create", _i, [_i, _i, _i, _i, _i, _i, _ip, _ip, ctypes.POINTER(_vp)]),
+    ("msfno_band_plan_create2", _i, [_i, _i, _i, _i, _i, _i, _i, _i, _ip, _ip, _ip,
+                                     ctypes.POINTER(_vp)]),
+    ("msfno_band_plan_exchange_counts", _i, [_vp, _i, _i, _llp, _llp]),
+    ("msfno_band_linear_modes", _i, [_vp, _llp, _llp]),
     ("msfno_band_plan_destroy", _i, [_vp]),
     ("msfno_band_plan_load_tables", _i, [_vp, _vp, _vp, _vp]),
     ("msfno_band_workspace_size", _sz, [ctypes.POINTER(BlockDesc), _vp, _i]),
     ("msfno_band_block_stage", _i, [ctypes.POINTER(BlockDesc), _vp, _i, ctypes.POINTER(BandIO),
                                     _i, _vp, _sz, _vp]),
     ("msfno_profile_enable", _i, [_i]),
+    ("msfno_profile_mark", _i, [_i, _vp]),
     ("msfno_profile_collect", _i, [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_i)]),
     ("msfno_profile_stage_name", ctypes.c_char_p, [_i]),
 ]
 
 PROF_NSTAGES = 32
+
+
+def profile_mark(stage_name: str, stream: int) -> None:
+    """Start stage `stage_name` on `stream` (a span lasts to the next mark there)."""
+    for i in range(PROF_NSTAGES):
+        if lib().msfno_profile_stage_name(i).decode() == stage_name:
+            check(lib().msfno_profile_mark(i, stream), "profile_mark")
+            return
+    raise ValueError(f"unknown profile stage {stage_name!r}")
 
 
 def profile_enable(on: bool) -> None:
@@ -165,6 +180,23 @@ def check(rc: int, what: str = "") -> None:
 
 def ptr(t) -> int | None:
     return None if t is None else t.data_ptr()
+
+
+def on_input_device(fn):
+    """Run ``fn`` with its first GPU tensor argument's device as the current HIP
+    device: kernels go to the null stream of the *current* device and the C side
+    keys its side streams by device, so a module on cuda:1 called while cuda:0 is
+    current must switch first."""
+    import functools
+
+    @functools.wraps(fn)
+    def wrapper(*args, **kwargs):
+        for a in list(args) + list(kwargs.values()):
+            if isinstance(a, torch.Tensor) and a.is_cuda:
+                with torch.cuda.device(a.device):
+                    return fn(*args, **kwargs)
+        return fn(*args, **kwargs)
+    return wrapper
 
 
 def stream_of(device) -> int:

@@ -80,6 +80,7 @@ class RealSHT(_SHTBase):
         self.register_buffer("weights", _legendre_table(self.mmax, self.lmax, nlat, grid, False,
                                                         csphase))
 
+    @N.on_input_device
     def forward(self, x):
         assert x.shape[-2] == self.nlat
         assert x.shape[-1] == self.nlon
@@ -109,6 +110,7 @@ class InverseRealSHT(_SHTBase):
         self.register_buffer("pct", _legendre_table(self.mmax, self.lmax, nlat, grid, True,
                                                     csphase))
 
+    @N.on_input_device
     def forward(self, x):
         assert x.shape[-2] == self.lmax
         assert x.shape[-1] == self.mmax

@@ -91,7 +91,10 @@ class Rollout:
             self._state.copy_(x)
             for i in range(steps):
                 self._graph.replay()
-                yield i, self.normalise(self._out, reverse=True)
+                # the graph's output buffer is overwritten by the next replay: hand the
+                # caller a tensor of its own (normalise(reverse) already makes one)
+                y = self.normalise(self._out, reverse=True)
+                yield i, (y.clone() if y is self._out else y)
                 self._state.copy_(self._out)
         else:
             for i in range(steps):

@@ -14,6 +14,7 @@ def _c(t, name):
     return t
 
 
+@N.on_input_device
 def compl_contract_fwd_c(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
     """einsum("bin,kin->bkn") on complex views (contractions.py:37-41)."""
     a = _c(a, "a")
@@ -30,6 +31,7 @@ def compl_contract_fwd_c(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
 compl_contract_fwd = compl_contract_fwd_c  # same result (contractions.py:28-33)
 
 
+@N.on_input_device
 def compl_mul2d_fwd_c(a: torch.Tensor, b: torch.Tensor, relu_real: bool = False) -> torch.Tensor:
     """einsum("bixy,io->boxy") on complex views (contractions.py:132-137)."""
     a = _c(a, "a")

@@ -18,6 +18,17 @@ Per block forward (include/msfno.h, "Latitude-band sharded SFNO-Block"):
     all_gather(norm1 partials)
     stage 4  norm1 (+FiLM) -> MLP (+outer skip)
 
+Resampling blocks (the network's first block, 721x1440 -> 120x240, and its
+last one back, sfnonet.py:573-614) take rows of the input grid and return rows
+of the output grid: the two grids have their own band partitions.  The linear
+filter's per-mode weight (C, C, T, 2) is sharded with the m-set: each rank keeps
+and streams only its modes' slice (layers.py:398-427, contractions.py:37-41).
+
+``forward(..., chunks=K)`` splits the batch into K sub-batches whose stages are
+software-pipelined: while one sub-batch's all-to-all is in flight (RCCL runs it
+on its own stream, ``async_op=True``), the others' FFTs, Legendre GEMMs and MLPs
+run on the compute stream — the comm/compute overlap of SURVEY.md §8e.
+
 The result equals ``block(x, gamma, beta, scale)`` on the gathered field up to
 fp32 rounding (Welford statistics are merged in fp64).  Collectives go through
 ``torch.distributed`` (backend "nccl" = RCCL over xGMI on MI355X; "gloo" is
@@ -52,6 +63,26 @@ def exchange_counts(world, rank, nlat, mmax, row_start, m_owner, R, phase):
     return list(sc), list(rc)
 
 
+class _Done:
+    def __init__(self, value=None):
+        self.value = value
+
+    def wait(self):
+        return self.value
+
+
+class _Pending:
+    """An in-flight collective: ``wait()`` makes the current stream wait for it
+    (no host block with RCCL) and returns its result tensor (or None)."""
+
+    def __init__(self, work, value=None):
+        self.work, self.value = work, value
+
+    def wait(self):
+        self.work.wait()
+        return self.value
+
+
 class TorchComm:
     """Collectives of one torch.distributed process group."""
 
@@ -80,6 +111,22 @@ class TorchComm:
             self.dist.all_to_all_single(recv[:nr], send[:ns], recv_counts, send_counts,
                                         group=self.group)
 
+    def all_gather_async(self, t):
+        if self.host:
+            return _Done(self.all_gather(t))
+        out = torch.empty((self.world,) + tuple(t.shape), dtype=t.dtype, device=t.device)
+        w = self.dist.all_gather_into_tensor(out, t, group=self.group, async_op=True)
+        return _Pending(w, out)
+
+    def all_to_all_async(self, send, send_counts, recv, recv_counts):
+        if self.host:
+            self.all_to_all(send, send_counts, recv, recv_counts)
+            return _Done()
+        ns, nr = sum(send_counts), sum(recv_counts)
+        w = self.dist.all_to_all_single(recv[:nr], send[:ns], recv_counts, send_counts,
+                                        group=self.group, async_op=True)
+        return _Pending(w)
+
 
 def _drive(gen, comm):
     """Run one rank's stage generator against `comm`."""
@@ -95,6 +142,46 @@ def _drive(gen, comm):
             req = gen.send(res)
         except StopIteration as stop:
             return stop.value
+
+
+def _issue(req, comm):
+    if req[0] == "all_gather":
+        return comm.all_gather_async(req[1])
+    _, send, sc, recv, rc = req
+    return comm.all_to_all_async(send, sc, recv, rc)
+
+
+def _drive_pipelined(gens, comm, stream):
+    """Software pipeline over sub-batch generators (one per sub-batch, stages
+    0..4 with a collective between consecutive stages).  At tick t every started
+    generator advances one stage, the one furthest along first, and sub-batch t
+    starts: the collective a stage issues (async) is waited for only one tick
+    later, after the other sub-batches' stages have been enqueued behind it.  A
+    profiler mark ("band_exchange") brackets each wait on the compute stream, so
+    the stage profile shows the exchange time that was NOT hidden."""
+    K = len(gens)
+    pending = [None] * K
+    alive = [True] * K
+    t = 0
+    while any(alive):
+        for k in range(min(t + 1, K)):
+            if not alive[k]:
+                continue
+            if t == k:
+                req = next(gens[k])
+            else:
+                h = pending[k]
+                if isinstance(h, _Pending):
+                    N.profile_mark("band_exchange", stream)
+                res = h.wait()
+                try:
+                    req = gens[k].send(res)
+                except StopIteration:
+                    alive[k] = False
+                    pending[k] = None
+                    continue
+            pending[k] = _issue(req, comm)
+        t += 1
 
 
 class LocalGroup:
@@ -144,14 +231,18 @@ class LocalGroup:
 
 
 class _BandPlan:
-    def __init__(self, nlat, nlon, lmax, mmax, world, rank, row_start, m_owner, device):
+    def __init__(self, grid_in, grid_out, lmax, mmax, world, rank, row_in, row_out, m_owner,
+                 device):
         self.device = device
         h = ctypes.c_void_p()
-        rs = (ctypes.c_int * (world + 1))(*row_start)
+        ri = (ctypes.c_int * (world + 1))(*row_in)
+        ro = (ctypes.c_int * (world + 1))(*row_out)
         mo = (ctypes.c_int * mmax)(*m_owner)
         with torch.cuda.device(device):
-            N.check(N.lib().msfno_band_plan_create(nlat, nlon, lmax, mmax, world, rank, rs, mo,
-                                                   ctypes.byref(h)), "msfno_band_plan_create")
+            N.check(N.lib().msfno_band_plan_create2(grid_in[0], grid_in[1], grid_out[0],
+                                                    grid_out[1], lmax, mmax, world, rank, ri, ro,
+                                                    mo, ctypes.byref(h)),
+                    "msfno_band_plan_create2")
         self.handle = h
         self.key = None
 
@@ -166,6 +257,23 @@ class _BandPlan:
         self._tables = (fwd_table, inv_table)
         self.key = key
 
+    def counts(self, R, phase):
+        sc = (ctypes.c_longlong * 64)()
+        rc = (ctypes.c_longlong * 64)()
+        N.check(N.lib().msfno_band_plan_exchange_counts(self.handle, R, phase, sc, rc),
+                "msfno_band_plan_exchange_counts")
+        return sc, rc
+
+    def linear_modes(self):
+        """Global tril indices of this rank's modes (ascending)."""
+        n = ctypes.c_longlong()
+        N.check(N.lib().msfno_band_linear_modes(self.handle, None, ctypes.byref(n)),
+                "msfno_band_linear_modes")
+        buf = (ctypes.c_longlong * max(n.value, 1))()
+        N.check(N.lib().msfno_band_linear_modes(self.handle, buf, ctypes.byref(n)),
+                "msfno_band_linear_modes")
+        return list(buf)[:n.value]
+
     def __del__(self):
         try:
             if self.handle:
@@ -178,29 +286,46 @@ class LatBandBlock:
     """One rank's share of a latitude-band sharded FourierNeuralOperatorBlock[_Filmed].
 
     ``block`` is the (replicated) block module; ``forward(x_local, gamma, beta,
-    scale)`` takes this rank's rows ``x[:, :, row_start[rank]:row_start[rank+1]]``
-    and returns the same rows of the block output."""
+    scale)`` takes this rank's rows of the input grid
+    ``x[:, :, rows_in[0]:rows_in[1]]`` and returns its rows of the output grid
+    (the same rows unless the block resamples).  ``row_start`` partitions the
+    input grid, ``row_start_out`` the output grid (default: balanced bands)."""
 
     def __init__(self, block, rank: int, world: int, row_start=None, m_owner=None,
-                 device=None):
+                 device=None, row_start_out=None):
         fwd, inv = block._transforms()
-        if (fwd.nlat, fwd.nlon) != (inv.nlat, inv.nlon):
-            raise NotImplementedError("latitude-band sharding needs equal input/output grids")
         self.block = block
         self.rank, self.world = rank, world
         self.nlat, self.nlon, self.lmax, self.mmax = fwd.nlat, fwd.nlon, fwd.lmax, fwd.mmax
+        self.nlat_out, self.nlon_out = inv.nlat, inv.nlon
         if row_start is None or m_owner is None:
-            row_start, m_owner = band_partition(world, self.nlat, self.lmax, self.mmax)
+            rs, own = band_partition(world, self.nlat, self.lmax, self.mmax)
+            row_start = rs if row_start is None else row_start
+            m_owner = own if m_owner is None else m_owner
+        if row_start_out is None:
+            if (self.nlat_out, self.nlon_out) == (self.nlat, self.nlon):
+                row_start_out = row_start
+            else:
+                row_start_out = band_partition(world, self.nlat_out, self.lmax, self.mmax)[0]
         self.row_start, self.m_owner = list(row_start), list(m_owner)
+        self.row_start_out = list(row_start_out)
         self.device = device if device is not None else torch.device("cuda",
                                                                     torch.cuda.current_device())
-        self.plan = _BandPlan(self.nlat, self.nlon, self.lmax, self.mmax, world, rank,
-                              self.row_start, self.m_owner, self.device)
+        self.plan = _BandPlan((self.nlat, self.nlon), (self.nlat_out, self.nlon_out), self.lmax,
+                              self.mmax, world, rank, self.row_start, self.row_start_out,
+                              self.m_owner, self.device)
         self._bufs = {}
+        self._lin = None   # (key, local weight slice)
 
     @property
     def rows(self):
+        """This rank's rows of the input grid."""
         return self.row_start[self.rank], self.row_start[self.rank + 1]
+
+    @property
+    def rows_out(self):
+        """This rank's rows of the output grid."""
+        return self.row_start_out[self.rank], self.row_start_out[self.rank + 1]
 
     def _tables(self):
         fwd, inv = self.block._transforms()
@@ -215,12 +340,29 @@ class LatBandBlock:
             tabs.append(t)
         self.plan.load(tabs[0], tabs[1], key)
 
-    def _buffers(self, B, C):
-        key = (B, C)
+    def _linear_weight(self, w):
+        """This rank's slice w[:, :, modes, :] of the per-mode weight (cached until
+        the parameter changes); the whole weight when the rank owns every mode."""
+        key = (w.data_ptr(), w._version, str(w.device))
+        if self._lin is not None and self._lin[0] == key:
+            return self._lin[1]
+        modes = self.plan.linear_modes()
+        if len(modes) == w.shape[2]:
+            local = w
+        else:
+            idx = torch.tensor(modes, dtype=torch.long, device=w.device)
+            local = w.detach().index_select(2, idx).contiguous()
+        self._lin = (key, local)
+        return local
+
+    def _buffers(self, B, C, slot):
+        key = (B, C, slot)
         if key not in self._bufs:
             R = 2 * B * C
-            cnt = [exchange_counts(self.world, self.rank, self.nlat, self.mmax, self.row_start,
-                                   self.m_owner, R, ph) for ph in (0, 1)]
+            cnt = []
+            for ph in (0, 1):
+                sc, rc = self.plan.counts(R, ph)
+                cnt.append((list(sc)[:self.world], list(rc)[:self.world]))
             n = max(max(sum(s), sum(r)) for s, r in cnt)
             dev = self.device
             self._bufs[key] = dict(
@@ -230,35 +372,44 @@ class LatBandBlock:
                 stats=torch.empty(B * C, 3, dtype=torch.float64, device=dev))
         return self._bufs[key]
 
-    def stages(self, x, gamma=None, beta=None, scale=1.0):
+    def stages(self, x, gamma=None, beta=None, scale=1.0, slot=0, out=None):
         """Generator over the five native stages; yields the collective requests
-        ("all_gather", tensor) / ("all_to_all", send, send_counts, recv, recv_counts)."""
+        ("all_gather", tensor) / ("all_to_all", send, send_counts, recv, recv_counts)
+        and returns this rank's output rows.  ``slot`` (0..63) must differ between
+        sub-batches in flight at the same time."""
         x = N.require_device_f32(x, "band block input")
         B, C, H, W = x.shape
         r0, r1 = self.rows
+        o0, o1 = self.rows_out
         if H != r1 - r0 or W != self.nlon or C != self.block.embed_dim_sfno:
             raise ValueError(f"x_local must be (B, {self.block.embed_dim_sfno}, {r1 - r0}, "
                              f"{self.nlon}), got {tuple(x.shape)}")
         self._tables()
         d, keep = self.block.native_desc()
+        if d.filter_type == N.FILTER_LINEAR:
+            wl = self._linear_weight(self.block.filter_layer.filter.w)
+            d.lin_w = wl.data_ptr()
+            keep.append(wl)
         if gamma is not None:
             gamma = gamma.detach().float().reshape(B, C).contiguous()
             beta = beta.detach().float().reshape(B, C).contiguous()
         L = N.lib()
-        bufs = self._buffers(B, C)
+        bufs = self._buffers(B, C, slot)
         nbytes = L.msfno_band_workspace_size(d, self.plan.handle, B)
         ws = torch.empty(nbytes, dtype=torch.uint8, device=x.device)
-        out = torch.empty_like(x)
+        if out is None:
+            out = torch.empty(B, C, o1 - o0, self.nlon_out, dtype=torch.float32, device=x.device)
         io = N.BandIO(x=x.data_ptr(), gamma=N.ptr(gamma), beta=N.ptr(beta),
                       film_scale=float(scale), out=out.data_ptr(), send=bufs["send"].data_ptr(),
                       recv=bufs["recv"].data_ptr(), stats_local=bufs["stats"].data_ptr(),
-                      stats_all=None)
+                      stats_all=None, slot=int(slot))
         stream = N.stream_of(x.device)
 
         def stage(i):
-            N.check(L.msfno_band_block_stage(d, self.plan.handle, i, ctypes.byref(io), B,
-                                             ws.data_ptr(), nbytes, stream),
-                    f"band stage {i}")
+            with torch.cuda.device(x.device):
+                N.check(L.msfno_band_block_stage(d, self.plan.handle, i, ctypes.byref(io), B,
+                                                 ws.data_ptr(), nbytes, stream),
+                        f"band stage {i}")
 
         (sc0, rc0), (sc1, rc1) = bufs["counts"]
         stage(0)
@@ -275,10 +426,32 @@ class LatBandBlock:
         del keep, st, st2
         return out
 
-    def forward(self, x, gamma=None, beta=None, scale=1.0, comm=None):
-        gen = self.stages(x, gamma, beta, scale)
+    def forward(self, x, gamma=None, beta=None, scale=1.0, comm=None, chunks=1):
+        """This rank's output rows.  ``chunks`` > 1 pipelines that many sub-batches
+        (exchanges overlapped with the other sub-batches' compute)."""
+        B = x.shape[0]
+        K = max(1, min(int(chunks), B, 64))
+        if K == 1:
+            gen = self.stages(x, gamma, beta, scale)
+            if self.world == 1 and comm is None:
+                return LocalGroup.run([gen])[0]
+            return _drive(gen, comm if comm is not None else TorchComm())
+        x = N.require_device_f32(x, "band block input")
+        o0, o1 = self.rows_out
+        out = torch.empty(B, x.shape[1], o1 - o0, self.nlon_out, dtype=torch.float32,
+                          device=x.device)
+        bounds = [B * k // K for k in range(K + 1)]
+        gens = []
+        for k in range(K):
+            b0, b1 = bounds[k], bounds[k + 1]
+            g = gamma[b0:b1] if gamma is not None else None
+            be = beta[b0:b1] if beta is not None else None
+            gens.append(self.stages(x[b0:b1], g, be, scale, slot=k, out=out[b0:b1]))
         if self.world == 1 and comm is None:
-            return LocalGroup.run([gen])[0]
-        return _drive(gen, comm if comm is not None else TorchComm())
+            for gen in gens:
+                LocalGroup.run([gen])
+            return out
+        _drive_pipelined(gens, comm if comm is not None else TorchComm(), N.stream_of(x.device))
+        return out
 
     __call__ = forward

@@ -102,6 +102,7 @@ class MLP(nn.Module):
         d.fc1_w, d.fc1_b, d.fc2_w, d.fc2_b = w1.data_ptr(), b1.data_ptr(), w2.data_ptr(), N.ptr(b2)
         return d, keep
 
+    @N.on_input_device
     def native_forward(self, x, x2=None, addend=None):
         """out = fc2(GELU(fc1(cat(x, x2)))) (+ addend, broadcast over the batch when its
         leading dimension is 1) in two MFMA GEMMs (msfno_mlp_forward); the channel
@@ -133,6 +134,7 @@ class MLP(nn.Module):
         del keep
         return out.to(dtype)
 
+    @N.on_input_device
     def native_backward_input(self, x, dy, x2=None):
         """dL/dx of fc2(GELU(fc1(cat(x, x2)))) for frozen weights
         (msfno_mlp_backward_input): the decoder's backward in FiLM fine-tuning."""
@@ -201,6 +203,7 @@ class _S2FilterBase(nn.Module):
         self._fill_desc(d, keep)
         return d, keep
 
+    @N.on_input_device
     def forward(self, x):
         dtype = x.dtype
         x = N.require_device_f32(x, "filter input")

@@ -150,9 +150,12 @@ class FourierNeuralOperatorBlock(nn.Module):
             d.outer_skip = N.SKIP_NONE
         if hasattr(self, "mlp"):
             seq = self.mlp.fwd
-            if len(seq) != 3 or not _is_exact_gelu(seq[1]):
-                if self.training:
-                    raise NotImplementedError("MLP dropout in training mode is not fused")
+            # the fused MLP applies GELU(erf) whatever the module says: refuse anything else
+            # (layers.py:161-178 builds fc1, act, [drop], fc2, [drop])
+            if len(seq) not in (3, 5) or not _is_exact_gelu(seq[1]):
+                raise NotImplementedError("the block MLP fuses fc1 -> nn.GELU() (erf) -> fc2 only")
+            if len(seq) == 5 and self.training:
+                raise NotImplementedError("MLP dropout in training mode is not fused")
             fc1, fc2 = seq[0], seq[-2] if len(seq) == 5 else seq[2]
             w1 = fc1.weight.detach().float().contiguous()
             b1 = fc1.bias.detach().float().contiguous() if fc1.bias is not None else None
@@ -169,6 +172,7 @@ class FourierNeuralOperatorBlock(nn.Module):
     def _transforms(self):
         return self.filter_layer.filter._transforms()
 
+    @N.on_input_device
     def _native_forward(self, x, gamma=None, beta=None, scale=1.0):
         dtype = x.dtype
         x = N.require_device_f32(x, "block input")
@@ -205,6 +209,7 @@ class FourierNeuralOperatorBlock_Filmed(FourierNeuralOperatorBlock):
             return _FilmedBlockFn.apply(x, gamma, beta, float(scale), self)
         return self._native_forward(x, gamma, beta, scale)
 
+    @N.on_input_device
     def native_film_backward(self, x, gamma, beta, scale, dout):
         """(dL/dgamma, dL/dbeta) of this block for dout = dL/d(out), SFNO weights frozen
         (msfno_block_film_backward; the forward up to x1 is recomputed)."""

@@ -3,7 +3,9 @@ C-ABI stages (msfno_band_*): W virtual ranks run in lock step on one GPU
 (LocalGroup — the all-to-alls become device copies), and the re-assembled
 output is compared with the reference golden vectors (max-abs < 1e-4, the
 north-star bar) and with the unsharded native block (same kernels, only the
-statistics merge order differs: max-abs < 2e-5)."""
+statistics merge order differs: max-abs < 2e-5).  Every golden fixture is
+covered: both filters (the linear one with its per-mode weight sharded by
+m-set) and the resampling first/last blocks (separate input / output bands)."""
 import os
 
 import pytest
@@ -15,8 +17,7 @@ from golden_util import golden_files, load
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
 
-SAME_GRID_NL = [p for p in golden_files()
-                if "_nl_" in os.path.basename(p) and not os.path.basename(p).startswith(("down", "up"))]
+ALL_BLOCKS = golden_files()
 
 
 def _sharded(blk, x, gamma, beta, scale, world, row_start=None, m_owner=None):
@@ -31,10 +32,10 @@ def _sharded(blk, x, gamma, beta, scale, world, row_start=None, m_owner=None):
 
 
 @pytest.mark.parametrize("world", [1, 2, 3, 5])
-@pytest.mark.parametrize("path", SAME_GRID_NL, ids=lambda p: os.path.basename(p)[:-4])
+@pytest.mark.parametrize("path", ALL_BLOCKS, ids=lambda p: os.path.basename(p)[:-4])
 def test_sharded_block_matches_golden(path, world):
     meta, params, arrays, _ = load(path)
-    if meta["nlat"] < world:
+    if min(meta["nlat"], meta.get("out_nlat", meta["nlat"])) < world:
         pytest.skip("fewer latitude rows than ranks")
     blk, _, _ = make_block(meta, params)
     blk = blk.to(DEV)
@@ -67,15 +68,49 @@ def test_sharded_block_custom_partition_with_idle_rank():
     assert (y - arrays["y"]).abs().max().item() < 1e-4
 
 
-def test_sharded_block_rejects_linear_filter():
-    path = [p for p in golden_files() if os.path.basename(p) == "c1_lin_film_middle.npz"][0]
-    meta, params, arrays, _ = load(path)
+@pytest.mark.parametrize("name", ["c1b2_lin_film_middle.npz", "c1b2_nl_film_middle.npz",
+                                  "down_lin_film_first.npz", "up_nl_film_last.npz"])
+@pytest.mark.parametrize("chunks", [2, 3])
+def test_sharded_block_pipelined_chunks(name, chunks):
+    """The sub-batch pipeline (forward(chunks=K)): world 1, the batch split into
+    K sub-batches with their own slots / buffers; fields are independent, so each
+    equals the golden output of its field."""
+    from msfno_amd.sfno import LatBandBlock
+    meta, params, arrays, _ = load([p for p in golden_files() if os.path.basename(p) == name][0])
     blk, _, _ = make_block(meta, params)
     blk = blk.to(DEV)
-    from msfno_amd.sfno import LatBandBlock
+    x = arrays["x"].to(DEV)
+    g, b = arrays["gamma"].to(DEV), arrays["beta"].to(DEV)
+    reps = 3   # a batch of 3 copies of the fixture batch
+    xr, gr, br = x.repeat(reps, 1, 1, 1), g.repeat(reps, 1), b.repeat(reps, 1)
     s = LatBandBlock(blk, 0, 1)
-    with pytest.raises(NotImplementedError):
-        s(arrays["x"].to(DEV), arrays["gamma"].to(DEV), arrays["beta"].to(DEV), 1.0)
+    with torch.no_grad():
+        y = s(xr, gr, br, meta["scale"], chunks=chunks).cpu()
+    want = arrays["y"].repeat(reps, 1, 1, 1)
+    assert (y - want).abs().max().item() < 1e-4
+
+
+def test_sharded_linear_weight_slice_is_the_rank_modes():
+    """The linear filter's weight is sharded by m-set: each rank's slice holds
+    exactly the tril modes whose m it owns, and the slices partition the modes."""
+    from msfno_amd.sfno import LatBandBlock
+    meta, params, arrays, _ = load([p for p in golden_files()
+                                    if os.path.basename(p) == "c1_lin_film_middle.npz"][0])
+    blk, _, _ = make_block(meta, params)
+    blk = blk.to(DEV)
+    lmax, mmax = meta["lmax"], meta["mmax"]
+    ii, jj = torch.tril_indices(lmax, mmax)
+    seen = []
+    for r in range(3):
+        s = LatBandBlock(blk, r, 3)
+        modes = s.plan.linear_modes()
+        assert modes == sorted(modes)
+        assert all(s.m_owner[int(jj[n])] == r for n in modes)
+        w = s._linear_weight(blk.filter_layer.filter.w)
+        assert w.shape[2] == len(modes)
+        assert torch.equal(w.cpu(), blk.filter_layer.filter.w.detach().cpu()[:, :, modes])
+        seen += modes
+    assert sorted(seen) == list(range(ii.shape[0]))
 
 
 @pytest.mark.slow
@@ -97,7 +132,7 @@ def test_sharded_block_config2_matches_unsharded():
     assert err < 2e-5, err
 
 
-def _dist_rank(rank, world, port, path, q):
+def _dist_rank(rank, world, port, path, q, chunks=1):
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
     for p in (here, os.path.dirname(here),
@@ -120,26 +155,31 @@ def _dist_rank(rank, world, port, path, q):
         x = arrays["x"][:, :, r0:r1].contiguous().to(DEV)
         with torch.no_grad():
             y = shard(x, arrays["gamma"].to(DEV), arrays["beta"].to(DEV), meta["scale"],
-                      comm=TorchComm())
+                      comm=TorchComm(), chunks=chunks)
         q.put((rank, y.cpu().numpy()))
     finally:
         dist.destroy_process_group()
 
 
-def test_sharded_block_two_processes_gloo():
+@pytest.mark.parametrize("name,chunks", [("c1b2_nl_film_middle.npz", 1),
+                                         ("c1b2_nl_film_middle.npz", 2),
+                                         ("c1b2_lin_film_middle.npz", 2),
+                                         ("down_nl_film_first.npz", 1)])
+def test_sharded_block_two_processes_gloo(name, chunks):
     """Two processes on the one GPU, collectives through torch.distributed (gloo,
-    host-staged): exercises TorchComm + the native stages end to end."""
+    host-staged): exercises TorchComm + the native stages end to end, with and
+    without the sub-batch pipeline."""
     import socket
 
     import torch.multiprocessing as mp
-    path = [p for p in golden_files() if os.path.basename(p) == "c1b2_nl_film_middle.npz"][0]
+    path = [p for p in golden_files() if os.path.basename(p) == name][0]
     meta, params, arrays, _ = load(path)
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
         port = s.getsockname()[1]
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    ps = [ctx.Process(target=_dist_rank, args=(r, 2, port, path, q)) for r in range(2)]
+    ps = [ctx.Process(target=_dist_rank, args=(r, 2, port, path, q, chunks)) for r in range(2)]
     for p in ps:
         p.start()
     try:
