@@ -1,0 +1,201 @@
+"""GPU parity at the BASELINE.json configurations the golden fixtures cannot hold.
+
+* Linear spectral filter at C=256 (the north-star "per-(l,m) complex spectral
+  weight multiply", SpectralConvS2, layers.py:336-427 / contractions.py:37-41):
+  the whole block on a 91x180 grid (lmax 45: a 0.54 GB weight the host oracle
+  can hold) against the oracle, and the C=256, lmax=360 contraction itself (34 GB
+  per-mode weight, drawn on the device) on a sample of modes against an fp64
+  einsum of those modes, at the batch sizes that select each kernel variant.
+* Config 3 at its real geometry: the 12-block FourierNeuralOperatorNet_Filmed
+  (721x1440 equiangular -> 120x240 Legendre-Gauss lmax 120 -> back, C=256,
+  73 channels, FiLM on the last block; sfnonet.py:699-860) against
+  oracle.sfno_ref.net_forward on the host.
+* Config 5 in shape: a 112-step autoregressive rollout (model.py:289-372) of a
+  12-block, 73-channel filmed network, stepped by msfno_amd.rollout.Rollout
+  (HIP-graph replay) and by the oracle, compared along the whole trajectory.
+  The grid is reduced (121x240 -> 30x60) so the host oracle finishes in
+  seconds; config 5's 721x1440 geometry per step is config 3's test.
+
+Bar: max-abs < 1e-4 * max(1, |y|) (the north-star tolerance) unless stated."""
+import pytest
+import torch
+
+from oracle import sfno_ref
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _threads():
+    torch.set_num_threads(max(1, min(16, torch.get_num_threads())))
+
+
+def _block(p, cfg, C, nlat, nlon, lmax, mmax):
+    from functools import partial
+
+    from msfno_amd.harmonics import InverseRealSHT, RealSHT
+    from msfno_amd.sfno import FourierNeuralOperatorBlock_Filmed
+    sht = RealSHT(nlat, nlon, lmax=lmax, mmax=mmax, grid="equiangular").float()
+    isht = InverseRealSHT(nlat, nlon, lmax=lmax, mmax=mmax, grid="equiangular").float()
+    sht.weights = sht.weights * 1e5
+    isht.pct = isht.pct / 1e5
+    norm = partial(torch.nn.InstanceNorm2d, num_features=C, eps=1e-6, affine=True,
+                   track_running_stats=False)
+    blk = FourierNeuralOperatorBlock_Filmed(sht, isht, C, filter_type=cfg.filter_type,
+                                            mlp_ratio=2.0, norm_layer=(norm, norm),
+                                            inner_skip=cfg.inner_skip, outer_skip=cfg.outer_skip,
+                                            mlp_mode="distributed" if cfg.has_mlp else "none",
+                                            spectral_layers=3)
+    blk.load_state_dict(p, strict=False)
+    return blk.eval().to(DEV)
+
+
+@pytest.mark.parametrize("B", [1, 2])
+def test_linear_filter_block_c256_matches_oracle(B):
+    """Linear filter, C=256, 91x180 lmax 45: the full filmed block vs the oracle."""
+    _threads()
+    C, nlat, nlon, lmax, mmax = 256, 91, 180, 45, 46
+    cfg = sfno_ref.BlockCfg(filter_type="linear")
+    p = sfno_ref.make_block_params(C, lmax, mmax, cfg, seed=5, randomize_affine=True)
+    g = torch.Generator().manual_seed(6)
+    x = torch.randn(B, C, nlat, nlon, generator=g)
+    gamma = 0.1 * torch.randn(B, C, generator=g)
+    beta = 0.1 * torch.randn(B, C, generator=g)
+    blk = _block(p, cfg, C, nlat, nlon, lmax, mmax)
+    with torch.no_grad():
+        y = blk(x.to(DEV), gamma.to(DEV), beta.to(DEV), 0.9).cpu()
+    o_sht, o_isht = sfno_ref.make_transforms(nlat, nlon, lmax, mmax)
+    with torch.no_grad():
+        want = sfno_ref.block_forward(p, x, o_sht, o_isht, cfg, gamma, beta, 0.9)
+    err = (y - want).abs().max().item()
+    print(f"linear C=256 91x180 B={B}: max-abs {err:.3e} |y|max {want.abs().max():.3f}")
+    assert err < 1e-4 * max(1.0, want.abs().max().item())
+
+
+@pytest.fixture(scope="module")
+def lmax360_weight():
+    """The C=256, lmax=360 per-mode weight (C, C, T, 2), T = |tril(360, 361)| =
+    64980: 34.1 GB, drawn on the device with the reference init 0.02*randn
+    (layers.py:386-387)."""
+    C, T = 256, 360 * 361 // 2
+    g = torch.Generator(device=DEV).manual_seed(11)
+    w = torch.empty(C, C, T, 2, device=DEV)
+    for i in range(C):  # row by row: keeps the generator's temporaries small
+        w[i] = 0.02 * torch.randn(C, T, 2, generator=g, device=DEV)
+    yield w
+    del w
+    torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("B", [1, 2, 8])
+def test_linear_contraction_c256_lmax360_sampled_modes(lmax360_weight, B):
+    """msfno_compl_contract_fwd_c at the config-2 size (the block's linear-filter
+    kernel: the LDS-DMA weight stream at B=1, the batched register kernels at
+    B=2 / 8) on 97 sampled modes, including the first and last, against an fp64
+    einsum of those modes."""
+    from msfno_amd.sfno.contractions import compl_contract_fwd_c
+    w = lmax360_weight
+    C, T = w.shape[0], w.shape[2]
+    g = torch.Generator(device=DEV).manual_seed(12 + B)
+    a = torch.randn(B, C, T, 2, generator=g, device=DEV)
+    y = compl_contract_fwd_c(a, w)
+    torch.cuda.synchronize()
+    gi = torch.Generator().manual_seed(13)
+    modes = torch.cat((torch.tensor([0, 1, T - 2, T - 1]),
+                       torch.randint(2, T - 2, (93,), generator=gi))).to(DEV)
+    ac = torch.view_as_complex(a[:, :, modes].double().contiguous())
+    wc = torch.view_as_complex(w[:, :, modes].double().contiguous())
+    want = torch.view_as_real(torch.einsum("bin,kin->bkn", ac, wc))
+    got = y[:, :, modes].double()
+    err = (got - want).abs().max().item()
+    scale = want.abs().max().item()
+    print(f"contract C=256 T={T} B={B}: max-abs {err:.3e} |y|max {scale:.3f}")
+    assert err < 2e-6 * max(1.0, scale)
+
+
+def test_config3_net_matches_oracle():
+    """Config 3: 12-block FourierNeuralOperatorNet_Filmed at 721x1440, C=256, 73
+    channels, film_layers 1 (the reference default), against the oracle."""
+    from msfno_amd.sfno import FourierNeuralOperatorNet_Filmed
+    _threads()
+    torch.manual_seed(21)
+    net = FourierNeuralOperatorNet_Filmed("cpu", None, film_layers=1, advanced_logging=False,
+                                          model_depth=None, img_size=(721, 1440), in_chans=73,
+                                          out_chans=73, embed_dim_sfno=256, num_layers=12,
+                                          filter_type="non-linear", spectral_layers=3).eval()
+    # reference-shaped parameters: the oracle takes the same state-dict keys
+    params = {k: v.detach().clone() for k, v in net.state_dict().items()
+              if not k.endswith((".weights", ".pct"))}
+    g = torch.Generator().manual_seed(22)
+    with torch.no_grad():  # non-trivial norms / biases / position embedding
+        for k, v in params.items():
+            if k.endswith("norm0.weight") or k.endswith("norm1.weight"):
+                v.copy_(1.0 + 0.1 * torch.randn(v.shape, generator=g))
+            elif k.endswith(".bias") or k == "pos_embed":
+                v.copy_(0.02 * torch.randn(v.shape, generator=g))
+    net.load_state_dict(params, strict=False)
+    net = net.to(DEV)
+    x = torch.randn(1, 73, 721, 1440, generator=g)
+    gamma = 0.1 * torch.randn(1, 1, 256, generator=g)
+    beta = 0.1 * torch.randn(1, 1, 256, generator=g)
+    with torch.no_grad():
+        got = net(x.to(DEV), torch.stack((gamma, beta), dim=1).to(DEV), 1.0).cpu()
+    del net
+    torch.cuda.empty_cache()
+    ncfg = sfno_ref.NetCfg(img_size=(721, 1440), scale_factor=6, num_layers=12)
+    with torch.no_grad():
+        want = sfno_ref.net_forward(params, x, ncfg, film=(gamma, beta), scale=1.0)
+    err = (got - want).abs().max().item()
+    rms = (got - want).pow(2).mean().sqrt().item()
+    print(f"config3 net: max-abs {err:.3e} rms {rms:.3e} |y|max {want.abs().max():.3f}")
+    assert got.shape == want.shape == (1, 73, 721, 1440)
+    assert err < 1e-4 * max(1.0, want.abs().max().item())
+
+
+@pytest.mark.parametrize("graph", [True, False])
+def test_rollout_112_steps_matches_oracle(graph):
+    """Config 5 in shape: 112 six-hour steps (28 days) of a 12-block, 73-channel
+    filmed network with normalisation (model.py:273-279), on the device, against
+    the oracle iterated on the host.  Every 8th step and the last are compared;
+    the rollout's outputs are collected without cloning (each must be its own
+    tensor)."""
+    from msfno_amd.rollout import Rollout
+    from msfno_amd.sfno import FourierNeuralOperatorNet_Filmed
+    _threads()
+    img, sf, C, ch, steps = (121, 240), 4, 32, 73, 112
+    torch.manual_seed(31)
+    net = FourierNeuralOperatorNet_Filmed("cpu", None, film_layers=1, advanced_logging=False,
+                                          model_depth=None, img_size=img, scale_factor=sf,
+                                          in_chans=ch, out_chans=ch, embed_dim_sfno=C,
+                                          num_layers=12, filter_type="non-linear",
+                                          spectral_layers=3).eval()
+    # decoder weights x6.5 over the reference init: with init-scale weights the state
+    # collapses to a fixed point within a few steps (a vacuous comparison); at x6.5
+    # it keeps moving at O(1) amplitude for all 112 steps without blowing up
+    params = {k: (6.5 * v if k.startswith("decoder.") and k.endswith("weight") else v)
+              for k, v in net.state_dict().items() if not k.endswith((".weights", ".pct"))}
+    net.load_state_dict(params, strict=False)
+    net = net.to(DEV)
+    g = torch.Generator().manual_seed(32)
+    means = torch.randn(1, ch, 1, 1, generator=g)
+    stds = torch.rand(1, ch, 1, 1, generator=g) + 0.5
+    x0 = torch.randn(1, ch, *img, generator=g) * stds + means
+    film = 0.1 * torch.randn(1, 2, 1, C, generator=g)
+    r = Rollout(net, means.to(DEV), stds.to(DEV), film=film.to(DEV), scale=1.0, graph=graph)
+    outs = [o for _, o in r.run(x0.to(DEV), steps)]
+    assert len({o.data_ptr() for o in outs}) == steps
+    ncfg = sfno_ref.NetCfg(img_size=img, scale_factor=sf, num_layers=12)
+    tr = sfno_ref.make_net_transforms(ncfg)
+    check = set(range(0, steps, 8)) | {steps - 1}
+    worst = 0.0
+    with torch.no_grad():
+        s = (x0 - means) / stds
+        for i in range(steps):
+            s = sfno_ref.net_forward(params, s, ncfg, transforms=tr,
+                                     film=(film[:, 0], film[:, 1]), scale=1.0)
+            if i in check:
+                want = s * stds + means
+                err = (outs[i].cpu() - want).abs().max().item() / max(1.0, want.abs().max().item())
+                worst = max(worst, err)
+                assert err < 1e-4, (i, err)
+    print(f"rollout {steps} steps (graph={graph}): worst relative max-abs {worst:.3e}")
