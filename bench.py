@@ -65,12 +65,14 @@ STAGE_KERNEL_X6 = {
     # fc2: h planes staged by LDS-DMA (x6p), bias + outer skip (EPI 3)
     "mlp_fc2": "void msfno::gemm_x6p_kernel<3, 2, 8, 256>(msfno::GemmParams)",
     "inner_skip": "void msfno::gemm_x6p_kernel<1, 2, 8, 256>(msfno::GemmParams)",
+    # fc1 -> GELU -> fc2 in one kernel, hidden activation on-chip (csrc/mlp_fused.hip)
+    "mlp_fused": "msfno::(anonymous namespace)::mlp_fused_kernel(msfno::(anonymous namespace)::MlpFusedParams)",
 }
 STAGE_KERNEL_F32 = {
     "mlp_fc1": "void msfno::gemm_f32_kernel<128, 256, 16, true, 5>(msfno::GemmParams)",
     "mlp_fc2": "void msfno::gemm_f32_kernel<256, 128, 16, true, 3>(msfno::GemmParams)",
 }
-X6_STAGES = {"mlp_fc1", "mlp_fc2", "inner_skip"}
+X6_STAGES = {"mlp_fc1", "mlp_fc2", "inner_skip", "mlp_fused"}
 X6_SPEC_STAGES = {"spectral_l0", "spectral_l1", "spectral_l2", "spectral_out"}
 
 
@@ -80,6 +82,13 @@ def x6_engine():
     dense = os.environ.get("MSFNO_GEMM", "") != "f32"
     spec = dense and not os.environ.get("MSFNO_SPEC_X6", "").startswith("0")
     return dense, spec
+
+
+def mlp_fused(C, hid):
+    """The block MLP runs as one fused kernel (csrc/mlp_fused.hip: C 256, H 512, x6
+    engine; MSFNO_MLP_FUSED=0 keeps the fc1 / fc2 GEMM pair): x1 then stays fp32."""
+    return x6_engine()[0] and C == 256 and hid == 512 and \
+        not os.environ.get("MSFNO_MLP_FUSED", "").startswith("0")
 
 
 def mfma_peak(stage):
@@ -165,6 +174,7 @@ def stage_work(name, B, C, nlat, nlon, lmax, mmax, hid, shid, rows=None, mset=No
     tab = {
         "mlp_fc1": ("mfma", 2 * B * P * C * hid),
         "mlp_fc2": ("mfma", 2 * B * P * C * hid),
+        "mlp_fused": ("mfma", 4 * B * P * C * hid),
         "inner_skip": ("mfma", 2 * B * P * C * C),
         "spectral_l0": ("mfma", 8 * B * T * C * shid),
         "spectral_l1": ("mfma", 8 * B * T * shid * shid),
@@ -178,8 +188,10 @@ def stage_work(name, B, C, nlat, nlon, lmax, mmax, hid, shid, rows=None, mset=No
         "fft_fwd": ("hbm", BC * rows * (nlon * 4 + mmax * 8 +
                                         (nlon * 6 if x6_engine()[0] and mset is None else 0))),
         # irfft: Yn read + skip-branch row read + x1 written (bf16x3 planes, 6 B per
-        # value, on the x6 engine with an MLP)
-        "fft_inv": ("hbm", BC * rows * (mmax * 8 + nlon * 4 + nlon * (6 if x6_engine()[0] else 4))),
+        # value, on the x6 engine with the unfused MLP; fp32 for the fused one)
+        "fft_inv": ("hbm", BC * rows * (mmax * 8 + nlon * 4 +
+                                        nlon * (6 if x6_engine()[0] and not mlp_fused(C, hid)
+                                                else 4))),
         "transpose_fwd": ("hbm", 2 * BC * rows * mmax * 8),
         "transpose_inv": ("hbm", 2 * BC * rows * mmax * 8),
         "linear_contract": ("hbm", 8 * C * C * T + 2 * 8 * BC * T),

@@ -157,7 +157,7 @@ static const char* kStageNames[MSFNO_PROF_NSTAGES] = {
     "spectral_l1", "spectral_l2", "spectral_l3", "spectral_out", "linear_gather",
     "linear_contract", "linear_scatter", "legendre_inv", "transpose_inv", "fft_inv",
     "inner_skip", "norm1_film_fold", "mlp_fc1", "mlp_fc2", "out_affine", "band_pack",
-    "band_gather", "band_scatter", "band_exchange", "end"};
+    "band_gather", "band_scatter", "band_exchange", "mlp_fused", "end"};
 
 struct Profiler {
   bool on = false;
@@ -569,18 +569,21 @@ void carve_block(Carve& cv, BlockBufs& b, const msfno_block_desc* d,
   b.st1 = nullptr;
   b.sc1 = b.sh1 = b.W1f = b.b1f = b.h = nullptr;
   b.x1p = nullptr;
+  b.mfimg = nullptr;
   if (!with_norms) return;
   b.x1 = cv.take<float>(BC * P);
   b.st1 = cv.take<float2>(BC * g->nlat);
   b.sc1 = cv.take<float>(BC);
   b.sh1 = cv.take<float>(BC);
-  if (d->has_mlp) {
+  if (mlp_fused(d, P)) {
+    b.mfimg = cv.take<unsigned short>(mlp_fused_image_bytes() / 2);
+  } else if (d->has_mlp) {
     const int64_t Hd = d->mlp_hidden;
     b.W1f = cv.take<float>((int64_t)B * Hd * C);
     b.b1f = cv.take<float>((int64_t)B * Hd);
     b.h = cv.take<float>(mlp_h_floats(B, Hd, P));
   }
-  b.x1p = x1_planes(d, g) ? cv.take<unsigned short>(BC * 3 * P) : nullptr;
+  b.x1p = x1p_buffer(d, g) ? cv.take<unsigned short>(BC * 3 * P) : nullptr;
   carve_dense_ws(cv, b.dw, d, B);
 }
 
@@ -1057,8 +1060,33 @@ bool x1_planes(const msfno_block_desc* d, const msfno_sht_plan_s* g) {
     const char* e = getenv("MSFNO_X1_PLANES");
     return !(e && e[0] == '0');
   }();
-  return on && d->has_mlp && mlp_h_planes(true) &&
+  return on && d->has_mlp && mlp_h_planes(true) && !mlp_fused(d, (int64_t)g->nlat * g->nlon) &&
          ((int64_t)g->nlat * g->nlon) % 8 == 0 && fft_c2r_planes_supported(g->fft, g->mmax);
+}
+
+bool mlp_fused(const msfno_block_desc* d, int64_t P) {
+  return d->has_mlp && gemm_use_x6() && d->fc1_b != nullptr && P % 4 == 0 && P >= 4 &&
+         mlp_fused_supported((int)d->C, (int)d->mlp_hidden);
+}
+
+bool x1p_buffer(const msfno_block_desc* d, const msfno_sht_plan_s* g) {
+  return x1_planes(d, g) || (mlp_fused(d, (int64_t)g->nlat * g->nlon) &&
+                             d->inner_skip == MSFNO_SKIP_LINEAR && mlp_h_planes(true));
+}
+
+int run_block_mlp(const msfno_block_desc* d, const float* x1, const unsigned short* x1p,
+                  const float* sc1, const float* sh1, float* W1f, float* b1f, float* h,
+                  unsigned short* mfimg, float* out, const float* resid, int B, int64_t P,
+                  const DenseWs& dw, hipStream_t s) {
+  MSFNO_REQUIRE(d->fc1_w && d->fc2_w, MSFNO_EINVAL, "missing MLP weights");
+  if (mfimg) {
+    prof(ST_MLP_FUSED, s);
+    MSFNO_TRY(launch_mlp_fused_images(d->fc1_w, d->fc2_w, mfimg, s));
+    return launch_mlp_fused(x1, sc1, sh1, resid, out, mfimg, d->fc1_b, d->fc2_b, B, P, s);
+  }
+  const int64_t C = d->C, Hd = d->mlp_hidden;
+  MSFNO_TRY(launch_fold_affine(d->fc1_w, d->fc1_b, sc1, sh1, W1f, b1f, B, (int)Hd, (int)C, s));
+  return run_mlp(d, W1f, b1f, x1, h, out, resid, B, P, dw, s, x1p);
 }
 
 // MLP hidden activation in the bf16x3 plane format (x6 engine; MSFNO_H_PLANES=0
@@ -1324,7 +1352,8 @@ int msfno_block_forward(const msfno_block_desc* d, msfno_sht_plan_t f, msfno_sht
   // ---- filter output + skip (+ GELU for the linear filter) -> x1, norm1 partials ---
   const float* skip_src = d->inner_skip == MSFNO_SKIP_LINEAR ? x1
                           : (d->inner_skip == MSFNO_SKIP_IDENTITY ? x : nullptr);
-  MSFNO_TRY(run_inverse_fft(g, b, B, (int)C, x1, skip_src, b.st1, act, s, b.x1p));
+  unsigned short* x1p = x1_planes(d, g) ? b.x1p : nullptr;  // irfft writes x1 as planes
+  MSFNO_TRY(run_inverse_fft(g, b, B, (int)C, x1, skip_src, b.st1, act, s, x1p));
   const int64_t np = g->nlat, cnt = g->nlon, cnt_last = g->nlon;
   // ---- norm1 (+ FiLM) as a per-(b,c) affine --------------------------------------
   prof(ST_NORM1, s);
@@ -1332,11 +1361,8 @@ int msfno_block_forward(const msfno_block_desc* d, msfno_sht_plan_t f, msfno_sht
                                d->norm_eps, gamma, beta, film_scale, b.sc1, b.sh1, s));
   const float* resid = d->outer_skip == MSFNO_SKIP_IDENTITY ? x : nullptr;
   if (d->has_mlp) {
-    MSFNO_REQUIRE(d->fc1_w && d->fc2_w, MSFNO_EINVAL, "missing MLP weights");
-    const int64_t Hd = d->mlp_hidden;
-    MSFNO_TRY(launch_fold_affine(d->fc1_w, d->fc1_b, b.sc1, b.sh1, b.W1f, b.b1f, B, (int)Hd,
-                                 (int)C, s));
-    MSFNO_TRY(run_mlp(d, b.W1f, b.b1f, x1, b.h, out, resid, B, P, b.dw, s, b.x1p));
+    MSFNO_TRY(run_block_mlp(d, x1, x1p, b.sc1, b.sh1, b.W1f, b.b1f, b.h, b.mfimg, out, resid, B,
+                            P, b.dw, s));
   } else {
     prof(ST_OUT_AFFINE, s);
     MSFNO_TRY(launch_affine_rows(x1, b.sc1, b.sh1, resid, out, BC, P, 0, nullptr, 0, s));

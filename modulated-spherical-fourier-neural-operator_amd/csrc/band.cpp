@@ -127,13 +127,15 @@ void carve_band(Carve& cv, BandBufs& b, const msfno_block_desc* d, const msfno_b
   }
   b.x1 = cv.take<float>(BC * Pout);
   b.W1f = b.b1f = b.h = nullptr;
-  if (d->has_mlp) {
+  if (mlp_fused(d, Pout)) {
+    b.fb.mfimg = cv.take<unsigned short>(mlp_fused_image_bytes() / 2);
+  } else if (d->has_mlp) {
     const int64_t Hd = d->mlp_hidden;
     b.W1f = cv.take<float>((int64_t)B * Hd * C);
     b.b1f = cv.take<float>((int64_t)B * Hd);
     b.h = cv.take<float>(mlp_h_floats(B, Hd, Pout));
   }
-  b.fb.x1p = (x1_planes(d, p->inv) && Pout % 8 == 0)
+  b.fb.x1p = (x1p_buffer(d, p->inv) && Pout % 8 == 0)
                  ? cv.take<unsigned short>(BC * 3 * std::max(Pin, Pout))
                  : nullptr;
   carve_dense_ws(cv, b.fb.dw, d, B);
@@ -436,7 +438,7 @@ int msfno_band_block_stage(const msfno_block_desc* d, msfno_band_plan_t p, int s
       const C2RPlanes x1p{b.fb.x1p, (int)C, p->rows_out};
       MSFNO_TRY(launch_fft_c2r_rows(p->inv->fft, b.Xn, b.x1, skip_src, b.rs, BC * p->rows_out,
                                     p->mmax, d->filter_type == MSFNO_FILTER_LINEAR ? 1 : 0, s,
-                                    b.fb.x1p ? &x1p : nullptr));
+                                    (b.fb.x1p && x1_planes(d, p->inv)) ? &x1p : nullptr));
       prof(ST_NORM1, s);
       MSFNO_TRY(launch_stats_partial(b.rs, p->rows_out, p->nlon_out, BC, io->stats_local, s));
       prof(ST_END, s);
@@ -454,12 +456,9 @@ int msfno_band_block_stage(const msfno_block_desc* d, msfno_band_plan_t p, int s
       MSFNO_REQUIRE(d->outer_skip != MSFNO_SKIP_IDENTITY || io->x, MSFNO_EINVAL,
                     "stage 4 needs x for the outer skip");
       if (d->has_mlp) {
-        MSFNO_REQUIRE(d->fc1_w && d->fc2_w, MSFNO_EINVAL, "missing MLP weights");
-        const int64_t Hd = d->mlp_hidden;
-        MSFNO_TRY(launch_fold_affine(d->fc1_w, d->fc1_b, b.sc1, b.sh1, b.W1f, b.b1f, B, (int)Hd,
-                                     (int)C, s));
-        MSFNO_TRY(run_mlp(d, b.W1f, b.b1f, b.x1, b.h, io->out, resid, B, Pout, b.fb.dw, s,
-                          b.fb.x1p));
+        MSFNO_TRY(run_block_mlp(d, b.x1, x1_planes(d, p->inv) ? b.fb.x1p : nullptr, b.sc1, b.sh1,
+                                b.W1f, b.b1f, b.h, b.fb.mfimg, io->out, resid, B, Pout, b.fb.dw,
+                                s));
       } else {
         prof(ST_OUT_AFFINE, s);
         MSFNO_TRY(launch_affine_rows(b.x1, b.sc1, b.sh1, resid, io->out, BC, Pout, 0, nullptr, 0,

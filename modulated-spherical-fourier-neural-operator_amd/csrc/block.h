@@ -10,7 +10,7 @@ enum Stage {
   ST_FFT_FWD = 0, ST_NORM0, ST_TRANSPOSE_FWD, ST_LEG_FWD, ST_SPEC_PREP, ST_SPEC_L0, ST_SPEC_L1,
   ST_SPEC_L2, ST_SPEC_L3, ST_SPEC_OUT, ST_LIN_GATHER, ST_LIN_CONTRACT, ST_LIN_SCATTER, ST_LEG_INV,
   ST_TRANSPOSE_INV, ST_FFT_INV, ST_SKIP, ST_NORM1, ST_FC1, ST_FC2, ST_OUT_AFFINE, ST_BAND_PACK,
-  ST_BAND_GATHER, ST_BAND_SCATTER, ST_BAND_EXCHANGE, ST_END
+  ST_BAND_GATHER, ST_BAND_SCATTER, ST_BAND_EXCHANGE, ST_MLP_FUSED, ST_END
 };
 void prof(int stage, hipStream_t s);
 
@@ -56,6 +56,7 @@ struct BlockBufs {
   unsigned short* x1p;  // x1 as bf16x3 planes for fc1 (x6 engine), else null
   unsigned short* Xtp;  // x6 Legendre: forward slabs as bf16x3 planes, else null
   unsigned short* Sp;   // x6 Legendre: filter output S as planes [plane][R][ldT]
+  unsigned short* mfimg;  // fused MLP weight image (mlp_fused), else null
   DenseWs dw;
 };
 
@@ -82,6 +83,17 @@ int run_mlp(const msfno_block_desc* d, const float* W1f, const float* b1f, const
             float* h, float* out, const float* resid, int B, int64_t P, const DenseWs& dw,
             hipStream_t s, const unsigned short* x1p = nullptr);
 bool mlp_h_planes(bool have_ws);
+// the block MLP as one fused kernel (mlp_fused.hip): x6 engine, C 256, H 512, fc1 bias,
+// P % 4 == 0 (16-B rows for the kernel's LDS-DMA tile staging)
+bool mlp_fused(const msfno_block_desc* d, int64_t P);
+// x1p buffer needed: x1 planes from the irfft, or x planes from the rfft for the skip GEMM
+bool x1p_buffer(const msfno_block_desc* d, const msfno_sht_plan_s* g);
+// MLP stage of the block on x1 (fp32, or planes x1p when x1_planes): norm1/FiLM affine
+// (sc1, sh1) applied in the fused kernel, or folded into (W1f, b1f) for run_mlp
+int run_block_mlp(const msfno_block_desc* d, const float* x1, const unsigned short* x1p,
+                  const float* sc1, const float* sh1, float* W1f, float* b1f, float* h,
+                  unsigned short* mfimg, float* out, const float* resid, int B, int64_t P,
+                  const DenseWs& dw, hipStream_t s);
 int64_t mlp_chunk(int64_t P);
 int64_t mlp_h_floats(int B, int64_t Hd, int64_t P);
 bool x1_planes(const msfno_block_desc* d, const msfno_sht_plan_s* g);

@@ -76,6 +76,15 @@ int launch_fold_affine(const float* W, const float* bias, const float* scale, co
 int launch_affine_rows(const float* x, const float* scale, const float* shift,
                        const float* addend, float* out, int64_t BC, int64_t P, int act,
                        float2* stats, int stats_ld, hipStream_t s);
+// ---- mlp_fused.hip: the block MLP with the hidden activation on-chip ----------
+// out = W2·GELU(W1·(scale ⊙ x1 + shift) + b1) + b2 (+ resid), C = 256, H = 512 only
+bool mlp_fused_supported(int C, int H);
+size_t mlp_fused_image_bytes();
+// W1 (H x C), W2 (C x H) fp32 -> the kernel's bf16x3 weight image (mlp_fused_image_bytes)
+int launch_mlp_fused_images(const float* W1, const float* W2, unsigned short* img, hipStream_t s);
+int launch_mlp_fused(const float* x1, const float* scale, const float* shift, const float* resid,
+                     float* out, const unsigned short* img, const float* b1, const float* b2,
+                     int B, int64_t P, hipStream_t s);
 // ---- cgemm.hip -----------------------------------------------------------------
 // complex (Ci,Co,2) weight -> Ar, Ai (Co x Ci) row-major (Ar[o][i] = Re w[i][o])
 int launch_split_complex_weight(const float* w, float* Ar, float* Ai, int Ci, int Co,

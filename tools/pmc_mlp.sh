@@ -1,0 +1,9 @@
+#!/bin/bash
+# PMC passes over the fused block MLP kernel inside bench.py (one field, config 2):
+#   bash tools/pmc_mlp.sh <outdir> [ENV=VAL ...]  (run on the GPU box from the repo root)
+O=${1:-gpurun_out/pmc_mlp}; shift
+for kv in "$@"; do export "$kv"; done
+cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT && mkdir -p $O
+K="--kernel-include-regex mlp_fused_kernel"
+timeout -s KILL 120 rocprofv3 $K --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_INST_LDS SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_MFMA SQ_INSTS_VALU --kernel-trace -d $O/p1 -o p1 -f csv -- python3 bench.py --steps 2 --warmup 1 --cpu-baseline 0 > $O/p1.txt 2>&1 && \
+timeout -s KILL 120 rocprofv3 $K --pmc GRBM_GUI_ACTIVE SQ_WAIT_INST_ANY SQ_INSTS_LDS SQ_ACTIVE_INST_VALU SQ_INST_LEVEL_LDS SQ_INSTS_SALU SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT --kernel-trace -d $O/p2 -o p2 -f csv -- python3 bench.py --steps 2 --warmup 1 --cpu-baseline 0 > $O/p2.txt 2>&1
