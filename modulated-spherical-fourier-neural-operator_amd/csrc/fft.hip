@@ -1242,6 +1242,9 @@ static int launch_c2r(const FFTArgs& a, const float2* in, float* x, const float*
         MSFNO_TRY(go(fft_c2r_dma_kernel<CL, true, 4, 1, true>, 4, per));
       else if (planes)
         MSFNO_TRY(go(fft_c2r_dma_kernel<CL, false, 4, 1, true>, 4, per));
+      else if (addsrc && areg && tw + 16 * per_reg <= 160 * 1024)
+        // fp32 x1 for the fused MLP: the same 16-wave register-skip kernel
+        MSFNO_TRY(go(fft_c2r_dma_kernel<CL, true, 16, 1, false, true>, 16, per_reg));
       else if (addsrc)
         MSFNO_TRY(go(fft_c2r_dma_kernel<CL, true, 4, 1, false>, 4, per));
       else
