@@ -127,7 +127,19 @@ typedef struct msfno_block_desc {
   const float* skip_w; const float* skip_b;         /* inner_skip (C,C,1,1), (C)    */
   const float* fc1_w; const float* fc1_b;           /* mlp.fwd.0 (H,C,1,1), (H)     */
   const float* fc2_w; const float* fc2_b;           /* mlp.fwd.2 (C,H,1,1), (C)     */
+  /* Prepared-weight cache (optional).  The kernels consume the weights as bf16x3
+   * "images" (the spectral-MLP 3M A images, the fused block MLP's slice image).
+   * wcache: device buffer of msfno_block_wcache_size(d) bytes owned by the caller
+   * (one per module), or NULL: the images are rebuilt in the workspace on every
+   * call.  wcache_valid = 1: wcache already holds the images of the current weight
+   * values (the call skips the preparation); 0: the call rebuilds them into
+   * wcache.  The caller tracks weight changes (the Python mirror keys it on the
+   * parameters' (data_ptr, _version)). */
+  void* wcache;
+  int wcache_valid;
 } msfno_block_desc;
+
+size_t msfno_block_wcache_size(const msfno_block_desc* d);
 
 size_t msfno_block_workspace_size(const msfno_block_desc* d, msfno_sht_plan_t fwd,
                                   msfno_sht_plan_t inv, int B);

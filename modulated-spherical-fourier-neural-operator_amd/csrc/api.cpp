@@ -552,7 +552,13 @@ void carve_block(Carve& cv, BlockBufs& b, const msfno_block_desc* d,
       const int64_t co = (l == d->spectral_layers) ? C : Hs;
       b.Wexp[l] = cv.take<float>(4 * ci * co);
     }
-    carve_spec_ws(cv, b.dw, d);
+    if (d->wcache) {
+      Carve wc;
+      wc.base = static_cast<char*>(d->wcache);
+      carve_spec_ws(wc, b.dw, d);
+    } else {
+      carve_spec_ws(cv, b.dw, d);
+    }
   } else {
     b.xt = cv.take<float>(BC * L.T * 2);
     b.yt = cv.take<float>(BC * L.T * 2);
@@ -576,7 +582,8 @@ void carve_block(Carve& cv, BlockBufs& b, const msfno_block_desc* d,
   b.sc1 = cv.take<float>(BC);
   b.sh1 = cv.take<float>(BC);
   if (mlp_fused(d, P)) {
-    b.mfimg = cv.take<unsigned short>(mlp_fused_image_bytes() / 2);
+    b.mfimg = wcache_mfimg(d);
+    if (!b.mfimg) b.mfimg = cv.take<unsigned short>(mlp_fused_image_bytes() / 2);
   } else if (d->has_mlp) {
     const int64_t Hd = d->mlp_hidden;
     b.W1f = cv.take<float>((int64_t)B * Hd * C);
@@ -618,6 +625,29 @@ int64_t spec_hidden_floats(int B, int64_t Hs, const SpecLayout& L) {
   return std::max<int64_t>((int64_t)B * 2 * Hs * L.ldT,
                            cdiv((int64_t)B * planes * Hs * round_up(L.Tp, 8) * 2, 4));
 }
+
+// prepared-weight cache layout (msfno_block_desc.wcache): the spectral images
+// (carve_spec_ws order), then the fused MLP image
+static size_t wcache_layout(const msfno_block_desc* d, unsigned short** mfimg) {
+  Carve wc;
+  wc.base = static_cast<char*>(d->wcache);
+  DenseWs w;
+  if (d->filter_type == MSFNO_FILTER_NONLINEAR) carve_spec_ws(wc, w, d);
+  unsigned short* m = nullptr;
+  if (d->has_mlp && gemm_use_x6() && d->fc1_b && mlp_fused_supported((int)d->C, (int)d->mlp_hidden))
+    m = wc.take<unsigned short>(mlp_fused_image_bytes() / 2);
+  if (mfimg) *mfimg = m;
+  return wc.off;
+}
+
+unsigned short* wcache_mfimg(const msfno_block_desc* d) {
+  if (!d->wcache) return nullptr;
+  unsigned short* m = nullptr;
+  wcache_layout(d, &m);
+  return m;
+}
+
+bool wcache_ready(const msfno_block_desc* d) { return d->wcache && d->wcache_valid; }
 
 // split-A planes of the real-ified spectral MLP weights (x6 engine)
 void carve_spec_ws(Carve& cv, DenseWs& w, const msfno_block_desc* d) {
@@ -674,7 +704,7 @@ int run_filter(const msfno_block_desc* d, msfno_sht_plan_s* f, msfno_sht_plan_s*
         sw.out[l] = static_cast<unsigned short*>(b.dw.spec[l]);
       }
       spec_weights_3m_layout(sw);
-      MSFNO_TRY(launch_spec_weights_3m(sw, s));
+      if (!wcache_ready(d)) MSFNO_TRY(launch_spec_weights_3m(sw, s));
       const int ldTx = (int)round_up(L.Tp, 8);
       unsigned short* cur = reinterpret_cast<unsigned short*>(b.Sc);
       MSFNO_TRY(launch_split3m(b.Sa, cur, B, (int)C, (int)L.Tp, (int)L.ldT, ldTx, s));
@@ -701,7 +731,7 @@ int run_filter(const msfno_block_desc* d, msfno_sht_plan_s* f, msfno_sht_plan_s*
         sw.out[l] = static_cast<unsigned short*>(b.dw.spec[l]);
       }
       spec_weights_x6p_layout(sw);
-      MSFNO_TRY(launch_spec_weights_x6p(sw, s));
+      if (!wcache_ready(d)) MSFNO_TRY(launch_spec_weights_x6p(sw, s));
     }
     for (int l = 0; l <= nl; ++l) {
       const int ci = (l == 0) ? (int)C : (int)Hs;
@@ -1081,7 +1111,8 @@ int run_block_mlp(const msfno_block_desc* d, const float* x1, const unsigned sho
   MSFNO_REQUIRE(d->fc1_w && d->fc2_w, MSFNO_EINVAL, "missing MLP weights");
   if (mfimg) {
     prof(ST_MLP_FUSED, s);
-    MSFNO_TRY(launch_mlp_fused_images(d->fc1_w, d->fc2_w, mfimg, s));
+    if (!(wcache_ready(d) && mfimg == wcache_mfimg(d)))
+      MSFNO_TRY(launch_mlp_fused_images(d->fc1_w, d->fc2_w, mfimg, s));
     return launch_mlp_fused(x1, sc1, sh1, resid, out, mfimg, d->fc1_b, d->fc2_b, B, P, s);
   }
   const int64_t C = d->C, Hd = d->mlp_hidden;
@@ -1111,7 +1142,7 @@ using namespace msfno;
 extern "C" {
 
 const char* msfno_last_error(void) { return g_last_error.c_str(); }
-int msfno_abi_version(void) { return 2; }
+int msfno_abi_version(void) { return 3; }
 
 int msfno_quadrature(int nlat, int grid, double* nodes, double* weights) {
   std::vector<double> x, w;
@@ -1254,6 +1285,13 @@ int msfno_compl_mul2d_fwd_c(const float* a, const float* w, float* y, int B, int
   MSFNO_REQUIRE(a && w && y && B > 0 && Ci > 0 && Co > 0 && XY > 0, MSFNO_EINVAL,
                 "bad compl_mul2d_fwd_c arguments");
   return launch_compl_mul2d(a, w, y, B, Ci, Co, XY, relu_real, (hipStream_t)stream);
+}
+
+size_t msfno_block_wcache_size(const msfno_block_desc* d) {
+  if (!d) return 0;
+  msfno_block_desc t = *d;
+  t.wcache = nullptr;
+  return wcache_layout(&t, nullptr);
 }
 
 size_t msfno_block_workspace_size(const msfno_block_desc* d, msfno_sht_plan_t f,

@@ -120,7 +120,13 @@ void carve_band(Carve& cv, BandBufs& b, const msfno_block_desc* d, const msfno_b
       const int64_t co = (l == d->spectral_layers) ? C : Hs;
       b.fb.Wexp[l] = cv.take<float>(4 * ci * co);
     }
-    carve_spec_ws(cv, b.fb.dw, d);
+    if (d->wcache) {
+      Carve wc;
+      wc.base = static_cast<char*>(d->wcache);
+      carve_spec_ws(wc, b.fb.dw, d);
+    } else {
+      carve_spec_ws(cv, b.fb.dw, d);
+    }
   } else {
     b.fb.xt = cv.take<float>(std::max<int64_t>(BC * L.T * 2, 4));
     b.fb.yt = cv.take<float>(std::max<int64_t>(BC * L.T * 2, 4));
@@ -128,7 +134,8 @@ void carve_band(Carve& cv, BandBufs& b, const msfno_block_desc* d, const msfno_b
   b.x1 = cv.take<float>(BC * Pout);
   b.W1f = b.b1f = b.h = nullptr;
   if (mlp_fused(d, Pout)) {
-    b.fb.mfimg = cv.take<unsigned short>(mlp_fused_image_bytes() / 2);
+    b.fb.mfimg = wcache_mfimg(d);
+    if (!b.fb.mfimg) b.fb.mfimg = cv.take<unsigned short>(mlp_fused_image_bytes() / 2);
   } else if (d->has_mlp) {
     const int64_t Hd = d->mlp_hidden;
     b.W1f = cv.take<float>((int64_t)B * Hd * C);

@@ -83,6 +83,10 @@ int run_mlp(const msfno_block_desc* d, const float* W1f, const float* b1f, const
             float* h, float* out, const float* resid, int B, int64_t P, const DenseWs& dw,
             hipStream_t s, const unsigned short* x1p = nullptr);
 bool mlp_h_planes(bool have_ws);
+// prepared-weight cache (msfno_block_desc.wcache): the fused MLP image inside it (or
+// null), and whether the cached images are current (the preparation is skipped)
+unsigned short* wcache_mfimg(const msfno_block_desc* d);
+bool wcache_ready(const msfno_block_desc* d);
 // the block MLP as one fused kernel (mlp_fused.hip): x6 engine, C 256, H 512, fc1 bias,
 // P % 4 == 0 (16-B rows for the kernel's LDS-DMA tile staging)
 bool mlp_fused(const msfno_block_desc* d, int64_t P);

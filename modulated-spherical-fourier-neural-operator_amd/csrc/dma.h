@@ -32,6 +32,28 @@ __device__ __forceinline__ void glds16(const void* gsrc, uint32_t lds) {
       : "memory");
 }
 
+// six wave-instructions in one block (one m0 save / restore): lane l copies 16 B
+// from sbase + voff[i] to LDS byte lds + i * lds_step + 16 l.  sbase and lds must be
+// wave-uniform (SGPR operands); voff[i] are the lane's byte offsets (SADDR + VADDR
+// form, instruction offset 0); m0 advances by lds_step between the pieces.
+template <int LDS_STEP>
+__device__ __forceinline__ void glds16x6(uint64_t sbase, const uint32_t (&voff)[6], uint32_t lds) {
+  unsigned keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %8\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %2, %1\n\t"
+      "s_add_u32 m0, m0, %9\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %3, %1\n\t"
+      "s_add_u32 m0, m0, %9\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %4, %1\n\t"
+      "s_add_u32 m0, m0, %9\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %5, %1\n\t"
+      "s_add_u32 m0, m0, %9\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %6, %1\n\t"
+      "s_add_u32 m0, m0, %9\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %7, %1\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "s"(sbase), "v"(voff[0]), "v"(voff[1]), "v"(voff[2]), "v"(voff[3]), "v"(voff[4]),
+        "v"(voff[5]), "s"(lds), "i"(LDS_STEP)
+      : "memory");
+}
+
 // s_waitcnt vmcnt(n) for a run-time n, rounded down to a supported immediate
 // (waiting for more than needed is safe)
 __device__ __forceinline__ void wait_vmcnt(int n) {

@@ -157,7 +157,8 @@ template <int SCHED, int STAMP, int DBG = 0, int MF_AHEAD = 2>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
 void mlp_fused_kernel(MlpFusedParams p) {
   // DBG (diagnostic timing builds only, wrong results): 1 no ring waits / barriers /
-  // refills in the steps, 2 no MFMAs
+  // refills in the steps, 2 no MFMAs, 4 no GELU / split of the hidden blocks, 8 the
+  // A fragments of every k-step re-use the first k-step's (no ds_reads in the loop)
   // diagnostic phase clock (MSFNO_MF_STAMPS=1; never in the product launch): wave 0 of
   // each workgroup records s_memtime at phase boundaries and the cycles it spent in
   // the ring waits + barriers
@@ -191,14 +192,17 @@ void mlp_fused_kernel(MlpFusedParams p) {
   const bool valid = px < P;
 
   const uint32_t ring_lds = lds_addr(ring);
-  auto issue = [&](int q) {
-    const unsigned short* src = mf_slice_src(p, q) + lane * 8;
-    const uint32_t base = ring_lds + (uint32_t)((q % MF_NS) * MF_SLICE_ELEMS * 2);
+  // slice q -> ring slot q % 4: this wave's 1-KB pieces wave + 4 i, one asm block with
+  // SGPR bases (wave-uniform) and the lane offset in a VGPR
+  const int wave_u = __builtin_amdgcn_readfirstlane(wave);
+  static_assert(MF_PIECES == 6, "glds16x6");
+  uint32_t piece_off[6];  // piece wave + 4 i: byte offset i * 4 KB + the lane's 16 B
 #pragma unroll
-    for (int i = 0; i < MF_PIECES; ++i) {
-      const int piece = wave + MF_WAVES * i;
-      glds16(src + piece * 512, base + (uint32_t)(piece * 1024));
-    }
+  for (int i = 0; i < 6; ++i) piece_off[i] = (uint32_t)(i * MF_WAVES * 1024 + lane * 16);
+  auto issue = [&](int q) {
+    const uint64_t src = reinterpret_cast<uint64_t>(mf_slice_src(p, q)) + (uint64_t)wave_u * 1024;
+    const uint32_t base = ring_lds + (uint32_t)((q % MF_NS) * MF_SLICE_ELEMS * 2 + wave_u * 1024);
+    glds16x6<MF_WAVES * 1024>(src, piece_off, base);
   };
   // a [256 channel][128 pixel] fp32 tile of a (B, C, P) tensor -> LDS by LDS-DMA:
   // 1-KB piece i = channel rows 2i, 2i + 1; pixels past P are clamped (P % 4 == 0)
@@ -330,6 +334,10 @@ void mlp_fused_kernel(MlpFusedParams p) {
   uint32_t hfu[2][3][4];  // fc2 B fragments as bf16 pairs [k-step s][plane][pair]
   auto conv_pair = [&](int j, int e2, auto par_c) {
     constexpr int PAR = decltype(par_c)::value;
+    if constexpr ((DBG & 4) != 0) {
+      hfu[e2 >> 2][0][e2 & 3] = __float_as_uint(hacc[PAR][2 * e2]);
+      return;
+    }
     const int r = 2 * e2;
     const float2 b = *reinterpret_cast<const float2*>(b1s + 32 * j + (r >> 2) * 8 + 4 * half + (r & 3));
     f32x2 v = {hacc[PAR][r] + b.x, hacc[PAR][r + 1] + b.y};
@@ -356,13 +364,13 @@ void mlp_fused_kernel(MlpFusedParams p) {
         a[k][pl] = *reinterpret_cast<const bf16x8*>(slot + (pl * 8 + k) * 512 + a_lane);
 #pragma unroll
     for (int ks = 0; ks < 8; ++ks) {
-      if (ks + MF_AHEAD < 8) {
+      if (ks + MF_AHEAD < 8 && (DBG & 8) == 0) {
 #pragma unroll
         for (int pl = 0; pl < 3; ++pl)
           a[(ks + MF_AHEAD) % (MF_AHEAD + 1)][pl] =
               *reinterpret_cast<const bf16x8*>(slot + (pl * 8 + ks + MF_AHEAD) * 512 + a_lane);
       }
-      hacc[PAR] = mfma6(a[ks % (MF_AHEAD + 1)], xf[KH * 8 + ks], hacc[PAR]);
+      hacc[PAR] = mfma6(a[(DBG & 8) ? 0 : ks % (MF_AHEAD + 1)], xf[KH * 8 + ks], hacc[PAR]);
       if (ks == 0) refill(q);
       if constexpr (CONV) {
         if (ks & 1) conv_pair(jc, 4 * KH + (ks >> 1), PPrev{});
@@ -387,7 +395,7 @@ void mlp_fused_kernel(MlpFusedParams p) {
       for (int pl = 0; pl < 3; ++pl) a[k][pl] = *reinterpret_cast<const bf16x8*>(slot + aoff(k, pl));
 #pragma unroll
     for (int it = 0; it < 8; ++it) {
-      if (it + MF_AHEAD < 8) {
+      if (it + MF_AHEAD < 8 && (DBG & 8) == 0) {
 #pragma unroll
         for (int pl = 0; pl < 3; ++pl)
           a[(it + MF_AHEAD) % (MF_AHEAD + 1)][pl] =
@@ -397,7 +405,8 @@ void mlp_fused_kernel(MlpFusedParams p) {
       const bf16x8 hb[3] = {mf_frag(hfu[s][0][0], hfu[s][0][1], hfu[s][0][2], hfu[s][0][3]),
                             mf_frag(hfu[s][1][0], hfu[s][1][1], hfu[s][1][2], hfu[s][1][3]),
                             mf_frag(hfu[s][2][0], hfu[s][2][1], hfu[s][2][2], hfu[s][2][3])};
-      oacc[OH * 4 + (it >> 1)] = mfma6(a[it % (MF_AHEAD + 1)], hb, oacc[OH * 4 + (it >> 1)]);
+      oacc[OH * 4 + (it >> 1)] =
+          mfma6(a[(DBG & 8) ? 0 : it % (MF_AHEAD + 1)], hb, oacc[OH * 4 + (it >> 1)]);
       if (it == 0) refill(q);
       kstep_schedule(it + MF_AHEAD < 8);
     }
@@ -531,6 +540,12 @@ int mlp_fused_stamped(MlpFusedParams p, int64_t tiles, int sched, hipStream_t s)
     hipLaunchKernelGGL((mlp_fused_kernel<1, 1, 1>), dim3((unsigned)tiles), dim3(256), 0, s, p);
   else if (dbg == 2)
     hipLaunchKernelGGL((mlp_fused_kernel<1, 1, 2>), dim3((unsigned)tiles), dim3(256), 0, s, p);
+  else if (dbg == 4)
+    hipLaunchKernelGGL((mlp_fused_kernel<1, 1, 4>), dim3((unsigned)tiles), dim3(256), 0, s, p);
+  else if (dbg == 8)
+    hipLaunchKernelGGL((mlp_fused_kernel<1, 1, 8>), dim3((unsigned)tiles), dim3(256), 0, s, p);
+  else if (dbg == 13)
+    hipLaunchKernelGGL((mlp_fused_kernel<1, 1, 13>), dim3((unsigned)tiles), dim3(256), 0, s, p);
   else if (sched)
     hipLaunchKernelGGL((mlp_fused_kernel<1, 1>), dim3((unsigned)tiles), dim3(256), 0, s, p);
   else

@@ -45,6 +45,7 @@ class BlockDesc(ctypes.Structure):
         ("spec_w", _vp * 8), ("spec_wout", _vp), ("lin_w", _vp),
         ("skip_w", _vp), ("skip_b", _vp),
         ("fc1_w", _vp), ("fc1_b", _vp), ("fc2_w", _vp), ("fc2_b", _vp),
+        ("wcache", _vp), ("wcache_valid", _i),
     ]
 
 
@@ -85,6 +86,7 @@ SIGNATURES = [
     ("msfno_compl_contract_fwd_c", _i, [_vp, _vp, _vp, _i, _i, _i, _i, _vp]),
     ("msfno_compl_mul2d_fwd_c", _i, [_vp, _vp, _vp, _i, _i, _i, ctypes.c_longlong, _i, _vp]),
     ("msfno_block_workspace_size", _sz, [ctypes.POINTER(BlockDesc), _vp, _vp, _i]),
+    ("msfno_block_wcache_size", _sz, [ctypes.POINTER(BlockDesc)]),
     ("msfno_block_forward", _i, [ctypes.POINTER(BlockDesc), _vp, _vp, _vp, _vp, _vp, _f, _vp,
                                  _i, _vp, _sz, _vp]),
     ("msfno_filter_forward", _i, [ctypes.POINTER(BlockDesc), _vp, _vp, _vp, _vp, _i, _vp, _sz,

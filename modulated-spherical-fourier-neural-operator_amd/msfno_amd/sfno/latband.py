@@ -394,6 +394,7 @@ class LatBandBlock:
             gamma = gamma.detach().float().reshape(B, C).contiguous()
             beta = beta.detach().float().reshape(B, C).contiguous()
         L = N.lib()
+        wkey = self.block.wcache_attach(d, keep, x.device)  # prepared-weight images
         bufs = self._buffers(B, C, slot)
         nbytes = L.msfno_band_workspace_size(d, self.plan.handle, B)
         ws = torch.empty(nbytes, dtype=torch.uint8, device=x.device)
@@ -423,6 +424,7 @@ class LatBandBlock:
         st2 = yield ("all_gather", bufs["stats"])
         io.stats_all = st2.data_ptr()
         stage(4)
+        self.block.wcache_commit(wkey)
         del keep, st, st2
         return out
 

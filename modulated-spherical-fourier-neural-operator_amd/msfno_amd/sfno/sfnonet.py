@@ -172,6 +172,32 @@ class FourierNeuralOperatorBlock(nn.Module):
     def _transforms(self):
         return self.filter_layer.filter._transforms()
 
+    def wcache_attach(self, d, keep, device):
+        """Point the descriptor at this module's prepared-weight cache (bf16x3 weight
+        images, msfno_block_desc.wcache) and mark it valid when the weights are
+        unchanged since it was filled: keyed on every tensor the descriptor points
+        at, by (data_ptr, _version).  Returns the key to pass to wcache_commit once
+        the native call has been issued.  In-place weight updates bump _version, so
+        the next call rebuilds the images; a HIP graph captured with a valid cache
+        replays without the preparation (weights frozen, as in Rollout)."""
+        L = N.lib()
+        nbytes = L.msfno_block_wcache_size(d)
+        if nbytes == 0:
+            return None
+        buf = getattr(self, "_wcache_buf", None)
+        if buf is None or buf.device != device or buf.numel() < nbytes:
+            buf = self._wcache_buf = torch.empty(nbytes, dtype=torch.uint8, device=device)
+            self._wcache_key = None
+        key = (str(device), nbytes) + tuple((t.data_ptr(), t._version) for t in keep
+                                            if isinstance(t, torch.Tensor))
+        d.wcache = buf.data_ptr()
+        d.wcache_valid = int(key == getattr(self, "_wcache_key", None))
+        return key
+
+    def wcache_commit(self, key):
+        if key is not None:
+            self._wcache_key = key
+
     @N.on_input_device
     def _native_forward(self, x, gamma=None, beta=None, scale=1.0):
         dtype = x.dtype
@@ -186,6 +212,7 @@ class FourierNeuralOperatorBlock(nn.Module):
             gamma = gamma.detach().float().reshape(B, C).contiguous()
             beta = beta.detach().float().reshape(B, C).contiguous()
         L = N.lib()
+        wkey = self.wcache_attach(d, keep, x.device)
         nbytes = L.msfno_block_workspace_size(d, pf.handle, pi.handle, B)
         ws = torch.empty(nbytes, dtype=torch.uint8, device=x.device)
         out = torch.empty(B, C, inv.nlat, inv.nlon, dtype=torch.float32, device=x.device)
@@ -193,6 +220,7 @@ class FourierNeuralOperatorBlock(nn.Module):
                                       N.ptr(beta), float(scale), out.data_ptr(), B, ws.data_ptr(),
                                       nbytes, N.stream_of(x.device)),
                 type(self).__name__ + ".forward")
+        self.wcache_commit(wkey)
         del keep
         return out.to(dtype)
 

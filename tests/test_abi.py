@@ -32,13 +32,15 @@ def test_library_exports_every_declared_symbol():
         assert hasattr(lib, s), s
     # and the ctypes binding covers all of them
     assert {n for n, _, _ in N.SIGNATURES} == set(_declared_symbols())
-    assert lib.msfno_abi_version() == 2
+    assert lib.msfno_abi_version() == 3
 
 
 def test_block_desc_struct_layout():
     from msfno_amd import _native as N
-    # 8 ints + float, 4 norm ptrs, 8 spec_w, wout, lin_w, 6 more pointers
-    assert ctypes.sizeof(N.BlockDesc) == 9 * 4 + 4 + (4 + 8 + 2 + 6) * 8
+    # 8 ints + float, 4 norm ptrs, 8 spec_w, wout, lin_w, 6 more pointers, the weight
+    # cache pointer and its valid flag (padded to 8)
+    assert ctypes.sizeof(N.BlockDesc) == 9 * 4 + 4 + (4 + 8 + 2 + 6 + 1) * 8 + 8
+    assert N.BlockDesc.wcache.offset == 9 * 4 + 4 + (4 + 8 + 2 + 6) * 8
 
 
 @pytest.mark.parametrize("grid", ["equiangular", "legendre-gauss"])

@@ -112,3 +112,29 @@ def test_fused_equals_unfused_gemm_pair(tmp_path):
 
 if __name__ == "__main__":
     np.savez(sys.argv[1], **{f"c{i}": _native(c).numpy() for i, c in enumerate(CASES[:2])})
+
+
+def test_weight_cache_reuse_and_invalidation():
+    """The prepared-weight cache (msfno_block_desc.wcache): the second call reuses the
+    images (same output), an in-place weight update (a new _version) rebuilds them
+    (the output follows the new weights, equal to a fresh module's)."""
+    case = CASES[0]
+    cfg, p, x, gamma, beta = _case(*case)
+    blk = _block(cfg, p, *case[1:4])
+    x, gamma, beta = x.to(DEV), gamma.to(DEV), beta.to(DEV)
+    with torch.no_grad():
+        y0 = blk(x, gamma, beta, 0.7)
+        assert blk._wcache_key is not None
+        y1 = blk(x, gamma, beta, 0.7)
+        assert torch.equal(y0, y1)
+        blk.mlp.fwd[0].weight.mul_(1.25)                     # fused-MLP image
+        blk.filter_layer.filter.w[1].mul_(0.8)               # spectral 3M images
+        y2 = blk(x, gamma, beta, 0.7)
+    p2 = {k: v.clone() for k, v in p.items()}
+    p2["mlp.fwd.0.weight"] = p2["mlp.fwd.0.weight"] * 1.25
+    p2["filter_layer.filter.w.1"] = p2["filter_layer.filter.w.1"] * 0.8
+    fresh = _block(cfg, p2, *case[1:4])
+    with torch.no_grad():
+        want = fresh(x, gamma, beta, 0.7)
+    assert (y2 - y0).abs().max().item() > 1e-3
+    assert torch.equal(y2, want)
