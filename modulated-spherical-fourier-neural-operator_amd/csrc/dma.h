@@ -39,6 +39,10 @@ __device__ __forceinline__ void glds16(const void* gsrc, uint32_t lds) {
 template <int LDS_STEP>
 __device__ __forceinline__ void glds16x6(uint64_t sbase, const uint32_t (&voff)[6], uint32_t lds) {
   unsigned keep;
+  // make the uniformity explicit (SGPR operands)
+  sbase = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(sbase >> 32)) << 32) |
+          (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)sbase);
+  lds = (uint32_t)__builtin_amdgcn_readfirstlane((int)lds);
   asm volatile(
       "s_mov_b32 %0, m0\n\t"
       "s_mov_b32 m0, %8\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %2, %1\n\t"

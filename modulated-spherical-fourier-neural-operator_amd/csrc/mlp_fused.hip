@@ -334,15 +334,16 @@ void mlp_fused_kernel(MlpFusedParams p) {
   uint32_t hfu[2][3][4];  // fc2 B fragments as bf16 pairs [k-step s][plane][pair]
   auto conv_pair = [&](int j, int e2, auto par_c) {
     constexpr int PAR = decltype(par_c)::value;
+    uint32_t (&h)[2][3][4] = hfu;
     if constexpr ((DBG & 4) != 0) {
-      hfu[e2 >> 2][0][e2 & 3] = __float_as_uint(hacc[PAR][2 * e2]);
+      h[e2 >> 2][0][e2 & 3] = __float_as_uint(hacc[PAR][2 * e2]);
       return;
     }
     const int r = 2 * e2;
     const float2 b = *reinterpret_cast<const float2*>(b1s + 32 * j + (r >> 2) * 8 + 4 * half + (r & 3));
     f32x2 v = {hacc[PAR][r] + b.x, hacc[PAR][r + 1] + b.y};
     v = gelu_erf2(v);
-    split2(v.x, v.y, hfu[e2 >> 2][0][e2 & 3], hfu[e2 >> 2][1][e2 & 3], hfu[e2 >> 2][2][e2 & 3]);
+    split2(v.x, v.y, h[e2 >> 2][0][e2 & 3], h[e2 >> 2][1][e2 & 3], h[e2 >> 2][2][e2 & 3]);
   };
 
   // fc1 slice W1(j, KH) into hacc[PAR]; CONV: pairs 4 KH .. 4 KH + 3 of block jc
@@ -402,9 +403,10 @@ void mlp_fused_kernel(MlpFusedParams p) {
               *reinterpret_cast<const bf16x8*>(slot + aoff(it + MF_AHEAD, pl));
       }
       const int s = it & 1;
-      const bf16x8 hb[3] = {mf_frag(hfu[s][0][0], hfu[s][0][1], hfu[s][0][2], hfu[s][0][3]),
-                            mf_frag(hfu[s][1][0], hfu[s][1][1], hfu[s][1][2], hfu[s][1][3]),
-                            mf_frag(hfu[s][2][0], hfu[s][2][1], hfu[s][2][2], hfu[s][2][3])};
+      const uint32_t (&h)[2][3][4] = hfu;
+      const bf16x8 hb[3] = {mf_frag(h[s][0][0], h[s][0][1], h[s][0][2], h[s][0][3]),
+                            mf_frag(h[s][1][0], h[s][1][1], h[s][1][2], h[s][1][3]),
+                            mf_frag(h[s][2][0], h[s][2][1], h[s][2][2], h[s][2][3])};
       oacc[OH * 4 + (it >> 1)] =
           mfma6(a[(DBG & 8) ? 0 : it % (MF_AHEAD + 1)], hb, oacc[OH * 4 + (it >> 1)]);
       if (it == 0) refill(q);
@@ -546,6 +548,7 @@ int mlp_fused_stamped(MlpFusedParams p, int64_t tiles, int sched, hipStream_t s)
     hipLaunchKernelGGL((mlp_fused_kernel<1, 1, 8>), dim3((unsigned)tiles), dim3(256), 0, s, p);
   else if (dbg == 13)
     hipLaunchKernelGGL((mlp_fused_kernel<1, 1, 13>), dim3((unsigned)tiles), dim3(256), 0, s, p);
+
   else if (sched)
     hipLaunchKernelGGL((mlp_fused_kernel<1, 1>), dim3((unsigned)tiles), dim3(256), 0, s, p);
   else
@@ -615,7 +618,7 @@ int launch_mlp_fused(const float* x1, const float* scale, const float* shift, co
   // MSFNO_MF_SCHED=0: no explicit MFMA / VALU interleave (the compiler's schedule), for A/B
   static const int sched = [] {
     const char* e = getenv("MSFNO_MF_SCHED");
-    return (e && e[0] == '0') ? 0 : 1;
+    return e ? atoi(e) : 1;
   }();
   static const bool stamps = [] {
     const char* e = getenv("MSFNO_MF_STAMPS");
@@ -630,6 +633,7 @@ int launch_mlp_fused(const float* x1, const float* scale, const float* shift, co
   const dim3 grid((unsigned)tiles), blk(256);
   if (!sched)
     hipLaunchKernelGGL((mlp_fused_kernel<0, 0, 0, 2>), grid, blk, 0, s, p);
+
   else if (ahead == 1)
     hipLaunchKernelGGL((mlp_fused_kernel<1, 0, 0, 1>), grid, blk, 0, s, p);
   else if (ahead == 3)
