@@ -202,6 +202,14 @@ int side_ctx(SideCtx** out, hipStream_t caller) {
   }
   *out = nullptr;
   if (!enabled) return MSFNO_OK;
+  // no fork while the caller's stream is being captured into a HIP graph: the
+  // captured fork/join made a 12-block network step 19.0 ms instead of 12.4 ms
+  // (replayed, config 3); the graph runs the skip GEMM in line
+  if (caller) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(caller, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone)
+      return MSFNO_OK;
+  }
   // one side stream + fork/join pair per (device, caller stream): the device comes
   // from the caller's stream (not the thread's current device), and two caller
   // streams never share fork/join events

@@ -13,6 +13,8 @@ residual adds live in GEMM epilogues.  Inference semantics (no autograd graph).
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.nn as nn
 
@@ -58,6 +60,10 @@ class FiLM(nn.Module):
 
 def _is_exact_gelu(m):
     return isinstance(m, nn.GELU) and getattr(m, "approximate", "none") == "none"
+
+
+# MSFNO_WCACHE=0: rebuild the weight images on every call (A/B of the prepared-weight cache)
+_WCACHE = not os.environ.get("MSFNO_WCACHE", "").startswith("0")
 
 
 class FourierNeuralOperatorBlock(nn.Module):
@@ -182,7 +188,7 @@ class FourierNeuralOperatorBlock(nn.Module):
         replays without the preparation (weights frozen, as in Rollout)."""
         L = N.lib()
         nbytes = L.msfno_block_wcache_size(d)
-        if nbytes == 0:
+        if nbytes == 0 or not _WCACHE:
             return None
         buf = getattr(self, "_wcache_buf", None)
         if buf is None or buf.device != device or buf.numel() < nbytes:
