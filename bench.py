@@ -593,12 +593,11 @@ def main():
         from msfno_amd.sfno import LatBandBlock, TorchComm
         B = args.batch * world
         shard = LatBandBlock(blk, rank, world, device=dev)
-        r0, r1 = shard.rows
-        rows, mset = r1 - r0, [m for m, o in enumerate(shard.m_owner) if o == rank]
+        rows, mset = len(shard.rows), [m for m, o in enumerate(shard.m_owner) if o == rank]
         gd = torch.Generator(device=dev).manual_seed(0)
         x = torch.empty(B, C, rows, args.nlon, device=dev)
         for b in range(B):  # field b is identical on every rank; keep this rank's rows
-            x[b] = torch.randn(C, args.nlat, args.nlon, generator=gd, device=dev)[:, r0:r1]
+            x[b] = shard.take(torch.randn(1, C, args.nlat, args.nlon, generator=gd, device=dev))[0]
         gamma = 0.1 * torch.randn(B, C, generator=gd, device=dev)
         beta = 0.1 * torch.randn(B, C, generator=gd, device=dev)
         comm = TorchComm() if dist else None

@@ -216,9 +216,15 @@ int msfno_mlp_backward_input(const msfno_mlp_desc* d, const float* x, const floa
  * Latitude-band sharded SFNO-Block (multi-GPU form of
  * msfno_block_forward).  The reference runs one block per process on the whole
  * field (DDP = replicas, MSFNO/main.py:1153); this splits ONE field batch over
- * `world` ranks: rank r owns latitude rows [row_start[r], row_start[r+1]) for
- * every pointwise / FFT / 1x1-conv / MLP stage and the zonal wavenumbers
- * {m : m_owner[m] == r} for the Legendre transforms and the spectral filter.
+ * `world` ranks.  row_start (world + 1 entries) partitions the northern half of
+ * the grid, rows [0, nlat - nlat/2) (the equator row of an odd grid included):
+ * rank r owns the band [row_start[r], row_start[r+1]) and the mirror rows
+ * nlat-1-k of its band rows k < nlat/2, for every pointwise / FFT / 1x1-conv /
+ * MLP stage (msfno_band_local_rows lists them: the band ascending, then the
+ * mirrors ascending), and the zonal wavenumbers {m : m_owner[m] == r} for the
+ * Legendre transforms and the spectral filter.  Owning mirror pairs keeps the
+ * hemisphere fold of the symmetric Legendre transform local, and the exchange
+ * buffers are the Legendre GEMMs' own operands (no re-layout pass).
  * The caller (Python, torch.distributed over RCCL) performs the collectives
  * between the stages; the library never communicates:
  *
@@ -245,15 +251,20 @@ int msfno_mlp_backward_input(const msfno_mlp_desc* d, const float* x, const floa
  * ------------------------------------------------------------------------- */
 typedef struct msfno_band_plan_s* msfno_band_plan_t;
 
-/* Default partition (host only, no GPU): balanced contiguous latitude bands and
+/* Default partition (host only, no GPU): balanced bands of the northern half and
  * a zig-zag (snake) assignment of m = 0..mact-1 that balances both the count of
  * m and the Legendre/filter work sum(lmax - m) per rank; m >= lmax -> -1. */
 int msfno_band_partition(int world, int nlat, int lmax, int mmax, int* row_start, int* m_owner);
 /* all-to-all element counts (floats) per peer for `rank` (host only):
- * phase 0 (spectra rows->m), phase 1 (m->rows); R = 2*B*C. */
+ * phase 0 (spectra rows->m), phase 1 (m->rows); R = 2*B*C.  Every exchanged slab
+ * row holds 2W floats, W = the widest band rounded up to 16. */
 int msfno_band_exchange_counts(int world, int rank, int nlat, int mmax, const int* row_start,
                                const int* m_owner, int R, int phase, long long* send_counts,
                                long long* recv_counts);
+/* The global latitude rows of `rank`'s local rows, in local order (rows may be
+ * NULL to query *count = band rows + mirror rows). */
+int msfno_band_local_rows(int world, int rank, int nlat, const int* row_start, int* rows,
+                          int* count);
 int msfno_band_plan_create(int nlat, int nlon, int lmax, int mmax, int world, int rank,
                            const int* row_start, const int* m_owner, msfno_band_plan_t* plan);
 /* Resampling form: rows of the input grid (nlat_in x nlon_in, the forward
@@ -277,7 +288,7 @@ int msfno_band_plan_load_tables(msfno_band_plan_t plan, const float* fwd_table,
                                 const float* inv_table, void* stream);
 
 typedef struct msfno_band_io {
-  const float* x;           /* (B, C, rows_local, nlon)                         */
+  const float* x;           /* (B, C, rows_local, nlon), msfno_band_local_rows  */
   const float* gamma;       /* (B, C) or NULL                                   */
   const float* beta;        /* (B, C) or NULL                                   */
   float film_scale;

@@ -285,6 +285,43 @@ int ensure_desc(msfno_sht_plan_s* p, int R, int other_ld, int64_t ldT) {
     GemmDesc g{};
     g.M = R;
     g.flags = flags;
+    if (p->band_world) {
+      // band plan: A (forward) / C (inverse) is the exchange buffer [p][slab][R][2W],
+      // its K / N index the exchange columns (segmented in the launch, legendre_*)
+      const int W = p->band_W, ld = 2 * W, Kb = p->band_K();
+      const int64_t bs = (int64_t)p->slab[m] * R * ld;
+      if (!p->sym) {
+        if (!p->inverse) {
+          g.N = L.Lp[m]; g.K = Kb; g.lda = ld; g.ldb = L.Lp[m]; g.ldc = (int)ldT;
+          g.offA = bs; g.offB = p->tab_off[m]; g.offC = L.off[m];
+        } else {
+          g.N = Kb; g.K = L.Lp[m]; g.lda = (int)ldT; g.ldb = Kb; g.ldc = ld;
+          g.offA = L.off[m]; g.offB = p->tab_off[m]; g.offC = bs;
+        }
+        push(g);
+      } else if (!p->inverse) {
+        GemmDesc e = g;  // even: Xs (R x Kb) . We (Kb x Lpe)
+        e.N = lpe; e.K = Kb; e.lda = ld; e.ldb = lpe; e.ldc = (int)ldT;
+        e.offA = bs; e.offB = p->tab_off[m]; e.offC = L.off[m];
+        push(e);
+        if (lo > 0) {
+          GemmDesc o = g;  // odd: Xa (R x Kb) . Wo (Kb x Lpo)
+          o.N = lpo; o.K = Kb; o.lda = ld; o.ldb = lpo; o.ldc = (int)ldT;
+          o.offA = bs + W; o.offB = p->tab_off[m] + (int64_t)Kb * lpe; o.offC = L.off[m] + lpe;
+          push(o);
+        }
+      } else {
+        GemmDesc e = g;  // even: E (R x Kb) = S_e (R x Le) . Pe (Le x Kb)
+        e.N = Kb; e.K = le; e.lda = (int)ldT; e.ldb = Kb; e.ldc = ld;
+        e.offA = L.off[m]; e.offB = p->tab_off[m]; e.offC = bs;
+        push(e);
+        GemmDesc o = g;  // odd: O (R x Kb); K = 0 writes zeros (the receiver reads O)
+        o.N = Kb; o.K = lo; o.lda = (int)ldT; o.ldb = Kb; o.ldc = ld;
+        o.offA = L.off[m] + lpe; o.offB = p->tab_off[m] + (int64_t)lpe * Kb; o.offC = bs + W;
+        push(o);
+      }
+      continue;
+    }
     if (!p->sym) {
       if (!p->inverse) {
         g.N = L.Lp[m]; g.K = p->nlat;
@@ -519,6 +556,10 @@ int legendre_fwd(msfno_sht_plan_s* f, const float* Xt, float* S, int R, hipStrea
   GemmEpi e;
   e.rowscale = rowscale;
   e.rs_C = C;
+  if (f->band_world) {  // Xt is the phase-0 receive buffer: one block per source rank
+    e.segA_w = f->band_seg();
+    e.segA_stride = (int64_t)f->nslab * R * 2 * f->band_W;
+  }
   return gemm_desc(leg_tile(0), Xt, f->table, S, f->d_desc, f->ndesc,
                    f->desc_tiles, e, s);
 }
@@ -526,6 +567,10 @@ int legendre_fwd(msfno_sht_plan_s* f, const float* Xt, float* S, int R, hipStrea
 int legendre_inv(msfno_sht_plan_s* g, const float* S, float* Yt, int R, hipStream_t s) {
   MSFNO_TRY(ensure_desc(g, R, 0, g->spec.ldT));
   GemmEpi e;
+  if (g->band_world) {  // Yt is the phase-1 send buffer: one block per destination rank
+    e.segC_w = g->band_seg();
+    e.segC_stride = (int64_t)g->nslab * R * 2 * g->band_W;
+  }
   return gemm_desc(leg_tile(1), S, g->table, Yt, g->d_desc, g->ndesc,
                    g->desc_tiles, e, s);
 }
@@ -923,13 +968,17 @@ void set_table_offsets(msfno_sht_plan_s* p, int sym) {
     p->tab_off[m] = acc;
     if (L.L[m] == 0) continue;
     const int64_t lpe = L.Lpe[m], lpo = L.Lp[m] - L.Lpe[m];
+    if (p->band_world) {  // band plans: W / P blocks over the band_K() exchange columns
+      acc += (int64_t)p->band_K() * L.Lp[m];
+      continue;
+    }
     if (!sym)
       acc += p->inverse ? (int64_t)L.Lp[m] * p->ldk : (int64_t)p->nlat * L.Lp[m];
     else
       acc += p->inverse ? lpe * p->ldke + lpo * round_up(p->Ko, 4)
                         : (int64_t)p->Ke * lpe + (int64_t)p->Ko * lpo;
   }
-  if (!sym) p->table_elems = acc;
+  p->table_elems = acc;
 }
 
 int plan_create(int nlat, int nlon, int lmax, int mmax, int inverse,
@@ -957,7 +1006,8 @@ int plan_create(int nlat, int nlon, int lmax, int mmax, int inverse,
   // table sized for the general (non-symmetric) layout, the larger of the two
   set_table_offsets(p, 0);
   const int64_t acc = p->table_elems;
-  hipError_t e = hipMalloc(&p->table, std::max<int64_t>(acc, 4) * sizeof(float));
+  p->table_cap = std::max<int64_t>(acc, 4);
+  hipError_t e = hipMalloc(&p->table, p->table_cap * sizeof(float));
   if (e == hipSuccess) e = hipMalloc(&p->d_tab_off, mmax * sizeof(int64_t));
   if (e == hipSuccess) e = hipMalloc(&p->d_Lp, mmax * sizeof(int));
   if (e == hipSuccess) e = hipMalloc(&p->d_off, mmax * sizeof(int));
@@ -1186,6 +1236,7 @@ int msfno_sht_plan_destroy(msfno_sht_plan_t p) {
   if (p->d_tabx_offe) (void)hipFree(p->d_tabx_offe);
   if (p->d_tabx_offo) (void)hipFree(p->d_tabx_offo);
   if (p->d_descx) (void)hipFree(p->d_descx);
+  if (p->d_kmap) (void)hipFree(p->d_kmap);
   delete p;
   return MSFNO_OK;
 }
@@ -1212,13 +1263,26 @@ int msfno_sht_plan_load_table(msfno_sht_plan_t p, const float* table, void* stre
   }
   p->sym = sym;
   set_table_offsets(p, sym);
+  if (p->table_elems > p->table_cap) {  // band plans: the exchange layout can be larger
+    MSFNO_CHECK_HIP(hipFree(p->table));
+    p->table = nullptr;
+    p->table_cap = p->table_elems;
+    MSFNO_CHECK_HIP(hipMalloc(&p->table, p->table_cap * sizeof(float)));
+  }
+  if (p->band_world) {
+    const std::vector<int>& km = sym ? p->kmap_sym : p->kmap_gen;
+    if (!p->d_kmap)
+      MSFNO_CHECK_HIP(hipMalloc(&p->d_kmap, p->kmap_gen.size() * sizeof(int)));
+    MSFNO_CHECK_HIP(hipMemcpy(p->d_kmap, km.data(), km.size() * sizeof(int),
+                              hipMemcpyHostToDevice));
+  }
   MSFNO_CHECK_HIP(hipMemcpy(p->d_tab_off, p->tab_off.data(), p->mmax * sizeof(int64_t),
                             hipMemcpyHostToDevice));
   p->desc_R = -1;  // descriptors depend on the layout
   MSFNO_TRY(launch_relayout_table(*p, table, s));
   p->descx_R = -1;
   // the bf16x3 table image only feeds the x6 Legendre GEMMs (MSFNO_LEG_X6=1)
-  if (sym && leg_x6_enabled()) MSFNO_TRY(build_table_x6(p, table, s));
+  if (sym && leg_x6_enabled() && !p->band_world) MSFNO_TRY(build_table_x6(p, table, s));
   p->table_loaded = 1;
   return MSFNO_OK;
 }

@@ -2,13 +2,21 @@
 // the five per-rank stages between which the caller runs the collectives
 // (include/msfno.h, "Latitude-band sharded SFNO-Block").
 //
-// Exchange layout.  Spectra leave stage 1 as slabs (R = 2BC rows, H_r latitude
-// columns), one slab per owned-elsewhere m, ordered by (owner, m): the
-// all-to-all block for rank q is then contiguous.  perm[m] is that slab index
-// (the same order is used for the return trip in stage 3).  On the owner the
-// received blocks are per source band p: (nm_r * R, H_p) at offset
-// nm_r * R * row0[p]; band_copy re-assembles full-latitude (nm_r, R, ldk) slabs
-// for the Legendre GEMMs and splits them again afterwards.
+// Ownership.  row_start partitions the northern half [0, Ke) of the grid (Ke =
+// nlat - nlat/2, the equator row included); rank r owns its band [a, b) and the
+// mirror rows nlat-1-k of the band rows k < nlat/2.  Its local rows are the band
+// ascending, then the mirrors ascending, so local row H-1-i is the mirror of local
+// row i: the hemisphere fold of the symmetric Legendre transform is local.
+//
+// Exchange layout.  Every slab row has 2W floats (W = the widest band rounded up
+// to 16): [Xs | Xa] folded on a symmetric plan, the local rows on a general one,
+// zero padded.  Slabs leave stage 1 ordered by (owner of m, m), so the block for
+// each peer is contiguous, and the receiver's buffer [source p][slab][R][2W] is
+// read by the forward Legendre GEMM directly (its K index runs over the source
+// blocks, common.h msfno_sht_plan_s band fields); the inverse GEMM writes the
+// phase-1 send buffer [destination p][slab][R][2W] the same way.  No re-layout
+// pass between the FFTs and the Legendre GEMMs beyond the one transpose each way
+// that the unsharded block has too.
 #include <algorithm>
 #include <cmath>
 #include <cstring>
@@ -23,16 +31,15 @@ struct msfno_band_plan_s {
   // the last block back)
   int nlat_in = 0, nlon_in = 0, nlat_out = 0, nlon_out = 0;
   int lmax = 0, mmax = 0, world = 0, rank = 0;
-  std::vector<int> row_in, row_out;  // world + 1 band boundaries on each grid
+  std::vector<int> row_in, row_out;  // world + 1 band boundaries (northern half) on each grid
+  int W_in = 0, W_out = 0;           // exchange slab rows hold 2W floats
   std::vector<int> owner;            // per m, -1: no coefficients (m >= lmax)
   std::vector<int> nm_of;            // per rank: number of owned m
-  int rows_in = 0, rows_out = 0;     // local latitude rows
+  int rows_in = 0, rows_out = 0;     // local latitude rows (band + mirrors)
   int nm = 0;                        // local m count
   int mact = 0;                      // global count of m with lmax - m > 0
   msfno_sht_plan_s* fwd = nullptr;
   msfno_sht_plan_s* inv = nullptr;
-  int* d_row_in = nullptr;
-  int* d_row_out = nullptr;
   int* d_perm = nullptr;
   // inner-skip join events, one per in-flight sub-batch slot (msfno_band_io.slot):
   // several sub-batches of one forward can be between stage 0 and stage 3 at once
@@ -42,10 +49,53 @@ struct msfno_band_plan_s {
 
 namespace {
 
+struct BandRows {
+  int a, b, bw, np, H;  // band [a, b), bw = b - a, np mirrored rows, H = bw + np
+};
+BandRows band_rows(int nlat, const int* rs, int r) {
+  BandRows o;
+  o.a = rs[r];
+  o.b = rs[r + 1];
+  o.bw = o.b - o.a;
+  o.np = std::max(0, std::min(o.b, nlat / 2) - o.a);
+  o.H = o.bw + o.np;
+  return o;
+}
+int band_width(int world, const int* rs) {
+  int w = 1;
+  for (int r = 0; r < world; ++r) w = std::max(w, rs[r + 1] - rs[r]);
+  return (int)round_up(w, 16);
+}
+// global latitude of local row i of rank r
+int band_global_row(int nlat, const BandRows& o, int i) {
+  return i < o.bw ? o.a + i : nlat - (o.a + o.np) + (i - o.bw);
+}
+// this rank's local rows as a small symmetric grid for the pack / unpack transposes
+LatGeom band_geom(const msfno_sht_plan_s* sp, const BandRows& o, int W) {
+  return LatGeom{sp->sym, o.H, o.np, o.bw, o.np, W, 2 * W};
+}
+// exchange-column -> latitude maps of a band plan (common.h msfno_sht_plan_s)
+void set_band_maps(msfno_sht_plan_s* sp, int world, const int* rs, int W) {
+  sp->band_world = world;
+  sp->band_W = W;
+  sp->kmap_sym.assign((size_t)world * W, -1);
+  sp->kmap_gen.assign((size_t)world * 2 * W, -1);
+  for (int p = 0; p < world; ++p) {
+    const BandRows o = band_rows(sp->nlat, rs, p);
+    for (int j = 0; j < o.bw; ++j) sp->kmap_sym[(size_t)p * W + j] = o.a + j;
+    for (int i = 0; i < o.H; ++i)
+      sp->kmap_gen[(size_t)p * 2 * W + i] = band_global_row(sp->nlat, o, i);
+  }
+}
+
+}  // namespace
+
+namespace {
+
 int validate_rows(int world, int nlat, const int* row_start) {
   MSFNO_REQUIRE(row_start, MSFNO_EINVAL, "null row partition");
-  MSFNO_REQUIRE(row_start[0] == 0 && row_start[world] == nlat, MSFNO_EINVAL,
-                "row_start must run from 0 to nlat");
+  MSFNO_REQUIRE(row_start[0] == 0 && row_start[world] == nlat - nlat / 2, MSFNO_EINVAL,
+                "row_start must run from 0 to nlat - nlat/2 (the northern half and equator)");
   for (int r = 0; r < world; ++r)
     MSFNO_REQUIRE(row_start[r + 1] > row_start[r], MSFNO_EINVAL,
                   "every rank needs at least one latitude row");
@@ -65,19 +115,17 @@ int validate_partition(int world, int nlat, int lmax, int mmax, const int* row_s
   return MSFNO_OK;
 }
 
-// counts (floats) per peer: phase 0 sends my input rows of q's m-set, phase 1 my
-// m-set's slabs of q's output rows
-void exchange_counts(int world, int rank, const std::vector<int>& nm, const int* row_in,
-                     const int* row_out, long long R, int phase, long long* sc, long long* rc) {
+// counts (floats) per peer: phase 0 sends my rows of q's m-set, phase 1 my m-set's
+// slabs of q's rows; every slab row is 2W floats (W_in / W_out of the two grids)
+void exchange_counts(int world, int rank, const std::vector<int>& nm, int W_in, int W_out,
+                     long long R, int phase, long long* sc, long long* rc) {
   for (int q = 0; q < world; ++q) {
     if (phase == 0) {
-      const long long hr = row_in[rank + 1] - row_in[rank], hq = row_in[q + 1] - row_in[q];
-      sc[q] = nm[q] * R * hr;
-      rc[q] = nm[rank] * R * hq;
+      sc[q] = nm[q] * R * 2 * W_in;
+      rc[q] = nm[rank] * R * 2 * W_in;
     } else {
-      const long long hr = row_out[rank + 1] - row_out[rank], hq = row_out[q + 1] - row_out[q];
-      sc[q] = nm[rank] * R * hq;
-      rc[q] = nm[q] * R * hr;
+      sc[q] = nm[rank] * R * 2 * W_out;
+      rc[q] = nm[q] * R * 2 * W_out;
     }
   }
 }
@@ -86,7 +134,6 @@ struct BandBufs {
   float2* Xn;   // (BC, max(rows_in, rows_out), mmax) spectra of local rows; reused as Yn
   float2* rs;   // (BC, max rows) row (mean, M2), norm0 then norm1
   float *sc0, *sh0, *sc1, *sh1;
-  float* Xt;    // (nm, R, max ldk) full-latitude slabs; reused as Yt
   BlockBufs fb; // filter buffers (Sa, Sb, Sc, Wexp / xt, yt) in the local spectral layout
   float* x1;    // (B, C, rows_out*nlon_out)
   float *W1f, *b1f, *h;
@@ -107,8 +154,6 @@ void carve_band(Carve& cv, BandBufs& b, const msfno_block_desc* d, const msfno_b
   b.sh0 = cv.take<float>(BC);
   b.sc1 = cv.take<float>(BC);
   b.sh1 = cv.take<float>(BC);
-  b.Xt = cv.take<float>(std::max<int64_t>((int64_t)p->nm * R * std::max(p->fwd->ldk, p->inv->ldk),
-                                          4));
   std::memset(&b.fb, 0, sizeof(b.fb));
   b.fb.Sa = cv.take<float>(R * L.ldT);
   if (d->filter_type == MSFNO_FILTER_NONLINEAR) {
@@ -183,9 +228,13 @@ extern "C" {
 
 int msfno_band_partition(int world, int nlat, int lmax, int mmax, int* row_start, int* m_owner) {
   MSFNO_REQUIRE(world >= 1 && world <= 64, MSFNO_EUNSUPPORTED, "band sharding needs 1..64 ranks");
-  MSFNO_REQUIRE(nlat >= world, MSFNO_EINVAL, "need at least one latitude row per rank");
+  const int ke = nlat - nlat / 2;
+  MSFNO_REQUIRE(ke >= world, MSFNO_EINVAL,
+                "need at least one northern latitude row per rank (nlat - nlat/2 >= world)");
   MSFNO_REQUIRE(lmax > 0 && mmax > 0 && row_start && m_owner, MSFNO_EINVAL, "bad partition args");
-  const int q = nlat / world, rem = nlat % world;
+  // bands of the northern half (+ equator); the equator row (odd nlat) has no
+  // mirror, so the last band takes the smaller share
+  const int q = ke / world, rem = ke % world;
   row_start[0] = 0;
   for (int r = 0; r < world; ++r) row_start[r + 1] = row_start[r] + q + (r < rem ? 1 : 0);
   // snake over m ascending (work lmax - m descending): 0..W-1, W-1..0, ...
@@ -213,7 +262,20 @@ int msfno_band_exchange_counts(int world, int rank, int nlat, int mmax, const in
   std::vector<int> nm(world, 0);
   for (int m = 0; m < mmax; ++m)
     if (m_owner[m] >= 0) ++nm[m_owner[m]];
-  exchange_counts(world, rank, nm, row_start, row_start, R, phase, send_counts, recv_counts);
+  const int W = band_width(world, row_start);
+  exchange_counts(world, rank, nm, W, W, R, phase, send_counts, recv_counts);
+  return MSFNO_OK;
+}
+
+int msfno_band_local_rows(int world, int rank, int nlat, const int* row_start, int* rows,
+                          int* count) {
+  MSFNO_REQUIRE(world >= 1 && world <= 64 && rank >= 0 && rank < world && count, MSFNO_EINVAL,
+                "bad local-rows arguments");
+  MSFNO_TRY(validate_rows(world, nlat, row_start));
+  const BandRows o = band_rows(nlat, row_start, rank);
+  *count = o.H;
+  if (rows)
+    for (int i = 0; i < o.H; ++i) rows[i] = band_global_row(nlat, o, i);
   return MSFNO_OK;
 }
 
@@ -222,8 +284,8 @@ int msfno_band_plan_exchange_counts(msfno_band_plan_t p, int R, int phase, long 
   MSFNO_REQUIRE(p && R > 0 && send_counts && recv_counts, MSFNO_EINVAL,
                 "bad exchange-count arguments");
   MSFNO_REQUIRE(phase == 0 || phase == 1, MSFNO_EINVAL, "phase must be 0 or 1");
-  exchange_counts(p->world, p->rank, p->nm_of, p->row_in.data(), p->row_out.data(), R, phase,
-                  send_counts, recv_counts);
+  exchange_counts(p->world, p->rank, p->nm_of, p->W_in, p->W_out, R, phase, send_counts,
+                  recv_counts);
   return MSFNO_OK;
 }
 
@@ -231,8 +293,6 @@ int msfno_band_plan_destroy(msfno_band_plan_t p) {
   if (!p) return MSFNO_OK;
   msfno_sht_plan_destroy(p->fwd);
   msfno_sht_plan_destroy(p->inv);
-  if (p->d_row_in) (void)hipFree(p->d_row_in);
-  if (p->d_row_out) (void)hipFree(p->d_row_out);
   if (p->d_perm) (void)hipFree(p->d_perm);
   for (hipEvent_t e : p->join)
     if (e) (void)hipEventDestroy(e);
@@ -254,8 +314,10 @@ int msfno_band_plan_create2(int nlat_in, int nlon_in, int nlat_out, int nlon_out
   p->row_in.assign(row_in, row_in + world + 1);
   p->row_out.assign(row_out, row_out + world + 1);
   p->owner.assign(m_owner, m_owner + mmax);
-  p->rows_in = row_in[rank + 1] - row_in[rank];
-  p->rows_out = row_out[rank + 1] - row_out[rank];
+  p->rows_in = band_rows(nlat_in, row_in, rank).H;
+  p->rows_out = band_rows(nlat_out, row_out, rank).H;
+  p->W_in = band_width(world, row_in);
+  p->W_out = band_width(world, row_out);
   p->nm_of.assign(world, 0);
   std::vector<char> mask(mmax, 0);
   for (int m = 0; m < mmax; ++m) {
@@ -276,14 +338,9 @@ int msfno_band_plan_create2(int nlat_in, int nlon_in, int nlat_out, int nlon_out
     msfno_band_plan_destroy(p);
     return rc;
   }
-  hipError_t e = hipMalloc(&p->d_row_in, (world + 1) * sizeof(int));
-  if (e == hipSuccess) e = hipMalloc(&p->d_row_out, (world + 1) * sizeof(int));
-  if (e == hipSuccess) e = hipMalloc(&p->d_perm, mmax * sizeof(int));
-  if (e == hipSuccess)
-    e = hipMemcpy(p->d_row_in, p->row_in.data(), (world + 1) * sizeof(int), hipMemcpyHostToDevice);
-  if (e == hipSuccess)
-    e = hipMemcpy(p->d_row_out, p->row_out.data(), (world + 1) * sizeof(int),
-                  hipMemcpyHostToDevice);
+  set_band_maps(p->fwd, world, row_in, p->W_in);
+  set_band_maps(p->inv, world, row_out, p->W_out);
+  hipError_t e = hipMalloc(&p->d_perm, mmax * sizeof(int));
   if (e == hipSuccess)
     e = hipMemcpy(p->d_perm, perm.data(), mmax * sizeof(int), hipMemcpyHostToDevice);
   if (e != hipSuccess) {
@@ -339,7 +396,6 @@ int msfno_band_block_stage(const msfno_block_desc* d, msfno_band_plan_t p, int s
   carve_band(cv, b, d, p, B);
   const int64_t C = d->C, BC = (int64_t)B * C, R = 2 * BC;
   const int64_t Pout = (int64_t)p->rows_out * p->nlon_out;
-  const int64_t slab_rows = (int64_t)p->nm * R;
   switch (stage) {
     case 0: {
       MSFNO_REQUIRE(io->x && io->stats_local, MSFNO_EINVAL, "stage 0 needs x and stats_local");
@@ -399,33 +455,30 @@ int msfno_band_block_stage(const msfno_block_desc* d, msfno_band_plan_t p, int s
                                          d->norm0_b, d->norm_eps, nullptr, nullptr, 0.f, b.sc0,
                                          b.sh0, s));
       prof(ST_BAND_PACK, s);
-      MSFNO_TRY(launch_transpose_fwd(b.Xn, io->send, B, (int)C, p->rows_in, p->mmax, p->rows_in,
-                                     b.sc0, b.sh0, s, p->d_perm));
+      const BandRows o = band_rows(p->nlat_in, p->row_in.data(), p->rank);
+      MSFNO_TRY(launch_band_pack(b.Xn, io->send, B, (int)C, band_geom(p->fwd, o, p->W_in),
+                                 p->mmax, b.sc0, b.sh0, p->d_perm, p->W_in, s));
       prof(ST_END, s);
       break;
     }
     case 2: {
       MSFNO_REQUIRE(io->send && io->recv, MSFNO_EINVAL, "stage 2 needs send and recv");
       if (p->nm == 0) break;  // this rank owns no zonal wavenumber
-      prof(ST_BAND_GATHER, s);
-      MSFNO_TRY(launch_band_copy(io->recv, b.Xt, slab_rows, p->fwd->geom(), p->d_row_in,
-                                 p->world, false, s));
+      // the GEMMs read the phase-0 receive buffer and write the phase-1 send buffer
       prof(ST_LEG_FWD, s);
-      MSFNO_TRY(legendre_fwd(p->fwd, b.Xt, b.fb.Sa, (int)R, s));
+      MSFNO_TRY(legendre_fwd(p->fwd, io->recv, b.fb.Sa, (int)R, s));
       MSFNO_TRY(run_filter(d, p->fwd, p->inv, b.fb, B, s));
       prof(ST_LEG_INV, s);
-      MSFNO_TRY(legendre_inv(p->inv, b.fb.Sa, b.Xt, (int)R, s));
-      prof(ST_BAND_SCATTER, s);
-      MSFNO_TRY(launch_band_copy(b.Xt, io->send, slab_rows, p->inv->geom(), p->d_row_out,
-                                 p->world, true, s));
+      MSFNO_TRY(legendre_inv(p->inv, b.fb.Sa, io->send, (int)R, s));
       prof(ST_END, s);
       break;
     }
     case 3: {
       MSFNO_REQUIRE(io->recv && io->stats_local, MSFNO_EINVAL, "stage 3 needs recv and stats_local");
       prof(ST_TRANSPOSE_INV, s);
-      MSFNO_TRY(launch_transpose_inv(io->recv, b.Xn, B, (int)C, p->rows_out, p->mmax, p->mact,
-                                     p->rows_out, s, p->d_perm));
+      const BandRows o = band_rows(p->nlat_out, p->row_out.data(), p->rank);
+      MSFNO_TRY(launch_band_unpack(io->recv, b.Xn, B, (int)C, band_geom(p->inv, o, p->W_out),
+                                   p->mmax, p->mact, p->d_perm, s));
       const float* skip_src = nullptr;
       if (d->inner_skip == MSFNO_SKIP_LINEAR) {
         SideCtx* side = nullptr;

@@ -140,6 +140,11 @@ struct GemmEpi {
   // gemm_x6p only: A already split into its image ([3][KT][Mp][16], e.g. by
   // launch_spec_weights_x6p); the fp32 A pointer and the workspace are unused
   const unsigned short* a_planes = nullptr;
+  // fp32 descriptor GEMM only (band plans, common.h msfno_sht_plan_s): A's K index
+  // (segA) / C's column index (segC) is split into blocks of seg_w columns, block
+  // q at q * seg_stride floats from the operand base (0: contiguous)
+  int segA_w = 0, segC_w = 0;
+  int64_t segA_stride = 0, segC_stride = 0;
 };
 
 enum GemmTile {
@@ -264,5 +269,20 @@ struct msfno_sht_plan_s {
   int descx_R = -1;
   msfno::GemmDesc* d_descx = nullptr;
   int ndescx = 0, descx_tiles = 0;
+  // Latitude-band plans (band.cpp): the Legendre GEMMs read / write the all-to-all
+  // buffers directly.  Their slabs are [src or dst rank p][slab][R][band_ld] blocks:
+  // a K (forward) or N (inverse) column k' = p * seg + j lies in rank p's block.
+  //   symmetric:  band_ld = 2W, Xs / E at [0, W), Xa / O at [W, 2W), seg = W,
+  //               kmap[k'] = the folded (northern) latitude of j in p's band;
+  //   general:    band_ld = 2W, the rank's local rows at [0, 2W), seg = 2W,
+  //               kmap[k'] = the latitude of p's local row j;
+  // kmap = -1 on pads (zeros in the buffers and in the table).  band_world = 0:
+  // not a band plan.
+  int band_world = 0, band_W = 0;
+  std::vector<int> kmap_sym, kmap_gen;  // world * W and world * 2W entries
+  int* d_kmap = nullptr;                // device copy of the one in use
+  int band_seg() const { return sym ? band_W : 2 * band_W; }
+  int band_K() const { return band_world * band_seg(); }
+  int64_t table_cap = 0;         // floats allocated for `table`
   msfno::LatGeom geom() const { return {sym, nlat, nh, Ke, Ko, ldke, ldk}; }
 };

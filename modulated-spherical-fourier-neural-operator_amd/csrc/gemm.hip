@@ -96,6 +96,10 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmParams p) {
       const int row = min(m0 + idx / (BK / 4), Mc);
       const int k = k0 + (idx % (BK / 4)) * 4;
       const float* src = A + (int64_t)row * lda;
+      if (p.segA_w) {  // band exchange layout: k-tiles never straddle a block (seg_w % 16 == 0)
+        const int blk = min(k, Kc) / p.segA_w;
+        src += blk * (p.segA_stride - p.segA_w);
+      }
       if constexpr (VEC) {
         ra[q] = *reinterpret_cast<const float4*>(src + min(k, Kc & ~3));
       } else {
@@ -295,6 +299,8 @@ static GemmParams make_params(const float* A, const float* B, float* C, const Ge
   p.ldd = e.ldd; p.act = e.act; p.relu_period = e.relu_period; p.relu_rows = e.relu_rows;
   p.rowscale = e.rowscale;
   p.rs_C = e.rs_C;
+  p.segA_w = e.segA_w; p.segA_stride = e.segA_stride;
+  p.segC_w = e.segC_w; p.segC_stride = e.segC_stride;
   return p;
 }
 

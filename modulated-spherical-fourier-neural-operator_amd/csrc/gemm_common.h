@@ -39,6 +39,9 @@ struct GemmParams {
   unsigned short* Cx;
   int64_t sCxp;
   int cx16;  // plane rows 16-B aligned (ldc, sC, sCxp % 8 == 0, Cx 16-B aligned): uint4 stores
+  // segmented K of A / columns of C (GemmEpi::segA_w ...; 0 = contiguous)
+  int segA_w, segC_w;
+  int64_t segA_stride, segC_stride;
 };
 
 __device__ __forceinline__ int xcd_remap(int orig, int nwg) {
@@ -295,6 +298,10 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, AccV (&acc)[M
           }
         } else if (row < M) {
           float* dst = C + (int64_t)row * ldc + col;
+          if (p.segC_w) {  // band exchange layout (seg_w % 4 == 0: a float4 stays in a block)
+            const int q = col / p.segC_w;
+            dst += q * (p.segC_stride - p.segC_w);
+          }
           if (vecC && col + 3 < N) {
             *reinterpret_cast<float4*>(dst) = v;
           } else {

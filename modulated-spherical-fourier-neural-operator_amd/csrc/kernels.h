@@ -46,7 +46,7 @@ int launch_dc_fixup(float* Xt, int B, int C, int nlat, int ldk, const float* nsc
 // slab (device, optional, size mmax): Xt slab of each m (-1 = skip); default slab = m.
 int launch_transpose_fwd(const float2* Xn, float* Xt, int B, int C, int nlat, int mmax, int ldk,
                          const float* nscale, const float* nshift, hipStream_t s,
-                         const int* slab = nullptr);
+                         const int* slab = nullptr, int kpad = 0);
 // Yt (mmax, R, ldk) -> Yn (BC, nlat, mmax); m >= mact written as 0.
 int launch_transpose_inv(const float* Yt, float2* Yn, int B, int C, int nlat, int mmax, int mact,
                          int ldk, hipStream_t s, const int* slab = nullptr);
@@ -65,10 +65,16 @@ int launch_stats_partial(const float2* rowstats, int64_t np, int64_t cnt, int64_
 int launch_chan_affine_parts(const double* parts, int nparts, int B, int C, const float* w,
                              const float* b, float eps, const float* gamma, const float* beta,
                              float film_scale, float* scale, float* shift, hipStream_t s);
-// slabs (rows, g.ldk) <-> per-band blocks (rows, H_p) at offset rows*row0[p];
-// symmetric geometry folds / unfolds the hemispheres on the way
-int launch_band_copy(const float* src, float* dst, int64_t rows, const LatGeom& g,
-                     const int* d_row0, int W, bool to_bands, hipStream_t s);
+// the all-to-all buffers are the Legendre GEMMs' own operands: [p][slab][R][2W]
+// blocks (common.h msfno_sht_plan_s band fields).  g: the rank's local rows as a
+// small symmetric grid (Ke = its band, nh = the band rows that have a mirror row,
+// stored after the band, ascending), ldke = W, ldk = 2W.  pack: Xn (local rows)
+// -> send (slab perm[m], norm0 affine, fold, zero pads); unpack: recv -> Yn.
+int launch_band_pack(const float2* Xn, float* send, int B, int C, const LatGeom& g, int mmax,
+                     const float* nscale, const float* nshift, const int* perm, int W,
+                     hipStream_t s);
+int launch_band_unpack(const float* recv, float2* Yn, int B, int C, const LatGeom& g, int mmax,
+                       int mact, const int* perm, hipStream_t s);
 // W' [b] = W·diag(scale[b]),  b'[b] = bias + W·shift[b]
 int launch_fold_affine(const float* W, const float* bias, const float* scale, const float* shift,
                        float* Wf, float* bf, int B, int O, int I, hipStream_t s);

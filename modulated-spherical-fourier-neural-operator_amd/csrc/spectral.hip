@@ -26,7 +26,8 @@ __global__ __launch_bounds__(256) void transpose_fwd_kernel(const float2* __rest
                                                             int nlat, int mmax, int ldk,
                                                             const float* __restrict__ nscale,
                                                             const float* __restrict__ nshift,
-                                                            const int* __restrict__ slab) {
+                                                            const int* __restrict__ slab,
+                                                            int kpad) {
   __shared__ float2 tile[TMM][TK + 1];
   const int k0 = blockIdx.x * TK, m0 = blockIdx.y * TMM;
   const int bc = blockIdx.z;
@@ -56,6 +57,10 @@ __global__ __launch_bounds__(256) void transpose_fwd_kernel(const float2* __rest
       float* dst = Xt + (int64_t)sl * R * ldk;
       dst[rre * ldk + k] = v.x;
       dst[rim * ldk + k] = v.y;
+    } else if (k < kpad && sl >= 0) {  // band exchange pads (read by the GEMM)
+      float* dst = Xt + (int64_t)sl * R * ldk;
+      dst[rre * ldk + k] = 0.f;
+      dst[rim * ldk + k] = 0.f;
     }
   }
 }
@@ -88,10 +93,10 @@ int launch_dc_fixup(float* Xt, int B, int C, int nlat, int ldk, const float* nsc
 
 int launch_transpose_fwd(const float2* Xn, float* Xt, int B, int C, int nlat, int mmax, int ldk,
                          const float* nscale, const float* nshift, hipStream_t s,
-                         const int* slab) {
-  dim3 grid((unsigned)cdiv(nlat, TK), (unsigned)cdiv(mmax, TMM), (unsigned)(B * C));
+                         const int* slab, int kpad) {
+  dim3 grid((unsigned)cdiv(std::max(nlat, kpad), TK), (unsigned)cdiv(mmax, TMM), (unsigned)(B * C));
   hipLaunchKernelGGL(transpose_fwd_kernel, grid, dim3(256), 0, s, Xn, Xt, B, C, nlat, mmax, ldk,
-                     nscale, nshift, slab);
+                     nscale, nshift, slab, kpad);
   return launch_check("transpose_fwd");
 }
 
@@ -143,7 +148,8 @@ int launch_transpose_inv(const float* Yt, float2* Yn, int B, int C, int nlat, in
 template <int TKx, int TMx>
 __global__ __launch_bounds__(256) void transpose_fwd_sym_kernel(
     const float2* __restrict__ Xn, float* __restrict__ Xt, int B, int C, LatGeom g, int mmax,
-    const float* __restrict__ nscale, const float* __restrict__ nshift) {
+    const float* __restrict__ nscale, const float* __restrict__ nshift,
+    const int* __restrict__ slab, int kpad) {
   __shared__ float2 tn[TMx][TKx + 1], ts[TMx][TKx + 1];
   const int k0 = blockIdx.x * TKx, m0 = blockIdx.y * TMx;
   const int bc = blockIdx.z;
@@ -169,10 +175,21 @@ __global__ __launch_bounds__(256) void transpose_fwd_sym_kernel(
   for (int i = threadIdx.x; i < TKx * TMx; i += 256) {
     const int mm = i / TKx, kk = i - mm * TKx;
     const int k = k0 + kk, m = m0 + mm;
-    if (k >= g.Ke || m >= mmax) continue;
+    if (m >= mmax) continue;
+    const int sl = slab ? slab[m] : m;
+    if (sl < 0) continue;
+    float* dst = Xt + (int64_t)sl * R * g.ldk;
+    if (k >= g.Ke) {  // band exchange pads (read by the GEMM): Xs [Ke, kpad), Xa [nh, kpad)
+      if (k < kpad) {
+        dst[rre * g.ldk + k] = 0.f;
+        dst[rim * g.ldk + k] = 0.f;
+        dst[rre * g.ldk + g.ldke + k] = 0.f;
+        dst[rim * g.ldk + g.ldke + k] = 0.f;
+      }
+      continue;
+    }
     const float2 n = tn[mm][kk], q = ts[mm][kk];
     const float shm = (m == 0) ? sh : 0.f;
-    float* dst = Xt + (int64_t)m * R * g.ldk;
     const bool pair = k < g.nh;
     // affine per row, then fold: s(N + S) + 2t  /  s(N - S)
     dst[rre * g.ldk + k] = pair ? fmaf(sc, n.x + q.x, 2.f * shm) : fmaf(sc, n.x, shm);
@@ -180,6 +197,9 @@ __global__ __launch_bounds__(256) void transpose_fwd_sym_kernel(
     if (pair) {
       dst[rre * g.ldk + g.ldke + k] = sc * (n.x - q.x);
       dst[rim * g.ldk + g.ldke + k] = sc * (n.y - q.y);
+    } else if (k < kpad) {
+      dst[rre * g.ldk + g.ldke + k] = 0.f;
+      dst[rim * g.ldk + g.ldke + k] = 0.f;
     }
   }
 }
@@ -188,8 +208,24 @@ int launch_transpose_fwd_sym(const float2* Xn, float* Xt, int B, int C, const La
                              const float* nscale, const float* nshift, hipStream_t s) {
   dim3 grid((unsigned)cdiv(g.Ke, TK_FWD), (unsigned)cdiv(mmax, TM_FWD), (unsigned)(B * C));
   hipLaunchKernelGGL((transpose_fwd_sym_kernel<TK_FWD, TM_FWD>), grid, dim3(256), 0, s, Xn, Xt, B,
-                     C, g, mmax, nscale, nshift);
+                     C, g, mmax, nscale, nshift, nullptr, 0);
   return launch_check("transpose_fwd_sym");
+}
+
+// Latitude-band pack (band.cpp stage 1): this rank's spectra Xn (local rows, geometry
+// g: rows [0, Ke) its band, [Ke, nlat) the mirrors of its first nh rows) -> the
+// phase-0 send buffer, slab perm[m] (ordered by owner), slab rows of ldk = 2W:
+// folded [Xs | Xa] on a symmetric plan, the local rows on a general one; pads zero.
+int launch_band_pack(const float2* Xn, float* send, int B, int C, const LatGeom& g, int mmax,
+                     const float* nscale, const float* nshift, const int* perm, int W,
+                     hipStream_t s) {
+  if (!g.sym)
+    return launch_transpose_fwd(Xn, send, B, C, g.nlat, mmax, g.ldk, nscale, nshift, s, perm,
+                                2 * W);
+  dim3 grid((unsigned)cdiv(W, TK_FWD), (unsigned)cdiv(mmax, TM_FWD), (unsigned)(B * C));
+  hipLaunchKernelGGL((transpose_fwd_sym_kernel<TK_FWD, TM_FWD>), grid, dim3(256), 0, s, Xn, send,
+                     B, C, g, mmax, nscale, nshift, perm, W);
+  return launch_check("band_pack");
 }
 
 // The same fold + affine, written as bf16x3 planes Xtp[plane][m][R][ldk] (the A
@@ -334,7 +370,8 @@ template <int TKx, int TMx>
 __global__ __launch_bounds__(256) void transpose_inv_sym_kernel(const float* __restrict__ Yt,
                                                                 float2* __restrict__ Yn, int B,
                                                                 int C, LatGeom g, int mmax,
-                                                                int mact) {
+                                                                int mact,
+                                                                const int* __restrict__ slab) {
   __shared__ float2 tn[TMx][TKx + 1], ts[TMx][TKx + 1];
   const int k0 = blockIdx.x * TKx, m0 = blockIdx.y * TMx;
   const int bc = blockIdx.z;
@@ -346,8 +383,9 @@ __global__ __launch_bounds__(256) void transpose_inv_sym_kernel(const float* __r
     const int mm = i / TKx, kk = i - mm * TKx;
     const int k = k0 + kk, m = m0 + mm;
     float2 n = make_float2(0.f, 0.f), q = n;
-    if (k < g.Ke && m < mact) {
-      const float* src = Yt + (int64_t)m * R * g.ldk;
+    const int sl = (m < mact) ? (slab ? slab[m] : m) : -1;
+    if (k < g.Ke && sl >= 0) {
+      const float* src = Yt + (int64_t)sl * R * g.ldk;
       const float2 e = make_float2(src[rre * g.ldk + k], src[rim * g.ldk + k]);
       if (k < g.nh) {
         const float2 o = make_float2(src[rre * g.ldk + g.ldke + k], src[rim * g.ldk + g.ldke + k]);
@@ -375,8 +413,19 @@ int launch_transpose_inv_sym(const float* Yt, float2* Yn, int B, int C, const La
                              int mact, hipStream_t s) {
   dim3 grid((unsigned)cdiv(g.Ke, TK_INV), (unsigned)cdiv(mmax, TM_INV), (unsigned)(B * C));
   hipLaunchKernelGGL((transpose_inv_sym_kernel<TK_INV, TM_INV>), grid, dim3(256), 0, s, Yt, Yn, B,
-                     C, g, mmax, mact);
+                     C, g, mmax, mact, nullptr);
   return launch_check("transpose_inv_sym");
+}
+
+// Latitude-band unpack (band.cpp stage 3): the phase-1 receive buffer (slab perm[m],
+// rows of ldk = 2W holding [E | O] or the local rows) -> this rank's spectra Yn
+int launch_band_unpack(const float* recv, float2* Yn, int B, int C, const LatGeom& g, int mmax,
+                       int mact, const int* perm, hipStream_t s) {
+  if (!g.sym) return launch_transpose_inv(recv, Yn, B, C, g.nlat, mmax, mact, g.ldk, s, perm);
+  dim3 grid((unsigned)cdiv(g.Ke, TK_INV), (unsigned)cdiv(mmax, TM_INV), (unsigned)(B * C));
+  hipLaunchKernelGGL((transpose_inv_sym_kernel<TK_INV, TM_INV>), grid, dim3(256), 0, s, recv, Yn,
+                     B, C, g, mmax, mact, perm);
+  return launch_check("band_unpack");
 }
 
 // ---------------------------------------------------------------------------
@@ -533,82 +582,6 @@ int launch_chan_affine_parts(const double* parts, int nparts, int B, int C, cons
   return launch_check("chan_affine_parts");
 }
 
-// Full-latitude slabs F (rows, ldk) [row = mi*R + r]  <->  band buffer Q laid out
-// per band p as (rows, H_p) at offset rows * row0[p]   (the all-to-all block of p).
-// One wave per row.  TO_BANDS: F -> Q (pack), else Q -> F (unpack, zero pads).
-// Symmetric geometry: F rows are [Xs | Xa] (unpack folds the hemispheres) and
-// [E | O] (pack unfolds them), as transpose_fwd_sym / transpose_inv_sym.
-__device__ __forceinline__ int64_t band_pos(const int* r0, int W, int64_t rows, int64_t row,
-                                           int k) {
-  int lo = 0, hi = W - 1;  // band with r0[p] <= k < r0[p+1]
-  while (lo < hi) {
-    const int mid = (lo + hi + 1) >> 1;
-    if (r0[mid] <= k) lo = mid; else hi = mid - 1;
-  }
-  return rows * r0[lo] + row * (r0[lo + 1] - r0[lo]) + (k - r0[lo]);
-}
-
-template <bool TO_BANDS>
-__global__ __launch_bounds__(256) void band_copy_kernel(const float* __restrict__ src,
-                                                        float* __restrict__ dst, int64_t rows,
-                                                        LatGeom g, const int* __restrict__ row0,
-                                                        int W) {
-  __shared__ int r0[65];
-  for (int i = threadIdx.x; i <= W; i += 256) r0[i] = row0[i];
-  __syncthreads();
-  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (row >= rows) return;
-  const int lane = threadIdx.x & 63;
-  const float* F = TO_BANDS ? src + row * g.ldk : nullptr;
-  if (TO_BANDS) {
-    for (int k = lane; k < g.nlat; k += 64) {
-      float v;
-      if (!g.sym) {
-        v = F[k];
-      } else if (k < g.nh) {
-        v = F[k] + F[g.ldke + k];
-      } else if (k >= g.nlat - g.nh) {
-        const int kn = g.nlat - 1 - k;
-        v = F[kn] - F[g.ldke + kn];
-      } else {
-        v = F[k];  // equator row of an odd grid
-      }
-      dst[band_pos(r0, W, rows, row, k)] = v;
-    }
-  } else {
-    float* D = dst + row * g.ldk;
-    for (int c = lane; c < g.ldk; c += 64) {
-      float v = 0.f;
-      if (!g.sym) {
-        if (c < g.nlat) v = src[band_pos(r0, W, rows, row, c)];
-      } else if (c < g.Ke) {
-        v = src[band_pos(r0, W, rows, row, c)];
-        if (c < g.nh) v += src[band_pos(r0, W, rows, row, g.nlat - 1 - c)];
-      } else if (c >= g.ldke && c < g.ldke + g.Ko) {
-        const int k = c - g.ldke;
-        v = src[band_pos(r0, W, rows, row, k)] - src[band_pos(r0, W, rows, row, g.nlat - 1 - k)];
-      }
-      D[c] = v;
-    }
-  }
-}
-
-int launch_band_copy(const float* src, float* dst, int64_t rows, const LatGeom& g,
-                     const int* d_row0, int W, bool to_bands, hipStream_t s) {
-  if (W > 64) {
-    set_error("latitude-band sharding supports at most 64 ranks");
-    return MSFNO_EUNSUPPORTED;
-  }
-  if (rows == 0) return MSFNO_OK;
-  const dim3 grid((unsigned)cdiv(rows, 4));
-  if (to_bands)
-    hipLaunchKernelGGL(band_copy_kernel<true>, grid, dim3(256), 0, s, src, dst, rows, g, d_row0, W);
-  else
-    hipLaunchKernelGGL(band_copy_kernel<false>, grid, dim3(256), 0, s, src, dst, rows, g, d_row0,
-                       W);
-  return launch_check("band_copy");
-}
-
 // W'[b][o][i] = W[o][i]·scale[b][i];  b'[b][o] = bias[o] + Σ_i W[o][i]·shift[b][i]
 __global__ __launch_bounds__(256) void fold_affine_kernel(const float* __restrict__ W,
                                                           const float* __restrict__ bias,
@@ -734,7 +707,8 @@ int launch_expand_complex_weight(const float* w, float* Wexp, int Ci, int Co, hi
 __global__ void relayout_table_kernel(const float* __restrict__ tab, float* __restrict__ out,
                                       const int64_t* __restrict__ tab_off,
                                       const int* __restrict__ Lp, const int* __restrict__ Lpe,
-                                      int lmax, LatGeom g, int inverse) {
+                                      int lmax, LatGeom g, int inverse,
+                                      const int* __restrict__ kmap, int Kb) {
   const int m = blockIdx.y;
   const int L = lmax - m;
   const int lp = Lp[m], lpe = Lpe[m], lpo = lp - lpe;
@@ -746,6 +720,33 @@ __global__ void relayout_table_kernel(const float* __restrict__ tab, float* __re
     return (j < L) ? t[(int64_t)(m + j) * g.nlat + k] : 0.f;
   };
   auto jcol = [&](int c) { return c < lpe ? 2 * c : 2 * (c - lpe) + 1; };
+  if (kmap) {
+    // band plan (common.h): the K (forward) / N (inverse) index is an exchange
+    // column k' whose latitude is kmap[k'] (-1: pad)
+    const int64_t n = (int64_t)Kb * lp;
+    for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < n;
+         e += (int64_t)gridDim.x * blockDim.x) {
+      int kb, j;
+      if (g.sym) {
+        const int64_t ne = (int64_t)Kb * lpe;
+        const bool ev = e < ne;
+        const int64_t f = ev ? e : e - ne;
+        const int w = ev ? lpe : lpo;
+        int c;
+        if (inverse) { c = (int)(f / Kb); kb = (int)(f - (int64_t)c * Kb); }
+        else { kb = (int)(f / w); c = (int)(f - (int64_t)kb * w); }
+        j = ev ? 2 * c : 2 * c + 1;
+      } else {
+        int c;
+        if (inverse) { c = (int)(e / Kb); kb = (int)(e - (int64_t)c * Kb); }
+        else { kb = (int)(e / lp); c = (int)(e - (int64_t)kb * lp); }
+        j = jcol(c);
+      }
+      const int k = kmap[kb];
+      o[e] = k >= 0 ? at(j, k) : 0.f;
+    }
+    return;
+  }
   const int ldko = (g.Ko + 3) & ~3;
   int64_t n;
   if (!g.sym) n = inverse ? (int64_t)lp * g.ldk : (int64_t)g.nlat * lp;
@@ -790,7 +791,8 @@ __global__ void relayout_table_kernel(const float* __restrict__ tab, float* __re
 int launch_relayout_table(const msfno_sht_plan_s& p, const float* table, hipStream_t s) {
   dim3 grid(256, (unsigned)p.mmax);
   hipLaunchKernelGGL(relayout_table_kernel, grid, dim3(256), 0, s, table, p.table, p.d_tab_off,
-                     p.d_Lp, p.d_Lpe, p.lmax, p.geom(), p.inverse);
+                     p.d_Lp, p.d_Lpe, p.lmax, p.geom(), p.inverse,
+                     p.band_world ? p.d_kmap : nullptr, p.band_world ? p.band_K() : 0);
   return launch_check("relayout_table");
 }
 

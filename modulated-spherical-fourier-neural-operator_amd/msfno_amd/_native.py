@@ -103,6 +103,7 @@ SIGNATURES = [
                                       ctypes.c_longlong, _vp, _sz, _vp]),
     ("msfno_band_partition", _i, [_i, _i, _i, _i, _ip, _ip]),
     ("msfno_band_exchange_counts", _i, [_i, _i, _i, _i, _ip, _ip, _i, _i, _llp, _llp]),
+    ("msfno_band_local_rows", _i, [_i, _i, _i, _ip, _ip, _ip]),
     ("msfno_band_plan_create", _i, [_i, _i, _i, _i, _i, _i, _ip, _ip, ctypes.POINTER(_vp)]),
     ("msfno_band_plan_create2", _i, [_i, _i, _i, _i, _i, _i, _i, _i, _ip, _ip, _ip,
                                      ctypes.POINTER(_vp)]),

@@ -10,4 +10,5 @@ from .sfnonet import (  # noqa: F401
     FourierNeuralOperatorNet_Filmed,
     SpectralFilterLayer,
 )
-from .latband import LatBandBlock, LocalGroup, TorchComm, band_partition, exchange_counts  # noqa: F401,E501
+from .latband import (LatBandBlock, LocalGroup, TorchComm, band_partition,  # noqa: F401
+                      exchange_counts, local_rows)

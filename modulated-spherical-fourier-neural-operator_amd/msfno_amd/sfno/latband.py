@@ -2,10 +2,14 @@
 
 The reference scales only by data-parallel replicas (one whole field per
 process, MSFNO/main.py:1153).  Here ONE batch of fields is split over the ranks
-of a process group: rank r keeps latitude rows [row_start[r], row_start[r+1])
-of every field for the pointwise / FFT / 1x1-conv / MLP work and the zonal
-wavenumbers {m : m_owner[m] == r} for the Legendre transforms and the spectral
-filter, which couple all latitudes of one m but are independent across m.
+of a process group: rank r keeps a band of the northern half, rows
+[row_start[r], row_start[r+1]) of [0, nlat - nlat//2), plus the mirror rows
+nlat-1-k of that band (``local_rows``), of every field for the pointwise / FFT /
+1x1-conv / MLP work, and the zonal wavenumbers {m : m_owner[m] == r} for the
+Legendre transforms and the spectral filter, which couple all latitudes of one m
+but are independent across m.  Owning mirror pairs keeps the hemisphere fold of
+the symmetric Legendre transform local, so the exchange buffers are the Legendre
+GEMMs' operands as they are (include/msfno.h).
 Per block forward (include/msfno.h, "Latitude-band sharded SFNO-Block"):
 
     stage 0  skip GEMM (side stream) + FFT of local rows      -> norm0 partials
@@ -45,11 +49,25 @@ from .. import _native as N
 
 
 def band_partition(world: int, nlat: int, lmax: int, mmax: int):
-    """Default partition: balanced latitude bands + zig-zag m ownership."""
+    """Default partition: balanced bands of the northern half (world + 1 row
+    boundaries over [0, nlat - nlat//2)) + zig-zag m ownership."""
     rows = (ctypes.c_int * (world + 1))()
     own = (ctypes.c_int * mmax)()
     N.check(N.lib().msfno_band_partition(world, nlat, lmax, mmax, rows, own), "band_partition")
     return list(rows), list(own)
+
+
+def local_rows(world: int, rank: int, nlat: int, row_start):
+    """Global latitude rows of `rank`'s local rows, in local order: its band
+    ascending, then the band's mirror rows ascending."""
+    rs = (ctypes.c_int * (world + 1))(*row_start)
+    cnt = ctypes.c_int()
+    N.check(N.lib().msfno_band_local_rows(world, rank, nlat, rs, None, ctypes.byref(cnt)),
+            "band_local_rows")
+    rows = (ctypes.c_int * max(cnt.value, 1))()
+    N.check(N.lib().msfno_band_local_rows(world, rank, nlat, rs, rows, ctypes.byref(cnt)),
+            "band_local_rows")
+    return list(rows)[:cnt.value]
 
 
 def exchange_counts(world, rank, nlat, mmax, row_start, m_owner, R, phase):
@@ -286,10 +304,11 @@ class LatBandBlock:
     """One rank's share of a latitude-band sharded FourierNeuralOperatorBlock[_Filmed].
 
     ``block`` is the (replicated) block module; ``forward(x_local, gamma, beta,
-    scale)`` takes this rank's rows of the input grid
-    ``x[:, :, rows_in[0]:rows_in[1]]`` and returns its rows of the output grid
-    (the same rows unless the block resamples).  ``row_start`` partitions the
-    input grid, ``row_start_out`` the output grid (default: balanced bands)."""
+    scale)`` takes this rank's rows of the input grid, ``take(x)`` =
+    ``x[:, :, rows]``, and returns its rows of the output grid, ``rows_out`` (the
+    same rows unless the block resamples); ``assemble`` puts the ranks' outputs
+    back together.  ``row_start`` partitions the northern half of the input grid,
+    ``row_start_out`` that of the output grid (default: balanced bands)."""
 
     def __init__(self, block, rank: int, world: int, row_start=None, m_owner=None,
                  device=None, row_start_out=None):
@@ -317,15 +336,30 @@ class LatBandBlock:
         self._bufs = {}
         self._lin = None   # (key, local weight slice)
 
-    @property
-    def rows(self):
-        """This rank's rows of the input grid."""
-        return self.row_start[self.rank], self.row_start[self.rank + 1]
+        self.rows = local_rows(world, rank, self.nlat, self.row_start)
+        self.rows_out = local_rows(world, rank, self.nlat_out, self.row_start_out)
+        self._idx = {}
 
-    @property
-    def rows_out(self):
-        """This rank's rows of the output grid."""
-        return self.row_start_out[self.rank], self.row_start_out[self.rank + 1]
+    def _index(self, rows, device):
+        key = (id(rows), str(device))
+        if key not in self._idx:
+            self._idx[key] = torch.tensor(rows, dtype=torch.long, device=device)
+        return self._idx[key]
+
+    def take(self, x):
+        """This rank's input rows x[:, :, rows] (contiguous)."""
+        return x.index_select(2, self._index(self.rows, x.device)).contiguous()
+
+    @staticmethod
+    def assemble(shards, outs):
+        """The full output field from every rank's output rows (``shards[r]``'s
+        ``forward`` result in ``outs[r]``)."""
+        o = outs[0]
+        nlat = shards[0].nlat_out
+        y = torch.empty(o.shape[0], o.shape[1], nlat, o.shape[3], dtype=o.dtype, device=o.device)
+        for s, t in zip(shards, outs):
+            y.index_copy_(2, s._index(s.rows_out, t.device), t)
+        return y
 
     def _tables(self):
         fwd, inv = self.block._transforms()
@@ -379,10 +413,8 @@ class LatBandBlock:
         sub-batches in flight at the same time."""
         x = N.require_device_f32(x, "band block input")
         B, C, H, W = x.shape
-        r0, r1 = self.rows
-        o0, o1 = self.rows_out
-        if H != r1 - r0 or W != self.nlon or C != self.block.embed_dim_sfno:
-            raise ValueError(f"x_local must be (B, {self.block.embed_dim_sfno}, {r1 - r0}, "
+        if H != len(self.rows) or W != self.nlon or C != self.block.embed_dim_sfno:
+            raise ValueError(f"x_local must be (B, {self.block.embed_dim_sfno}, {len(self.rows)}, "
                              f"{self.nlon}), got {tuple(x.shape)}")
         self._tables()
         d, keep = self.block.native_desc()
@@ -399,7 +431,8 @@ class LatBandBlock:
         nbytes = L.msfno_band_workspace_size(d, self.plan.handle, B)
         ws = torch.empty(nbytes, dtype=torch.uint8, device=x.device)
         if out is None:
-            out = torch.empty(B, C, o1 - o0, self.nlon_out, dtype=torch.float32, device=x.device)
+            out = torch.empty(B, C, len(self.rows_out), self.nlon_out, dtype=torch.float32,
+                              device=x.device)
         io = N.BandIO(x=x.data_ptr(), gamma=N.ptr(gamma), beta=N.ptr(beta),
                       film_scale=float(scale), out=out.data_ptr(), send=bufs["send"].data_ptr(),
                       recv=bufs["recv"].data_ptr(), stats_local=bufs["stats"].data_ptr(),
@@ -439,8 +472,7 @@ class LatBandBlock:
                 return LocalGroup.run([gen])[0]
             return _drive(gen, comm if comm is not None else TorchComm())
         x = N.require_device_f32(x, "band block input")
-        o0, o1 = self.rows_out
-        out = torch.empty(B, x.shape[1], o1 - o0, self.nlon_out, dtype=torch.float32,
+        out = torch.empty(B, x.shape[1], len(self.rows_out), self.nlon_out, dtype=torch.float32,
                           device=x.device)
         bounds = [B * k // K for k in range(K + 1)]
         gens = []

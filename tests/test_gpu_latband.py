@@ -23,20 +23,17 @@ ALL_BLOCKS = golden_files()
 def _sharded(blk, x, gamma, beta, scale, world, row_start=None, m_owner=None):
     from msfno_amd.sfno import LatBandBlock, LocalGroup
     shards = [LatBandBlock(blk, r, world, row_start, m_owner) for r in range(world)]
-    gens = []
-    for s in shards:
-        r0, r1 = s.rows
-        gens.append(s.stages(x[:, :, r0:r1].contiguous(), gamma, beta, scale))
-    outs = LocalGroup.run(gens)
-    return torch.cat(outs, dim=2)
+    gens = [s.stages(s.take(x), gamma, beta, scale) for s in shards]
+    return LatBandBlock.assemble(shards, LocalGroup.run(gens))
 
 
 @pytest.mark.parametrize("world", [1, 2, 3, 5])
 @pytest.mark.parametrize("path", ALL_BLOCKS, ids=lambda p: os.path.basename(p)[:-4])
 def test_sharded_block_matches_golden(path, world):
     meta, params, arrays, _ = load(path)
-    if min(meta["nlat"], meta.get("out_nlat", meta["nlat"])) < world:
-        pytest.skip("fewer latitude rows than ranks")
+    ke = min(n - n // 2 for n in (meta["nlat"], meta.get("out_nlat", meta["nlat"])))
+    if ke < world:
+        pytest.skip("fewer northern latitude rows than ranks")
     blk, _, _ = make_block(meta, params)
     blk = blk.to(DEV)
     x = arrays["x"].to(DEV)
@@ -52,6 +49,23 @@ def test_sharded_block_matches_golden(path, world):
     assert (y - y1).abs().max().item() < 2e-5
 
 
+@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("name", ["c1b2_nl_film_middle.npz", "down_lin_film_first.npz",
+                                  "mid_nl_film_middle.npz"])
+def test_sharded_block_general_layout(name, world, monkeypatch):
+    """MSFNO_NO_SYM=1: the tables load in the general (non-folded) layout, so the
+    exchange slabs carry each rank's local rows unfolded (2W columns per source)."""
+    monkeypatch.setenv("MSFNO_NO_SYM", "1")
+    meta, params, arrays, _ = load([p for p in golden_files() if os.path.basename(p) == name][0])
+    blk, _, _ = make_block(meta, params)
+    blk = blk.to(DEV)
+    x = arrays["x"].to(DEV)
+    g, b = arrays["gamma"].to(DEV), arrays["beta"].to(DEV)
+    with torch.no_grad():
+        y = _sharded(blk, x, g, b, meta["scale"], world).cpu()
+    assert (y - arrays["y"]).abs().max().item() < 1e-4
+
+
 def test_sharded_block_custom_partition_with_idle_rank():
     """Uneven bands and a rank that owns no zonal wavenumber."""
     path = [p for p in golden_files() if os.path.basename(p) == "c1b2_nl_film_middle.npz"][0]
@@ -60,7 +74,7 @@ def test_sharded_block_custom_partition_with_idle_rank():
     blk = blk.to(DEV)
     x = arrays["x"].to(DEV)
     nlat, lmax, mmax = meta["nlat"], meta["lmax"], meta["mmax"]
-    rows = [0, 3, 20, nlat]
+    rows = [0, 3, 11, nlat - nlat // 2]   # bands of the northern half
     own = [(m % 2) if m < min(lmax, mmax) else -1 for m in range(mmax)]   # rank 2 owns none
     with torch.no_grad():
         y = _sharded(blk, x, arrays["gamma"].to(DEV), arrays["beta"].to(DEV), meta["scale"], 3,
@@ -151,12 +165,11 @@ def _dist_rank(rank, world, port, path, q, chunks=1):
         blk, _, _ = mk(meta, params)
         blk = blk.to(DEV)
         shard = LatBandBlock(blk, rank, world)
-        r0, r1 = shard.rows
-        x = arrays["x"][:, :, r0:r1].contiguous().to(DEV)
+        x = shard.take(arrays["x"].to(DEV))
         with torch.no_grad():
             y = shard(x, arrays["gamma"].to(DEV), arrays["beta"].to(DEV), meta["scale"],
                       comm=TorchComm(), chunks=chunks)
-        q.put((rank, y.cpu().numpy()))
+        q.put((rank, (shard.rows_out, y.cpu().numpy())))
     finally:
         dist.destroy_process_group()
 
@@ -189,5 +202,8 @@ def test_sharded_block_two_processes_gloo(name, chunks):
             p.join(timeout=60)
             if p.is_alive():
                 p.kill()
-    y = torch.cat([torch.from_numpy(res[0]), torch.from_numpy(res[1])], dim=2)
+    y = torch.full_like(arrays["y"], float("nan"))
+    for r in range(2):
+        rows, part = res[r]
+        y[:, :, rows] = torch.from_numpy(part)
     assert (y - arrays["y"]).abs().max().item() < 1e-4

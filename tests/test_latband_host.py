@@ -1,11 +1,13 @@
 """Host-side checks of the latitude-band sharded path, no GPU:
-the partition and exchange counts exported by libmsfno, and the full data
-movement of one sharded block forward — pack by owner of m, all-to-all,
-re-assembly of full-latitude slabs, the return trip and the fp64 statistics
-merge — run over a real world-size-2/3 ``gloo`` process group through
-``msfno_amd.sfno.latband.TorchComm``.  The device kernels' index maps
-(transpose_fwd/inv with the slab permutation, band_copy) are restated here in
-numpy; the GPU tests (test_gpu_latband.py) check the kernels themselves."""
+the partition (bands of the northern half + their mirror rows) and exchange
+counts exported by libmsfno, and the full data movement of one sharded block
+forward — the folding pack by owner of m, all-to-all, the receive buffer read as
+the forward Legendre GEMM's segmented operand, the return trip into the inverse
+GEMM's segmented output, the unfolding unpack and the fp64 statistics merge — run
+over a real world-size-2/3 ``gloo`` process group through
+``msfno_amd.sfno.latband.TorchComm``.  The device kernels' index maps (band_pack /
+band_unpack with the slab permutation, the GEMM's exchange-column addressing) are
+restated here in numpy; the GPU tests (test_gpu_latband.py) check the kernels."""
 import os
 import socket
 
@@ -28,7 +30,14 @@ def _free_port():
 def test_partition_properties(world, nlat, lmax, mmax):
     rows, own = latband.band_partition(world, nlat, lmax, mmax)
     h = np.diff(rows)
-    assert rows[0] == 0 and rows[-1] == nlat and h.min() >= 1 and h.max() - h.min() <= 1
+    assert rows[0] == 0 and rows[-1] == nlat - nlat // 2 and h.min() >= 1
+    assert h.max() - h.min() <= 1
+    # the ranks' local rows (band + mirrors) cover every latitude exactly once
+    loc = [latband.local_rows(world, r, nlat, rows) for r in range(world)]
+    assert sorted(sum(loc, [])) == list(range(nlat))
+    for r, lr in enumerate(loc):   # local row H-1-i is the mirror of local row i
+        npair = max(0, min(rows[r + 1], nlat // 2) - rows[r])
+        assert all(lr[len(lr) - 1 - i] == nlat - 1 - lr[i] for i in range(npair))
     own = np.array(own)
     mact = min(lmax, mmax)
     assert (own[:mact] >= 0).all() and (own[mact:] == -1).all()
@@ -49,14 +58,17 @@ def test_exchange_counts_are_symmetric(world):
             for q in range(world):
                 assert c[r][0][q] == c[q][1][r]
         tot = sum(sum(s) for s, _ in c)
-        assert tot == R * nlat * min(lmax, mmax)   # every (row, m) of every field moves once
+        # every (m, spectral row) moves once per source band: 2W floats (>= its rows)
+        W = -(-max(np.diff(rows)) // 16) * 16
+        assert tot == R * world * 2 * W * min(lmax, mmax)
+        assert world * 2 * W <= nlat + world * 2 * 16
 
 
 def test_partition_rejects_bad_input():
     with pytest.raises(NotImplementedError):
         latband.band_partition(65, 721, 360, 361)
     with pytest.raises(ValueError):
-        latband.band_partition(8, 4, 4, 5)          # fewer rows than ranks
+        latband.band_partition(8, 14, 4, 5)         # fewer northern rows than ranks
     rows, own = latband.band_partition(2, 16, 8, 9)
     own[0] = -1                                      # m = 0 unowned
     with pytest.raises(ValueError):
@@ -80,52 +92,50 @@ def _rows_of(B, C):   # spectral row r = (b*2 + ri)*C + c
     return [(b, ri, c) for b in range(B) for ri in range(2) for c in range(C)]
 
 
-def _pack_fwd(Xn, perm, B, C):
-    """transpose_fwd with slab map: Xn (BC, H, mmax) complex -> slabs (perm, R, H)."""
-    H, mmax = Xn.shape[1], Xn.shape[2]
+def _width(rows):     # exchange slab rows hold 2W floats
+    return int(-(-max(np.diff(rows)) // 16) * 16)
+
+
+def _band(rows, rank, nlat):  # (a, bw, np): band [a, a+bw), np rows with a mirror
+    a, b = rows[rank], rows[rank + 1]
+    return a, b - a, max(0, min(b, nlat // 2) - a)
+
+
+def _pack_fwd(Xl, perm, B, C, bw, npair, W):
+    """band_pack (symmetric): local spectra (BC, H, mmax) -> slabs (perm, R, 2W) of
+    [Xs = X_i + X_{H-1-i} | Xa = X_i - X_{H-1-i}], zero pads."""
+    H, mmax = Xl.shape[1], Xl.shape[2]
     R = 2 * B * C
-    out = np.zeros(((perm >= 0).sum(), R, H), dtype=np.float32)
+    out = np.zeros(((perm >= 0).sum(), R, 2 * W), dtype=np.float32)
     for m in range(mmax):
         if perm[m] < 0:
             continue
         for r, (b, ri, c) in enumerate(_rows_of(B, C)):
-            v = Xn[b * C + c, :, m]
-            out[perm[m], r] = v.real if ri == 0 else v.imag
+            v = Xl[b * C + c, :, m]
+            v = v.real if ri == 0 else v.imag
+            for i in range(bw):
+                out[perm[m], r, i] = v[i] + (v[H - 1 - i] if i < npair else 0)
+                if i < npair:
+                    out[perm[m], r, W + i] = v[i] - v[H - 1 - i]
     return out.reshape(-1)
 
 
-def _band_unpack(buf, nm, R, rows, nlat):
-    """band_copy(to_bands=False): per-band blocks (nm*R, H_p) -> (nm*R, nlat)."""
-    n = nm * R
-    F = np.zeros((n, nlat), dtype=np.float32)
-    for p in range(len(rows) - 1):
-        hp = rows[p + 1] - rows[p]
-        F[:, rows[p]:rows[p + 1]] = buf[n * rows[p]:n * rows[p] + n * hp].reshape(n, hp)
-    return F
-
-
-def _band_pack(F, rows):
-    n = F.shape[0]
-    out = np.zeros(n * rows[-1], dtype=np.float32)
-    for p in range(len(rows) - 1):
-        hp = rows[p + 1] - rows[p]
-        out[n * rows[p]:n * rows[p] + n * hp] = F[:, rows[p]:rows[p + 1]].reshape(-1)
-    return out
-
-
-def _unpack_inv(buf, perm, mact, B, C, H, mmax):
-    """transpose_inv with slab map: slabs (perm, R, H) -> Yn (BC, H, mmax) complex."""
-    R = 2 * B * C
+def _unpack_inv(buf, perm, mact, B, C, bw, npair, W, mmax):
+    """band_unpack (symmetric): slabs (perm, R, 2W) of [E | O] -> local Yn
+    (BC, H, mmax): Y_i = E_i + O_i, Y_{H-1-i} = E_i - O_i."""
+    R, H = 2 * B * C, bw + npair
     Y = np.zeros((B * C, H, mmax), dtype=np.complex64)
-    sl = buf.reshape(-1, R, H)
+    sl = buf.reshape(-1, R, 2 * W)
     for m in range(min(mact, mmax)):
         if perm[m] < 0:
             continue
         for r, (b, ri, c) in enumerate(_rows_of(B, C)):
-            if ri == 0:
-                Y[b * C + c, :, m] += sl[perm[m], r]
-            else:
-                Y[b * C + c, :, m] += 1j * sl[perm[m], r]
+            E, O = sl[perm[m], r, :bw], sl[perm[m], r, W:W + npair]
+            y = np.zeros(H, dtype=np.float32)
+            y[:bw] = E
+            y[:npair] += O
+            y[bw:] = (E[:npair] - O)[::-1]
+            Y[b * C + c, :, m] += y if ri == 0 else 1j * y
     return Y
 
 
@@ -153,44 +163,71 @@ def _rank_main(rank, world, port, B, C, nlat, lmax, mmax, q):
     try:
         comm = latband.TorchComm()
         rows, own = latband.band_partition(world, nlat, lmax, mmax)
-        R, mact = 2 * B * C, min(lmax, mmax)
+        R, mact, W = 2 * B * C, min(lmax, mmax), _width(rows)
         rng = np.random.default_rng(0)
         X = (rng.standard_normal((B * C, nlat, mmax))
              + 1j * rng.standard_normal((B * C, nlat, mmax))).astype(np.complex64)
         field = rng.standard_normal((B * C, nlat, 12))
-        r0, r1 = rows[rank], rows[rank + 1]
+        loc = latband.local_rows(world, rank, nlat, rows)
+        a, bw, npair = _band(rows, rank, nlat)
+        assert loc == list(range(a, a + bw)) + list(range(nlat - a - npair, nlat - a))
         perm = _perm(own, world)
         mine = [m for m in range(mmax) if own[m] == rank]
         nm = len(mine)
         # statistics partials -> all_gather -> fp64 merge
-        st = torch.tensor(np.stack([_welford(field[i, r0:r1]) for i in range(B * C)]))
+        st = torch.tensor(np.stack([_welford(field[i, loc]) for i in range(B * C)]))
         allst = comm.all_gather(st).numpy()
         for i in range(B * C):
             n, mean, m2 = _merge([allst[p, i] for p in range(world)])
             assert n == field[i].size
             np.testing.assert_allclose(mean, field[i].mean(), rtol=1e-12, atol=1e-12)
             np.testing.assert_allclose(m2 / n, field[i].var(), rtol=1e-10)
-        # phase 0: rows -> m
+        # phase 0: rows -> m; the receive buffer is the forward Legendre GEMM's A:
+        # exchange column k' = p*W + j of slab i, row r at p*(nm*R*2W) + (i*R + r)*2W + j
         sc, rc = latband.exchange_counts(world, rank, nlat, mmax, rows, own, R, 0)
-        send = torch.from_numpy(_pack_fwd(X[:, r0:r1], perm, B, C))
+        send = torch.from_numpy(_pack_fwd(X[:, loc], perm, B, C, bw, npair, W))
         assert send.numel() == sum(sc)
         recv = torch.zeros(sum(rc))
         comm.all_to_all(send, sc, recv, rc)
-        F = _band_unpack(recv.numpy(), nm, R, rows, nlat).reshape(nm, R, nlat)
-        for i, m in enumerate(mine):
-            for r, (b, ri, c) in enumerate(_rows_of(B, C)):
-                want = X[b * C + c, :, m]
-                np.testing.assert_array_equal(F[i, r], want.real if ri == 0 else want.imag)
-        # phase 1: m -> rows (send the assembled slabs back)
+        buf = recv.numpy()
+        blk = nm * R * 2 * W
+        E = np.zeros((nm, R, world * W), dtype=np.float32)   # what the inverse GEMM writes
+        O = np.zeros((nm, R, world * W), dtype=np.float32)
+        for p in range(world):
+            ap, bwp, npp = _band(rows, p, nlat)
+            for i, m in enumerate(mine):
+                for r, (b, ri, c) in enumerate(_rows_of(B, C)):
+                    v = X[b * C + c, :, m]
+                    v = v.real if ri == 0 else v.imag
+                    base = p * blk + (i * R + r) * 2 * W
+                    ks = np.arange(ap, ap + bwp)
+                    kp = ks[:npp]
+                    xs = v[ks].copy()
+                    xs[:npp] += v[nlat - 1 - kp]
+                    np.testing.assert_allclose(buf[base:base + bwp], xs, rtol=1e-6, atol=1e-6)
+                    np.testing.assert_allclose(buf[base + W:base + W + npp],
+                                               v[kp] - v[nlat - 1 - kp], rtol=1e-6, atol=1e-6)
+                    assert not buf[base + bwp:base + W].any()
+                    assert not buf[base + W + npp:base + 2 * W].any()
+                    # identity "transform": E = Xs / 2 on pairs (Xs on the equator), O = Xa / 2
+                    e = buf[base:base + bwp].copy()
+                    e[:npp] *= 0.5
+                    E[i, r, p * W:p * W + bwp] = e
+                    O[i, r, p * W:p * W + npp] = 0.5 * buf[base + W:base + W + npp]
+        # phase 1: m -> rows; the send buffer [dst p][slab][R][E_p | O_p]
         sc1, rc1 = latband.exchange_counts(world, rank, nlat, mmax, rows, own, R, 1)
-        send1 = torch.from_numpy(_band_pack(F.reshape(nm * R, nlat), rows))
+        send1 = np.zeros((world, nm, R, 2 * W), dtype=np.float32)
+        for p in range(world):
+            send1[p, :, :, :W] = E[:, :, p * W:(p + 1) * W]
+            send1[p, :, :, W:] = O[:, :, p * W:(p + 1) * W]
+        send1 = torch.from_numpy(send1.reshape(-1))
         assert send1.numel() == sum(sc1)
         recv1 = torch.zeros(sum(rc1))
         comm.all_to_all(send1, sc1, recv1, rc1)
-        Y = _unpack_inv(recv1.numpy(), perm, mact, B, C, r1 - r0, mmax)
-        want = X[:, r0:r1].copy()
+        Y = _unpack_inv(recv1.numpy(), perm, mact, B, C, bw, npair, W, mmax)
+        want = X[:, loc].copy()
         want[:, :, mact:] = 0
-        np.testing.assert_array_equal(Y, want)
+        np.testing.assert_allclose(Y, want, rtol=1e-5, atol=1e-5)
         q.put((rank, "ok"))
     except Exception as e:  # report to the parent
         q.put((rank, repr(e)))
