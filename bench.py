@@ -196,10 +196,8 @@ def stage_work(name, B, C, nlat, nlon, lmax, mmax, hid, shid, rows=None, mset=No
         "transpose_fwd": ("hbm", 2 * BC * rows * mmax * 8),
         "transpose_inv": ("hbm", 2 * BC * rows * mmax * 8),
         "linear_contract": ("hbm", 8 * C * C * T + 2 * 8 * BC * T),
-        # latitude-band exchange re-layouts (this rank's rows / m-set)
+        # latitude-band pack: the forward transpose into the send buffer (this rank's rows)
         "band_pack": ("hbm", 2 * BC * rows * mmax * 8),
-        "band_gather": ("hbm", 2 * 2 * BC * nlat * len(ms) * 4),
-        "band_scatter": ("hbm", 2 * 2 * BC * nlat * len(ms) * 4),
     }
     return tab.get(name)
 

@@ -157,7 +157,7 @@ static const char* kStageNames[MSFNO_PROF_NSTAGES] = {
     "spectral_l1", "spectral_l2", "spectral_l3", "spectral_out", "linear_gather",
     "linear_contract", "linear_scatter", "legendre_inv", "transpose_inv", "fft_inv",
     "inner_skip", "norm1_film_fold", "mlp_fc1", "mlp_fc2", "out_affine", "band_pack",
-    "band_gather", "band_scatter", "band_exchange", "mlp_fused", "end"};
+    "band_exchange", "mlp_fused", "end"};
 
 struct Profiler {
   bool on = false;
@@ -1200,7 +1200,7 @@ using namespace msfno;
 extern "C" {
 
 const char* msfno_last_error(void) { return g_last_error.c_str(); }
-int msfno_abi_version(void) { return 3; }
+int msfno_abi_version(void) { return 4; }
 
 int msfno_quadrature(int nlat, int grid, double* nodes, double* weights) {
   std::vector<double> x, w;
