@@ -55,7 +55,7 @@ __device__ __forceinline__ void glds16x6(uint64_t sbase, const uint32_t (&voff)[
       : "=&s"(keep)
       : "s"(sbase), "v"(voff[0]), "v"(voff[1]), "v"(voff[2]), "v"(voff[3]), "v"(voff[4]),
         "v"(voff[5]), "s"(lds), "i"(LDS_STEP)
-      : "memory");
+      : "memory", "scc");  // s_add_u32 writes SCC
 }
 
 // s_waitcnt vmcnt(n) for a run-time n, rounded down to a supported immediate

@@ -19,6 +19,8 @@
 // wave 32 x 64 with three accumulator sets (P1, P2, P3).  Stage (72 KB) = A: 3
 // matrices x 3 planes x [128][16] + B: 3 x 3 x [16][128]; two stages, one k-tile
 // in flight (LDS-DMA, dma.h).  LDS swizzles as in gemm_x6p_kernel.
+#include <cstdlib>
+
 #include "dma.h"
 #include "gemm_common.h"
 
@@ -168,11 +170,14 @@ __global__ void split3m_kernel(const float* __restrict__ S, unsigned short* __re
   }
 }
 
-template <bool PLANES_OUT>
-__global__ __launch_bounds__(512) void gemm_x6c_kernel(X6CParams p) {
+// WGM x WGN waves: 4 x 2 (32 x 64 per wave, two waves per SIMD) or 2 x 2 (64 x 64
+// per wave, one wave per SIMD: a third fewer LDS fragment reads per MFMA)
+template <bool PLANES_OUT, int WGM = 4, int WGN = 2>
+__global__ __launch_bounds__(64 * WGM * WGN) void gemm_x6c_kernel(X6CParams p) {
   constexpr int BM = X6C_BM, BN = X6C_BN, BK = X6C_BK;
-  constexpr int WGM = 4, WGN = 2;
-  constexpr int WM = BM / WGM, WN = BN / WGN;  // 32 x 64
+  constexpr int NW = WGM * WGN;
+  constexpr int NPC = 72 / NW;  // 1-KB DMA pieces per wave and k-tile
+  constexpr int WM = BM / WGM, WN = BN / WGN;
   constexpr int MT = WM / 32, NT = WN / 32;
   constexpr int A_PLANE = BM * BK, B_PLANE = BK * BN;  // bf16 elements per matrix plane
   constexpr int A_ALL = 9 * A_PLANE;
@@ -199,14 +204,14 @@ __global__ __launch_bounds__(512) void gemm_x6c_kernel(X6CParams p) {
   const int nk = (K + BK - 1) / BK;
   const unsigned short* X = p.X + z * p.x_b;
 
-  // LDS-DMA pieces c = wave + 8 q (q < 9): c < 36 -> A (matrix-plane c / 4, rows
+  // LDS-DMA pieces c = wave + NW q (q < NPC): c < 36 -> A (matrix-plane c / 4, rows
   // 32 (c % 4) ..), else B (matrix-plane (c - 36) / 4, k rows 4 ((c - 36) % 4) ..)
-  const unsigned short* src[9];
-  int dst[9];
-  int brow[9];  // B: k row of this lane within the k-tile (-1 for A pieces)
+  const unsigned short* src[NPC];
+  int dst[NPC];
+  int brow[NPC];  // B: k row of this lane within the k-tile (-1 for A pieces)
 #pragma unroll
-  for (int q = 0; q < 9; ++q) {
-    const int c = wave + 8 * q;
+  for (int q = 0; q < NPC; ++q) {
+    const int c = wave + NW * q;
     if (c < 36) {
       const int mp = c >> 2, mb = c & 3;
       const int mat = mp / 3, pl = mp - 3 * mat;
@@ -231,7 +236,7 @@ __global__ __launch_bounds__(512) void gemm_x6c_kernel(X6CParams p) {
   auto issue = [&](int kt, int st) {
     const uint32_t base = ring_lds + (uint32_t)(st * STAGE * 2);
 #pragma unroll
-    for (int q = 0; q < 9; ++q) {
+    for (int q = 0; q < NPC; ++q) {
       const unsigned short* g = brow[q] < 0
                                     ? src[q] + kt * a_kstride
                                     : src[q] + (int64_t)min(kt * BK + brow[q], K - 1) * ldx;
@@ -429,10 +434,21 @@ int gemm_x6c(const unsigned short* Aw, int co, int ci, const unsigned short* X, 
   p.tiles_n = (int)cdiv(N, X6C_BN);
   p.relu = relu ? 1 : 0;
   const dim3 grid(p.tiles_m * p.tiles_n, 1, B);
-  if (Y)
-    hipLaunchKernelGGL(gemm_x6c_kernel<true>, grid, dim3(512), 0, s, p);
-  else
-    hipLaunchKernelGGL(gemm_x6c_kernel<false>, grid, dim3(512), 0, s, p);
+  static const int waves = [] {
+    const char* e = getenv("MSFNO_X6C_WAVES");
+    return (e && atoi(e) == 4) ? 4 : 8;
+  }();
+  if (waves == 4) {
+    if (Y)
+      hipLaunchKernelGGL((gemm_x6c_kernel<true, 2, 2>), grid, dim3(256), 0, s, p);
+    else
+      hipLaunchKernelGGL((gemm_x6c_kernel<false, 2, 2>), grid, dim3(256), 0, s, p);
+  } else {
+    if (Y)
+      hipLaunchKernelGGL((gemm_x6c_kernel<true, 4, 2>), grid, dim3(512), 0, s, p);
+    else
+      hipLaunchKernelGGL((gemm_x6c_kernel<false, 4, 2>), grid, dim3(512), 0, s, p);
+  }
   return launch_check("gemm_x6c");
 }
 

@@ -153,7 +153,9 @@ __device__ __forceinline__ const unsigned short* mf_slice_src(const MlpFusedPara
 }
 
 // MF_AHEAD: k-steps of A fragments read ahead of the MFMAs (LDS latency cover)
-template <int SCHED, int STAMP, int DBG = 0, int MF_AHEAD = 2>
+// XS: the read-ahead crosses slice boundaries (XS = 1: two k-steps ahead, always;
+// the next slice's barrier runs inside the current step, see xstep below)
+template <int SCHED, int STAMP, int DBG = 0, int MF_AHEAD = 2, int XS = 0>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
 void mlp_fused_kernel(MlpFusedParams p) {
   // DBG (diagnostic timing builds only, wrong results): 1 no ring waits / barriers /
@@ -441,7 +443,8 @@ void mlp_fused_kernel(MlpFusedParams p) {
     constexpr int c = decltype(c_c)::value;
     const float* rs = stage_res + (c % 3) * (MF_RES_CHUNK / 4) + 32 * wave + l32;
 #pragma unroll
-    for (int r = 0; r < 16; ++r) oacc[c][r] += rs[((r >> 2) * 8 + 4 * half + (r & 3)) * MF_PX];
+    for (int r = 0; r < 16; ++r)
+      oacc[c][r] += rs[((r >> 2) * 8 + 4 * half + (r & 3)) * MF_PX];
   };
   auto do_round = [&](int j, auto par_c) {
     const int q = 2 + 4 * (j - 1);
@@ -458,6 +461,145 @@ void mlp_fused_kernel(MlpFusedParams p) {
     fc2_step(step_begin(q + 3, ex), q + 3, I1{});
   };
 
+  if constexpr (XS) {
+    // ---- cross-step schedule --------------------------------------------------------
+    // Fragment f of the current slice lives in af[f & 3].  Inside step q, after the
+    // MFMAs of k-step 6, slice_wait(q + 1) makes slice q + 1 visible (every wave's DMA
+    // of it landed, and every wave has finished reading slice q: its slot takes slice
+    // q + 4 right away), and the first two fragments of slice q + 1 are read under
+    // k-steps 6 and 7: the MFMA pipe does not restart from an LDS read at each slice.
+    using K1 = std::integral_constant<int, 0>;  // W1 slice
+    using K2 = std::integral_constant<int, 1>;  // W2 slice
+    using KN = std::integral_constant<int, 2>;  // no next slice
+    constexpr int QA = 2 + 4 * (MF_HB - 4), QB = 2 + 4 * (MF_HB - 2);  // residual issue steps
+    bf16x8 af[4][3];
+    auto load_frag = [&](int q, auto kind_c, int f) {
+      constexpr int KIND = decltype(kind_c)::value;
+      const unsigned short* slot = ring + (q % MF_NS) * MF_SLICE_ELEMS;
+#pragma unroll
+      for (int pl = 0; pl < 3; ++pl) {
+        const int off = KIND == 0 ? (pl * 8 + f) * 512 + a_lane
+                                  : ((pl * 2 + (f & 1)) * 128 + (f >> 1) * 32) * 16 + a_lane;
+        af[f & 3][pl] = *reinterpret_cast<const bf16x8*>(slot + off);
+      }
+    };
+    // slice q visible to every wave; DMA instructions this wave issued after slice q:
+    // slices q + 1, q + 2 (6 each) and, around the residual issues, 12 more
+    auto slice_wait = [&](int q) {
+      if constexpr ((DBG & 1) != 0) return;
+      unsigned long long w0 = 0;
+      if constexpr (STAMP) w0 = __builtin_amdgcn_s_memtime();
+      const int after = min(2, MF_NSLICE - 1 - q);
+      const bool ex = has_res && ((q >= QA + 2 && q <= QA + 4) || (q >= QB + 2 && q <= QB + 3));
+      if (after >= 2 && ex)
+        asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
+      else if (after >= 2)
+        asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+      else if (after == 1)
+        asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+      else
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      if constexpr (STAMP) st_wait += __builtin_amdgcn_s_memtime() - w0;
+    };
+    // step q: a W1 slice (KIND 0: hidden block into hacc[PAR], converting block jc of
+    // hacc[PAR ^ 1] under it when CONV) or a W2 slice (KIND 1: out rows 128 SUB ..)
+    auto xstep = [&](int q, auto kind_c, auto next_c, auto sub_c, auto par_c, auto conv_c,
+                     int jc) {
+      constexpr int KIND = decltype(kind_c)::value, NEXT = decltype(next_c)::value;
+      constexpr int SUB = decltype(sub_c)::value, PAR = decltype(par_c)::value;
+      constexpr bool CONV = decltype(conv_c)::value;
+      using PPrev = std::integral_constant<int, PAR ^ 1>;
+#pragma unroll
+      for (int ks = 0; ks < 8; ++ks) {
+        if (ks + 2 < 8 && (DBG & 8) == 0) load_frag(q, kind_c, ks + 2);
+        const int fi = (DBG & 8) ? 0 : (ks & 3);
+        if constexpr (KIND == 0) {
+          hacc[PAR] = mfma6(af[fi], xf[SUB * 8 + ks], hacc[PAR]);
+          if constexpr (CONV) {
+            if (ks & 1) conv_pair(jc, 4 * SUB + (ks >> 1), PPrev{});
+          }
+        } else {
+          const int sh = ks & 1;
+          const uint32_t (&h)[2][3][4] = hfu;
+          const bf16x8 hb[3] = {mf_frag(h[sh][0][0], h[sh][0][1], h[sh][0][2], h[sh][0][3]),
+                                mf_frag(h[sh][1][0], h[sh][1][1], h[sh][1][2], h[sh][1][3]),
+                                mf_frag(h[sh][2][0], h[sh][2][1], h[sh][2][2], h[sh][2][3])};
+          oacc[SUB * 4 + (ks >> 1)] = mfma6(af[fi], hb, oacc[SUB * 4 + (ks >> 1)]);
+        }
+        kstep_schedule(ks + 2 < 8 && (DBG & 8) == 0);
+        if constexpr (NEXT != 2) {
+          if (ks == 6) {
+            slice_wait(q + 1);
+            refill(q + 1);
+          }
+          if (ks >= 6 && (DBG & 8) == 0)
+            load_frag(q + 1, std::integral_constant<int, NEXT>{}, ks - 6);
+        }
+      }
+      if constexpr (KIND == 0 && CONV && SUB == 1) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) hacc[PAR ^ 1][r] = 0.f;
+      }
+    };
+    auto xround = [&](int j, auto par_c) {
+      const int q = 2 + 4 * (j - 1);
+      xstep(q, K1{}, K1{}, I0{}, par_c, T{}, j - 1);
+      if (has_res && j == MF_HB - 3) {  // q == QA; slices up to q + 4 issued
+        issue_res(0);
+        issue_res(1);
+        issue_res(2);
+      }
+      xstep(q + 1, K1{}, K2{}, I1{}, par_c, T{}, j - 1);
+      xstep(q + 2, K2{}, K2{}, I0{}, I0{}, F{}, 0);
+      xstep(q + 3, K2{}, K1{}, I1{}, I0{}, F{}, 0);
+    };
+    // slice 0 landed (prologue); its slot's successor slice 3 (the x1 staging is free)
+    issue(3);
+    load_frag(0, K1{}, 0);
+    load_frag(0, K1{}, 1);
+    xstep(0, K1{}, K1{}, I0{}, I0{}, F{}, 0);
+    xstep(1, K1{}, K1{}, I1{}, I0{}, F{}, 0);
+    for (int j = 1; j < MF_HB - 1; j += 2) {
+      xround(j, I1{});
+      xround(j + 1, I0{});
+    }
+    // round 15 (peeled): residual chunks 0-2 in (slice_wait(58) retired them), 3-5 out
+    if (has_res) {
+      add_res(I0{});
+      add_res(I1{});
+      add_res(std::integral_constant<int, 2>{});
+    }
+    xstep(QB, K1{}, K1{}, I0{}, I1{}, T{}, MF_HB - 2);
+    if (has_res) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();  // regions 0-2 read by every wave
+      issue_res(3);
+      issue_res(4);
+      issue_res(5);
+    }
+    xstep(QB + 1, K1{}, K2{}, I1{}, I1{}, T{}, MF_HB - 2);
+    xstep(QB + 2, K2{}, K2{}, I0{}, I0{}, F{}, 0);
+    xstep(QB + 3, K2{}, K2{}, I1{}, I0{}, F{}, 0);  // slice_wait(62): vmcnt(6) retired chunks 3-5
+    if (has_res) {
+      add_res(std::integral_constant<int, 3>{});
+      add_res(std::integral_constant<int, 4>{});
+      add_res(std::integral_constant<int, 5>{});
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      issue_res(6);
+      issue_res(7);
+    }
+#pragma unroll
+    for (int e2 = 0; e2 < 8; ++e2) conv_pair(MF_HB - 1, e2, I1{});
+    xstep(MF_NSLICE - 2, K2{}, K2{}, I0{}, I0{}, F{}, 0);  // slice_wait(63): vmcnt(0), chunks 6, 7
+    xstep(MF_NSLICE - 1, K2{}, KN{}, I1{}, I0{}, F{}, 0);
+    if (has_res) {
+      add_res(std::integral_constant<int, 6>{});
+      add_res(std::integral_constant<int, 7>{});
+    }
+  } else {
   fc1_step(step_begin(0), 0, I0{}, I0{}, F{}, 0);
   fc1_step(step_begin(1), 1, I1{}, I0{}, F{}, 0);
   for (int j = 1; j < MF_HB - 1; j += 2) {
@@ -508,6 +650,7 @@ void mlp_fused_kernel(MlpFusedParams p) {
       add_res(std::integral_constant<int, 7>{});
     }
   }
+  }  // XS
 
   if constexpr (STAMP) stamp(3, __builtin_amdgcn_s_memtime());
   // ---- store (all DMA retired: the last step waited vmcnt(0)) ------------------------
@@ -629,9 +772,17 @@ int launch_mlp_fused(const float* x1, const float* scale, const float* shift, co
     const char* e = getenv("MSFNO_MF_AHEAD");
     return e ? atoi(e) : 2;
   }();
+  // MSFNO_MF_XS=1: cross-step A-fragment prefetch (the next slice's barrier inside the
+  // current step), for A/B
+  static const int xs = [] {
+    const char* e = getenv("MSFNO_MF_XS");
+    return e ? atoi(e) : 0;
+  }();
   if (stamps) return mlp_fused_stamped(p, tiles, sched, s);
   const dim3 grid((unsigned)tiles), blk(256);
-  if (!sched)
+  if (xs)
+    hipLaunchKernelGGL((mlp_fused_kernel<1, 0, 0, 2, 1>), grid, blk, 0, s, p);
+  else if (!sched)
     hipLaunchKernelGGL((mlp_fused_kernel<0, 0, 0, 2>), grid, blk, 0, s, p);
 
   else if (ahead == 1)
