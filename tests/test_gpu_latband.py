@@ -146,6 +146,27 @@ def test_sharded_block_config2_matches_unsharded():
     assert err < 2e-5, err
 
 
+@pytest.mark.slow
+def test_sharded_block_config4_geometry_eight_ranks():
+    """Config 4's sharding (721x1440, C=256, lmax=360, 8 ranks: bands of 45/46 rows +
+    mirrors, W = 48, 8 source blocks in the Legendre GEMMs' K) on 8 lock-step virtual
+    ranks, a batch of 2 fields, against the unsharded native block."""
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    args = bench.parse_args([])
+    blk, _, _ = bench.build_block(args, torch.device(DEV))
+    gen = torch.Generator().manual_seed(4)
+    x = torch.randn(2, 256, 721, 1440, generator=gen).to(DEV)
+    g = (0.1 * torch.randn(2, 256, generator=gen)).to(DEV)
+    b = (0.1 * torch.randn(2, 256, generator=gen)).to(DEV)
+    with torch.no_grad():
+        y1 = blk(x, g, b, 1.0)
+        y = _sharded(blk, x, g, b, 1.0, 8)
+    err = (y - y1).abs().max().item()
+    assert err < 2e-5, err
+
+
 def _dist_rank(rank, world, port, path, q, chunks=1):
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
