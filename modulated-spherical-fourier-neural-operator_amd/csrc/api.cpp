@@ -1526,8 +1526,9 @@ size_t msfno_mlp_workspace_size(const msfno_mlp_desc* d, int B, long long P) {
   if (!d || B <= 0 || P <= 0) return 0;
   Carve cv;
   cv.take<float>(std::max<int64_t>((int64_t)B * d->Hid * P, mlp_h_floats(B, d->Hid, P)));  // h
-  if (d->Cin2 > 0) cv.take<float>((int64_t)B * d->Hid * P);  // first half of fc1
-  cv.take<char>(gemm_dense_workspace(d->Hid, d->Cin, 1));   // split fc1 weights
+  // first half of fc1 (two-GEMM concatenation on the fp32 engine only)
+  if (d->Cin2 > 0 && !gemm_use_x6()) cv.take<float>((int64_t)B * d->Hid * P);
+  cv.take<char>(gemm_dense_workspace(d->Hid, d->Cin + d->Cin2, 1));  // split fc1 weights
   if (d->Cin2 > 0) cv.take<char>(gemm_dense_workspace(d->Hid, d->Cin2, 1));
   cv.take<char>(gemm_dense_workspace(d->Cout, d->Hid, 1));  // split fc2 weights
   return cv.off;
@@ -1550,8 +1551,8 @@ int msfno_mlp_forward(const msfno_mlp_desc* d, const float* x, const float* x2,
   cv.base = (char*)ws;
   const int64_t Hd = d->Hid, Ct = d->Cin + d->Cin2;
   float* h = cv.take<float>(std::max<int64_t>((int64_t)B * Hd * P, mlp_h_floats(B, Hd, P)));
-  float* t = d->Cin2 > 0 ? cv.take<float>((int64_t)B * Hd * P) : nullptr;
-  const size_t w1b = gemm_dense_workspace((int)Hd, d->Cin, 1);
+  float* t = (d->Cin2 > 0 && !gemm_use_x6()) ? cv.take<float>((int64_t)B * Hd * P) : nullptr;
+  const size_t w1b = gemm_dense_workspace((int)Hd, (int)Ct, 1);
   void* w1 = cv.take<char>(w1b);
   const size_t w1b2 = d->Cin2 > 0 ? gemm_dense_workspace((int)Hd, d->Cin2, 1) : 0;
   void* w12 = d->Cin2 > 0 ? cv.take<char>(w1b2) : nullptr;
@@ -1565,7 +1566,18 @@ int msfno_mlp_forward(const msfno_mlp_desc* d, const float* x, const float* x2,
   const int64_t ldh = planes ? round_up(P, 8) : P;
   unsigned short* hx = planes ? reinterpret_cast<unsigned short*>(h) : nullptr;
   prof(ST_FC1, s);
-  if (d->Cin2 > 0) {
+  if (d->Cin2 > 0 && gemm_use_x6()) {
+    // fc1 over the concatenation [x ; x2] as one GEMM, K = Cin + Cin2: the B rows past
+    // Cin are read from x2 in place (GemmEpi::b2)
+    GemmEpi e1;
+    e1.bias = d->fc1_b;
+    e1.act = 1;
+    e1.b2 = x2; e1.b2_k = d->Cin; e1.b2_ld = Pi; e1.b2_stride = (int64_t)d->Cin2 * P;
+    if (planes) { e1.c_planes = hx; e1.c_plane_stride = Hd * ldh; }
+    MSFNO_TRY(gemm_dense(ROLE_FC1, TILE_128x256, d->fc1_w, x, h, (int)Hd, Pi, (int)Ct, (int)Ct, Pi,
+                         (int)ldh, 0, (int64_t)d->Cin * P, (planes ? 3 : 1) * Hd * ldh, B, e1, w1,
+                         w1b, s));
+  } else if (d->Cin2 > 0) {
     // fc1 over the concatenation [x ; x2]: t = W1[:, :Cin]·x, then h = GELU(W1[:, Cin:]·x2 + b1 + t)
     GemmEpi e0;
     MSFNO_TRY(gemm_dense(ROLE_FC1, TILE_128x256, d->fc1_w, x, t, (int)Hd, Pi, d->Cin, (int)Ct, Pi,

@@ -145,6 +145,11 @@ struct GemmEpi {
   // q at q * seg_stride floats from the operand base (0: contiguous)
   int segA_w = 0, segC_w = 0;
   int64_t segA_stride = 0, segC_stride = 0;
+  // gemm_x6 with fp32 B only: B rows k >= b2_k come from b2 (row k - b2_k, ld b2_ld,
+  // batch stride b2_stride): the K concatenation [B ; b2] without materialising it
+  const float* b2 = nullptr;
+  int b2_k = 0, b2_ld = 0;
+  int64_t b2_stride = 0;
 };
 
 enum GemmTile {

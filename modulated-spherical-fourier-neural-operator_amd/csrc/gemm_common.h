@@ -42,6 +42,10 @@ struct GemmParams {
   // segmented K of A / columns of C (GemmEpi::segA_w ...; 0 = contiguous)
   int segA_w, segC_w;
   int64_t segA_stride, segC_stride;
+  // K-concatenated fp32 B (GemmEpi::b2): rows k >= kb2 at B2 + (k - kb2) * ldb2
+  const float* B2;
+  int kb2, ldb2;
+  int64_t sB2;
 };
 
 __device__ __forceinline__ int xcd_remap(int orig, int nwg) {

@@ -94,6 +94,7 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_x6_kernel(GemmParams p) {
   const int z = blockIdx.z;
   const unsigned short* Ax = p.Ax + z * p.sAx;
   const float* B = p.B + z * p.sB;
+  const float* B2 = p.B2 ? p.B2 + z * p.sB2 : nullptr;
   float* C = p.C + z * p.sC;
   const float* bias = p.bias ? p.bias + z * p.sBias : nullptr;
   const float* addend = p.addend ? p.addend + z * p.sD : nullptr;
@@ -147,7 +148,8 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_x6_kernel(GemmParams p) {
       const int f = tid + NTHR * q;
       const int kr = min(kt * BK + f / (BN / 4), Kc);
       const int col = n0 + 4 * (f % (BN / 4));
-      const float* src = B + (int64_t)kr * ldb;
+      const float* src = (B2 && kr >= p.kb2) ? B2 + (int64_t)(kr - p.kb2) * p.ldb2
+                                             : B + (int64_t)kr * ldb;
       if constexpr (VEC) {
         rb[q] = *reinterpret_cast<const float4*>(src + min(col, Nc & ~3));
       } else {
@@ -388,6 +390,13 @@ int gemm_x6(GemmTile tile, const float* A, const float* B, float* C, int M, int 
   p.rowscale = epi.rowscale;
   p.Ax = Ax; p.sAxp = (int64_t)Mp * Kp; p.sAx = sA == 0 ? 0 : 3 * p.sAxp; p.ldax = Kp;
   p.vecB = (ldb % 4 == 0) && (sB % 4 == 0) && ((reinterpret_cast<uintptr_t>(B) & 15) == 0);
+  p.B2 = epi.b2; p.kb2 = epi.b2_k; p.ldb2 = epi.b2_ld; p.sB2 = epi.b2_stride;
+  if (p.B2) {
+    MSFNO_REQUIRE(!epi.b_planes && epi.b2_k > 0 && epi.b2_k < K, MSFNO_EINVAL,
+                  "gemm_x6: bad K concatenation");
+    p.vecB = p.vecB && (p.ldb2 % 4 == 0) && (p.sB2 % 4 == 0) &&
+             ((reinterpret_cast<uintptr_t>(p.B2) & 15) == 0);
+  }
   p.Bx = epi.b_planes; p.sBxp = epi.b_plane_stride;
   p.Cx = epi.c_planes; p.sCxp = epi.c_plane_stride;
   p.cx16 = cx16_enabled() && p.Cx && ldc % 8 == 0 && sC % 8 == 0 && p.sCxp % 8 == 0 &&
