@@ -153,7 +153,7 @@ def parse(argv=None):
                          "(RCCL all-to-all; the auto default) or independent replicas")
     ap.add_argument("--band-chunks", type=int, default=0,
                     help="latband: sub-batches pipelined so exchanges overlap compute "
-                         "(0: one sub-batch per field pair, at most 4)")
+                         "(0: one sub-batch per field, at most 4)")
     ap.add_argument("--replicas-check", type=int, default=1,
                     help="latband, N>1: also time the replica mode (comm-free upper bound)")
     ap.add_argument("--dry-run", action="store_true",
@@ -599,7 +599,9 @@ def main():
         gamma = 0.1 * torch.randn(B, C, generator=gd, device=dev)
         beta = 0.1 * torch.randn(B, C, generator=gd, device=dev)
         comm = TorchComm() if dist else None
-        chunks = args.band_chunks if args.band_chunks > 0 else max(1, min(4, B // 2))
+        # at least two sub-batches whenever the batch allows (N = 2 exchanges over a
+        # single xGMI link: one sub-batch's all-to-all hides behind the other's compute)
+        chunks = args.band_chunks if args.band_chunks > 0 else max(1, min(4, B))
 
         def step():
             return shard(x, gamma, beta, 1.0, comm=comm, chunks=chunks)
