@@ -66,7 +66,7 @@ STAGE_KERNEL_X6 = {
     "mlp_fc2": "void msfno::gemm_x6p_kernel<3, 2, 8, 256>(msfno::GemmParams)",
     "inner_skip": "void msfno::gemm_x6p_kernel<1, 2, 8, 256>(msfno::GemmParams)",
     # fc1 -> GELU -> fc2 in one kernel, hidden activation on-chip (csrc/mlp_fused.hip)
-    "mlp_fused": "void msfno::(anonymous namespace)::mlp_fused_kernel<1, 0, 0, 2>"
+    "mlp_fused": "void msfno::(anonymous namespace)::mlp_fused_kernel<1, 0, 0, 2, 0>"
                  "(msfno::(anonymous namespace)::MlpFusedParams)",
 }
 STAGE_KERNEL_F32 = {
