@@ -64,7 +64,9 @@ STAGE_KERNEL_X6 = {
     "mlp_fc1": "void msfno::gemm_x6p_kernel<133, 2, 8, 256>(msfno::GemmParams)",
     # fc2: h planes staged by LDS-DMA (x6p), bias + outer skip (EPI 3)
     "mlp_fc2": "void msfno::gemm_x6p_kernel<3, 2, 8, 256>(msfno::GemmParams)",
-    "inner_skip": "void msfno::gemm_x6p_kernel<1, 2, 8, 256>(msfno::GemmParams)",
+    # inner skip: fp32 x split in-kernel (gemm_x6, bias epilogue); the plane form
+    # (MSFNO_SKIP_PLANES=1) is gemm_x6p_kernel<1, 2, 8, 256>
+    "inner_skip": "void msfno::gemm_x6_kernel<256, 256, 4, 2, true, 1, false>(msfno::GemmParams)",
     # fc1 -> GELU -> fc2 in one kernel, hidden activation on-chip (csrc/mlp_fused.hip)
     "mlp_fused": "void msfno::(anonymous namespace)::mlp_fused_kernel<1, 0, 0, 2, 0>"
                  "(msfno::(anonymous namespace)::MlpFusedParams)",
@@ -184,10 +186,11 @@ def stage_work(name, B, C, nlat, nlon, lmax, mmax, hid, shid, rows=None, mset=No
         "legendre_fwd": ("mfma", 2 * (2 * BC) * nlat * T),
         "legendre_inv": ("mfma", 2 * (2 * BC) * nlat * T),
         # HBM-bound stages: compulsory bytes moved
-        # rfft: x read + spectrum written (+ x as bf16x3 planes for the inner-skip GEMM on
-        # the x6 engine, whole-field block only)
+        # rfft: x read + spectrum written (+ x as bf16x3 planes for the inner-skip GEMM
+        # with MSFNO_SKIP_PLANES=1 on the x6 engine, whole-field block only)
         "fft_fwd": ("hbm", BC * rows * (nlon * 4 + mmax * 8 +
-                                        (nlon * 6 if x6_engine()[0] and mset is None else 0))),
+                                        (nlon * 6 if x6_engine()[0] and mset is None and
+                                         os.environ.get("MSFNO_SKIP_PLANES") == "1" else 0))),
         # irfft: Yn read + skip-branch row read + x1 written (bf16x3 planes, 6 B per
         # value, on the x6 engine with the unfused MLP; fp32 for the fused one)
         "fft_inv": ("hbm", BC * rows * (mmax * 8 + nlon * 4 +

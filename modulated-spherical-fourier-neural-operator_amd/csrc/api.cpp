@@ -1118,15 +1118,22 @@ int run_mlp(const msfno_block_desc* d, const float* W1f, const float* b1f, const
                     dw.fc2_b, s);
 }
 
-// the inner-skip GEMM reads x as bf16x3 planes written by the forward FFT (into the
-// x1 plane buffer); MSFNO_SKIP_PLANES=0 keeps the in-kernel split (gemm_x6) for A/B
-bool skip_planes(const msfno_block_desc* d, const msfno_sht_plan_s* f, const BlockBufs& b) {
+// the inner-skip GEMM reads fp32 x and splits it in-kernel (gemm_x6), forked before
+// the forward FFT; MSFNO_SKIP_PLANES=1: x as bf16x3 planes written by the forward FFT
+// (into the x1 plane buffer), the GEMM forked after it.  With the fused MLP the fp32
+// form measured 2.8 % faster per block (rfft 0.70 -> 0.51 ms without the 1.6 GB of
+// plane stores)
+static bool skip_planes_env() {
   static const bool on = [] {
     const char* e = getenv("MSFNO_SKIP_PLANES");
-    return !(e && e[0] == '0');
+    return e && e[0] == '1';
   }();
-  return on && b.x1p && b.dw.skip && d->inner_skip == MSFNO_SKIP_LINEAR && !use_fft_tile(f) &&
-         fft_r2c_planes_supported(f->fft, f->mmax);
+  return on;
+}
+
+bool skip_planes(const msfno_block_desc* d, const msfno_sht_plan_s* f, const BlockBufs& b) {
+  return skip_planes_env() && b.x1p && b.dw.skip && d->inner_skip == MSFNO_SKIP_LINEAR &&
+         !use_fft_tile(f) && fft_r2c_planes_supported(f->fft, f->mmax);
 }
 
 // pixels per fc1 -> fc2 chunk of the block MLP (MSFNO_MLP_CHUNK, multiple of 256;
@@ -1158,8 +1165,9 @@ bool mlp_fused(const msfno_block_desc* d, int64_t P) {
 }
 
 bool x1p_buffer(const msfno_block_desc* d, const msfno_sht_plan_s* g) {
-  return x1_planes(d, g) || (mlp_fused(d, (int64_t)g->nlat * g->nlon) &&
-                             d->inner_skip == MSFNO_SKIP_LINEAR && mlp_h_planes(true));
+  return x1_planes(d, g) ||
+         (skip_planes_env() && mlp_fused(d, (int64_t)g->nlat * g->nlon) &&
+          d->inner_skip == MSFNO_SKIP_LINEAR && mlp_h_planes(true));
 }
 
 int run_block_mlp(const msfno_block_desc* d, const float* x1, const unsigned short* x1p,

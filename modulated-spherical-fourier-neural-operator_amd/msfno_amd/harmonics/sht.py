@@ -15,6 +15,8 @@ on the next call, so the reference's construction recipe keeps working.
 """
 from __future__ import annotations
 
+import weakref
+
 import numpy as np
 import torch
 import torch.nn as nn
@@ -129,3 +131,67 @@ class InverseRealSHT(_SHTBase):
                                           ws.data_ptr(), ws.numel(), N.stream_of(x.device)),
                 "InverseRealSHT.forward")
         return out
+
+
+# ---- foreign transforms ------------------------------------------------------------
+# A block built around torch_harmonics.RealSHT / InverseRealSHT objects (the reference's
+# own, sfnonet.py:537-548) runs on the native plans too: adopt() wraps such an object in
+# the matching class of this module WITHOUT copying its table.  The wrapper reads the
+# foreign buffer (``weights`` / ``pct``) on every call, so the reference's later
+# re-assignment of it (the x1e5 rescale, sfnonet.py:551-555, ``.to(device)``) is seen
+# exactly as for the native classes.  Accepted: any object with nlat, nlon, lmax, mmax
+# and a (mmax, lmax, nlat) table buffer, with norm "ortho" if it says.
+_ADOPTED = weakref.WeakKeyDictionary()
+
+
+class _AdoptedRealSHT(RealSHT):
+    def __init__(self, src):
+        nn.Module.__init__(self)
+        object.__setattr__(self, "_src", src)
+        self.nlat, self.nlon, self.lmax, self.mmax = src.nlat, src.nlon, src.lmax, src.mmax
+        self.grid = getattr(src, "grid", "equiangular")
+        self.norm, self.csphase = "ortho", getattr(src, "csphase", True)
+        self._plans = {}
+
+    @property
+    def weights(self):
+        return self._src.weights
+
+
+class _AdoptedInverseRealSHT(InverseRealSHT):
+    def __init__(self, src):
+        nn.Module.__init__(self)
+        object.__setattr__(self, "_src", src)
+        self.nlat, self.nlon, self.lmax, self.mmax = src.nlat, src.nlon, src.lmax, src.mmax
+        self.grid = getattr(src, "grid", "equiangular")
+        self.norm, self.csphase = "ortho", getattr(src, "csphase", True)
+        self._plans = {}
+
+    @property
+    def pct(self):
+        return self._src.pct
+
+
+def adopt(t, inverse: bool):
+    """This module's transform for `t`: `t` itself when it already is one, else a
+    table-sharing wrapper of a torch-harmonics-style transform (NotImplementedError
+    when `t` does not look like one)."""
+    ours = InverseRealSHT if inverse else RealSHT
+    if isinstance(t, ours):
+        return t
+    name = "pct" if inverse else "weights"
+    kind = "InverseRealSHT" if inverse else "RealSHT"
+    tab = getattr(t, name, None)
+    if not isinstance(tab, torch.Tensor) or not all(
+            hasattr(t, a) for a in ("nlat", "nlon", "lmax", "mmax")):
+        raise NotImplementedError(f"expected a {kind} (torch_harmonics or msfno_amd.harmonics), "
+                                  f"got {type(t).__name__}")
+    if getattr(t, "norm", "ortho") != "ortho":
+        raise NotImplementedError(f"Unsupported SHT normalisation {t.norm!r} (only 'ortho')")
+    if tuple(tab.shape) != (t.mmax, t.lmax, t.nlat):
+        raise NotImplementedError(f"{kind}.{name} must have shape (mmax, lmax, nlat)")
+    w = _ADOPTED.get(t)
+    if w is None:
+        w = (_AdoptedInverseRealSHT if inverse else _AdoptedRealSHT)(t)
+        _ADOPTED[t] = w
+    return w

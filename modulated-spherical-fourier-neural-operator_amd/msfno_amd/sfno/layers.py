@@ -16,7 +16,7 @@ import torch
 import torch.nn as nn
 
 from .. import _native as N
-from ..harmonics import InverseRealSHT, RealSHT
+from ..harmonics import adopt
 from .activations import ComplexReLU
 
 
@@ -183,10 +183,12 @@ class _MLPFn(torch.autograd.Function):
 
 
 def _check_transforms(fwd, inv):
-    if not isinstance(fwd, RealSHT) or not isinstance(inv, InverseRealSHT):
-        raise NotImplementedError("MI355X spectral filters require msfno_amd.harmonics transforms")
+    """The native transforms for the filter's (fwd, inv): msfno_amd.harmonics objects as
+    they are, torch-harmonics-style ones wrapped around their own tables (harmonics.adopt)."""
+    fwd, inv = adopt(fwd, False), adopt(inv, True)
     assert inv.lmax == fwd.lmax
     assert inv.mmax == fwd.mmax
+    return fwd, inv
 
 
 class _S2FilterBase(nn.Module):
@@ -250,8 +252,7 @@ class SpectralConvS2(_S2FilterBase):
             raise NotImplementedError("SpectralConvS2(bias=True) is not on the MI355X path")
 
     def _transforms(self):
-        _check_transforms(self.forward_transform, self.inverse_transform)
-        return self.forward_transform, self.inverse_transform
+        return _check_transforms(self.forward_transform, self.inverse_transform)
 
     def _fill_desc(self, d, keep):
         if self.sparsity_threshold != 0.0:
@@ -300,10 +301,7 @@ class SpectralAttentionS2(_S2FilterBase):
         self.activation = ComplexReLU(mode=complex_activation, bias_shape=(self.hidden_size, 1, 1))
 
     def _transforms(self):
-        fwd = self.forward_transform.__self__
-        inv = self.inverse_transform.__self__
-        _check_transforms(fwd, inv)
-        return fwd, inv
+        return _check_transforms(self.forward_transform.__self__, self.inverse_transform.__self__)
 
     def _fill_desc(self, d, keep):
         if self.activation.mode != "real":

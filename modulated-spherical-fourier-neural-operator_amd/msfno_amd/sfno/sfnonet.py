@@ -19,8 +19,17 @@ import torch
 import torch.nn as nn
 
 from .. import _native as N
-from ..harmonics import RealSHT
+from ..harmonics import RealSHT, adopt
 from .layers import MLP, DropPath, SpectralAttentionS2, SpectralConvS2
+
+
+def _is_real_sht(t):
+    """A RealSHT of this package or of torch-harmonics (harmonics.adopt wraps the latter)."""
+    try:
+        adopt(t, False)
+        return True
+    except NotImplementedError:
+        return False
 
 
 class SpectralFilterLayer(nn.Module):
@@ -29,13 +38,13 @@ class SpectralFilterLayer(nn.Module):
                  compression=None, rank=128, complex_network=True, complex_activation="real",
                  spectral_layers=1, drop_rate=0.0):
         super().__init__()
-        if filter_type == "non-linear" and isinstance(forward_transform, RealSHT):
+        if filter_type == "non-linear" and _is_real_sht(forward_transform):
             self.filter = SpectralAttentionS2(
                 forward_transform, inverse_transform, embed_dim_sfno, sparsity_threshold,
                 use_complex_network=complex_network, use_complex_kernels=use_complex_kernels,
                 hidden_size_factor=hidden_size_factor, complex_activation=complex_activation,
                 spectral_layers=spectral_layers, drop_rate=drop_rate, bias=False)
-        elif filter_type == "linear" and isinstance(forward_transform, RealSHT):
+        elif filter_type == "linear" and _is_real_sht(forward_transform):
             self.filter = SpectralConvS2(
                 forward_transform, inverse_transform, embed_dim_sfno, sparsity_threshold,
                 use_complex_kernels=use_complex_kernels, compression=compression, rank=rank,

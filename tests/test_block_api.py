@@ -45,3 +45,28 @@ def test_linear_filter_weight_shape_and_tril_buffers():
     ii, jj = torch.tril_indices(16, 17)
     assert m.w.shape == (4, 4, ii.numel(), 2)
     assert torch.equal(m.ii, ii) and torch.equal(m.jj, jj)
+
+
+def test_torch_harmonics_style_transforms_are_adopted():
+    """A filter built around torch-harmonics-style transforms (here the oracle's
+    restatement of torch_harmonics.RealSHT / InverseRealSHT: same attributes and buffer
+    names) runs on the native plans over the foreign tables, without copying them; a
+    later re-assignment of the foreign buffer (the reference's x1e5 rescale,
+    sfnonet.py:551-555) is seen."""
+    from msfno_amd.harmonics import InverseRealSHT, RealSHT
+    from msfno_amd.sfno import SpectralFilterLayer
+    from oracle import sht_ref as S
+    f = S.RealSHT(16, 32, lmax=16, mmax=17).float()
+    g = S.InverseRealSHT(16, 32, lmax=16, mmax=17).float()
+    for kind in ("linear", "non-linear"):
+        layer = SpectralFilterLayer(f, g, 8, kind)
+        fwd, inv = layer.filter._transforms()
+        assert isinstance(fwd, RealSHT) and isinstance(inv, InverseRealSHT)
+        assert fwd.weights is f.weights and inv.pct is g.pct
+        assert (fwd.nlat, fwd.nlon, fwd.lmax, fwd.mmax) == (16, 32, 16, 17)
+    f.weights = f.weights * 1e5
+    assert layer.filter._transforms()[0].weights is f.weights
+    bad = S.RealSHT(16, 32, lmax=16, mmax=17)
+    bad.norm = "schmidt"
+    with pytest.raises(NotImplementedError):
+        SpectralFilterLayer(bad, g, 8, "linear").filter._transforms()

@@ -225,3 +225,39 @@ def test_rescale_invariance_nonlinear_filter():
     isht.pct = isht.pct * 1e5
     y2 = blk.filter_layer(x)
     assert (y1 - y2).abs().max().item() < 1e-5 * max(1.0, y1.abs().max().item())
+
+
+def test_block_over_torch_harmonics_style_transforms():
+    """The block built around torch-harmonics-style transform objects (the oracle's
+    restatement of torch_harmonics.RealSHT / InverseRealSHT, rescaled x1e5 / /1e5 as
+    sfnonet.py:551-555 does) equals the block built around msfno_amd.harmonics ones."""
+    from functools import partial
+
+    from msfno_amd.harmonics import InverseRealSHT, RealSHT
+    from msfno_amd.sfno import FourierNeuralOperatorBlock_Filmed
+    from oracle import sht_ref as S
+    C, nlat, nlon, lmax = 32, 33, 64, 32
+
+    def build(Fwd, Inv):
+        sht = Fwd(nlat, nlon, lmax=lmax, mmax=lmax + 1, grid="equiangular").float()
+        isht = Inv(nlat, nlon, lmax=lmax, mmax=lmax + 1, grid="equiangular").float()
+        sht.weights = sht.weights * 1e5
+        isht.pct = isht.pct / 1e5
+        norm = partial(torch.nn.InstanceNorm2d, num_features=C, eps=1e-6, affine=True,
+                       track_running_stats=False)
+        torch.manual_seed(3)
+        return FourierNeuralOperatorBlock_Filmed(sht, isht, C, filter_type="non-linear",
+                                                 mlp_ratio=2.0, norm_layer=(norm, norm),
+                                                 inner_skip="linear", outer_skip="identity",
+                                                 mlp_mode="distributed",
+                                                 spectral_layers=3).eval().to(DEV)
+
+    a = build(RealSHT, InverseRealSHT)
+    b = build(S.RealSHT, S.InverseRealSHT)
+    b.load_state_dict(a.state_dict(), strict=False)
+    g = torch.Generator().manual_seed(5)
+    x = torch.randn(2, C, nlat, nlon, generator=g).to(DEV)
+    gm, bt = (0.2 * torch.randn(2, C, generator=g)).to(DEV), (0.2 * torch.randn(2, C, generator=g)).to(DEV)
+    with torch.no_grad():
+        ya, yb = a(x, gm, bt, 0.7), b(x, gm, bt, 0.7)
+    assert (ya - yb).abs().max().item() < 1e-5 * max(1.0, ya.abs().max().item())
