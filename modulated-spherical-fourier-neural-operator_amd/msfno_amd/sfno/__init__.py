@@ -10,5 +10,5 @@ from .sfnonet import (  # noqa: F401
     FourierNeuralOperatorNet_Filmed,
     SpectralFilterLayer,
 )
-from .latband import (LatBandBlock, LocalGroup, TorchComm, band_partition,  # noqa: F401
-                      exchange_counts, local_rows)
+from .latband import (LatBandBlock, LatBandNet, LocalGroup, TorchComm,  # noqa: F401
+                      band_partition, exchange_counts, local_rows)

@@ -489,3 +489,65 @@ class LatBandBlock:
         return out
 
     __call__ = forward
+
+
+class LatBandNet:
+    """One rank's share of a latitude-band sharded FourierNeuralOperatorNet[_Filmed]
+    forward (sfnonet.py:406-860): the multi-GPU form of configs 3 / 5 (one 6 h step
+    of ONE field spread over the ranks).  The encoder and decoder are pointwise, so
+    each rank runs them on its own rows (pos_embed sliced to them); the 12 blocks are
+    LatBandBlocks whose band partitions chain (block 0 takes rows of the full grid
+    and returns rows of the (h, w) Gauss grid, the last block maps back).  ``rows``
+    are this rank's rows of the full grid (``take`` / ``LatBandBlock.assemble``
+    conventions); ``forward(x_local, sst, scale)`` returns its rows of the output."""
+
+    def __init__(self, net, rank: int, world: int, device=None, comm=None):
+        self.net = net
+        self.rank, self.world = rank, world
+        self.comm = comm
+        self.shards = [LatBandBlock(blk, rank, world, device=device) for blk in net.blocks]
+        for a, b in zip(self.shards, self.shards[1:]):
+            assert a.rows_out == b.rows, "block band partitions do not chain"
+        self.rows = self.shards[0].rows
+        self.rows_out = self.shards[-1].rows_out
+        self.nlat_out = self.shards[-1].nlat_out
+        self._pos = None
+
+    def take(self, x):
+        return self.shards[0].take(x)
+
+    def _pos_local(self, device):
+        pe = self.net.pos_embed
+        key = (pe.data_ptr(), pe._version, str(device))
+        if self._pos is None or self._pos[0] != key:
+            idx = torch.tensor(self.rows, dtype=torch.long, device=pe.device)
+            self._pos = (key, pe.detach().index_select(2, idx).to(device).contiguous())
+        return self._pos[1]
+
+    def stages(self, x, sst=None, scale=1.0):
+        """Generator over the whole network's exchanges (see LatBandBlock.stages);
+        returns this rank's output rows."""
+        net = self.net
+        filmed = getattr(net, "_filmed", None)
+        gamma = beta = None
+        if filmed is not None:
+            film_mod = net.film_gen(sst) if net.film_gen is not None else sst
+            gamma, beta = film_mod[:, 0], film_mod[:, 1]
+        residual = x
+        h = net.encoder.native_forward(x, addend=self._pos_local(x.device))
+        for i, s in enumerate(self.shards):
+            if filmed is not None and filmed(i):
+                k = i - (net.num_layers - net.film_layers)
+                h = yield from s.stages(h, gamma[:, k], beta[:, k], scale)
+            else:
+                h = yield from s.stages(h)
+        return net.decode(h, residual)
+
+    def forward(self, x, sst=None, scale=1.0, comm=None):
+        gen = self.stages(x, sst, scale)
+        comm = comm if comm is not None else self.comm
+        if self.world == 1 and comm is None:
+            return LocalGroup.run([gen])[0]
+        return _drive(gen, comm if comm is not None else TorchComm())
+
+    __call__ = forward

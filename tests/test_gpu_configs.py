@@ -199,3 +199,30 @@ def test_rollout_112_steps_matches_oracle(graph):
                 worst = max(worst, err)
                 assert err < 1e-4, (i, err)
     print(f"rollout {steps} steps (graph={graph}): worst relative max-abs {worst:.3e}")
+
+
+def test_config5_geometry_sharded_rollout_eight_ranks():
+    """Config 5's multi-GPU form at its real geometry: the 12-block filmed network
+    (721x1440 -> 120x240 -> 721x1440, C=256, 73 channels) latitude-band sharded over 8
+    lock-step virtual ranks (LatBandNet), stepped autoregressively 3 times, against
+    the unsharded network stepped the same way."""
+    from msfno_amd.sfno import FourierNeuralOperatorNet_Filmed, LatBandBlock, LatBandNet, LocalGroup
+    torch.manual_seed(31)
+    net = FourierNeuralOperatorNet_Filmed("cpu", None, film_layers=1, advanced_logging=False,
+                                          model_depth=None, img_size=(721, 1440), in_chans=73,
+                                          out_chans=73, embed_dim_sfno=256, num_layers=12,
+                                          filter_type="non-linear", spectral_layers=3).eval().to(DEV)
+    g = torch.Generator().manual_seed(32)
+    x = torch.randn(1, 73, 721, 1440, generator=g).to(DEV)
+    film = torch.stack((0.1 * torch.randn(1, 1, 256, generator=g),
+                        0.1 * torch.randn(1, 1, 256, generator=g)), dim=1).to(DEV)
+    shards = [LatBandNet(net, r, 8) for r in range(8)]
+    with torch.no_grad():
+        want = x
+        parts = [s.take(x) for s in shards]
+        for _ in range(3):
+            want = net(want, film, 1.0)
+            parts = LocalGroup.run([s.stages(p, film, 1.0) for s, p in zip(shards, parts)])
+        got = LatBandBlock.assemble([s.shards[-1] for s in shards], parts)
+    err = (got - want).abs().max().item()
+    assert err < 1e-4 * max(1.0, want.abs().max().item()), err

@@ -72,3 +72,40 @@ def test_native_mlp_concat_and_broadcast_addend():
         want = sfno_ref.mlp(xx, {f"fwd.{k}": v for k, v in m2.fwd.state_dict().items()}, "fwd.")
         got = m2.to(DEV)(xx.to(DEV)).cpu()
     assert (got - want).abs().max().item() < 1e-5 * max(1.0, want.abs().max().item())
+
+
+def _sharded_net(net, x, world, sst=None, scale=1.0):
+    from msfno_amd.sfno import LatBandBlock, LatBandNet, LocalGroup
+    shards = [LatBandNet(net, r, world) for r in range(world)]
+    gens = [s.stages(s.take(x), sst, scale) for s in shards]
+    outs = LocalGroup.run(gens)
+    return LatBandBlock.assemble([s.shards[-1] for s in shards], outs)
+
+
+@pytest.mark.parametrize("world", [2, 3, 4])
+@pytest.mark.parametrize("path", NET_FIXTURES, ids=lambda p: os.path.basename(p)[:-4])
+def test_latband_net_matches_reference_golden(path, world):
+    """The network forward latitude-band sharded over `world` lock-step virtual ranks
+    (LatBandNet: encoder / decoder on each rank's rows, every block a LatBandBlock, the
+    resampling blocks chaining the 33x64 and 8x16 band partitions) against the
+    reference network's output."""
+    meta, params, x, y, _ = load_net(path)
+    net = _build(meta, params)
+    with torch.no_grad():
+        got = _sharded_net(net, x.to(DEV), world).cpu()
+    assert (got - y).abs().max().item() < 1e-4 * max(1.0, y.abs().max().item())
+
+
+@pytest.mark.parametrize("path", NET_FIXTURES, ids=lambda p: os.path.basename(p)[:-4])
+def test_latband_filmed_net_matches_unsharded(path):
+    meta, params, x, y, _ = load_net(path)
+    net = _build(meta, params, filmed=True, film_layers=2)
+    g = torch.Generator().manual_seed(3)
+    B, C = x.shape[0], meta["C"]
+    film = torch.stack((0.1 * torch.randn(B, 2, C, generator=g),
+                        0.1 * torch.randn(B, 2, C, generator=g)), dim=1).to(DEV)
+    x = x.to(DEV)
+    with torch.no_grad():
+        want = net(x, film, 0.8)
+        got = _sharded_net(net, x, 3, film, 0.8)
+    assert (got - want).abs().max().item() < 2e-5 * max(1.0, want.abs().max().item())
