@@ -5,6 +5,8 @@
 //   * weight preparation (complex block expansion, norm/FiLM folding into fc1),
 //   * the linear filter's per-mode complex contraction (HBM weight stream),
 //   * S-layout conversions (reference dense (l,m) / torch.tril_indices order).
+#include <string>
+
 #include "bf16x3.h"
 #include "dma.h"
 #include "kernels.h"
@@ -204,11 +206,42 @@ __global__ __launch_bounds__(256) void transpose_fwd_sym_kernel(
   }
 }
 
+// tile shape (latitudes x m) of the symmetric transposes: MSFNO_TR_FWD / MSFNO_TR_INV =
+// "64x32" | "32x64" | "32x128" | "16x128" (A/B; defaults 64x32 forward, 16x128 inverse:
+// 0.257 vs 0.268 ms for 32x64 at 721x1440, C = 256; the 32x128 tiles (67 KB of LDS)
+// lose occupancy: 0.58 / 0.34 ms)
+static int tr_tile(const char* var, int dflt) {
+  const char* e = getenv(var);
+  if (!e) return dflt;
+  const std::string v(e);
+  return v == "64x32" ? 0 : v == "32x64" ? 1 : v == "32x128" ? 2 : v == "16x128" ? 3 : dflt;
+}
+
+template <int TKx, int TMx>
+static void fwd_sym_launch(const float2* Xn, float* Xt, int B, int C, const LatGeom& g, int mmax,
+                           const float* nscale, const float* nshift, const int* perm, int kpad,
+                           hipStream_t s) {
+  dim3 grid((unsigned)cdiv(std::max(g.Ke, kpad), TKx), (unsigned)cdiv(mmax, TMx),
+            (unsigned)(B * C));
+  hipLaunchKernelGGL((transpose_fwd_sym_kernel<TKx, TMx>), grid, dim3(256), 0, s, Xn, Xt, B, C,
+                     g, mmax, nscale, nshift, perm, kpad);
+}
+
+static void fwd_sym_dispatch(const float2* Xn, float* Xt, int B, int C, const LatGeom& g,
+                             int mmax, const float* nscale, const float* nshift, const int* perm,
+                             int kpad, hipStream_t s) {
+  static const int t = tr_tile("MSFNO_TR_FWD", 0);
+  switch (t) {
+    case 1: fwd_sym_launch<32, 64>(Xn, Xt, B, C, g, mmax, nscale, nshift, perm, kpad, s); break;
+    case 2: fwd_sym_launch<32, 128>(Xn, Xt, B, C, g, mmax, nscale, nshift, perm, kpad, s); break;
+    case 3: fwd_sym_launch<16, 128>(Xn, Xt, B, C, g, mmax, nscale, nshift, perm, kpad, s); break;
+    default: fwd_sym_launch<TK_FWD, TM_FWD>(Xn, Xt, B, C, g, mmax, nscale, nshift, perm, kpad, s);
+  }
+}
+
 int launch_transpose_fwd_sym(const float2* Xn, float* Xt, int B, int C, const LatGeom& g, int mmax,
                              const float* nscale, const float* nshift, hipStream_t s) {
-  dim3 grid((unsigned)cdiv(g.Ke, TK_FWD), (unsigned)cdiv(mmax, TM_FWD), (unsigned)(B * C));
-  hipLaunchKernelGGL((transpose_fwd_sym_kernel<TK_FWD, TM_FWD>), grid, dim3(256), 0, s, Xn, Xt, B,
-                     C, g, mmax, nscale, nshift, nullptr, 0);
+  fwd_sym_dispatch(Xn, Xt, B, C, g, mmax, nscale, nshift, nullptr, 0, s);
   return launch_check("transpose_fwd_sym");
 }
 
@@ -222,9 +255,7 @@ int launch_band_pack(const float2* Xn, float* send, int B, int C, const LatGeom&
   if (!g.sym)
     return launch_transpose_fwd(Xn, send, B, C, g.nlat, mmax, g.ldk, nscale, nshift, s, perm,
                                 2 * W);
-  dim3 grid((unsigned)cdiv(W, TK_FWD), (unsigned)cdiv(mmax, TM_FWD), (unsigned)(B * C));
-  hipLaunchKernelGGL((transpose_fwd_sym_kernel<TK_FWD, TM_FWD>), grid, dim3(256), 0, s, Xn, send,
-                     B, C, g, mmax, nscale, nshift, perm, W);
+  fwd_sym_dispatch(Xn, send, B, C, g, mmax, nscale, nshift, perm, W, s);
   return launch_check("band_pack");
 }
 
@@ -409,11 +440,28 @@ __global__ __launch_bounds__(256) void transpose_inv_sym_kernel(const float* __r
   }
 }
 
+template <int TKx, int TMx>
+static void inv_sym_launch(const float* Yt, float2* Yn, int B, int C, const LatGeom& g, int mmax,
+                           int mact, const int* perm, hipStream_t s) {
+  dim3 grid((unsigned)cdiv(g.Ke, TKx), (unsigned)cdiv(mmax, TMx), (unsigned)(B * C));
+  hipLaunchKernelGGL((transpose_inv_sym_kernel<TKx, TMx>), grid, dim3(256), 0, s, Yt, Yn, B, C,
+                     g, mmax, mact, perm);
+}
+
+static void inv_sym_dispatch(const float* Yt, float2* Yn, int B, int C, const LatGeom& g,
+                             int mmax, int mact, const int* perm, hipStream_t s) {
+  static const int t = tr_tile("MSFNO_TR_INV", 3);
+  switch (t) {
+    case 0: inv_sym_launch<64, 32>(Yt, Yn, B, C, g, mmax, mact, perm, s); break;
+    case 1: inv_sym_launch<TK_INV, TM_INV>(Yt, Yn, B, C, g, mmax, mact, perm, s); break;
+    case 2: inv_sym_launch<32, 128>(Yt, Yn, B, C, g, mmax, mact, perm, s); break;
+    default: inv_sym_launch<16, 128>(Yt, Yn, B, C, g, mmax, mact, perm, s);
+  }
+}
+
 int launch_transpose_inv_sym(const float* Yt, float2* Yn, int B, int C, const LatGeom& g, int mmax,
                              int mact, hipStream_t s) {
-  dim3 grid((unsigned)cdiv(g.Ke, TK_INV), (unsigned)cdiv(mmax, TM_INV), (unsigned)(B * C));
-  hipLaunchKernelGGL((transpose_inv_sym_kernel<TK_INV, TM_INV>), grid, dim3(256), 0, s, Yt, Yn, B,
-                     C, g, mmax, mact, nullptr);
+  inv_sym_dispatch(Yt, Yn, B, C, g, mmax, mact, nullptr, s);
   return launch_check("transpose_inv_sym");
 }
 
@@ -422,9 +470,7 @@ int launch_transpose_inv_sym(const float* Yt, float2* Yn, int B, int C, const La
 int launch_band_unpack(const float* recv, float2* Yn, int B, int C, const LatGeom& g, int mmax,
                        int mact, const int* perm, hipStream_t s) {
   if (!g.sym) return launch_transpose_inv(recv, Yn, B, C, g.nlat, mmax, mact, g.ldk, s, perm);
-  dim3 grid((unsigned)cdiv(g.Ke, TK_INV), (unsigned)cdiv(mmax, TM_INV), (unsigned)(B * C));
-  hipLaunchKernelGGL((transpose_inv_sym_kernel<TK_INV, TM_INV>), grid, dim3(256), 0, s, recv, Yn,
-                     B, C, g, mmax, mact, perm);
+  inv_sym_dispatch(recv, Yn, B, C, g, mmax, mact, perm, s);
   return launch_check("band_unpack");
 }
 
