@@ -206,6 +206,131 @@ __global__ __launch_bounds__(256) void transpose_fwd_sym_kernel(
   }
 }
 
+// Two-phase variants: ONE LDS tile, written twice (Xs then Xa forward, north then
+// south rows inverse) from values the threads hold in registers, so a 32 x 128 tile
+// fits in 33 KB: rows of 128 m (1 KB) on the spectrum side and whole 128-B lines of
+// 32 latitudes on the slab side (the one-phase 16 x 128 / 64 x 32 tiles fetch half
+// lines: PMC read bytes 2.0x / 1.5x the algorithmic ones)
+template <int TKx, int TMx>
+__global__ __launch_bounds__(256) void transpose_fwd_sym2_kernel(
+    const float2* __restrict__ Xn, float* __restrict__ Xt, int B, int C, LatGeom g, int mmax,
+    const float* __restrict__ nscale, const float* __restrict__ nshift,
+    const int* __restrict__ slab, int kpad) {
+  constexpr int PER = TKx * TMx / 256;
+  static_assert(PER * 256 == TKx * TMx, "tile");
+  __shared__ float2 tile[TMx][TKx + 1];
+  const int k0 = blockIdx.x * TKx, m0 = blockIdx.y * TMx;
+  const int bc = blockIdx.z;
+  const int b = bc / C, c = bc - b * C;
+  const float2* src = Xn + (int64_t)bc * g.nlat * mmax;
+  const float sc = nscale ? nscale[bc] : 1.f;
+  const float sh = nshift ? nshift[bc] * kTwoPi : 0.f;
+  float2 xs[PER], xa[PER];
+#pragma unroll
+  for (int q = 0; q < PER; ++q) {
+    const int i = threadIdx.x + 256 * q;
+    const int kk = i / TMx, mm = i - kk * TMx;
+    const int k = k0 + kk, m = m0 + mm;
+    float2 n = make_float2(0.f, 0.f), t = n;
+    if (k < g.Ke && m < mmax) {
+      n = src[(int64_t)k * mmax + m];
+      if (k < g.nh) t = src[(int64_t)(g.nlat - 1 - k) * mmax + m];
+    }
+    const bool pair = k < g.nh;
+    const float shm = (m == 0) ? sh : 0.f;
+    // affine per row, then fold: s(N + S) + 2t  /  s(N - S)
+    xs[q] = k >= g.Ke ? make_float2(0.f, 0.f)  // band pads
+            : pair ? make_float2(fmaf(sc, n.x + t.x, 2.f * shm), sc * (n.y + t.y))
+                   : make_float2(fmaf(sc, n.x, shm), sc * n.y);
+    xa[q] = pair ? make_float2(sc * (n.x - t.x), sc * (n.y - t.y)) : make_float2(0.f, 0.f);
+  }
+  const int64_t R = 2LL * B * C;
+  const int64_t rre = (int64_t)(b * 2 + 0) * C + c;
+  const int64_t rim = (int64_t)(b * 2 + 1) * C + c;
+  const int kend = max(g.Ke, kpad);
+#pragma unroll
+  for (int ph = 0; ph < 2; ++ph) {
+    if (ph) __syncthreads();
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+      const int i = threadIdx.x + 256 * q;
+      const int kk = i / TMx, mm = i - kk * TMx;
+      tile[mm][kk] = ph ? xa[q] : xs[q];
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < TKx * TMx; i += 256) {
+      const int mm = i / TKx, kk = i - mm * TKx;
+      const int k = k0 + kk, m = m0 + mm;
+      if (k >= kend || m >= mmax) continue;
+      const int sl = slab ? slab[m] : m;
+      if (sl < 0) continue;
+      // real values for k < Ke (Xs) / k < nh (Xa); zeros on the pads up to kpad
+      if (k >= (ph ? (kpad > 0 ? kend : g.nh) : kend)) continue;
+      const float2 v = tile[mm][kk];
+      float* dst = Xt + (int64_t)sl * R * g.ldk + (ph ? g.ldke : 0) + k;
+      dst[rre * g.ldk] = v.x;
+      dst[rim * g.ldk] = v.y;
+    }
+  }
+}
+
+template <int TKx, int TMx>
+__global__ __launch_bounds__(256) void transpose_inv_sym2_kernel(const float* __restrict__ Yt,
+                                                                 float2* __restrict__ Yn, int B,
+                                                                 int C, LatGeom g, int mmax,
+                                                                 int mact,
+                                                                 const int* __restrict__ slab) {
+  constexpr int PER = TKx * TMx / 256;
+  static_assert(PER * 256 == TKx * TMx, "tile");
+  __shared__ float2 tile[TMx][TKx + 1];
+  const int k0 = blockIdx.x * TKx, m0 = blockIdx.y * TMx;
+  const int bc = blockIdx.z;
+  const int b = bc / C, c = bc - b * C;
+  const int64_t R = 2LL * B * C;
+  const int64_t rre = (int64_t)(b * 2 + 0) * C + c;
+  const int64_t rim = (int64_t)(b * 2 + 1) * C + c;
+  float2 yn[PER], ys[PER];
+#pragma unroll
+  for (int q = 0; q < PER; ++q) {
+    const int i = threadIdx.x + 256 * q;
+    const int mm = i / TKx, kk = i - mm * TKx;
+    const int k = k0 + kk, m = m0 + mm;
+    float2 n = make_float2(0.f, 0.f), t = n;
+    const int sl = (m < mact) ? (slab ? slab[m] : m) : -1;
+    if (k < g.Ke && sl >= 0) {
+      const float* srcp = Yt + (int64_t)sl * R * g.ldk;
+      const float2 e = make_float2(srcp[rre * g.ldk + k], srcp[rim * g.ldk + k]);
+      if (k < g.nh) {
+        const float2 o = make_float2(srcp[rre * g.ldk + g.ldke + k], srcp[rim * g.ldk + g.ldke + k]);
+        n = make_float2(e.x + o.x, e.y + o.y);
+        t = make_float2(e.x - o.x, e.y - o.y);
+      } else {
+        n = e;
+      }
+    }
+    yn[q] = n;
+    ys[q] = t;
+  }
+  float2* dst = Yn + (int64_t)bc * g.nlat * mmax;
+#pragma unroll
+  for (int ph = 0; ph < 2; ++ph) {
+    if (ph) __syncthreads();
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+      const int i = threadIdx.x + 256 * q;
+      const int mm = i / TKx, kk = i - mm * TKx;
+      tile[mm][kk] = ph ? ys[q] : yn[q];
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < TKx * TMx; i += 256) {
+      const int kk = i / TMx, mm = i - kk * TMx;
+      const int k = k0 + kk, m = m0 + mm;
+      if (m >= mmax || k >= (ph ? g.nh : g.Ke)) continue;
+      dst[(int64_t)(ph ? g.nlat - 1 - k : k) * mmax + m] = tile[mm][kk];
+    }
+  }
+}
+
 // tile shape (latitudes x m) of the symmetric transposes: MSFNO_TR_FWD / MSFNO_TR_INV =
 // "64x32" | "32x64" | "32x128" | "16x128" (A/B; defaults 64x32 forward, 16x128 inverse:
 // 0.257 vs 0.268 ms for 32x64 at 721x1440, C = 256; the 32x128 tiles (67 KB of LDS)
@@ -214,7 +339,8 @@ static int tr_tile(const char* var, int dflt) {
   const char* e = getenv(var);
   if (!e) return dflt;
   const std::string v(e);
-  return v == "64x32" ? 0 : v == "32x64" ? 1 : v == "32x128" ? 2 : v == "16x128" ? 3 : dflt;
+  return v == "64x32" ? 0 : v == "32x64" ? 1 : v == "32x128" ? 2 : v == "16x128" ? 3
+         : v == "2p" ? 4 : dflt;
 }
 
 template <int TKx, int TMx>
@@ -235,6 +361,13 @@ static void fwd_sym_dispatch(const float2* Xn, float* Xt, int B, int C, const La
     case 1: fwd_sym_launch<32, 64>(Xn, Xt, B, C, g, mmax, nscale, nshift, perm, kpad, s); break;
     case 2: fwd_sym_launch<32, 128>(Xn, Xt, B, C, g, mmax, nscale, nshift, perm, kpad, s); break;
     case 3: fwd_sym_launch<16, 128>(Xn, Xt, B, C, g, mmax, nscale, nshift, perm, kpad, s); break;
+    case 4: {
+      dim3 grid((unsigned)cdiv(std::max(g.Ke, kpad), 32), (unsigned)cdiv(mmax, 128),
+                (unsigned)(B * C));
+      hipLaunchKernelGGL((transpose_fwd_sym2_kernel<32, 128>), grid, dim3(256), 0, s, Xn, Xt, B,
+                         C, g, mmax, nscale, nshift, perm, kpad);
+      break;
+    }
     default: fwd_sym_launch<TK_FWD, TM_FWD>(Xn, Xt, B, C, g, mmax, nscale, nshift, perm, kpad, s);
   }
 }
@@ -455,6 +588,12 @@ static void inv_sym_dispatch(const float* Yt, float2* Yn, int B, int C, const La
     case 0: inv_sym_launch<64, 32>(Yt, Yn, B, C, g, mmax, mact, perm, s); break;
     case 1: inv_sym_launch<TK_INV, TM_INV>(Yt, Yn, B, C, g, mmax, mact, perm, s); break;
     case 2: inv_sym_launch<32, 128>(Yt, Yn, B, C, g, mmax, mact, perm, s); break;
+    case 4: {
+      dim3 grid((unsigned)cdiv(g.Ke, 32), (unsigned)cdiv(mmax, 128), (unsigned)(B * C));
+      hipLaunchKernelGGL((transpose_inv_sym2_kernel<32, 128>), grid, dim3(256), 0, s, Yt, Yn, B,
+                         C, g, mmax, mact, perm);
+      break;
+    }
     default: inv_sym_launch<16, 128>(Yt, Yn, B, C, g, mmax, mact, perm, s);
   }
 }
