@@ -27,11 +27,14 @@ def main(d, sub=""):
     if durs:
         print(f"{'duration_ms (profiled)':28s} {sum(durs) / len(durs):16.4g}  (n={len(durs)})")
     g = out.get("GRBM_GUI_ACTIVE")
+    # MI355X: GRBM_GUI_ACTIVE is counted once per XCD (8), the SQ MFMA-busy cycles per
+    # SIMD over 256 CUs x 4 SIMDs; the sums above run over those instances
     if g and durs:
-        print(f"{'clock_GHz':28s} {g / (sum(durs) / len(durs) * 1e6):16.4g}")
-    if "SQ_VALU_MFMA_BUSY_CYCLES" in out and "SQ_BUSY_CYCLES" in out:
-        print(f"{'mfma_busy_frac':28s} {out['SQ_VALU_MFMA_BUSY_CYCLES'] / out['SQ_BUSY_CYCLES'] / 4:16.4g}"
-              "  (MFMA busy cycles / (busy cycles x 4 SIMDs))")
+        cyc = g / 8
+        print(f"{'clock_GHz':28s} {cyc / (sum(durs) / len(durs) * 1e6):16.4g}  (GRBM_GUI_ACTIVE / 8 XCDs / duration)")
+        if "SQ_VALU_MFMA_BUSY_CYCLES" in out:
+            print(f"{'mfma_busy_frac':28s} {out['SQ_VALU_MFMA_BUSY_CYCLES'] / (256 * 4 * cyc):16.4g}"
+                  "  (MFMA busy cycles / (256 CUs x 4 SIMDs x GPU cycles))")
     return out
 
 
