@@ -235,7 +235,9 @@ class LocalGroup:
                     for p in range(W):
                         n = rc[p]
                         assert reqs[p][2][q] == n, "send/recv counts disagree"
-                        recv[acc:acc + n].copy_(reqs[p][1][offs[p][q]:offs[p][q] + n])
+                        src = reqs[p][1][offs[p][q]:offs[p][q] + n]
+                        if src.data_ptr() != recv[acc:acc + n].data_ptr():
+                            recv[acc:acc + n].copy_(src)
                         acc += n
             nxt = []
             for i in live:
@@ -399,10 +401,13 @@ class LatBandBlock:
                 cnt.append((list(sc)[:self.world], list(rc)[:self.world]))
             n = max(max(sum(s), sum(r)) for s, r in cnt)
             dev = self.device
+            send = torch.empty(max(n, 1), dtype=torch.float32, device=dev)
+            # one rank: the exchange is the identity, so the receive buffer IS the send
+            # buffer (stage 2's inverse GEMM overwrites the forward GEMM's input only
+            # after that GEMM has run: stream order)
+            recv = send if self.world == 1 else torch.empty_like(send)
             self._bufs[key] = dict(
-                counts=cnt,
-                send=torch.empty(max(n, 1), dtype=torch.float32, device=dev),
-                recv=torch.empty(max(n, 1), dtype=torch.float32, device=dev),
+                counts=cnt, send=send, recv=recv,
                 stats=torch.empty(B * C, 3, dtype=torch.float64, device=dev))
         return self._bufs[key]
 
