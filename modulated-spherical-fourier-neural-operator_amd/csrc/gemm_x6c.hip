@@ -48,6 +48,11 @@ struct X6CParams {
   int co, ci, N;
   int tiles_m, tiles_n;
   int relu;
+  // BF32 (layer 0): X given as fp32 rows instead of 3M planes: Re rows at
+  // Xf + b*xf_b, Im rows at + xf_im, ld ldxf; split (and Re + Im formed) while staged
+  const float* Xf;
+  int64_t xf_b, xf_im;
+  int ldxf;
 };
 
 // A image of one layer: Wr, Wi, Ws = Wr + Wi (co x ci each) from the reference
@@ -172,11 +177,15 @@ __global__ void split3m_kernel(const float* __restrict__ S, unsigned short* __re
 
 // WGM x WGN waves: 4 x 2 (32 x 64 per wave, two waves per SIMD) or 2 x 2 (64 x 64
 // per wave, one wave per SIMD: a third fewer LDS fragment reads per MFMA)
-template <bool PLANES_OUT, int WGM = 4, int WGN = 2>
+// BF32: the B operand arrives as fp32 Re / Im rows (layer 0, straight from the
+// forward Legendre GEMM): each thread loads a float4 of Re and of Im for the next
+// k-tile before the current one's MFMAs, and after them forms Re + Im, splits the
+// three into bf16x3 and writes the nine B planes into the LDS stage; only A is DMA'd
+template <bool PLANES_OUT, int WGM = 4, int WGN = 2, bool BF32 = false>
 __global__ __launch_bounds__(64 * WGM * WGN) void gemm_x6c_kernel(X6CParams p) {
   constexpr int BM = X6C_BM, BN = X6C_BN, BK = X6C_BK;
   constexpr int NW = WGM * WGN;
-  constexpr int NPC = 72 / NW;  // 1-KB DMA pieces per wave and k-tile
+  constexpr int NPC = BF32 ? (36 + NW - 1) / NW : 72 / NW;  // 1-KB DMA pieces per wave and k-tile
   constexpr int WM = BM / WGM, WN = BN / WGN;
   constexpr int MT = WM / 32, NT = WN / 32;
   constexpr int A_PLANE = BM * BK, B_PLANE = BK * BN;  // bf16 elements per matrix plane
@@ -212,7 +221,11 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_x6c_kernel(X6CParams p) {
 #pragma unroll
   for (int q = 0; q < NPC; ++q) {
     const int c = wave + NW * q;
-    if (c < 36) {
+    if (BF32 && c >= 36) {  // no B pieces; this slot idles
+      src[q] = nullptr;
+      dst[q] = 0;
+      brow[q] = -2;
+    } else if (c < 36) {
       const int mp = c >> 2, mb = c & 3;
       const int mat = mp / 3, pl = mp - 3 * mat;
       const int m = 32 * mb + (lane >> 1);
@@ -237,10 +250,48 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_x6c_kernel(X6CParams p) {
     const uint32_t base = ring_lds + (uint32_t)(st * STAGE * 2);
 #pragma unroll
     for (int q = 0; q < NPC; ++q) {
+      if (BF32 && brow[q] == -2) continue;
       const unsigned short* g = brow[q] < 0
                                     ? src[q] + kt * a_kstride
                                     : src[q] + (int64_t)min(kt * BK + brow[q], K - 1) * ldx;
       glds16(g, base + (uint32_t)(dst[q] * 2));
+    }
+  };
+  // BF32 B staging: thread -> (k row, 4 columns); NW * 64 threads cover 16 x 128
+  static_assert(!BF32 || NW * 64 * 4 == BK * BN, "BF32 staging: one float4 per thread");
+  const int brow_f = tid / (BN / 4), bcol_f = 4 * (tid % (BN / 4));
+  const float* Xf = BF32 ? p.Xf + z * p.xf_b : nullptr;
+  float4 fre = make_float4(0.f, 0.f, 0.f, 0.f), fim = fre;
+  auto load_bf = [&](int kt) {
+    const int k = kt * BK + brow_f;
+    const int kc = min(k, K - 1);
+    const int col = min(n0 + bcol_f, (N - 1) & ~3);
+    const float* r = Xf + (int64_t)kc * p.ldxf + col;
+    fre = *reinterpret_cast<const float4*>(r);
+    fim = *reinterpret_cast<const float4*>(r + p.xf_im);
+  };
+  auto store_bf = [&](int kt, int st) {
+    const int k = kt * BK + brow_f;
+    float re[4] = {fre.x, fre.y, fre.z, fre.w}, im[4] = {fim.x, fim.y, fim.z, fim.w};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {  // zero what is out of range (K tail, ragged N)
+      const bool ok = k < K && n0 + bcol_f + e < N;
+      re[e] = ok ? re[e] : 0.f;
+      im[e] = ok ? im[e] : 0.f;
+    }
+    const float sm[4] = {re[0] + im[0], re[1] + im[1], re[2] + im[2], re[3] + im[3]};
+    const float* v[3] = {re, im, sm};
+    unsigned short* base = ring + st * STAGE + A_ALL;
+    const int u = bcol_f >> 3, h = (bcol_f >> 2) & 1;
+    const int off = brow_f * BN + ((u ^ (4 * (brow_f & 3))) << 3) + 4 * h;
+#pragma unroll
+    for (int mat = 0; mat < 3; ++mat) {
+      uint32_t a0, a1, a2, b0, b1, b2;
+      split2(v[mat][0], v[mat][1], a0, a1, a2);
+      split2(v[mat][2], v[mat][3], b0, b1, b2);
+      *reinterpret_cast<uint2*>(base + (mat * 3 + 0) * B_PLANE + off) = make_uint2(a0, b0);
+      *reinterpret_cast<uint2*>(base + (mat * 3 + 1) * B_PLANE + off) = make_uint2(a1, b1);
+      *reinterpret_cast<uint2*>(base + (mat * 3 + 2) * B_PLANE + off) = make_uint2(a2, b2);
     }
   };
 
@@ -307,14 +358,24 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_x6c_kernel(X6CParams p) {
   };
 
   issue(0, 0);
+  if constexpr (BF32) {
+    load_bf(0);
+    store_bf(0, 0);
+  }
   for (int kt = 0; kt < nk; ++kt) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // my DMA of k-tile kt landed
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();  // everyone's landed; stage (kt + 1) & 1 is free
-    if (kt + 1 < nk) issue(kt + 1, (kt + 1) & 1);
+    if (kt + 1 < nk) {
+      issue(kt + 1, (kt + 1) & 1);
+      if constexpr (BF32) load_bf(kt + 1);  // after the DMA: in-order vmcnt
+    }
     __builtin_amdgcn_s_setprio(1);
     mfma_tile(kt & 1);
     __builtin_amdgcn_s_setprio(0);
+    if constexpr (BF32) {
+      if (kt + 1 < nk) store_bf(kt + 1, (kt + 1) & 1);
+    }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
@@ -399,6 +460,38 @@ int launch_split3m(const float* S, unsigned short* X, int B, int C, int N, int l
   hipLaunchKernelGGL(split3m_kernel, dim3(blocks, B), dim3(256), 0, s, S, X, C, N, ldS, ldx,
                      9 * x_plane, 3 * x_plane, x_plane);
   return launch_check("split3m");
+}
+
+// layer 0 on fp32 input rows (Re at Sin + b*2*ci*ldSin, Im ci rows later): the
+// split3m pass folded into the GEMM's B staging; output 3M planes (ld ldy)
+int gemm_x6c_f32b(const unsigned short* Aw, int co, int ci, const float* Sin, int ldSin, int N,
+                  unsigned short* Y, int ldy, bool relu, int B, hipStream_t s) {
+  if (co <= 0 || N <= 0 || B <= 0) return MSFNO_OK;
+  MSFNO_REQUIRE(ldSin % 4 == 0 && (reinterpret_cast<uintptr_t>(Sin) & 15) == 0 && ldy % 8 == 0,
+                MSFNO_EINVAL, "gemm_x6c_f32b: fp32 rows need ld % 4 == 0 and 16-B alignment");
+  X6CParams p{};
+  p.Mp = (int)round_up(co, X6C_BM);
+  const int KT = (int)cdiv(ci, X6C_BK);
+  p.Aw = Aw;
+  p.a_plane = (int64_t)p.Mp * KT * 16;
+  p.a_mat = 3 * p.a_plane;
+  p.Xf = Sin;
+  p.xf_b = 2LL * ci * ldSin;
+  p.xf_im = (int64_t)ci * ldSin;
+  p.ldxf = ldSin;
+  p.ldx = 8;  // unused (no B planes)
+  p.Y = Y;
+  p.y_plane = (int64_t)co * ldy;
+  p.y_mat = 3 * p.y_plane;
+  p.y_b = 3 * p.y_mat;
+  p.ldy = ldy;
+  p.co = co; p.ci = ci; p.N = N;
+  p.tiles_m = p.Mp / X6C_BM;
+  p.tiles_n = (int)cdiv(N, X6C_BN);
+  p.relu = relu ? 1 : 0;
+  const dim3 grid(p.tiles_m * p.tiles_n, 1, B);
+  hipLaunchKernelGGL((gemm_x6c_kernel<true, 4, 2, true>), grid, dim3(512), 0, s, p);
+  return launch_check("gemm_x6c_f32b");
 }
 
 // one spectral-MLP layer: X (3M planes, ci rows, ld ldx) -> Y (3M planes, co rows,

@@ -35,6 +35,11 @@ VARIANTS = [
     {"MSFNO_CONTRACT_DMA": "0"},
     {"MSFNO_CONTRACT_NS": "3"},
     {"MSFNO_CX16": "0"},
+    {"MSFNO_SPEC_L0F32": "0"},
+    {"MSFNO_MF_XS": "1"},
+    {"MSFNO_X6C_WAVES": "24"},
+    {"MSFNO_X6C_WAVES": "4"},
+    {"MSFNO_TR_FWD": "2p", "MSFNO_TR_INV": "2p"},
 ]
 
 
