@@ -767,6 +767,23 @@ int run_filter(const msfno_block_desc* d, msfno_sht_plan_s* f, msfno_sht_plan_s*
         return !(e && e[0] == '0');
       }();
       const bool f32b = l0f32 && nl >= 1 && L.ldT % 4 == 0;
+      // MSFNO_SPEC_HF32=1: the hidden activations stay fp32 rows (8 B per complex value
+      // instead of 18 B of 3M planes); every layer splits its input while staging
+      static const bool hf32 = [] {
+        const char* e = getenv("MSFNO_SPEC_HF32");
+        return e && e[0] == '1';
+      }();
+      if (f32b && hf32) {
+        const float* in = b.Sa;
+        for (int l = 0; l <= nl; ++l) {
+          prof(l == nl ? ST_SPEC_OUT : ST_SPEC_L0 + std::min(l, 3), s);
+          float* out = l == nl ? b.Sa : ((l & 1) ? b.Sc : b.Sb);
+          MSFNO_TRY(gemm_x6c_f32b(sw.out[l], sw.co[l], sw.ci[l], in, (int)L.ldT, (int)L.Tp,
+                                  nullptr, 0, out, (int)L.ldT, l < nl, B, s));
+          in = out;
+        }
+        return MSFNO_OK;
+      }
       if (!f32b) MSFNO_TRY(launch_split3m(b.Sa, cur, B, (int)C, (int)L.Tp, (int)L.ldT, ldTx, s));
       for (int l = 0; l <= nl; ++l) {
         prof(l == nl ? ST_SPEC_OUT : ST_SPEC_L0 + std::min(l, 3), s);
@@ -774,7 +791,7 @@ int run_filter(const msfno_block_desc* d, msfno_sht_plan_s* f, msfno_sht_plan_s*
                                       : reinterpret_cast<unsigned short*>((l & 1) ? b.Sc : b.Sb);
         if (l == 0 && f32b)
           MSFNO_TRY(gemm_x6c_f32b(sw.out[0], sw.co[0], sw.ci[0], b.Sa, (int)L.ldT, (int)L.Tp, out,
-                                  ldTx, true, B, s));
+                                  ldTx, nullptr, 0, true, B, s));
         else
           MSFNO_TRY(gemm_x6c(sw.out[l], sw.co[l], sw.ci[l], cur, (int)L.Tp, ldTx, out,
                              l == nl ? b.Sa : nullptr, (int)L.ldT, l < nl, B, s));

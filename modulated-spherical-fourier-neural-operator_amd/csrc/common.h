@@ -216,7 +216,8 @@ int launch_spec_weights_3m(const SpecWeightsX6p& a, hipStream_t s);
 int launch_split3m(const float* S, unsigned short* X, int B, int C, int N, int ldS, int ldx,
                    hipStream_t s);
 int gemm_x6c_f32b(const unsigned short* Aw, int co, int ci, const float* Sin, int ldSin, int N,
-                  unsigned short* Y, int ldy, bool relu, int B, hipStream_t s);
+                  unsigned short* Y, int ldy, float* Sout, int ldSout, bool relu, int B,
+                  hipStream_t s);
 int gemm_x6c(const unsigned short* Aw, int co, int ci, const unsigned short* X, int N, int ldx,
              unsigned short* Y, float* S, int ldS, bool relu, int B, hipStream_t s);
 // fp32 x[z][r][c] (ld ldx, batch stride sx) -> bf16x3 planes xp[z][plane][r][c]

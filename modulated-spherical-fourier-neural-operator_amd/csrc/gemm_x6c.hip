@@ -462,13 +462,16 @@ int launch_split3m(const float* S, unsigned short* X, int B, int C, int N, int l
   return launch_check("split3m");
 }
 
-// layer 0 on fp32 input rows (Re at Sin + b*2*ci*ldSin, Im ci rows later): the
-// split3m pass folded into the GEMM's B staging; output 3M planes (ld ldy)
+// a layer on fp32 input rows (Re at Sin + b*2*ci*ldSin, Im ci rows later), split
+// while staged: out 3M planes Y (ld ldy) or fp32 rows [b][re/im][co] of Sout (ld ldSout)
 int gemm_x6c_f32b(const unsigned short* Aw, int co, int ci, const float* Sin, int ldSin, int N,
-                  unsigned short* Y, int ldy, bool relu, int B, hipStream_t s) {
+                  unsigned short* Y, int ldy, float* Sout, int ldSout, bool relu, int B,
+                  hipStream_t s) {
   if (co <= 0 || N <= 0 || B <= 0) return MSFNO_OK;
-  MSFNO_REQUIRE(ldSin % 4 == 0 && (reinterpret_cast<uintptr_t>(Sin) & 15) == 0 && ldy % 8 == 0,
+  MSFNO_REQUIRE(ldSin % 4 == 0 && (reinterpret_cast<uintptr_t>(Sin) & 15) == 0 && ldSin >= N,
                 MSFNO_EINVAL, "gemm_x6c_f32b: fp32 rows need ld % 4 == 0 and 16-B alignment");
+  MSFNO_REQUIRE((Y != nullptr) != (Sout != nullptr), MSFNO_EINVAL, "gemm_x6c_f32b: one output");
+  MSFNO_REQUIRE(!Y || ldy % 8 == 0, MSFNO_EINVAL, "gemm_x6c_f32b: plane ld % 8 != 0");
   X6CParams p{};
   p.Mp = (int)round_up(co, X6C_BM);
   const int KT = (int)cdiv(ci, X6C_BK);
@@ -485,12 +488,19 @@ int gemm_x6c_f32b(const unsigned short* Aw, int co, int ci, const float* Sin, in
   p.y_mat = 3 * p.y_plane;
   p.y_b = 3 * p.y_mat;
   p.ldy = ldy;
+  p.S = Sout;
+  p.s_b = 2LL * co * ldSout;
+  p.s_im = (int64_t)co * ldSout;
+  p.ldS = ldSout;
   p.co = co; p.ci = ci; p.N = N;
   p.tiles_m = p.Mp / X6C_BM;
   p.tiles_n = (int)cdiv(N, X6C_BN);
   p.relu = relu ? 1 : 0;
   const dim3 grid(p.tiles_m * p.tiles_n, 1, B);
-  hipLaunchKernelGGL((gemm_x6c_kernel<true, 4, 2, true>), grid, dim3(512), 0, s, p);
+  if (Y)
+    hipLaunchKernelGGL((gemm_x6c_kernel<true, 4, 2, true>), grid, dim3(512), 0, s, p);
+  else
+    hipLaunchKernelGGL((gemm_x6c_kernel<false, 4, 2, true>), grid, dim3(512), 0, s, p);
   return launch_check("gemm_x6c_f32b");
 }
 

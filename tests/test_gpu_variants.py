@@ -36,6 +36,7 @@ VARIANTS = [
     {"MSFNO_CONTRACT_NS": "3"},
     {"MSFNO_CX16": "0"},
     {"MSFNO_SPEC_L0F32": "0"},
+    {"MSFNO_SPEC_HF32": "1"},
     {"MSFNO_MF_XS": "1"},
     {"MSFNO_X6C_WAVES": "24"},
     {"MSFNO_X6C_WAVES": "4"},
