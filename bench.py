@@ -638,7 +638,6 @@ def main():
 
     with torch.no_grad():
         y, elapsed, stages = timed(step, args, dist, dev, backend)
-    assert torch.isfinite(y).all()
     fields = (B if band else world * B) * args.steps
     value = fields / elapsed
     ms_per_step = 1000.0 * elapsed / args.steps
@@ -647,6 +646,7 @@ def main():
     roof = roofline(stages, args, B_launch, C, rows, mset)
     if args.stages:
         print_stages(stages, args, B_launch, C, rows, mset, tag=f"rank{rank} ")
+    assert torch.isfinite(y).all()
 
     replicas = None
     if band and dist and args.replicas_check:

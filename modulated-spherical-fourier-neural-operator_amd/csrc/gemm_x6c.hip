@@ -181,7 +181,9 @@ __global__ void split3m_kernel(const float* __restrict__ S, unsigned short* __re
 // forward Legendre GEMM): each thread loads a float4 of Re and of Im for the next
 // k-tile before the current one's MFMAs, and after them forms Re + Im, splits the
 // three into bf16x3 and writes the nine B planes into the LDS stage; only A is DMA'd
-template <bool PLANES_OUT, int WGM = 4, int WGN = 2, bool BF32 = false>
+// DBG (diagnostic timing builds only, wrong results; MSFNO_X6C_DBG): 1 no vmcnt wait
+// for the k-tile DMA, 2 no DMA in the loop at all (stale stages), 4 no MFMAs
+template <bool PLANES_OUT, int WGM = 4, int WGN = 2, bool BF32 = false, int DBG = 0>
 __global__ __launch_bounds__(64 * WGM * WGN) void gemm_x6c_kernel(X6CParams p) {
   constexpr int BM = X6C_BM, BN = X6C_BN, BK = X6C_BK;
   constexpr int NW = WGM * WGN;
@@ -363,15 +365,16 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_x6c_kernel(X6CParams p) {
     store_bf(0, 0);
   }
   for (int kt = 0; kt < nk; ++kt) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // my DMA of k-tile kt landed
+    if constexpr ((DBG & 1) == 0)
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // my DMA of k-tile kt landed
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();  // everyone's landed; stage (kt + 1) & 1 is free
     if (kt + 1 < nk) {
-      issue(kt + 1, (kt + 1) & 1);
+      if constexpr ((DBG & 2) == 0) issue(kt + 1, (kt + 1) & 1);
       if constexpr (BF32) load_bf(kt + 1);  // after the DMA: in-order vmcnt
     }
     __builtin_amdgcn_s_setprio(1);
-    mfma_tile(kt & 1);
+    if constexpr ((DBG & 4) == 0) mfma_tile(kt & 1);
     __builtin_amdgcn_s_setprio(0);
     if constexpr (BF32) {
       if (kt + 1 < nk) store_bf(kt + 1, (kt + 1) & 1);
@@ -555,10 +558,24 @@ int gemm_x6c(const unsigned short* Aw, int co, int ci, const unsigned short* X, 
     else
       hipLaunchKernelGGL((gemm_x6c_kernel<false, 2, 2>), grid, dim3(256), 0, s, p);
   } else {
-    if (Y)
+    static const int dbg = [] {
+      const char* e = getenv("MSFNO_X6C_DBG");
+      return e ? atoi(e) : 0;
+    }();
+    if (dbg == 1) {
+      if (Y) hipLaunchKernelGGL((gemm_x6c_kernel<true, 4, 2, false, 1>), grid, dim3(512), 0, s, p);
+      else hipLaunchKernelGGL((gemm_x6c_kernel<false, 4, 2, false, 1>), grid, dim3(512), 0, s, p);
+    } else if (dbg == 2) {
+      if (Y) hipLaunchKernelGGL((gemm_x6c_kernel<true, 4, 2, false, 2>), grid, dim3(512), 0, s, p);
+      else hipLaunchKernelGGL((gemm_x6c_kernel<false, 4, 2, false, 2>), grid, dim3(512), 0, s, p);
+    } else if (dbg == 4) {
+      if (Y) hipLaunchKernelGGL((gemm_x6c_kernel<true, 4, 2, false, 4>), grid, dim3(512), 0, s, p);
+      else hipLaunchKernelGGL((gemm_x6c_kernel<false, 4, 2, false, 4>), grid, dim3(512), 0, s, p);
+    } else if (Y) {
       hipLaunchKernelGGL((gemm_x6c_kernel<true, 4, 2>), grid, dim3(512), 0, s, p);
-    else
+    } else {
       hipLaunchKernelGGL((gemm_x6c_kernel<false, 4, 2>), grid, dim3(512), 0, s, p);
+    }
   }
   return launch_check("gemm_x6c");
 }
