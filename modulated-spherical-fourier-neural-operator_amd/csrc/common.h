@@ -217,9 +217,10 @@ int launch_split3m(const float* S, unsigned short* X, int B, int C, int N, int l
                    hipStream_t s);
 int gemm_x6c_f32b(const unsigned short* Aw, int co, int ci, const float* Sin, int ldSin, int N,
                   unsigned short* Y, int ldy, float* Sout, int ldSout, bool relu, int B,
-                  hipStream_t s);
+                  hipStream_t s, bool tiled_out = false);
+int64_t x6c_tiled_elems(int rows, int N);
 int gemm_x6c(const unsigned short* Aw, int co, int ci, const unsigned short* X, int N, int ldx,
-             unsigned short* Y, float* S, int ldS, bool relu, int B, hipStream_t s);
+             unsigned short* Y, float* S, int ldS, bool relu, int B, hipStream_t s, int lay = 0);
 // fp32 x[z][r][c] (ld ldx, batch stride sx) -> bf16x3 planes xp[z][plane][r][c]
 int launch_split_planes(const float* x, unsigned short* xp, int rows, int cols, int ldx,
                         int64_t sx, int ldp, int64_t pstride, int64_t sxp, int batch,

@@ -53,7 +53,20 @@ struct X6CParams {
   const float* Xf;
   int64_t xf_b, xf_im;
   int ldxf;
+  // LAY (tiled activations): k-tiles per column tile of the planes input / output
+  // (round_up(rows, 128) / 16 of the producing layer)
+  int kt_in, kt_out;
 };
+
+// Tiled 3M activations (LAY, MSFNO_X6C_TILED): the planes of a layer's activation
+// stored as the LDS image of the next layer's B stages, [b][tn][kt][mat*3+plane][16
+// rows][128 columns, 8-column chunks XOR-swizzled by 4 (row & 3)]: one k-tile stage of
+// one column tile is a contiguous 36 KB, so the B DMA reads whole 1-KB pieces and the
+// epilogue writes whole rows of 256 B (the row layout reads 4 rows of 256 B at a
+// 130-KB stride per piece).  Pad rows (>= co) and columns (>= N) hold 0.
+__device__ __forceinline__ int x6c_tile_swz(int r, int c) {
+  return ((((c >> 3) ^ (4 * (r & 3)))) << 3) + (c & 7);
+}
 
 // A image of one layer: Wr, Wi, Ws = Wr + Wi (co x ci each) from the reference
 // weight w (ci, co, 2), each split into [plane][kt][Mp][16]
@@ -183,7 +196,8 @@ __global__ void split3m_kernel(const float* __restrict__ S, unsigned short* __re
 // three into bf16x3 and writes the nine B planes into the LDS stage; only A is DMA'd
 // DBG (diagnostic timing builds only, wrong results; MSFNO_X6C_DBG): 1 no vmcnt wait
 // for the k-tile DMA, 2 no DMA in the loop at all (stale stages), 4 no MFMAs
-template <bool PLANES_OUT, int WGM = 4, int WGN = 2, bool BF32 = false, int DBG = 0>
+// LAY: bit 1 = B planes read in the tiled layout, bit 2 = planes written tiled
+template <bool PLANES_OUT, int WGM = 4, int WGN = 2, bool BF32 = false, int DBG = 0, int LAY = 0>
 __global__ __launch_bounds__(64 * WGM * WGN) void gemm_x6c_kernel(X6CParams p) {
   constexpr int BM = X6C_BM, BN = X6C_BN, BK = X6C_BK;
   constexpr int NW = WGM * WGN;
@@ -241,7 +255,11 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_x6c_kernel(X6CParams p) {
       const int mat = mp / 3, pl = mp - 3 * mat;
       const int row = 4 * rq + (lane >> 4);
       const int gu = (lane & 15) ^ (4 * (row & 3));
-      src[q] = X + mat * p.x_mat + pl * p.x_plane + min(n0 + 8 * gu, ldx - 8);
+      if constexpr ((LAY & 1) != 0)
+        src[q] = X + ((int64_t)tn * p.kt_in * 9 + mp) * B_PLANE + rq * 4 * BN + 8 * (lane & 15) +
+                 BN * (lane >> 4);
+      else
+        src[q] = X + mat * p.x_mat + pl * p.x_plane + min(n0 + 8 * gu, ldx - 8);
       dst[q] = A_ALL + mp * B_PLANE + rq * 4 * BN;
       brow[q] = row;
     }
@@ -255,7 +273,8 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_x6c_kernel(X6CParams p) {
       if (BF32 && brow[q] == -2) continue;
       const unsigned short* g = brow[q] < 0
                                     ? src[q] + kt * a_kstride
-                                    : src[q] + (int64_t)min(kt * BK + brow[q], K - 1) * ldx;
+                                    : ((LAY & 1) ? src[q] + (int64_t)kt * 9 * B_PLANE
+                                                 : src[q] + (int64_t)min(kt * BK + brow[q], K - 1) * ldx);
       glds16(g, base + (uint32_t)(dst[q] * 2));
     }
   };
@@ -401,7 +420,39 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_x6c_kernel(X6CParams p) {
   float* lds = reinterpret_cast<float*>(lds_raw);
   GemmParams q{};
   q.vecC = 1;
-  if constexpr (PLANES_OUT) {
+  if constexpr (PLANES_OUT && (LAY & 2) != 0) {
+    // tiled planes: every row and column of the tile (pad rows / columns are 0)
+    constexpr int CS_LD = BN + 8;
+    unsigned short* Yt = p.Y + z * p.y_b + (int64_t)tn * p.kt_out * 9 * B_PLANE;
+#pragma unroll
+    for (int mat = 0; mat < 3; ++mat) {
+#pragma unroll
+      for (int i = 0; i < MT; ++i)
+#pragma unroll
+        for (int j = 0; j < NT; ++j)
+#pragma unroll
+          for (int r = 0; r < 16; ++r)
+            lds[(wm * WM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * half) * CS_LD + wn * WN + j * 32 +
+                l32] = acc[mat][i][j][r];
+      __syncthreads();
+      constexpr int NQ = BM * BN / 4 / (64 * NW);
+#pragma unroll
+      for (int qq = 0; qq < NQ; ++qq) {
+        const int idx = tid + 64 * NW * qq;
+        const int lr = idx / (BN / 4), c = 4 * (idx % (BN / 4));
+        const float4 v = *reinterpret_cast<const float4*>(lds + lr * CS_LD + c);
+        uint32_t a0, a1, a2, b0, b1, b2;
+        split2(v.x, v.y, a0, a1, a2);
+        split2(v.z, v.w, b0, b1, b2);
+        const int m = m0 + lr, r = m & 15;
+        unsigned short* d = Yt + ((int64_t)(m >> 4) * 9 + mat * 3) * B_PLANE + r * BN + x6c_tile_swz(r, c);
+        *reinterpret_cast<uint2*>(d) = make_uint2(a0, b0);
+        *reinterpret_cast<uint2*>(d + B_PLANE) = make_uint2(a1, b1);
+        *reinterpret_cast<uint2*>(d + 2 * B_PLANE) = make_uint2(a2, b2);
+      }
+      __syncthreads();
+    }
+  } else if constexpr (PLANES_OUT) {
 #pragma unroll
     for (int mat = 0; mat < 3; ++mat) {
       q.Cx = p.Y + mat * p.y_mat;
@@ -469,7 +520,7 @@ int launch_split3m(const float* S, unsigned short* X, int B, int C, int N, int l
 // while staged: out 3M planes Y (ld ldy) or fp32 rows [b][re/im][co] of Sout (ld ldSout)
 int gemm_x6c_f32b(const unsigned short* Aw, int co, int ci, const float* Sin, int ldSin, int N,
                   unsigned short* Y, int ldy, float* Sout, int ldSout, bool relu, int B,
-                  hipStream_t s) {
+                  hipStream_t s, bool tiled_out) {
   if (co <= 0 || N <= 0 || B <= 0) return MSFNO_OK;
   MSFNO_REQUIRE(ldSin % 4 == 0 && (reinterpret_cast<uintptr_t>(Sin) & 15) == 0 && ldSin >= N,
                 MSFNO_EINVAL, "gemm_x6c_f32b: fp32 rows need ld % 4 == 0 and 16-B alignment");
@@ -500,17 +551,26 @@ int gemm_x6c_f32b(const unsigned short* Aw, int co, int ci, const float* Sin, in
   p.tiles_n = (int)cdiv(N, X6C_BN);
   p.relu = relu ? 1 : 0;
   const dim3 grid(p.tiles_m * p.tiles_n, 1, B);
-  if (Y)
+  if (Y && tiled_out) {
+    p.kt_out = p.Mp / 16;
+    p.y_b = x6c_tiled_elems(co, N);
+    hipLaunchKernelGGL((gemm_x6c_kernel<true, 4, 2, true, 0, 2>), grid, dim3(512), 0, s, p);
+  } else if (Y)
     hipLaunchKernelGGL((gemm_x6c_kernel<true, 4, 2, true>), grid, dim3(512), 0, s, p);
   else
     hipLaunchKernelGGL((gemm_x6c_kernel<false, 4, 2, true>), grid, dim3(512), 0, s, p);
   return launch_check("gemm_x6c_f32b");
 }
 
+// elements of one field's tiled 3M activation with `rows` channel rows, N columns
+int64_t x6c_tiled_elems(int rows, int N) {
+  return cdiv(N, X6C_BN) * round_up(rows, X6C_BM) * 9 * X6C_BN;
+}
+
 // one spectral-MLP layer: X (3M planes, ci rows, ld ldx) -> Y (3M planes, co rows,
 // ld ldx; relu) or, with S given, fp32 rows [b][re/im][co] of S (ld ldS)
 int gemm_x6c(const unsigned short* Aw, int co, int ci, const unsigned short* X, int N, int ldx,
-             unsigned short* Y, float* S, int ldS, bool relu, int B, hipStream_t s) {
+             unsigned short* Y, float* S, int ldS, bool relu, int B, hipStream_t s, int lay) {
   if (co <= 0 || N <= 0 || B <= 0) return MSFNO_OK;
   MSFNO_REQUIRE(ldx % 8 == 0 && ldx >= 8 && (reinterpret_cast<uintptr_t>(X) & 15) == 0,
                 MSFNO_EINVAL, "gemm_x6c: X planes need ld % 8 == 0 and 16-B alignment");
@@ -540,6 +600,18 @@ int gemm_x6c(const unsigned short* Aw, int co, int ci, const unsigned short* X, 
   p.tiles_n = (int)cdiv(N, X6C_BN);
   p.relu = relu ? 1 : 0;
   const dim3 grid(p.tiles_m * p.tiles_n, 1, B);
+  if (lay) {  // tiled activations (input must be tiled: the hidden layers / output layer)
+    MSFNO_REQUIRE((lay & 1) != 0 && ((lay & 2) == 0 || Y), MSFNO_EINVAL, "gemm_x6c: tiled layout");
+    p.x_b = x6c_tiled_elems(ci, N);
+    p.kt_in = (int)round_up(ci, X6C_BM) / 16;
+    p.kt_out = p.Mp / 16;
+    if (Y) p.y_b = x6c_tiled_elems(co, N);
+    if (Y)
+      hipLaunchKernelGGL((gemm_x6c_kernel<true, 4, 2, false, 0, 3>), grid, dim3(512), 0, s, p);
+    else
+      hipLaunchKernelGGL((gemm_x6c_kernel<false, 4, 2, false, 0, 1>), grid, dim3(512), 0, s, p);
+    return launch_check("gemm_x6c");
+  }
   // MSFNO_X6C_WAVES: 8 (4 x 2 waves of 32 x 64), 24 (2 x 4 waves of 64 x 32: the same
   // fragment bytes in 20 % fewer LDS read instructions), 4 (2 x 2 waves of 64 x 64)
   static const int waves = [] {
@@ -562,15 +634,18 @@ int gemm_x6c(const unsigned short* Aw, int co, int ci, const unsigned short* X, 
       const char* e = getenv("MSFNO_X6C_DBG");
       return e ? atoi(e) : 0;
     }();
-    if (dbg == 1) {
-      if (Y) hipLaunchKernelGGL((gemm_x6c_kernel<true, 4, 2, false, 1>), grid, dim3(512), 0, s, p);
-      else hipLaunchKernelGGL((gemm_x6c_kernel<false, 4, 2, false, 1>), grid, dim3(512), 0, s, p);
-    } else if (dbg == 2) {
-      if (Y) hipLaunchKernelGGL((gemm_x6c_kernel<true, 4, 2, false, 2>), grid, dim3(512), 0, s, p);
-      else hipLaunchKernelGGL((gemm_x6c_kernel<false, 4, 2, false, 2>), grid, dim3(512), 0, s, p);
-    } else if (dbg == 4) {
-      if (Y) hipLaunchKernelGGL((gemm_x6c_kernel<true, 4, 2, false, 4>), grid, dim3(512), 0, s, p);
-      else hipLaunchKernelGGL((gemm_x6c_kernel<false, 4, 2, false, 4>), grid, dim3(512), 0, s, p);
+    if (dbg > 0 && dbg < 8) {
+      static void (*const kp[8])(X6CParams) = {
+          nullptr, gemm_x6c_kernel<true, 4, 2, false, 1>, gemm_x6c_kernel<true, 4, 2, false, 2>,
+          gemm_x6c_kernel<true, 4, 2, false, 3>, gemm_x6c_kernel<true, 4, 2, false, 4>,
+          gemm_x6c_kernel<true, 4, 2, false, 5>, gemm_x6c_kernel<true, 4, 2, false, 6>,
+          gemm_x6c_kernel<true, 4, 2, false, 7>};
+      static void (*const kf[8])(X6CParams) = {
+          nullptr, gemm_x6c_kernel<false, 4, 2, false, 1>, gemm_x6c_kernel<false, 4, 2, false, 2>,
+          gemm_x6c_kernel<false, 4, 2, false, 3>, gemm_x6c_kernel<false, 4, 2, false, 4>,
+          gemm_x6c_kernel<false, 4, 2, false, 5>, gemm_x6c_kernel<false, 4, 2, false, 6>,
+          gemm_x6c_kernel<false, 4, 2, false, 7>};
+      hipLaunchKernelGGL((Y ? kp[dbg] : kf[dbg]), grid, dim3(512), 0, s, p);
     } else if (Y) {
       hipLaunchKernelGGL((gemm_x6c_kernel<true, 4, 2>), grid, dim3(512), 0, s, p);
     } else {
