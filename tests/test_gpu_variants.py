@@ -39,8 +39,8 @@ VARIANTS = [
     {"MSFNO_SPEC_HF32": "1"},
     {"MSFNO_X6C_TILED": "0"},
     {"MSFNO_MF_XS": "1"},
-    {"MSFNO_X6C_WAVES": "24"},
-    {"MSFNO_X6C_WAVES": "4"},
+    {"MSFNO_X6C_WAVES": "24", "MSFNO_X6C_TILED": "0"},
+    {"MSFNO_X6C_WAVES": "4", "MSFNO_X6C_TILED": "0"},
     {"MSFNO_TR_FWD": "2p", "MSFNO_TR_INV": "2p"},
 ]
 
