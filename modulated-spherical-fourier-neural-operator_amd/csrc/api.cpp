@@ -774,6 +774,24 @@ int run_filter(const msfno_block_desc* d, msfno_sht_plan_s* f, msfno_sht_plan_s*
         const char* e = getenv("MSFNO_SPEC_HF32");
         return e && e[0] == '1';
       }();
+      // MSFNO_SPEC_HF32T=1: fp32 hidden activations in the tiled layout (8 B per complex
+      // value, 16-KB contiguous stages), every layer splitting its input while staging
+      static const bool hf32t = [] {
+        const char* e = getenv("MSFNO_SPEC_HF32T");
+        return e && e[0] == '1';
+      }();
+      if (f32b && hf32t) {
+        const float* in = b.Sa;
+        for (int l = 0; l <= nl; ++l) {
+          prof(l == nl ? ST_SPEC_OUT : ST_SPEC_L0 + std::min(l, 3), s);
+          float* out = l == nl ? b.Sa : ((l & 1) ? b.Sc : b.Sb);
+          MSFNO_TRY(gemm_x6c_f32t(sw.out[l], sw.co[l], sw.ci[l], in, (int)L.ldT, l > 0, (int)L.Tp,
+                                  l < nl ? out : nullptr, l < nl ? nullptr : out, (int)L.ldT, l < nl,
+                                  B, s));
+          in = out;
+        }
+        return MSFNO_OK;
+      }
       if (f32b && hf32) {
         const float* in = b.Sa;
         for (int l = 0; l <= nl; ++l) {

@@ -219,6 +219,9 @@ int gemm_x6c_f32b(const unsigned short* Aw, int co, int ci, const float* Sin, in
                   unsigned short* Y, int ldy, float* Sout, int ldSout, bool relu, int B,
                   hipStream_t s, bool tiled_out = false);
 int64_t x6c_tiled_elems(int rows, int N);
+int gemm_x6c_f32t(const unsigned short* Aw, int co, int ci, const float* Sin, int ldSin,
+                  bool tiled_in, int N, float* Tout, float* Sout, int ldSout, bool relu, int B,
+                  hipStream_t s);
 int gemm_x6c(const unsigned short* Aw, int co, int ci, const unsigned short* X, int N, int ldx,
              unsigned short* Y, float* S, int ldS, bool relu, int B, hipStream_t s, int lay = 0);
 // fp32 x[z][r][c] (ld ldx, batch stride sx) -> bf16x3 planes xp[z][plane][r][c]

@@ -38,6 +38,7 @@ VARIANTS = [
     {"MSFNO_SPEC_L0F32": "0"},
     {"MSFNO_SPEC_HF32": "1"},
     {"MSFNO_X6C_TILED": "0"},
+    {"MSFNO_SPEC_HF32T": "1"},
     {"MSFNO_MF_XS": "1"},
     {"MSFNO_X6C_WAVES": "24", "MSFNO_X6C_TILED": "0"},
     {"MSFNO_X6C_WAVES": "4", "MSFNO_X6C_TILED": "0"},
