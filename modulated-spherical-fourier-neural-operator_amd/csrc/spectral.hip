@@ -332,9 +332,10 @@ __global__ __launch_bounds__(256) void transpose_inv_sym2_kernel(const float* __
 }
 
 // tile shape (latitudes x m) of the symmetric transposes: MSFNO_TR_FWD / MSFNO_TR_INV =
-// "64x32" | "32x64" | "32x128" | "16x128" (A/B; defaults 64x32 forward, 16x128 inverse:
-// 0.257 vs 0.268 ms for 32x64 at 721x1440, C = 256; the 32x128 tiles (67 KB of LDS)
-// lose occupancy: 0.58 / 0.34 ms)
+// "64x32" | "32x64" | "32x128" | "16x128" | "2p" (A/B; defaults 64x32 forward, 2p
+// inverse: 0.247-0.248 vs 0.255-0.258 ms for 16x128 in four interleaved in-block runs
+// at 721x1440, C = 256 (16x128: 0.257 vs 0.268 ms for 32x64); the 32x128 one-phase
+// tiles (67 KB of LDS) lose occupancy: 0.58 / 0.34 ms)
 static int tr_tile(const char* var, int dflt) {
   const char* e = getenv(var);
   if (!e) return dflt;
@@ -583,7 +584,7 @@ static void inv_sym_launch(const float* Yt, float2* Yn, int B, int C, const LatG
 
 static void inv_sym_dispatch(const float* Yt, float2* Yn, int B, int C, const LatGeom& g,
                              int mmax, int mact, const int* perm, hipStream_t s) {
-  static const int t = tr_tile("MSFNO_TR_INV", 3);
+  static const int t = tr_tile("MSFNO_TR_INV", 4);
   switch (t) {
     case 0: inv_sym_launch<64, 32>(Yt, Yn, B, C, g, mmax, mact, perm, s); break;
     case 1: inv_sym_launch<TK_INV, TM_INV>(Yt, Yn, B, C, g, mmax, mact, perm, s); break;
