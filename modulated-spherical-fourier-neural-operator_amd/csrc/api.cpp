@@ -229,7 +229,20 @@ int side_ctx(SideCtx** out, hipStream_t caller) {
     const char* pe = getenv("MSFNO_SIDE_PRIO");
     int least = 0, greatest = 0;
     hipError_t e = hipDeviceGetStreamPriorityRange(&least, &greatest);
-    if (e == hipSuccess) {
+    // MSFNO_SIDE_CUSTRIDE=k (A/B): the side stream runs on every k-th CU only (a CU
+    // mask; k coprime with 8 spreads it over all XCDs), at normal priority
+    const char* ce = getenv("MSFNO_SIDE_CUSTRIDE");
+    const int custride = ce ? atoi(ce) : 0;
+    if (e == hipSuccess && custride > 1) {
+      hipDeviceProp_t prop;
+      e = hipGetDeviceProperties(&prop, dev);
+      if (e == hipSuccess) {
+        const int ncu = prop.multiProcessorCount;
+        std::vector<uint32_t> mask((size_t)(ncu + 31) / 32, 0u);
+        for (int i = 0; i < ncu; i += custride) mask[(size_t)i / 32] |= 1u << (i % 32);
+        e = hipExtStreamCreateWithCUMask(&c.side, (uint32_t)mask.size(), mask.data());
+      }
+    } else if (e == hipSuccess) {
       if (pe && std::string(pe) == "normal")
         e = hipStreamCreateWithFlags(&c.side, hipStreamNonBlocking);
       else
