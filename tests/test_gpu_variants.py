@@ -44,6 +44,7 @@ VARIANTS = [
     {"MSFNO_X6C_WAVES": "4", "MSFNO_X6C_TILED": "0"},
     {"MSFNO_TR_FWD": "2p", "MSFNO_TR_INV": "2p"},
     {"MSFNO_TR_INV": "16x128"},
+    {"MSFNO_SIDE_CUSTRIDE": "3"},
 ]
 
 
