@@ -158,6 +158,9 @@ def parse(argv=None):
                          "(0: one sub-batch per field, at most 4)")
     ap.add_argument("--replicas-check", type=int, default=1,
                     help="latband, N>1: also time the replica mode (comm-free upper bound)")
+    ap.add_argument("--linear-check", type=int, default=1,
+                    help="N=1, non-linear headline: also time config 2's linear filter (the "
+                         "per-mode weight stream) and print it as the line's 'linear' object")
     ap.add_argument("--dry-run", action="store_true",
                     help="launcher / process-group check only (gloo, no GPU): ranks report in")
     return ap.parse_args(argv)
@@ -298,6 +301,8 @@ def cpu_baseline(args, p, cfg):
         C = 32
         p = sfno_ref.make_block_params(C, lmax, lmax + 1, cfg, seed=1)
         note = " (linear filter timed at C=32)"
+    if p is None:
+        p = sfno_ref.make_block_params(C, lmax, lmax + 1, cfg, seed=1)
     sht, isht = sfno_ref.make_transforms(nlat, nlon, lmax, lmax + 1)
     g = torch.Generator().manual_seed(0)
     x = torch.randn(1, C, nlat, nlon, generator=g)
@@ -490,10 +495,10 @@ def timed(step, args, dist, dev, backend):
 NON_KERNEL_STAGES = {"band_exchange"}
 
 
-def roofline(stages, args, B, C, rows, mset):
+def roofline(stages, args, B, C, rows, mset, name=None):
     """Roofline of the dominant kernel: the main-stream stage with the largest device
     time (the inner-skip GEMM overlaps the SHT on a side stream: its event span is not
-    a kernel duration, so it is not eligible)."""
+    a kernel duration, so it is not eligible), or of stage ``name``."""
     mmax = args.lmax + 1
     hid = shid = 2 * C
     side = os.environ.get("MSFNO_SIDE_STREAM", "1") != "0"
@@ -501,6 +506,8 @@ def roofline(stages, args, B, C, rows, mset):
             if not (side and k in SIDE_STAGES) and k not in NON_KERNEL_STAGES
             and stage_work(k, B, C, args.nlat, args.nlon, args.lmax, mmax, hid, shid,
                            rows, mset) is not None}
+    if name is not None:
+        elig = {k: v for k, v in elig.items() if k == name}
     if not elig:
         return None
     name, (tot_ms, cnt) = max(elig.items(), key=lambda kv: kv[1][0])
@@ -540,6 +547,36 @@ def print_stages(stages, args, B, C, rows, mset, tag=""):
             else:
                 extra = f" {a / 1e9:.0f} GB/s ({100 * a / 1e9 / PEAK_HBM_GBS:.0f}%)"
         print(f"  {tag}stage {k:18s} {ms / c:8.3f} ms x{c}{extra}", file=sys.stderr)
+
+
+def linear_line(args, dev):
+    """Config 2's second filter (SURVEY.md §8d "measure both filters"): the same
+    block with the linear per-mode filter (SpectralConvS2, layers.py:398-427: the
+    (C, C, T, 2) weight, 34.07 GB at C = 256, streamed once per field), same K / W.
+    Its roofline is the weight-streaming contraction's (HBM); the CPU baseline is
+    the oracle at C = 32 (the 34 GB weight does not fit the sample budget)."""
+    import copy
+    la = copy.copy(args)
+    la.filter = "linear"
+    torch.cuda.empty_cache()
+    blk, p, cfg = build_block(la, dev)
+    g = torch.Generator().manual_seed(0)
+    x = torch.randn(args.batch, args.C, args.nlat, args.nlon, generator=g).to(dev)
+    gamma = (0.1 * torch.randn(args.batch, args.C, generator=g)).to(dev)
+    beta = (0.1 * torch.randn(args.batch, args.C, generator=g)).to(dev)
+    with torch.no_grad():
+        y, elapsed, stages = timed(lambda: blk(x, gamma, beta, 1.0), la, False, dev, "nccl")
+    assert torch.isfinite(y).all()
+    roof = roofline(stages, la, args.batch, args.C, None, None, name="linear_contract")
+    del blk, x, y
+    torch.cuda.empty_cache()
+    cpu = None
+    if args.cpu_baseline:
+        cpu = cpu_baseline(la, None, cfg)
+    return {"filter": "linear", "value": round(args.batch * args.steps / elapsed, 3),
+            "unit": "fields/s", "ms_per_step": round(1000.0 * elapsed / args.steps, 3),
+            "workload": f"sfno_block_fwd_{args.nlat}x{args.nlon}_C{args.C}_lmax{args.lmax}_"
+                        "linear_filmed", "roofline": roof, "cpu_baseline": cpu}
 
 
 def dry_run(rank, world):
@@ -687,6 +724,10 @@ def main():
         torch.cuda.empty_cache()
         cpu = cpu_baseline(args, p, cfg)
 
+    linear = None
+    if world == 1 and args.linear_check and args.filter == "non-linear" and not band:
+        linear = linear_line(args, dev)
+
     if rank == 0:
         out = {
             "metric": "SFNO-Block forward fields/sec on 721x1440x256; rocprof HBM GB/s vs peak",
@@ -718,6 +759,8 @@ def main():
             out["per_rank"] = per_rank
         if replicas:
             out["replicas_upper_bound"] = replicas
+        if linear:
+            out["linear"] = linear
         print(json.dumps(out), flush=True)
     if dist:
         torch.distributed.destroy_process_group()

@@ -194,6 +194,35 @@ void prof(int stage, hipStream_t s) { g_prof.mark(stage, s); }
 // through events; capture-safe).  MSFNO_SIDE_STREAM=0 disables it.
 // ---------------------------------------------------------------------------
 
+// side stream at the lowest priority: the skip GEMM fills what the spectral path
+// leaves (+1 % over equal priority, measured); MSFNO_SIDE_PRIO=normal|high for A/B.
+// MSFNO_SIDE_CUSTRIDE=k (A/B): the side stream runs on every k-th CU only (a CU
+// mask; k coprime with 8 spreads it over all XCDs), at normal priority.
+static hipError_t create_side_stream(hipStream_t* s, int dev) {
+  const char* pe = getenv("MSFNO_SIDE_PRIO");
+  int least = 0, greatest = 0;
+  hipError_t e = hipDeviceGetStreamPriorityRange(&least, &greatest);
+  const char* ce = getenv("MSFNO_SIDE_CUSTRIDE");
+  const int custride = ce ? atoi(ce) : 0;
+  if (e == hipSuccess && custride > 1) {
+    hipDeviceProp_t prop;
+    e = hipGetDeviceProperties(&prop, dev);
+    if (e == hipSuccess) {
+      const int ncu = prop.multiProcessorCount;
+      std::vector<uint32_t> mask((size_t)(ncu + 31) / 32, 0u);
+      for (int i = 0; i < ncu; i += custride) mask[(size_t)i / 32] |= 1u << (i % 32);
+      e = hipExtStreamCreateWithCUMask(s, (uint32_t)mask.size(), mask.data());
+    }
+  } else if (e == hipSuccess) {
+    if (pe && std::string(pe) == "normal")
+      e = hipStreamCreateWithFlags(s, hipStreamNonBlocking);
+    else
+      e = hipStreamCreateWithPriority(s, hipStreamNonBlocking,
+                                      (pe && std::string(pe) == "high") ? greatest : least);
+  }
+  return e;
+}
+
 int side_ctx(SideCtx** out, hipStream_t caller) {
   static int enabled = -1;
   if (enabled < 0) {
@@ -210,47 +239,48 @@ int side_ctx(SideCtx** out, hipStream_t caller) {
     if (hipStreamIsCapturing(caller, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone)
       return MSFNO_OK;
   }
-  // one side stream + fork/join pair per (device, caller stream): the device comes
-  // from the caller's stream (not the thread's current device), and two caller
-  // streams never share fork/join events
+  // one side stream per device (pooled: every caller stream of that device forks to
+  // it) + one fork/join event pair per (device, caller stream).  The device comes
+  // from the caller's stream (not the thread's current device); two caller streams
+  // never share fork/join events.  The per-caller map is bounded (LRU, kMaxCallers):
+  // a caller that creates and destroys many streams recycles the oldest pair
+  // instead of leaking events (an evicted pair is destroyed; HIP releases an event
+  // whose recorded work is still pending once it completes).
   static std::mutex mu;
-  static std::map<std::pair<int, hipStream_t>, SideCtx> ctx;
+  static std::map<int, hipStream_t> side_of_dev;
+  struct Entry {
+    SideCtx c;
+    uint64_t used = 0;
+  };
+  static std::map<std::pair<int, hipStream_t>, Entry> ctx;
+  static uint64_t tick = 0;
+  constexpr size_t kMaxCallers = 64;
   int dev = 0;
   if (caller) MSFNO_CHECK_HIP(hipStreamGetDevice(caller, &dev));
   else MSFNO_CHECK_HIP(hipGetDevice(&dev));
   std::lock_guard<std::mutex> lk(mu);
-  SideCtx& c = ctx[{dev, caller}];
-  if (!c.side) {
+  auto it = ctx.find({dev, caller});
+  if (it == ctx.end() && ctx.size() >= kMaxCallers) {
+    auto lru = ctx.begin();
+    for (auto j = ctx.begin(); j != ctx.end(); ++j)
+      if (j->second.used < lru->second.used) lru = j;
+    (void)hipEventDestroy(lru->second.c.fork);
+    (void)hipEventDestroy(lru->second.c.join);
+    ctx.erase(lru);
+  }
+  Entry& en = ctx[{dev, caller}];
+  en.used = ++tick;
+  SideCtx& c = en.c;
+  if (!c.side || !c.fork || !c.join) {
     int cur = 0;
     MSFNO_CHECK_HIP(hipGetDevice(&cur));
     if (cur != dev) MSFNO_CHECK_HIP(hipSetDevice(dev));
-    // side stream at the lowest priority: the skip GEMM fills what the spectral path
-    // leaves (+1 % over equal priority, measured); MSFNO_SIDE_PRIO=normal|high for A/B
-    const char* pe = getenv("MSFNO_SIDE_PRIO");
-    int least = 0, greatest = 0;
-    hipError_t e = hipDeviceGetStreamPriorityRange(&least, &greatest);
-    // MSFNO_SIDE_CUSTRIDE=k (A/B): the side stream runs on every k-th CU only (a CU
-    // mask; k coprime with 8 spreads it over all XCDs), at normal priority
-    const char* ce = getenv("MSFNO_SIDE_CUSTRIDE");
-    const int custride = ce ? atoi(ce) : 0;
-    if (e == hipSuccess && custride > 1) {
-      hipDeviceProp_t prop;
-      e = hipGetDeviceProperties(&prop, dev);
-      if (e == hipSuccess) {
-        const int ncu = prop.multiProcessorCount;
-        std::vector<uint32_t> mask((size_t)(ncu + 31) / 32, 0u);
-        for (int i = 0; i < ncu; i += custride) mask[(size_t)i / 32] |= 1u << (i % 32);
-        e = hipExtStreamCreateWithCUMask(&c.side, (uint32_t)mask.size(), mask.data());
-      }
-    } else if (e == hipSuccess) {
-      if (pe && std::string(pe) == "normal")
-        e = hipStreamCreateWithFlags(&c.side, hipStreamNonBlocking);
-      else
-        e = hipStreamCreateWithPriority(&c.side, hipStreamNonBlocking,
-                                        (pe && std::string(pe) == "high") ? greatest : least);
-    }
-    if (e == hipSuccess) e = hipEventCreateWithFlags(&c.fork, hipEventDisableTiming);
-    if (e == hipSuccess) e = hipEventCreateWithFlags(&c.join, hipEventDisableTiming);
+    hipError_t e = hipSuccess;
+    hipStream_t& pooled = side_of_dev[dev];
+    if (!pooled) e = create_side_stream(&pooled, dev);
+    c.side = pooled;
+    if (e == hipSuccess && !c.fork) e = hipEventCreateWithFlags(&c.fork, hipEventDisableTiming);
+    if (e == hipSuccess && !c.join) e = hipEventCreateWithFlags(&c.join, hipEventDisableTiming);
     if (cur != dev) (void)hipSetDevice(cur);
     if (e != hipSuccess) {
       set_error(std::string("side stream creation failed: ") + hipGetErrorString(e));

@@ -180,6 +180,7 @@ def _drive_pipelined(gens, comm, stream):
     K = len(gens)
     pending = [None] * K
     alive = [True] * K
+    outs = [None] * K
     t = 0
     while any(alive):
         for k in range(min(t + 1, K)):
@@ -194,12 +195,14 @@ def _drive_pipelined(gens, comm, stream):
                 res = h.wait()
                 try:
                     req = gens[k].send(res)
-                except StopIteration:
+                except StopIteration as stop:
                     alive[k] = False
                     pending[k] = None
+                    outs[k] = stop.value
                     continue
             pending[k] = _issue(req, comm)
         t += 1
+    return outs
 
 
 class LocalGroup:
@@ -208,45 +211,83 @@ class LocalGroup:
     sharded path on one GPU, and by world-size-1 runs."""
 
     @staticmethod
+    def _exchange(reqs):
+        """Serve one collective posted by every virtual rank (``reqs[r]``); returns
+        each rank's result."""
+        W = len(reqs)
+        kind = reqs[0][0]
+        assert all(r[0] == kind for r in reqs), "ranks out of step"
+        if kind == "all_gather":
+            stacked = torch.stack([r[1] for r in reqs])
+            return [stacked] * W
+        offs = []
+        for p in range(W):
+            o, acc = [], 0
+            for c in reqs[p][2]:
+                o.append(acc)
+                acc += c
+            offs.append(o)
+        for q in range(W):
+            recv, rc = reqs[q][3], reqs[q][4]
+            acc = 0
+            for p in range(W):
+                n = rc[p]
+                assert reqs[p][2][q] == n, "send/recv counts disagree"
+                src = reqs[p][1][offs[p][q]:offs[p][q] + n]
+                if src.data_ptr() != recv[acc:acc + n].data_ptr():
+                    recv[acc:acc + n].copy_(src)
+                acc += n
+        return [None] * W
+
+    @staticmethod
     def run(gens):
         reqs = [next(g) for g in gens]
         outs = [None] * len(gens)
         live = list(range(len(gens)))
         while live:
-            kind = reqs[live[0]][0]
-            assert all(reqs[i][0] == kind for i in live), "ranks out of step"
-            res = [None] * len(gens)
-            if kind == "all_gather":
-                stacked = torch.stack([reqs[i][1] for i in live])
-                res = [stacked] * len(gens)
-            else:
-                W = len(gens)
-                offs = []
-                for p in range(W):
-                    sc = reqs[p][2]
-                    o, acc = [], 0
-                    for c in sc:
-                        o.append(acc)
-                        acc += c
-                    offs.append(o)
-                for q in range(W):
-                    recv, rc = reqs[q][3], reqs[q][4]
-                    acc = 0
-                    for p in range(W):
-                        n = rc[p]
-                        assert reqs[p][2][q] == n, "send/recv counts disagree"
-                        src = reqs[p][1][offs[p][q]:offs[p][q] + n]
-                        if src.data_ptr() != recv[acc:acc + n].data_ptr():
-                            recv[acc:acc + n].copy_(src)
-                        acc += n
+            res = LocalGroup._exchange([reqs[i] for i in live])
             nxt = []
-            for i in live:
+            for j, i in enumerate(live):
                 try:
-                    reqs[i] = gens[i].send(res[i])
+                    reqs[i] = gens[i].send(res[j])
                     nxt.append(i)
                 except StopIteration as stop:
                     outs[i] = stop.value
             live = nxt
+        return outs
+
+    @staticmethod
+    def run_pipelined(gens):
+        """Lock-step virtual ranks with the sub-batch pipeline of ``_drive_pipelined``:
+        ``gens[r][k]`` is rank r's generator of sub-batch k.  The stages are enqueued
+        in the same interleaved order as on a real rank (at tick t every started
+        sub-batch advances one stage, the one furthest along first, then sub-batch t
+        starts); each exchange is served once every rank has posted it."""
+        W, K = len(gens), len(gens[0])
+        reqs = [[None] * K for _ in range(W)]
+        outs = [[None] * K for _ in range(W)]
+        alive = [True] * K
+        t = 0
+        while any(alive):
+            for k in range(min(t + 1, K)):
+                if not alive[k]:
+                    continue
+                if t == k:
+                    for r in range(W):
+                        reqs[r][k] = next(gens[r][k])
+                    continue
+                res = LocalGroup._exchange([reqs[r][k] for r in range(W)])
+                done = 0
+                for r in range(W):
+                    try:
+                        reqs[r][k] = gens[r][k].send(res[r])
+                    except StopIteration as stop:
+                        outs[r][k] = stop.value
+                        done += 1
+                assert done in (0, W), "ranks out of step"
+                if done:
+                    alive[k] = False
+            t += 1
         return outs
 
 
@@ -379,15 +420,17 @@ class LatBandBlock:
     def _linear_weight(self, w):
         """This rank's slice w[:, :, modes, :] of the per-mode weight (cached until
         the parameter changes); the whole weight when the rank owns every mode."""
-        key = (w.data_ptr(), w._version, str(w.device))
+        key = (w.data_ptr(), w._version, w.dtype, str(w.device))
         if self._lin is not None and self._lin[0] == key:
             return self._lin[1]
         modes = self.plan.linear_modes()
+        # the contraction reads fp32 (C, C, T, 2) contiguous, as _fill_desc passes it
+        wf = w.detach().float().contiguous()
         if len(modes) == w.shape[2]:
-            local = w
+            local = wf
         else:
             idx = torch.tensor(modes, dtype=torch.long, device=w.device)
-            local = w.detach().index_select(2, idx).contiguous()
+            local = wf.index_select(2, idx).contiguous()
         self._lin = (key, local)
         return local
 
@@ -466,6 +509,23 @@ class LatBandBlock:
         del keep, st, st2
         return out
 
+    def chunk_stages(self, x, gamma=None, beta=None, scale=1.0, chunks=1):
+        """(out, generators): the batch split into ``chunks`` sub-batches, each with
+        its own slot, writing its rows of ``out`` (the pipeline of ``forward``)."""
+        x = N.require_device_f32(x, "band block input")
+        B = x.shape[0]
+        K = max(1, min(int(chunks), B, 64))
+        out = torch.empty(B, x.shape[1], len(self.rows_out), self.nlon_out, dtype=torch.float32,
+                          device=x.device)
+        bounds = [B * k // K for k in range(K + 1)]
+        gens = []
+        for k in range(K):
+            b0, b1 = bounds[k], bounds[k + 1]
+            g = gamma[b0:b1] if gamma is not None else None
+            be = beta[b0:b1] if beta is not None else None
+            gens.append(self.stages(x[b0:b1], g, be, scale, slot=k, out=out[b0:b1]))
+        return out, gens
+
     def forward(self, x, gamma=None, beta=None, scale=1.0, comm=None, chunks=1):
         """This rank's output rows.  ``chunks`` > 1 pipelines that many sub-batches
         (exchanges overlapped with the other sub-batches' compute)."""
@@ -476,16 +536,7 @@ class LatBandBlock:
             if self.world == 1 and comm is None:
                 return LocalGroup.run([gen])[0]
             return _drive(gen, comm if comm is not None else TorchComm())
-        x = N.require_device_f32(x, "band block input")
-        out = torch.empty(B, x.shape[1], len(self.rows_out), self.nlon_out, dtype=torch.float32,
-                          device=x.device)
-        bounds = [B * k // K for k in range(K + 1)]
-        gens = []
-        for k in range(K):
-            b0, b1 = bounds[k], bounds[k + 1]
-            g = gamma[b0:b1] if gamma is not None else None
-            be = beta[b0:b1] if beta is not None else None
-            gens.append(self.stages(x[b0:b1], g, be, scale, slot=k, out=out[b0:b1]))
+        out, gens = self.chunk_stages(x, gamma, beta, scale, K)
         if self.world == 1 and comm is None:
             for gen in gens:
                 LocalGroup.run([gen])
@@ -506,10 +557,11 @@ class LatBandNet:
     are this rank's rows of the full grid (``take`` / ``LatBandBlock.assemble``
     conventions); ``forward(x_local, sst, scale)`` returns its rows of the output."""
 
-    def __init__(self, net, rank: int, world: int, device=None, comm=None):
+    def __init__(self, net, rank: int, world: int, device=None, comm=None, chunks=1):
         self.net = net
         self.rank, self.world = rank, world
         self.comm = comm
+        self.chunks = chunks
         self.shards = [LatBandBlock(blk, rank, world, device=device) for blk in net.blocks]
         for a, b in zip(self.shards, self.shards[1:]):
             assert a.rows_out == b.rows, "block band partitions do not chain"
@@ -529,9 +581,10 @@ class LatBandNet:
             self._pos = (key, pe.detach().index_select(2, idx).to(device).contiguous())
         return self._pos[1]
 
-    def stages(self, x, sst=None, scale=1.0):
+    def stages(self, x, sst=None, scale=1.0, slot=0):
         """Generator over the whole network's exchanges (see LatBandBlock.stages);
-        returns this rank's output rows."""
+        returns this rank's output rows.  ``slot`` as in LatBandBlock.stages (one per
+        sub-batch in flight)."""
         net = self.net
         filmed = getattr(net, "_filmed", None)
         gamma = beta = None
@@ -540,19 +593,40 @@ class LatBandNet:
             gamma, beta = film_mod[:, 0], film_mod[:, 1]
         residual = x
         h = net.encoder.native_forward(x, addend=self._pos_local(x.device))
+        h = net.pos_drop(h)  # sfnonet.py:674 / 827 (identity in eval)
         for i, s in enumerate(self.shards):
             if filmed is not None and filmed(i):
                 k = i - (net.num_layers - net.film_layers)
-                h = yield from s.stages(h, gamma[:, k], beta[:, k], scale)
+                h = yield from s.stages(h, gamma[:, k], beta[:, k], scale, slot=slot)
             else:
-                h = yield from s.stages(h)
+                h = yield from s.stages(h, slot=slot)
         return net.decode(h, residual)
 
-    def forward(self, x, sst=None, scale=1.0, comm=None):
-        gen = self.stages(x, sst, scale)
+    def chunk_stages(self, x, sst=None, scale=1.0, chunks=1):
+        """Generators of ``chunks`` sub-batches (fields are independent), each with its
+        own exchange slot; the ``sst`` / modulation batch is split the same way."""
+        B = x.shape[0]
+        K = max(1, min(int(chunks), B, 64))
+        bounds = [B * k // K for k in range(K + 1)]
+        return [self.stages(x[bounds[k]:bounds[k + 1]],
+                            sst[bounds[k]:bounds[k + 1]] if sst is not None else None,
+                            scale, slot=k) for k in range(K)]
+
+    def forward(self, x, sst=None, scale=1.0, comm=None, chunks=None):
+        """This rank's output rows.  ``chunks`` > 1 pipelines that many sub-batches
+        through the whole network: while one sub-batch's exchange is in flight the
+        others' blocks run (the LatBandBlock pipeline, across all 12 blocks)."""
         comm = comm if comm is not None else self.comm
+        gens = self.chunk_stages(x, sst, scale, self.chunks if chunks is None else chunks)
+        if len(gens) == 1:
+            if self.world == 1 and comm is None:
+                return LocalGroup.run(gens)[0]
+            return _drive(gens[0], comm if comm is not None else TorchComm())
         if self.world == 1 and comm is None:
-            return LocalGroup.run([gen])[0]
-        return _drive(gen, comm if comm is not None else TorchComm())
+            outs = [LocalGroup.run([g])[0] for g in gens]
+        else:
+            outs = _drive_pipelined(gens, comm if comm is not None else TorchComm(),
+                                    N.stream_of(x.device))
+        return torch.cat(outs, dim=0)
 
     __call__ = forward

@@ -187,14 +187,26 @@ class FourierNeuralOperatorBlock(nn.Module):
     def _transforms(self):
         return self.filter_layer.filter._transforms()
 
+    def _wcache_key_of(self, device, nbytes):
+        """The prepared images depend only on the module's own weights: key on the
+        Parameters themselves (data_ptr, _version, dtype), not on the fp32 copies the
+        descriptor points at (those are fresh tensors, version 0, often at a reused
+        address)."""
+        return (str(device), nbytes) + tuple(
+            (p.data_ptr(), p._version, p.dtype) for p in self.parameters())
+
     def wcache_attach(self, d, keep, device):
         """Point the descriptor at this module's prepared-weight cache (bf16x3 weight
         images, msfno_block_desc.wcache) and mark it valid when the weights are
-        unchanged since it was filled: keyed on every tensor the descriptor points
-        at, by (data_ptr, _version).  Returns the key to pass to wcache_commit once
+        unchanged since it was filled.  Returns the key to pass to wcache_commit once
         the native call has been issued.  In-place weight updates bump _version, so
         the next call rebuilds the images; a HIP graph captured with a valid cache
-        replays without the preparation (weights frozen, as in Rollout)."""
+        replays without the preparation (weights frozen, as in Rollout).
+
+        Stream safety: the images were written (and last read) on the stream of the
+        previous committed call; a call on another stream first waits for that call's
+        completion event, so it neither reads unwritten images nor rebuilds them under
+        a reader."""
         L = N.lib()
         nbytes = L.msfno_block_wcache_size(d)
         if nbytes == 0 or not _WCACHE:
@@ -203,15 +215,30 @@ class FourierNeuralOperatorBlock(nn.Module):
         if buf is None or buf.device != device or buf.numel() < nbytes:
             buf = self._wcache_buf = torch.empty(nbytes, dtype=torch.uint8, device=device)
             self._wcache_key = None
-        key = (str(device), nbytes) + tuple((t.data_ptr(), t._version) for t in keep
-                                            if isinstance(t, torch.Tensor))
+            self._wcache_event = None
+        cur = torch.cuda.current_stream(device)
+        ev = getattr(self, "_wcache_event", None)
+        if ev is not None and ev[0] != cur.cuda_stream \
+                and not torch.cuda.is_current_stream_capturing():
+            cur.wait_event(ev[1])
+        key = self._wcache_key_of(device, nbytes)
         d.wcache = buf.data_ptr()
         d.wcache_valid = int(key == getattr(self, "_wcache_key", None))
         return key
 
     def wcache_commit(self, key):
-        if key is not None:
-            self._wcache_key = key
+        """Mark the images valid after the native call that (re)built them.  Never
+        while the stream is being captured: the preparation then lives only in the
+        graph, and the buffer has not been written yet (a capture that found the
+        images valid leaves the key as it was)."""
+        if key is None or torch.cuda.is_current_stream_capturing():
+            return
+        dev = self._wcache_buf.device
+        cur = torch.cuda.current_stream(dev)
+        e = torch.cuda.Event()
+        e.record(cur)
+        self._wcache_event = (cur.cuda_stream, e)
+        self._wcache_key = key
 
     @N.on_input_device
     def _native_forward(self, x, gamma=None, beta=None, scale=1.0):

@@ -109,3 +109,83 @@ def test_latband_filmed_net_matches_unsharded(path):
         want = net(x, film, 0.8)
         got = _sharded_net(net, x, 3, film, 0.8)
     assert (got - want).abs().max().item() < 2e-5 * max(1.0, want.abs().max().item())
+
+
+def _rollout_rank(rank, world, port, path, q, chunks):
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    for p in (here, os.path.dirname(here),
+              os.path.join(os.path.dirname(here), "modulated-spherical-fourier-neural-operator_amd")):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    import torch.distributed as dist
+    from test_oracle_net import load_net as ld
+    from msfno_amd.rollout import Rollout
+    from msfno_amd.sfno import LatBandNet, TorchComm
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        meta, params, x, _, _ = ld(path)
+        net = _build(meta, params, filmed=True, film_layers=2)
+        film, means, stds = _rollout_inputs(meta, x)
+        shard = LatBandNet(net, rank, world, comm=TorchComm(), chunks=chunks)
+        r = Rollout(shard, means.to(DEV), stds.to(DEV), film=film.to(DEV), scale=0.8)
+        x0 = shard.take((x.to(DEV) * stds.to(DEV) + means.to(DEV)).repeat(2, 1, 1, 1))
+        outs = [o.cpu().numpy() for _, o in r.run(x0, 3)]
+        q.put((rank, (shard.rows_out, outs)))
+    finally:
+        dist.destroy_process_group()
+
+
+def _rollout_inputs(meta, x):
+    g = torch.Generator().manual_seed(9)
+    C, ch = meta["C"], meta["in_chans"]
+    B = 2 * x.shape[0]
+    film = torch.stack((0.1 * torch.randn(B, 2, C, generator=g),
+                        0.1 * torch.randn(B, 2, C, generator=g)), dim=1)
+    means = torch.randn(1, ch, 1, 1, generator=g)
+    stds = torch.rand(1, ch, 1, 1, generator=g) + 0.5
+    return film, means, stds
+
+
+@pytest.mark.parametrize("chunks", [1, 2])
+def test_rollout_of_latband_net_two_processes_gloo(chunks):
+    """Rollout driving one rank's LatBandNet (normalise, step, denormalise on the
+    rank's rows) in two processes over torch.distributed (gloo), with and without
+    the sub-batch pipeline across the whole network, against the unsharded
+    Rollout: three 6 h steps of the filmed fixture network."""
+    import socket
+
+    import torch.multiprocessing as mp
+    from msfno_amd.rollout import Rollout
+    path = NET_FIXTURES[0]
+    meta, params, x, _, _ = load_net(path)
+    net = _build(meta, params, filmed=True, film_layers=2)
+    film, means, stds = _rollout_inputs(meta, x)
+    x0 = (x.to(DEV) * stds.to(DEV) + means.to(DEV)).repeat(2, 1, 1, 1)
+    r = Rollout(net, means.to(DEV), stds.to(DEV), film=film.to(DEV), scale=0.8, graph=False)
+    want = [o.cpu() for _, o in r.run(x0, 3)]
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_rollout_rank, args=(rk, 2, port, path, q, chunks))
+          for rk in range(2)]
+    for p in ps:
+        p.start()
+    try:
+        res = dict(q.get(timeout=300) for _ in range(2))
+    finally:
+        for p in ps:
+            p.join(timeout=60)
+            if p.is_alive():
+                p.kill()
+    for i in range(3):
+        y = torch.full_like(want[i], float("nan"))
+        for rk in range(2):
+            rows, parts = res[rk]
+            y[:, :, rows] = torch.from_numpy(parts[i])
+        sc = max(1.0, want[i].abs().max().item())
+        assert (y - want[i]).abs().max().item() < 2e-5 * sc, i

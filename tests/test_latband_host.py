@@ -249,3 +249,75 @@ def test_sharded_exchange_over_gloo(world, B, C, nlat, lmax, mmax):
     for p in ps:
         p.join(timeout=60)
     assert res == {r: "ok" for r in range(world)}, res
+
+
+class _FakeWork:
+    def __init__(self, log, tag):
+        self.log, self.tag = log, tag
+
+    def wait(self):
+        self.log.append(("wait",) + self.tag)
+
+
+class _FakeComm:
+    """Deferred collectives (the RCCL path's shape): issue returns a _Pending whose
+    wait() is logged; nothing completes until then."""
+
+    def __init__(self, log):
+        self.log = log
+
+    def all_gather_async(self, t):
+        tag = ("all_gather", t["k"], t["stage"])
+        self.log.append(("issue",) + tag)
+        return latband._Pending(_FakeWork(self.log, tag), value=("gathered", t["k"], t["stage"]))
+
+    def all_to_all_async(self, send, sc, recv, rc):
+        tag = ("all_to_all", send["k"], send["stage"])
+        self.log.append(("issue",) + tag)
+        return latband._Pending(_FakeWork(self.log, tag))
+
+
+def _fake_sub_batch(k, log, nstages=5):
+    """A stage generator shaped like LatBandBlock.stages: stage s runs (logged), then
+    posts a collective on its slot's buffers; the next stage may only run (and so
+    reuse the slot's buffers) after that collective's wait."""
+    for s in range(nstages - 1):
+        log.append(("stage", k, s))
+        buf = {"k": k, "stage": s}
+        if s % 3 == 0:
+            res = yield ("all_gather", buf)
+            assert res == ("gathered", k, s)
+        else:
+            res = yield ("all_to_all", buf, [1], buf, [1])
+            assert res is None
+    log.append(("stage", k, nstages - 1))
+    return f"out{k}"
+
+
+@pytest.mark.parametrize("K", [1, 2, 4])
+def test_drive_pipelined_issue_wait_order_with_deferred_handles(K):
+    """_drive_pipelined against deferred (RCCL-style) handles: every collective is
+    waited for exactly once, before its sub-batch's next stage runs (so a slot's
+    send/recv buffers are reused only after the wait), each wait comes after the
+    other started sub-batches' stages were enqueued behind the issue (the overlap),
+    and the generators' return values come back in sub-batch order."""
+    log = []
+    gens = [_fake_sub_batch(k, log) for k in range(K)]
+    outs = latband._drive_pipelined(gens, _FakeComm(log), stream=0)
+    assert outs == [f"out{k}" for k in range(K)]
+    issues = [e for e in log if e[0] == "issue"]
+    waits = [e for e in log if e[0] == "wait"]
+    assert sorted(i[1:] for i in issues) == sorted(w[1:] for w in waits)
+    assert len(issues) == 4 * K
+    pos = {e: i for i, e in enumerate(log)}
+    for (_, kind, k, s) in issues:
+        i_issue, i_wait = pos[("issue", kind, k, s)], pos[("wait", kind, k, s)]
+        i_next = pos[("stage", k, s + 1)]
+        assert i_issue < i_wait < i_next
+        # between the issue and its wait, every other live sub-batch enqueued a stage
+        if K > 1:
+            between = {e[1] for e in log[i_issue:i_wait] if e[0] == "stage"}
+            live = {j for j in range(K)
+                    if ("stage", j, 0) in pos and pos[("stage", j, 0)] < i_wait
+                    and pos[("stage", j, 4)] > i_issue and j != k}
+            assert live <= between, (kind, k, s, live, between)
