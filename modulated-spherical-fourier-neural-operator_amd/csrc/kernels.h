@@ -91,6 +91,14 @@ int launch_mlp_fused_images(const float* W1, const float* W2, unsigned short* im
 int launch_mlp_fused(const float* x1, const float* scale, const float* shift, const float* resid,
                      float* out, const unsigned short* img, const float* b1, const float* b2,
                      int B, int64_t P, hipStream_t s);
+// mlp_fused2.hip: the same MLP re-tiled for two workgroups per CU (16x16x32 MFMAs,
+// 16 pixels per wave); its own weight-image layout (same size).  launch_mlp_fused*
+// dispatch to it unless MSFNO_MF2=0.
+bool mlp_fused2_env();
+int launch_mlp_fused2_images(const float* W1, const float* W2, unsigned short* img, hipStream_t s);
+int launch_mlp_fused2(const float* x1, const float* scale, const float* shift, const float* resid,
+                      float* out, const unsigned short* img, const float* b1, const float* b2,
+                      int B, int64_t P, hipStream_t s);
 // ---- cgemm.hip -----------------------------------------------------------------
 // complex (Ci,Co,2) weight -> Ar, Ai (Co x Ci) row-major (Ar[o][i] = Re w[i][o])
 int launch_split_complex_weight(const float* w, float* Ar, float* Ai, int Ci, int Co,
