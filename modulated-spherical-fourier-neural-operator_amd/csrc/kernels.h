@@ -93,9 +93,17 @@ int launch_mlp_fused(const float* x1, const float* scale, const float* shift, co
                      int B, int64_t P, hipStream_t s);
 // mlp_fused2.hip: the same MLP re-tiled for two workgroups per CU (16x16x32 MFMAs,
 // 16 pixels per wave); its own weight-image layout (same size).  launch_mlp_fused*
-// dispatch to it unless MSFNO_MF2=0.
+// dispatch to it with MSFNO_MF2=1 (A/B: measured equal to mlp_fused.hip).
 bool mlp_fused2_env();
 int launch_mlp_fused2_images(const float* W1, const float* W2, unsigned short* img, hipStream_t s);
+// mlp_fused_h.hip: the MLP on the x3h engine (fp32 as two fp16 terms, three fp16
+// MFMAs per product, row-scaled weights); MSFNO_ENGINE=x3h
+bool mlp_fused_h_env();
+size_t mlp_fused_h_image_bytes();
+int launch_mlp_fused_h_images(const float* W1, const float* W2, unsigned short* img, hipStream_t s);
+int launch_mlp_fused_h(const float* x1, const float* scale, const float* shift, const float* resid,
+                       float* out, const unsigned short* img, const float* b1, const float* b2,
+                       int B, int64_t P, hipStream_t s);
 int launch_mlp_fused2(const float* x1, const float* scale, const float* shift, const float* resid,
                       float* out, const unsigned short* img, const float* b1, const float* b2,
                       int B, int64_t P, hipStream_t s);

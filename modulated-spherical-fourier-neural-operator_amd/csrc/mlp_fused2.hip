@@ -349,7 +349,7 @@ __global__ __launch_bounds__(256, 2) void mlp_fused2_kernel(Mlp2Params p) {
 bool mlp_fused2_env() {
   static const bool on = [] {
     const char* e = getenv("MSFNO_MF2");
-    return !(e && e[0] == '0');
+    return e && e[0] == '1';
   }();
   return on;
 }

@@ -1,0 +1,458 @@
+// Fused block MLP on the "x3h" engine (gfx950): out = W2·GELU(W1·(a ⊙ x1 + t) + b1)
+// + b2 + resid, C = 256, H = 512, hidden activation on-chip — the tiling of
+// mlp_fused2.hip (16x16x32 MFMAs, 16 pixels per wave, 64 per workgroup, two
+// workgroups per CU, x1 straight from global memory into registers) with fp32
+// emulated by TWO fp16 terms instead of three bf16 ones:
+//
+//   v = v0 + v1,  v0 = fp16(v) (RNE), v1 = fp16(v - v0)   (|v - v0 - v1| <= 2^-22 |v|)
+//   a·b ~= a1·b0 + a0·b1 + a0·b0     (three fp16 MFMAs, fp32 accumulation; a1·b1 and
+//                                     the representation residuals are O(2^-22))
+//
+// (the split of Ootomo & Yokota, "Recovering single precision accuracy from Tensor
+// Cores while surpassing the FP32 theoretical peak performance", 2022).  Products of
+// fp16 values are exact in fp32, so the only errors beyond an fp32 GEMM's own
+// accumulation rounding are the O(2^-22) representation terms; measured against
+// fp64 the GEMM error equals that of the fp32-MFMA and x6 engines (DESIGN.md §4,
+// tests/test_gpu_x3h.py).  Half the MFMAs of x6 (the x6 kernels sit at the chip's
+// sustained bf16 MFMA rate: MFMA-busy × clock is the same for every x6 kernel,
+// DESIGN.md §8), two planes instead of three (a third less weight stream and
+// register image).
+//
+// Range: fp16 holds |v| < 65504.  Every weight row is scaled by a power of two so
+// that its largest entry lies in [2^14, 2^15) (exact; undone in fp32 after the
+// contraction: the fc1 rows before bias + GELU, the fc2 rows in the epilogue), so
+// no weight term is subnormal unless it is < 2^-24 of its row's maximum.  The
+// activations (the InstanceNorm output a ⊙ x1 + t, |.| <= sqrt(P) |a| + |t|, and
+// the GELU outputs) are used unscaled; a low term below 2^-14 is subnormal and then
+// carries 2^-24 absolute precision.
+//
+// Slices (24-KB slices of mlp_fused2.hip become 16 KB):
+//   W1(j,kh): hidden rows 32j..+31, channels 128kh..+127: [pl 2][ks 4][t 2][r 16][32]
+//   W2(j,oh): out rows 128oh..+127, hidden block j:       [pl 2][ot 8][r 16][32 (perm)]
+// ring of four 16-KB slots; image = 64 slices, then the row scales (inverse) of W1
+// (512) and W2 (256) as fp32.
+#include "dma.h"
+#include "gemm_common.h"
+#include "kernels.h"
+
+#include <string>
+#include <type_traits>
+
+namespace msfno {
+
+namespace {
+
+typedef _Float16 half8 __attribute__((ext_vector_type(8)));
+typedef _Float16 half2v __attribute__((ext_vector_type(2)));
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+typedef float f2v __attribute__((ext_vector_type(2)));
+
+constexpr int MH_C = 256, MH_H = 512;
+constexpr int MH_WAVES = 4, MH_PX = 16 * MH_WAVES;  // pixels per workgroup tile
+constexpr int MH_HB = MH_H / 32;                    // hidden blocks
+constexpr int MH_PLANE = 4096;                      // fp16 per plane within a slice
+constexpr int MH_SLICE = 2 * MH_PLANE;              // fp16 per 16-KB slice
+constexpr int MH_NS = 4;                            // ring slots
+constexpr int MH_NSLICE = 4 * MH_HB;                // slices per tile
+constexpr int MH_RING_BYTES = MH_NS * MH_SLICE * 2;
+constexpr int MH_LDS = MH_RING_BYTES + 2 * MH_H * 4;  // ring + b1 + 1 / s1
+constexpr int64_t MH_IMG_ELEMS = (int64_t)MH_NSLICE * MH_SLICE;  // before the scales
+
+struct MlpHParams {
+  const float* x1;      // [B][C][P]
+  const float* scale;   // [B][C]  x1 affine (norm1 + FiLM): a
+  const float* shift;   // [B][C]  t
+  const float* resid;   // [B][C][P] or null
+  float* out;           // [B][C][P]
+  const unsigned short* w1img;  // [HB][2 kh] slices
+  const unsigned short* w2img;  // [HB][2 oh] slices
+  const float* inv_s1;  // [H] 1 / (W1 row scale)
+  const float* inv_s2;  // [C] 1 / (W2 row scale)
+  const float* b1;      // [H]
+  const float* b2;      // [C] or null
+  int64_t P;
+  int tiles_per_field;
+};
+
+__host__ __device__ __forceinline__ int mh_swz(int r) { return ((r >> 2) & 1) << 1; }
+
+__host__ __device__ __forceinline__ int mh_perm(int kappa) {
+  const int g = kappa >> 3, e = kappa & 7;
+  return e < 4 ? 4 * g + e : 16 + 4 * g + (e - 4);
+}
+
+// (a, b) -> packed fp16x2 terms h0 + h1 (RNE; v_cvt_pk_f16_f32)
+__device__ __forceinline__ void split2h(float a, float b, uint32_t& t0, uint32_t& t1) {
+  const f2v v = {a, b};
+  const half2v h0 = __builtin_convertvector(v, half2v);
+  const f2v r = v - __builtin_convertvector(h0, f2v);
+  const half2v h1 = __builtin_convertvector(r, half2v);
+  t0 = __builtin_bit_cast(uint32_t, h0);
+  t1 = __builtin_bit_cast(uint32_t, h1);
+}
+
+__device__ __forceinline__ half8 mh_frag(uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
+  return __builtin_bit_cast(half8, make_uint4(a, b, c, d));
+}
+
+// row scales: 2^(15 - e) with max |row| = f 2^e, f in [0.5, 1) -> max scaled in [2^14, 2^15)
+__global__ void mh_scale_kernel(const float* __restrict__ W1, const float* __restrict__ W2,
+                                float* __restrict__ s1, float* __restrict__ s2) {
+  const int r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= MH_H + MH_C) return;
+  const bool first = r < MH_H;
+  const float* row = first ? W1 + (int64_t)r * MH_C : W2 + (int64_t)(r - MH_H) * MH_H;
+  const int n = first ? MH_C : MH_H;
+  float m = 0.f;
+  for (int k = 0; k < n; ++k) m = fmaxf(m, fabsf(row[k]));
+  float sc = 1.f;
+  if (m > 0.f && isfinite(m)) {
+    int e;
+    frexpf(m, &e);
+    sc = ldexpf(1.f, 15 - e);
+  }
+  if (first) s1[r] = sc; else s2[r - MH_H] = sc;
+}
+
+// W1 (H x C fp32) · diag(s1) -> [j][kh][pl][ks][t][r][32]
+__global__ void mh_w1_image_kernel(const float* __restrict__ W1, const float* __restrict__ s1,
+                                   unsigned short* __restrict__ img) {
+  constexpr int64_t PAIRS = (int64_t)MH_HB * 2 * 4 * 2 * 16 * 16;
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < PAIRS;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const int kkp = (int)(e & 15);
+    const int r = (int)((e >> 4) & 15);
+    const int t = (int)((e >> 8) & 1);
+    const int ks = (int)((e >> 9) & 3);
+    const int kh = (int)((e >> 11) & 1);
+    const int j = (int)(e >> 12);
+    const int kk = 2 * kkp;
+    const int g = (kk >> 3) ^ mh_swz(r);
+    const int k = 128 * kh + 32 * ks + 8 * g + (kk & 7);
+    const int row = 32 * j + 16 * t + r;
+    const float* src = W1 + (int64_t)row * MH_C + k;
+    const float sc = s1[row];
+    uint32_t t0, t1;
+    split2h(src[0] * sc, src[1] * sc, t0, t1);
+    uint32_t* o = reinterpret_cast<uint32_t*>(
+        img + (int64_t)(j * 2 + kh) * MH_SLICE + ((ks * 2 + t) * 16 + r) * 32 + kk);
+    o[0] = t0;
+    o[MH_PLANE / 2] = t1;
+  }
+}
+
+// W2 (C x H fp32) · row scales -> [j][oh][pl][ot][r][32], hidden index permuted by mh_perm
+__global__ void mh_w2_image_kernel(const float* __restrict__ W2, const float* __restrict__ s2,
+                                   unsigned short* __restrict__ img) {
+  constexpr int64_t PAIRS = (int64_t)MH_HB * 2 * 8 * 16 * 16;
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < PAIRS;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const int kkp = (int)(e & 15);
+    const int r = (int)((e >> 4) & 15);
+    const int ot = (int)((e >> 8) & 7);
+    const int oh = (int)((e >> 11) & 1);
+    const int j = (int)(e >> 12);
+    const int kk = 2 * kkp;
+    const int kap = 8 * ((kk >> 3) ^ mh_swz(r)) + (kk & 7);
+    const int orow = 128 * oh + 16 * ot + r;
+    const float* row = W2 + (int64_t)orow * MH_H + 32 * j;
+    const float sc = s2[orow];
+    uint32_t t0, t1;
+    split2h(row[mh_perm(kap)] * sc, row[mh_perm(kap + 1)] * sc, t0, t1);
+    uint32_t* o = reinterpret_cast<uint32_t*>(
+        img + (int64_t)(j * 2 + oh) * MH_SLICE + (ot * 16 + r) * 32 + kk);
+    o[0] = t0;
+    o[MH_PLANE / 2] = t1;
+  }
+}
+
+// 1 / scale, in place
+__global__ void mh_invert_kernel(float* __restrict__ s) {
+  const int r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r < MH_H + MH_C) s[r] = 1.f / s[r];
+}
+
+__device__ __forceinline__ const unsigned short* mh_slice_src(const MlpHParams& p, int q) {
+  if (q < 2) return p.w1img + (int64_t)q * MH_SLICE;
+  if (q >= MH_NSLICE - 2)
+    return p.w2img + (int64_t)(2 * (MH_HB - 1) + (q - (MH_NSLICE - 2))) * MH_SLICE;
+  const int j = 1 + ((q - 2) >> 2), r = (q - 2) & 3;
+  return r < 2 ? p.w1img + (int64_t)(2 * j + r) * MH_SLICE
+               : p.w2img + (int64_t)(2 * (j - 1) + (r - 2)) * MH_SLICE;
+}
+
+// four wave-instructions (one m0 save / restore): lane l copies 16 B from sbase +
+// voff[i] to LDS byte lds + i * LDS_STEP + 16 l (dma.h glds16x6, four pieces)
+template <int LDS_STEP>
+__device__ __forceinline__ void glds16x4(uint64_t sbase, const uint32_t (&voff)[4], uint32_t lds) {
+  unsigned keep;
+  sbase = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(sbase >> 32)) << 32) |
+          (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)sbase);
+  lds = (uint32_t)__builtin_amdgcn_readfirstlane((int)lds);
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %6\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %2, %1\n\t"
+      "s_add_u32 m0, m0, %7\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %3, %1\n\t"
+      "s_add_u32 m0, m0, %7\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %4, %1\n\t"
+      "s_add_u32 m0, m0, %7\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %5, %1\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "s"(sbase), "v"(voff[0]), "v"(voff[1]), "v"(voff[2]), "v"(voff[3]), "s"(lds),
+        "i"(LDS_STEP)
+      : "memory", "scc");
+}
+
+template <int AHEAD>
+__global__ __launch_bounds__(256, 2) void mlp_fused_h_kernel(MlpHParams p) {
+  __shared__ __attribute__((aligned(16))) char lds_raw[MH_LDS];
+  unsigned short* const ring = reinterpret_cast<unsigned short*>(lds_raw);
+  float* const b1s = reinterpret_cast<float*>(lds_raw + MH_RING_BYTES);
+  float* const is1s = b1s + MH_H;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int r16 = lane & 15, g = lane >> 4;
+  const int lin = xcd_remap(blockIdx.x, gridDim.x);
+  const int z = lin / p.tiles_per_field;
+  const int64_t P = p.P;
+  const int64_t px = (int64_t)(lin - z * p.tiles_per_field) * MH_PX + 16 * wave + r16;
+  const bool valid = px < P;
+  const int64_t pxc = valid ? px : P - 1;
+
+  // ---- slices 0..3 in flight ---------------------------------------------------------
+  const uint32_t ring_lds = lds_addr(ring);
+  const int wave_u = __builtin_amdgcn_readfirstlane(wave);
+  uint32_t piece_off[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) piece_off[i] = (uint32_t)(i * MH_WAVES * 1024 + lane * 16);
+  auto issue = [&](int q) {
+    const uint64_t src = reinterpret_cast<uint64_t>(mh_slice_src(p, q)) + (uint64_t)wave_u * 1024;
+    const uint32_t base = ring_lds + (uint32_t)((q % MH_NS) * MH_SLICE * 2 + wave_u * 1024);
+    glds16x4<MH_WAVES * 1024>(src, piece_off, base);
+  };
+#pragma unroll
+  for (int q = 0; q < MH_NS; ++q) issue(q);
+
+  // ---- x1 -> normalised fp16x2 B fragments (k-step ks: channels 32 ks + 8 g + 0..7) --
+  const float* xcol = p.x1 + (int64_t)z * MH_C * P + pxc;
+  const float* sc = p.scale + (int64_t)z * MH_C;
+  const float* sh = p.shift + (int64_t)z * MH_C;
+  half8 xf[8][2];
+#pragma unroll
+  for (int ks = 0; ks < 8; ++ks) {
+    const int c0 = 32 * ks + 8 * g;
+    float xv[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) xv[e] = __builtin_nontemporal_load(xcol + (int64_t)(c0 + e) * P);
+    const float4 sa = *reinterpret_cast<const float4*>(sc + c0);
+    const float4 sb = *reinterpret_cast<const float4*>(sc + c0 + 4);
+    const float4 ta = *reinterpret_cast<const float4*>(sh + c0);
+    const float4 tb = *reinterpret_cast<const float4*>(sh + c0 + 4);
+    const float sv[8] = {sa.x, sa.y, sa.z, sa.w, sb.x, sb.y, sb.z, sb.w};
+    const float tv[8] = {ta.x, ta.y, ta.z, ta.w, tb.x, tb.y, tb.z, tb.w};
+    uint32_t t[2][4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+      split2h(fmaf(sv[2 * e], xv[2 * e], tv[2 * e]), fmaf(sv[2 * e + 1], xv[2 * e + 1], tv[2 * e + 1]),
+              t[0][e], t[1][e]);
+#pragma unroll
+    for (int pl = 0; pl < 2; ++pl) xf[ks][pl] = mh_frag(t[pl][0], t[pl][1], t[pl][2], t[pl][3]);
+  }
+  floatx4 oacc[16];
+#pragma unroll
+  for (int ot = 0; ot < 16; ++ot) oacc[ot] = floatx4{0.f, 0.f, 0.f, 0.f};
+  for (int i = tid; i < MH_H; i += 256) {
+    b1s[i] = p.b1[i];
+    is1s[i] = p.inv_s1[i];
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // slices 0-3 and every load landed
+  __syncthreads();
+
+  floatx4 hacc[2][2];  // [parity][tile]
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int t = 0; t < 2; ++t) hacc[a][t] = floatx4{0.f, 0.f, 0.f, 0.f};
+  uint32_t hfu[2][4];  // fc2 B fragment of the converted block [plane][pair]
+
+  const int a_lane = r16 * 32 + 8 * (g ^ mh_swz(r16));
+
+  // step q: slice q landed for every wave (slices q + 1, q + 2 may stay in flight);
+  // the slot of slice q - 1 is free and takes slice q + 3
+  auto step_begin = [&](int q) {
+    const int after = min(2, MH_NSLICE - 1 - q);
+    if (after >= 2)
+      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else if (after == 1)
+      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    return ring + (q % MH_NS) * MH_SLICE;
+  };
+  auto refill = [&](int q) {
+    if (q >= 1 && q + 3 < MH_NSLICE) issue(q + 3);
+  };
+
+  auto mfma3 = [](const half8 (&a)[2], const half8 (&b)[2], floatx4 c) {
+    c = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[1], b[0], c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[0], b[1], c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[0], b[0], c, 0, 0, 0);
+    return c;
+  };
+
+  // pair e2 (0..3) of hidden block j in hacc[PAR]: unscale, + b1, GELU(erf), split -> hfu
+  auto conv_pair = [&](int j, int e2, auto par_c) {
+    constexpr int PAR = decltype(par_c)::value;
+    const int t = e2 >> 1, i = 2 * (e2 & 1);
+    const int row = 32 * j + 16 * t + 4 * g + i;
+    const float2 b = *reinterpret_cast<const float2*>(b1s + row);
+    const float2 is = *reinterpret_cast<const float2*>(is1s + row);
+    f32x2 v = {fmaf(hacc[PAR][t][i], is.x, b.x), fmaf(hacc[PAR][t][i + 1], is.y, b.y)};
+    v = gelu_erf2(v);
+    split2h(v.x, v.y, hfu[0][e2], hfu[1][e2]);
+  };
+
+  auto fc1_step = [&](const unsigned short* slot, int q, auto kh_c, auto par_c, auto conv_c,
+                      int jc) {
+    constexpr int KH = decltype(kh_c)::value, PAR = decltype(par_c)::value;
+    constexpr bool CONV = decltype(conv_c)::value;
+    using PPrev = std::integral_constant<int, PAR ^ 1>;
+    auto aoff = [&](int u, int pl) { return ((pl * 4 + (u >> 1)) * 2 + (u & 1)) * 512 + a_lane; };
+    half8 a[AHEAD + 1][2];
+#pragma unroll
+    for (int k = 0; k < AHEAD; ++k)
+#pragma unroll
+      for (int pl = 0; pl < 2; ++pl) a[k][pl] = *reinterpret_cast<const half8*>(slot + aoff(k, pl));
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      if (u + AHEAD < 8) {
+#pragma unroll
+        for (int pl = 0; pl < 2; ++pl)
+          a[(u + AHEAD) % (AHEAD + 1)][pl] = *reinterpret_cast<const half8*>(slot + aoff(u + AHEAD, pl));
+      }
+      hacc[PAR][u & 1] = mfma3(a[u % (AHEAD + 1)], xf[KH * 4 + (u >> 1)], hacc[PAR][u & 1]);
+      if (u == 0) refill(q);
+      if constexpr (CONV) {
+        if (u == 2 || u == 6) conv_pair(jc, 2 * KH + (u >> 2), PPrev{});
+      }
+    }
+    if constexpr (CONV && KH == 1) {
+#pragma unroll
+      for (int t = 0; t < 2; ++t) hacc[PAR ^ 1][t] = floatx4{0.f, 0.f, 0.f, 0.f};
+    }
+  };
+  auto fc2_step = [&](const unsigned short* slot, int q, auto oh_c) {
+    constexpr int OH = decltype(oh_c)::value;
+    auto aoff = [&](int u, int pl) { return (pl * 8 + u) * 512 + a_lane; };
+    const half8 hb[2] = {mh_frag(hfu[0][0], hfu[0][1], hfu[0][2], hfu[0][3]),
+                         mh_frag(hfu[1][0], hfu[1][1], hfu[1][2], hfu[1][3])};
+    half8 a[AHEAD + 1][2];
+#pragma unroll
+    for (int k = 0; k < AHEAD; ++k)
+#pragma unroll
+      for (int pl = 0; pl < 2; ++pl) a[k][pl] = *reinterpret_cast<const half8*>(slot + aoff(k, pl));
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      if (u + AHEAD < 8) {
+#pragma unroll
+        for (int pl = 0; pl < 2; ++pl)
+          a[(u + AHEAD) % (AHEAD + 1)][pl] = *reinterpret_cast<const half8*>(slot + aoff(u + AHEAD, pl));
+      }
+      oacc[OH * 8 + u] = mfma3(a[u % (AHEAD + 1)], hb, oacc[OH * 8 + u]);
+      if (u == 0) refill(q);
+    }
+  };
+
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+  using F = std::false_type;
+  using T = std::true_type;
+  auto do_round = [&](int j, auto par_c) {
+    const int q = 2 + 4 * (j - 1);
+    fc1_step(step_begin(q), q, I0{}, par_c, T{}, j - 1);
+    fc1_step(step_begin(q + 1), q + 1, I1{}, par_c, T{}, j - 1);
+    fc2_step(step_begin(q + 2), q + 2, I0{});
+    fc2_step(step_begin(q + 3), q + 3, I1{});
+  };
+  fc1_step(step_begin(0), 0, I0{}, I0{}, F{}, 0);
+  fc1_step(step_begin(1), 1, I1{}, I0{}, F{}, 0);
+  for (int j = 1; j < MH_HB; j += 2) {
+    do_round(j, I1{});
+    if (j + 1 < MH_HB) do_round(j + 1, I0{});
+  }
+#pragma unroll
+  for (int e2 = 0; e2 < 4; ++e2) conv_pair(MH_HB - 1, e2, I1{});
+  fc2_step(step_begin(MH_NSLICE - 2), MH_NSLICE - 2, I0{});
+  fc2_step(step_begin(MH_NSLICE - 1), MH_NSLICE - 1, I1{});
+
+  // ---- epilogue: unscale + b2 + residual, store (rows 16 ot + 4 g + i) ----------------
+  if (valid) {
+    float* o = p.out + (int64_t)z * MH_C * P + px;
+    const float* rs = p.resid ? p.resid + (int64_t)z * MH_C * P + px : nullptr;
+#pragma unroll
+    for (int ot = 0; ot < 16; ++ot) {
+      const int r0 = 16 * ot + 4 * g;
+      const float4 is = *reinterpret_cast<const float4*>(p.inv_s2 + r0);
+      float4 b = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (p.b2) b = *reinterpret_cast<const float4*>(p.b2 + r0);
+      const float isv[4] = {is.x, is.y, is.z, is.w}, bv[4] = {b.x, b.y, b.z, b.w};
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        float v = fmaf(oacc[ot][i], isv[i], bv[i]);
+        if (rs) v += __builtin_nontemporal_load(rs + (int64_t)(r0 + i) * P);
+        o[(int64_t)(r0 + i) * P] = v;
+      }
+    }
+  }
+}
+
+}  // namespace
+
+bool mlp_fused_h_env() {
+  static const bool on = [] {
+    const char* e = getenv("MSFNO_ENGINE");
+    return e && std::string(e) == "x3h";
+  }();
+  return on;
+}
+
+size_t mlp_fused_h_image_bytes() {
+  return (size_t)MH_IMG_ELEMS * 2 + (size_t)(MH_H + MH_C) * 4;
+}
+
+int launch_mlp_fused_h_images(const float* W1, const float* W2, unsigned short* img, hipStream_t s) {
+  float* sc = reinterpret_cast<float*>(img + MH_IMG_ELEMS);
+  hipLaunchKernelGGL(mh_scale_kernel, dim3((MH_H + MH_C + 255) / 256), dim3(256), 0, s, W1, W2, sc,
+                     sc + MH_H);
+  MSFNO_TRY(launch_check("mh_scale"));
+  hipLaunchKernelGGL(mh_w1_image_kernel, dim3(256), dim3(256), 0, s, W1, sc, img);
+  MSFNO_TRY(launch_check("mh_w1_image"));
+  hipLaunchKernelGGL(mh_w2_image_kernel, dim3(256), dim3(256), 0, s, W2, sc + MH_H,
+                     img + (int64_t)MH_HB * 2 * MH_SLICE);
+  MSFNO_TRY(launch_check("mh_w2_image"));
+  hipLaunchKernelGGL(mh_invert_kernel, dim3((MH_H + MH_C + 255) / 256), dim3(256), 0, s, sc);
+  return launch_check("mh_invert");
+}
+
+int launch_mlp_fused_h(const float* x1, const float* scale, const float* shift, const float* resid,
+                       float* out, const unsigned short* img, const float* b1, const float* b2,
+                       int B, int64_t P, hipStream_t s) {
+  MSFNO_REQUIRE(x1 && scale && shift && out && img && b1 && B > 0 && P >= 1, MSFNO_EINVAL,
+                "mlp_fused_h: bad arguments");
+  MlpHParams p{};
+  p.x1 = x1; p.scale = scale; p.shift = shift; p.resid = resid; p.out = out;
+  p.w1img = img;
+  p.w2img = img + (int64_t)MH_HB * 2 * MH_SLICE;
+  const float* sc = reinterpret_cast<const float*>(img + MH_IMG_ELEMS);
+  p.inv_s1 = sc;
+  p.inv_s2 = sc + MH_H;
+  p.b1 = b1; p.b2 = b2; p.P = P;
+  p.tiles_per_field = (int)cdiv(P, MH_PX);
+  const int64_t tiles = (int64_t)B * p.tiles_per_field;
+  MSFNO_REQUIRE(tiles < (1LL << 31), MSFNO_EINVAL, "mlp_fused_h: grid too large");
+  hipLaunchKernelGGL((mlp_fused_h_kernel<2>), dim3((unsigned)tiles), dim3(256), 0, s, p);
+  return launch_check("mlp_fused_h");
+}
+
+}  // namespace msfno

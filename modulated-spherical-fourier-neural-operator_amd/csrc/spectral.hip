@@ -274,6 +274,62 @@ __global__ __launch_bounds__(256) void transpose_fwd_sym2_kernel(
   }
 }
 
+// Vector-store variant: the fold + affine in registers on the load side (8-B loads of
+// the north and mirror rows), the four slab rows of one m (Xs re / im, Xa re / im)
+// as LDS rows of TKx floats, stored as 16-B vectors (a 64-lane instruction writes
+// four 256-B row segments; the scalar-store kernels above write one).  Whole float4
+// units up to round4(end of the valid k range) are written, zeros past it (pads).
+template <int TKx, int TMx>
+__global__ __launch_bounds__(256) void transpose_fwd_sym4_kernel(
+    const float2* __restrict__ Xn, float* __restrict__ Xt, int B, int C, LatGeom g, int mmax,
+    const float* __restrict__ nscale, const float* __restrict__ nshift,
+    const int* __restrict__ slab, int kpad) {
+  constexpr int LD = TKx + 4;  // 16-B aligned LDS rows
+  constexpr int KV = TKx / 4;  // float4 units per row
+  __shared__ __attribute__((aligned(16))) float tile[4 * TMx * LD];  // [h][c][m][k]
+  const int k0 = blockIdx.x * TKx, m0 = blockIdx.y * TMx;
+  const int bc = blockIdx.z;
+  const int b = bc / C, c = bc - b * C;
+  const float2* src = Xn + (int64_t)bc * g.nlat * mmax;
+  const float sc = nscale ? nscale[bc] : 1.f;
+  const float sh = nshift ? nshift[bc] * kTwoPi : 0.f;
+  for (int i = threadIdx.x; i < TKx * TMx; i += 256) {
+    const int kk = i / TMx, mm = i - kk * TMx;
+    const int k = k0 + kk, m = m0 + mm;
+    float2 n = make_float2(0.f, 0.f), t = n;
+    if (k < g.Ke && m < mmax) {
+      n = src[(int64_t)k * mmax + m];
+      if (k < g.nh) t = src[(int64_t)(g.nlat - 1 - k) * mmax + m];
+    }
+    const bool pair = k < g.nh;
+    const float shm = (m == 0) ? sh : 0.f;
+    // affine per row, then fold: s(N + S) + 2t  /  s(N - S); zeros past Ke / nh
+    const float sre = pair ? fmaf(sc, n.x + t.x, 2.f * shm) : (k < g.Ke ? fmaf(sc, n.x, shm) : 0.f);
+    const float sim = pair ? sc * (n.y + t.y) : sc * n.y;
+    tile[(0 * TMx + mm) * LD + kk] = sre;
+    tile[(1 * TMx + mm) * LD + kk] = sim;
+    tile[(2 * TMx + mm) * LD + kk] = pair ? sc * (n.x - t.x) : 0.f;
+    tile[(3 * TMx + mm) * LD + kk] = pair ? sc * (n.y - t.y) : 0.f;
+  }
+  __syncthreads();
+  const int64_t R = 2LL * B * C;
+  const int kend = max(g.Ke, kpad);
+  const int kend_a = kpad > 0 ? kend : g.nh;
+  for (int i = threadIdx.x; i < 4 * TMx * KV; i += 256) {
+    const int row = i / KV, kv = i - row * KV;
+    const int hc = row / TMx, mm = row - hc * TMx;
+    const int h = hc >> 1, ri = hc & 1;
+    const int k = k0 + 4 * kv, m = m0 + mm;
+    if (m >= mmax || k >= (h ? kend_a : kend)) continue;
+    const int sl = slab ? slab[m] : m;
+    if (sl < 0) continue;
+    const float4 v = *reinterpret_cast<const float4*>(tile + row * LD + 4 * kv);
+    float* dst = Xt + (int64_t)sl * R * g.ldk + ((int64_t)(b * 2 + ri) * C + c) * g.ldk +
+                 (h ? g.ldke : 0) + k;
+    *reinterpret_cast<float4*>(dst) = v;
+  }
+}
+
 template <int TKx, int TMx>
 __global__ __launch_bounds__(256) void transpose_inv_sym2_kernel(const float* __restrict__ Yt,
                                                                  float2* __restrict__ Yn, int B,
@@ -341,7 +397,7 @@ static int tr_tile(const char* var, int dflt) {
   if (!e) return dflt;
   const std::string v(e);
   return v == "64x32" ? 0 : v == "32x64" ? 1 : v == "32x128" ? 2 : v == "16x128" ? 3
-         : v == "2p" ? 4 : dflt;
+         : v == "2p" ? 4 : v == "v4" ? 5 : dflt;
 }
 
 template <int TKx, int TMx>
@@ -366,6 +422,13 @@ static void fwd_sym_dispatch(const float2* Xn, float* Xt, int B, int C, const La
       dim3 grid((unsigned)cdiv(std::max(g.Ke, kpad), 32), (unsigned)cdiv(mmax, 128),
                 (unsigned)(B * C));
       hipLaunchKernelGGL((transpose_fwd_sym2_kernel<32, 128>), grid, dim3(256), 0, s, Xn, Xt, B,
+                         C, g, mmax, nscale, nshift, perm, kpad);
+      break;
+    }
+    case 5: {
+      dim3 grid((unsigned)cdiv(std::max(g.Ke, kpad), 64), (unsigned)cdiv(mmax, 32),
+                (unsigned)(B * C));
+      hipLaunchKernelGGL((transpose_fwd_sym4_kernel<64, 32>), grid, dim3(256), 0, s, Xn, Xt, B,
                          C, g, mmax, nscale, nshift, perm, kpad);
       break;
     }
