@@ -636,6 +636,7 @@ void carve_block(Carve& cv, BlockBufs& b, const msfno_block_desc* d,
   b.sh0 = cv.take<float>(BC);
   b.Sa = cv.take<float>(R * L.ldT);
   b.Sb = b.Sc = nullptr;
+  b.cs = nullptr;
   for (auto& w : b.Wexp) w = nullptr;
   b.dw = DenseWs{};
   b.xt = b.yt = nullptr;
@@ -643,6 +644,7 @@ void carve_block(Carve& cv, BlockBufs& b, const msfno_block_desc* d,
     const int64_t Hs = d->spec_hidden;
     b.Sb = cv.take<float>(spec_hidden_floats(B, Hs, L));
     b.Sc = cv.take<float>(spec_hidden_floats(B, Hs, L));
+    b.cs = cv.take<float>(2LL * B * round_up(L.Tp, 4));
     for (int l = 0; l <= d->spectral_layers; ++l) {
       const int64_t ci = (l == 0) ? C : Hs;
       const int64_t co = (l == d->spectral_layers) ? C : Hs;

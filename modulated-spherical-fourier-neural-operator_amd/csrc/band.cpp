@@ -160,6 +160,7 @@ void carve_band(Carve& cv, BandBufs& b, const msfno_block_desc* d, const msfno_b
     const int64_t Hs = d->spec_hidden;
     b.fb.Sb = cv.take<float>(spec_hidden_floats(B, Hs, L));
     b.fb.Sc = cv.take<float>(spec_hidden_floats(B, Hs, L));
+    b.fb.cs = cv.take<float>(2LL * B * round_up(L.Tp, 4));
     for (int l = 0; l <= d->spectral_layers && l < 9; ++l) {
       const int64_t ci = (l == 0) ? C : Hs;
       const int64_t co = (l == d->spectral_layers) ? C : Hs;

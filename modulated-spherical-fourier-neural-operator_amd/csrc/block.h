@@ -57,6 +57,7 @@ struct BlockBufs {
   unsigned short* Xtp;  // x6 Legendre: forward slabs as bf16x3 planes, else null
   unsigned short* Sp;   // x6 Legendre: filter output S as planes [plane][R][ldT]
   unsigned short* mfimg;  // fused MLP weight image (mlp_fused), else null
+  float* cs;  // x3h spectral MLP: per-(b, column) input scale and its inverse [2][B][ld]
   DenseWs dw;
 };
 

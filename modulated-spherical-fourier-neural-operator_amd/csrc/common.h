@@ -154,7 +154,8 @@ struct GemmEpi {
 
 enum GemmTile {
   TILE_128x128 = 0, TILE_128x64 = 1, TILE_64x64 = 2, TILE_256x64 = 3, TILE_256x128 = 4,
-  TILE_128x256 = 5, TILE_256x256 = 6  // 256x256: gemm_x6 only
+  TILE_128x256 = 5, TILE_256x256 = 6,  // 256x256: gemm_x6 only
+  TILE_256x32 = 7, TILE_128x32 = 8      // fp32 descriptor (Legendre) GEMMs only
 };
 // GEMM role -> tile (defaults chosen by measurement); MSFNO_TILES
 // ("skip=4,fc1=1,...", values = GemmTile) overrides them for A/B experiments
@@ -199,6 +200,9 @@ struct SpecWeightsX6p {
   int ci[9], co[9];
   int64_t start[10];  // pair offsets of each layer in the flattened index space
   int nlayers;
+  // x3h 3M images (gemm_x6c.hip, NP = 2): per layer {weight scale tau, epilogue
+  // multiplier} (2 floats per layer, device; spec_scales_x3h_kernel)
+  float* scl = nullptr;
 };
 size_t spec_weights_x6p_layout(SpecWeightsX6p& a);
 int launch_spec_weights_x6p(const SpecWeightsX6p& a, hipStream_t s);
@@ -224,6 +228,20 @@ int gemm_x6c_f32t(const unsigned short* Aw, int co, int ci, const float* Sin, in
                   hipStream_t s);
 int gemm_x6c(const unsigned short* Aw, int co, int ci, const unsigned short* X, int N, int ldx,
              unsigned short* Y, float* S, int ldS, bool relu, int B, hipStream_t s, int lay = 0);
+// the same chain on the x3h engine (two fp16 terms, three MFMAs per product; tiled
+// hidden activations of 6 planes).  Scaling (all powers of two): the weights of layer
+// l by a.scl[2l] (spec_scales_x3h_kernel), layer 0's input column (b, n) by
+// cs[b * ldcs + n] (launch_spec_colscale: its max |Re|, |Im| into [2^13, 2^14)),
+// the hidden layers' outputs by a.scl[2l + 1]; the output layer undoes everything
+// (a.scl[2L + 1] and the inverse column scales cs[B * ldcs + ...]).
+int launch_spec_weights_3m_x3h(const SpecWeightsX6p& a, hipStream_t s);
+int launch_spec_colscale(const float* S, int B, int C, int N, int ldS, float* cs, int ldcs,
+                         hipStream_t s);
+int64_t x3c_tiled_elems(int rows, int N);
+int gemm_x3c(const unsigned short* Aw, int co, int ci, const float* Sin, int ldSin,
+             const unsigned short* X, int N, unsigned short* Y, float* Sout, int ldSout,
+             bool relu, const float* lscale, const float* colscale, int64_t cs_b, int B,
+             hipStream_t s);
 // fp32 x[z][r][c] (ld ldx, batch stride sx) -> bf16x3 planes xp[z][plane][r][c]
 int launch_split_planes(const float* x, unsigned short* xp, int rows, int cols, int ldx,
                         int64_t sx, int ldp, int64_t pstride, int64_t sxp, int batch,

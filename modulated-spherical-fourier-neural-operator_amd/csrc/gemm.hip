@@ -14,19 +14,24 @@
 
 namespace msfno {
 
-template <int BM, int BN, int BK, bool VEC, int EPI>
+// WGM x (4 / WGM) waves: 2 x 2 (default) or 4 x 1 (the 32-column tiles: ragged
+// narrow Legendre problems waste less padding)
+template <int BM, int BN, int BK, bool VEC, int EPI, int WGM = 2>
 __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmParams p) {
-  constexpr int WM = BM / 2, WN = BN / 2;
+  constexpr int WGN = 4 / WGM;
+  constexpr int WM = BM / WGM, WN = BN / WGN;
   constexpr int MT = WM / 32, NT = WN / 32;
   constexpr int LDA_S = BM + 2;  // staging-write conflict-free (see header)
   constexpr int LDB_S = BN;
   constexpr int A_LD = BM * BK / 1024;  // float4 staging loads per thread
-  constexpr int B_LD = BN * BK / 1024;
+  constexpr int B_LD = (BN * BK + 1023) / 1024;
+  constexpr int B_N4 = BN * BK / 4;  // float4 of a B tile (< 256 for BN = 32: some threads idle)
   // one LDS array: the double-buffered A/B staging, reused by the epilogue as a
   // 64-row x (BN + 8) row-major image of the accumulators
   constexpr int CS_LD = BN + 8;
   constexpr int STAGE = 2 * BK * LDA_S + 2 * BK * LDB_S;
-  constexpr int LDS_FLOATS = STAGE > 64 * CS_LD ? STAGE : 64 * CS_LD;
+  constexpr int EPI_FLOATS = 32 * WGM * CS_LD;  // gemm_epilogue's row-tile image
+  constexpr int LDS_FLOATS = STAGE > EPI_FLOATS ? STAGE : EPI_FLOATS;
   // + the tile's BM bias values, staged once: read from global inside the
   // epilogue they were serialised behind the C stores (possible aliasing),
   // one L2 round trip per float4 stored
@@ -39,7 +44,7 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmParams p) {
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = tid >> 6;
-  const int wm = wave >> 1, wn = wave & 1;
+  const int wm = wave / WGN, wn = wave % WGN;
 
   // ---- tile -> problem mapping ----------------------------------------------
   const float* A = p.A;
@@ -113,6 +118,7 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmParams p) {
 #pragma unroll
     for (int q = 0; q < B_LD; ++q) {
       const int idx = tid + 256 * q;
+      if (B_N4 % 256 != 0 && idx >= B_N4) continue;  // wave-uniform (B_N4 = 128)
       const int kr = min(k0 + idx / (BN / 4), Kc);
       const int col = n0 + (idx % (BN / 4)) * 4;
       const float* src = B + (int64_t)kr * ldb;
@@ -145,6 +151,7 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmParams p) {
 #pragma unroll
     for (int q = 0; q < B_LD; ++q) {
       const int idx = tid + 256 * q;
+      if (B_N4 % 256 != 0 && idx >= B_N4) continue;
       const int kr = idx / (BN / 4);
       const int col = (idx % (BN / 4)) * 4;
       const bool kok = k0 + kr < K;
@@ -250,7 +257,7 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmParams p) {
     }
   }
 
-  gemm_epilogue<BM, BN, EPI>(p, acc, lds, bias_s, C, addend, M, N, ldc, m0, n0, dflags);
+  gemm_epilogue<BM, BN, EPI, WGM, WGN>(p, acc, lds, bias_s, C, addend, M, N, ldc, m0, n0, dflags);
 }
 
 GemmTile role_tile(GemmRole r, GemmTile dflt) {
@@ -276,7 +283,7 @@ GemmTile role_tile(GemmRole r, GemmTile dflt) {
     init = true;
   }
   const int t = table[r];
-  return (t >= 0 && t <= TILE_256x256) ? (GemmTile)t : dflt;
+  return (t >= 0 && t <= TILE_128x32) ? (GemmTile)t : dflt;
 }
 
 void gemm_tile_dims(GemmTile tile, int* bm, int* bn) {
@@ -287,6 +294,8 @@ void gemm_tile_dims(GemmTile tile, int* bm, int* bn) {
     case TILE_256x128: *bm = 256; *bn = 128; break;
     case TILE_128x256: *bm = 128; *bn = 256; break;
     case TILE_256x256: *bm = 256; *bn = 256; break;
+    case TILE_256x32: *bm = 256; *bn = 32; break;
+    case TILE_128x32: *bm = 128; *bn = 32; break;
     default: *bm = 64; *bn = 64; break;
   }
 }
@@ -304,18 +313,34 @@ static GemmParams make_params(const float* A, const float* B, float* C, const Ge
   return p;
 }
 
-template <int BM, int BN, int BK, int EPI>
+template <int BM, int BN, int BK, int EPI, int WGM = 2>
 static void launch_e(const GemmParams& p, dim3 grid, hipStream_t s) {
   if (p.vecA && p.vecB)
-    hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, BK, true, EPI>), grid, dim3(256), 0, s, p);
+    hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, BK, true, EPI, WGM>), grid, dim3(256), 0, s, p);
   else
-    hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, BK, false, EPI>), grid, dim3(256), 0, s, p);
+    hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, BK, false, EPI, WGM>), grid, dim3(256), 0, s, p);
 }
+
+
 
 static int epi_code(const GemmParams& p) {
   return (p.bias ? EPI_BIAS : 0) | (p.addend ? EPI_ADD : 0) | (p.act == 1 ? EPI_GELU : 0) |
          (p.relu_period ? EPI_RELU : 0) |
          (p.rowscale ? EPI_ROWSCALE : 0) | (p.act == 2 ? EPI_GELU_B : 0);
+}
+
+// the 32-column tiles (4 x 1 waves): the Legendre descriptor GEMMs only (no epilogue
+// or the forward row scale)
+template <int BM, int BN, int BK>
+static int launch_narrow(const GemmParams& p, dim3 grid, hipStream_t s) {
+  switch (epi_code(p)) {
+    case 0: launch_e<BM, BN, BK, 0, 4>(p, grid, s); break;
+    case EPI_ROWSCALE: launch_e<BM, BN, BK, EPI_ROWSCALE, 4>(p, grid, s); break;
+    default:
+      set_error("gemm: 32-column tiles take no epilogue");
+      return MSFNO_EUNSUPPORTED;
+  }
+  return MSFNO_OK;
 }
 
 // the epilogue combinations the block uses (anything else is rejected)
@@ -353,6 +378,8 @@ static int dispatch(GemmTile tile, const GemmParams& p, dim3 grid, hipStream_t s
     case TILE_256x64: rc = launch<256, 64, MSFNO_GEMM_BK>(p, grid, s); break;
     case TILE_256x128: rc = launch<256, 128, MSFNO_GEMM_BK>(p, grid, s); break;
     case TILE_128x256: rc = launch<128, 256, MSFNO_GEMM_BK>(p, grid, s); break;
+    case TILE_256x32: rc = launch_narrow<256, 32, MSFNO_GEMM_BK>(p, grid, s); break;
+    case TILE_128x32: rc = launch_narrow<128, 32, MSFNO_GEMM_BK>(p, grid, s); break;
     default: rc = launch<64, 64, MSFNO_GEMM_BK>(p, grid, s); break;
   }
   if (rc != MSFNO_OK) return rc;

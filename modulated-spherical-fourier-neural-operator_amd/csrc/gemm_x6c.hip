@@ -27,8 +27,49 @@
 namespace msfno {
 
 typedef __bf16 bf16x8c __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x8c __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x2c __attribute__((ext_vector_type(2)));
+typedef float f32x2c __attribute__((ext_vector_type(2)));
 typedef short s16x4c __attribute__((ext_vector_type(4)));
 typedef short s16x8c __attribute__((ext_vector_type(8)));
+
+// NP planes per value: 3 = the x6 engine (bf16 terms, six MFMAs per product), 2 = the
+// x3h engine (fp16 terms, three MFMAs; operands power-of-two scaled into fp16 range,
+// see the scale arrays of X6CParams and spec_scales_x3h_kernel)
+template <int NP>
+struct X6CEng;
+template <>
+struct X6CEng<3> {
+  typedef bf16x8c frag;
+  __device__ static void split(float a, float b, uint32_t (&t)[3]) { split2(a, b, t[0], t[1], t[2]); }
+  __device__ static floatx16 prod(const frag (&a)[3], const frag (&b)[3], floatx16 c) {
+    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2], b[0], c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[1], c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[2], c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[0], c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[1], c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[0], c, 0, 0, 0);
+    return c;
+  }
+};
+template <>
+struct X6CEng<2> {
+  typedef f16x8c frag;
+  __device__ static void split(float a, float b, uint32_t (&t)[2]) {
+    const f32x2c v = {a, b};
+    const f16x2c h0 = __builtin_convertvector(v, f16x2c);
+    const f32x2c r = v - __builtin_convertvector(h0, f32x2c);
+    const f16x2c h1 = __builtin_convertvector(r, f16x2c);
+    t[0] = __builtin_bit_cast(uint32_t, h0);
+    t[1] = __builtin_bit_cast(uint32_t, h1);
+  }
+  __device__ static floatx16 prod(const frag (&a)[2], const frag (&b)[2], floatx16 c) {
+    c = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[1], b[0], c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[0], b[1], c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[0], b[0], c, 0, 0, 0);
+    return c;
+  }
+};
 
 constexpr int X6C_BM = 128, X6C_BN = 128, X6C_BK = 16;
 
@@ -56,6 +97,13 @@ struct X6CParams {
   // LAY (tiled activations): k-tiles per column tile of the planes input / output
   // (round_up(rows, 128) / 16 of the producing layer)
   int kt_in, kt_out;
+  // x3h (NP = 2) scaling, all powers of two: *lscale multiplies the accumulators
+  // before the epilogue (layer constant: weight scale undone, output range set);
+  // colscale[b * cs_b + column] multiplies the fp32 B values while staged (BF32 layer
+  // 0: the per-column input scale) or the outputs in the epilogue (output layer)
+  const float* lscale;
+  const float* colscale;
+  int64_t cs_b;
 };
 
 // Tiled 3M activations (LAY, MSFNO_X6C_TILED): the planes of a layer's activation
@@ -68,8 +116,64 @@ __device__ __forceinline__ int x6c_tile_swz(int r, int c) {
   return ((((c >> 3) ^ (4 * (r & 3)))) << 3) + (c & 7);
 }
 
+// x3h scales of the spectral MLP (one workgroup): per layer l a weight scale
+// tau_l = 2^(15 - e) for the largest of |Wr|, |Wi|, |Wr + Wi| (= f 2^e, f in
+// [0.5, 1)), and the row bound nu_l = max_o sum_i (|Wr| + |Wi|): a layer whose
+// inputs are bounded by 2^14 in absolute value (re and im) has outputs bounded by
+// nu_l 2^14, which sigma_l = 2^-ceil(log2 nu_l) brings back under 2^14 (so the next
+// B operand Xr + Xi stays under 2^15 < 65504).  The hidden layers' epilogue
+// multiplier is sigma_l / tau_l; the output layer's 1 / (tau_L prod sigma_l) (the
+// per-column input scale of layer 0 is undone separately).  scl[2 l] = tau_l,
+// scl[2 l + 1] = the multiplier.
+__global__ void spec_scales_x3h_kernel(SpecWeightsX6p a) {
+  __shared__ float red_m[256], red_n[256];
+  float prod_sigma = 1.f;
+  for (int l = 0; l < a.nlayers; ++l) {
+    const int ci = a.ci[l], co = a.co[l];
+    float m = 0.f, nu = 0.f;
+    for (int o = threadIdx.x; o < co; o += blockDim.x) {
+      float rsum = 0.f;
+      for (int i = 0; i < ci; ++i) {
+        const float wr = a.w[l][((int64_t)i * co + o) * 2], wi = a.w[l][((int64_t)i * co + o) * 2 + 1];
+        m = fmaxf(m, fmaxf(fmaxf(fabsf(wr), fabsf(wi)), fabsf(wr + wi)));
+        rsum += fabsf(wr) + fabsf(wi);
+      }
+      nu = fmaxf(nu, rsum);
+    }
+    red_m[threadIdx.x] = m;
+    red_n[threadIdx.x] = nu;
+    __syncthreads();
+    for (int s = blockDim.x / 2; s > 0; s >>= 1) {
+      if ((int)threadIdx.x < s) {
+        red_m[threadIdx.x] = fmaxf(red_m[threadIdx.x], red_m[threadIdx.x + s]);
+        red_n[threadIdx.x] = fmaxf(red_n[threadIdx.x], red_n[threadIdx.x + s]);
+      }
+      __syncthreads();
+    }
+    m = red_m[0];
+    nu = red_n[0];
+    __syncthreads();
+    int e = 0;
+    float tau = 1.f;
+    if (m > 0.f && isfinite(m)) {
+      frexpf(m, &e);
+      tau = ldexpf(1.f, 15 - e);
+    }
+    float sigma = 1.f;
+    if (nu > 0.f && isfinite(nu)) sigma = ldexpf(1.f, -(int)ceilf(log2f(nu)));
+    const bool last = l == a.nlayers - 1;
+    if (threadIdx.x == 0) {
+      a.scl[2 * l] = tau;
+      a.scl[2 * l + 1] = last ? 1.f / (tau * prod_sigma) : sigma / tau;
+    }
+    prod_sigma *= sigma;
+  }
+}
+
 // A image of one layer: Wr, Wi, Ws = Wr + Wi (co x ci each) from the reference
-// weight w (ci, co, 2), each split into [plane][kt][Mp][16]
+// weight w (ci, co, 2), each split into [plane][kt][Mp][16]; NP = 2: scaled by
+// tau_l (a.scl) and split into two fp16 terms
+template <int NP = 3>
 __global__ void spec_weights_3m_kernel(SpecWeightsX6p a) {
   const int64_t total = a.start[a.nlayers];
   for (int64_t g = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; g < total;
@@ -86,6 +190,7 @@ __global__ void spec_weights_3m_kernel(SpecWeightsX6p a) {
     const int kt = (int)(idx / ((int64_t)Mp * 16));
     const int rem = (int)(idx - (int64_t)kt * Mp * 16);
     const int o = rem >> 4, k0 = kt * 16 + (rem & 15);
+    const float tau = NP == 2 ? a.scl[2 * l] : 1.f;
     float v[2];
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
@@ -95,14 +200,13 @@ __global__ void spec_weights_3m_kernel(SpecWeightsX6p a) {
         const float wr = a.w[l][((int64_t)i * co + o) * 2], wi = a.w[l][((int64_t)i * co + o) * 2 + 1];
         x = mat == 0 ? wr : (mat == 1 ? wi : wr + wi);
       }
-      v[t] = x;
+      v[t] = x * tau;
     }
-    uint32_t t0, t1, t2;
-    split2(v[0], v[1], t0, t1, t2);
-    uint32_t* out = reinterpret_cast<uint32_t*>(a.out[l]) + mat * 3 * n + f;
-    out[0] = t0;
-    out[n] = t1;
-    out[2 * n] = t2;
+    uint32_t t[NP];
+    X6CEng<NP>::split(v[0], v[1], t);
+    uint32_t* out = reinterpret_cast<uint32_t*>(a.out[l]) + mat * NP * n + f;
+#pragma unroll
+    for (int pl = 0; pl < NP; ++pl) out[pl * n] = t[pl];
   }
 }
 
@@ -197,21 +301,27 @@ __global__ void split3m_kernel(const float* __restrict__ S, unsigned short* __re
 // DBG (diagnostic timing builds only, wrong results; MSFNO_X6C_DBG): 1 no vmcnt wait
 // for the k-tile DMA, 2 no DMA in the loop at all (stale stages), 4 no MFMAs
 // LAY: bit 1 = B planes read in the tiled layout, bit 2 = planes written tiled
-template <bool PLANES_OUT, int WGM = 4, int WGN = 2, bool BF32 = false, int DBG = 0, int LAY = 0>
+template <bool PLANES_OUT, int WGM = 4, int WGN = 2, bool BF32 = false, int DBG = 0, int LAY = 0,
+          int NP = 3>
 __global__ __launch_bounds__(64 * WGM * WGN) void gemm_x6c_kernel(X6CParams p) {
   constexpr int BM = X6C_BM, BN = X6C_BN, BK = X6C_BK;
   constexpr int NW = WGM * WGN;
-  constexpr int NPC = BF32 ? (36 + NW - 1) / NW : 72 / NW;  // 1-KB DMA pieces per wave and k-tile
+  constexpr int NMP = 3 * NP;                 // matrix-planes per operand
+  constexpr int APC = 4 * NMP;                // A pieces (1 KB) per k-tile
+  constexpr int NPC = BF32 ? (APC + NW - 1) / NW : 2 * APC / NW;  // DMA pieces per wave and k-tile
   constexpr int WM = BM / WGM, WN = BN / WGN;
   constexpr int MT = WM / 32, NT = WN / 32;
-  constexpr int A_PLANE = BM * BK, B_PLANE = BK * BN;  // bf16 elements per matrix plane
-  constexpr int A_ALL = 9 * A_PLANE;
-  constexpr int STAGE = 9 * (A_PLANE + B_PLANE);        // 72 KB
+  constexpr int A_PLANE = BM * BK, B_PLANE = BK * BN;  // 16-bit elements per matrix plane
+  constexpr int A_ALL = NMP * A_PLANE;
+  constexpr int STAGE = NMP * (A_PLANE + B_PLANE);      // 72 KB (x6) / 48 KB (x3h)
   constexpr int NSTAGE = 2;
   constexpr int RING_BYTES = NSTAGE * STAGE * 2;
   constexpr int EPI_BYTES = 32 * WGM * (BN + 8) * 4;
   constexpr int LDS_BYTES = RING_BYTES > EPI_BYTES ? RING_BYTES : EPI_BYTES;
-  static_assert(STAGE * 2 == 72 * 1024, "stage = 72 pieces of 1 KB");
+  static_assert(STAGE * 2 == 2 * APC * 1024, "stage = A + B pieces of 1 KB");
+  // the x3h engine writes hidden planes in the tiled layout only
+  static_assert(NP == 3 || !PLANES_OUT || (LAY & 2) != 0, "x3h: tiled plane output only");
+  typedef typename X6CEng<NP>::frag Frag;
   __shared__ __attribute__((aligned(16))) char lds_raw[LDS_BYTES];
   unsigned short* const ring = reinterpret_cast<unsigned short*>(lds_raw);
 
@@ -229,34 +339,34 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_x6c_kernel(X6CParams p) {
   const int nk = (K + BK - 1) / BK;
   const unsigned short* X = p.X + z * p.x_b;
 
-  // LDS-DMA pieces c = wave + NW q (q < NPC): c < 36 -> A (matrix-plane c / 4, rows
-  // 32 (c % 4) ..), else B (matrix-plane (c - 36) / 4, k rows 4 ((c - 36) % 4) ..)
+  // LDS-DMA pieces c = wave + NW q (q < NPC): c < APC -> A (matrix-plane c / 4, rows
+  // 32 (c % 4) ..), else B (matrix-plane (c - APC) / 4, k rows 4 ((c - APC) % 4) ..)
   const unsigned short* src[NPC];
   int dst[NPC];
   int brow[NPC];  // B: k row of this lane within the k-tile (-1 for A pieces)
 #pragma unroll
   for (int q = 0; q < NPC; ++q) {
     const int c = wave + NW * q;
-    if (BF32 && c >= 36) {  // no B pieces; this slot idles
+    if (BF32 && c >= APC) {  // no B pieces; this slot idles
       src[q] = nullptr;
       dst[q] = 0;
       brow[q] = -2;
-    } else if (c < 36) {
+    } else if (c < APC) {
       const int mp = c >> 2, mb = c & 3;
-      const int mat = mp / 3, pl = mp - 3 * mat;
+      const int mat = mp / NP, pl = mp - NP * mat;
       const int m = 32 * mb + (lane >> 1);
       const int h = (lane & 1) ^ ((m >> 3) & 1);
       src[q] = p.Aw + mat * p.a_mat + pl * p.a_plane + (int64_t)(m0 + m) * 16 + 8 * h;
       dst[q] = mp * A_PLANE + mb * 32 * BK;
       brow[q] = -1;
     } else {
-      const int cb = c - 36;
+      const int cb = c - APC;
       const int mp = cb >> 2, rq = cb & 3;
-      const int mat = mp / 3, pl = mp - 3 * mat;
+      const int mat = mp / NP, pl = mp - NP * mat;
       const int row = 4 * rq + (lane >> 4);
       const int gu = (lane & 15) ^ (4 * (row & 3));
       if constexpr ((LAY & 1) != 0)
-        src[q] = X + ((int64_t)tn * p.kt_in * 9 + mp) * B_PLANE + rq * 4 * BN + 8 * (lane & 15) +
+        src[q] = X + ((int64_t)tn * p.kt_in * NMP + mp) * B_PLANE + rq * 4 * BN + 8 * (lane & 15) +
                  BN * (lane >> 4);
       else
         src[q] = X + mat * p.x_mat + pl * p.x_plane + min(n0 + 8 * gu, ldx - 8);
@@ -273,7 +383,7 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_x6c_kernel(X6CParams p) {
       if (BF32 && brow[q] == -2) continue;
       const unsigned short* g = brow[q] < 0
                                     ? src[q] + kt * a_kstride
-                                    : ((LAY & 1) ? src[q] + (int64_t)kt * 9 * B_PLANE
+                                    : ((LAY & 1) ? src[q] + (int64_t)kt * NMP * B_PLANE
                                                  : src[q] + (int64_t)min(kt * BK + brow[q], K - 1) * ldx);
       glds16(g, base + (uint32_t)(dst[q] * 2));
     }
@@ -283,6 +393,14 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_x6c_kernel(X6CParams p) {
   const int brow_f = tid / (BN / 4), bcol_f = 4 * (tid % (BN / 4));
   const float* Xf = BF32 ? p.Xf + z * p.xf_b : nullptr;
   float4 fre = make_float4(0.f, 0.f, 0.f, 0.f), fim = fre;
+  float csb[4] = {1.f, 1.f, 1.f, 1.f};  // x3h BF32: per-column input scale of this thread's columns
+  if constexpr (BF32 && NP == 2) {
+    if (p.colscale) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        csb[e] = p.colscale[z * p.cs_b + min(n0 + bcol_f + e, N - 1)];
+    }
+  }
   auto load_bf = [&](int kt) {
     if constexpr ((LAY & 1) != 0) {  // tiled fp32: [tn][kt][re/im][16][128], 16 KB per stage
       const float* r = Xf + ((int64_t)tn * p.kt_in + kt) * 2 * B_PLANE + brow_f * BN + bcol_f;
@@ -303,8 +421,8 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_x6c_kernel(X6CParams p) {
 #pragma unroll
     for (int e = 0; e < 4; ++e) {  // zero what is out of range (K tail, ragged N)
       const bool ok = k < K && n0 + bcol_f + e < N;
-      re[e] = ok ? re[e] : 0.f;
-      im[e] = ok ? im[e] : 0.f;
+      re[e] = ok ? re[e] * csb[e] : 0.f;  // x3h: the column's input scale (else 1)
+      im[e] = ok ? im[e] * csb[e] : 0.f;
     }
     const float sm[4] = {re[0] + im[0], re[1] + im[1], re[2] + im[2], re[3] + im[3]};
     const float* v[3] = {re, im, sm};
@@ -313,12 +431,12 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_x6c_kernel(X6CParams p) {
     const int off = brow_f * BN + ((u ^ (4 * (brow_f & 3))) << 3) + 4 * h;
 #pragma unroll
     for (int mat = 0; mat < 3; ++mat) {
-      uint32_t a0, a1, a2, b0, b1, b2;
-      split2(v[mat][0], v[mat][1], a0, a1, a2);
-      split2(v[mat][2], v[mat][3], b0, b1, b2);
-      *reinterpret_cast<uint2*>(base + (mat * 3 + 0) * B_PLANE + off) = make_uint2(a0, b0);
-      *reinterpret_cast<uint2*>(base + (mat * 3 + 1) * B_PLANE + off) = make_uint2(a1, b1);
-      *reinterpret_cast<uint2*>(base + (mat * 3 + 2) * B_PLANE + off) = make_uint2(a2, b2);
+      uint32_t ta[NP], tb[NP];
+      X6CEng<NP>::split(v[mat][0], v[mat][1], ta);
+      X6CEng<NP>::split(v[mat][2], v[mat][3], tb);
+#pragma unroll
+      for (int pl = 0; pl < NP; ++pl)
+        *reinterpret_cast<uint2*>(base + (mat * NP + pl) * B_PLANE + off) = make_uint2(ta[pl], tb[pl]);
     }
   };
 
@@ -350,36 +468,27 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_x6c_kernel(X6CParams p) {
     const unsigned short* base = ring + st * STAGE;
 #pragma unroll
     for (int mat = 0; mat < 3; ++mat) {
-      bf16x8c a[MT][3];
+      Frag a[MT][NP];
 #pragma unroll
       for (int i = 0; i < MT; ++i)
 #pragma unroll
-        for (int pl = 0; pl < 3; ++pl)
-          a[i][pl] = *reinterpret_cast<const bf16x8c*>(base + (mat * 3 + pl) * A_PLANE + a_off[i]);
+        for (int pl = 0; pl < NP; ++pl)
+          a[i][pl] = *reinterpret_cast<const Frag*>(base + (mat * NP + pl) * A_PLANE + a_off[i]);
 #pragma unroll
       for (int j = 0; j < NT; ++j) {
-        bf16x8c b[3];
+        Frag b[NP];
 #pragma unroll
-        for (int pl = 0; pl < 3; ++pl) {
-          const unsigned short* q = base + (mat * 3 + pl) * B_PLANE + b_off[j];
+        for (int pl = 0; pl < NP; ++pl) {
+          const unsigned short* q = base + (mat * NP + pl) * B_PLANE + b_off[j];
           const s16x4c lo4 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
               (lds_s16x4*)((__attribute__((address_space(3))) unsigned short*)q));
           const s16x4c hi4 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
               (lds_s16x4*)((__attribute__((address_space(3))) unsigned short*)(q + 4 * BN)));
           const s16x8c v = {lo4[0], lo4[1], lo4[2], lo4[3], hi4[0], hi4[1], hi4[2], hi4[3]};
-          b[pl] = __builtin_bit_cast(bf16x8c, v);
+          b[pl] = __builtin_bit_cast(Frag, v);
         }
 #pragma unroll
-        for (int i = 0; i < MT; ++i) {
-          floatx16 c = acc[mat][i][j];
-          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i][2], b[0], c, 0, 0, 0);
-          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i][1], b[1], c, 0, 0, 0);
-          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i][0], b[2], c, 0, 0, 0);
-          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i][1], b[0], c, 0, 0, 0);
-          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i][0], b[1], c, 0, 0, 0);
-          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i][0], b[0], c, 0, 0, 0);
-          acc[mat][i][j] = c;
-        }
+        for (int i = 0; i < MT; ++i) acc[mat][i][j] = X6CEng<NP>::prod(a[i], b, acc[mat][i][j]);
       }
     }
   };
@@ -408,6 +517,21 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_x6c_kernel(X6CParams p) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
+  // x3h: the layer multiplier (weight scale undone, output range) and, for the fp32
+  // output rows of the last layer, the per-column factor (layer 0's input scale undone)
+  float mul[NT];
+#pragma unroll
+  for (int j = 0; j < NT; ++j) mul[j] = 1.f;
+  if constexpr (NP == 2) {
+    const float ls = *p.lscale;
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+      mul[j] = ls;
+      if constexpr (!PLANES_OUT && (LAY & 2) == 0) {
+        if (p.colscale) mul[j] *= p.colscale[z * p.cs_b + min(n0 + wn * WN + j * 32 + l32, N - 1)];
+      }
+    }
+  }
   // Re = P1 - P2 (ComplexReLU on hidden layers), Im = P3 - P1 - P2, Ys = Re + Im
 #pragma unroll
   for (int i = 0; i < MT; ++i)
@@ -415,7 +539,8 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_x6c_kernel(X6CParams p) {
     for (int j = 0; j < NT; ++j)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const float p1 = acc[0][i][j][r], p2 = acc[1][i][j][r], p3 = acc[2][i][j][r];
+        const float p1 = acc[0][i][j][r] * mul[j], p2 = acc[1][i][j][r] * mul[j],
+                    p3 = acc[2][i][j][r] * mul[j];
         float re = p1 - p2;
         const float im = p3 - p1 - p2;
         if (p.relu) re = fmaxf(re, 0.f);
@@ -429,7 +554,7 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_x6c_kernel(X6CParams p) {
   if constexpr (PLANES_OUT && (LAY & 2) != 0) {
     // tiled planes: every row and column of the tile (pad rows / columns are 0)
     constexpr int CS_LD = BN + 8;
-    unsigned short* Yt = p.Y + z * p.y_b + (int64_t)tn * p.kt_out * 9 * B_PLANE;
+    unsigned short* Yt = p.Y + z * p.y_b + (int64_t)tn * p.kt_out * NMP * B_PLANE;
 #pragma unroll
     for (int mat = 0; mat < 3; ++mat) {
 #pragma unroll
@@ -447,14 +572,14 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_x6c_kernel(X6CParams p) {
         const int idx = tid + 64 * NW * qq;
         const int lr = idx / (BN / 4), c = 4 * (idx % (BN / 4));
         const float4 v = *reinterpret_cast<const float4*>(lds + lr * CS_LD + c);
-        uint32_t a0, a1, a2, b0, b1, b2;
-        split2(v.x, v.y, a0, a1, a2);
-        split2(v.z, v.w, b0, b1, b2);
+        uint32_t ta[NP], tb[NP];
+        X6CEng<NP>::split(v.x, v.y, ta);
+        X6CEng<NP>::split(v.z, v.w, tb);
         const int m = m0 + lr, r = m & 15;
-        unsigned short* d = Yt + ((int64_t)(m >> 4) * 9 + mat * 3) * B_PLANE + r * BN + x6c_tile_swz(r, c);
-        *reinterpret_cast<uint2*>(d) = make_uint2(a0, b0);
-        *reinterpret_cast<uint2*>(d + B_PLANE) = make_uint2(a1, b1);
-        *reinterpret_cast<uint2*>(d + 2 * B_PLANE) = make_uint2(a2, b2);
+        unsigned short* d = Yt + ((int64_t)(m >> 4) * NMP + mat * NP) * B_PLANE + r * BN + x6c_tile_swz(r, c);
+#pragma unroll
+        for (int pl = 0; pl < NP; ++pl)
+          *reinterpret_cast<uint2*>(d + pl * B_PLANE) = make_uint2(ta[pl], tb[pl]);
       }
       __syncthreads();
     }
@@ -526,7 +651,7 @@ size_t spec_weights_3m_layout(SpecWeightsX6p& a) {
 int launch_spec_weights_3m(const SpecWeightsX6p& a, hipStream_t s) {
   if (a.nlayers <= 0) return MSFNO_OK;
   const int blocks = (int)std::min<int64_t>(cdiv(a.start[a.nlayers], 256), 4096);
-  hipLaunchKernelGGL(spec_weights_3m_kernel, dim3(blocks), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(spec_weights_3m_kernel<3>, dim3(blocks), dim3(256), 0, s, a);
   return launch_check("spec_weights_3m");
 }
 
@@ -732,6 +857,102 @@ int gemm_x6c(const unsigned short* Aw, int co, int ci, const unsigned short* X, 
     }
   }
   return launch_check("gemm_x6c");
+}
+
+// ---- x3h spectral chain --------------------------------------------------------
+
+int launch_spec_weights_3m_x3h(const SpecWeightsX6p& a, hipStream_t s) {
+  if (a.nlayers <= 0) return MSFNO_OK;
+  MSFNO_REQUIRE(a.scl, MSFNO_EINVAL, "spec_weights_3m_x3h: no scale array");
+  hipLaunchKernelGGL(spec_scales_x3h_kernel, dim3(1), dim3(256), 0, s, a);
+  MSFNO_TRY(launch_check("spec_scales_x3h"));
+  const int blocks = (int)std::min<int64_t>(cdiv(a.start[a.nlayers], 256), 4096);
+  hipLaunchKernelGGL(spec_weights_3m_kernel<2>, dim3(blocks), dim3(256), 0, s, a);
+  return launch_check("spec_weights_3m_x3h");
+}
+
+// per (b, column n): m = max over the C rows of |Re|, |Im| (S rows [b][re/im][c], ld
+// ldS); alpha = 2^(14 - e) with m = f 2^e, f in [0.5, 1) (1 for an all-zero column)
+__global__ void spec_colscale_kernel(const float* __restrict__ S, int C, int N, int ldS,
+                                     float* __restrict__ cs, int ldcs, int B) {
+  const int b = blockIdx.y;
+  const int n = blockIdx.x * blockDim.x + threadIdx.x;
+  if (n >= ldcs) return;
+  float m = 0.f;
+  if (n < N) {
+    const float* p = S + (int64_t)b * 2 * C * ldS + n;
+    for (int r = 0; r < 2 * C; ++r) m = fmaxf(m, fabsf(p[(int64_t)r * ldS]));
+  }
+  float a = 1.f;
+  if (m > 0.f && isfinite(m)) {
+    int e;
+    frexpf(m, &e);
+    a = ldexpf(1.f, 14 - e);
+  }
+  cs[(int64_t)b * ldcs + n] = a;
+  cs[(int64_t)(B + b) * ldcs + n] = 1.f / a;
+}
+
+int launch_spec_colscale(const float* S, int B, int C, int N, int ldS, float* cs, int ldcs,
+                         hipStream_t s) {
+  if (B <= 0 || N <= 0) return MSFNO_OK;
+  MSFNO_REQUIRE(cs && ldcs >= N, MSFNO_EINVAL, "spec_colscale: bad arguments");
+  hipLaunchKernelGGL(spec_colscale_kernel, dim3((unsigned)cdiv(ldcs, 256), (unsigned)B), dim3(256),
+                     0, s, S, C, N, ldS, cs, ldcs, B);
+  return launch_check("spec_colscale");
+}
+
+int64_t x3c_tiled_elems(int rows, int N) {
+  return cdiv(N, X6C_BN) * round_up(rows, X6C_BM) * 6 * X6C_BN;
+}
+
+int gemm_x3c(const unsigned short* Aw, int co, int ci, const float* Sin, int ldSin,
+             const unsigned short* X, int N, unsigned short* Y, float* Sout, int ldSout,
+             bool relu, const float* lscale, const float* colscale, int64_t cs_b, int B,
+             hipStream_t s) {
+  if (co <= 0 || N <= 0 || B <= 0) return MSFNO_OK;
+  MSFNO_REQUIRE((Sin != nullptr) != (X != nullptr), MSFNO_EINVAL, "gemm_x3c: one input");
+  MSFNO_REQUIRE((Y != nullptr) != (Sout != nullptr), MSFNO_EINVAL, "gemm_x3c: one output");
+  MSFNO_REQUIRE(lscale, MSFNO_EINVAL, "gemm_x3c: no layer scale");
+  MSFNO_REQUIRE(!Sin || (ldSin % 4 == 0 && ldSin >= N && (reinterpret_cast<uintptr_t>(Sin) & 15) == 0),
+                MSFNO_EINVAL, "gemm_x3c: fp32 rows need ld % 4 == 0 and 16-B alignment");
+  MSFNO_REQUIRE(!(Sin && Sout), MSFNO_EINVAL, "gemm_x3c: an fp32 layer writes planes");
+  X6CParams p{};
+  p.Mp = (int)round_up(co, X6C_BM);
+  const int KT = (int)cdiv(ci, X6C_BK);
+  p.Aw = Aw;
+  p.a_plane = (int64_t)p.Mp * KT * 16;
+  p.a_mat = 2 * p.a_plane;
+  p.Xf = Sin;
+  p.xf_b = 2LL * ci * ldSin;
+  p.xf_im = (int64_t)ci * ldSin;
+  p.ldxf = ldSin;
+  p.X = X;
+  p.x_b = x3c_tiled_elems(ci, N);
+  p.ldx = 8;
+  p.kt_in = (int)round_up(ci, X6C_BM) / 16;
+  p.Y = Y;
+  p.y_b = x3c_tiled_elems(co, N);
+  p.kt_out = p.Mp / 16;
+  p.S = Sout;
+  p.s_b = 2LL * co * ldSout;
+  p.s_im = (int64_t)co * ldSout;
+  p.ldS = ldSout;
+  p.co = co; p.ci = ci; p.N = N;
+  p.tiles_m = p.Mp / X6C_BM;
+  p.tiles_n = (int)cdiv(N, X6C_BN);
+  p.relu = relu ? 1 : 0;
+  p.lscale = lscale;
+  p.colscale = colscale;
+  p.cs_b = cs_b;
+  const dim3 grid(p.tiles_m * p.tiles_n, 1, B);
+  if (Sin)
+    hipLaunchKernelGGL((gemm_x6c_kernel<true, 4, 2, true, 0, 2, 2>), grid, dim3(512), 0, s, p);
+  else if (Y)
+    hipLaunchKernelGGL((gemm_x6c_kernel<true, 4, 2, false, 0, 3, 2>), grid, dim3(512), 0, s, p);
+  else
+    hipLaunchKernelGGL((gemm_x6c_kernel<false, 4, 2, false, 0, 1, 2>), grid, dim3(512), 0, s, p);
+  return launch_check("gemm_x3c");
 }
 
 }  // namespace msfno

@@ -1,0 +1,96 @@
+"""Accuracy of the "x3h" engine (MSFNO_ENGINE=x3h: every fp32 GEMM operand split
+into two fp16 terms, three fp16 MFMAs per product, fp32 accumulation; DESIGN.md
+§4) against the default x6 engine (three bf16 terms, six MFMAs: exactly the fp32
+significand).
+
+The reference computes the block in fp32 (sfnonet.py:359-393).  Both engines are
+compared with the oracle evaluated in fp64 (oracle/sfno_ref.py with float64
+transforms and parameters) on the same inputs, each in its own process (the
+engine is chosen once per process).  The x3h engine must be as accurate as the x6
+one: its max-abs error vs fp64 within 2x of x6's (x6 itself matches an fp32 GEMM,
+tests/test_gpu_gemm_x6.py) and far inside the north-star bar (1e-4).
+"""
+import json
+import os
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+if __name__ == "__main__":
+    _repo = os.path.dirname(HERE)
+    for _d in (HERE, _repo, os.path.join(_repo, "modulated-spherical-fourier-neural-operator_amd")):
+        sys.path.insert(0, _d)
+
+import pytest  # noqa: E402
+import torch  # noqa: E402
+
+from oracle import sfno_ref  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+# (filter, nlat, nlon, lmax, B): the fused MLP (C = 256) on ragged tiles, both filters
+CASES = [("non-linear", 90, 180, 45, 2), ("linear", 45, 96, 23, 1)]
+
+
+def _inputs(filter_type, nlat, nlon, lmax, B, seed=11):
+    C = 256
+    cfg = sfno_ref.BlockCfg(filter_type=filter_type)
+    p = sfno_ref.make_block_params(C, lmax, lmax + 1, cfg, seed=seed, randomize_affine=True)
+    g = torch.Generator().manual_seed(seed + 1)
+    x = torch.randn(B, C, nlat, nlon, generator=g)
+    gamma = 0.2 * torch.randn(B, C, generator=g)
+    beta = 0.2 * torch.randn(B, C, generator=g)
+    return cfg, p, x, gamma, beta
+
+
+def _fp64(case):
+    cfg, p, x, gamma, beta = _inputs(*case)
+    nlat, nlon, lmax = case[1:4]
+    sht, isht = sfno_ref.make_transforms(nlat, nlon, lmax, lmax + 1, dtype=torch.float64)
+    p64 = {k: v.double() if v.is_floating_point() else v for k, v in p.items()}
+    with torch.no_grad():
+        return sfno_ref.block_forward(p64, x.double(), sht, isht, cfg, gamma.double(),
+                                      beta.double(), 0.7)
+
+
+def _gpu(case):
+    from test_gpu_mlp_fused import _block
+    cfg, p, x, gamma, beta = _inputs(*case)
+    blk = _block(cfg, p, *case[1:4])
+    with torch.no_grad():
+        return blk(x.to(DEV), gamma.to(DEV), beta.to(DEV), 0.7).double().cpu()
+
+
+def _errors():
+    out = []
+    for case in CASES:
+        want = _fp64(case)
+        got = _gpu(case)
+        out.append(((got - want).abs().max().item(), want.abs().max().item()))
+    return out
+
+
+def _in_child(engine):
+    env = dict(os.environ, MSFNO_ENGINE=engine)
+    r = subprocess.run([sys.executable, os.path.abspath(__file__)], env=env, cwd=HERE,
+                       capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    return json.loads(r.stdout.strip().splitlines()[-1])
+
+
+def test_x3h_block_as_accurate_as_x6():
+    torch.set_num_threads(max(1, min(16, torch.get_num_threads())))
+    x6 = _in_child("x6")
+    x3h = _in_child("x3h")
+    for case, (e6, ymax), (e3, _) in zip(CASES, x6, x3h):
+        print(f"{case}: max-abs vs fp64  x6 {e6:.3e}  x3h {e3:.3e}  (|y|max {ymax:.3f})")
+        assert e3 < max(2.0 * e6, 1e-6 * max(1.0, ymax)), (case, e3, e6)
+        assert e3 < 1e-5 * max(1.0, ymax), (case, e3)
+
+
+if __name__ == "__main__":
+    sys.path.insert(0, os.path.dirname(HERE))
+    import conftest  # noqa: F401  (puts the package on sys.path)
+    torch.set_num_threads(max(1, min(16, torch.get_num_threads())))
+    print(json.dumps(_errors()))
