@@ -49,6 +49,11 @@ PEAK_BF16_MFMA_TFLOPS = 2500.0  # MI355X_MICROARCH.md: bf16 MFMA ~2.5 PF dense (
 # fp32 GEMMs on the "x6" engine (csrc/gemm_x6.hip): six bf16 MFMAs per fp32 product
 # block (exact three-term operand split), so their roof is the bf16 peak / 6
 PEAK_X6_TFLOPS = PEAK_BF16_MFMA_TFLOPS / 6.0
+# the "x3h" engine (default; csrc/mlp_fused_h.hip, gemm_x6c.hip gemm_x3c, gemm_x6.hip
+# gemm_x3): fp32 as two fp16 terms, three fp16 MFMAs per product (fp16 dense MFMA
+# peak = the bf16 one, MI355X_MICROARCH.md), so the roof is 2.5 PF / 3
+PEAK_FP16_MFMA_TFLOPS = 2500.0
+PEAK_X3H_TFLOPS = PEAK_FP16_MFMA_TFLOPS / 3.0
 PEAK_HBM_GBS = 8000.0           # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 
 
@@ -75,8 +80,23 @@ STAGE_KERNEL_F32 = {
     "mlp_fc1": "void msfno::gemm_f32_kernel<128, 256, 16, true, 5>(msfno::GemmParams)",
     "mlp_fc2": "void msfno::gemm_f32_kernel<256, 128, 16, true, 3>(msfno::GemmParams)",
 }
+# x3h engine: the fused MLP, the inner skip (fp32 x, bias epilogue) and the spectral
+# MLP chain; the unfused fc1 / fc2 pair stays on x6
+STAGE_KERNEL_X3H = dict(STAGE_KERNEL_X6, **{
+    "inner_skip": "void msfno::gemm_x6_kernel<256, 256, 4, 2, true, 1, false, 2>(msfno::GemmParams)",
+    "mlp_fused": "void msfno::(anonymous namespace)::mlp_fused_h_kernel<2>"
+                 "(msfno::(anonymous namespace)::MlpHParams)",
+})
 X6_STAGES = {"mlp_fc1", "mlp_fc2", "inner_skip", "mlp_fused"}
 X6_SPEC_STAGES = {"spectral_l0", "spectral_l1", "spectral_l2", "spectral_out"}
+X3H_STAGES = {"inner_skip", "mlp_fused"} | X6_SPEC_STAGES
+
+
+def x3h_engine():
+    """The x3h engine is the library default (mlp_fused_h.hip mlp_fused_h_env:
+    MSFNO_ENGINE=x6 selects the six-bf16-MFMA engine instead; MSFNO_GEMM=f32 the fp32
+    MFMA kernels)."""
+    return x6_engine()[0] and os.environ.get("MSFNO_ENGINE", "") != "x6"
 
 
 def x6_engine():
@@ -96,6 +116,8 @@ def mlp_fused(C, hid):
 
 def mfma_peak(stage):
     dense, spec = x6_engine()
+    if x3h_engine() and stage in X3H_STAGES:
+        return PEAK_X3H_TFLOPS, "x3h (fp32 via 2-term fp16 split, fp16 MFMA / 3)"
     if (dense and stage in X6_STAGES) or (spec and stage in X6_SPEC_STAGES):
         return PEAK_X6_TFLOPS, "x6 (fp32 via 3-term bf16 split, bf16 MFMA / 6)"
     return PEAK_FP32_MFMA_TFLOPS, "f32 MFMA"
@@ -105,7 +127,8 @@ def pmc_traffic(stage):
     """HBM bytes per launch of the stage's kernel from the newest committed PMC
     summary (profiles/*/pmc_traffic.json, written by tools/rocpd_summary.py from
     separate FETCH_SIZE / WRITE_SIZE passes, gfx950-corrected), or None."""
-    sym = (STAGE_KERNEL_X6 if x6_engine()[0] else STAGE_KERNEL_F32).get(stage)
+    sym = (STAGE_KERNEL_X3H if x3h_engine() else
+           STAGE_KERNEL_X6 if x6_engine()[0] else STAGE_KERNEL_F32).get(stage)
     if sym is None:
         return None, None
     import glob

@@ -689,6 +689,7 @@ void carve_block(Carve& cv, BlockBufs& b, const msfno_block_desc* d,
     b.h = cv.take<float>(mlp_h_floats(B, Hd, P));
   }
   b.x1p = x1p_buffer(d, g) ? cv.take<unsigned short>(BC * 3 * P) : nullptr;
+  b.xs = skip_x3(d) ? cv.take<float>(BC) : nullptr;
   carve_dense_ws(cv, b.dw, d, B);
 }
 
@@ -696,7 +697,8 @@ void carve_dense_ws(Carve& cv, DenseWs& w, const msfno_block_desc* d, int B) {
   w.skip = w.fc1 = w.fc2 = nullptr;
   w.skip_b = w.fc1_b = w.fc2_b = 0;
   const int C = (int)d->C;
-  if (d->inner_skip == MSFNO_SKIP_LINEAR && (w.skip_b = gemm_dense_workspace(C, C, 1)))
+  if (d->inner_skip == MSFNO_SKIP_LINEAR &&
+      (w.skip_b = std::max(gemm_dense_workspace(C, C, 1), skip_x3(d) ? gemm_x3_workspace(C, C, B) : 0)))
     w.skip = cv.take<char>(w.skip_b);
   if (d->has_mlp) {
     const int Hd = (int)d->mlp_hidden;
@@ -713,6 +715,18 @@ bool spec_use_3m() {
     return !(e && e[0] == '0');
   }();
   return on && spec_use_x6();
+}
+
+// spectral MLP on the x3h engine (gemm_x3c: fp32 as two fp16 terms, three fp16 MFMAs
+// per product, power-of-two scaled operands) by default; MSFNO_ENGINE=x6 or
+// MSFNO_SPEC_X3H=0 keep the x6 chain (A/B)
+bool spec_use_x3h() {
+  static const bool on = [] {
+    const char* e = getenv("MSFNO_SPEC_X3H");
+    if (e) return e[0] == '1';
+    return mlp_fused_h_env();
+  }();
+  return on && spec_use_3m();
 }
 
 // floats to reserve for one spectral-MLP hidden buffer (B, 2 Hs, T): fp32, or
@@ -803,6 +817,31 @@ int run_filter(const msfno_block_desc* d, msfno_sht_plan_s* f, msfno_sht_plan_s*
         sw.out[l] = static_cast<unsigned short*>(b.dw.spec[l]);
       }
       spec_weights_3m_layout(sw);
+      if (spec_use_x3h() && b.cs && L.ldT % 4 == 0) {
+        // x3h engine: two fp16 planes per value, three MFMAs per product; the layer
+        // scales (2 floats per layer) live behind layer 0's A image (inside wcache when
+        // the images are cached), the per-column input scales in b.cs
+        const int64_t a0 = round_up(6LL * round_up(sw.co[0], 128) * round_up(sw.ci[0], 16) * 2, 256);
+        MSFNO_REQUIRE((size_t)a0 + 2 * (nl + 1) * sizeof(float) <= b.dw.spec_b[0], MSFNO_EWORKSPACE,
+                      "x3h spectral scales do not fit behind layer 0's image");
+        sw.scl = reinterpret_cast<float*>(static_cast<char*>(b.dw.spec[0]) + a0);
+        if (!wcache_ready(d)) MSFNO_TRY(launch_spec_weights_3m_x3h(sw, s));
+        const int ldcs = (int)round_up(L.Tp, 4);
+        MSFNO_TRY(launch_spec_colscale(b.Sa, B, (int)C, (int)L.Tp, (int)L.ldT, b.cs, ldcs, s));
+        unsigned short* cur = nullptr;
+        for (int l = 0; l <= nl; ++l) {
+          prof(l == nl ? ST_SPEC_OUT : ST_SPEC_L0 + std::min(l, 3), s);
+          unsigned short* out = l == nl ? nullptr
+                                        : reinterpret_cast<unsigned short*>((l & 1) ? b.Sc : b.Sb);
+          MSFNO_TRY(gemm_x3c(sw.out[l], sw.co[l], sw.ci[l], l == 0 ? b.Sa : nullptr, (int)L.ldT,
+                             l == 0 ? nullptr : cur, (int)L.Tp, out, l == nl ? b.Sa : nullptr,
+                             (int)L.ldT, l < nl, sw.scl + 2 * l + 1,
+                             l == 0 ? b.cs : (l == nl ? b.cs + (int64_t)B * ldcs : nullptr), ldcs, B,
+                             s));
+          cur = out;
+        }
+        return MSFNO_OK;
+      }
       if (!wcache_ready(d)) MSFNO_TRY(launch_spec_weights_3m(sw, s));
       const int ldTx = (int)round_up(L.Tp, 8);
       unsigned short* cur = reinterpret_cast<unsigned short*>(b.Sc);
@@ -994,7 +1033,8 @@ int run_filter(const msfno_block_desc* d, msfno_sht_plan_s* f, msfno_sht_plan_s*
 int run_spectral(const msfno_block_desc* d, msfno_sht_plan_s* f, msfno_sht_plan_s* g,
                  const BlockBufs& b, const float* x, int B, bool norm0, hipStream_t s,
                  const C2RPlanes* xplanes = nullptr,
-                 const std::function<int()>& after_fft = std::function<int()>()) {
+                 const std::function<int()>& after_fft = std::function<int()>(),
+                 const std::function<int()>& after_norm0 = std::function<int()>()) {
   const int64_t C = d->C, BC = (int64_t)B * C, R = 2 * BC;
   // x6 Legendre: symmetric plans, slab / coefficient planes carved, row path
   const bool lx6 = b.Xtp && b.Sp && f->sym && g->sym && !use_fft_tile(f) &&
@@ -1009,7 +1049,8 @@ int run_spectral(const msfno_block_desc* d, msfno_sht_plan_s* f, msfno_sht_plan_
       prof(ST_NORM0, s);
       MSFNO_TRY(launch_chan_affine(b.rs0, f->nlat, f->nlon, f->nlon, B, (int)C, d->norm0_w,
                                    d->norm0_b, d->norm_eps, nullptr, nullptr, 0.f, b.sc0, b.sh0,
-                                   s));
+                                   s, b.xs));
+      if (after_norm0) MSFNO_TRY(after_norm0());
       MSFNO_TRY(launch_dc_fixup(b.Xt, B, (int)C, f->nlat, f->ldk, b.sc0, b.sh0, s));
     }
     prof(ST_LEG_FWD, s);
@@ -1022,7 +1063,8 @@ int run_spectral(const msfno_block_desc* d, msfno_sht_plan_s* f, msfno_sht_plan_
       prof(ST_NORM0, s);
       MSFNO_TRY(launch_chan_affine(b.rs0, f->nlat, f->nlon, f->nlon, B, (int)C, d->norm0_w,
                                    d->norm0_b, d->norm_eps, nullptr, nullptr, 0.f, b.sc0, b.sh0,
-                                   s));
+                                   s, b.xs));
+      if (after_norm0) MSFNO_TRY(after_norm0());
     }
     prof(ST_TRANSPOSE_FWD, s);
     if (lx6) {
@@ -1242,6 +1284,16 @@ static bool skip_planes_env() {
     return e && e[0] == '1';
   }();
   return on;
+}
+
+// the inner skip on the x3h engine by default (MSFNO_ENGINE=x6 or MSFNO_SKIP_X3H=0 keep x6)
+bool skip_x3(const msfno_block_desc* d) {
+  static const bool on = [] {
+    const char* e = getenv("MSFNO_SKIP_X3H");
+    if (e) return e[0] == '1';
+    return mlp_fused_h_env();
+  }();
+  return on && gemm_use_x6() && !skip_planes_env() && d->inner_skip == MSFNO_SKIP_LINEAR;
 }
 
 bool skip_planes(const msfno_block_desc* d, const msfno_sht_plan_s* f, const BlockBufs& b) {
@@ -1554,7 +1606,10 @@ int msfno_block_forward(const msfno_block_desc* d, msfno_sht_plan_t f, msfno_sht
     prof(ST_SKIP, ss);
     GemmEpi e;
     e.bias = d->skip_b;
-    if (xpl) {
+    if (b.xs) {
+      MSFNO_TRY(gemm_x3(d->skip_w, (int)C, b.xs, x, x1, (int)C, (int)P, (int)C, (int)P, (int)P,
+                        C * P, C * P, B, e, b.dw.skip, b.dw.skip_b, ss));
+    } else if (xpl) {
       e.b_planes = b.x1p;
       e.b_plane_stride = C * P;
       MSFNO_TRY(gemm_x6p(d->skip_w, x1, (int)C, (int)P, (int)C, (int)C, (int)P, (int)P, 0,
@@ -1573,9 +1628,11 @@ int msfno_block_forward(const msfno_block_desc* d, msfno_sht_plan_t f, msfno_sht
   if (d->inner_skip == MSFNO_SKIP_LINEAR) {
     MSFNO_REQUIRE(d->skip_w, MSFNO_EINVAL, "missing inner_skip weight");
     MSFNO_TRY(side_ctx(&side, s));
-    if (!xpl) MSFNO_TRY(launch_skip());
+    if (!xpl && !b.xs) MSFNO_TRY(launch_skip());
   }
-  if (xpl)
+  if (b.xs)  // x3h: the skip needs x's per-channel bounds (norm0 statistics) first
+    MSFNO_TRY(run_spectral(d, f, g, b, x, B, true, s, nullptr, std::function<int()>(), launch_skip));
+  else if (xpl)
     MSFNO_TRY(run_spectral(d, f, g, b, x, B, true, s, &xp, launch_skip));
   else
     MSFNO_TRY(run_spectral(d, f, g, b, x, B, true, s));

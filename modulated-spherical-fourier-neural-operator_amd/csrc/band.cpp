@@ -191,6 +191,7 @@ void carve_band(Carve& cv, BandBufs& b, const msfno_block_desc* d, const msfno_b
   b.fb.x1p = (x1p_buffer(d, p->inv) && Pout % 8 == 0)
                  ? cv.take<unsigned short>(BC * 3 * std::max(Pin, Pout))
                  : nullptr;
+  b.fb.xs = skip_x3(d) ? cv.take<float>((int64_t)B * d->C) : nullptr;
   carve_dense_ws(cv, b.fb.dw, d, B);
 }
 
@@ -397,46 +398,52 @@ int msfno_band_block_stage(const msfno_block_desc* d, msfno_band_plan_t p, int s
   carve_band(cv, b, d, p, B);
   const int64_t C = d->C, BC = (int64_t)B * C, R = 2 * BC;
   const int64_t Pout = (int64_t)p->rows_out * p->nlon_out;
+  // the skip GEMM as in msfno_block_forward: on x planes written by the rfft (forked
+  // after it) when the plane buffer exists, on fp32 x on the x3h engine (forked in
+  // stage 1 once the global statistics give its scales: the unsharded block's scales,
+  // so both round alike), else on fp32 x (forked first)
+  const bool xpl = skip_planes(d, p->fwd, b.fb);
+  const int64_t Pl = (int64_t)p->rows_in * p->nlon_in;
+  auto launch_skip = [&]() -> int {
+    SideCtx* side = nullptr;
+    MSFNO_TRY(side_ctx(&side, s));
+    hipStream_t ss = s;
+    hipEvent_t join = side ? slot_event(p, io->slot) : nullptr;
+    MSFNO_REQUIRE(!side || join, MSFNO_EHIP, "band slot event unavailable (slot must be 0..63)");
+    if (side) {
+      MSFNO_CHECK_HIP(hipEventRecord(side->fork, s));
+      MSFNO_CHECK_HIP(hipStreamWaitEvent(side->side, side->fork, 0));
+      ss = side->side;
+    }
+    prof(ST_SKIP, ss);
+    GemmEpi e;
+    e.bias = d->skip_b;
+    if (b.fb.xs) {  // x3h: B-row scales from the global norm0 statistics (stage 1)
+      MSFNO_TRY(gemm_x3(d->skip_w, (int)C, b.fb.xs, io->x, b.x1, (int)C, (int)Pl, (int)C,
+                        (int)Pl, (int)Pl, C * Pl, C * Pl, B, e, b.fb.dw.skip, b.fb.dw.skip_b,
+                        ss));
+    } else if (xpl) {
+      e.b_planes = b.fb.x1p;
+      e.b_plane_stride = C * Pl;
+      MSFNO_TRY(gemm_x6p(d->skip_w, b.x1, (int)C, (int)Pl, (int)C, (int)C, (int)Pl, (int)Pl,
+                         0, 3 * C * Pl, C * Pl, B, e, b.fb.dw.skip, b.fb.dw.skip_b, ss));
+    } else {
+      MSFNO_TRY(gemm_dense(ROLE_SKIP, TILE_128x256, d->skip_w, io->x, b.x1, (int)C, (int)Pl,
+                           (int)C, (int)C, (int)Pl, (int)Pl, 0, C * Pl, C * Pl, B, e,
+                           b.fb.dw.skip, b.fb.dw.skip_b, ss));
+    }
+    if (side) {
+      prof(ST_END, ss);
+      MSFNO_CHECK_HIP(hipEventRecord(join, ss));
+    }
+    return MSFNO_OK;
+  };
   switch (stage) {
     case 0: {
       MSFNO_REQUIRE(io->x && io->stats_local, MSFNO_EINVAL, "stage 0 needs x and stats_local");
-      // the skip GEMM as in msfno_block_forward: on x planes written by the rfft (forked
-      // after it) when the plane buffer exists, else on fp32 x (forked first)
-      const bool xpl = skip_planes(d, p->fwd, b.fb);
-      const int64_t Pl = (int64_t)p->rows_in * p->nlon_in;
-      auto launch_skip = [&]() -> int {
-        SideCtx* side = nullptr;
-        MSFNO_TRY(side_ctx(&side, s));
-        hipStream_t ss = s;
-        hipEvent_t join = side ? slot_event(p, io->slot) : nullptr;
-        MSFNO_REQUIRE(!side || join, MSFNO_EHIP, "band slot event unavailable (slot must be 0..63)");
-        if (side) {
-          MSFNO_CHECK_HIP(hipEventRecord(side->fork, s));
-          MSFNO_CHECK_HIP(hipStreamWaitEvent(side->side, side->fork, 0));
-          ss = side->side;
-        }
-        prof(ST_SKIP, ss);
-        GemmEpi e;
-        e.bias = d->skip_b;
-        if (xpl) {
-          e.b_planes = b.fb.x1p;
-          e.b_plane_stride = C * Pl;
-          MSFNO_TRY(gemm_x6p(d->skip_w, b.x1, (int)C, (int)Pl, (int)C, (int)C, (int)Pl, (int)Pl,
-                             0, 3 * C * Pl, C * Pl, B, e, b.fb.dw.skip, b.fb.dw.skip_b, ss));
-        } else {
-          MSFNO_TRY(gemm_dense(ROLE_SKIP, TILE_128x256, d->skip_w, io->x, b.x1, (int)C, (int)Pl,
-                               (int)C, (int)C, (int)Pl, (int)Pl, 0, C * Pl, C * Pl, B, e,
-                               b.fb.dw.skip, b.fb.dw.skip_b, ss));
-        }
-        if (side) {
-          prof(ST_END, ss);
-          MSFNO_CHECK_HIP(hipEventRecord(join, ss));
-        }
-        return MSFNO_OK;
-      };
       if (d->inner_skip == MSFNO_SKIP_LINEAR) {
         MSFNO_REQUIRE(d->skip_w, MSFNO_EINVAL, "missing inner_skip weight");
-        if (!xpl) MSFNO_TRY(launch_skip());
+        if (!xpl && !b.fb.xs) MSFNO_TRY(launch_skip());
       }
       prof(ST_FFT_FWD, s);
       const float scale = (float)(2.0 * M_PI / p->nlon_in);
@@ -454,7 +461,11 @@ int msfno_band_block_stage(const msfno_block_desc* d, msfno_band_plan_t p, int s
       prof(ST_NORM0, s);
       MSFNO_TRY(launch_chan_affine_parts(io->stats_all, p->world, B, (int)C, d->norm0_w,
                                          d->norm0_b, d->norm_eps, nullptr, nullptr, 0.f, b.sc0,
-                                         b.sh0, s));
+                                         b.sh0, s, b.fb.xs));
+      if (b.fb.xs && d->inner_skip == MSFNO_SKIP_LINEAR) {
+        MSFNO_REQUIRE(io->x && d->skip_w, MSFNO_EINVAL, "stage 1 needs x for the x3h skip");
+        MSFNO_TRY(launch_skip());
+      }
       prof(ST_BAND_PACK, s);
       const BandRows o = band_rows(p->nlat_in, p->row_in.data(), p->rank);
       MSFNO_TRY(launch_band_pack(b.Xn, io->send, B, (int)C, band_geom(p->fwd, o, p->W_in),

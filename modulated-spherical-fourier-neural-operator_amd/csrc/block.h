@@ -58,6 +58,7 @@ struct BlockBufs {
   unsigned short* Sp;   // x6 Legendre: filter output S as planes [plane][R][ldT]
   unsigned short* mfimg;  // fused MLP weight image (mlp_fused), else null
   float* cs;  // x3h spectral MLP: per-(b, column) input scale and its inverse [2][B][ld]
+  float* xs = nullptr;  // x3h inner skip: per-(b, c) power-of-two scale of x (B-row scales)
   DenseWs dw;
 };
 
@@ -104,6 +105,8 @@ int64_t mlp_h_floats(int B, int64_t Hd, int64_t P);
 bool x1_planes(const msfno_block_desc* d, const msfno_sht_plan_s* g);
 bool skip_planes(const msfno_block_desc* d, const msfno_sht_plan_s* f, const BlockBufs& b);
 bool leg_x6_enabled();
+// the inner-skip GEMM on the x3h engine (gemm_x3), forked after the norm0 statistics
+bool skip_x3(const msfno_block_desc* d);
 // plan construction (mask: optional m-set, see SpecLayout::build)
 int plan_create(int nlat, int nlon, int lmax, int mmax, int inverse,
                 const std::vector<char>* mask, msfno_sht_plan_s** out);

@@ -180,6 +180,13 @@ int gemm_x6(GemmTile tile, const float* A, const float* B, float* C, int M, int 
             void* ws, size_t ws_bytes, hipStream_t s);
 int launch_split_a(const float* A, unsigned short* Ax, int M, int K, int lda, int64_t sA,
                    int batch, hipStream_t s);
+// the same GEMM on the x3h engine (two fp16 terms, three MFMAs; gemm_x6.hip): B rows
+// scaled by the powers of two bscale[z * K + k] while staged (every |scaled| < 2^14),
+// A re-imaged per batch into ws (>= gemm_x3_workspace); bias-only epilogue
+size_t gemm_x3_workspace(int M, int K, int batch);
+int gemm_x3(const float* A, int lda, const float* bscale, const float* B, float* C, int M, int N,
+            int K, int ldb, int ldc, int64_t sB, int64_t sC, int batch, const GemmEpi& epi,
+            void* ws, size_t ws_bytes, hipStream_t s);
 // x6 GEMM with B (and optionally C) in the bf16x3 plane format (gemm_x6p.hip):
 // epi.b_planes required (ldb, sB, b_plane_stride % 8 == 0, 16-B aligned); A fp32
 // is split per call into ws (>= gemm_x6p_workspace(M, K, sA == 0 ? 1 : batch))

@@ -46,6 +46,12 @@ struct GemmParams {
   const float* B2;
   int kb2, ldb2;
   int64_t sB2;
+  // gemm_x6 on the x3h engine (NP = 2; gemm_x3_skip): B row k of batch z multiplied by
+  // x3_bscale[z * K + k] while staged, accumulator row m by x3_rowmul[z * x3_ldrm + m]
+  // before the epilogue (both powers of two)
+  const float* x3_bscale;
+  const float* x3_rowmul;
+  int x3_ldrm;
 };
 
 __device__ __forceinline__ int xcd_remap(int orig, int nwg) {

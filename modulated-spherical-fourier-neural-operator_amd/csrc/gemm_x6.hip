@@ -32,6 +32,9 @@
 namespace msfno {
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef short s16x4 __attribute__((ext_vector_type(4)));
 typedef short s16x8 __attribute__((ext_vector_type(8)));
 __global__ void split_a_kernel(const float* __restrict__ A, unsigned short* __restrict__ Ax, int M,
@@ -54,25 +57,66 @@ __global__ void split_a_kernel(const float* __restrict__ A, unsigned short* __re
   }
 }
 
+// NP planes per value: 3 = x6 (bf16 terms, six MFMAs per product), 2 = x3h (fp16
+// terms h0 = fp16(v), h1 = fp16(v - h0); a1·b0 + a0·b1 + a0·b0, three MFMAs; the
+// operands power-of-two scaled into fp16 range: p.x3_bscale per B row, the A image
+// row-scaled by the host, p.x3_rowmul undoing that per C row)
+template <int NP>
+struct X6Eng;
+template <>
+struct X6Eng<3> {
+  typedef bf16x8 frag;
+  __device__ static void split(float a, float b, uint32_t (&t)[3]) { split2(a, b, t[0], t[1], t[2]); }
+  __device__ static floatx16 prod(const frag (&a)[3], const frag (&b)[3], floatx16 c) {
+    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2], b[0], c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[1], c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[2], c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[0], c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[1], c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[0], c, 0, 0, 0);
+    return c;
+  }
+};
+template <>
+struct X6Eng<2> {
+  typedef f16x8 frag;
+  __device__ static void split(float a, float b, uint32_t (&t)[2]) {
+    const f32x2 v = {a, b};
+    const f16x2 h0 = __builtin_convertvector(v, f16x2);
+    const f32x2 r = v - __builtin_convertvector(h0, f32x2);
+    const f16x2 h1 = __builtin_convertvector(r, f16x2);
+    t[0] = __builtin_bit_cast(uint32_t, h0);
+    t[1] = __builtin_bit_cast(uint32_t, h1);
+  }
+  __device__ static floatx16 prod(const frag (&a)[2], const frag (&b)[2], floatx16 c) {
+    c = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[1], b[0], c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[0], b[1], c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[0], b[0], c, 0, 0, 0);
+    return c;
+  }
+};
+
 // BPL: B arrives pre-split as bf16 planes (p.Bx), staged without conversion
-template <int BM, int BN, int WGM, int WGN, bool VEC, int EPI, bool BPL>
+template <int BM, int BN, int WGM, int WGN, bool VEC, int EPI, bool BPL, int NP = 3>
 __global__ __launch_bounds__(64 * WGM * WGN) void gemm_x6_kernel(GemmParams p) {
+  static_assert(NP == 3 || !BPL, "x3h: fp32 B only");
+  typedef typename X6Eng<NP>::frag Frag;
   constexpr int BK = 16;
   constexpr int NTHR = 64 * WGM * WGN;
   constexpr int WM = BM / WGM, WN = BN / WGN;
   constexpr int MT = WM / 32, NT = WN / 32;
   constexpr int A_PLANE = BM * BK;  // bf16 elements
-  constexpr int A_STAGE = 3 * A_PLANE;
+  constexpr int A_STAGE = NP * A_PLANE;
   constexpr int B_ROW = BN + 32;
   constexpr int B_PLANE = BK * B_ROW;
-  constexpr int B_STAGE = 3 * B_PLANE;
+  constexpr int B_STAGE = NP * B_PLANE;
   constexpr int STAGE_BYTES = 2 * (A_STAGE + B_STAGE) * 2;
   constexpr int EPI_BYTES = 32 * WGM * (BN + 8) * 4;
   constexpr int LDS_BYTES = STAGE_BYTES > EPI_BYTES ? STAGE_BYTES : EPI_BYTES;
   constexpr bool HAS_BIAS = (EPI & EPI_BIAS) != 0;
-  constexpr int A_LD = 6 * BM / NTHR;       // 16-B chunks of split A per thread
+  constexpr int A_LD = 2 * NP * BM / NTHR;  // 16-B chunks of split A per thread
   constexpr int B_LD = BK * BN / 4 / NTHR;  // float4 of B per thread
-  static_assert(A_LD * NTHR == 6 * BM && B_LD * NTHR * 4 == BK * BN, "tile shape");
+  static_assert(A_LD * NTHR == 2 * NP * BM && B_LD * NTHR * 4 == BK * BN, "tile shape");
   // pre-split B: chunks of BCH bf16 (16 or 8 bytes), BPQ per thread
   constexpr int BCH = ((3 * BK * BN / 8) % NTHR == 0) ? 8 : 4;
   constexpr int BPQ = 3 * BK * BN / BCH / NTHR;
@@ -193,13 +237,17 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_x6_kernel(GemmParams p) {
       v.y = (kok && cg + 1 < N) ? v.y : 0.f;
       v.z = (kok && cg + 2 < N) ? v.z : 0.f;
       v.w = (kok && cg + 3 < N) ? v.w : 0.f;
-      uint32_t a0, a1, a2, b0, b1, b2;
-      split2(v.x, v.y, a0, a1, a2);
-      split2(v.z, v.w, b0, b1, b2);
+      if constexpr (NP == 2) {  // the B row's power-of-two scale (|scaled| < 2^14)
+        const float bs = kok ? p.x3_bscale[z * K + kt * BK + kr] : 0.f;
+        v.x *= bs; v.y *= bs; v.z *= bs; v.w *= bs;
+      }
+      uint32_t ta[NP], tb[NP];
+      X6Eng<NP>::split(v.x, v.y, ta);
+      X6Eng<NP>::split(v.z, v.w, tb);
       unsigned short* dst = Bs + buf * B_STAGE + kr * B_ROW + c4;
-      *reinterpret_cast<uint2*>(dst) = make_uint2(a0, b0);
-      *reinterpret_cast<uint2*>(dst + B_PLANE) = make_uint2(a1, b1);
-      *reinterpret_cast<uint2*>(dst + 2 * B_PLANE) = make_uint2(a2, b2);
+#pragma unroll
+      for (int pl = 0; pl < NP; ++pl)
+        *reinterpret_cast<uint2*>(dst + pl * B_PLANE) = make_uint2(ta[pl], tb[pl]);
     }
   };
 
@@ -225,36 +273,27 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_x6_kernel(GemmParams p) {
     typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
     const unsigned short* as = As + buf * A_STAGE;
     const unsigned short* bs = Bs + buf * B_STAGE;
-    bf16x8 a[MT][3];
+    Frag a[MT][NP];
 #pragma unroll
     for (int i = 0; i < MT; ++i)
 #pragma unroll
-      for (int pl = 0; pl < 3; ++pl)
-        a[i][pl] = *reinterpret_cast<const bf16x8*>(as + pl * A_PLANE + a_off[i]);
+      for (int pl = 0; pl < NP; ++pl)
+        a[i][pl] = *reinterpret_cast<const Frag*>(as + pl * A_PLANE + a_off[i]);
 #pragma unroll
     for (int j = 0; j < NT; ++j) {
-      bf16x8 b[3];
+      Frag b[NP];
 #pragma unroll
-      for (int pl = 0; pl < 3; ++pl) {
+      for (int pl = 0; pl < NP; ++pl) {
         const unsigned short* q = bs + pl * B_PLANE + b_off + j * 32;
         const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
             (lds_s16x4*)((__attribute__((address_space(3))) unsigned short*)q));
         const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
             (lds_s16x4*)((__attribute__((address_space(3))) unsigned short*)(q + 4 * B_ROW)));
         const s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-        b[pl] = __builtin_bit_cast(bf16x8, v);
+        b[pl] = __builtin_bit_cast(Frag, v);
       }
 #pragma unroll
-      for (int i = 0; i < MT; ++i) {
-        floatx16 c = acc[i][j];
-        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i][2], b[0], c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i][1], b[1], c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i][0], b[2], c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i][1], b[0], c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i][0], b[1], c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i][0], b[0], c, 0, 0, 0);
-        acc[i][j] = c;
-      }
+      for (int i = 0; i < MT; ++i) acc[i][j] = X6Eng<NP>::prod(a[i], b, acc[i][j]);
     }
   };
 
@@ -277,6 +316,17 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_x6_kernel(GemmParams p) {
       store_B(cur ^ 1, kt + 1);
     }
     __syncthreads();
+  }
+  if constexpr (NP == 2) {  // undo the A image's row scales (32x32 C layout)
+    const float* rm = p.x3_rowmul + (int64_t)z * p.x3_ldrm + m0;
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float f = rm[wm * WM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * half];
+#pragma unroll
+        for (int j = 0; j < NT; ++j) acc[i][j][r] *= f;
+      }
   }
   gemm_epilogue<BM, BN, EPI, WGM, WGN>(p, acc, reinterpret_cast<float*>(lds_raw), bias_s, C, addend, M, N,
                              ldc, m0, n0, 0);
@@ -431,6 +481,113 @@ int gemm_x6(GemmTile tile, const float* A, const float* B, float* C, int M, int 
   }
   if (rc != MSFNO_OK) return rc;
   return launch_check("gemm_x6");
+}
+
+// ---- x3h engine (NP = 2): the inner-skip GEMM ----------------------------------
+
+// A image per batch z: W (M x K, ld lda) · diag(1 / bscale[z]) with row m scaled by
+// tau = 2^(15 - e) (the row's max = f 2^e, f in [0.5, 1): scaled entries < 2^15), split
+// into two fp16 planes [z][2][Mp][Kp]; rowmul[z * Mp + m] = 1 / tau.  One workgroup
+// per (row, batch)
+__global__ __launch_bounds__(256) void x3_image_kernel(const float* __restrict__ W, int M, int K,
+                                                       int lda, const float* __restrict__ bscale,
+                                                       unsigned short* __restrict__ img,
+                                                       float* __restrict__ rowmul, int Mp, int Kp) {
+  __shared__ float red[256];
+  const int m = blockIdx.x, z = blockIdx.y;
+  const float* w = W + (int64_t)min(m, M - 1) * lda;
+  const float* bs = bscale + (int64_t)z * K;
+  float mx = 0.f;
+  if (m < M)
+    for (int k = threadIdx.x; k < K; k += 256) mx = fmaxf(mx, fabsf(w[k] / bs[k]));
+  red[threadIdx.x] = mx;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) red[threadIdx.x] = fmaxf(red[threadIdx.x], red[threadIdx.x + o]);
+    __syncthreads();
+  }
+  mx = red[0];
+  float tau = 1.f;
+  if (mx > 0.f && isfinite(mx)) {
+    int e;
+    frexpf(mx, &e);
+    tau = ldexpf(1.f, 15 - e);
+  }
+  const int64_t plane = (int64_t)Mp * Kp;
+  uint32_t* o = reinterpret_cast<uint32_t*>(img + (int64_t)z * 2 * plane + (int64_t)m * Kp);
+  for (int kk = threadIdx.x; kk < Kp / 2; kk += 256) {
+    const int k = 2 * kk;
+    const float v0 = (m < M && k < K) ? w[k] / bs[k] * tau : 0.f;
+    const float v1 = (m < M && k + 1 < K) ? w[k + 1] / bs[k + 1] * tau : 0.f;
+    uint32_t t[2];
+    X6Eng<2>::split(v0, v1, t);
+    o[kk] = t[0];
+    o[plane / 2 + kk] = t[1];
+  }
+  if (threadIdx.x == 0) rowmul[(int64_t)z * Mp + m] = 1.f / tau;
+}
+
+size_t gemm_x3_workspace(int M, int K, int batch) {
+  const int64_t Mp = round_up(M, 256), Kp = round_up(K, 16);
+  return (size_t)(round_up(2 * Mp * Kp * 2 * (int64_t)batch, 256) + round_up(Mp * 4 * (int64_t)batch, 256));
+}
+
+template <int BM, int BN, int WGM, int WGN, int EPI>
+static void launch_x3_e(const GemmParams& p, dim3 grid, hipStream_t s) {
+  if (p.vecB)
+    hipLaunchKernelGGL((gemm_x6_kernel<BM, BN, WGM, WGN, true, EPI, false, 2>), grid,
+                       dim3(64 * WGM * WGN), 0, s, p);
+  else
+    hipLaunchKernelGGL((gemm_x6_kernel<BM, BN, WGM, WGN, false, EPI, false, 2>), grid,
+                       dim3(64 * WGM * WGN), 0, s, p);
+}
+
+// C[z] = A · (B[z] rows scaled by bscale[z]) / bscale-corrected A = A · B[z] (+ bias),
+// fp32 in and out, on the x3h engine.  bscale[z * K + k] are powers of two under which
+// every element of B row k has magnitude < 2^14 (launch_chan_affine's xscale); A is
+// re-imaged per batch (x3_image_kernel) into the workspace
+int gemm_x3(const float* A, int lda, const float* bscale, const float* B, float* C, int M, int N,
+            int K, int ldb, int ldc, int64_t sB, int64_t sC, int batch, const GemmEpi& epi,
+            void* ws, size_t ws_bytes, hipStream_t s) {
+  if (M <= 0 || N <= 0 || batch <= 0) return MSFNO_OK;
+  MSFNO_REQUIRE(ws && ws_bytes >= gemm_x3_workspace(M, K, batch), MSFNO_EINVAL,
+                "gemm_x3: workspace too small");
+  MSFNO_REQUIRE(bscale && batch <= 65535, MSFNO_EINVAL, "gemm_x3: bad arguments");
+  MSFNO_REQUIRE(!epi.addend && !epi.act && !epi.relu_period && !epi.rowscale && !epi.b_planes &&
+                    !epi.c_planes && !epi.b2,
+                MSFNO_EUNSUPPORTED, "gemm_x3: bias-only epilogue");
+  const int Mp = (int)round_up(M, 256), Kp = (int)round_up(K, 16);
+  unsigned short* Ax = static_cast<unsigned short*>(ws);
+  float* rowmul = reinterpret_cast<float*>(static_cast<char*>(ws) +
+                                           round_up(2LL * Mp * Kp * 2 * batch, 256));
+  hipLaunchKernelGGL(x3_image_kernel, dim3(Mp, batch), dim3(256), 0, s, A, M, K, lda, bscale, Ax,
+                     rowmul, Mp, Kp);
+  MSFNO_TRY(launch_check("x3_image"));
+  GemmParams p{};
+  p.B = B; p.C = C;
+  p.M = M; p.N = N; p.K = K; p.ldb = ldb; p.ldc = ldc;
+  p.sB = sB; p.sC = sC;
+  p.bias = epi.bias; p.sBias = epi.sBias;
+  p.Ax = Ax; p.sAxp = (int64_t)Mp * Kp; p.sAx = 2 * p.sAxp; p.ldax = Kp;
+  p.vecB = (ldb % 4 == 0) && (sB % 4 == 0) && ((reinterpret_cast<uintptr_t>(B) & 15) == 0);
+  p.vecC = (ldc % 4 == 0) && (sC % 4 == 0) && ((reinterpret_cast<uintptr_t>(C) & 15) == 0);
+  p.x3_bscale = bscale;
+  p.x3_rowmul = rowmul;
+  p.x3_ldrm = Mp;
+  const GemmTile tile = x6_tile(M, N, batch);
+  const bool big = tile == TILE_256x256;
+  const int bm = big ? 256 : 128, bn = big ? 256 : 128;
+  p.tiles_m = (int)cdiv(M, bm);
+  p.tiles_n = (int)cdiv(N, bn);
+  const dim3 grid(p.tiles_m * p.tiles_n, 1, batch);
+  if (big) {
+    if (p.bias) launch_x3_e<256, 256, 4, 2, EPI_BIAS>(p, grid, s);
+    else launch_x3_e<256, 256, 4, 2, 0>(p, grid, s);
+  } else {
+    if (p.bias) launch_x3_e<128, 128, 2, 2, EPI_BIAS>(p, grid, s);
+    else launch_x3_e<128, 128, 2, 2, 0>(p, grid, s);
+  }
+  return launch_check("gemm_x3");
 }
 
 int gemm_dense(GemmRole role, GemmTile f32_tile, const float* A, const float* B, float* C, int M,

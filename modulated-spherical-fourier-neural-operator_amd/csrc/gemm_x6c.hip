@@ -872,32 +872,62 @@ int launch_spec_weights_3m_x3h(const SpecWeightsX6p& a, hipStream_t s) {
 }
 
 // per (b, column n): m = max over the C rows of |Re|, |Im| (S rows [b][re/im][c], ld
-// ldS); alpha = 2^(14 - e) with m = f 2^e, f in [0.5, 1) (1 for an all-zero column)
-__global__ void spec_colscale_kernel(const float* __restrict__ S, int C, int N, int ldS,
-                                     float* __restrict__ cs, int ldcs, int B) {
+// ldS); alpha = 2^(14 - e) with m = f 2^e, f in [0.5, 1) (1 for an all-zero column).
+// A workgroup = 64 columns x 16 row slices (a thread: 4 columns by float4, every 16th
+// row), the slices combined through LDS: 16-B coalesced loads, 1024+ workgroups at
+// the production shape instead of one latency-bound row walk per thread
+__global__ __launch_bounds__(256) void spec_colscale_kernel(const float* __restrict__ S, int C, int N,
+                                                            int ldS, float* __restrict__ cs,
+                                                            int ldcs, int B) {
+  __shared__ float4 red[16][16];
   const int b = blockIdx.y;
-  const int n = blockIdx.x * blockDim.x + threadIdx.x;
-  if (n >= ldcs) return;
-  float m = 0.f;
-  if (n < N) {
-    const float* p = S + (int64_t)b * 2 * C * ldS + n;
-    for (int r = 0; r < 2 * C; ++r) m = fmaxf(m, fabsf(p[(int64_t)r * ldS]));
+  const int cg = threadIdx.x & 15, sl = threadIdx.x >> 4;
+  const int n = blockIdx.x * 64 + 4 * cg;
+  const float* p = S + (int64_t)b * 2 * C * ldS;
+  float4 m = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (n + 3 < N && (ldS & 3) == 0) {
+#pragma unroll 4
+    for (int r = sl; r < 2 * C; r += 16) {
+      const float4 v = *reinterpret_cast<const float4*>(p + (int64_t)r * ldS + n);
+      m.x = fmaxf(m.x, fabsf(v.x)); m.y = fmaxf(m.y, fabsf(v.y));
+      m.z = fmaxf(m.z, fabsf(v.z)); m.w = fmaxf(m.w, fabsf(v.w));
+    }
+  } else if (n < N) {
+    for (int r = sl; r < 2 * C; r += 16) {
+      const float* q = p + (int64_t)r * ldS + n;
+      m.x = fmaxf(m.x, fabsf(q[0]));
+      if (n + 1 < N) m.y = fmaxf(m.y, fabsf(q[1]));
+      if (n + 2 < N) m.z = fmaxf(m.z, fabsf(q[2]));
+      if (n + 3 < N) m.w = fmaxf(m.w, fabsf(q[3]));
+    }
   }
+  red[sl][cg] = m;
+  __syncthreads();
+  if (threadIdx.x >= 64) return;
+  const int c4 = threadIdx.x >> 2, e = threadIdx.x & 3;
+  float mx = 0.f;
+#pragma unroll
+  for (int t = 0; t < 16; ++t) {
+    const float4 v = red[t][c4];
+    mx = fmaxf(mx, e == 0 ? v.x : (e == 1 ? v.y : (e == 2 ? v.z : v.w)));
+  }
+  const int col = blockIdx.x * 64 + threadIdx.x;
+  if (col >= ldcs) return;
   float a = 1.f;
-  if (m > 0.f && isfinite(m)) {
-    int e;
-    frexpf(m, &e);
-    a = ldexpf(1.f, 14 - e);
+  if (col < N && mx > 0.f && isfinite(mx)) {
+    int ex;
+    frexpf(mx, &ex);
+    a = ldexpf(1.f, 14 - ex);
   }
-  cs[(int64_t)b * ldcs + n] = a;
-  cs[(int64_t)(B + b) * ldcs + n] = 1.f / a;
+  cs[(int64_t)b * ldcs + col] = a;
+  cs[(int64_t)(B + b) * ldcs + col] = 1.f / a;
 }
 
 int launch_spec_colscale(const float* S, int B, int C, int N, int ldS, float* cs, int ldcs,
                          hipStream_t s) {
   if (B <= 0 || N <= 0) return MSFNO_OK;
-  MSFNO_REQUIRE(cs && ldcs >= N, MSFNO_EINVAL, "spec_colscale: bad arguments");
-  hipLaunchKernelGGL(spec_colscale_kernel, dim3((unsigned)cdiv(ldcs, 256), (unsigned)B), dim3(256),
+  MSFNO_REQUIRE(cs && ldcs >= N && B <= 65535, MSFNO_EINVAL, "spec_colscale: bad arguments");
+  hipLaunchKernelGGL(spec_colscale_kernel, dim3((unsigned)cdiv(ldcs, 64), (unsigned)B), dim3(256),
                      0, s, S, C, N, ldS, cs, ldcs, B);
   return launch_check("spec_colscale");
 }

@@ -52,19 +52,24 @@ int launch_transpose_inv(const float* Yt, float2* Yn, int B, int C, int nlat, in
                          int ldk, hipStream_t s, const int* slab = nullptr);
 // Combine per-(bc) partial (mean, M2) statistics (np partials, each over `cnt`
 // elements except the last over `cnt_last`) and produce the affine that
-// implements InstanceNorm (+ optional FiLM): y = scale·x + shift.
+// implements InstanceNorm (+ optional FiLM): y = scale·x + shift.  xscale (or null):
+// per (b,c) the power of two 2^(14 - e), |mean| + sqrt(M2) = f 2^e (f in [0.5, 1)),
+// under which every element of the channel scales below 2^14 in magnitude
+// (|x - mean| <= sqrt(sum (x - mean)^2)): the x3h skip GEMM's B-row scales
 int launch_chan_affine(const float2* partials, int64_t np, int64_t cnt, int64_t cnt_last,
                        int B, int C, const float* w, const float* b, float eps,
                        const float* gamma, const float* beta, float film_scale, float* scale,
-                       float* shift, hipStream_t s);
+                       float* shift, hipStream_t s, float* xscale = nullptr);
 // latitude-band sharding helpers (band.cpp)
-// rowstats (BC, np) (mean, M2) over cnt each -> out (BC, 3) fp64 {n, mean, M2}
+// rowstats (BC, np) (mean, M2) over cnt each -> out (BC, 3) fp64 {n, mean, M2}; xscale
+// (or null): the local x3h skip B-row scales as in launch_chan_affine
 int launch_stats_partial(const float2* rowstats, int64_t np, int64_t cnt, int64_t BC, double* out,
-                         hipStream_t s);
+                         hipStream_t s, float* xscale = nullptr);
 // parts (nparts, BC, 3) fp64 -> InstanceNorm (+FiLM) per-(b,c) affine
 int launch_chan_affine_parts(const double* parts, int nparts, int B, int C, const float* w,
                              const float* b, float eps, const float* gamma, const float* beta,
-                             float film_scale, float* scale, float* shift, hipStream_t s);
+                             float film_scale, float* scale, float* shift, hipStream_t s,
+                             float* xscale = nullptr);
 // the all-to-all buffers are the Legendre GEMMs' own operands: [p][slab][R][2W]
 // blocks (common.h msfno_sht_plan_s band fields).  g: the rank's local rows as a
 // small symmetric grid (Ke = its band, nh = the band rows that have a mirror row,
@@ -97,7 +102,7 @@ int launch_mlp_fused(const float* x1, const float* scale, const float* shift, co
 bool mlp_fused2_env();
 int launch_mlp_fused2_images(const float* W1, const float* W2, unsigned short* img, hipStream_t s);
 // mlp_fused_h.hip: the MLP on the x3h engine (fp32 as two fp16 terms, three fp16
-// MFMAs per product, row-scaled weights); MSFNO_ENGINE=x3h
+// MFMAs per product, row-scaled weights); default (MSFNO_ENGINE=x6 selects the x6 engine)
 bool mlp_fused_h_env();
 size_t mlp_fused_h_image_bytes();
 int launch_mlp_fused_h_images(const float* W1, const float* W2, unsigned short* img, hipStream_t s);

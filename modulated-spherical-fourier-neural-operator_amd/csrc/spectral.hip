@@ -695,11 +695,21 @@ __device__ __forceinline__ Welford wcombine(Welford a, Welford b) {
   return r;
 }
 
+// the x3h skip GEMM's B-row scale of a channel with mean mu and sum of squared
+// deviations m2: every element satisfies |x| <= |mu| + sqrt(m2), mapped below 2^14
+__device__ __forceinline__ float x3_bound_scale(double mu, double m2) {
+  const double bound = (fabs(mu) + sqrt(m2)) * (1.0 + 1e-3);
+  if (!(bound > 0.0 && bound < 1e300)) return 1.f;
+  int e;
+  frexp(bound, &e);
+  return (float)ldexp(1.0, min(max(14 - e, -100), 100));
+}
+
 __global__ __launch_bounds__(256) void chan_affine_kernel(
     const float2* __restrict__ part, int64_t np, int64_t cnt, int64_t cnt_last, int C,
     const float* __restrict__ w, const float* __restrict__ bsh, float eps,
     const float* __restrict__ gamma, const float* __restrict__ beta, float film_scale,
-    float* __restrict__ scale, float* __restrict__ shift) {
+    float* __restrict__ scale, float* __restrict__ shift, float* __restrict__ xscale) {
   __shared__ double sn[256], smean[256], sm2[256];
   const int bc = blockIdx.x;
   const int c = bc % C;
@@ -738,15 +748,16 @@ __global__ __launch_bounds__(256) void chan_affine_kernel(
     }
     scale[bc] = (float)sc;
     shift[bc] = (float)sh;
+    if (xscale) xscale[bc] = x3_bound_scale(mu, sm2[0]);
   }
 }
 
 int launch_chan_affine(const float2* partials, int64_t np, int64_t cnt, int64_t cnt_last, int B,
                        int C, const float* w, const float* b, float eps, const float* gamma,
                        const float* beta, float film_scale, float* scale, float* shift,
-                       hipStream_t s) {
+                       hipStream_t s, float* xscale) {
   hipLaunchKernelGGL(chan_affine_kernel, dim3(B * C), dim3(256), 0, s, partials, np, cnt,
-                     cnt_last, C, w, b, eps, gamma, beta, film_scale, scale, shift);
+                     cnt_last, C, w, b, eps, gamma, beta, film_scale, scale, shift, xscale);
   return launch_check("chan_affine");
 }
 
@@ -757,7 +768,8 @@ int launch_chan_affine(const float2* partials, int64_t np, int64_t cnt, int64_t 
 // rowstats (BC, np) (mean, M2) over cnt elements each -> out (BC, 3) fp64 {n, mean, M2}
 __global__ __launch_bounds__(256) void stats_partial_kernel(const float2* __restrict__ part,
                                                             int64_t np, int64_t cnt,
-                                                            double* __restrict__ out) {
+                                                            double* __restrict__ out,
+                                                            float* __restrict__ xscale) {
   __shared__ double sn[256], smean[256], sm2[256];
   const int bc = blockIdx.x;
   const float2* p = part + (int64_t)bc * np;
@@ -784,13 +796,14 @@ __global__ __launch_bounds__(256) void stats_partial_kernel(const float2* __rest
     out[3 * (int64_t)bc + 0] = sn[0];
     out[3 * (int64_t)bc + 1] = smean[0];
     out[3 * (int64_t)bc + 2] = sm2[0];
+    if (xscale) xscale[bc] = x3_bound_scale(smean[0], sm2[0]);
   }
 }
 
 int launch_stats_partial(const float2* rowstats, int64_t np, int64_t cnt, int64_t BC, double* out,
-                         hipStream_t s) {
+                         hipStream_t s, float* xscale) {
   hipLaunchKernelGGL(stats_partial_kernel, dim3((unsigned)BC), dim3(256), 0, s, rowstats, np, cnt,
-                     out);
+                     out, xscale);
   return launch_check("stats_partial");
 }
 
@@ -800,7 +813,8 @@ __global__ void chan_affine_parts_kernel(const double* __restrict__ parts, int n
                                          const float* __restrict__ bsh, float eps,
                                          const float* __restrict__ gamma,
                                          const float* __restrict__ beta, float film_scale,
-                                         float* __restrict__ scale, float* __restrict__ shift) {
+                                         float* __restrict__ scale, float* __restrict__ shift,
+                                         float* __restrict__ xscale) {
   const int bc = blockIdx.x * blockDim.x + threadIdx.x;
   if (bc >= BC) return;
   const int c = bc % C;
@@ -820,14 +834,17 @@ __global__ void chan_affine_parts_kernel(const double* __restrict__ parts, int n
   }
   scale[bc] = (float)sc;
   shift[bc] = (float)sh;
+  if (xscale) xscale[bc] = x3_bound_scale(acc.mean, acc.m2);
 }
 
 int launch_chan_affine_parts(const double* parts, int nparts, int B, int C, const float* w,
                              const float* b, float eps, const float* gamma, const float* beta,
-                             float film_scale, float* scale, float* shift, hipStream_t s) {
+                             float film_scale, float* scale, float* shift, hipStream_t s,
+                             float* xscale) {
   const int BC = B * C;
   hipLaunchKernelGGL(chan_affine_parts_kernel, dim3((unsigned)cdiv(BC, 256)), dim3(256), 0, s,
-                     parts, nparts, BC, C, w, b, eps, gamma, beta, film_scale, scale, shift);
+                     parts, nparts, BC, C, w, b, eps, gamma, beta, film_scale, scale, shift,
+                     xscale);
   return launch_check("chan_affine_parts");
 }
 

@@ -304,8 +304,10 @@ def test_config5_112_steps_full_geometry():
     73 channels, with normalisation.  The HIP-graph replayed Rollout is compared
     with eager stepping and with the network latitude-band sharded over 8 lock-step
     virtual ranks (LatBandNet) stepped the same way, at every 8th step and the last
-    (bar 1e-4 * max(1, |y|)).  Decoder weights x6.5 as in the reduced-grid test so
-    the state keeps moving at O(1) instead of settling to a fixed point (checked)."""
+    (bar 1e-4 * max(1, |y|)).  Decoder weights x2: at this geometry the state then
+    keeps moving by O(|y|) per step with |y|max ~ 8-10 for all 112 steps (gain 1
+    settles to a fixed point, gain 6.5 grows x1.45 per step to 1e20; scan:
+    tools/c5_gain.py, profiles/r03_v2/c5_gain.txt) — both checked below."""
     from msfno_amd.rollout import Rollout
     from msfno_amd.sfno import FourierNeuralOperatorNet_Filmed, LatBandBlock, LatBandNet, LocalGroup
     steps, ch = 112, 73
@@ -317,7 +319,7 @@ def test_config5_112_steps_full_geometry():
     with torch.no_grad():
         for k, v in net.decoder.state_dict().items():
             if k.endswith("weight"):
-                v.mul_(6.5)
+                v.mul_(2.0)
     net = net.to(DEV)
     g = torch.Generator(device=DEV).manual_seed(52)
     means = torch.randn(1, ch, 1, 1, generator=g, device=DEV)
@@ -341,6 +343,7 @@ def test_config5_112_steps_full_geometry():
         eager, _ = collect(Rollout(net, means, stds, film=film, graph=False), x0)
         # the state must keep moving (no fixed point) for the comparison to mean anything
         assert min(moved[-16:]) > 1e-3, moved[-16:]
+        assert max(v.abs().max().item() for v in ref.values()) < 1e3  # bounded, not blowing up
         shards = [LatBandNet(net, r, 8) for r in range(8)]
         parts = [(s.take(x0) - means) / stds for s in shards]
         worst = 0.0
@@ -352,6 +355,7 @@ def test_config5_112_steps_full_geometry():
                 e_eager = (eager[i] - ref[i]).abs().max().item() / sc
                 e_band = (y - ref[i]).abs().max().item() / sc
                 worst = max(worst, e_eager, e_band)
+                print(f"config5 step {i}: eager {e_eager:.3e} band {e_band:.3e} |y|max {sc:.3e}", flush=True)
                 assert e_eager < 1e-4 and e_band < 1e-4, (i, e_eager, e_band)
     print(f"config5 112 steps 721x1440: worst relative max-abs {worst:.3e}, "
           f"last-step change {moved[-1]:.3e}")

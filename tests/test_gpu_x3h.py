@@ -8,7 +8,10 @@ compared with the oracle evaluated in fp64 (oracle/sfno_ref.py with float64
 transforms and parameters) on the same inputs, each in its own process (the
 engine is chosen once per process).  The x3h engine must be as accurate as the x6
 one: its max-abs error vs fp64 within 2x of x6's (x6 itself matches an fp32 GEMM,
-tests/test_gpu_gemm_x6.py) and far inside the north-star bar (1e-4).
+tests/test_gpu_gemm_x6.py) and far inside the north-star bar (1e-4).  The oracle
+evaluated in plain fp32 on the CPU (what the reference's own fp32 arithmetic gives)
+is printed beside them: x3h must stay within 2x of its error (measured: x3h 0.5x,
+x6 3-4x of it).
 """
 import json
 import os
@@ -29,16 +32,22 @@ from oracle import sfno_ref  # noqa: E402
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
 
-# (filter, nlat, nlon, lmax, B): the fused MLP (C = 256) on ragged tiles, both filters
-CASES = [("non-linear", 90, 180, 45, 2), ("linear", 45, 96, 23, 1)]
+# (filter, nlat, nlon, lmax, B, wide): the fused MLP (C = 256) on ragged tiles, both
+# filters; wide: channel magnitudes spread over 10^-3 .. 10^4 (the x3h operand scaling
+# of the inner skip: per-channel powers of two from the norm0 statistics)
+CASES = [("non-linear", 90, 180, 45, 2, False), ("linear", 45, 96, 23, 1, False),
+         ("non-linear", 46, 96, 23, 2, True)]
 
 
-def _inputs(filter_type, nlat, nlon, lmax, B, seed=11):
+def _inputs(filter_type, nlat, nlon, lmax, B, wide=False, seed=11):
     C = 256
     cfg = sfno_ref.BlockCfg(filter_type=filter_type)
     p = sfno_ref.make_block_params(C, lmax, lmax + 1, cfg, seed=seed, randomize_affine=True)
     g = torch.Generator().manual_seed(seed + 1)
     x = torch.randn(B, C, nlat, nlon, generator=g)
+    if wide:
+        x = x * torch.pow(10.0, -3.0 + 7.0 * torch.rand(1, C, 1, 1, generator=g)) + \
+            torch.randn(B, C, 1, 1, generator=g)
     gamma = 0.2 * torch.randn(B, C, generator=g)
     beta = 0.2 * torch.randn(B, C, generator=g)
     return cfg, p, x, gamma, beta
@@ -52,6 +61,14 @@ def _fp64(case):
     with torch.no_grad():
         return sfno_ref.block_forward(p64, x.double(), sht, isht, cfg, gamma.double(),
                                       beta.double(), 0.7)
+
+
+def _fp32(case):
+    cfg, p, x, gamma, beta = _inputs(*case)
+    nlat, nlon, lmax = case[1:4]
+    sht, isht = sfno_ref.make_transforms(nlat, nlon, lmax, lmax + 1)
+    with torch.no_grad():
+        return sfno_ref.block_forward(p, x, sht, isht, cfg, gamma, beta, 0.7).double()
 
 
 def _gpu(case):
@@ -84,9 +101,13 @@ def test_x3h_block_as_accurate_as_x6():
     x6 = _in_child("x6")
     x3h = _in_child("x3h")
     for case, (e6, ymax), (e3, _) in zip(CASES, x6, x3h):
-        print(f"{case}: max-abs vs fp64  x6 {e6:.3e}  x3h {e3:.3e}  (|y|max {ymax:.3f})")
-        assert e3 < max(2.0 * e6, 1e-6 * max(1.0, ymax)), (case, e3, e6)
-        assert e3 < 1e-5 * max(1.0, ymax), (case, e3)
+        e32 = (_fp32(case) - _fp64(case)).abs().max().item()
+        ymax = max(ymax, 1.0)
+        print(f"{case}: max-abs vs fp64  x6 {e6:.3e}  x3h {e3:.3e}  cpu-fp32 {e32:.3e}"
+              f"  (|y|max {ymax:.3f})")
+        assert e3 < max(2.0 * e6, 1e-6 * ymax), (case, e3, e6)
+        assert e3 < max(2.0 * e32, 1e-6 * ymax), (case, e3, e32)
+        assert e3 < 1e-5 * ymax, (case, e3)
 
 
 if __name__ == "__main__":
