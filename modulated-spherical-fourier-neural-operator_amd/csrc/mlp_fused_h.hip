@@ -48,14 +48,12 @@ typedef float floatx4 __attribute__((ext_vector_type(4)));
 typedef float f2v __attribute__((ext_vector_type(2)));
 
 constexpr int MH_C = 256, MH_H = 512;
-constexpr int MH_WAVES = 4, MH_PX = 16 * MH_WAVES;  // pixels per workgroup tile
+constexpr int MH_WAVES = 4;
 constexpr int MH_HB = MH_H / 32;                    // hidden blocks
 constexpr int MH_PLANE = 4096;                      // fp16 per plane within a slice
 constexpr int MH_SLICE = 2 * MH_PLANE;              // fp16 per 16-KB slice
 constexpr int MH_NS = 4;                            // ring slots
 constexpr int MH_NSLICE = 4 * MH_HB;                // slices per tile
-constexpr int MH_RING_BYTES = MH_NS * MH_SLICE * 2;
-constexpr int MH_LDS = MH_RING_BYTES + 2 * MH_H * 4;  // ring + b1 + 1 / s1
 constexpr int64_t MH_IMG_ELEMS = (int64_t)MH_NSLICE * MH_SLICE;  // before the scales
 
 struct MlpHParams {
@@ -202,103 +200,170 @@ __device__ __forceinline__ void glds16x4(uint64_t sbase, const uint32_t (&voff)[
       : "memory", "scc");
 }
 
-template <int AHEAD>
-__global__ __launch_bounds__(256, 2) void mlp_fused_h_kernel(MlpHParams p) {
-  __shared__ __attribute__((aligned(16))) char lds_raw[MH_LDS];
+// NG: 16-pixel groups per wave (1: two workgroups of 64 pixels per CU; 2: one
+// workgroup of 128 pixels per CU, a wave's A fragment feeding both groups — half the
+// LDS fragment reads and half the weight stream per pixel, 1 wave per SIMD with the
+// output accumulators in AGPRs).  NS: ring slots (NS - 2 slices in flight while one
+// is consumed).  DBG (diagnostic timing builds only, wrong results; MSFNO_MH_DBG):
+// 1 no weight slices streamed after the first NS (stale ring), 2 no MFMAs, 4 no LDS
+// fragment reads (A from registers)
+// W waves per workgroup: 4 (two workgroups per CU) or 8 (one workgroup of 128 pixels
+// per CU sharing one weight stream: half the L2 -> LDS slice traffic per pixel)
+// two pieces (as glds16x4)
+template <int LDS_STEP>
+__device__ __forceinline__ void glds16x2(uint64_t sbase, const uint32_t (&voff)[4], uint32_t lds) {
+  unsigned keep;
+  sbase = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(sbase >> 32)) << 32) |
+          (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)sbase);
+  lds = (uint32_t)__builtin_amdgcn_readfirstlane((int)lds);
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %4\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %2, %1\n\t"
+      "s_add_u32 m0, m0, %5\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %3, %1\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "s"(sbase), "v"(voff[0]), "v"(voff[1]), "s"(lds), "i"(LDS_STEP)
+      : "memory", "scc");
+}
+
+template <int AHEAD, int DBG = 0, int NG = 1, int NS = MH_NS, int W = MH_WAVES>
+__global__ __launch_bounds__(64 * W, (NG == 1 && W == 4) ? 2 : 1) void mlp_fused_h_kernel(MlpHParams p) {
+  static_assert(W == 4 || W == 8, "4 or 8 waves");
+  constexpr int PPW = 16 / W;  // 1-KB DMA pieces per wave and slice
+  constexpr int RING_BYTES = NS * MH_SLICE * 2;
+  constexpr int TPX = 16 * NG * W;  // pixels per workgroup tile
+  __shared__ __attribute__((aligned(16))) char lds_raw[RING_BYTES + 2 * (MH_H + MH_C) * 4];
   unsigned short* const ring = reinterpret_cast<unsigned short*>(lds_raw);
-  float* const b1s = reinterpret_cast<float*>(lds_raw + MH_RING_BYTES);
+  float* const b1s = reinterpret_cast<float*>(lds_raw + RING_BYTES);
   float* const is1s = b1s + MH_H;
+  float* const b2s = is1s + MH_H;  // the epilogue's vectors (no global loads there)
+  float* const is2s = b2s + MH_C;
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r16 = lane & 15, g = lane >> 4;
   const int lin = xcd_remap(blockIdx.x, gridDim.x);
   const int z = lin / p.tiles_per_field;
   const int64_t P = p.P;
-  const int64_t px = (int64_t)(lin - z * p.tiles_per_field) * MH_PX + 16 * wave + r16;
-  const bool valid = px < P;
-  const int64_t pxc = valid ? px : P - 1;
+  const int64_t px0 = (int64_t)(lin - z * p.tiles_per_field) * TPX + 16 * NG * wave + r16;
 
-  // ---- slices 0..3 in flight ---------------------------------------------------------
+  // ---- slices 0..NS-1 in flight --------------------------------------------------------
   const uint32_t ring_lds = lds_addr(ring);
   const int wave_u = __builtin_amdgcn_readfirstlane(wave);
   uint32_t piece_off[4];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) piece_off[i] = (uint32_t)(i * MH_WAVES * 1024 + lane * 16);
+  for (int i = 0; i < 4; ++i) piece_off[i] = (uint32_t)(i * W * 1024 + lane * 16);
   auto issue = [&](int q) {
     const uint64_t src = reinterpret_cast<uint64_t>(mh_slice_src(p, q)) + (uint64_t)wave_u * 1024;
-    const uint32_t base = ring_lds + (uint32_t)((q % MH_NS) * MH_SLICE * 2 + wave_u * 1024);
-    glds16x4<MH_WAVES * 1024>(src, piece_off, base);
+    const uint32_t base = ring_lds + (uint32_t)((q % NS) * MH_SLICE * 2 + wave_u * 1024);
+    if constexpr (PPW == 4)
+      glds16x4<W * 1024>(src, piece_off, base);
+    else
+      glds16x2<W * 1024>(src, piece_off, base);
   };
 #pragma unroll
-  for (int q = 0; q < MH_NS; ++q) issue(q);
+  for (int q = 0; q < NS; ++q) issue(q);
 
   // ---- x1 -> normalised fp16x2 B fragments (k-step ks: channels 32 ks + 8 g + 0..7) --
-  const float* xcol = p.x1 + (int64_t)z * MH_C * P + pxc;
   const float* sc = p.scale + (int64_t)z * MH_C;
   const float* sh = p.shift + (int64_t)z * MH_C;
-  half8 xf[8][2];
+  half8 xf[NG][8][2];
 #pragma unroll
-  for (int ks = 0; ks < 8; ++ks) {
-    const int c0 = 32 * ks + 8 * g;
-    float xv[8];
+  for (int gr = 0; gr < NG; ++gr) {
+    const int64_t px = px0 + 16 * gr;
+    const float* xcol = p.x1 + (int64_t)z * MH_C * P + (px < P ? px : P - 1);
 #pragma unroll
-    for (int e = 0; e < 8; ++e) xv[e] = __builtin_nontemporal_load(xcol + (int64_t)(c0 + e) * P);
-    const float4 sa = *reinterpret_cast<const float4*>(sc + c0);
-    const float4 sb = *reinterpret_cast<const float4*>(sc + c0 + 4);
-    const float4 ta = *reinterpret_cast<const float4*>(sh + c0);
-    const float4 tb = *reinterpret_cast<const float4*>(sh + c0 + 4);
-    const float sv[8] = {sa.x, sa.y, sa.z, sa.w, sb.x, sb.y, sb.z, sb.w};
-    const float tv[8] = {ta.x, ta.y, ta.z, ta.w, tb.x, tb.y, tb.z, tb.w};
-    uint32_t t[2][4];
+    for (int ks = 0; ks < 8; ++ks) {
+      const int c0 = 32 * ks + 8 * g;
+      float xv[8];
 #pragma unroll
-    for (int e = 0; e < 4; ++e)
-      split2h(fmaf(sv[2 * e], xv[2 * e], tv[2 * e]), fmaf(sv[2 * e + 1], xv[2 * e + 1], tv[2 * e + 1]),
-              t[0][e], t[1][e]);
+      for (int e = 0; e < 8; ++e) xv[e] = __builtin_nontemporal_load(xcol + (int64_t)(c0 + e) * P);
+      const float4 sa = *reinterpret_cast<const float4*>(sc + c0);
+      const float4 sb = *reinterpret_cast<const float4*>(sc + c0 + 4);
+      const float4 ta = *reinterpret_cast<const float4*>(sh + c0);
+      const float4 tb = *reinterpret_cast<const float4*>(sh + c0 + 4);
+      const float sv[8] = {sa.x, sa.y, sa.z, sa.w, sb.x, sb.y, sb.z, sb.w};
+      const float tv[8] = {ta.x, ta.y, ta.z, ta.w, tb.x, tb.y, tb.z, tb.w};
+      uint32_t t[2][4];
 #pragma unroll
-    for (int pl = 0; pl < 2; ++pl) xf[ks][pl] = mh_frag(t[pl][0], t[pl][1], t[pl][2], t[pl][3]);
+      for (int e = 0; e < 4; ++e)
+        split2h(fmaf(sv[2 * e], xv[2 * e], tv[2 * e]), fmaf(sv[2 * e + 1], xv[2 * e + 1], tv[2 * e + 1]),
+                t[0][e], t[1][e]);
+#pragma unroll
+      for (int pl = 0; pl < 2; ++pl) xf[gr][ks][pl] = mh_frag(t[pl][0], t[pl][1], t[pl][2], t[pl][3]);
+    }
   }
-  floatx4 oacc[16];
+  floatx4 oacc[NG][16];
 #pragma unroll
-  for (int ot = 0; ot < 16; ++ot) oacc[ot] = floatx4{0.f, 0.f, 0.f, 0.f};
-  for (int i = tid; i < MH_H; i += 256) {
+  for (int gr = 0; gr < NG; ++gr)
+#pragma unroll
+    for (int ot = 0; ot < 16; ++ot) oacc[gr][ot] = floatx4{0.f, 0.f, 0.f, 0.f};
+  for (int i = tid; i < MH_H; i += 64 * W) {
     b1s[i] = p.b1[i];
     is1s[i] = p.inv_s1[i];
   }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // slices 0-3 and every load landed
+  for (int i = tid; i < MH_C; i += 64 * W) {
+    b2s[i] = p.b2 ? p.b2[i] : 0.f;
+    is2s[i] = p.inv_s2[i];
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the first NS slices and every load landed
   __syncthreads();
 
-  floatx4 hacc[2][2];  // [parity][tile]
+  floatx4 hacc[2][2][NG];  // [parity][tile][group]
 #pragma unroll
   for (int a = 0; a < 2; ++a)
 #pragma unroll
-    for (int t = 0; t < 2; ++t) hacc[a][t] = floatx4{0.f, 0.f, 0.f, 0.f};
-  uint32_t hfu[2][4];  // fc2 B fragment of the converted block [plane][pair]
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int gr = 0; gr < NG; ++gr) hacc[a][t][gr] = floatx4{0.f, 0.f, 0.f, 0.f};
+  uint32_t hfu[NG][2][4];  // fc2 B fragment of the converted block [group][plane][pair]
 
   const int a_lane = r16 * 32 + 8 * (g ^ mh_swz(r16));
+  // A fragment read (DBG & 4: from registers instead of LDS, diagnostic)
+  auto afrag = [&](const unsigned short* q, int u, int pl) -> half8 {
+    if constexpr ((DBG & 4) != 0) return xf[0][u & 7][pl];
+    return *reinterpret_cast<const half8*>(q);
+  };
 
-  // step q: slice q landed for every wave (slices q + 1, q + 2 may stay in flight);
-  // the slot of slice q - 1 is free and takes slice q + 3
+  // step q: slice q landed for every wave (slices up to q + NS - 2 may stay in flight);
+  // the slot of slice q - 1 is free and takes slice q + NS - 1
   auto step_begin = [&](int q) {
-    const int after = min(2, MH_NSLICE - 1 - q);
-    if (after >= 2)
-      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-    else if (after == 1)
-      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    else
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const int after = (DBG & 1) ? 0 : min(NS - 2, MH_NSLICE - 1 - q);
+    if constexpr (PPW != 4) {
+      wait_vmcnt(after * PPW);
+    } else if constexpr (NS >= 8) {
+      if (after >= 6) asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
+      else if (after == 5) asm volatile("s_waitcnt vmcnt(20)" ::: "memory");
+      else if (after == 4) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+      else if (after == 3) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+      else if (after == 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      else if (after == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else {
+      if (after >= 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      else if (after == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
-    return ring + (q % MH_NS) * MH_SLICE;
+    return ring + (q % NS) * MH_SLICE;
   };
   auto refill = [&](int q) {
-    if (q >= 1 && q + 3 < MH_NSLICE) issue(q + 3);
+    if ((DBG & 1) == 0 && q >= 1 && q + NS - 1 < MH_NSLICE) issue(q + NS - 1);
   };
 
-  auto mfma3 = [](const half8 (&a)[2], const half8 (&b)[2], floatx4 c) {
-    c = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[1], b[0], c, 0, 0, 0);
-    c = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[0], b[1], c, 0, 0, 0);
-    c = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[0], b[0], c, 0, 0, 0);
-    return c;
+  // c[gr] += a (x) b[gr], three fp16 MFMAs each, the groups interleaved
+  auto mfma3 = [](const half8 (&a)[2], const half8 (&b)[NG][2], floatx4 (&c)[NG]) {
+    if constexpr ((DBG & 2) != 0) {  // keep the fragment reads alive
+#pragma unroll
+      for (int gr = 0; gr < NG; ++gr) c[gr][0] += (float)a[0][0] + (float)a[1][0] + (float)b[gr][0][0];
+      return;
+    }
+#pragma unroll
+    for (int gr = 0; gr < NG; ++gr) c[gr] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[1], b[gr][0], c[gr], 0, 0, 0);
+#pragma unroll
+    for (int gr = 0; gr < NG; ++gr) c[gr] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[0], b[gr][1], c[gr], 0, 0, 0);
+#pragma unroll
+    for (int gr = 0; gr < NG; ++gr) c[gr] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[0], b[gr][0], c[gr], 0, 0, 0);
   };
 
   // pair e2 (0..3) of hidden block j in hacc[PAR]: unscale, + b1, GELU(erf), split -> hfu
@@ -308,9 +373,12 @@ __global__ __launch_bounds__(256, 2) void mlp_fused_h_kernel(MlpHParams p) {
     const int row = 32 * j + 16 * t + 4 * g + i;
     const float2 b = *reinterpret_cast<const float2*>(b1s + row);
     const float2 is = *reinterpret_cast<const float2*>(is1s + row);
-    f32x2 v = {fmaf(hacc[PAR][t][i], is.x, b.x), fmaf(hacc[PAR][t][i + 1], is.y, b.y)};
-    v = gelu_erf2(v);
-    split2h(v.x, v.y, hfu[0][e2], hfu[1][e2]);
+#pragma unroll
+    for (int gr = 0; gr < NG; ++gr) {
+      f32x2 v = {fmaf(hacc[PAR][t][gr][i], is.x, b.x), fmaf(hacc[PAR][t][gr][i + 1], is.y, b.y)};
+      v = gelu_erf2(v);
+      split2h(v.x, v.y, hfu[gr][0][e2], hfu[gr][1][e2]);
+    }
   };
 
   auto fc1_step = [&](const unsigned short* slot, int q, auto kh_c, auto par_c, auto conv_c,
@@ -323,15 +391,21 @@ __global__ __launch_bounds__(256, 2) void mlp_fused_h_kernel(MlpHParams p) {
 #pragma unroll
     for (int k = 0; k < AHEAD; ++k)
 #pragma unroll
-      for (int pl = 0; pl < 2; ++pl) a[k][pl] = *reinterpret_cast<const half8*>(slot + aoff(k, pl));
+      for (int pl = 0; pl < 2; ++pl) a[k][pl] = afrag(slot + aoff(k, pl), k, pl);
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
       if (u + AHEAD < 8) {
 #pragma unroll
         for (int pl = 0; pl < 2; ++pl)
-          a[(u + AHEAD) % (AHEAD + 1)][pl] = *reinterpret_cast<const half8*>(slot + aoff(u + AHEAD, pl));
+          a[(u + AHEAD) % (AHEAD + 1)][pl] = afrag(slot + aoff(u + AHEAD, pl), u + AHEAD, pl);
       }
-      hacc[PAR][u & 1] = mfma3(a[u % (AHEAD + 1)], xf[KH * 4 + (u >> 1)], hacc[PAR][u & 1]);
+      half8 xb[NG][2];
+#pragma unroll
+      for (int gr = 0; gr < NG; ++gr) {
+        xb[gr][0] = xf[gr][KH * 4 + (u >> 1)][0];
+        xb[gr][1] = xf[gr][KH * 4 + (u >> 1)][1];
+      }
+      mfma3(a[u % (AHEAD + 1)], xb, hacc[PAR][u & 1]);
       if (u == 0) refill(q);
       if constexpr (CONV) {
         if (u == 2 || u == 6) conv_pair(jc, 2 * KH + (u >> 2), PPrev{});
@@ -339,27 +413,38 @@ __global__ __launch_bounds__(256, 2) void mlp_fused_h_kernel(MlpHParams p) {
     }
     if constexpr (CONV && KH == 1) {
 #pragma unroll
-      for (int t = 0; t < 2; ++t) hacc[PAR ^ 1][t] = floatx4{0.f, 0.f, 0.f, 0.f};
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int gr = 0; gr < NG; ++gr) hacc[PAR ^ 1][t][gr] = floatx4{0.f, 0.f, 0.f, 0.f};
     }
   };
   auto fc2_step = [&](const unsigned short* slot, int q, auto oh_c) {
     constexpr int OH = decltype(oh_c)::value;
     auto aoff = [&](int u, int pl) { return (pl * 8 + u) * 512 + a_lane; };
-    const half8 hb[2] = {mh_frag(hfu[0][0], hfu[0][1], hfu[0][2], hfu[0][3]),
-                         mh_frag(hfu[1][0], hfu[1][1], hfu[1][2], hfu[1][3])};
+    half8 hb[NG][2];
+#pragma unroll
+    for (int gr = 0; gr < NG; ++gr) {
+      hb[gr][0] = mh_frag(hfu[gr][0][0], hfu[gr][0][1], hfu[gr][0][2], hfu[gr][0][3]);
+      hb[gr][1] = mh_frag(hfu[gr][1][0], hfu[gr][1][1], hfu[gr][1][2], hfu[gr][1][3]);
+    }
     half8 a[AHEAD + 1][2];
 #pragma unroll
     for (int k = 0; k < AHEAD; ++k)
 #pragma unroll
-      for (int pl = 0; pl < 2; ++pl) a[k][pl] = *reinterpret_cast<const half8*>(slot + aoff(k, pl));
+      for (int pl = 0; pl < 2; ++pl) a[k][pl] = afrag(slot + aoff(k, pl), k, pl);
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
       if (u + AHEAD < 8) {
 #pragma unroll
         for (int pl = 0; pl < 2; ++pl)
-          a[(u + AHEAD) % (AHEAD + 1)][pl] = *reinterpret_cast<const half8*>(slot + aoff(u + AHEAD, pl));
+          a[(u + AHEAD) % (AHEAD + 1)][pl] = afrag(slot + aoff(u + AHEAD, pl), u + AHEAD, pl);
       }
-      oacc[OH * 8 + u] = mfma3(a[u % (AHEAD + 1)], hb, oacc[OH * 8 + u]);
+      floatx4 c[NG];
+#pragma unroll
+      for (int gr = 0; gr < NG; ++gr) c[gr] = oacc[gr][OH * 8 + u];
+      mfma3(a[u % (AHEAD + 1)], hb, c);
+#pragma unroll
+      for (int gr = 0; gr < NG; ++gr) oacc[gr][OH * 8 + u] = c[gr];
       if (u == 0) refill(q);
     }
   };
@@ -383,26 +468,46 @@ __global__ __launch_bounds__(256, 2) void mlp_fused_h_kernel(MlpHParams p) {
   }
 #pragma unroll
   for (int e2 = 0; e2 < 4; ++e2) conv_pair(MH_HB - 1, e2, I1{});
+  // the residual of every output row, all loads in flight at once and under the last
+  // two steps' MFMAs (the x1 fragments are dead: their registers take it)
+  float rv[NG][16][4];
+  if (p.resid) {
+#pragma unroll
+    for (int gr = 0; gr < NG; ++gr) {
+      const int64_t px = px0 + 16 * gr;
+      const float* rs = p.resid + (int64_t)z * MH_C * P + (px < P ? px : P - 1);
+#pragma unroll
+      for (int ot = 0; ot < 16; ++ot)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          rv[gr][ot][i] = __builtin_nontemporal_load(rs + (int64_t)(16 * ot + 4 * g + i) * P);
+    }
+  } else {
+#pragma unroll
+    for (int gr = 0; gr < NG; ++gr)
+#pragma unroll
+      for (int ot = 0; ot < 16; ++ot)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) rv[gr][ot][i] = 0.f;
+  }
   fc2_step(step_begin(MH_NSLICE - 2), MH_NSLICE - 2, I0{});
   fc2_step(step_begin(MH_NSLICE - 1), MH_NSLICE - 1, I1{});
 
   // ---- epilogue: unscale + b2 + residual, store (rows 16 ot + 4 g + i) ----------------
-  if (valid) {
+#pragma unroll
+  for (int gr = 0; gr < NG; ++gr) {
+    const int64_t px = px0 + 16 * gr;
+    if (px >= P) continue;
     float* o = p.out + (int64_t)z * MH_C * P + px;
-    const float* rs = p.resid ? p.resid + (int64_t)z * MH_C * P + px : nullptr;
 #pragma unroll
     for (int ot = 0; ot < 16; ++ot) {
       const int r0 = 16 * ot + 4 * g;
-      const float4 is = *reinterpret_cast<const float4*>(p.inv_s2 + r0);
-      float4 b = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (p.b2) b = *reinterpret_cast<const float4*>(p.b2 + r0);
+      const float4 is = *reinterpret_cast<const float4*>(is2s + r0);
+      const float4 b = *reinterpret_cast<const float4*>(b2s + r0);
       const float isv[4] = {is.x, is.y, is.z, is.w}, bv[4] = {b.x, b.y, b.z, b.w};
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        float v = fmaf(oacc[ot][i], isv[i], bv[i]);
-        if (rs) v += __builtin_nontemporal_load(rs + (int64_t)(r0 + i) * P);
-        o[(int64_t)(r0 + i) * P] = v;
-      }
+      for (int i = 0; i < 4; ++i)
+        o[(int64_t)(r0 + i) * P] = fmaf(oacc[gr][ot][i], isv[i], bv[i]) + rv[gr][ot][i];
     }
   }
 }
@@ -450,10 +555,41 @@ int launch_mlp_fused_h(const float* x1, const float* scale, const float* shift, 
   p.inv_s1 = sc;
   p.inv_s2 = sc + MH_H;
   p.b1 = b1; p.b2 = b2; p.P = P;
-  p.tiles_per_field = (int)cdiv(P, MH_PX);
+  // MSFNO_MH_NG: 16-pixel groups per wave (1 or 2); MSFNO_MH_W: waves per workgroup
+  // (4: two workgroups per CU, 8: one workgroup of 128 pixels per CU)
+  static const int ng = [] {
+    const char* e = getenv("MSFNO_MH_NG");
+    return (e && atoi(e) == 2) ? 2 : 1;
+  }();
+  static const int nw = [] {
+    const char* e = getenv("MSFNO_MH_W");
+    return (e && atoi(e) == 8) ? 8 : 4;
+  }();
+  static const int dbg = [] {
+    const char* e = getenv("MSFNO_MH_DBG");
+    return e ? atoi(e) : 0;
+  }();
+  const int waves = ng == 2 ? 4 : nw;
+  p.tiles_per_field = (int)cdiv(P, 16 * ng * waves);
   const int64_t tiles = (int64_t)B * p.tiles_per_field;
   MSFNO_REQUIRE(tiles < (1LL << 31), MSFNO_EINVAL, "mlp_fused_h: grid too large");
-  hipLaunchKernelGGL((mlp_fused_h_kernel<2>), dim3((unsigned)tiles), dim3(256), 0, s, p);
+  void (*kern)(MlpHParams);
+  if (ng == 2)
+    kern = dbg == 1 ? mlp_fused_h_kernel<2, 1, 2, 8>
+         : dbg == 2 ? mlp_fused_h_kernel<2, 2, 2, 8>
+         : dbg == 3 ? mlp_fused_h_kernel<2, 3, 2, 8> : mlp_fused_h_kernel<2, 0, 2, 8>;
+  else if (nw == 8)
+    kern = dbg == 1 ? mlp_fused_h_kernel<2, 1, 1, 8, 8>
+         : dbg == 7 ? mlp_fused_h_kernel<2, 7, 1, 8, 8> : mlp_fused_h_kernel<2, 0, 1, 8, 8>;
+  else
+    kern = dbg == 1 ? mlp_fused_h_kernel<2, 1>
+         : dbg == 2 ? mlp_fused_h_kernel<2, 2>
+         : dbg == 3 ? mlp_fused_h_kernel<2, 3>
+         : dbg == 4 ? mlp_fused_h_kernel<2, 4>
+         : dbg == 5 ? mlp_fused_h_kernel<2, 5>
+         : dbg == 6 ? mlp_fused_h_kernel<2, 6>
+         : dbg == 7 ? mlp_fused_h_kernel<2, 7> : mlp_fused_h_kernel<2>;
+  hipLaunchKernelGGL(kern, dim3((unsigned)tiles), dim3(64 * waves), 0, s, p);
   return launch_check("mlp_fused_h");
 }
 
