@@ -300,24 +300,13 @@ static GemmTile leg_tile(int inverse) {
   return inverse ? role_tile(ROLE_LEGI, TILE_128x128) : role_tile(ROLE_LEG, TILE_128x64);
 }
 
-int ensure_desc(msfno_sht_plan_s* p, int R, int other_ld, int64_t ldT) {
-  // forward: A = Xt slab (R x K), B = table, C = S (ld ldT)
-  // inverse: A = S (ld ldT), B = table, C = Yt slab (R x N)
-  // symmetric plans: one even-parity and one odd-parity problem per m
-  if (p->desc_R == R && p->d_desc) return MSFNO_OK;
-  int bm, bn;
-  gemm_tile_dims(leg_tile(p->inverse), &bm, &bn);
-  std::vector<GemmDesc> d;
-  int tiles = 0;
+// the per-(m, parity) Legendre problems of a plan for R rows, in launch order:
+// forward A = Xt slab (R x K), B = table, C = S (ld ldT); inverse A = S (ld ldT),
+// B = table, C = Yt slab (R x N); symmetric plans: one even- and one odd-parity
+// problem per m (tiles not set)
+static void leg_problems(const msfno_sht_plan_s* p, int R, int64_t ldT,
+                         const std::function<void(GemmDesc)>& push) {
   const SpecLayout& L = p->spec;
-  auto push = [&](GemmDesc g) {
-    g.tiles_m = (int)cdiv(g.M, bm);
-    g.tiles_n = (int)cdiv(g.N, bn);
-    if (g.tiles_m * g.tiles_n == 0) return;
-    g.tile_start = tiles;
-    tiles += g.tiles_m * g.tiles_n;
-    d.push_back(g);
-  };
   const int ldko = (int)round_up(p->Ko, 4);
   for (int m = 0; m < L.mact; ++m) {
     if (L.L[m] == 0) continue;  // m outside a sharded plan's m-set
@@ -402,6 +391,22 @@ int ensure_desc(msfno_sht_plan_s* p, int R, int other_ld, int64_t ldT) {
       push(o);  // also for lo == 0 (K = 0 writes zeros): transpose_inv_sym reads O
     }
   }
+}
+
+int ensure_desc(msfno_sht_plan_s* p, int R, int other_ld, int64_t ldT) {
+  if (p->desc_R == R && p->d_desc) return MSFNO_OK;
+  int bm, bn;
+  gemm_tile_dims(leg_tile(p->inverse), &bm, &bn);
+  std::vector<GemmDesc> d;
+  int tiles = 0;
+  leg_problems(p, R, ldT, [&](GemmDesc g) {
+    g.tiles_m = (int)cdiv(g.M, bm);
+    g.tiles_n = (int)cdiv(g.N, bn);
+    if (g.tiles_m * g.tiles_n == 0) return;
+    g.tile_start = tiles;
+    tiles += g.tiles_m * g.tiles_n;
+    d.push_back(g);
+  });
   (void)other_ld;
   if (p->d_desc) MSFNO_CHECK_HIP(hipFree(p->d_desc));
   p->d_desc = nullptr;
@@ -411,6 +416,67 @@ int ensure_desc(msfno_sht_plan_s* p, int R, int other_ld, int64_t ldT) {
   p->ndesc = (int)d.size();
   p->desc_tiles = tiles;
   p->desc_R = R;
+  return MSFNO_OK;
+}
+
+// ---- x3h Legendre (legendre_x3.hip) -------------------------------------------------
+// The same problems on the x3h engine: the table as a column-scaled two-plane fp16
+// image ([plane][n][Kp] per problem, built on first use after a table load), A split
+// in-kernel under per-row scales.  Opt-in (MSFNO_LEG_X3=1): measured slower than the
+// fp32-MFMA descriptor GEMM at 721x1440 (side stream off: forward 0.40 vs 0.38 ms,
+// inverse 0.60 vs 0.53 ms with 128x64 tiles; 128x192 tiles slower still) — these
+// narrow problems are bound by their per-tile latency, not by matrix-core cycles
+// (DESIGN.md §8).
+bool leg_x3_enabled() {
+  static const bool on = [] {
+    const char* e = getenv("MSFNO_LEG_X3");
+    return e && e[0] == '1' && gemm_use_x6();
+  }();
+  return on;
+}
+
+static int ensure_desc3(msfno_sht_plan_s* p, int R, int64_t ldT, hipStream_t s) {
+  if (p->desc3_R == R && p->d_desc3 && p->tab3_valid) return MSFNO_OK;
+  std::vector<GemmDesc> d;
+  int tiles = 0;
+  int64_t img = 0, sc = 0;
+  leg_problems(p, R, ldT, [&](GemmDesc g) {
+    g.tiles_m = (int)cdiv(g.M, X3D_BM);
+    g.tiles_n = (int)cdiv(g.N, x3d_bn(p->inverse));
+    // every problem gets its image, also K = 0 ones (written as zeros)
+    g.offBx = img;
+    g.offBs = sc;
+    img += 2LL * g.N * round_up(std::max(g.K, 1), X3D_BK);
+    sc += g.N;
+    if (g.tiles_m * g.tiles_n == 0) return;
+    g.tile_start = tiles;
+    tiles += g.tiles_m * g.tiles_n;
+    d.push_back(g);
+  });
+  if (p->d_desc3) MSFNO_CHECK_HIP(hipFree(p->d_desc3));
+  p->d_desc3 = nullptr;
+  MSFNO_CHECK_HIP(hipMalloc(&p->d_desc3, std::max<size_t>(1, d.size()) * sizeof(GemmDesc)));
+  if (!d.empty())
+    MSFNO_CHECK_HIP(hipMemcpy(p->d_desc3, d.data(), d.size() * sizeof(GemmDesc), hipMemcpyHostToDevice));
+  p->ndesc3 = (int)d.size();
+  p->desc3_tiles = tiles;
+  p->desc3_R = R;
+  if (!p->tab3_valid || img > p->tab3_elems || sc > p->tab3s_elems) {
+    if (img > p->tab3_elems) {
+      if (p->tab3) MSFNO_CHECK_HIP(hipFree(p->tab3));
+      p->tab3 = nullptr;
+      MSFNO_CHECK_HIP(hipMalloc(&p->tab3, std::max<int64_t>(1, img) * sizeof(unsigned short)));
+      p->tab3_elems = img;
+    }
+    if (sc > p->tab3s_elems) {
+      if (p->tab3s) MSFNO_CHECK_HIP(hipFree(p->tab3s));
+      p->tab3s = nullptr;
+      MSFNO_CHECK_HIP(hipMalloc(&p->tab3s, std::max<int64_t>(1, sc) * sizeof(float)));
+      p->tab3s_elems = sc;
+    }
+    MSFNO_TRY(launch_legendre_x3_image(p->table, p->d_desc3, p->ndesc3, p->tab3, p->tab3s, s));
+    p->tab3_valid = 1;
+  }
   return MSFNO_OK;
 }
 
@@ -595,6 +661,16 @@ int legendre_inv_x6(msfno_sht_plan_s* g, const unsigned short* Sp, float* Yt, in
 
 int legendre_fwd(msfno_sht_plan_s* f, const float* Xt, float* S, int R, hipStream_t s,
                  const float* rowscale, int C) {
+  if (leg_x3_enabled() && !rowscale) {
+    MSFNO_TRY(ensure_desc3(f, R, f->spec.ldT, s));
+    GemmEpi e;
+    if (f->band_world) {
+      e.segA_w = f->band_seg();
+      e.segA_stride = (int64_t)f->nslab * R * 2 * f->band_W;
+    }
+    return legendre_x3(Xt, f->tab3, f->tab3s, S, f->d_desc3, f->ndesc3, f->desc3_tiles,
+                       x3d_bn(0), e, s);
+  }
   MSFNO_TRY(ensure_desc(f, R, 0, f->spec.ldT));
   GemmEpi e;
   e.rowscale = rowscale;
@@ -608,6 +684,16 @@ int legendre_fwd(msfno_sht_plan_s* f, const float* Xt, float* S, int R, hipStrea
 }
 
 int legendre_inv(msfno_sht_plan_s* g, const float* S, float* Yt, int R, hipStream_t s) {
+  if (leg_x3_enabled()) {
+    MSFNO_TRY(ensure_desc3(g, R, g->spec.ldT, s));
+    GemmEpi e;
+    if (g->band_world) {
+      e.segC_w = g->band_seg();
+      e.segC_stride = (int64_t)g->nslab * R * 2 * g->band_W;
+    }
+    return legendre_x3(S, g->tab3, g->tab3s, Yt, g->d_desc3, g->ndesc3, g->desc3_tiles,
+                       x3d_bn(1), e, s);
+  }
   MSFNO_TRY(ensure_desc(g, R, 0, g->spec.ldT));
   GemmEpi e;
   if (g->band_world) {  // Yt is the phase-1 send buffer: one block per destination rank
@@ -1409,6 +1495,9 @@ int msfno_sht_plan_destroy(msfno_sht_plan_t p) {
   if (p->d_tabx_offe) (void)hipFree(p->d_tabx_offe);
   if (p->d_tabx_offo) (void)hipFree(p->d_tabx_offo);
   if (p->d_descx) (void)hipFree(p->d_descx);
+  if (p->d_desc3) (void)hipFree(p->d_desc3);
+  if (p->tab3) (void)hipFree(p->tab3);
+  if (p->tab3s) (void)hipFree(p->tab3s);
   if (p->d_kmap) (void)hipFree(p->d_kmap);
   delete p;
   return MSFNO_OK;
@@ -1454,6 +1543,8 @@ int msfno_sht_plan_load_table(msfno_sht_plan_t p, const float* table, void* stre
   p->desc_R = -1;  // descriptors depend on the layout
   MSFNO_TRY(launch_relayout_table(*p, table, s));
   p->descx_R = -1;
+  p->desc3_R = -1;
+  p->tab3_valid = 0;  // the x3h image is rebuilt from the new table on first use
   // the bf16x3 table image only feeds the x6 Legendre GEMMs (MSFNO_LEG_X6=1)
   if (sym && leg_x6_enabled() && !p->band_world) MSFNO_TRY(build_table_x6(p, table, s));
   p->table_loaded = 1;

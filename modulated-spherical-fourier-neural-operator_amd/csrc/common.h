@@ -119,6 +119,7 @@ struct GemmDesc {
   int tiles_m, tiles_n;
   int tile_start;
   int flags;  // bit 0: apply GemmEpi::rowscale (Legendre-forward m >= 1)
+  int64_t offBx, offBs;  // x3h Legendre: the problem's table image / column scales
 };
 
 struct GemmEpi {
@@ -183,6 +184,14 @@ int launch_split_a(const float* A, unsigned short* Ax, int M, int K, int lda, in
 // the same GEMM on the x3h engine (two fp16 terms, three MFMAs; gemm_x6.hip): B rows
 // scaled by the powers of two bscale[z * K + k] while staged (every |scaled| < 2^14),
 // A re-imaged per batch into ws (>= gemm_x3_workspace); bias-only epilogue
+// x3h Legendre descriptor GEMM (legendre_x3.hip): tiles X3D_BM x x3d_bn(), k-tile X3D_BK
+constexpr int X3D_BM = 128, X3D_BK = 32;
+int x3d_bn(int inverse);
+int launch_legendre_x3_image(const float* table, const GemmDesc* descs, int ndesc,
+                             unsigned short* img, float* invs, hipStream_t s);
+int legendre_x3(const float* A, const unsigned short* img, const float* invs, float* C,
+                const GemmDesc* descs, int ndesc, int tiles, int bn, const GemmEpi& e,
+                hipStream_t s);
 size_t gemm_x3_workspace(int M, int K, int batch);
 int gemm_x3(const float* A, int lda, const float* bscale, const float* B, float* C, int M, int N,
             int K, int ldb, int ldc, int64_t sB, int64_t sC, int batch, const GemmEpi& epi,
@@ -306,6 +315,15 @@ struct msfno_sht_plan_s {
   int descx_R = -1;
   msfno::GemmDesc* d_descx = nullptr;
   int ndescx = 0, descx_tiles = 0;
+  // x3h Legendre (legendre_x3.hip): descriptor cache, the table image (two fp16
+  // planes per problem, column-scaled) and the inverse column scales
+  int desc3_R = -1;
+  msfno::GemmDesc* d_desc3 = nullptr;
+  int ndesc3 = 0, desc3_tiles = 0;
+  unsigned short* tab3 = nullptr;
+  float* tab3s = nullptr;
+  int64_t tab3_elems = 0, tab3s_elems = 0;
+  int tab3_valid = 0;
   // Latitude-band plans (band.cpp): the Legendre GEMMs read / write the all-to-all
   // buffers directly.  Their slabs are [src or dst rank p][slab][R][band_ld] blocks:
   // a K (forward) or N (inverse) column k' = p * seg + j lies in rank p's block.

@@ -181,7 +181,7 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, AccV (&acc)[M
   // epilogue VGPR-light, and the global traffic in full lines.
   float* Cs = lds;  // the main loop ended with a barrier: staging memory is free
   constexpr int QPT = (RB * WGM * BN / 4) / NTHR;  // float4 per thread per row-tile
-  constexpr int QC = QPT < 8 ? QPT : 8;
+  constexpr int QC = QPT <= 8 ? QPT : (QPT % 8 == 0 ? 8 : (QPT % 6 == 0 ? 6 : 4));
   static_assert(QPT * NTHR * 4 == RB * WGM * BN && QPT % QC == 0, "epilogue mapping");
   const bool vecC = p.vecC;
   // plane output: a thread takes two adjacent float4 (8 columns) so each plane is

@@ -1,0 +1,371 @@
+// Legendre contractions of the SHT on the "x3h" engine, for gfx950.
+//
+// The per-(m, parity) problems of the forward and inverse Legendre transform
+// (the reference's einsum in RealSHT / InverseRealSHT, driven from
+// sfnonet.py:537-555) as one descriptor launch, C[R x N] = A[R x K] · B[K x N]:
+//   forward  A = the latitude slab of one m (rows r = (b, re/im, c), K latitudes),
+//            B = the table (K latitudes x N degrees l), C = the coefficients S;
+//   inverse  A = S (K degrees), B = the table (K degrees x N latitudes), C = the slab.
+// fp32 is emulated by two fp16 terms per operand (v = v0 + v1, v0 = fp16(v),
+// v1 = fp16(v - v0)) and three fp16 MFMAs per product (a1·b0 + a0·b1 + a0·b0,
+// fp32 accumulation; Ootomo & Yokota 2022, as gemm_x6c.hip's x3h chain).  fp16's
+// range is kept by exact power-of-two scales: every row of A by sigma_r (the
+// row's max over K maps below 2^15: a pre-pass over the workgroup's rows), every
+// column of B by tau_n (its max maps into [2^14, 2^15): in the table image, built
+// once per table load).  An entry below 2^-24 of its row's (column's) maximum
+// loses its low term: an error under the fp32 rounding of the dot product it
+// enters.  The epilogue multiplies by 1 / (sigma_r tau_n).
+//
+// Tile 128 (rows) x BN (n: 192 by default, 64) x 32 (k), 4 waves as 2 x 2, each
+// 64 x BN/2 as 32x32x16 MFMA tiles; both operands k-contiguous in LDS ([plane][k16][row][16], the two
+// 16-B halves of a row swapped when (row >> 3) & 1, gemm_x6.hip's A layout), two
+// stages.  The table image is B^T: [plane][n][Kp] per problem (Kp = K rounded up
+// to 32, zero padded), so its staging is plain 16-B copies.
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <type_traits>
+
+#include "gemm_common.h"
+
+namespace msfno {
+
+namespace {
+
+typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+typedef _Float16 h2v __attribute__((ext_vector_type(2)));
+typedef float f2v __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ void x3_split(float a, float b, uint32_t& t0, uint32_t& t1) {
+  const f2v v = {a, b};
+  const h2v h0 = __builtin_convertvector(v, h2v);
+  const f2v r = v - __builtin_convertvector(h0, f2v);
+  const h2v h1 = __builtin_convertvector(r, h2v);
+  t0 = __builtin_bit_cast(uint32_t, h0);
+  t1 = __builtin_bit_cast(uint32_t, h1);
+}
+
+// 2^(s - e) for m = f 2^e, f in [0.5, 1); 1 for m = 0 or non-finite; exponent clamped
+__device__ __forceinline__ float pow2_scale(float m, int s) {
+  if (!(m > 0.f) || !isfinite(m)) return 1.f;
+  int e;
+  frexpf(m, &e);
+  return ldexpf(1.f, min(max(s - e, -100), 100));
+}
+
+// A column of a segmented (band exchange layout) operand: k -> k + block * (stride - w)
+__device__ __forceinline__ int64_t seg_k(int k, int w, int64_t stride) {
+  return w ? k + (int64_t)(k / w) * (stride - w) : k;
+}
+
+// One workgroup per problem: per column n the scale tau_n, then the image
+// [plane][n][Kp] of B^T · tau (zero padded to Kp) and 1 / tau_n.
+__global__ __launch_bounds__(256) void x3d_image_kernel(const float* __restrict__ table,
+                                                        const GemmDesc* __restrict__ descs,
+                                                        unsigned short* __restrict__ img,
+                                                        float* __restrict__ invs) {
+  const GemmDesc d = descs[blockIdx.x];
+  const float* B = table + d.offB;
+  const int K = d.K, N = d.N, ldb = d.ldb;
+  const int Kp = (max(K, 1) + X3D_BK - 1) / X3D_BK * X3D_BK;
+  unsigned short* o = img + d.offBx;
+  for (int n = threadIdx.x; n < N; n += blockDim.x) {
+    float m = 0.f;
+    for (int k = 0; k < K; ++k) m = fmaxf(m, fabsf(B[(int64_t)k * ldb + n]));
+    const float tau = pow2_scale(m, 15);
+    invs[d.offBs + n] = 1.f / tau;
+    uint32_t* o0 = reinterpret_cast<uint32_t*>(o + (int64_t)n * Kp);
+    uint32_t* o1 = reinterpret_cast<uint32_t*>(o + ((int64_t)N + n) * Kp);
+    for (int k = 0; k < Kp; k += 2) {
+      const float v0 = k < K ? B[(int64_t)k * ldb + n] * tau : 0.f;
+      const float v1 = k + 1 < K ? B[(int64_t)(k + 1) * ldb + n] * tau : 0.f;
+      uint32_t t0, t1;
+      x3_split(v0, v1, t0, t1);
+      o0[k >> 1] = t0;
+      o1[k >> 1] = t1;
+    }
+  }
+}
+
+struct X3DParams {
+  const float* A;
+  const unsigned short* img;
+  const float* invs;
+  float* C;
+  const GemmDesc* descs;
+  int ndesc;
+  int segA_w, segC_w;
+  int64_t segA_stride, segC_stride;
+  int vecC;
+};
+
+constexpr int BM = X3D_BM, BK = X3D_BK;
+constexpr int KS = BK / 16;                 // 32x32x16 k-steps per k-tile
+constexpr int A_PL = KS * BM * 16;          // fp16 per A plane in a stage
+constexpr int WGM = 2, WGN = 2, WM = BM / WGM, MT = WM / 32;
+
+__device__ __forceinline__ int swz(int row) { return (row >> 3) & 1; }
+
+// BN: 64 or 192 columns per tile (192: one tile spans a whole problem's N <= 184 — A
+// is read once, not once per 64 columns); PF: k-tiles in flight in registers (1, 2)
+template <int BN, int PF>
+__global__ __launch_bounds__(256) void legendre_x3_kernel(X3DParams p) {
+  constexpr int B_PL = KS * BN * 16;
+  constexpr int STAGE = 2 * A_PL + 2 * B_PL;  // fp16 per stage
+  constexpr int WN = BN / WGN, NT = WN / 32;
+  constexpr int NB = 2 * BN * BK / 8 / 256;  // 16-B B pieces per thread and k-tile
+  constexpr int EPI_FLOATS = 32 * WGM * (BN + 8);
+  constexpr int LDS_BYTES = (2 * STAGE * 2 > EPI_FLOATS * 4) ? 2 * STAGE * 2 : EPI_FLOATS * 4;
+  __shared__ __attribute__((aligned(16))) char lds_raw[LDS_BYTES];
+  __shared__ float sig_s[BM], isig_s[BM];
+  __shared__ float red_s[256];
+  unsigned short* const ring = reinterpret_cast<unsigned short*>(lds_raw);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WGN, wn = wave % WGN;
+  const int half = lane >> 5, l32 = lane & 31;
+
+  // ---- tile -> problem ----------------------------------------------------------------
+  const int lin = xcd_remap(blockIdx.x, gridDim.x);
+  int lo = 0, hi = p.ndesc - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (p.descs[mid].tile_start <= lin) lo = mid; else hi = mid - 1;
+  }
+  const GemmDesc d = p.descs[lo];
+  const int local = lin - d.tile_start;
+  const int tm = local % d.tiles_m, tn = local / d.tiles_m;
+  const int M = d.M, N = d.N, K = d.K, lda = d.lda;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const float* A = p.A + d.offA;
+  const int Kp = (max(K, 1) + BK - 1) / BK * BK;
+  const unsigned short* Bimg = p.img + d.offBx;
+  const int nk = (K + BK - 1) / BK;
+
+  // ---- staging: A fp32 -> two fp16 planes (row-scaled); B image 16-B copies -----------
+  // A: 128 rows x 32 k = 1024 float4, 4 per thread (thread -> row idx / 8, k 4 (idx % 8))
+  float4 ra[PF][4];
+  uint4 rb[PF][NB];
+  const int Kc = K > 0 ? K - 1 : 0;
+  auto load = [&](int kt, auto buf_c) {
+    constexpr int BUF = decltype(buf_c)::value;
+    const int k0 = kt * BK;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int idx = tid + 256 * q;
+      const int row = min(m0 + (idx >> 3), M - 1);
+      const int k = k0 + 4 * (idx & 7);
+      const float* a = A + (int64_t)row * lda;
+      ra[BUF][q] = *reinterpret_cast<const float4*>(a + seg_k(min(k, Kc & ~3), p.segA_w, p.segA_stride));
+    }
+    // B: 2 planes x BN n x 32 k fp16 = 8 BN pieces of 16 B, NB per thread
+#pragma unroll
+    for (int q = 0; q < NB; ++q) {
+      const int idx = tid + 256 * q;
+      const int pl = idx / (4 * BN), n = (idx >> 2) % BN, c = idx & 3;
+      const int ng = min(n0 + n, N - 1);
+      rb[BUF][q] = *reinterpret_cast<const uint4*>(Bimg + ((int64_t)pl * N + ng) * Kp + k0 + 8 * c);
+    }
+  };
+  auto store = [&](int st, int kt, auto buf_c) {
+    constexpr int BUF = decltype(buf_c)::value;
+    unsigned short* base = ring + st * STAGE;
+    const int k0 = kt * BK;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int idx = tid + 256 * q;
+      const int r = idx >> 3, kk = 4 * (idx & 7);  // k within the tile: 0..28
+      const bool rok = m0 + r < M;
+      const float sg = sig_s[r];
+      float v[4] = {ra[BUF][q].x, ra[BUF][q].y, ra[BUF][q].z, ra[BUF][q].w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = (rok && k0 + kk + e < K) ? v[e] * sg : 0.f;
+      uint32_t a0, a1, b0, b1;
+      x3_split(v[0], v[1], a0, a1);
+      x3_split(v[2], v[3], b0, b1);
+      const int ks = kk >> 4, c = (kk >> 3) & 1, w = kk & 7;
+      unsigned short* dst = base + (ks * BM + r) * 16 + 8 * (c ^ swz(r)) + w;
+      *reinterpret_cast<uint2*>(dst) = make_uint2(a0, b0);
+      *reinterpret_cast<uint2*>(dst + A_PL) = make_uint2(a1, b1);
+    }
+#pragma unroll
+    for (int q = 0; q < NB; ++q) {
+      const int idx = tid + 256 * q;
+      const int pl = idx / (4 * BN), n = (idx >> 2) % BN, c = idx & 3;
+      const int ks = c >> 1, hc = c & 1;
+      uint4 v = rb[BUF][q];
+      if (n0 + n >= N) v = make_uint4(0, 0, 0, 0);
+      *reinterpret_cast<uint4*>(base + 2 * A_PL + pl * B_PL + (ks * BN + n) * 16 + 8 * (hc ^ swz(n))) = v;
+    }
+  };
+
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+  // the first k-tiles' loads go out before the row-scale pass (they need no scale)
+  if (nk > 0) load(0, I0{});
+  if constexpr (PF == 2) {
+    if (nk > 1) load(1, I1{});
+  }
+  // ---- row scales: max over K of each of the tile's rows (two threads per row) -------
+  // (rows padded to 4 floats and segments to 16: a float4 at k % 4 == 0 stays in
+  // its row and block; elements past K are masked)
+  {
+    const int r = tid >> 1, h = tid & 1;
+    const int row = min(m0 + r, M - 1);
+    const float* a = A + (int64_t)row * lda;
+    float mx = 0.f;
+    if (m0 + r < M)
+      for (int k = 4 * h; k < K; k += 8) {
+        const float4 v = *reinterpret_cast<const float4*>(a + seg_k(k, p.segA_w, p.segA_stride));
+        mx = fmaxf(mx, fabsf(v.x));
+        if (k + 1 < K) mx = fmaxf(mx, fabsf(v.y));
+        if (k + 2 < K) mx = fmaxf(mx, fabsf(v.z));
+        if (k + 3 < K) mx = fmaxf(mx, fabsf(v.w));
+      }
+    red_s[tid] = mx;
+    __syncthreads();
+    if (h == 0) {
+      const float sg = pow2_scale(fmaxf(red_s[tid], red_s[tid + 1]), 15);
+      sig_s[r] = sg;
+      isig_s[r] = 1.f / sg;
+    }
+    __syncthreads();
+  }
+
+  floatx16 acc[MT][NT];
+#pragma unroll
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int j = 0; j < NT; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  auto mfma_tile = [&](int st) {
+    const unsigned short* base = ring + st * STAGE;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      h8 a[MT][2], b[NT][2];
+#pragma unroll
+      for (int i = 0; i < MT; ++i) {
+        const int row = wm * WM + i * 32 + l32;
+#pragma unroll
+        for (int pl = 0; pl < 2; ++pl)
+          a[i][pl] = *reinterpret_cast<const h8*>(base + pl * A_PL + (ks * BM + row) * 16 +
+                                                  8 * (half ^ swz(row)));
+      }
+#pragma unroll
+      for (int j = 0; j < NT; ++j) {
+        const int n = wn * WN + j * 32 + l32;
+#pragma unroll
+        for (int pl = 0; pl < 2; ++pl)
+          b[j][pl] = *reinterpret_cast<const h8*>(base + 2 * A_PL + pl * B_PL + (ks * BN + n) * 16 +
+                                                  8 * (half ^ swz(n)));
+      }
+#pragma unroll
+      for (int i = 0; i < MT; ++i)
+#pragma unroll
+        for (int j = 0; j < NT; ++j) {
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[i][1], b[j][0], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[i][0], b[j][1], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[i][0], b[j][0], acc[i][j], 0, 0, 0);
+        }
+    }
+  };
+
+  if (nk > 0) store(0, 0, I0{});
+  __syncthreads();
+  if constexpr (PF == 1) {
+    for (int kt = 0; kt < nk; ++kt) {
+      if (kt + 1 < nk) load(kt + 1, I0{});
+      mfma_tile(kt & 1);
+      if (kt + 1 < nk) store((kt + 1) & 1, kt + 1, I0{});
+      __syncthreads();
+    }
+  } else {
+    // register buffer b holds k-tiles of parity b: tile kt + 1 was loaded an iteration
+    // ago, tile kt + 2 goes into the buffer tile kt left
+    auto iter = [&](int kt, auto buf_c) {
+      constexpr int BUF = decltype(buf_c)::value;
+      using Other = std::integral_constant<int, BUF ^ 1>;
+      if (kt + 2 < nk) load(kt + 2, buf_c);
+      mfma_tile(BUF);
+      if (kt + 1 < nk) store(BUF ^ 1, kt + 1, Other{});
+      __syncthreads();
+    };
+    for (int kt = 0; kt < nk; kt += 2) {
+      iter(kt, I0{});
+      if (kt + 1 < nk) iter(kt + 1, I1{});
+    }
+  }
+
+  // ---- 1 / (sigma_r tau_n), then the shared fp32 epilogue ----------------------------
+#pragma unroll
+  for (int j = 0; j < NT; ++j) {
+    const float it = p.invs[d.offBs + min(n0 + wn * WN + j * 32 + l32, N - 1)];
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r)
+        acc[i][j][r] *= it * isig_s[wm * WM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * half];
+  }
+  GemmParams q{};
+  q.vecC = p.vecC;
+  q.segC_w = p.segC_w;
+  q.segC_stride = p.segC_stride;
+  gemm_epilogue<BM, BN, 0, WGM, WGN>(q, acc, reinterpret_cast<float*>(lds_raw), nullptr,
+                                     p.C + d.offC, nullptr, M, N, d.ldc, m0, n0, 0);
+}
+
+}  // namespace
+
+int launch_legendre_x3_image(const float* table, const GemmDesc* descs, int ndesc,
+                             unsigned short* img, float* invs, hipStream_t s) {
+  if (ndesc <= 0) return MSFNO_OK;
+  hipLaunchKernelGGL(x3d_image_kernel, dim3(ndesc), dim3(256), 0, s, table, descs, img, invs);
+  return launch_check("legendre_x3_image");
+}
+
+// tile width of the x3h Legendre problems (MSFNO_LEG_X3_BN=64|192, per direction:
+// MSFNO_LEG_X3_BN=<forward>,<inverse>)
+int x3d_bn(int inverse) {
+  static int bn[2] = {0, 0};
+  if (!bn[0]) {
+    bn[0] = bn[1] = 192;
+    if (const char* e = getenv("MSFNO_LEG_X3_BN")) {
+      int a = 0, b = 0;
+      const int n = sscanf(e, "%d,%d", &a, &b);
+      if (n >= 1) bn[0] = bn[1] = a;
+      if (n == 2) bn[1] = b;
+    }
+    for (int& v : bn)
+      if (v != 64) v = 192;
+  }
+  return bn[inverse ? 1 : 0];
+}
+
+int legendre_x3(const float* A, const unsigned short* img, const float* invs, float* C,
+                const GemmDesc* descs, int ndesc, int tiles, int bn, const GemmEpi& e,
+                hipStream_t s) {
+  if (ndesc <= 0 || tiles <= 0) return MSFNO_OK;
+  MSFNO_REQUIRE(A && img && invs && C && descs, MSFNO_EINVAL, "legendre_x3: null operand");
+  MSFNO_REQUIRE(!e.rowscale && !e.bias && !e.addend, MSFNO_EUNSUPPORTED,
+                "legendre_x3: plain epilogue only");
+  X3DParams p{};
+  p.A = A; p.img = img; p.invs = invs; p.C = C;
+  p.descs = descs; p.ndesc = ndesc;
+  p.segA_w = e.segA_w; p.segA_stride = e.segA_stride;
+  p.segC_w = e.segC_w; p.segC_stride = e.segC_stride;
+  p.vecC = (reinterpret_cast<uintptr_t>(C) & 15) == 0;  // every ldc / offC is a multiple of 4
+  static const int pf = [] {
+    const char* e = getenv("MSFNO_LEG_X3_PF");
+    return (e && e[0] == '1') ? 1 : 2;
+  }();
+  if (bn == 64)
+    hipLaunchKernelGGL((pf == 1 ? legendre_x3_kernel<64, 1> : legendre_x3_kernel<64, 2>), dim3(tiles),
+                       dim3(256), 0, s, p);
+  else
+    hipLaunchKernelGGL((pf == 1 ? legendre_x3_kernel<192, 1> : legendre_x3_kernel<192, 2>),
+                       dim3(tiles), dim3(256), 0, s, p);
+  return launch_check("legendre_x3");
+}
+
+}  // namespace msfno

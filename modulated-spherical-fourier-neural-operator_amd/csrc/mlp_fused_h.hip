@@ -392,6 +392,7 @@ __global__ __launch_bounds__(64 * W, (NG == 1 && W == 4) ? 2 : 1) void mlp_fused
     for (int k = 0; k < AHEAD; ++k)
 #pragma unroll
       for (int pl = 0; pl < 2; ++pl) a[k][pl] = afrag(slot + aoff(k, pl), k, pl);
+    if constexpr (AHEAD >= 8) __builtin_amdgcn_sched_barrier(0);  // every read issued first
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
       if (u + AHEAD < 8) {
@@ -432,6 +433,7 @@ __global__ __launch_bounds__(64 * W, (NG == 1 && W == 4) ? 2 : 1) void mlp_fused
     for (int k = 0; k < AHEAD; ++k)
 #pragma unroll
       for (int pl = 0; pl < 2; ++pl) a[k][pl] = afrag(slot + aoff(k, pl), k, pl);
+    if constexpr (AHEAD >= 8) __builtin_amdgcn_sched_barrier(0);  // every read issued first
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
       if (u + AHEAD < 8) {
@@ -565,6 +567,10 @@ int launch_mlp_fused_h(const float* x1, const float* scale, const float* shift, 
     const char* e = getenv("MSFNO_MH_W");
     return (e && atoi(e) == 8) ? 8 : 4;
   }();
+  static const int ahead = [] {  // MSFNO_MH_AHEAD: fragment reads in flight (u steps)
+    const char* e = getenv("MSFNO_MH_AHEAD");
+    return e ? atoi(e) : 2;
+  }();
   static const int dbg = [] {
     const char* e = getenv("MSFNO_MH_DBG");
     return e ? atoi(e) : 0;
@@ -581,6 +587,14 @@ int launch_mlp_fused_h(const float* x1, const float* scale, const float* shift, 
   else if (nw == 8)
     kern = dbg == 1 ? mlp_fused_h_kernel<2, 1, 1, 8, 8>
          : dbg == 7 ? mlp_fused_h_kernel<2, 7, 1, 8, 8> : mlp_fused_h_kernel<2, 0, 1, 8, 8>;
+  else if (ahead == 3)
+    kern = mlp_fused_h_kernel<3>;
+  else if (ahead == 4)
+    kern = mlp_fused_h_kernel<4>;
+  else if (ahead == 6)
+    kern = mlp_fused_h_kernel<6>;
+  else if (ahead == 8)
+    kern = mlp_fused_h_kernel<8>;
   else
     kern = dbg == 1 ? mlp_fused_h_kernel<2, 1>
          : dbg == 2 ? mlp_fused_h_kernel<2, 2>
