@@ -84,7 +84,7 @@ STAGE_KERNEL_F32 = {
 # MLP chain; the unfused fc1 / fc2 pair stays on x6
 STAGE_KERNEL_X3H = dict(STAGE_KERNEL_X6, **{
     "inner_skip": "void msfno::gemm_x6_kernel<256, 256, 4, 2, true, 1, false, 2>(msfno::GemmParams)",
-    "mlp_fused": "void msfno::(anonymous namespace)::mlp_fused_h_kernel<2>"
+    "mlp_fused": "void msfno::(anonymous namespace)::mlp_fused_h_kernel<2, 0, 1, 4, 4>"
                  "(msfno::(anonymous namespace)::MlpHParams)",
 })
 X6_STAGES = {"mlp_fc1", "mlp_fc2", "inner_skip", "mlp_fused"}
