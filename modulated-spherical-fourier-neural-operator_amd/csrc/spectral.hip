@@ -388,8 +388,9 @@ __global__ __launch_bounds__(256) void transpose_inv_sym2_kernel(const float* __
 }
 
 // tile shape (latitudes x m) of the symmetric transposes: MSFNO_TR_FWD / MSFNO_TR_INV =
-// "64x32" | "32x64" | "32x128" | "16x128" | "2p" (A/B; defaults 64x32 forward, 2p
-// inverse: 0.247-0.248 vs 0.255-0.258 ms for 16x128 in four interleaved in-block runs
+// "64x32" | "32x64" | "32x128" | "16x128" | "2p" | "v4" (A/B; defaults v4 forward: the
+// 64x32 tile with 16-B stores, 0.265 vs 0.280 ms for 64x32 in two interleaved in-block
+// runs (round 3); 2p inverse: 0.247-0.248 vs 0.255-0.258 ms for 16x128 in four interleaved in-block runs
 // at 721x1440, C = 256 (16x128: 0.257 vs 0.268 ms for 32x64); the 32x128 one-phase
 // tiles (67 KB of LDS) lose occupancy: 0.58 / 0.34 ms)
 static int tr_tile(const char* var, int dflt) {
@@ -413,7 +414,7 @@ static void fwd_sym_launch(const float2* Xn, float* Xt, int B, int C, const LatG
 static void fwd_sym_dispatch(const float2* Xn, float* Xt, int B, int C, const LatGeom& g,
                              int mmax, const float* nscale, const float* nshift, const int* perm,
                              int kpad, hipStream_t s) {
-  static const int t = tr_tile("MSFNO_TR_FWD", 0);
+  static const int t = tr_tile("MSFNO_TR_FWD", 5);
   switch (t) {
     case 1: fwd_sym_launch<32, 64>(Xn, Xt, B, C, g, mmax, nscale, nshift, perm, kpad, s); break;
     case 2: fwd_sym_launch<32, 128>(Xn, Xt, B, C, g, mmax, nscale, nshift, perm, kpad, s); break;
