@@ -574,15 +574,19 @@ int gemm_x3(const float* A, int lda, const float* bscale, const float* B, float*
   p.x3_bscale = bscale;
   p.x3_rowmul = rowmul;
   p.x3_ldrm = Mp;
+  // tiles as x6_tile (MSFNO_X6_TILE overrides: 6 = 256x256, 4 = 256x128, 0 = 128x128)
   const GemmTile tile = x6_tile(M, N, batch);
-  const bool big = tile == TILE_256x256;
-  const int bm = big ? 256 : 128, bn = big ? 256 : 128;
+  const int bm = (tile == TILE_256x256 || tile == TILE_256x128) ? 256 : 128;
+  const int bn = tile == TILE_256x256 ? 256 : 128;
   p.tiles_m = (int)cdiv(M, bm);
   p.tiles_n = (int)cdiv(N, bn);
   const dim3 grid(p.tiles_m * p.tiles_n, 1, batch);
-  if (big) {
+  if (tile == TILE_256x256) {
     if (p.bias) launch_x3_e<256, 256, 4, 2, EPI_BIAS>(p, grid, s);
     else launch_x3_e<256, 256, 4, 2, 0>(p, grid, s);
+  } else if (tile == TILE_256x128) {
+    if (p.bias) launch_x3_e<256, 128, 4, 2, EPI_BIAS>(p, grid, s);
+    else launch_x3_e<256, 128, 4, 2, 0>(p, grid, s);
   } else {
     if (p.bias) launch_x3_e<128, 128, 2, 2, EPI_BIAS>(p, grid, s);
     else launch_x3_e<128, 128, 2, 2, 0>(p, grid, s);
