@@ -301,8 +301,9 @@ __global__ void split3m_kernel(const float* __restrict__ S, unsigned short* __re
 // DBG (diagnostic timing builds only, wrong results; MSFNO_X6C_DBG): 1 no vmcnt wait
 // for the k-tile DMA, 2 no DMA in the loop at all (stale stages), 4 no MFMAs
 // LAY: bit 1 = B planes read in the tiled layout, bit 2 = planes written tiled
+// NS: LDS stages (2; 3 for the x3h DMA-fed layers: two k-tiles in flight, 144 KB)
 template <bool PLANES_OUT, int WGM = 4, int WGN = 2, bool BF32 = false, int DBG = 0, int LAY = 0,
-          int NP = 3>
+          int NP = 3, int NS = 2>
 __global__ __launch_bounds__(64 * WGM * WGN) void gemm_x6c_kernel(X6CParams p) {
   constexpr int BM = X6C_BM, BN = X6C_BN, BK = X6C_BK;
   constexpr int NW = WGM * WGN;
@@ -314,7 +315,8 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_x6c_kernel(X6CParams p) {
   constexpr int A_PLANE = BM * BK, B_PLANE = BK * BN;  // 16-bit elements per matrix plane
   constexpr int A_ALL = NMP * A_PLANE;
   constexpr int STAGE = NMP * (A_PLANE + B_PLANE);      // 72 KB (x6) / 48 KB (x3h)
-  constexpr int NSTAGE = 2;
+  constexpr int NSTAGE = NS;
+  static_assert(NS == 2 || (NS == 3 && !BF32 && DBG == 0), "three stages: DMA-fed B only");
   constexpr int RING_BYTES = NSTAGE * STAGE * 2;
   constexpr int EPI_BYTES = 32 * WGM * (BN + 8) * 4;
   constexpr int LDS_BYTES = RING_BYTES > EPI_BYTES ? RING_BYTES : EPI_BYTES;
@@ -494,24 +496,44 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_x6c_kernel(X6CParams p) {
   };
 
   issue(0, 0);
+  if constexpr (NS == 3) {
+    if (nk > 1) issue(1, 1);
+  }
   if constexpr (BF32) {
     load_bf(0);
     store_bf(0, 0);
   }
-  for (int kt = 0; kt < nk; ++kt) {
-    if constexpr ((DBG & 1) == 0)
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // my DMA of k-tile kt landed
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();  // everyone's landed; stage (kt + 1) & 1 is free
-    if (kt + 1 < nk) {
-      if constexpr ((DBG & 2) == 0) issue(kt + 1, (kt + 1) & 1);
-      if constexpr (BF32) load_bf(kt + 1);  // after the DMA: in-order vmcnt
+  if constexpr (NS == 3) {
+    // k-tiles kt and kt + 1 in flight at the top of iteration kt: wait for kt only
+    // (NPC DMA instructions per wave and k-tile), then refill the stage kt - 1 left
+    for (int kt = 0; kt < nk; ++kt) {
+      if (kt + 1 < nk)
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NPC) : "memory");
+      else
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      if (kt + 2 < nk) issue(kt + 2, (kt + 2) % 3);
+      __builtin_amdgcn_s_setprio(1);
+      mfma_tile(kt % 3);
+      __builtin_amdgcn_s_setprio(0);
     }
-    __builtin_amdgcn_s_setprio(1);
-    if constexpr ((DBG & 4) == 0) mfma_tile(kt & 1);
-    __builtin_amdgcn_s_setprio(0);
-    if constexpr (BF32) {
-      if (kt + 1 < nk) store_bf(kt + 1, (kt + 1) & 1);
+  } else {
+    for (int kt = 0; kt < nk; ++kt) {
+      if constexpr ((DBG & 1) == 0)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // my DMA of k-tile kt landed
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();  // everyone's landed; stage (kt + 1) & 1 is free
+      if (kt + 1 < nk) {
+        if constexpr ((DBG & 2) == 0) issue(kt + 1, (kt + 1) & 1);
+        if constexpr (BF32) load_bf(kt + 1);  // after the DMA: in-order vmcnt
+      }
+      __builtin_amdgcn_s_setprio(1);
+      if constexpr ((DBG & 4) == 0) mfma_tile(kt & 1);
+      __builtin_amdgcn_s_setprio(0);
+      if constexpr (BF32) {
+        if (kt + 1 < nk) store_bf(kt + 1, (kt + 1) & 1);
+      }
     }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -976,10 +998,21 @@ int gemm_x3c(const unsigned short* Aw, int co, int ci, const float* Sin, int ldS
   p.colscale = colscale;
   p.cs_b = cs_b;
   const dim3 grid(p.tiles_m * p.tiles_n, 1, B);
+  // three LDS stages for the DMA-fed layers (two k-tiles in flight): layers 1/2
+  // 0.51 -> 0.49 ms, output 0.31 -> 0.29 ms (two interleaved pairs); MSFNO_X3C_NS=2
+  // keeps two (A/B)
+  static const int ns = [] {
+    const char* e = getenv("MSFNO_X3C_NS");
+    return (e && e[0] == '2') ? 2 : 3;
+  }();
   if (Sin)
     hipLaunchKernelGGL((gemm_x6c_kernel<true, 4, 2, true, 0, 2, 2>), grid, dim3(512), 0, s, p);
+  else if (Y && ns == 3)
+    hipLaunchKernelGGL((gemm_x6c_kernel<true, 4, 2, false, 0, 3, 2, 3>), grid, dim3(512), 0, s, p);
   else if (Y)
     hipLaunchKernelGGL((gemm_x6c_kernel<true, 4, 2, false, 0, 3, 2>), grid, dim3(512), 0, s, p);
+  else if (ns == 3)
+    hipLaunchKernelGGL((gemm_x6c_kernel<false, 4, 2, false, 0, 1, 2, 3>), grid, dim3(512), 0, s, p);
   else
     hipLaunchKernelGGL((gemm_x6c_kernel<false, 4, 2, false, 0, 1, 2>), grid, dim3(512), 0, s, p);
   return launch_check("gemm_x3c");
