@@ -92,6 +92,12 @@ X6_SPEC_STAGES = {"spectral_l0", "spectral_l1", "spectral_l2", "spectral_out"}
 X3H_STAGES = {"inner_skip", "mlp_fused"} | X6_SPEC_STAGES
 
 
+def leg_x3h():
+    """The Legendre GEMMs run on the x3h engine (legendre_x3.hip) unless MSFNO_LEG_X3=0."""
+    e = os.environ.get("MSFNO_LEG_X3")
+    return e == "1" if e is not None else x3h_engine()
+
+
 def x3h_engine():
     """The x3h engine is the library default (mlp_fused_h.hip mlp_fused_h_env:
     MSFNO_ENGINE=x6 selects the six-bf16-MFMA engine instead; MSFNO_GEMM=f32 the fp32
@@ -116,7 +122,7 @@ def mlp_fused(C, hid):
 
 def mfma_peak(stage):
     dense, spec = x6_engine()
-    if x3h_engine() and stage in X3H_STAGES:
+    if (x3h_engine() and stage in X3H_STAGES) or (stage.startswith("legendre") and leg_x3h()):
         return PEAK_X3H_TFLOPS, "x3h (fp32 via 2-term fp16 split, fp16 MFMA / 3)"
     if (dense and stage in X6_STAGES) or (spec and stage in X6_SPEC_STAGES):
         return PEAK_X6_TFLOPS, "x6 (fp32 via 3-term bf16 split, bf16 MFMA / 6)"

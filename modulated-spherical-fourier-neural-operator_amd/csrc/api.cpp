@@ -399,7 +399,25 @@ int ensure_desc(msfno_sht_plan_s* p, int R, int other_ld, int64_t ldT) {
   gemm_tile_dims(leg_tile(p->inverse), &bm, &bn);
   std::vector<GemmDesc> d;
   int tiles = 0;
+  // MSFNO_LEG_COMPACT=1 (diagnostic timing only, wrong results): the S operand of every
+  // problem as its own compact [R][N] block instead of columns of the [R][ldT] rows
+  static const bool compact = [] {
+    const char* e = getenv("MSFNO_LEG_COMPACT");
+    return e && e[0] == '1';
+  }();
+  int64_t coff = 0;
   leg_problems(p, R, ldT, [&](GemmDesc g) {
+    if (compact && !p->band_world) {
+      if (!p->inverse) {
+        g.ldc = (int)round_up(g.N, 4);
+        g.offC = coff;
+        coff += (int64_t)R * g.ldc;
+      } else {
+        g.lda = (int)round_up(std::max(g.K, 1), 4);
+        g.offA = coff;
+        coff += (int64_t)R * g.lda;
+      }
+    }
     g.tiles_m = (int)cdiv(g.M, bm);
     g.tiles_n = (int)cdiv(g.N, bn);
     if (g.tiles_m * g.tiles_n == 0) return;
@@ -422,15 +440,14 @@ int ensure_desc(msfno_sht_plan_s* p, int R, int other_ld, int64_t ldT) {
 // ---- x3h Legendre (legendre_x3.hip) -------------------------------------------------
 // The same problems on the x3h engine: the table as a column-scaled two-plane fp16
 // image ([plane][n][Kp] per problem, built on first use after a table load), A split
-// in-kernel under per-row scales.  Opt-in (MSFNO_LEG_X3=1): measured slower than the
-// fp32-MFMA descriptor GEMM at 721x1440 (side stream off: forward 0.40 vs 0.38 ms,
-// inverse 0.60 vs 0.53 ms with 128x64 tiles; 128x192 tiles slower still) — these
-// narrow problems are bound by their per-tile latency, not by matrix-core cycles
-// (DESIGN.md §8).
+// in-kernel under per-(row, k-tile) scales.  Default with the x3h engine (side stream
+// off, two interleaved pairs: forward 0.32 vs 0.39 ms, inverse 0.52 vs 0.55 ms for the
+// fp32-MFMA descriptor GEMM); MSFNO_LEG_X3=0 keeps the fp32 GEMM.
 bool leg_x3_enabled() {
   static const bool on = [] {
     const char* e = getenv("MSFNO_LEG_X3");
-    return e && e[0] == '1' && gemm_use_x6();
+    if (e) return e[0] == '1' && gemm_use_x6();
+    return mlp_fused_h_env() && gemm_use_x6();
   }();
   return on;
 }
@@ -454,10 +471,17 @@ static int ensure_desc3(msfno_sht_plan_s* p, int R, int64_t ldT, hipStream_t s) 
     d.push_back(g);
   });
   if (p->d_desc3) MSFNO_CHECK_HIP(hipFree(p->d_desc3));
+  if (p->d_tile3) MSFNO_CHECK_HIP(hipFree(p->d_tile3));
   p->d_desc3 = nullptr;
+  p->d_tile3 = nullptr;
   MSFNO_CHECK_HIP(hipMalloc(&p->d_desc3, std::max<size_t>(1, d.size()) * sizeof(GemmDesc)));
   if (!d.empty())
     MSFNO_CHECK_HIP(hipMemcpy(p->d_desc3, d.data(), d.size() * sizeof(GemmDesc), hipMemcpyHostToDevice));
+  std::vector<int> t2d((size_t)std::max(tiles, 1), 0);
+  for (size_t i = 0; i < d.size(); ++i)
+    for (int t = 0; t < d[i].tiles_m * d[i].tiles_n; ++t) t2d[d[i].tile_start + t] = (int)i;
+  MSFNO_CHECK_HIP(hipMalloc(&p->d_tile3, t2d.size() * sizeof(int)));
+  MSFNO_CHECK_HIP(hipMemcpy(p->d_tile3, t2d.data(), t2d.size() * sizeof(int), hipMemcpyHostToDevice));
   p->ndesc3 = (int)d.size();
   p->desc3_tiles = tiles;
   p->desc3_R = R;
@@ -668,8 +692,8 @@ int legendre_fwd(msfno_sht_plan_s* f, const float* Xt, float* S, int R, hipStrea
       e.segA_w = f->band_seg();
       e.segA_stride = (int64_t)f->nslab * R * 2 * f->band_W;
     }
-    return legendre_x3(Xt, f->tab3, f->tab3s, S, f->d_desc3, f->ndesc3, f->desc3_tiles,
-                       x3d_bn(0), e, s);
+    return legendre_x3(Xt, f->tab3, f->tab3s, S, f->d_desc3, f->d_tile3, f->ndesc3,
+                       f->desc3_tiles, x3d_bn(0), e, s);
   }
   MSFNO_TRY(ensure_desc(f, R, 0, f->spec.ldT));
   GemmEpi e;
@@ -691,8 +715,8 @@ int legendre_inv(msfno_sht_plan_s* g, const float* S, float* Yt, int R, hipStrea
       e.segC_w = g->band_seg();
       e.segC_stride = (int64_t)g->nslab * R * 2 * g->band_W;
     }
-    return legendre_x3(S, g->tab3, g->tab3s, Yt, g->d_desc3, g->ndesc3, g->desc3_tiles,
-                       x3d_bn(1), e, s);
+    return legendre_x3(S, g->tab3, g->tab3s, Yt, g->d_desc3, g->d_tile3, g->ndesc3,
+                       g->desc3_tiles, x3d_bn(1), e, s);
   }
   MSFNO_TRY(ensure_desc(g, R, 0, g->spec.ldT));
   GemmEpi e;
@@ -1496,6 +1520,7 @@ int msfno_sht_plan_destroy(msfno_sht_plan_t p) {
   if (p->d_tabx_offo) (void)hipFree(p->d_tabx_offo);
   if (p->d_descx) (void)hipFree(p->d_descx);
   if (p->d_desc3) (void)hipFree(p->d_desc3);
+  if (p->d_tile3) (void)hipFree(p->d_tile3);
   if (p->tab3) (void)hipFree(p->tab3);
   if (p->tab3s) (void)hipFree(p->tab3s);
   if (p->d_kmap) (void)hipFree(p->d_kmap);

@@ -190,8 +190,8 @@ int x3d_bn(int inverse);
 int launch_legendre_x3_image(const float* table, const GemmDesc* descs, int ndesc,
                              unsigned short* img, float* invs, hipStream_t s);
 int legendre_x3(const float* A, const unsigned short* img, const float* invs, float* C,
-                const GemmDesc* descs, int ndesc, int tiles, int bn, const GemmEpi& e,
-                hipStream_t s);
+                const GemmDesc* descs, const int* tile_desc, int ndesc, int tiles, int bn,
+                const GemmEpi& e, hipStream_t s);
 size_t gemm_x3_workspace(int M, int K, int batch);
 int gemm_x3(const float* A, int lda, const float* bscale, const float* B, float* C, int M, int N,
             int K, int ldb, int ldc, int64_t sB, int64_t sC, int batch, const GemmEpi& epi,
@@ -319,6 +319,7 @@ struct msfno_sht_plan_s {
   // planes per problem, column-scaled) and the inverse column scales
   int desc3_R = -1;
   msfno::GemmDesc* d_desc3 = nullptr;
+  int* d_tile3 = nullptr;  // tile -> descriptor index
   int ndesc3 = 0, desc3_tiles = 0;
   unsigned short* tab3 = nullptr;
   float* tab3s = nullptr;

@@ -9,14 +9,15 @@
 // fp32 is emulated by two fp16 terms per operand (v = v0 + v1, v0 = fp16(v),
 // v1 = fp16(v - v0)) and three fp16 MFMAs per product (a1·b0 + a0·b1 + a0·b0,
 // fp32 accumulation; Ootomo & Yokota 2022, as gemm_x6c.hip's x3h chain).  fp16's
-// range is kept by exact power-of-two scales: every row of A by sigma_r (the
-// row's max over K maps below 2^15: a pre-pass over the workgroup's rows), every
-// column of B by tau_n (its max maps into [2^14, 2^15): in the table image, built
-// once per table load).  An entry below 2^-24 of its row's (column's) maximum
-// loses its low term: an error under the fp32 rounding of the dot product it
-// enters.  The epilogue multiplies by 1 / (sigma_r tau_n).
+// range is kept by exact power-of-two scales: every row of A by sigma_r,t per
+// k-tile t (the row's max over the tile's 32 k maps into [2^14, 2^15), found while
+// the tile is staged), every column of B by tau_n (its max maps into [2^14, 2^15):
+// in the table image, built once per table load).  An entry below 2^-24 of its row's
+// (column's) maximum loses its low term: an error under the fp32 rounding of the dot
+// product it enters.  Each k-tile's products are scaled back by 1 / sigma_r,t as
+// they are added to the accumulator, the epilogue by 1 / tau_n.
 //
-// Tile 128 (rows) x BN (n: 192 by default, 64) x 32 (k), 4 waves as 2 x 2, each
+// Tile 128 (rows) x BN (n: 64 by default, 128, 192) x 32 (k), 4 waves as 2 x 2, each
 // 64 x BN/2 as 32x32x16 MFMA tiles; both operands k-contiguous in LDS ([plane][k16][row][16], the two
 // 16-B halves of a row swapped when (row >> 3) & 1, gemm_x6.hip's A layout), two
 // stages.  The table image is B^T: [plane][n][Kp] per problem (Kp = K rounded up
@@ -93,6 +94,7 @@ struct X3DParams {
   const float* invs;
   float* C;
   const GemmDesc* descs;
+  const int* tile_desc;  // tile -> descriptor index (or null: binary search)
   int ndesc;
   int segA_w, segC_w;
   int64_t segA_stride, segC_stride;
@@ -108,7 +110,15 @@ __device__ __forceinline__ int swz(int row) { return (row >> 3) & 1; }
 
 // BN: 64 or 192 columns per tile (192: one tile spans a whole problem's N <= 184 — A
 // is read once, not once per 64 columns); PF: k-tiles in flight in registers (1, 2)
-template <int BN, int PF>
+// DBG (diagnostic timing builds, wrong results; MSFNO_LEG_X3_DBG): 1 no MFMAs, 4 no
+// main-loop loads (stale registers)
+//
+// Row scales per k-tile: the 8 threads that stage one row's 32 k of a k-tile reduce
+// their max by lane shuffles and split the row under sigma = 2^(15 - e) of it; the
+// k-tile's products go to a zeroed accumulator that is added to the running one times
+// 1 / sigma (per row, from LDS) — no separate pass over A (a whole-K row-max pass
+// per workgroup cost 0.13 / 0.18 ms of the forward / inverse 0.39 / 0.57).
+template <int BN, int PF, int DBG = 0>
 __global__ __launch_bounds__(256) void legendre_x3_kernel(X3DParams p) {
   constexpr int B_PL = KS * BN * 16;
   constexpr int STAGE = 2 * A_PL + 2 * B_PL;  // fp16 per stage
@@ -117,8 +127,7 @@ __global__ __launch_bounds__(256) void legendre_x3_kernel(X3DParams p) {
   constexpr int EPI_FLOATS = 32 * WGM * (BN + 8);
   constexpr int LDS_BYTES = (2 * STAGE * 2 > EPI_FLOATS * 4) ? 2 * STAGE * 2 : EPI_FLOATS * 4;
   __shared__ __attribute__((aligned(16))) char lds_raw[LDS_BYTES];
-  __shared__ float sig_s[BM], isig_s[BM];
-  __shared__ float red_s[256];
+  __shared__ __attribute__((aligned(16))) float isg_s[2][BM];  // 1 / sigma per stage and row
   unsigned short* const ring = reinterpret_cast<unsigned short*>(lds_raw);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WGN, wn = wave % WGN;
@@ -127,9 +136,13 @@ __global__ __launch_bounds__(256) void legendre_x3_kernel(X3DParams p) {
   // ---- tile -> problem ----------------------------------------------------------------
   const int lin = xcd_remap(blockIdx.x, gridDim.x);
   int lo = 0, hi = p.ndesc - 1;
-  while (lo < hi) {
-    const int mid = (lo + hi + 1) >> 1;
-    if (p.descs[mid].tile_start <= lin) lo = mid; else hi = mid - 1;
+  if (p.tile_desc) {
+    lo = p.tile_desc[lin];
+  } else {
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (p.descs[mid].tile_start <= lin) lo = mid; else hi = mid - 1;
+    }
   }
   const GemmDesc d = p.descs[lo];
   const int local = lin - d.tile_start;
@@ -141,13 +154,18 @@ __global__ __launch_bounds__(256) void legendre_x3_kernel(X3DParams p) {
   const unsigned short* Bimg = p.img + d.offBx;
   const int nk = (K + BK - 1) / BK;
 
-  // ---- staging: A fp32 -> two fp16 planes (row-scaled); B image 16-B copies -----------
-  // A: 128 rows x 32 k = 1024 float4, 4 per thread (thread -> row idx / 8, k 4 (idx % 8))
+  // ---- staging: A fp32 -> two fp16 planes (row-scaled per k-tile); B image copies -----
+  // A: 128 rows x 32 k = 1024 float4, 4 per thread (thread -> row idx / 8, k 4 (idx % 8):
+  // the 8 lanes of a row are adjacent); (rows padded to 4 floats and segments to 16: a
+  // float4 at k % 4 == 0 stays in its row and block; elements past K are masked)
   float4 ra[PF][4];
   uint4 rb[PF][NB];
   const int Kc = K > 0 ? K - 1 : 0;
   auto load = [&](int kt, auto buf_c) {
     constexpr int BUF = decltype(buf_c)::value;
+    if constexpr ((DBG & 4) != 0) {
+      if (kt > 1) return;
+    }
     const int k0 = kt * BK;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
@@ -157,7 +175,6 @@ __global__ __launch_bounds__(256) void legendre_x3_kernel(X3DParams p) {
       const float* a = A + (int64_t)row * lda;
       ra[BUF][q] = *reinterpret_cast<const float4*>(a + seg_k(min(k, Kc & ~3), p.segA_w, p.segA_stride));
     }
-    // B: 2 planes x BN n x 32 k fp16 = 8 BN pieces of 16 B, NB per thread
 #pragma unroll
     for (int q = 0; q < NB; ++q) {
       const int idx = tid + 256 * q;
@@ -175,13 +192,21 @@ __global__ __launch_bounds__(256) void legendre_x3_kernel(X3DParams p) {
       const int idx = tid + 256 * q;
       const int r = idx >> 3, kk = 4 * (idx & 7);  // k within the tile: 0..28
       const bool rok = m0 + r < M;
-      const float sg = sig_s[r];
       float v[4] = {ra[BUF][q].x, ra[BUF][q].y, ra[BUF][q].z, ra[BUF][q].w};
+      float mx = 0.f;
 #pragma unroll
-      for (int e = 0; e < 4; ++e) v[e] = (rok && k0 + kk + e < K) ? v[e] * sg : 0.f;
+      for (int e = 0; e < 4; ++e) {
+        v[e] = (rok && k0 + kk + e < K) ? v[e] : 0.f;
+        mx = fmaxf(mx, fabsf(v[e]));
+      }
+      mx = fmaxf(mx, __shfl_xor(mx, 1));
+      mx = fmaxf(mx, __shfl_xor(mx, 2));
+      mx = fmaxf(mx, __shfl_xor(mx, 4));
+      const float sg = pow2_scale(mx, 15);
+      if ((idx & 7) == 0) isg_s[st][r] = 1.f / sg;
       uint32_t a0, a1, b0, b1;
-      x3_split(v[0], v[1], a0, a1);
-      x3_split(v[2], v[3], b0, b1);
+      x3_split(v[0] * sg, v[1] * sg, a0, a1);
+      x3_split(v[2] * sg, v[3] * sg, b0, b1);
       const int ks = kk >> 4, c = (kk >> 3) & 1, w = kk & 7;
       unsigned short* dst = base + (ks * BM + r) * 16 + 8 * (c ^ swz(r)) + w;
       *reinterpret_cast<uint2*>(dst) = make_uint2(a0, b0);
@@ -198,39 +223,6 @@ __global__ __launch_bounds__(256) void legendre_x3_kernel(X3DParams p) {
     }
   };
 
-  using I0 = std::integral_constant<int, 0>;
-  using I1 = std::integral_constant<int, 1>;
-  // the first k-tiles' loads go out before the row-scale pass (they need no scale)
-  if (nk > 0) load(0, I0{});
-  if constexpr (PF == 2) {
-    if (nk > 1) load(1, I1{});
-  }
-  // ---- row scales: max over K of each of the tile's rows (two threads per row) -------
-  // (rows padded to 4 floats and segments to 16: a float4 at k % 4 == 0 stays in
-  // its row and block; elements past K are masked)
-  {
-    const int r = tid >> 1, h = tid & 1;
-    const int row = min(m0 + r, M - 1);
-    const float* a = A + (int64_t)row * lda;
-    float mx = 0.f;
-    if (m0 + r < M)
-      for (int k = 4 * h; k < K; k += 8) {
-        const float4 v = *reinterpret_cast<const float4*>(a + seg_k(k, p.segA_w, p.segA_stride));
-        mx = fmaxf(mx, fabsf(v.x));
-        if (k + 1 < K) mx = fmaxf(mx, fabsf(v.y));
-        if (k + 2 < K) mx = fmaxf(mx, fabsf(v.z));
-        if (k + 3 < K) mx = fmaxf(mx, fabsf(v.w));
-      }
-    red_s[tid] = mx;
-    __syncthreads();
-    if (h == 0) {
-      const float sg = pow2_scale(fmaxf(red_s[tid], red_s[tid + 1]), 15);
-      sig_s[r] = sg;
-      isig_s[r] = 1.f / sg;
-    }
-    __syncthreads();
-  }
-
   floatx16 acc[MT][NT];
 #pragma unroll
   for (int i = 0; i < MT; ++i)
@@ -241,6 +233,13 @@ __global__ __launch_bounds__(256) void legendre_x3_kernel(X3DParams p) {
 
   auto mfma_tile = [&](int st) {
     const unsigned short* base = ring + st * STAGE;
+    floatx16 t[MT][NT];
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+      for (int j = 0; j < NT; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) t[i][j][r] = 0.f;
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) {
       h8 a[MT][2], b[NT][2];
@@ -264,13 +263,36 @@ __global__ __launch_bounds__(256) void legendre_x3_kernel(X3DParams p) {
       for (int i = 0; i < MT; ++i)
 #pragma unroll
         for (int j = 0; j < NT; ++j) {
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[i][1], b[j][0], acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[i][0], b[j][1], acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[i][0], b[j][0], acc[i][j], 0, 0, 0);
+          if constexpr ((DBG & 1) != 0) {
+            t[i][j][0] += (float)a[i][0][0] + (float)a[i][1][0] + (float)b[j][0][0] + (float)b[j][1][0];
+            continue;
+          }
+          t[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[i][1], b[j][0], t[i][j], 0, 0, 0);
+          t[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[i][0], b[j][1], t[i][j], 0, 0, 0);
+          t[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[i][0], b[j][0], t[i][j], 0, 0, 0);
         }
+    }
+    // acc += t / sigma (rows (r & 3) + 8 (r >> 2) + 4 half of the 32-row block)
+#pragma unroll
+    for (int i = 0; i < MT; ++i) {
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        const float4 is = *reinterpret_cast<const float4*>(&isg_s[st][wm * WM + i * 32 + 8 * g4 + 4 * half]);
+        const float isv[4] = {is.x, is.y, is.z, is.w};
+#pragma unroll
+        for (int j = 0; j < NT; ++j)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) acc[i][j][4 * g4 + e] = fmaf(t[i][j][4 * g4 + e], isv[e], acc[i][j][4 * g4 + e]);
+      }
     }
   };
 
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+  if (nk > 0) load(0, I0{});
+  if constexpr (PF == 2) {
+    if (nk > 1) load(1, I1{});
+  }
   if (nk > 0) store(0, 0, I0{});
   __syncthreads();
   if constexpr (PF == 1) {
@@ -297,15 +319,14 @@ __global__ __launch_bounds__(256) void legendre_x3_kernel(X3DParams p) {
     }
   }
 
-  // ---- 1 / (sigma_r tau_n), then the shared fp32 epilogue ----------------------------
+  // ---- 1 / tau_n, then the shared fp32 epilogue ---------------------------------------
 #pragma unroll
   for (int j = 0; j < NT; ++j) {
     const float it = p.invs[d.offBs + min(n0 + wn * WN + j * 32 + l32, N - 1)];
 #pragma unroll
     for (int i = 0; i < MT; ++i)
 #pragma unroll
-      for (int r = 0; r < 16; ++r)
-        acc[i][j][r] *= it * isig_s[wm * WM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * half];
+      for (int r = 0; r < 16; ++r) acc[i][j][r] *= it;
   }
   GemmParams q{};
   q.vecC = p.vecC;
@@ -324,12 +345,12 @@ int launch_legendre_x3_image(const float* table, const GemmDesc* descs, int ndes
   return launch_check("legendre_x3_image");
 }
 
-// tile width of the x3h Legendre problems (MSFNO_LEG_X3_BN=64|192, per direction:
+// tile width of the x3h Legendre problems (MSFNO_LEG_X3_BN=64|128|192, per direction:
 // MSFNO_LEG_X3_BN=<forward>,<inverse>)
 int x3d_bn(int inverse) {
   static int bn[2] = {0, 0};
   if (!bn[0]) {
-    bn[0] = bn[1] = 192;
+    bn[0] = bn[1] = 64;
     if (const char* e = getenv("MSFNO_LEG_X3_BN")) {
       int a = 0, b = 0;
       const int n = sscanf(e, "%d,%d", &a, &b);
@@ -337,31 +358,44 @@ int x3d_bn(int inverse) {
       if (n == 2) bn[1] = b;
     }
     for (int& v : bn)
-      if (v != 64) v = 192;
+      if (v != 128 && v != 192) v = 64;
   }
   return bn[inverse ? 1 : 0];
 }
 
 int legendre_x3(const float* A, const unsigned short* img, const float* invs, float* C,
-                const GemmDesc* descs, int ndesc, int tiles, int bn, const GemmEpi& e,
-                hipStream_t s) {
+                const GemmDesc* descs, const int* tile_desc, int ndesc, int tiles, int bn,
+                const GemmEpi& e, hipStream_t s) {
   if (ndesc <= 0 || tiles <= 0) return MSFNO_OK;
   MSFNO_REQUIRE(A && img && invs && C && descs, MSFNO_EINVAL, "legendre_x3: null operand");
   MSFNO_REQUIRE(!e.rowscale && !e.bias && !e.addend, MSFNO_EUNSUPPORTED,
                 "legendre_x3: plain epilogue only");
   X3DParams p{};
   p.A = A; p.img = img; p.invs = invs; p.C = C;
-  p.descs = descs; p.ndesc = ndesc;
+  p.descs = descs; p.tile_desc = tile_desc; p.ndesc = ndesc;
   p.segA_w = e.segA_w; p.segA_stride = e.segA_stride;
   p.segC_w = e.segC_w; p.segC_stride = e.segC_stride;
   p.vecC = (reinterpret_cast<uintptr_t>(C) & 15) == 0;  // every ldc / offC is a multiple of 4
-  static const int pf = [] {
+  static const int pf = [] {  // k-tiles of register prefetch (2 measured no faster)
     const char* e = getenv("MSFNO_LEG_X3_PF");
-    return (e && e[0] == '1') ? 1 : 2;
+    return (e && e[0] == '2') ? 2 : 1;
   }();
-  if (bn == 64)
+  static const int dbg = [] {
+    const char* e = getenv("MSFNO_LEG_X3_DBG");
+    return e ? atoi(e) & 7 : 0;
+  }();
+  static void (*const kd[8])(X3DParams) = {
+      legendre_x3_kernel<64, 2, 0>, legendre_x3_kernel<64, 2, 1>, legendre_x3_kernel<64, 2, 0>,
+      legendre_x3_kernel<64, 2, 1>, legendre_x3_kernel<64, 2, 4>, legendre_x3_kernel<64, 2, 5>,
+      legendre_x3_kernel<64, 2, 4>, legendre_x3_kernel<64, 2, 5>};
+  if (dbg)
+    hipLaunchKernelGGL(kd[dbg], dim3(tiles), dim3(256), 0, s, p);
+  else if (bn == 64)
     hipLaunchKernelGGL((pf == 1 ? legendre_x3_kernel<64, 1> : legendre_x3_kernel<64, 2>), dim3(tiles),
                        dim3(256), 0, s, p);
+  else if (bn == 128)
+    hipLaunchKernelGGL((pf == 1 ? legendre_x3_kernel<128, 1> : legendre_x3_kernel<128, 2>),
+                       dim3(tiles), dim3(256), 0, s, p);
   else
     hipLaunchKernelGGL((pf == 1 ? legendre_x3_kernel<192, 1> : legendre_x3_kernel<192, 2>),
                        dim3(tiles), dim3(256), 0, s, p);
