@@ -452,14 +452,30 @@ bool leg_x3_enabled() {
   return on;
 }
 
+// inverse problems on the register-resident kernel (legendre_x3r) when every problem
+// fits it (K <= X3R_KMAX, N <= X3R_NMAX); MSFNO_LEG_X3R=0 keeps the tiled kernel
+static bool x3r_env() {
+  static const bool on = [] {
+    const char* e = getenv("MSFNO_LEG_X3R");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 static int ensure_desc3(msfno_sht_plan_s* p, int R, int64_t ldT, hipStream_t s) {
   if (p->desc3_R == R && p->d_desc3 && p->tab3_valid) return MSFNO_OK;
+  bool res = p->inverse && x3r_env();
+  if (res)
+    leg_problems(p, R, ldT, [&](GemmDesc g) {
+      if (g.K > X3R_KMAX || g.N > X3R_NMAX || g.N <= 0) res = false;
+    });
+  p->desc3_res = res ? 1 : 0;
   std::vector<GemmDesc> d;
   int tiles = 0;
   int64_t img = 0, sc = 0;
   leg_problems(p, R, ldT, [&](GemmDesc g) {
     g.tiles_m = (int)cdiv(g.M, X3D_BM);
-    g.tiles_n = (int)cdiv(g.N, x3d_bn(p->inverse));
+    g.tiles_n = res ? 1 : (int)cdiv(g.N, x3d_bn(p->inverse));
     // every problem gets its image, also K = 0 ones (written as zeros)
     g.offBx = img;
     g.offBs = sc;
@@ -715,6 +731,9 @@ int legendre_inv(msfno_sht_plan_s* g, const float* S, float* Yt, int R, hipStrea
       e.segC_w = g->band_seg();
       e.segC_stride = (int64_t)g->nslab * R * 2 * g->band_W;
     }
+    if (g->desc3_res)
+      return legendre_x3r(S, g->tab3, g->tab3s, Yt, g->d_desc3, g->d_tile3, g->ndesc3,
+                          g->desc3_tiles, e, s);
     return legendre_x3(S, g->tab3, g->tab3s, Yt, g->d_desc3, g->d_tile3, g->ndesc3,
                        g->desc3_tiles, x3d_bn(1), e, s);
   }

@@ -187,11 +187,16 @@ int launch_split_a(const float* A, unsigned short* Ax, int M, int K, int lda, in
 // x3h Legendre descriptor GEMM (legendre_x3.hip): tiles X3D_BM x x3d_bn(), k-tile X3D_BK
 constexpr int X3D_BM = 128, X3D_BK = 32;
 int x3d_bn(int inverse);
+// register-resident variant (legendre_x3r): every problem K <= X3R_KMAX, N <= X3R_NMAX
+constexpr int X3R_KMAX = 192, X3R_NMAX = 1024;
 int launch_legendre_x3_image(const float* table, const GemmDesc* descs, int ndesc,
                              unsigned short* img, float* invs, hipStream_t s);
 int legendre_x3(const float* A, const unsigned short* img, const float* invs, float* C,
                 const GemmDesc* descs, const int* tile_desc, int ndesc, int tiles, int bn,
                 const GemmEpi& e, hipStream_t s);
+int legendre_x3r(const float* A, const unsigned short* img, const float* invs, float* C,
+                 const GemmDesc* descs, const int* tile_desc, int ndesc, int tiles,
+                 const GemmEpi& e, hipStream_t s);
 size_t gemm_x3_workspace(int M, int K, int batch);
 int gemm_x3(const float* A, int lda, const float* bscale, const float* B, float* C, int M, int N,
             int K, int ldb, int ldc, int64_t sB, int64_t sC, int batch, const GemmEpi& epi,
@@ -325,6 +330,7 @@ struct msfno_sht_plan_s {
   float* tab3s = nullptr;
   int64_t tab3_elems = 0, tab3s_elems = 0;
   int tab3_valid = 0;
+  int desc3_res = 0;  // inverse problems on legendre_x3r (one tile per 128 rows)
   // Latitude-band plans (band.cpp): the Legendre GEMMs read / write the all-to-all
   // buffers directly.  Their slabs are [src or dst rank p][slab][R][band_ld] blocks:
   // a K (forward) or N (inverse) column k' = p * seg + j lies in rank p's block.

@@ -27,6 +27,7 @@
 #include <cstdlib>
 #include <type_traits>
 
+#include "dma.h"
 #include "gemm_common.h"
 
 namespace msfno {
@@ -336,7 +337,183 @@ __global__ __launch_bounds__(256) void legendre_x3_kernel(X3DParams p) {
                                      p.C + d.offC, nullptr, M, N, d.ldc, m0, n0, 0);
 }
 
+// ---- register-resident A (the inverse problems, K <= X3R_KMAX) -------------------------
+// Inverse problems have a short K (the degrees of one parity, <= 181 at lmax 360) and
+// a wide N (the latitudes): the tiled kernel above spends most of its time on per-tile
+// prologues and epilogues (K = 3 k-tiles, 17 k tiles at config 2).  Here one workgroup
+// owns 128 rows of one problem for ALL its columns: every wave loads its 32 rows x Kp
+// of A once, splits them under one power-of-two scale per row (its max over the whole
+// K into [2^14, 2^15)) and keeps both fp16 planes in registers (16 VGPRs per 32 k);
+// the table image streams through a three-stage LDS ring by LDS-DMA in chunks of 32
+// columns ([plane][ks][n 32][16], 16-B halves swapped by (n >> 3) & 1), one barrier per
+// chunk; each chunk's 32 x 32 block per wave is scaled back (1 / sigma_row,
+// 1 / tau_n) and stored straight from the accumulator (a row's 32 columns are 128
+// contiguous bytes).  A and the output are touched once; the table once per 128 rows.
+constexpr int X3R_NSTG = 3;
+constexpr int X3R_STAGE = 2 * (X3R_KMAX / 16) * 1024;  // bytes per stage (max Kp)
+
+// masked lanes store here, so every wave issues exactly 16 stores per chunk (the
+// DMA waits count them)
+__device__ float x3r_sink[64];
+
+__device__ __forceinline__ int x3r_swz(int n) { return (n >> 3) & 1; }
+
+template <int NK>
+__device__ __forceinline__ void x3r_body(const X3DParams& p, const GemmDesc& d, int m0,
+                                         unsigned char* ring, float* tau_s) {
+  constexpr int KS = 2 * NK;       // 16-deep k-steps
+  constexpr int KP = 32 * NK;      // padded K of the image
+  constexpr int NI = KP / 32;      // DMA wave-instructions per wave and stage (= NK)
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int half = lane >> 5, l32 = lane & 31;
+  const int M = d.M, N = d.N, K = d.K;
+  const int nch = (N + 31) / 32;
+  const unsigned short* Bimg = p.img + d.offBx;
+  const uint32_t ring_lds = lds_addr(ring);
+
+  // stage s <- columns 32 j .. +31 of the image; wave w issues pieces i = w + 4 q
+  // (piece (pl, ks) is one 1-KB block of the stage)
+  auto issue = [&](int j, int s) {
+    const int n = lane >> 1, hc = (lane & 1) ^ x3r_swz(lane >> 1);
+    const int ng = min(32 * j + n, N - 1);
+#pragma unroll
+    for (int q = 0; q < NI; ++q) {
+      const int i = wave + 4 * q;
+      const int pl = i / KS, ks = i % KS;
+      const unsigned short* src = Bimg + ((int64_t)pl * N + ng) * KP + 16 * ks + 8 * hc;
+      glds16(src, ring_lds + s * X3R_STAGE + i * 1024);
+    }
+  };
+  if (nch > 0) issue(0, 0);
+  if (nch > 1) issue(1, 1);
+  // 1 / tau_n of every column into LDS (no global load inside the chunk loop: hipcc
+  // would wait for it with a vmcnt that also drains the DMA in flight)
+  for (int n = tid; n < N; n += 256) tau_s[n] = p.invs[d.offBs + n];
+
+  // A: this lane's row, k = 16 ks + 8 half .. + 7 for every ks; one scale per row
+  const int row = m0 + 32 * wave + l32;
+  const float* Ar = p.A + d.offA + (int64_t)min(row, M - 1) * d.lda;
+  float4 av[KS][2];
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) {
+    const int k = 16 * ks + 8 * half;
+    if (k < K) {
+      av[ks][0] = *reinterpret_cast<const float4*>(Ar + k);
+      av[ks][1] = *reinterpret_cast<const float4*>(Ar + k + 4);
+    } else {
+      av[ks][0] = av[ks][1] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  float mx = 0.f;
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) {
+    float v[8] = {av[ks][0].x, av[ks][0].y, av[ks][0].z, av[ks][0].w,
+                  av[ks][1].x, av[ks][1].y, av[ks][1].z, av[ks][1].w};
+    const int k = 16 * ks + 8 * half;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      v[e] = (row < M && k + e < K) ? v[e] : 0.f;
+      mx = fmaxf(mx, fabsf(v[e]));
+    }
+    av[ks][0] = make_float4(v[0], v[1], v[2], v[3]);
+    av[ks][1] = make_float4(v[4], v[5], v[6], v[7]);
+  }
+  mx = fmaxf(mx, __shfl_xor(mx, 32));
+  const float sg = pow2_scale(mx, 15);
+  h8 a[KS][2];
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) {
+    uint32_t t0[4], t1[4];
+    x3_split(av[ks][0].x * sg, av[ks][0].y * sg, t0[0], t1[0]);
+    x3_split(av[ks][0].z * sg, av[ks][0].w * sg, t0[1], t1[1]);
+    x3_split(av[ks][1].x * sg, av[ks][1].y * sg, t0[2], t1[2]);
+    x3_split(av[ks][1].z * sg, av[ks][1].w * sg, t0[3], t1[3]);
+    a[ks][0] = __builtin_bit_cast(h8, make_uint4(t0[0], t0[1], t0[2], t0[3]));
+    a[ks][1] = __builtin_bit_cast(h8, make_uint4(t1[0], t1[1], t1[2], t1[3]));
+  }
+  // 1 / sigma of the 16 rows this lane's accumulator holds: (r & 3) + 8 (r >> 2) + 4 half
+  float isv[16];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) isv[r] = __shfl(1.f / sg, (r & 3) + 8 * (r >> 2) + 4 * half);
+
+  const int rbase = m0 + 32 * wave + 4 * half;
+  float* Cb = p.C + d.offC;
+  for (int j = 0; j < nch; ++j) {
+    const int s = j % X3R_NSTG;
+    // chunk j's DMA (j >= 2) was issued before chunk j-2's 16 stores, chunk j+1's NI
+    // pieces and chunk j-1's 16 stores (chunks 0, 1 were drained with A)
+    if (j + 1 < nch) wait_vmcnt(32 + NI); else wait_vmcnt(32);
+    __syncthreads();
+    if (j + 2 < nch) issue(j + 2, (j + 2) % X3R_NSTG);
+    const unsigned char* st = ring + s * X3R_STAGE;
+    floatx16 acc;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      const int off = ks * 1024 + l32 * 32 + 16 * (half ^ x3r_swz(l32));
+      const h8 b0 = *reinterpret_cast<const h8*>(st + off);
+      const h8 b1 = *reinterpret_cast<const h8*>(st + KS * 1024 + off);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[ks][1], b0, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[ks][0], b1, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[ks][0], b0, acc, 0, 0, 0);
+    }
+    const int col = 32 * j + l32;
+    const float it = tau_s[min(col, N - 1)];
+    const int64_t cc = seg_k(col, p.segC_w, p.segC_stride);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int rr = rbase + (r & 3) + 8 * (r >> 2);
+      float* dst = (rr < M && col < N) ? Cb + (int64_t)rr * d.ldc + cc : x3r_sink + lane;
+      *dst = acc[r] * isv[r] * it;
+    }
+  }
+}
+
+// K = 0 problems (an odd parity without degrees): the output block is zero
+__device__ __forceinline__ void x3r_zero(const X3DParams& p, const GemmDesc& d, int m0) {
+  float* Cb = p.C + d.offC;
+  for (int e = threadIdx.x; e < X3D_BM * d.N; e += blockDim.x) {
+    const int r = m0 + e / d.N, c = e % d.N;
+    if (r < d.M) Cb[(int64_t)r * d.ldc + seg_k(c, p.segC_w, p.segC_stride)] = 0.f;
+  }
+}
+
+__global__ __launch_bounds__(256) void legendre_x3r_kernel(X3DParams p) {
+  __shared__ __attribute__((aligned(16))) unsigned char ring[X3R_NSTG * X3R_STAGE];
+  __shared__ float tau_s[X3R_NMAX];
+  const int lin = xcd_remap(blockIdx.x, gridDim.x);
+  const GemmDesc d = p.descs[p.tile_desc[lin]];
+  const int m0 = (lin - d.tile_start) * X3D_BM;
+  switch ((d.K + 31) / 32) {
+    case 0: x3r_zero(p, d, m0); break;
+    case 1: x3r_body<1>(p, d, m0, ring, tau_s); break;
+    case 2: x3r_body<2>(p, d, m0, ring, tau_s); break;
+    case 3: x3r_body<3>(p, d, m0, ring, tau_s); break;
+    case 4: x3r_body<4>(p, d, m0, ring, tau_s); break;
+    case 5: x3r_body<5>(p, d, m0, ring, tau_s); break;
+    default: x3r_body<6>(p, d, m0, ring, tau_s); break;
+  }
+}
+
 }  // namespace
+
+int legendre_x3r(const float* A, const unsigned short* img, const float* invs, float* C,
+                 const GemmDesc* descs, const int* tile_desc, int ndesc, int tiles,
+                 const GemmEpi& e, hipStream_t s) {
+  if (ndesc <= 0 || tiles <= 0) return MSFNO_OK;
+  MSFNO_REQUIRE(A && img && invs && C && descs && tile_desc, MSFNO_EINVAL,
+                "legendre_x3r: null operand");
+  MSFNO_REQUIRE(!e.rowscale && !e.bias && !e.addend && !e.segA_w, MSFNO_EUNSUPPORTED,
+                "legendre_x3r: plain epilogue, unsegmented A only");
+  X3DParams p{};
+  p.A = A; p.img = img; p.invs = invs; p.C = C;
+  p.descs = descs; p.tile_desc = tile_desc; p.ndesc = ndesc;
+  p.segC_w = e.segC_w; p.segC_stride = e.segC_stride;
+  hipLaunchKernelGGL(legendre_x3r_kernel, dim3(tiles), dim3(256), 0, s, p);
+  return launch_check("legendre_x3r");
+}
 
 int launch_legendre_x3_image(const float* table, const GemmDesc* descs, int ndesc,
                              unsigned short* img, float* invs, hipStream_t s) {
