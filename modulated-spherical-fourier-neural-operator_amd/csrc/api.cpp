@@ -520,6 +520,70 @@ static int ensure_desc3(msfno_sht_plan_s* p, int R, int64_t ldT, hipStream_t s) 
   return MSFNO_OK;
 }
 
+// forward problems on legendre_x3f: the image and column scales of desc3, tiles of
+// X3F_RB rows x 64 columns (column blocks of one row block adjacent).  Default with the
+// x3h Legendre on symmetric, unsharded blocks with norm0 (the slab planes need its
+// per-channel bound); MSFNO_LEG_X3F=0 keeps legendre_x3 on the fp32 slab.
+bool x3f_env() {
+  static const bool on = [] {
+    const char* e = getenv("MSFNO_LEG_X3F");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
+bool x3f_usable(msfno_sht_plan_s* f) {
+  if (!x3f_env() || !leg_x3_enabled() || !f->sym || f->band_world || f->inverse) return false;
+  if (f->nslab != f->mmax) return false;
+  return f->Ke <= X3F_KMAX && f->Ko <= X3F_KMAX && f->ldke % 8 == 0 && f->ldk % 8 == 0 &&
+         std::max(f->ldke, f->ldk - f->ldke) <= cdiv(f->Ke, 64) * 64;
+}
+
+static int ensure_desc3f(msfno_sht_plan_s* p, int R, int64_t ldT, hipStream_t s) {
+  MSFNO_TRY(ensure_desc3(p, R, ldT, s));
+  if (p->desc3f_R == R && p->d_desc3f) return MSFNO_OK;
+  std::vector<GemmDesc> d;
+  int tiles = 0;
+  int64_t img = 0, sc = 0;
+  leg_problems(p, R, ldT, [&](GemmDesc g) {  // the offsets ensure_desc3 gave the image
+    g.offBx = img;
+    g.offBs = sc;
+    img += 2LL * g.N * round_up(std::max(g.K, 1), X3D_BK);
+    sc += g.N;
+    g.tiles_m = (int)cdiv(g.M, X3F_RB);
+    g.tiles_n = (int)cdiv(g.N, 64);
+    if (g.tiles_m * g.tiles_n == 0 || g.K <= 0) return;
+    g.tile_start = tiles;
+    tiles += g.tiles_m * g.tiles_n;
+    d.push_back(g);
+  });
+  if (p->d_desc3f) MSFNO_CHECK_HIP(hipFree(p->d_desc3f));
+  if (p->d_tile3f) MSFNO_CHECK_HIP(hipFree(p->d_tile3f));
+  p->d_desc3f = nullptr;
+  p->d_tile3f = nullptr;
+  MSFNO_CHECK_HIP(hipMalloc(&p->d_desc3f, std::max<size_t>(1, d.size()) * sizeof(GemmDesc)));
+  if (!d.empty())
+    MSFNO_CHECK_HIP(hipMemcpy(p->d_desc3f, d.data(), d.size() * sizeof(GemmDesc), hipMemcpyHostToDevice));
+  std::vector<int> t2d((size_t)std::max(tiles, 1), 0);
+  for (size_t i = 0; i < d.size(); ++i)
+    for (int t = 0; t < d[i].tiles_m * d[i].tiles_n; ++t) t2d[d[i].tile_start + t] = (int)i;
+  MSFNO_CHECK_HIP(hipMalloc(&p->d_tile3f, t2d.size() * sizeof(int)));
+  MSFNO_CHECK_HIP(hipMemcpy(p->d_tile3f, t2d.data(), t2d.size() * sizeof(int), hipMemcpyHostToDevice));
+  p->ndesc3f = (int)d.size();
+  p->desc3f_tiles = tiles;
+  p->desc3f_R = R;
+  return MSFNO_OK;
+}
+
+// forward Legendre on the slab planes of launch_transpose_fwd_sym_h (Xp: plane
+// stride pstride, isr: 1 / sigma per row) -> S
+int legendre_fwd_x3f(msfno_sht_plan_s* f, const unsigned short* Xp, int64_t pstride,
+                     const float* isr, float* S, int R, hipStream_t s) {
+  MSFNO_TRY(ensure_desc3f(f, R, f->spec.ldT, s));
+  return legendre_x3f(Xp, pstride, isr, f->tab3, f->tab3s, S, f->d_desc3f, f->d_tile3f,
+                      f->ndesc3f, f->desc3f_tiles, s);
+}
+
 // spectral MLP: Gauss 3M complex GEMM by default (MSFNO_SPEC_4M=1: the real-ified
 // 4-multiplication GEMM, kept as an A/B switch); MSFNO_C3M_TILE picks its tile
 bool use_c3m() {
@@ -819,6 +883,12 @@ void carve_block(Carve& cv, BlockBufs& b, const msfno_block_desc* d,
   }
   b.x1p = x1p_buffer(d, g) ? cv.take<unsigned short>(BC * 3 * P) : nullptr;
   b.xs = skip_x3(d) ? cv.take<float>(BC) : nullptr;
+  b.lsig = nullptr;
+  b.isr = nullptr;
+  if (x3f_env() && leg_x3_enabled()) {
+    b.lsig = cv.take<float>(BC);
+    b.isr = cv.take<float>(R);
+  }
   carve_dense_ws(cv, b.dw, d, B);
 }
 
@@ -1192,11 +1262,19 @@ int run_spectral(const msfno_block_desc* d, msfno_sht_plan_s* f, msfno_sht_plan_
       prof(ST_NORM0, s);
       MSFNO_TRY(launch_chan_affine(b.rs0, f->nlat, f->nlon, f->nlon, B, (int)C, d->norm0_w,
                                    d->norm0_b, d->norm_eps, nullptr, nullptr, 0.f, b.sc0, b.sh0,
-                                   s, b.xs));
+                                   s, b.xs, b.lsig));
       if (after_norm0) MSFNO_TRY(after_norm0());
     }
     prof(ST_TRANSPOSE_FWD, s);
-    if (lx6) {
+    if (!lx6 && norm0 && b.lsig && b.isr && x3f_usable(f)) {
+      // slab as x3h planes in the Xt buffer (two fp16 planes = the fp32 bytes)
+      const int64_t pstride = (int64_t)f->nslab * R * f->ldk;
+      unsigned short* Xp = reinterpret_cast<unsigned short*>(b.Xt);
+      MSFNO_TRY(launch_transpose_fwd_sym_h(b.Xn, Xp, pstride, B, (int)C, f->geom(), f->mmax,
+                                           b.sc0, b.sh0, b.lsig, b.isr, s));
+      prof(ST_LEG_FWD, s);
+      MSFNO_TRY(legendre_fwd_x3f(f, Xp, pstride, b.isr, b.Sa, (int)R, s));
+    } else if (lx6) {
       const int64_t xstride = (int64_t)f->nslab * R * f->ldk;
       MSFNO_TRY(launch_transpose_fwd_sym_planes(b.Xn, b.Xtp, xstride, B, (int)C, f->geom(),
                                                 f->mmax, norm0 ? b.sc0 : nullptr,
@@ -1539,6 +1617,8 @@ int msfno_sht_plan_destroy(msfno_sht_plan_t p) {
   if (p->d_tabx_offo) (void)hipFree(p->d_tabx_offo);
   if (p->d_descx) (void)hipFree(p->d_descx);
   if (p->d_desc3) (void)hipFree(p->d_desc3);
+  if (p->d_desc3f) (void)hipFree(p->d_desc3f);
+  if (p->d_tile3f) (void)hipFree(p->d_tile3f);
   if (p->d_tile3) (void)hipFree(p->d_tile3);
   if (p->tab3) (void)hipFree(p->tab3);
   if (p->tab3s) (void)hipFree(p->tab3s);
@@ -1588,6 +1668,7 @@ int msfno_sht_plan_load_table(msfno_sht_plan_t p, const float* table, void* stre
   MSFNO_TRY(launch_relayout_table(*p, table, s));
   p->descx_R = -1;
   p->desc3_R = -1;
+  p->desc3f_R = -1;
   p->tab3_valid = 0;  // the x3h image is rebuilt from the new table on first use
   // the bf16x3 table image only feeds the x6 Legendre GEMMs (MSFNO_LEG_X6=1)
   if (sym && leg_x6_enabled() && !p->band_world) MSFNO_TRY(build_table_x6(p, table, s));

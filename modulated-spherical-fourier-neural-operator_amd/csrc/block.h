@@ -59,6 +59,8 @@ struct BlockBufs {
   unsigned short* mfimg;  // fused MLP weight image (mlp_fused), else null
   float* cs;  // x3h spectral MLP: per-(b, column) input scale and its inverse [2][B][ld]
   float* xs = nullptr;  // x3h inner skip: per-(b, c) power-of-two scale of x (B-row scales)
+  float* lsig = nullptr;  // legendre_x3f: per-(b, c) slab scale sigma (chan_affine)
+  float* isr = nullptr;  // legendre_x3f: 1 / sigma per slab row (R)
   DenseWs dw;
 };
 

@@ -189,11 +189,16 @@ constexpr int X3D_BM = 128, X3D_BK = 32;
 int x3d_bn(int inverse);
 // register-resident variant (legendre_x3r): every problem K <= X3R_KMAX, N <= X3R_NMAX
 constexpr int X3R_KMAX = 192, X3R_NMAX = 1024;
+// register-B forward variant (legendre_x3f): K <= X3F_KMAX, X3F_RB rows x 64 columns per tile
+constexpr int X3F_KMAX = 384, X3F_RB = 256;
 int launch_legendre_x3_image(const float* table, const GemmDesc* descs, int ndesc,
                              unsigned short* img, float* invs, hipStream_t s);
 int legendre_x3(const float* A, const unsigned short* img, const float* invs, float* C,
                 const GemmDesc* descs, const int* tile_desc, int ndesc, int tiles, int bn,
                 const GemmEpi& e, hipStream_t s);
+int legendre_x3f(const unsigned short* Ap, int64_t pstride, const float* isr,
+                 const unsigned short* img, const float* invs, float* C, const GemmDesc* descs,
+                 const int* tile_desc, int ndesc, int tiles, hipStream_t s);
 int legendre_x3r(const float* A, const unsigned short* img, const float* invs, float* C,
                  const GemmDesc* descs, const int* tile_desc, int ndesc, int tiles,
                  const GemmEpi& e, hipStream_t s);
@@ -331,6 +336,11 @@ struct msfno_sht_plan_s {
   int64_t tab3_elems = 0, tab3s_elems = 0;
   int tab3_valid = 0;
   int desc3_res = 0;  // inverse problems on legendre_x3r (one tile per 128 rows)
+  // forward problems on legendre_x3f (tiles X3F_RB x 64; the image of desc3)
+  int desc3f_R = -1;
+  msfno::GemmDesc* d_desc3f = nullptr;
+  int* d_tile3f = nullptr;
+  int ndesc3f = 0, desc3f_tiles = 0;
   // Latitude-band plans (band.cpp): the Legendre GEMMs read / write the all-to-all
   // buffers directly.  Their slabs are [src or dst rank p][slab][R][band_ld] blocks:
   // a K (forward) or N (inverse) column k' = p * seg + j lies in rank p's block.

@@ -59,7 +59,8 @@ int launch_transpose_inv(const float* Yt, float2* Yn, int B, int C, int nlat, in
 int launch_chan_affine(const float2* partials, int64_t np, int64_t cnt, int64_t cnt_last,
                        int B, int C, const float* w, const float* b, float eps,
                        const float* gamma, const float* beta, float film_scale, float* scale,
-                       float* shift, hipStream_t s, float* xscale = nullptr);
+                       float* shift, hipStream_t s, float* xscale = nullptr,
+                       float* lsig = nullptr);
 // latitude-band sharding helpers (band.cpp)
 // rowstats (BC, np) (mean, M2) over cnt each -> out (BC, 3) fp64 {n, mean, M2}; xscale
 // (or null): the local x3h skip B-row scales as in launch_chan_affine
@@ -145,6 +146,12 @@ int launch_transpose_fwd_sym(const float2* Xn, float* Xt, int B, int C, const La
                              const float* nscale, const float* nshift, hipStream_t s);
 int launch_transpose_inv_sym(const float* Yt, float2* Yn, int B, int C, const LatGeom& g, int mmax,
                              int mact, hipStream_t s);
+// x3h planes (legendre_x3f's A): the folded slab as two fp16 planes [plane][m][R][ldk]
+// (plane stride pstride), scaled per channel by lsig (chan_affine; 1 / sigma -> isr[R])
+int launch_transpose_fwd_sym_h(const float2* Xn, unsigned short* Xp, int64_t pstride, int B, int C,
+                               const LatGeom& g, int mmax, const float* nscale,
+                               const float* nshift, const float* lsig, float* isr,
+                               hipStream_t s);
 // S layout <-> reference (bc, lmax, mmax) complex dense
 int launch_spec_to_ref(const msfno_sht_plan_s& p, const float* S, float2* out, int B, int C,
                        const int* d_off, hipStream_t s);

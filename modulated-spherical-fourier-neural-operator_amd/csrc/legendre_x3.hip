@@ -102,6 +102,17 @@ struct X3DParams {
   int vecC;
 };
 
+struct X3FParams {
+  const unsigned short* Ap;  // slab planes (plane stride pstride)
+  int64_t pstride;
+  const float* isr;          // 1 / sigma per slab row
+  const unsigned short* img;
+  const float* invs;
+  float* C;
+  const GemmDesc* descs;
+  const int* tile_desc;
+};
+
 constexpr int BM = X3D_BM, BK = X3D_BK;
 constexpr int KS = BK / 16;                 // 32x32x16 k-steps per k-tile
 constexpr int A_PL = KS * BM * 16;          // fp16 per A plane in a stage
@@ -497,7 +508,129 @@ __global__ __launch_bounds__(256) void legendre_x3r_kernel(X3DParams p) {
   }
 }
 
+// ---- register-resident B (the forward problems, Kp <= X3F_KMAX) ------------------------
+// Forward problems have a long K (the latitudes of one hemisphere fold, 361 at 721)
+// and a narrow N (the degrees of one parity, <= 181).  One workgroup owns 64 columns
+// of one problem and X3F_RB rows: every wave keeps its 16 table columns x Kp as both
+// fp16 planes in registers (the 16x16x32 B operand: 8 VGPRs per 32 k), the slab rows
+// arrive already split (launch_transpose_fwd_sym_h: two fp16 planes, one scale per
+// channel) and stream through a three-stage LDS ring by LDS-DMA, 16 rows per chunk
+// ([plane][ks][row 16][32 k], 16-B slots XOR-swizzled by (row >> 2) & 3: a fragment
+// read covers all 64 banks once per 16 lanes); one barrier per chunk, the 16 x 16
+// block per wave scaled back by 1 / sigma_row, 1 / tau_n and stored from the
+// accumulator.  No conversion work in the kernel.
+constexpr int X3F_NSTG = 3;
+constexpr int X3F_STAGE = 2 * (X3F_KMAX / 32) * 1024;  // bytes per stage (max Kp)
+
+typedef float f4v __attribute__((ext_vector_type(4)));
+
+template <int KS>
+__device__ __forceinline__ void x3f_body(const X3FParams& p, const GemmDesc& d, int m0, int n0,
+                                         unsigned char* ring, float* isr_s) {
+  constexpr int KP = 32 * KS;
+  constexpr int NP = 2 * KS;  // 1-KB pieces per stage
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int M = d.M, N = d.N, K = d.K;
+  const int rows = min(X3F_RB, M - m0);
+  const int nch = (rows + 15) / 16;
+  const uint32_t ring_lds = lds_addr(ring);
+  const int ni = (NP - wave + 3) / 4;  // pieces this wave issues per stage
+
+  // stage s <- rows m0 + 16 j .. + 15, all Kp, both planes
+  auto issue = [&](int j, int s) {
+    const int r = lane >> 2, kg = (lane & 3) ^ ((r >> 2) & 3);
+    const int row = min(m0 + 16 * j + r, M - 1);
+    const unsigned short* rowp = p.Ap + d.offA + (int64_t)row * d.lda;
+#pragma unroll
+    for (int q = 0; q < (NP + 3) / 4; ++q) {
+      const int i = wave + 4 * q;
+      if (i < NP) {
+        const int pl = i / KS, ks = i % KS;
+        const int k = 32 * ks + 8 * kg;
+        glds16(rowp + pl * p.pstride + (k < K ? k : 0), ring_lds + s * X3F_STAGE + i * 1024);
+      }
+    }
+  };
+  if (nch > 0) issue(0, 0);
+  if (nch > 1) issue(1, 1);
+
+  // B: this wave's 16 columns, lane (n = lane & 15, k = 32 ks + 8 (lane >> 4) .. + 7)
+  const int col = n0 + 16 * wave + (lane & 15);
+  const unsigned short* bp = p.img + d.offBx + (int64_t)min(col, N - 1) * KP + 8 * (lane >> 4);
+  h8 b[KS][2];
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+    for (int pl = 0; pl < 2; ++pl)
+      b[ks][pl] = *reinterpret_cast<const h8*>(bp + (int64_t)pl * N * KP + 32 * ks);
+  const float it = p.invs[d.offBs + min(col, N - 1)];
+  for (int r = tid; r < rows; r += 256) isr_s[r] = p.isr[m0 + r];
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+
+  float* Cb = p.C + d.offC;
+  const int ra = lane >> 4;  // the accumulator's rows 4 ra .. + 3
+  for (int j = 0; j < nch; ++j) {
+    const int s = j % X3F_NSTG;
+    // chunk j's DMA (j >= 2) was issued before chunk j-2's 4 stores, chunk j+1's ni
+    // pieces and chunk j-1's 4 stores (chunks 0, 1 were drained with B)
+    if (j + 1 < nch) wait_vmcnt(8 + ni); else wait_vmcnt(8);
+    __syncthreads();
+    if (j + 2 < nch) issue(j + 2, (j + 2) % X3F_NSTG);
+    const unsigned char* st = ring + s * X3F_STAGE;
+    const int r16 = lane & 15, kq = lane >> 4;
+    const int off = r16 * 64 + 16 * (kq ^ ((r16 >> 2) & 3));
+    f4v acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      const h8 a0 = *reinterpret_cast<const h8*>(st + ks * 1024 + off);
+      const h8 a1 = *reinterpret_cast<const h8*>(st + (KS + ks) * 1024 + off);
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1, b[ks][0], acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0, b[ks][1], acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0, b[ks][0], acc, 0, 0, 0);
+    }
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int rl = 16 * j + 4 * ra + e;  // row within the workgroup's block
+      const bool ok = rl < rows && col < N;
+      float* dst = ok ? Cb + (int64_t)(m0 + rl) * d.ldc + col : x3r_sink + lane;
+      *dst = acc[e] * isr_s[min(rl, X3F_RB - 1)] * it;
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void legendre_x3f_kernel(X3FParams p) {
+  __shared__ __attribute__((aligned(16))) unsigned char ring[X3F_NSTG * X3F_STAGE];
+  __shared__ float isr_s[X3F_RB];
+  const int lin = xcd_remap(blockIdx.x, gridDim.x);
+  const GemmDesc d = p.descs[p.tile_desc[lin]];
+  const int local = lin - d.tile_start;
+  // consecutive tiles share rows (the column blocks of one row block): A from L2
+  const int tn = local % d.tiles_n, tm = local / d.tiles_n;
+  const int m0 = tm * X3F_RB, n0 = tn * 64;
+  switch ((d.K + 31) / 32) {
+#define X3F_CASE(n) case n: x3f_body<n>(p, d, m0, n0, ring, isr_s); break;
+    X3F_CASE(1) X3F_CASE(2) X3F_CASE(3) X3F_CASE(4) X3F_CASE(5) X3F_CASE(6)
+    X3F_CASE(7) X3F_CASE(8) X3F_CASE(9) X3F_CASE(10) X3F_CASE(11) X3F_CASE(12)
+#undef X3F_CASE
+    default: break;  // K = 0 never reaches here (the host requires 0 < K <= X3F_KMAX)
+  }
+}
+
 }  // namespace
+
+int legendre_x3f(const unsigned short* Ap, int64_t pstride, const float* isr,
+                 const unsigned short* img, const float* invs, float* C, const GemmDesc* descs,
+                 const int* tile_desc, int ndesc, int tiles, hipStream_t s) {
+  if (ndesc <= 0 || tiles <= 0) return MSFNO_OK;
+  MSFNO_REQUIRE(Ap && isr && img && invs && C && descs && tile_desc, MSFNO_EINVAL,
+                "legendre_x3f: null operand");
+  X3FParams p{};
+  p.Ap = Ap; p.pstride = pstride; p.isr = isr;
+  p.img = img; p.invs = invs; p.C = C;
+  p.descs = descs; p.tile_desc = tile_desc;
+  hipLaunchKernelGGL(legendre_x3f_kernel, dim3(tiles), dim3(256), 0, s, p);
+  return launch_check("legendre_x3f");
+}
 
 int legendre_x3r(const float* A, const unsigned short* img, const float* invs, float* C,
                  const GemmDesc* descs, const int* tile_desc, int ndesc, int tiles,

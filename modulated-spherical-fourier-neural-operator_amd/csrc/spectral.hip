@@ -330,6 +330,110 @@ __global__ __launch_bounds__(256) void transpose_fwd_sym4_kernel(
   }
 }
 
+// x3h-plane variant of the vector-store kernel, for the register-B forward Legendre
+// (legendre_x3f): the slab as two fp16 planes [plane][slab][R][ldk] (v = v0 + v1,
+// v0 = fp16(v), v1 = fp16(v - v0): the same 4 bytes per value as fp32) under ONE
+// power-of-two scale per channel, sigma_bc = lsig[bc] from chan_affine: a bound of the
+// whole folded slab row (|x^| <= |s| sqrt(M2) + |s mean + t| for the norm0 output,
+// the rfft scaled by 2 pi / nlon gives |X^_m| <= 2 pi max |x^|, the fold doubles it)
+// mapped into [2^14, 2^15).
+// 1 / sigma goes to isr[r] for both slab rows r of the channel.  Pads are written as
+// zeros up to ldke (Xs) and ldk - ldke (Xa), so every 16-B piece the GEMM stages
+// below its K holds finite values.
+__device__ __forceinline__ void split_h2(float a, float b, uint32_t& t0, uint32_t& t1) {
+  typedef _Float16 h2_t __attribute__((ext_vector_type(2)));
+  typedef float f2_t __attribute__((ext_vector_type(2)));
+  const f2_t v = {a, b};
+  const h2_t h0 = __builtin_convertvector(v, h2_t);
+  const f2_t r = v - __builtin_convertvector(h0, f2_t);
+  const h2_t h1 = __builtin_convertvector(r, h2_t);
+  t0 = __builtin_bit_cast(uint32_t, h0);
+  t1 = __builtin_bit_cast(uint32_t, h1);
+}
+
+template <int TKx, int TMx>
+__global__ __launch_bounds__(256) void transpose_fwd_sym4h_kernel(
+    const float2* __restrict__ Xn, unsigned short* __restrict__ Xp, int64_t pstride, int B, int C,
+    LatGeom g, int mmax, const float* __restrict__ nscale, const float* __restrict__ nshift,
+    const float* __restrict__ lsig, float* __restrict__ isr) {
+  constexpr int LD = TKx + 4;
+  __shared__ __attribute__((aligned(16))) float tile[4 * TMx * LD];  // [h][c][m][k]
+  const int k0 = blockIdx.x * TKx, m0 = blockIdx.y * TMx;
+  const int bc = blockIdx.z;
+  const int b = bc / C, c = bc - b * C;
+  const float2* src = Xn + (int64_t)bc * g.nlat * mmax;
+  const float sc = nscale[bc];
+  const float sh = nshift[bc] * kTwoPi;
+  const float sig = lsig[bc];
+  const int64_t R = 2LL * B * C;
+  if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x < 2)
+    isr[(int64_t)(b * 2 + threadIdx.x) * C + c] = 1.f / sig;
+  for (int i = threadIdx.x; i < TKx * TMx; i += 256) {
+    const int kk = i / TMx, mm = i - kk * TMx;
+    const int k = k0 + kk, m = m0 + mm;
+    float2 n = make_float2(0.f, 0.f), t = n;
+    if (k < g.Ke && m < mmax) {
+      n = src[(int64_t)k * mmax + m];
+      if (k < g.nh) t = src[(int64_t)(g.nlat - 1 - k) * mmax + m];
+    }
+    const bool pair = k < g.nh;
+    const float shm = (m == 0) ? sh : 0.f;
+    const float sre = pair ? fmaf(sc, n.x + t.x, 2.f * shm) : (k < g.Ke ? fmaf(sc, n.x, shm) : 0.f);
+    const float sim = pair ? sc * (n.y + t.y) : sc * n.y;
+    tile[(0 * TMx + mm) * LD + kk] = sre * sig;
+    tile[(1 * TMx + mm) * LD + kk] = sim * sig;
+    tile[(2 * TMx + mm) * LD + kk] = pair ? sc * (n.x - t.x) * sig : 0.f;
+    tile[(3 * TMx + mm) * LD + kk] = pair ? sc * (n.y - t.y) * sig : 0.f;
+  }
+  __syncthreads();
+  // 8 k per thread: one 16-B store per plane (ldke, ldk are multiples of 8)
+  constexpr int KV8 = TKx / 8;
+  const int kend_s = g.ldke, kend_a = g.ldk - g.ldke;  // pads as zeros
+  for (int i = threadIdx.x; i < 4 * TMx * KV8; i += 256) {
+    const int row = i / KV8, kv = i - row * KV8;
+    const int hc = row / TMx, mm = row - hc * TMx;
+    const int h = hc >> 1, ri = hc & 1;
+    const int k = k0 + 8 * kv, m = m0 + mm;
+    if (m >= mmax || k >= (h ? kend_a : kend_s)) continue;
+    const float4 v = *reinterpret_cast<const float4*>(tile + row * LD + 8 * kv);
+    const float4 w = *reinterpret_cast<const float4*>(tile + row * LD + 8 * kv + 4);
+    uint4 hi, lo;
+    split_h2(v.x, v.y, hi.x, lo.x);
+    split_h2(v.z, v.w, hi.y, lo.y);
+    split_h2(w.x, w.y, hi.z, lo.z);
+    split_h2(w.z, w.w, hi.w, lo.w);
+    unsigned short* dst = Xp + (int64_t)m * R * g.ldk + ((int64_t)(b * 2 + ri) * C + c) * g.ldk +
+                          (h ? g.ldke : 0) + k;
+    *reinterpret_cast<uint4*>(dst) = hi;
+    *reinterpret_cast<uint4*>(dst + pstride) = lo;
+  }
+}
+
+int launch_transpose_fwd_sym_h(const float2* Xn, unsigned short* Xp, int64_t pstride, int B, int C,
+                               const LatGeom& g, int mmax, const float* nscale,
+                               const float* nshift, const float* lsig, float* isr,
+                               hipStream_t s) {
+  if (!nscale || !nshift || !lsig || !isr || !g.sym || (g.ldke & 7) || (g.ldk & 7) ||
+      std::max(g.ldke, g.ldk - g.ldke) > cdiv(g.Ke, 64) * 64)
+    return MSFNO_EINVAL;  // (a 128-row tile grid covers at least the 64-row one)
+  // MSFNO_TRH=128: 128 x 32 tiles (256-B plane segments, 67 KB of LDS; measured slower:
+  // 0.386 vs 0.33 ms in-block) instead of 64 x 32
+  static const int tk = [] {
+    const char* e = getenv("MSFNO_TRH");
+    return (e && atoi(e) == 128) ? 128 : 64;
+  }();
+  if (tk == 64) {
+    dim3 grid((unsigned)cdiv(g.Ke, 64), (unsigned)cdiv(mmax, 32), (unsigned)(B * C));
+    hipLaunchKernelGGL((transpose_fwd_sym4h_kernel<64, 32>), grid, dim3(256), 0, s, Xn, Xp,
+                       pstride, B, C, g, mmax, nscale, nshift, lsig, isr);
+  } else {
+    dim3 grid((unsigned)cdiv(g.Ke, 128), (unsigned)cdiv(mmax, 32), (unsigned)(B * C));
+    hipLaunchKernelGGL((transpose_fwd_sym4h_kernel<128, 32>), grid, dim3(256), 0, s, Xn, Xp,
+                       pstride, B, C, g, mmax, nscale, nshift, lsig, isr);
+  }
+  return launch_check("transpose_fwd_sym_h");
+}
+
 template <int TKx, int TMx>
 __global__ __launch_bounds__(256) void transpose_inv_sym2_kernel(const float* __restrict__ Yt,
                                                                  float2* __restrict__ Yn, int B,
@@ -710,7 +814,8 @@ __global__ __launch_bounds__(256) void chan_affine_kernel(
     const float2* __restrict__ part, int64_t np, int64_t cnt, int64_t cnt_last, int C,
     const float* __restrict__ w, const float* __restrict__ bsh, float eps,
     const float* __restrict__ gamma, const float* __restrict__ beta, float film_scale,
-    float* __restrict__ scale, float* __restrict__ shift, float* __restrict__ xscale) {
+    float* __restrict__ scale, float* __restrict__ shift, float* __restrict__ xscale,
+    float* __restrict__ lsig) {
   __shared__ double sn[256], smean[256], sm2[256];
   const int bc = blockIdx.x;
   const int c = bc % C;
@@ -750,15 +855,27 @@ __global__ __launch_bounds__(256) void chan_affine_kernel(
     scale[bc] = (float)sc;
     shift[bc] = (float)sh;
     if (xscale) xscale[bc] = x3_bound_scale(mu, sm2[0]);
+    if (lsig) {  // transpose_fwd_sym4h_kernel's sigma: |x^| <= |sc| sqrt(M2) + |sc mu + sh|,
+                 // |X^_m| <= 2 pi max |x^|, folded x 2
+      const double bound = 2.0 * 6.283185307179586 *
+                           (fabs(sc) * sqrt(sm2[0]) + fabs(sc * mu + sh)) * (1.0 + 1e-3);
+      float sig = 1.f;
+      if (bound > 0.0 && bound < 1e300) {
+        int e;
+        frexp(bound, &e);
+        sig = (float)ldexp(1.0, min(max(15 - e, -100), 100));
+      }
+      lsig[bc] = sig;
+    }
   }
 }
 
 int launch_chan_affine(const float2* partials, int64_t np, int64_t cnt, int64_t cnt_last, int B,
                        int C, const float* w, const float* b, float eps, const float* gamma,
                        const float* beta, float film_scale, float* scale, float* shift,
-                       hipStream_t s, float* xscale) {
+                       hipStream_t s, float* xscale, float* lsig) {
   hipLaunchKernelGGL(chan_affine_kernel, dim3(B * C), dim3(256), 0, s, partials, np, cnt,
-                     cnt_last, C, w, b, eps, gamma, beta, film_scale, scale, shift, xscale);
+                     cnt_last, C, w, b, eps, gamma, beta, film_scale, scale, shift, xscale, lsig);
   return launch_check("chan_affine");
 }
 
