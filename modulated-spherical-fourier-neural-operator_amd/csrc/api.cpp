@@ -897,7 +897,9 @@ void carve_dense_ws(Carve& cv, DenseWs& w, const msfno_block_desc* d, int B) {
   w.skip_b = w.fc1_b = w.fc2_b = 0;
   const int C = (int)d->C;
   if (d->inner_skip == MSFNO_SKIP_LINEAR &&
-      (w.skip_b = std::max(gemm_dense_workspace(C, C, 1), skip_x3(d) ? gemm_x3_workspace(C, C, B) : 0)))
+      (w.skip_b = std::max({gemm_dense_workspace(C, C, 1),
+                            skip_x3(d) ? gemm_x3_workspace(C, C, B) : 0,
+                            skip_x3(d) && C == 256 ? skip_h_workspace(B) : 0})))
     w.skip = cv.take<char>(w.skip_b);
   if (d->has_mlp) {
     const int Hd = (int)d->mlp_hidden;
@@ -1233,7 +1235,8 @@ int run_spectral(const msfno_block_desc* d, msfno_sht_plan_s* f, msfno_sht_plan_
                  const BlockBufs& b, const float* x, int B, bool norm0, hipStream_t s,
                  const C2RPlanes* xplanes = nullptr,
                  const std::function<int()>& after_fft = std::function<int()>(),
-                 const std::function<int()>& after_norm0 = std::function<int()>()) {
+                 const std::function<int()>& after_norm0 = std::function<int()>(),
+                 const std::function<int()>& after_leg = std::function<int()>()) {
   const int64_t C = d->C, BC = (int64_t)B * C, R = 2 * BC;
   // x6 Legendre: symmetric plans, slab / coefficient planes carved, row path
   const bool lx6 = b.Xtp && b.Sp && f->sym && g->sym && !use_fft_tile(f) &&
@@ -1288,6 +1291,7 @@ int run_spectral(const msfno_block_desc* d, msfno_sht_plan_s* f, msfno_sht_plan_
       MSFNO_TRY(legendre_fwd(f, b.Xt, b.Sa, (int)R, s));
     }
   }
+  if (after_leg) MSFNO_TRY(after_leg());
   MSFNO_TRY(run_filter(d, f, g, b, B, s, lx6 ? b.Sp : nullptr));
   prof(ST_LEG_INV, s);
   if (lx6)
@@ -1822,7 +1826,9 @@ int msfno_block_forward(const msfno_block_desc* d, msfno_sht_plan_t f, msfno_sht
     prof(ST_SKIP, ss);
     GemmEpi e;
     e.bias = d->skip_b;
-    if (b.xs) {
+    if (b.xs && C == 256 && skip_h_env()) {
+      MSFNO_TRY(launch_skip_h(d->skip_w, b.xs, x, x1, d->skip_b, B, P, b.dw.skip, b.dw.skip_b, ss));
+    } else if (b.xs) {
       MSFNO_TRY(gemm_x3(d->skip_w, (int)C, b.xs, x, x1, (int)C, (int)P, (int)C, (int)P, (int)P,
                         C * P, C * P, B, e, b.dw.skip, b.dw.skip_b, ss));
     } else if (xpl) {
@@ -1846,7 +1852,16 @@ int msfno_block_forward(const msfno_block_desc* d, msfno_sht_plan_t f, msfno_sht
     MSFNO_TRY(side_ctx(&side, s));
     if (!xpl && !b.xs) MSFNO_TRY(launch_skip());
   }
-  if (b.xs)  // x3h: the skip needs x's per-channel bounds (norm0 statistics) first
+  // MSFNO_SKIP_AT=leg: fork the x3h skip after the forward Legendre instead of right
+  // after the norm0 statistics (A/B of the overlap window)
+  static const bool skip_at_leg = [] {
+    const char* e = getenv("MSFNO_SKIP_AT");
+    return e && std::string(e) == "leg";
+  }();
+  if (b.xs && skip_at_leg)
+    MSFNO_TRY(run_spectral(d, f, g, b, x, B, true, s, nullptr, std::function<int()>(),
+                           std::function<int()>(), launch_skip));
+  else if (b.xs)  // x3h: the skip needs x's per-channel bounds (norm0 statistics) first
     MSFNO_TRY(run_spectral(d, f, g, b, x, B, true, s, nullptr, std::function<int()>(), launch_skip));
   else if (xpl)
     MSFNO_TRY(run_spectral(d, f, g, b, x, B, true, s, &xp, launch_skip));

@@ -418,7 +418,10 @@ int msfno_band_block_stage(const msfno_block_desc* d, msfno_band_plan_t p, int s
     prof(ST_SKIP, ss);
     GemmEpi e;
     e.bias = d->skip_b;
-    if (b.fb.xs) {  // x3h: B-row scales from the global norm0 statistics (stage 1)
+    if (b.fb.xs && C == 256 && skip_h_env()) {  // as the unsharded block (api.cpp)
+      MSFNO_TRY(launch_skip_h(d->skip_w, b.fb.xs, io->x, b.x1, d->skip_b, B, Pl, b.fb.dw.skip,
+                              b.fb.dw.skip_b, ss));
+    } else if (b.fb.xs) {  // x3h: B-row scales from the global norm0 statistics (stage 1)
       MSFNO_TRY(gemm_x3(d->skip_w, (int)C, b.fb.xs, io->x, b.x1, (int)C, (int)Pl, (int)C,
                         (int)Pl, (int)Pl, C * Pl, C * Pl, B, e, b.fb.dw.skip, b.fb.dw.skip_b,
                         ss));

@@ -105,6 +105,12 @@ int launch_mlp_fused2_images(const float* W1, const float* W2, unsigned short* i
 // mlp_fused_h.hip: the MLP on the x3h engine (fp32 as two fp16 terms, three fp16
 // MFMAs per product, row-scaled weights); default (MSFNO_ENGINE=x6 selects the x6 engine)
 bool mlp_fused_h_env();
+// inner skip at C = 256 on the mlp_fused_h tiling (x3h): out = Ws·x + bs, x scaled by the
+// power-of-two channel scales xs (|xs x| < 2^14); ws >= skip_h_workspace(B)
+bool skip_h_env();
+size_t skip_h_workspace(int B);
+int launch_skip_h(const float* W, const float* xs, const float* x, float* out, const float* bias,
+                  int B, int64_t P, void* ws, size_t ws_bytes, hipStream_t s);
 size_t mlp_fused_h_image_bytes();
 int launch_mlp_fused_h_images(const float* W1, const float* W2, unsigned short* img, hipStream_t s);
 int launch_mlp_fused_h(const float* x1, const float* scale, const float* shift, const float* resid,

@@ -514,7 +514,219 @@ __global__ __launch_bounds__(64 * W, (NG == 1 && W == 4) ? 2 : 1) void mlp_fused
   }
 }
 
+// ---- inner skip (1x1 conv, C = 256) on the same tiling: out = Ws·x + bs -------------
+// The fc1 half of mlp_fused_h_kernel with 256 output rows and no hidden layer:
+// a wave's 16 pixels of x, scaled per channel by the power of two xs (chan_affine's
+// norm0 bound, |xs x| < 2^14) and split into fp16x2 B fragments in registers; the
+// per-batch weight image W'[c][k] = rs_c Ws[c][k] / xs_k (rs_c puts the row's maximum
+// into [2^14, 2^15)) streams through the four-slot LDS ring as 16 slices of 16 KB
+// (output block j of 32 rows, channel half kh: the W1 slice layout); all 256 x 16
+// outputs stay in the accumulators and are stored once, unscaled by 1 / rs_c, + bs.
+// (gemm_x3 with in-kernel split, 256 x 256 tiles: 0.83 ms at config 2.)
+constexpr int SK_NSLICE = 16;
+
+struct SkipHParams {
+  const float* x;       // [B][C][P]
+  const float* xs;      // [B][C] power-of-two channel scales
+  float* out;           // [B][C][P]
+  const unsigned short* img;  // [B][16 slices]
+  const float* inv_rs;  // [B][C]
+  const float* bias;    // [C] or null
+  int64_t P;
+  int tiles_per_field;
+};
+
+// rs[b][c] = 2^(15 - e), max_k |Ws[c][k] / xs[b][k]| = f 2^e; inv_rs = 1 / rs
+__global__ void sk_scale_kernel(const float* __restrict__ W, const float* __restrict__ xs,
+                                float* __restrict__ rs, float* __restrict__ inv_rs) {
+  const int b = blockIdx.y, c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= MH_C) return;
+  const float* row = W + (int64_t)c * MH_C;
+  const float* xsb = xs + (int64_t)b * MH_C;
+  float m = 0.f;
+  for (int k = 0; k < MH_C; ++k) m = fmaxf(m, fabsf(row[k] / xsb[k]));
+  float sc = 1.f;
+  if (m > 0.f && isfinite(m)) {
+    int e;
+    frexpf(m, &e);
+    sc = ldexpf(1.f, 15 - e);
+  }
+  rs[(int64_t)b * MH_C + c] = sc;
+  inv_rs[(int64_t)b * MH_C + c] = 1.f / sc;
+}
+
+// W' -> [b][j][kh][pl][ks][t][r][32] (mh_w1_image_kernel's slice layout, 8 blocks j)
+__global__ void sk_image_kernel(const float* __restrict__ W, const float* __restrict__ xs,
+                                const float* __restrict__ rs, unsigned short* __restrict__ img) {
+  constexpr int64_t PAIRS = (int64_t)8 * 2 * 4 * 2 * 16 * 16;
+  const int b = blockIdx.y;
+  const float* xsb = xs + (int64_t)b * MH_C;
+  unsigned short* ib = img + (int64_t)b * SK_NSLICE * MH_SLICE;
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < PAIRS;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const int kkp = (int)(e & 15);
+    const int r = (int)((e >> 4) & 15);
+    const int t = (int)((e >> 8) & 1);
+    const int ks = (int)((e >> 9) & 3);
+    const int kh = (int)((e >> 11) & 1);
+    const int j = (int)(e >> 12);
+    const int kk = 2 * kkp;
+    const int g = (kk >> 3) ^ mh_swz(r);
+    const int k = 128 * kh + 32 * ks + 8 * g + (kk & 7);
+    const int row = 32 * j + 16 * t + r;
+    const float* src = W + (int64_t)row * MH_C + k;
+    const float sc = rs[(int64_t)b * MH_C + row];
+    uint32_t t0, t1;
+    split2h(src[0] / xsb[k] * sc, src[1] / xsb[k + 1] * sc, t0, t1);
+    uint32_t* o = reinterpret_cast<uint32_t*>(
+        ib + (int64_t)(j * 2 + kh) * MH_SLICE + ((ks * 2 + t) * 16 + r) * 32 + kk);
+    o[0] = t0;
+    o[MH_PLANE / 2] = t1;
+  }
+}
+
+__global__ __launch_bounds__(256, 2) void skip_h_kernel(SkipHParams p) {
+  constexpr int NS = MH_NS, W = 4;
+  constexpr int RING_BYTES = NS * MH_SLICE * 2;
+  __shared__ __attribute__((aligned(16))) char lds_raw[RING_BYTES + 2 * MH_C * 4];
+  unsigned short* const ring = reinterpret_cast<unsigned short*>(lds_raw);
+  float* const irs = reinterpret_cast<float*>(lds_raw + RING_BYTES);
+  float* const bs = irs + MH_C;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int r16 = lane & 15, g = lane >> 4;
+  const int lin = xcd_remap(blockIdx.x, gridDim.x);
+  const int z = lin / p.tiles_per_field;
+  const int64_t P = p.P;
+  const int64_t px = (int64_t)(lin - z * p.tiles_per_field) * 64 + 16 * wave + r16;
+  const unsigned short* img = p.img + (int64_t)z * SK_NSLICE * MH_SLICE;
+
+  const uint32_t ring_lds = lds_addr(ring);
+  const int wave_u = __builtin_amdgcn_readfirstlane(wave);
+  uint32_t piece_off[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) piece_off[i] = (uint32_t)(i * W * 1024 + lane * 16);
+  auto issue = [&](int q) {
+    const uint64_t src = reinterpret_cast<uint64_t>(img + (int64_t)q * MH_SLICE) + (uint64_t)wave_u * 1024;
+    glds16x4<W * 1024>(src, piece_off, ring_lds + (uint32_t)((q % NS) * MH_SLICE * 2 + wave_u * 1024));
+  };
+#pragma unroll
+  for (int q = 0; q < NS; ++q) issue(q);
+
+  // x -> xs-scaled fp16x2 B fragments (k-step ks: channels 32 ks + 8 g + 0..7)
+  const float* xsb = p.xs + (int64_t)z * MH_C;
+  const float* xcol = p.x + (int64_t)z * MH_C * P + (px < P ? px : P - 1);
+  half8 xf[8][2];
+#pragma unroll
+  for (int ks = 0; ks < 8; ++ks) {
+    const int c0 = 32 * ks + 8 * g;
+    float xv[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) xv[e] = __builtin_nontemporal_load(xcol + (int64_t)(c0 + e) * P);
+    const float4 sa = *reinterpret_cast<const float4*>(xsb + c0);
+    const float4 sb = *reinterpret_cast<const float4*>(xsb + c0 + 4);
+    const float sv[8] = {sa.x, sa.y, sa.z, sa.w, sb.x, sb.y, sb.z, sb.w};
+    uint32_t t[2][4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+      split2h(sv[2 * e] * xv[2 * e], sv[2 * e + 1] * xv[2 * e + 1], t[0][e], t[1][e]);
+#pragma unroll
+    for (int pl = 0; pl < 2; ++pl) xf[ks][pl] = mh_frag(t[pl][0], t[pl][1], t[pl][2], t[pl][3]);
+  }
+  for (int i = tid; i < MH_C; i += 256) {
+    irs[i] = p.inv_rs[(int64_t)z * MH_C + i];
+    bs[i] = p.bias ? p.bias[i] : 0.f;
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  floatx4 oacc[16];
+#pragma unroll
+  for (int ot = 0; ot < 16; ++ot) oacc[ot] = floatx4{0.f, 0.f, 0.f, 0.f};
+  const int a_lane = r16 * 32 + 8 * (g ^ mh_swz(r16));
+
+#pragma unroll
+  for (int q = 0; q < SK_NSLICE; ++q) {
+    // slice q landed (up to NS - 2 later slices may stay in flight); slot of q - 1 free
+    const int after = min(NS - 2, SK_NSLICE - 1 - q);
+    if (after >= 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else if (after == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    const unsigned short* slot = ring + (q % NS) * MH_SLICE;
+    const int j = q >> 1, kh = q & 1;
+    auto aoff = [&](int u, int pl) { return ((pl * 4 + (u >> 1)) * 2 + (u & 1)) * 512 + a_lane; };
+    half8 a[3][2];
+#pragma unroll
+    for (int k = 0; k < 2; ++k)
+#pragma unroll
+      for (int pl = 0; pl < 2; ++pl) a[k][pl] = *reinterpret_cast<const half8*>(slot + aoff(k, pl));
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      if (u + 2 < 8) {
+#pragma unroll
+        for (int pl = 0; pl < 2; ++pl)
+          a[(u + 2) % 3][pl] = *reinterpret_cast<const half8*>(slot + aoff(u + 2, pl));
+      }
+      const half8* av = a[u % 3];
+      const half8* xb = xf[kh * 4 + (u >> 1)];
+      floatx4& c = oacc[2 * j + (u & 1)];
+      c = __builtin_amdgcn_mfma_f32_16x16x32_f16(av[1], xb[0], c, 0, 0, 0);
+      c = __builtin_amdgcn_mfma_f32_16x16x32_f16(av[0], xb[1], c, 0, 0, 0);
+      c = __builtin_amdgcn_mfma_f32_16x16x32_f16(av[0], xb[0], c, 0, 0, 0);
+      if (u == 0 && q >= 1 && q + NS - 1 < SK_NSLICE) issue(q + NS - 1);
+    }
+  }
+
+  // epilogue: rows 16 ot + 4 g + i of pixel px
+  if (px >= P) return;
+  float* o = p.out + (int64_t)z * MH_C * P + px;
+#pragma unroll
+  for (int ot = 0; ot < 16; ++ot) {
+    const int r0 = 16 * ot + 4 * g;
+    const float4 is = *reinterpret_cast<const float4*>(irs + r0);
+    const float4 b = *reinterpret_cast<const float4*>(bs + r0);
+    const float isv[4] = {is.x, is.y, is.z, is.w}, bv[4] = {b.x, b.y, b.z, b.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) o[(int64_t)(r0 + i) * P] = fmaf(oacc[ot][i], isv[i], bv[i]);
+  }
+}
+
 }  // namespace
+
+size_t skip_h_workspace(int B) {
+  return (size_t)B * SK_NSLICE * MH_SLICE * 2 + (size_t)B * MH_C * 4 * 2 + 256;
+}
+
+// MSFNO_SKIP_H=0 keeps gemm_x3 for the inner skip
+bool skip_h_env() {
+  static const bool on = [] {
+    const char* e = getenv("MSFNO_SKIP_H");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
+int launch_skip_h(const float* W, const float* xs, const float* x, float* out, const float* bias,
+                  int B, int64_t P, void* ws, size_t ws_bytes, hipStream_t s) {
+  MSFNO_REQUIRE(W && xs && x && out && ws && B > 0 && P >= 1 && ws_bytes >= skip_h_workspace(B),
+                MSFNO_EINVAL, "skip_h: bad arguments");
+  unsigned short* img = static_cast<unsigned short*>(ws);
+  float* rs = reinterpret_cast<float*>(img + (int64_t)B * SK_NSLICE * MH_SLICE);
+  float* inv_rs = rs + (int64_t)B * MH_C;
+  hipLaunchKernelGGL(sk_scale_kernel, dim3(1, B), dim3(256), 0, s, W, xs, rs, inv_rs);
+  MSFNO_TRY(launch_check("sk_scale"));
+  hipLaunchKernelGGL(sk_image_kernel, dim3(64, B), dim3(256), 0, s, W, xs, rs, img);
+  MSFNO_TRY(launch_check("sk_image"));
+  SkipHParams p{};
+  p.x = x; p.xs = xs; p.out = out; p.img = img; p.inv_rs = inv_rs; p.bias = bias; p.P = P;
+  p.tiles_per_field = (int)cdiv(P, 64);
+  const int64_t tiles = (int64_t)B * p.tiles_per_field;
+  MSFNO_REQUIRE(tiles < (1LL << 31), MSFNO_EINVAL, "skip_h: grid too large");
+  hipLaunchKernelGGL(skip_h_kernel, dim3((unsigned)tiles), dim3(256), 0, s, p);
+  return launch_check("skip_h");
+}
 
 // the x3h engine is the default (measured as accurate as fp32 against fp64, more so
 // than x6: tests/test_gpu_x3h.py); MSFNO_ENGINE=x6 selects the six-MFMA bf16 engine
