@@ -575,12 +575,12 @@ static int ensure_desc3f(msfno_sht_plan_s* p, int R, int64_t ldT, hipStream_t s)
   return MSFNO_OK;
 }
 
-// forward Legendre on the slab planes of launch_transpose_fwd_sym_h (Xp: plane
-// stride pstride, isr: 1 / sigma per row) -> S
-int legendre_fwd_x3f(msfno_sht_plan_s* f, const unsigned short* Xp, int64_t pstride,
-                     const float* isr, float* S, int R, hipStream_t s) {
+// forward Legendre on the slab planes of launch_transpose_fwd_sym_h (Xp: fp16 pairs
+// interleaved per 8 k, isr: 1 / sigma per row) -> S
+int legendre_fwd_x3f(msfno_sht_plan_s* f, const unsigned short* Xp, const float* isr, float* S,
+                     int R, hipStream_t s) {
   MSFNO_TRY(ensure_desc3f(f, R, f->spec.ldT, s));
-  return legendre_x3f(Xp, pstride, isr, f->tab3, f->tab3s, S, f->d_desc3f, f->d_tile3f,
+  return legendre_x3f(Xp, isr, f->tab3, f->tab3s, S, f->d_desc3f, f->d_tile3f,
                       f->ndesc3f, f->desc3f_tiles, s);
 }
 
@@ -1270,13 +1270,12 @@ int run_spectral(const msfno_block_desc* d, msfno_sht_plan_s* f, msfno_sht_plan_
     }
     prof(ST_TRANSPOSE_FWD, s);
     if (!lx6 && norm0 && b.lsig && b.isr && x3f_usable(f)) {
-      // slab as x3h planes in the Xt buffer (two fp16 planes = the fp32 bytes)
-      const int64_t pstride = (int64_t)f->nslab * R * f->ldk;
+      // slab as x3h fp16 pairs in the Xt buffer (the fp32 bytes)
       unsigned short* Xp = reinterpret_cast<unsigned short*>(b.Xt);
-      MSFNO_TRY(launch_transpose_fwd_sym_h(b.Xn, Xp, pstride, B, (int)C, f->geom(), f->mmax,
-                                           b.sc0, b.sh0, b.lsig, b.isr, s));
+      MSFNO_TRY(launch_transpose_fwd_sym_h(b.Xn, Xp, B, (int)C, f->geom(), f->mmax, b.sc0, b.sh0,
+                                           b.lsig, b.isr, s));
       prof(ST_LEG_FWD, s);
-      MSFNO_TRY(legendre_fwd_x3f(f, Xp, pstride, b.isr, b.Sa, (int)R, s));
+      MSFNO_TRY(legendre_fwd_x3f(f, Xp, b.isr, b.Sa, (int)R, s));
     } else if (lx6) {
       const int64_t xstride = (int64_t)f->nslab * R * f->ldk;
       MSFNO_TRY(launch_transpose_fwd_sym_planes(b.Xn, b.Xtp, xstride, B, (int)C, f->geom(),

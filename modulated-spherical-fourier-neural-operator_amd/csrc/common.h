@@ -196,7 +196,7 @@ int launch_legendre_x3_image(const float* table, const GemmDesc* descs, int ndes
 int legendre_x3(const float* A, const unsigned short* img, const float* invs, float* C,
                 const GemmDesc* descs, const int* tile_desc, int ndesc, int tiles, int bn,
                 const GemmEpi& e, hipStream_t s);
-int legendre_x3f(const unsigned short* Ap, int64_t pstride, const float* isr,
+int legendre_x3f(const unsigned short* Ap, const float* isr,
                  const unsigned short* img, const float* invs, float* C, const GemmDesc* descs,
                  const int* tile_desc, int ndesc, int tiles, hipStream_t s);
 int legendre_x3r(const float* A, const unsigned short* img, const float* invs, float* C,

@@ -152,9 +152,9 @@ int launch_transpose_fwd_sym(const float2* Xn, float* Xt, int B, int C, const La
                              const float* nscale, const float* nshift, hipStream_t s);
 int launch_transpose_inv_sym(const float* Yt, float2* Yn, int B, int C, const LatGeom& g, int mmax,
                              int mact, hipStream_t s);
-// x3h planes (legendre_x3f's A): the folded slab as two fp16 planes [plane][m][R][ldk]
-// (plane stride pstride), scaled per channel by lsig (chan_affine; 1 / sigma -> isr[R])
-int launch_transpose_fwd_sym_h(const float2* Xn, unsigned short* Xp, int64_t pstride, int B, int C,
+// x3h planes (legendre_x3f's A): the folded slab as fp16 pairs interleaved per 8 k
+// ([m][R][ldk / 8][plane][8]), scaled per channel by lsig (chan_affine; 1 / sigma -> isr[R])
+int launch_transpose_fwd_sym_h(const float2* Xn, unsigned short* Xp, int B, int C,
                                const LatGeom& g, int mmax, const float* nscale,
                                const float* nshift, const float* lsig, float* isr,
                                hipStream_t s);

@@ -103,8 +103,7 @@ struct X3DParams {
 };
 
 struct X3FParams {
-  const unsigned short* Ap;  // slab planes (plane stride pstride)
-  int64_t pstride;
+  const unsigned short* Ap;  // slab planes, interleaved per 8 k (2 x the fp32 offsets)
   const float* isr;          // 1 / sigma per slab row
   const unsigned short* img;
   const float* invs;
@@ -513,9 +512,9 @@ __global__ __launch_bounds__(256) void legendre_x3r_kernel(X3DParams p) {
 // and a narrow N (the degrees of one parity, <= 181).  One workgroup owns 64 columns
 // of one problem and X3F_RB rows: every wave keeps its 16 table columns x Kp as both
 // fp16 planes in registers (the 16x16x32 B operand: 8 VGPRs per 32 k), the slab rows
-// arrive already split (launch_transpose_fwd_sym_h: two fp16 planes, one scale per
-// channel) and stream through a three-stage LDS ring by LDS-DMA, 16 rows per chunk
-// ([plane][ks][row 16][32 k], 16-B slots XOR-swizzled by (row >> 2) & 3: a fragment
+// arrive already split (launch_transpose_fwd_sym_h: two fp16 terms interleaved per 8 k,
+// one scale per channel) and stream through a three-stage LDS ring by LDS-DMA, 16 rows
+// per chunk ([ks][plane][row 16][32 k], 16-B slots XOR-swizzled by (row >> 2) & 3: a fragment
 // read covers all 64 banks once per 16 lanes); one barrier per chunk, the 16 x 16
 // block per wave scaled back by 1 / sigma_row, 1 / tau_n and stored from the
 // accumulator.  No conversion work in the kernel.
@@ -537,17 +536,19 @@ __device__ __forceinline__ void x3f_body(const X3FParams& p, const GemmDesc& d, 
   const int ni = (NP - wave + 3) / 4;  // pieces this wave issues per stage
 
   // stage s <- rows m0 + 16 j .. + 15, all Kp, both planes
+  // piece i = (ks = i / 2, plane i % 2): both planes of a k-step from one wave, so the
+  // second instruction finds the 128-B lines of the first in L2
   auto issue = [&](int j, int s) {
     const int r = lane >> 2, kg = (lane & 3) ^ ((r >> 2) & 3);
     const int row = min(m0 + 16 * j + r, M - 1);
-    const unsigned short* rowp = p.Ap + d.offA + (int64_t)row * d.lda;
+    const unsigned short* rowp = p.Ap + 2 * (d.offA + (int64_t)row * d.lda);
 #pragma unroll
     for (int q = 0; q < (NP + 3) / 4; ++q) {
       const int i = wave + 4 * q;
       if (i < NP) {
-        const int pl = i / KS, ks = i % KS;
+        const int pl = i & 1, ks = i >> 1;
         const int k = 32 * ks + 8 * kg;
-        glds16(rowp + pl * p.pstride + (k < K ? k : 0), ring_lds + s * X3F_STAGE + i * 1024);
+        glds16(rowp + 2 * (k < K ? k : 0) + 8 * pl, ring_lds + s * X3F_STAGE + i * 1024);
       }
     }
   };
@@ -582,8 +583,8 @@ __device__ __forceinline__ void x3f_body(const X3FParams& p, const GemmDesc& d, 
     f4v acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) {
-      const h8 a0 = *reinterpret_cast<const h8*>(st + ks * 1024 + off);
-      const h8 a1 = *reinterpret_cast<const h8*>(st + (KS + ks) * 1024 + off);
+      const h8 a0 = *reinterpret_cast<const h8*>(st + (2 * ks) * 1024 + off);
+      const h8 a1 = *reinterpret_cast<const h8*>(st + (2 * ks + 1) * 1024 + off);
       acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1, b[ks][0], acc, 0, 0, 0);
       acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0, b[ks][1], acc, 0, 0, 0);
       acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0, b[ks][0], acc, 0, 0, 0);
@@ -618,14 +619,14 @@ __global__ __launch_bounds__(256) void legendre_x3f_kernel(X3FParams p) {
 
 }  // namespace
 
-int legendre_x3f(const unsigned short* Ap, int64_t pstride, const float* isr,
+int legendre_x3f(const unsigned short* Ap, const float* isr,
                  const unsigned short* img, const float* invs, float* C, const GemmDesc* descs,
                  const int* tile_desc, int ndesc, int tiles, hipStream_t s) {
   if (ndesc <= 0 || tiles <= 0) return MSFNO_OK;
   MSFNO_REQUIRE(Ap && isr && img && invs && C && descs && tile_desc, MSFNO_EINVAL,
                 "legendre_x3f: null operand");
   X3FParams p{};
-  p.Ap = Ap; p.pstride = pstride; p.isr = isr;
+  p.Ap = Ap; p.isr = isr;
   p.img = img; p.invs = invs; p.C = C;
   p.descs = descs; p.tile_desc = tile_desc;
   hipLaunchKernelGGL(legendre_x3f_kernel, dim3(tiles), dim3(256), 0, s, p);

@@ -537,14 +537,20 @@ struct SkipHParams {
 };
 
 // rs[b][c] = 2^(15 - e), max_k |Ws[c][k] / xs[b][k]| = f 2^e; inv_rs = 1 / rs
-__global__ void sk_scale_kernel(const float* __restrict__ W, const float* __restrict__ xs,
-                                float* __restrict__ rs, float* __restrict__ inv_rs) {
-  const int b = blockIdx.y, c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= MH_C) return;
-  const float* row = W + (int64_t)c * MH_C;
-  const float* xsb = xs + (int64_t)b * MH_C;
-  float m = 0.f;
-  for (int k = 0; k < MH_C; ++k) m = fmaxf(m, fabsf(row[k] / xsb[k]));
+// (one 256-thread workgroup per (row, batch): thread k, a max-reduction over the block)
+__global__ __launch_bounds__(256) void sk_scale_kernel(const float* __restrict__ W,
+                                                       const float* __restrict__ xs,
+                                                       float* __restrict__ rs,
+                                                       float* __restrict__ inv_rs) {
+  __shared__ float wmax[4];
+  const int b = blockIdx.y, c = blockIdx.x, k = threadIdx.x;
+  float m = fabsf(W[(int64_t)c * MH_C + k] / xs[(int64_t)b * MH_C + k]);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+  if ((k & 63) == 0) wmax[k >> 6] = m;
+  __syncthreads();
+  if (k != 0) return;
+  m = fmaxf(fmaxf(wmax[0], wmax[1]), fmaxf(wmax[2], wmax[3]));
   float sc = 1.f;
   if (m > 0.f && isfinite(m)) {
     int e;
@@ -715,7 +721,7 @@ int launch_skip_h(const float* W, const float* xs, const float* x, float* out, c
   unsigned short* img = static_cast<unsigned short*>(ws);
   float* rs = reinterpret_cast<float*>(img + (int64_t)B * SK_NSLICE * MH_SLICE);
   float* inv_rs = rs + (int64_t)B * MH_C;
-  hipLaunchKernelGGL(sk_scale_kernel, dim3(1, B), dim3(256), 0, s, W, xs, rs, inv_rs);
+  hipLaunchKernelGGL(sk_scale_kernel, dim3(MH_C, B), dim3(256), 0, s, W, xs, rs, inv_rs);
   MSFNO_TRY(launch_check("sk_scale"));
   hipLaunchKernelGGL(sk_image_kernel, dim3(64, B), dim3(256), 0, s, W, xs, rs, img);
   MSFNO_TRY(launch_check("sk_image"));

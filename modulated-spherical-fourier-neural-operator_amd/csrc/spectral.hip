@@ -331,8 +331,9 @@ __global__ __launch_bounds__(256) void transpose_fwd_sym4_kernel(
 }
 
 // x3h-plane variant of the vector-store kernel, for the register-B forward Legendre
-// (legendre_x3f): the slab as two fp16 planes [plane][slab][R][ldk] (v = v0 + v1,
-// v0 = fp16(v), v1 = fp16(v - v0): the same 4 bytes per value as fp32) under ONE
+// (legendre_x3f): the slab as two fp16 terms per value (v = v0 + v1, v0 = fp16(v),
+// v1 = fp16(v - v0): the same 4 bytes per value as fp32), interleaved per 8 k
+// ([slab][R][ldk / 8][plane][8]: a thread's 8 values are 32 contiguous bytes) under ONE
 // power-of-two scale per channel, sigma_bc = lsig[bc] from chan_affine: a bound of the
 // whole folded slab row (|x^| <= |s| sqrt(M2) + |s mean + t| for the norm0 output,
 // the rfft scaled by 2 pi / nlon gives |X^_m| <= 2 pi max |x^|, the fold doubles it)
@@ -353,7 +354,7 @@ __device__ __forceinline__ void split_h2(float a, float b, uint32_t& t0, uint32_
 
 template <int TKx, int TMx>
 __global__ __launch_bounds__(256) void transpose_fwd_sym4h_kernel(
-    const float2* __restrict__ Xn, unsigned short* __restrict__ Xp, int64_t pstride, int B, int C,
+    const float2* __restrict__ Xn, unsigned short* __restrict__ Xp, int B, int C,
     LatGeom g, int mmax, const float* __restrict__ nscale, const float* __restrict__ nshift,
     const float* __restrict__ lsig, float* __restrict__ isr) {
   constexpr int LD = TKx + 4;
@@ -402,14 +403,15 @@ __global__ __launch_bounds__(256) void transpose_fwd_sym4h_kernel(
     split_h2(v.z, v.w, hi.y, lo.y);
     split_h2(w.x, w.y, hi.z, lo.z);
     split_h2(w.z, w.w, hi.w, lo.w);
-    unsigned short* dst = Xp + (int64_t)m * R * g.ldk + ((int64_t)(b * 2 + ri) * C + c) * g.ldk +
-                          (h ? g.ldke : 0) + k;
+    // interleaved planes: 8 k of the high plane, then the same 8 k of the low plane
+    unsigned short* dst = Xp + 2 * ((int64_t)m * R * g.ldk +
+                                    ((int64_t)(b * 2 + ri) * C + c) * g.ldk + (h ? g.ldke : 0) + k);
     *reinterpret_cast<uint4*>(dst) = hi;
-    *reinterpret_cast<uint4*>(dst + pstride) = lo;
+    *reinterpret_cast<uint4*>(dst + 8) = lo;
   }
 }
 
-int launch_transpose_fwd_sym_h(const float2* Xn, unsigned short* Xp, int64_t pstride, int B, int C,
+int launch_transpose_fwd_sym_h(const float2* Xn, unsigned short* Xp, int B, int C,
                                const LatGeom& g, int mmax, const float* nscale,
                                const float* nshift, const float* lsig, float* isr,
                                hipStream_t s) {
@@ -425,11 +427,11 @@ int launch_transpose_fwd_sym_h(const float2* Xn, unsigned short* Xp, int64_t pst
   if (tk == 64) {
     dim3 grid((unsigned)cdiv(g.Ke, 64), (unsigned)cdiv(mmax, 32), (unsigned)(B * C));
     hipLaunchKernelGGL((transpose_fwd_sym4h_kernel<64, 32>), grid, dim3(256), 0, s, Xn, Xp,
-                       pstride, B, C, g, mmax, nscale, nshift, lsig, isr);
+                       B, C, g, mmax, nscale, nshift, lsig, isr);
   } else {
     dim3 grid((unsigned)cdiv(g.Ke, 128), (unsigned)cdiv(mmax, 32), (unsigned)(B * C));
     hipLaunchKernelGGL((transpose_fwd_sym4h_kernel<128, 32>), grid, dim3(256), 0, s, Xn, Xp,
-                       pstride, B, C, g, mmax, nscale, nshift, lsig, isr);
+                       B, C, g, mmax, nscale, nshift, lsig, isr);
   }
   return launch_check("transpose_fwd_sym_h");
 }
