@@ -1236,7 +1236,8 @@ int run_spectral(const msfno_block_desc* d, msfno_sht_plan_s* f, msfno_sht_plan_
                  const C2RPlanes* xplanes = nullptr,
                  const std::function<int()>& after_fft = std::function<int()>(),
                  const std::function<int()>& after_norm0 = std::function<int()>(),
-                 const std::function<int()>& after_leg = std::function<int()>()) {
+                 const std::function<int()>& after_leg = std::function<int()>(),
+                 const std::function<int()>& before_inv = std::function<int()>()) {
   const int64_t C = d->C, BC = (int64_t)B * C, R = 2 * BC;
   // x6 Legendre: symmetric plans, slab / coefficient planes carved, row path
   const bool lx6 = b.Xtp && b.Sp && f->sym && g->sym && !use_fft_tile(f) &&
@@ -1292,6 +1293,7 @@ int run_spectral(const msfno_block_desc* d, msfno_sht_plan_s* f, msfno_sht_plan_
   }
   if (after_leg) MSFNO_TRY(after_leg());
   MSFNO_TRY(run_filter(d, f, g, b, B, s, lx6 ? b.Sp : nullptr));
+  if (before_inv) MSFNO_TRY(before_inv());
   prof(ST_LEG_INV, s);
   if (lx6)
     MSFNO_TRY(legendre_inv_x6(g, b.Sp, b.Yt, (int)R, s));
@@ -1853,13 +1855,16 @@ int msfno_block_forward(const msfno_block_desc* d, msfno_sht_plan_t f, msfno_sht
   }
   // MSFNO_SKIP_AT=leg: fork the x3h skip after the forward Legendre instead of right
   // after the norm0 statistics (A/B of the overlap window)
-  static const bool skip_at_leg = [] {
+  // (inv: after the spectral filter, before the inverse Legendre)
+  static const int skip_at = [] {
     const char* e = getenv("MSFNO_SKIP_AT");
-    return e && std::string(e) == "leg";
+    return !e ? 0 : std::string(e) == "leg" ? 1 : std::string(e) == "inv" ? 2 : 0;
   }();
-  if (b.xs && skip_at_leg)
-    MSFNO_TRY(run_spectral(d, f, g, b, x, B, true, s, nullptr, std::function<int()>(),
-                           std::function<int()>(), launch_skip));
+  const std::function<int()> none;
+  if (b.xs && skip_at == 1)
+    MSFNO_TRY(run_spectral(d, f, g, b, x, B, true, s, nullptr, none, none, launch_skip));
+  else if (b.xs && skip_at == 2)
+    MSFNO_TRY(run_spectral(d, f, g, b, x, B, true, s, nullptr, none, none, none, launch_skip));
   else if (b.xs)  // x3h: the skip needs x's per-channel bounds (norm0 statistics) first
     MSFNO_TRY(run_spectral(d, f, g, b, x, B, true, s, nullptr, std::function<int()>(), launch_skip));
   else if (xpl)

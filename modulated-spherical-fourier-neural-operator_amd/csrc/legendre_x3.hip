@@ -518,12 +518,11 @@ __global__ __launch_bounds__(256) void legendre_x3r_kernel(X3DParams p) {
 // read covers all 64 banks once per 16 lanes); one barrier per chunk, the 16 x 16
 // block per wave scaled back by 1 / sigma_row, 1 / tau_n and stored from the
 // accumulator.  No conversion work in the kernel.
-constexpr int X3F_NSTG = 3;
 constexpr int X3F_STAGE = 2 * (X3F_KMAX / 32) * 1024;  // bytes per stage (max Kp)
 
 typedef float f4v __attribute__((ext_vector_type(4)));
 
-template <int KS>
+template <int KS, int NST>
 __device__ __forceinline__ void x3f_body(const X3FParams& p, const GemmDesc& d, int m0, int n0,
                                          unsigned char* ring, float* isr_s) {
   constexpr int KP = 32 * KS;
@@ -552,8 +551,9 @@ __device__ __forceinline__ void x3f_body(const X3FParams& p, const GemmDesc& d, 
       }
     }
   };
-  if (nch > 0) issue(0, 0);
-  if (nch > 1) issue(1, 1);
+#pragma unroll
+  for (int j = 0; j < NST - 1; ++j)
+    if (j < nch) issue(j, j);
 
   // B: this wave's 16 columns, lane (n = lane & 15, k = 32 ks + 8 (lane >> 4) .. + 7)
   const int col = n0 + 16 * wave + (lane & 15);
@@ -571,12 +571,16 @@ __device__ __forceinline__ void x3f_body(const X3FParams& p, const GemmDesc& d, 
   float* Cb = p.C + d.offC;
   const int ra = lane >> 4;  // the accumulator's rows 4 ra .. + 3
   for (int j = 0; j < nch; ++j) {
-    const int s = j % X3F_NSTG;
-    // chunk j's DMA (j >= 2) was issued before chunk j-2's 4 stores, chunk j+1's ni
-    // pieces and chunk j-1's 4 stores (chunks 0, 1 were drained with B)
-    if (j + 1 < nch) wait_vmcnt(8 + ni); else wait_vmcnt(8);
+    const int s = j % NST;
+    // chunk j's DMA (j >= NST - 1; the first NST - 1 were drained with B) was followed by
+    // the 4 stores of each of chunks j - NST + 1 .. j - 1 and the ni pieces of each
+    // chunk j + 1 .. j + NST - 2 that exists
+    int after = 4 * (NST - 1);
+#pragma unroll
+    for (int k = 1; k <= NST - 2; ++k) after += (j + k < nch) ? ni : 0;
+    wait_vmcnt(after);
     __syncthreads();
-    if (j + 2 < nch) issue(j + 2, (j + 2) % X3F_NSTG);
+    if (j + NST - 1 < nch) issue(j + NST - 1, (j + NST - 1) % NST);
     const unsigned char* st = ring + s * X3F_STAGE;
     const int r16 = lane & 15, kq = lane >> 4;
     const int off = r16 * 64 + 16 * (kq ^ ((r16 >> 2) & 3));
@@ -599,8 +603,9 @@ __device__ __forceinline__ void x3f_body(const X3FParams& p, const GemmDesc& d, 
   }
 }
 
+template <int NST>
 __global__ __launch_bounds__(256) void legendre_x3f_kernel(X3FParams p) {
-  __shared__ __attribute__((aligned(16))) unsigned char ring[X3F_NSTG * X3F_STAGE];
+  __shared__ __attribute__((aligned(16))) unsigned char ring[NST * X3F_STAGE];
   __shared__ float isr_s[X3F_RB];
   const int lin = xcd_remap(blockIdx.x, gridDim.x);
   const GemmDesc d = p.descs[p.tile_desc[lin]];
@@ -609,7 +614,7 @@ __global__ __launch_bounds__(256) void legendre_x3f_kernel(X3FParams p) {
   const int tn = local % d.tiles_n, tm = local / d.tiles_n;
   const int m0 = tm * X3F_RB, n0 = tn * 64;
   switch ((d.K + 31) / 32) {
-#define X3F_CASE(n) case n: x3f_body<n>(p, d, m0, n0, ring, isr_s); break;
+#define X3F_CASE(n) case n: x3f_body<n, NST>(p, d, m0, n0, ring, isr_s); break;
     X3F_CASE(1) X3F_CASE(2) X3F_CASE(3) X3F_CASE(4) X3F_CASE(5) X3F_CASE(6)
     X3F_CASE(7) X3F_CASE(8) X3F_CASE(9) X3F_CASE(10) X3F_CASE(11) X3F_CASE(12)
 #undef X3F_CASE
@@ -629,7 +634,15 @@ int legendre_x3f(const unsigned short* Ap, const float* isr,
   p.Ap = Ap; p.isr = isr;
   p.img = img; p.invs = invs; p.C = C;
   p.descs = descs; p.tile_desc = tile_desc;
-  hipLaunchKernelGGL(legendre_x3f_kernel, dim3(tiles), dim3(256), 0, s, p);
+  // MSFNO_X3F_NS=2: two LDS stages (49 KB, three workgroups per CU) instead of three
+  static const int ns = [] {
+    const char* e = getenv("MSFNO_X3F_NS");
+    return (e && e[0] == '2') ? 2 : 3;
+  }();
+  if (ns == 2)
+    hipLaunchKernelGGL(legendre_x3f_kernel<2>, dim3(tiles), dim3(256), 0, s, p);
+  else
+    hipLaunchKernelGGL(legendre_x3f_kernel<3>, dim3(tiles), dim3(256), 0, s, p);
   return launch_check("legendre_x3f");
 }
 

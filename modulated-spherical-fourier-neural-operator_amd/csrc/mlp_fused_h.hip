@@ -70,6 +70,7 @@ struct MlpHParams {
   const float* b2;      // [C] or null
   int64_t P;
   int tiles_per_field;
+  int stagger;  // s_sleep 127 rounds for the first tile of the second slot per CU
 };
 
 __host__ __device__ __forceinline__ int mh_swz(int r) { return ((r >> 2) & 1) << 1; }
@@ -241,6 +242,11 @@ __global__ __launch_bounds__(64 * W, (NG == 1 && W == 4) ? 2 : 1) void mlp_fused
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r16 = lane & 15, g = lane >> 4;
+  // phase shift: the workgroups that take the second slot of every CU first start
+  // about half a tile late, so the two co-resident tiles' memory phases (x1 in,
+  // output out) fall under each other's MFMA phases instead of all CUs loading at once
+  if (p.stagger && blockIdx.x >= 256 && blockIdx.x < 512)
+    for (int i = 0; i < p.stagger; ++i) __builtin_amdgcn_s_sleep(127);
   const int lin = xcd_remap(blockIdx.x, gridDim.x);
   const int z = lin / p.tiles_per_field;
   const int64_t P = p.P;
@@ -775,6 +781,11 @@ int launch_mlp_fused_h(const float* x1, const float* scale, const float* shift, 
   p.inv_s1 = sc;
   p.inv_s2 = sc + MH_H;
   p.b1 = b1; p.b2 = b2; p.P = P;
+  static const int stagger = [] {  // MSFNO_MH_STAGGER: s_sleep 127 rounds (A/B)
+    const char* e = getenv("MSFNO_MH_STAGGER");
+    return e ? atoi(e) : 0;
+  }();
+  p.stagger = stagger;
   // MSFNO_MH_NG: 16-pixel groups per wave (1 or 2); MSFNO_MH_W: waves per workgroup
   // (4: two workgroups per CU, 8: one workgroup of 128 pixels per CU)
   static const int ng = [] {
