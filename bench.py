@@ -83,10 +83,21 @@ STAGE_KERNEL_F32 = {
 # x3h engine: the fused MLP, the inner skip (fp32 x, bias epilogue) and the spectral
 # MLP chain; the unfused fc1 / fc2 pair stays on x6
 STAGE_KERNEL_X3H = dict(STAGE_KERNEL_X6, **{
-    "inner_skip": "void msfno::gemm_x6_kernel<256, 256, 4, 2, true, 1, false, 2>(msfno::GemmParams)",
+    # inner skip at C = 256 on the fused-MLP tiling (MSFNO_SKIP_H=0: gemm_x3)
+    "inner_skip": "msfno::(anonymous namespace)::skip_h_kernel("
+                  "msfno::(anonymous namespace)::SkipHParams)",
     "mlp_fused": "void msfno::(anonymous namespace)::mlp_fused_h_kernel<2, 0, 1, 4, 4>"
                  "(msfno::(anonymous namespace)::MlpHParams)",
+    "legendre_fwd": "void msfno::(anonymous namespace)::legendre_x3f_kernel<3>("
+                    "msfno::(anonymous namespace)::X3FParams)",
+    "legendre_inv": "msfno::(anonymous namespace)::legendre_x3r_kernel("
+                    "msfno::(anonymous namespace)::X3DParams)",
 })
+# the linear filter's weight stream at batch 1 (any engine)
+STAGE_KERNEL_LINEAR = {
+    "linear_contract": "void msfno::compl_contract_dma_kernel<2>(float const*, float const*, "
+                       "float*, int, int, long, int)",
+}
 X6_STAGES = {"mlp_fc1", "mlp_fc2", "inner_skip", "mlp_fused"}
 X6_SPEC_STAGES = {"spectral_l0", "spectral_l1", "spectral_l2", "spectral_out"}
 X3H_STAGES = {"inner_skip", "mlp_fused"} | X6_SPEC_STAGES
@@ -133,8 +144,9 @@ def pmc_traffic(stage):
     """HBM bytes per launch of the stage's kernel from the newest committed PMC
     summary (profiles/*/pmc_traffic.json, written by tools/rocpd_summary.py from
     separate FETCH_SIZE / WRITE_SIZE passes, gfx950-corrected), or None."""
-    sym = (STAGE_KERNEL_X3H if x3h_engine() else
-           STAGE_KERNEL_X6 if x6_engine()[0] else STAGE_KERNEL_F32).get(stage)
+    sym = STAGE_KERNEL_LINEAR.get(stage) or (
+        STAGE_KERNEL_X3H if x3h_engine() else
+        STAGE_KERNEL_X6 if x6_engine()[0] else STAGE_KERNEL_F32).get(stage)
     if sym is None:
         return None, None
     import glob
@@ -545,7 +557,8 @@ def roofline(stages, args, B, C, rows, mset, name=None):
                               rows, mset)
     whole = rows is None and mset is None
     tr, tr_src = pmc_traffic(name) if (B == 1 and C == 256 and args.nlat == 721 and whole
-                                        and args.filter == "non-linear") else (None, None)
+                                        and (args.filter == "non-linear"
+                                             or name == "linear_contract")) else (None, None)
     if kind == "mfma":
         ach = amount / avg_s / 1e12
         peak, engine = mfma_peak(name)
