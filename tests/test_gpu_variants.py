@@ -45,6 +45,14 @@ VARIANTS = [
     {"MSFNO_TR_FWD": "2p", "MSFNO_TR_INV": "2p"},
     {"MSFNO_TR_INV": "16x128"},
     {"MSFNO_SIDE_CUSTRIDE": "3"},
+    {"MSFNO_LEG_X3R": "0"},
+    {"MSFNO_LEG_X3F": "0"},
+    {"MSFNO_TRH": "128"},
+    {"MSFNO_X3F_NS": "2"},
+    {"MSFNO_SKIP_H": "0"},
+    {"MSFNO_SKIP_AT": "leg"},
+    {"MSFNO_SKIP_AT": "inv"},
+    {"MSFNO_MH_STAGGER": "4"},
 ]
 
 
