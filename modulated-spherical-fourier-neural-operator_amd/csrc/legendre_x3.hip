@@ -364,11 +364,15 @@ constexpr int X3R_STAGE = 2 * (X3R_KMAX / 16) * 1024;  // bytes per stage (max K
 
 // masked lanes store here, so every wave issues exactly 16 stores per chunk (the
 // DMA waits count them)
-__device__ float x3r_sink[64];
+__device__ float x3r_sink[256];
 
 __device__ __forceinline__ int x3r_swz(int n) { return (n >> 3) & 1; }
 
-template <int NK>
+// TR: the accumulator holds C^T (the table as the MFMA A operand): a lane keeps one
+// slab row and 4 consecutive latitudes per register group, stored as 16-B vectors
+// (4 stores per chunk instead of 16; unsegmented C, ldc and offC multiples of 4; the
+// last vector of a row may write up to 3 pad columns, which nothing reads)
+template <int NK, bool TR>
 __device__ __forceinline__ void x3r_body(const X3DParams& p, const GemmDesc& d, int m0,
                                          unsigned char* ring, float* tau_s) {
   constexpr int KS = 2 * NK;       // 16-deep k-steps
@@ -445,15 +449,16 @@ __device__ __forceinline__ void x3r_body(const X3DParams& p, const GemmDesc& d, 
   // 1 / sigma of the 16 rows this lane's accumulator holds: (r & 3) + 8 (r >> 2) + 4 half
   float isv[16];
 #pragma unroll
-  for (int r = 0; r < 16; ++r) isv[r] = __shfl(1.f / sg, (r & 3) + 8 * (r >> 2) + 4 * half);
+  for (int r = 0; r < 16; ++r) isv[r] = TR ? 1.f / sg : __shfl(1.f / sg, (r & 3) + 8 * (r >> 2) + 4 * half);
+  constexpr int NSTORE = TR ? 4 : 16;  // store instructions per chunk
 
   const int rbase = m0 + 32 * wave + 4 * half;
   float* Cb = p.C + d.offC;
   for (int j = 0; j < nch; ++j) {
     const int s = j % X3R_NSTG;
-    // chunk j's DMA (j >= 2) was issued before chunk j-2's 16 stores, chunk j+1's NI
-    // pieces and chunk j-1's 16 stores (chunks 0, 1 were drained with A)
-    if (j + 1 < nch) wait_vmcnt(32 + NI); else wait_vmcnt(32);
+    // chunk j's DMA (j >= 2) was issued before chunk j-2's stores, chunk j+1's NI
+    // pieces and chunk j-1's stores (chunks 0, 1 were drained with A)
+    if (j + 1 < nch) wait_vmcnt(2 * NSTORE + NI); else wait_vmcnt(2 * NSTORE);
     __syncthreads();
     if (j + 2 < nch) issue(j + 2, (j + 2) % X3R_NSTG);
     const unsigned char* st = ring + s * X3R_STAGE;
@@ -465,9 +470,28 @@ __device__ __forceinline__ void x3r_body(const X3DParams& p, const GemmDesc& d, 
       const int off = ks * 1024 + l32 * 32 + 16 * (half ^ x3r_swz(l32));
       const h8 b0 = *reinterpret_cast<const h8*>(st + off);
       const h8 b1 = *reinterpret_cast<const h8*>(st + KS * 1024 + off);
-      acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[ks][1], b0, acc, 0, 0, 0);
-      acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[ks][0], b1, acc, 0, 0, 0);
-      acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[ks][0], b0, acc, 0, 0, 0);
+      if constexpr (TR) {
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(b0, a[ks][1], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(b1, a[ks][0], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(b0, a[ks][0], acc, 0, 0, 0);
+      } else {
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[ks][1], b0, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[ks][0], b1, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[ks][0], b0, acc, 0, 0, 0);
+      }
+    }
+    if constexpr (TR) {
+      const int row = m0 + 32 * wave + l32;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int lat0 = 32 * j + 8 * g + 4 * half;
+        const float4 t4 = *reinterpret_cast<const float4*>(tau_s + lat0);
+        const float4 v = make_float4(acc[4 * g] * isv[0] * t4.x, acc[4 * g + 1] * isv[0] * t4.y,
+                                     acc[4 * g + 2] * isv[0] * t4.z, acc[4 * g + 3] * isv[0] * t4.w);
+        float* dst = (row < M && lat0 < N) ? Cb + (int64_t)row * d.ldc + lat0 : x3r_sink + 4 * lane;
+        *reinterpret_cast<float4*>(dst) = v;
+      }
+      continue;
     }
     const int col = 32 * j + l32;
     const float it = tau_s[min(col, N - 1)];
@@ -490,20 +514,21 @@ __device__ __forceinline__ void x3r_zero(const X3DParams& p, const GemmDesc& d, 
   }
 }
 
+template <bool TR>
 __global__ __launch_bounds__(256) void legendre_x3r_kernel(X3DParams p) {
   __shared__ __attribute__((aligned(16))) unsigned char ring[X3R_NSTG * X3R_STAGE];
-  __shared__ float tau_s[X3R_NMAX];
+  __shared__ __attribute__((aligned(16))) float tau_s[X3R_NMAX + 32];
   const int lin = xcd_remap(blockIdx.x, gridDim.x);
   const GemmDesc d = p.descs[p.tile_desc[lin]];
   const int m0 = (lin - d.tile_start) * X3D_BM;
   switch ((d.K + 31) / 32) {
     case 0: x3r_zero(p, d, m0); break;
-    case 1: x3r_body<1>(p, d, m0, ring, tau_s); break;
-    case 2: x3r_body<2>(p, d, m0, ring, tau_s); break;
-    case 3: x3r_body<3>(p, d, m0, ring, tau_s); break;
-    case 4: x3r_body<4>(p, d, m0, ring, tau_s); break;
-    case 5: x3r_body<5>(p, d, m0, ring, tau_s); break;
-    default: x3r_body<6>(p, d, m0, ring, tau_s); break;
+    case 1: x3r_body<1, TR>(p, d, m0, ring, tau_s); break;
+    case 2: x3r_body<2, TR>(p, d, m0, ring, tau_s); break;
+    case 3: x3r_body<3, TR>(p, d, m0, ring, tau_s); break;
+    case 4: x3r_body<4, TR>(p, d, m0, ring, tau_s); break;
+    case 5: x3r_body<5, TR>(p, d, m0, ring, tau_s); break;
+    default: x3r_body<6, TR>(p, d, m0, ring, tau_s); break;
   }
 }
 
@@ -658,7 +683,16 @@ int legendre_x3r(const float* A, const unsigned short* img, const float* invs, f
   p.A = A; p.img = img; p.invs = invs; p.C = C;
   p.descs = descs; p.tile_desc = tile_desc; p.ndesc = ndesc;
   p.segC_w = e.segC_w; p.segC_stride = e.segC_stride;
-  hipLaunchKernelGGL(legendre_x3r_kernel, dim3(tiles), dim3(256), 0, s, p);
+  // MSFNO_X3R_T=1: C^T accumulators, 16-B stores (unsegmented C only)
+  static const bool tr_env = [] {
+    const char* e = getenv("MSFNO_X3R_T");
+    return e && e[0] == '1';
+  }();
+  const bool tr = tr_env && !e.segC_w && (reinterpret_cast<uintptr_t>(C) & 15) == 0;
+  if (tr)
+    hipLaunchKernelGGL(legendre_x3r_kernel<true>, dim3(tiles), dim3(256), 0, s, p);
+  else
+    hipLaunchKernelGGL(legendre_x3r_kernel<false>, dim3(tiles), dim3(256), 0, s, p);
   return launch_check("legendre_x3r");
 }
 

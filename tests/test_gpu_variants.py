@@ -53,6 +53,7 @@ VARIANTS = [
     {"MSFNO_SKIP_AT": "leg"},
     {"MSFNO_SKIP_AT": "inv"},
     {"MSFNO_MH_STAGGER": "4"},
+    {"MSFNO_X3R_T": "1"},
 ]
 
 
