@@ -372,9 +372,15 @@ __device__ __forceinline__ int x3r_swz(int n) { return (n >> 3) & 1; }
 // slab row and 4 consecutive latitudes per register group, stored as 16-B vectors
 // (4 stores per chunk instead of 16; unsegmented C, ldc and offC multiples of 4; the
 // last vector of a row may write up to 3 pad columns, which nothing reads)
-template <int NK, bool TR>
+// DEEP: the ring holds as many stages of this problem's size as fit the 72 KB
+// (six for Kp <= 96, four for 128, three above): short-K problems are latency-bound
+// (a chunk's MFMAs are a few hundred cycles against one DMA round trip)
+template <int NK, bool TR, bool DEEP>
 __device__ __forceinline__ void x3r_body(const X3DParams& p, const GemmDesc& d, int m0,
                                          unsigned char* ring, float* tau_s) {
+  constexpr int STG = DEEP ? 4 * NK * 1024 : X3R_STAGE;  // bytes per stage
+  constexpr int NST = !DEEP ? X3R_NSTG : NK <= 3 ? 6 : NK == 4 ? 4 : 3;
+  static_assert(NST * STG <= X3R_NSTG * X3R_STAGE, "ring");
   constexpr int KS = 2 * NK;       // 16-deep k-steps
   constexpr int KP = 32 * NK;      // padded K of the image
   constexpr int NI = KP / 32;      // DMA wave-instructions per wave and stage (= NK)
@@ -395,11 +401,12 @@ __device__ __forceinline__ void x3r_body(const X3DParams& p, const GemmDesc& d, 
       const int i = wave + 4 * q;
       const int pl = i / KS, ks = i % KS;
       const unsigned short* src = Bimg + ((int64_t)pl * N + ng) * KP + 16 * ks + 8 * hc;
-      glds16(src, ring_lds + s * X3R_STAGE + i * 1024);
+      glds16(src, ring_lds + s * STG + i * 1024);
     }
   };
-  if (nch > 0) issue(0, 0);
-  if (nch > 1) issue(1, 1);
+#pragma unroll
+  for (int j = 0; j < NST - 1; ++j)
+    if (j < nch) issue(j, j);
   // 1 / tau_n of every column into LDS (no global load inside the chunk loop: hipcc
   // would wait for it with a vmcnt that also drains the DMA in flight)
   for (int n = tid; n < N; n += 256) tau_s[n] = p.invs[d.offBs + n];
@@ -455,13 +462,17 @@ __device__ __forceinline__ void x3r_body(const X3DParams& p, const GemmDesc& d, 
   const int rbase = m0 + 32 * wave + 4 * half;
   float* Cb = p.C + d.offC;
   for (int j = 0; j < nch; ++j) {
-    const int s = j % X3R_NSTG;
-    // chunk j's DMA (j >= 2) was issued before chunk j-2's stores, chunk j+1's NI
-    // pieces and chunk j-1's stores (chunks 0, 1 were drained with A)
-    if (j + 1 < nch) wait_vmcnt(2 * NSTORE + NI); else wait_vmcnt(2 * NSTORE);
+    const int s = j % NST;
+    // chunk j's DMA (j >= NST - 1; the first NST - 1 were drained with A) was followed
+    // by the stores of chunks j - NST + 1 .. j - 1 and the NI pieces of each chunk
+    // j + 1 .. j + NST - 2 that exists (wait_vmcnt caps the count: waiting longer is safe)
+    int after = (NST - 1) * NSTORE;
+#pragma unroll
+    for (int k = 1; k <= NST - 2; ++k) after += (j + k < nch) ? NI : 0;
+    wait_vmcnt(after);
     __syncthreads();
-    if (j + 2 < nch) issue(j + 2, (j + 2) % X3R_NSTG);
-    const unsigned char* st = ring + s * X3R_STAGE;
+    if (j + NST - 1 < nch) issue(j + NST - 1, (j + NST - 1) % NST);
+    const unsigned char* st = ring + s * STG;
     floatx16 acc;
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[r] = 0.f;
@@ -514,7 +525,7 @@ __device__ __forceinline__ void x3r_zero(const X3DParams& p, const GemmDesc& d, 
   }
 }
 
-template <bool TR>
+template <bool TR, bool DEEP>
 __global__ __launch_bounds__(256) void legendre_x3r_kernel(X3DParams p) {
   __shared__ __attribute__((aligned(16))) unsigned char ring[X3R_NSTG * X3R_STAGE];
   __shared__ __attribute__((aligned(16))) float tau_s[X3R_NMAX + 32];
@@ -523,12 +534,12 @@ __global__ __launch_bounds__(256) void legendre_x3r_kernel(X3DParams p) {
   const int m0 = (lin - d.tile_start) * X3D_BM;
   switch ((d.K + 31) / 32) {
     case 0: x3r_zero(p, d, m0); break;
-    case 1: x3r_body<1, TR>(p, d, m0, ring, tau_s); break;
-    case 2: x3r_body<2, TR>(p, d, m0, ring, tau_s); break;
-    case 3: x3r_body<3, TR>(p, d, m0, ring, tau_s); break;
-    case 4: x3r_body<4, TR>(p, d, m0, ring, tau_s); break;
-    case 5: x3r_body<5, TR>(p, d, m0, ring, tau_s); break;
-    default: x3r_body<6, TR>(p, d, m0, ring, tau_s); break;
+    case 1: x3r_body<1, TR, DEEP>(p, d, m0, ring, tau_s); break;
+    case 2: x3r_body<2, TR, DEEP>(p, d, m0, ring, tau_s); break;
+    case 3: x3r_body<3, TR, DEEP>(p, d, m0, ring, tau_s); break;
+    case 4: x3r_body<4, TR, DEEP>(p, d, m0, ring, tau_s); break;
+    case 5: x3r_body<5, TR, DEEP>(p, d, m0, ring, tau_s); break;
+    default: x3r_body<6, TR, DEEP>(p, d, m0, ring, tau_s); break;
   }
 }
 
@@ -689,10 +700,15 @@ int legendre_x3r(const float* A, const unsigned short* img, const float* invs, f
     return e && e[0] == '1';
   }();
   const bool tr = tr_env && !e.segC_w && (reinterpret_cast<uintptr_t>(C) & 15) == 0;
-  if (tr)
-    hipLaunchKernelGGL(legendre_x3r_kernel<true>, dim3(tiles), dim3(256), 0, s, p);
-  else
-    hipLaunchKernelGGL(legendre_x3r_kernel<false>, dim3(tiles), dim3(256), 0, s, p);
+  // MSFNO_X3R_DEEP=1: as many stages of the problem's own size as fit (measured equal:
+  // 0.285 vs 0.285 ms in-block — the kernel is not bound by DMA depth)
+  static const bool deep = [] {
+    const char* e = getenv("MSFNO_X3R_DEEP");
+    return e && e[0] == '1';
+  }();
+  void (*kern)(X3DParams) = tr ? (deep ? legendre_x3r_kernel<true, true> : legendre_x3r_kernel<true, false>)
+                                : (deep ? legendre_x3r_kernel<false, true> : legendre_x3r_kernel<false, false>);
+  hipLaunchKernelGGL(kern, dim3(tiles), dim3(256), 0, s, p);
   return launch_check("legendre_x3r");
 }
 

@@ -54,6 +54,7 @@ VARIANTS = [
     {"MSFNO_SKIP_AT": "inv"},
     {"MSFNO_MH_STAGGER": "4"},
     {"MSFNO_X3R_T": "1"},
+    {"MSFNO_X3R_DEEP": "1"},
 ]
 
 
