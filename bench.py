@@ -90,7 +90,7 @@ STAGE_KERNEL_X3H = dict(STAGE_KERNEL_X6, **{
                  "(msfno::(anonymous namespace)::MlpHParams)",
     "legendre_fwd": "void msfno::(anonymous namespace)::legendre_x3f_kernel<3>("
                     "msfno::(anonymous namespace)::X3FParams)",
-    "legendre_inv": "msfno::(anonymous namespace)::legendre_x3r_kernel("
+    "legendre_inv": "void msfno::(anonymous namespace)::legendre_x3r_kernel<false, false>("
                     "msfno::(anonymous namespace)::X3DParams)",
 })
 # the linear filter's weight stream at batch 1 (any engine)
