@@ -1817,6 +1817,8 @@ int msfno_block_forward(const msfno_block_desc* d, msfno_sht_plan_t f, msfno_sht
   SideCtx* side = nullptr;
   const bool xpl = skip_planes(d, f, b);
   const C2RPlanes xp{b.x1p, (int)C, f->nlat};
+  // skip_h with per-pixel scales needs no norm0 statistics: forked at the block start
+  const bool skip_px = b.xs && C == 256 && skip_h_env() && skip_px_env();
   auto launch_skip = [&]() -> int {
     hipStream_t ss = s;
     if (side) {  // fork
@@ -1828,7 +1830,8 @@ int msfno_block_forward(const msfno_block_desc* d, msfno_sht_plan_t f, msfno_sht
     GemmEpi e;
     e.bias = d->skip_b;
     if (b.xs && C == 256 && skip_h_env()) {
-      MSFNO_TRY(launch_skip_h(d->skip_w, b.xs, x, x1, d->skip_b, B, P, b.dw.skip, b.dw.skip_b, ss));
+      MSFNO_TRY(launch_skip_h(d->skip_w, skip_px ? nullptr : b.xs, x, x1, d->skip_b, B, P,
+                              b.dw.skip, b.dw.skip_b, ss));
     } else if (b.xs) {
       MSFNO_TRY(gemm_x3(d->skip_w, (int)C, b.xs, x, x1, (int)C, (int)P, (int)C, (int)P, (int)P,
                         C * P, C * P, B, e, b.dw.skip, b.dw.skip_b, ss));
@@ -1851,7 +1854,7 @@ int msfno_block_forward(const msfno_block_desc* d, msfno_sht_plan_t f, msfno_sht
   if (d->inner_skip == MSFNO_SKIP_LINEAR) {
     MSFNO_REQUIRE(d->skip_w, MSFNO_EINVAL, "missing inner_skip weight");
     MSFNO_TRY(side_ctx(&side, s));
-    if (!xpl && !b.xs) MSFNO_TRY(launch_skip());
+    if ((!xpl && !b.xs) || skip_px) MSFNO_TRY(launch_skip());
   }
   // MSFNO_SKIP_AT=leg: fork the x3h skip after the forward Legendre instead of right
   // after the norm0 statistics (A/B of the overlap window)
@@ -1861,7 +1864,9 @@ int msfno_block_forward(const msfno_block_desc* d, msfno_sht_plan_t f, msfno_sht
     return !e ? 0 : std::string(e) == "leg" ? 1 : std::string(e) == "inv" ? 2 : 0;
   }();
   const std::function<int()> none;
-  if (b.xs && skip_at == 1)
+  if (skip_px)
+    MSFNO_TRY(run_spectral(d, f, g, b, x, B, true, s));
+  else if (b.xs && skip_at == 1)
     MSFNO_TRY(run_spectral(d, f, g, b, x, B, true, s, nullptr, none, none, launch_skip));
   else if (b.xs && skip_at == 2)
     MSFNO_TRY(run_spectral(d, f, g, b, x, B, true, s, nullptr, none, none, none, launch_skip));

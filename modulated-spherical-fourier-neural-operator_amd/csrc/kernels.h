@@ -106,8 +106,10 @@ int launch_mlp_fused2_images(const float* W1, const float* W2, unsigned short* i
 // MFMAs per product, row-scaled weights); default (MSFNO_ENGINE=x6 selects the x6 engine)
 bool mlp_fused_h_env();
 // inner skip at C = 256 on the mlp_fused_h tiling (x3h): out = Ws·x + bs, x scaled by the
-// power-of-two channel scales xs (|xs x| < 2^14); ws >= skip_h_workspace(B)
+// power-of-two channel scales xs (|xs x| < 2^14), or per pixel in-kernel when xs is null;
+// ws >= skip_h_workspace(B)
 bool skip_h_env();
+bool skip_px_env();  // skip_h with per-pixel scales (xs = null) at the block start
 size_t skip_h_workspace(int B);
 int launch_skip_h(const float* W, const float* xs, const float* x, float* out, const float* bias,
                   int B, int64_t P, void* ws, size_t ws_bytes, hipStream_t s);

@@ -550,7 +550,7 @@ __global__ __launch_bounds__(256) void sk_scale_kernel(const float* __restrict__
                                                        float* __restrict__ inv_rs) {
   __shared__ float wmax[4];
   const int b = blockIdx.y, c = blockIdx.x, k = threadIdx.x;
-  float m = fabsf(W[(int64_t)c * MH_C + k] / xs[(int64_t)b * MH_C + k]);
+  float m = fabsf(xs ? W[(int64_t)c * MH_C + k] / xs[(int64_t)b * MH_C + k] : W[(int64_t)c * MH_C + k]);
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
   if ((k & 63) == 0) wmax[k >> 6] = m;
@@ -572,7 +572,7 @@ __global__ void sk_image_kernel(const float* __restrict__ W, const float* __rest
                                 const float* __restrict__ rs, unsigned short* __restrict__ img) {
   constexpr int64_t PAIRS = (int64_t)8 * 2 * 4 * 2 * 16 * 16;
   const int b = blockIdx.y;
-  const float* xsb = xs + (int64_t)b * MH_C;
+  const float* xsb = xs ? xs + (int64_t)b * MH_C : nullptr;
   unsigned short* ib = img + (int64_t)b * SK_NSLICE * MH_SLICE;
   for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < PAIRS;
        e += (int64_t)gridDim.x * blockDim.x) {
@@ -589,7 +589,10 @@ __global__ void sk_image_kernel(const float* __restrict__ W, const float* __rest
     const float* src = W + (int64_t)row * MH_C + k;
     const float sc = rs[(int64_t)b * MH_C + row];
     uint32_t t0, t1;
-    split2h(src[0] / xsb[k] * sc, src[1] / xsb[k + 1] * sc, t0, t1);
+    if (xsb)
+      split2h(src[0] / xsb[k] * sc, src[1] / xsb[k + 1] * sc, t0, t1);
+    else
+      split2h(src[0] * sc, src[1] * sc, t0, t1);
     uint32_t* o = reinterpret_cast<uint32_t*>(
         ib + (int64_t)(j * 2 + kh) * MH_SLICE + ((ks * 2 + t) * 16 + r) * 32 + kk);
     o[0] = t0;
@@ -597,6 +600,12 @@ __global__ void sk_image_kernel(const float* __restrict__ W, const float* __rest
   }
 }
 
+// PX: x scaled per pixel instead of per channel (xs null): the lane's 64 values and
+// those of the three other lanes of its pixel give max_c |x[c][px]| = f 2^e, the column
+// is split under 2^(15 - e) and the output column multiplied back by 2^(e - 15) — exact
+// powers of two, so no dependence on the norm0 statistics (the skip can start with the
+// block) and a batch-independent weight image
+template <bool PX>
 __global__ __launch_bounds__(256, 2) void skip_h_kernel(SkipHParams p) {
   constexpr int NS = MH_NS, W = 4;
   constexpr int RING_BYTES = NS * MH_SLICE * 2;
@@ -611,7 +620,8 @@ __global__ __launch_bounds__(256, 2) void skip_h_kernel(SkipHParams p) {
   const int z = lin / p.tiles_per_field;
   const int64_t P = p.P;
   const int64_t px = (int64_t)(lin - z * p.tiles_per_field) * 64 + 16 * wave + r16;
-  const unsigned short* img = p.img + (int64_t)z * SK_NSLICE * MH_SLICE;
+  const int zi = PX ? 0 : z;  // per-pixel scales: one image for every batch
+  const unsigned short* img = p.img + (int64_t)zi * SK_NSLICE * MH_SLICE;
 
   const uint32_t ring_lds = lds_addr(ring);
   const int wave_u = __builtin_amdgcn_readfirstlane(wave);
@@ -625,28 +635,61 @@ __global__ __launch_bounds__(256, 2) void skip_h_kernel(SkipHParams p) {
 #pragma unroll
   for (int q = 0; q < NS; ++q) issue(q);
 
-  // x -> xs-scaled fp16x2 B fragments (k-step ks: channels 32 ks + 8 g + 0..7)
-  const float* xsb = p.xs + (int64_t)z * MH_C;
+  // x -> scaled fp16x2 B fragments (k-step ks: channels 32 ks + 8 g + 0..7)
   const float* xcol = p.x + (int64_t)z * MH_C * P + (px < P ? px : P - 1);
   half8 xf[8][2];
+  float ipx = 1.f;  // PX: 1 / the pixel's scale
+  if constexpr (PX) {
+    float xv[8][8];
 #pragma unroll
-  for (int ks = 0; ks < 8; ++ks) {
-    const int c0 = 32 * ks + 8 * g;
-    float xv[8];
+    for (int ks = 0; ks < 8; ++ks)
 #pragma unroll
-    for (int e = 0; e < 8; ++e) xv[e] = __builtin_nontemporal_load(xcol + (int64_t)(c0 + e) * P);
-    const float4 sa = *reinterpret_cast<const float4*>(xsb + c0);
-    const float4 sb = *reinterpret_cast<const float4*>(xsb + c0 + 4);
-    const float sv[8] = {sa.x, sa.y, sa.z, sa.w, sb.x, sb.y, sb.z, sb.w};
-    uint32_t t[2][4];
+      for (int e = 0; e < 8; ++e)
+        xv[ks][e] = __builtin_nontemporal_load(xcol + (int64_t)(32 * ks + 8 * g + e) * P);
+    float m = 0.f;
 #pragma unroll
-    for (int e = 0; e < 4; ++e)
-      split2h(sv[2 * e] * xv[2 * e], sv[2 * e + 1] * xv[2 * e + 1], t[0][e], t[1][e]);
+    for (int ks = 0; ks < 8; ++ks)
 #pragma unroll
-    for (int pl = 0; pl < 2; ++pl) xf[ks][pl] = mh_frag(t[pl][0], t[pl][1], t[pl][2], t[pl][3]);
+      for (int e = 0; e < 8; ++e) m = fmaxf(m, fabsf(xv[ks][e]));
+    m = fmaxf(m, __shfl_xor(m, 16));
+    m = fmaxf(m, __shfl_xor(m, 32));
+    float sp = 1.f;
+    if (m > 0.f && isfinite(m)) {
+      int e;
+      frexpf(m, &e);
+      sp = ldexpf(1.f, 15 - e);
+      ipx = ldexpf(1.f, e - 15);
+    }
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks) {
+      uint32_t t[2][4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        split2h(sp * xv[ks][2 * e], sp * xv[ks][2 * e + 1], t[0][e], t[1][e]);
+#pragma unroll
+      for (int pl = 0; pl < 2; ++pl) xf[ks][pl] = mh_frag(t[pl][0], t[pl][1], t[pl][2], t[pl][3]);
+    }
+  } else {
+    const float* xsb = p.xs + (int64_t)z * MH_C;
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks) {
+      const int c0 = 32 * ks + 8 * g;
+      float xv[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) xv[e] = __builtin_nontemporal_load(xcol + (int64_t)(c0 + e) * P);
+      const float4 sa = *reinterpret_cast<const float4*>(xsb + c0);
+      const float4 sb = *reinterpret_cast<const float4*>(xsb + c0 + 4);
+      const float sv[8] = {sa.x, sa.y, sa.z, sa.w, sb.x, sb.y, sb.z, sb.w};
+      uint32_t t[2][4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        split2h(sv[2 * e] * xv[2 * e], sv[2 * e + 1] * xv[2 * e + 1], t[0][e], t[1][e]);
+#pragma unroll
+      for (int pl = 0; pl < 2; ++pl) xf[ks][pl] = mh_frag(t[pl][0], t[pl][1], t[pl][2], t[pl][3]);
+    }
   }
   for (int i = tid; i < MH_C; i += 256) {
-    irs[i] = p.inv_rs[(int64_t)z * MH_C + i];
+    irs[i] = p.inv_rs[(int64_t)zi * MH_C + i];
     bs[i] = p.bias ? p.bias[i] : 0.f;
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -699,7 +742,8 @@ __global__ __launch_bounds__(256, 2) void skip_h_kernel(SkipHParams p) {
     const int r0 = 16 * ot + 4 * g;
     const float4 is = *reinterpret_cast<const float4*>(irs + r0);
     const float4 b = *reinterpret_cast<const float4*>(bs + r0);
-    const float isv[4] = {is.x, is.y, is.z, is.w}, bv[4] = {b.x, b.y, b.z, b.w};
+    const float isv[4] = {is.x * ipx, is.y * ipx, is.z * ipx, is.w * ipx};
+    const float bv[4] = {b.x, b.y, b.z, b.w};
 #pragma unroll
     for (int i = 0; i < 4; ++i) o[(int64_t)(r0 + i) * P] = fmaf(oacc[ot][i], isv[i], bv[i]);
   }
@@ -709,6 +753,16 @@ __global__ __launch_bounds__(256, 2) void skip_h_kernel(SkipHParams p) {
 
 size_t skip_h_workspace(int B) {
   return (size_t)B * SK_NSLICE * MH_SLICE * 2 + (size_t)B * MH_C * 4 * 2 + 256;
+}
+
+// MSFNO_SKIP_PX=0: per-channel scales from the norm0 statistics (the skip then waits for
+// them) instead of per-pixel scales (the skip starts with the block)
+bool skip_px_env() {
+  static const bool on = [] {
+    const char* e = getenv("MSFNO_SKIP_PX");
+    return !(e && e[0] == '0');
+  }();
+  return on;
 }
 
 // MSFNO_SKIP_H=0 keeps gemm_x3 for the inner skip
@@ -722,21 +776,26 @@ bool skip_h_env() {
 
 int launch_skip_h(const float* W, const float* xs, const float* x, float* out, const float* bias,
                   int B, int64_t P, void* ws, size_t ws_bytes, hipStream_t s) {
-  MSFNO_REQUIRE(W && xs && x && out && ws && B > 0 && P >= 1 && ws_bytes >= skip_h_workspace(B),
+  MSFNO_REQUIRE(W && x && out && ws && B > 0 && P >= 1 && ws_bytes >= skip_h_workspace(B),
                 MSFNO_EINVAL, "skip_h: bad arguments");
+  // xs null: per-pixel scales, one batch-independent weight image
+  const int nimg = xs ? B : 1;
   unsigned short* img = static_cast<unsigned short*>(ws);
   float* rs = reinterpret_cast<float*>(img + (int64_t)B * SK_NSLICE * MH_SLICE);
   float* inv_rs = rs + (int64_t)B * MH_C;
-  hipLaunchKernelGGL(sk_scale_kernel, dim3(MH_C, B), dim3(256), 0, s, W, xs, rs, inv_rs);
+  hipLaunchKernelGGL(sk_scale_kernel, dim3(MH_C, nimg), dim3(256), 0, s, W, xs, rs, inv_rs);
   MSFNO_TRY(launch_check("sk_scale"));
-  hipLaunchKernelGGL(sk_image_kernel, dim3(64, B), dim3(256), 0, s, W, xs, rs, img);
+  hipLaunchKernelGGL(sk_image_kernel, dim3(64, nimg), dim3(256), 0, s, W, xs, rs, img);
   MSFNO_TRY(launch_check("sk_image"));
   SkipHParams p{};
   p.x = x; p.xs = xs; p.out = out; p.img = img; p.inv_rs = inv_rs; p.bias = bias; p.P = P;
   p.tiles_per_field = (int)cdiv(P, 64);
   const int64_t tiles = (int64_t)B * p.tiles_per_field;
   MSFNO_REQUIRE(tiles < (1LL << 31), MSFNO_EINVAL, "skip_h: grid too large");
-  hipLaunchKernelGGL(skip_h_kernel, dim3((unsigned)tiles), dim3(256), 0, s, p);
+  if (xs)
+    hipLaunchKernelGGL(skip_h_kernel<false>, dim3((unsigned)tiles), dim3(256), 0, s, p);
+  else
+    hipLaunchKernelGGL(skip_h_kernel<true>, dim3((unsigned)tiles), dim3(256), 0, s, p);
   return launch_check("skip_h");
 }
 
