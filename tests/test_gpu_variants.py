@@ -55,7 +55,7 @@ VARIANTS = [
     {"MSFNO_MH_STAGGER": "4"},
     {"MSFNO_X3R_T": "1"},
     {"MSFNO_X3R_DEEP": "1"},
-    {"MSFNO_SKIP_PX": "0"},
+    {"MSFNO_SKIP_PX": "1"},
 ]
 
 
