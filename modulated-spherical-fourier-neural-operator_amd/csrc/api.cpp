@@ -872,6 +872,7 @@ void carve_block(Carve& cv, BlockBufs& b, const msfno_block_desc* d,
   b.st1 = cv.take<float2>(BC * g->nlat);
   b.sc1 = cv.take<float>(BC);
   b.sh1 = cv.take<float>(BC);
+  b.ab1 = cv.take<float>(BC);
   if (mlp_fused(d, P)) {
     b.mfimg = wcache_mfimg(d);
     if (!b.mfimg) b.mfimg = cv.take<unsigned short>(mlp_fused_image_bytes() / 2);
@@ -1548,15 +1549,15 @@ bool x1p_buffer(const msfno_block_desc* d, const msfno_sht_plan_s* g) {
 }
 
 int run_block_mlp(const msfno_block_desc* d, const float* x1, const unsigned short* x1p,
-                  const float* sc1, const float* sh1, float* W1f, float* b1f, float* h,
+                  const float* sc1, const float* sh1, const float* ab1, float* W1f, float* b1f, float* h,
                   unsigned short* mfimg, float* out, const float* resid, int B, int64_t P,
                   const DenseWs& dw, hipStream_t s) {
   MSFNO_REQUIRE(d->fc1_w && d->fc2_w, MSFNO_EINVAL, "missing MLP weights");
   if (mfimg) {
     prof(ST_MLP_FUSED, s);
     if (!(wcache_ready(d) && mfimg == wcache_mfimg(d)))
-      MSFNO_TRY(launch_mlp_fused_images(d->fc1_w, d->fc2_w, mfimg, s));
-    return launch_mlp_fused(x1, sc1, sh1, resid, out, mfimg, d->fc1_b, d->fc2_b, B, P, s);
+      MSFNO_TRY(launch_mlp_fused_images(d->fc1_w, d->fc1_b, d->fc2_w, mfimg, s));
+    return launch_mlp_fused(x1, sc1, sh1, ab1, resid, out, mfimg, d->fc1_b, d->fc2_b, B, P, s);
   }
   const int64_t C = d->C, Hd = d->mlp_hidden;
   MSFNO_TRY(launch_fold_affine(d->fc1_w, d->fc1_b, sc1, sh1, W1f, b1f, B, (int)Hd, (int)C, s));
@@ -1851,10 +1852,30 @@ int msfno_block_forward(const msfno_block_desc* d, msfno_sht_plan_t f, msfno_sht
     }
     return MSFNO_OK;
   };
+  // MSFNO_PX_CHECK (diagnostic, PX mode only): 1 = snapshot x before the fork, and
+  // after the join recompute the skip serially and compare x1, the weight image and x
+  // bit for bit; 2 = also wait for the side stream on the host right after the skip is
+  // enqueued (nothing of this block overlaps it); 3 = wait for the caller's stream on
+  // the host before the fork
+  static const int px_check = [] {
+    const char* e = getenv("MSFNO_PX_CHECK");
+    return e ? atoi(e) : 0;
+  }();
+  static float* dbg_x = nullptr;
+  static int dbg_call = 0;
+  const bool pxc = px_check && skip_px && d->inner_skip == MSFNO_SKIP_LINEAR;
+  if (pxc) {
+    if (!dbg_x) {
+      MSFNO_CHECK_HIP(hipMalloc(&dbg_x, BC * P * sizeof(float)));
+    }
+    MSFNO_CHECK_HIP(hipMemcpyAsync(dbg_x, x, BC * P * sizeof(float), hipMemcpyDeviceToDevice, s));
+    if (px_check == 3) MSFNO_CHECK_HIP(hipStreamSynchronize(s));
+  }
   if (d->inner_skip == MSFNO_SKIP_LINEAR) {
     MSFNO_REQUIRE(d->skip_w, MSFNO_EINVAL, "missing inner_skip weight");
     MSFNO_TRY(side_ctx(&side, s));
     if ((!xpl && !b.xs) || skip_px) MSFNO_TRY(launch_skip());
+    if (pxc && px_check == 2 && side) MSFNO_CHECK_HIP(hipStreamSynchronize(side->side));
   }
   // MSFNO_SKIP_AT=leg: fork the x3h skip after the forward Legendre instead of right
   // after the norm0 statistics (A/B of the overlap window)
@@ -1877,6 +1898,56 @@ int msfno_block_forward(const msfno_block_desc* d, msfno_sht_plan_t f, msfno_sht
   else
     MSFNO_TRY(run_spectral(d, f, g, b, x, B, true, s));
   if (side) MSFNO_CHECK_HIP(hipStreamWaitEvent(s, side->join, 0));  // join
+  if (pxc) {
+    // serial recomputation: the skip, and the whole spectral path into a second
+    // workspace; every intermediate compared bit for bit with this call's
+    static void* dbg_ws2 = nullptr;
+    static unsigned long long* dbg_r = nullptr;
+    const size_t wsb = msfno_block_workspace_size(d, f, g, B);
+    if (!dbg_ws2) {
+      MSFNO_CHECK_HIP(hipMalloc(&dbg_ws2, wsb));
+      MSFNO_CHECK_HIP(hipMalloc(&dbg_r, 32 * sizeof(unsigned long long)));
+    }
+    Carve cv2;
+    cv2.base = static_cast<char*>(dbg_ws2);
+    BlockBufs b2;
+    carve_block(cv2, b2, d, f, g, B, true);
+    MSFNO_TRY(run_spectral(d, f, g, b2, x, B, true, s));
+    MSFNO_TRY(launch_skip_h(d->skip_w, nullptr, x, b2.x1, d->skip_b, B, P, b2.dw.skip,
+                            b2.dw.skip_b, s));
+    const int64_t R = 2 * BC;
+    struct Cmp { const char* name; const void* a; const void* b2; int64_t words; };
+    const Cmp cmps[] = {
+        {"x", dbg_x, x, BC * P},
+        {"x1", b.x1, b2.x1, BC * P},
+        {"skipimg", b.dw.skip, b2.dw.skip, (int64_t)(skip_h_workspace(B) - 256) / 4},
+        {"Xn", b.Xn, b2.Xn, BC * f->nlat * f->mmax * 2},
+        {"rs0", b.rs0, b2.rs0, BC * f->nlat * 2},
+        {"sc0", b.sc0, b2.sc0, BC},
+        {"sh0", b.sh0, b2.sh0, BC},
+        {"lsig", b.lsig, b2.lsig, b.lsig ? BC : 0},
+        {"isr", b.isr, b2.isr, b.isr ? R : 0},
+        {"Xt", b.Xt, b2.Xt, (int64_t)f->mmax * R * f->ldk},
+        {"S", b.Sa, b2.Sa, R * f->spec.ldT},
+        {"Yt", b.Yt, b2.Yt, (int64_t)g->mmax * R * g->ldk},
+    };
+    const int nc = (int)(sizeof(cmps) / sizeof(cmps[0]));
+    for (int i = 0; i < nc; ++i) {
+      MSFNO_CHECK_HIP(hipMemsetAsync(dbg_r + 2 * i, 0, sizeof(unsigned long long), s));
+      MSFNO_CHECK_HIP(hipMemsetAsync(dbg_r + 2 * i + 1, 0xff, sizeof(unsigned long long), s));
+      if (cmps[i].words > 0)
+        MSFNO_TRY(launch_debug_cmp(cmps[i].a, cmps[i].b2, cmps[i].words, dbg_r + 2 * i, s));
+    }
+    unsigned long long h[32];
+    MSFNO_CHECK_HIP(hipMemcpyAsync(h, dbg_r, 2 * nc * sizeof(unsigned long long),
+                                   hipMemcpyDeviceToHost, s));
+    MSFNO_CHECK_HIP(hipStreamSynchronize(s));
+    std::string line = "PX_CHECK call " + std::to_string(dbg_call++) + ":";
+    for (int i = 0; i < nc; ++i)
+      line += std::string(" ") + cmps[i].name + "=" + std::to_string(h[2 * i]) +
+              (h[2 * i] ? "@" + std::to_string((long long)h[2 * i + 1]) : std::string());
+    fprintf(stderr, "%s\n", line.c_str());
+  }
   // ---- filter output + skip (+ GELU for the linear filter) -> x1, norm1 partials ---
   const float* skip_src = d->inner_skip == MSFNO_SKIP_LINEAR ? x1
                           : (d->inner_skip == MSFNO_SKIP_IDENTITY ? x : nullptr);
@@ -1886,10 +1957,11 @@ int msfno_block_forward(const msfno_block_desc* d, msfno_sht_plan_t f, msfno_sht
   // ---- norm1 (+ FiLM) as a per-(b,c) affine --------------------------------------
   prof(ST_NORM1, s);
   MSFNO_TRY(launch_chan_affine(b.st1, np, cnt, cnt_last, B, (int)C, d->norm1_w, d->norm1_b,
-                               d->norm_eps, gamma, beta, film_scale, b.sc1, b.sh1, s));
+                               d->norm_eps, gamma, beta, film_scale, b.sc1, b.sh1, s, nullptr,
+                               nullptr, b.ab1));
   const float* resid = d->outer_skip == MSFNO_SKIP_IDENTITY ? x : nullptr;
   if (d->has_mlp) {
-    MSFNO_TRY(run_block_mlp(d, x1, x1p, b.sc1, b.sh1, b.W1f, b.b1f, b.h, b.mfimg, out, resid, B,
+    MSFNO_TRY(run_block_mlp(d, x1, x1p, b.sc1, b.sh1, b.ab1, b.W1f, b.b1f, b.h, b.mfimg, out, resid, B,
                             P, b.dw, s));
   } else {
     prof(ST_OUT_AFFINE, s);

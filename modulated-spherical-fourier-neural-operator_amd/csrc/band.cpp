@@ -133,7 +133,7 @@ void exchange_counts(int world, int rank, const std::vector<int>& nm, int W_in, 
 struct BandBufs {
   float2* Xn;   // (BC, max(rows_in, rows_out), mmax) spectra of local rows; reused as Yn
   float2* rs;   // (BC, max rows) row (mean, M2), norm0 then norm1
-  float *sc0, *sh0, *sc1, *sh1;
+  float *sc0, *sh0, *sc1, *sh1, *ab1;
   BlockBufs fb; // filter buffers (Sa, Sb, Sc, Wexp / xt, yt) in the local spectral layout
   float* x1;    // (B, C, rows_out*nlon_out)
   float *W1f, *b1f, *h;
@@ -154,6 +154,7 @@ void carve_band(Carve& cv, BandBufs& b, const msfno_block_desc* d, const msfno_b
   b.sh0 = cv.take<float>(BC);
   b.sc1 = cv.take<float>(BC);
   b.sh1 = cv.take<float>(BC);
+  b.ab1 = cv.take<float>(BC);
   std::memset(&b.fb, 0, sizeof(b.fb));
   b.fb.Sa = cv.take<float>(R * L.ldT);
   if (d->filter_type == MSFNO_FILTER_NONLINEAR) {
@@ -526,13 +527,13 @@ int msfno_band_block_stage(const msfno_block_desc* d, msfno_band_plan_t p, int s
       prof(ST_NORM1, s);
       MSFNO_TRY(launch_chan_affine_parts(io->stats_all, p->world, B, (int)C, d->norm1_w,
                                          d->norm1_b, d->norm_eps, io->gamma, io->beta,
-                                         io->film_scale, b.sc1, b.sh1, s));
+                                         io->film_scale, b.sc1, b.sh1, s, nullptr, b.ab1));
       const float* resid = d->outer_skip == MSFNO_SKIP_IDENTITY ? io->x : nullptr;
       MSFNO_REQUIRE(d->outer_skip != MSFNO_SKIP_IDENTITY || io->x, MSFNO_EINVAL,
                     "stage 4 needs x for the outer skip");
       if (d->has_mlp) {
         MSFNO_TRY(run_block_mlp(d, b.x1, x1_planes(d, p->inv) ? b.fb.x1p : nullptr, b.sc1, b.sh1,
-                                b.W1f, b.b1f, b.h, b.fb.mfimg, io->out, resid, B, Pout, b.fb.dw,
+                                b.ab1, b.W1f, b.b1f, b.h, b.fb.mfimg, io->out, resid, B, Pout, b.fb.dw,
                                 s));
       } else {
         prof(ST_OUT_AFFINE, s);

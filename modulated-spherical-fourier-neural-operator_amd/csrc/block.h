@@ -52,6 +52,7 @@ struct BlockBufs {
   float* xt; float* yt;
   float* Yt; float2* Yn; float* x1;
   float2* st1; float* sc1; float* sh1;
+  float* ab1 = nullptr;  // norm1 output bound per (b, c) (chan_affine abound; fused x3h MLP)
   float* W1f; float* b1f; float* h;
   unsigned short* x1p;  // x1 as bf16x3 planes for fc1 (x6 engine), else null
   unsigned short* Xtp;  // x6 Legendre: forward slabs as bf16x3 planes, else null
@@ -99,7 +100,7 @@ bool x1p_buffer(const msfno_block_desc* d, const msfno_sht_plan_s* g);
 // MLP stage of the block on x1 (fp32, or planes x1p when x1_planes): norm1/FiLM affine
 // (sc1, sh1) applied in the fused kernel, or folded into (W1f, b1f) for run_mlp
 int run_block_mlp(const msfno_block_desc* d, const float* x1, const unsigned short* x1p,
-                  const float* sc1, const float* sh1, float* W1f, float* b1f, float* h,
+                  const float* sc1, const float* sh1, const float* ab1, float* W1f, float* b1f, float* h,
                   unsigned short* mfimg, float* out, const float* resid, int B, int64_t P,
                   const DenseWs& dw, hipStream_t s);
 int64_t mlp_chunk(int64_t P);

@@ -60,7 +60,9 @@ int launch_chan_affine(const float2* partials, int64_t np, int64_t cnt, int64_t 
                        int B, int C, const float* w, const float* b, float eps,
                        const float* gamma, const float* beta, float film_scale, float* scale,
                        float* shift, hipStream_t s, float* xscale = nullptr,
-                       float* lsig = nullptr);
+                       float* lsig = nullptr, float* abound = nullptr);
+// abound (or null): per (b,c) |scale| sqrt(M2) + |scale mean + shift| (x 1.001), a bound of
+// |scale x + shift| over the channel (|x - mean| <= sqrt(M2)): the fused MLP's x3h range
 // latitude-band sharding helpers (band.cpp)
 // rowstats (BC, np) (mean, M2) over cnt each -> out (BC, 3) fp64 {n, mean, M2}; xscale
 // (or null): the local x3h skip B-row scales as in launch_chan_affine
@@ -70,7 +72,7 @@ int launch_stats_partial(const float2* rowstats, int64_t np, int64_t cnt, int64_
 int launch_chan_affine_parts(const double* parts, int nparts, int B, int C, const float* w,
                              const float* b, float eps, const float* gamma, const float* beta,
                              float film_scale, float* scale, float* shift, hipStream_t s,
-                             float* xscale = nullptr);
+                             float* xscale = nullptr, float* abound = nullptr);
 // the all-to-all buffers are the Legendre GEMMs' own operands: [p][slab][R][2W]
 // blocks (common.h msfno_sht_plan_s band fields).  g: the rank's local rows as a
 // small symmetric grid (Ke = its band, nh = the band rows that have a mirror row,
@@ -93,15 +95,12 @@ int launch_affine_rows(const float* x, const float* scale, const float* shift,
 bool mlp_fused_supported(int C, int H);
 size_t mlp_fused_image_bytes();
 // W1 (H x C), W2 (C x H) fp32 -> the kernel's bf16x3 weight image (mlp_fused_image_bytes)
-int launch_mlp_fused_images(const float* W1, const float* W2, unsigned short* img, hipStream_t s);
-int launch_mlp_fused(const float* x1, const float* scale, const float* shift, const float* resid,
-                     float* out, const unsigned short* img, const float* b1, const float* b2,
-                     int B, int64_t P, hipStream_t s);
-// mlp_fused2.hip: the same MLP re-tiled for two workgroups per CU (16x16x32 MFMAs,
-// 16 pixels per wave); its own weight-image layout (same size).  launch_mlp_fused*
-// dispatch to it with MSFNO_MF2=1 (A/B: measured equal to mlp_fused.hip).
-bool mlp_fused2_env();
-int launch_mlp_fused2_images(const float* W1, const float* W2, unsigned short* img, hipStream_t s);
+int launch_mlp_fused_images(const float* W1, const float* b1, const float* W2,
+                            unsigned short* img, hipStream_t s);
+// abound: [B][C] bound of |scale ⊙ x1 + shift| (chan_affine), the x3h range scalars
+int launch_mlp_fused(const float* x1, const float* scale, const float* shift, const float* abound,
+                     const float* resid, float* out, const unsigned short* img, const float* b1,
+                     const float* b2, int B, int64_t P, hipStream_t s);
 // mlp_fused_h.hip: the MLP on the x3h engine (fp32 as two fp16 terms, three fp16
 // MFMAs per product, row-scaled weights); default (MSFNO_ENGINE=x6 selects the x6 engine)
 bool mlp_fused_h_env();
@@ -113,14 +112,16 @@ bool skip_px_env();  // skip_h with per-pixel scales (xs = null) at the block st
 size_t skip_h_workspace(int B);
 int launch_skip_h(const float* W, const float* xs, const float* x, float* out, const float* bias,
                   int B, int64_t P, void* ws, size_t ws_bytes, hipStream_t s);
+// diagnostics: res[0] += #words where a != b, res[1] = min index of such a word
+int launch_debug_cmp(const void* a, const void* b, int64_t nwords, unsigned long long* res,
+                     hipStream_t s);
 size_t mlp_fused_h_image_bytes();
-int launch_mlp_fused_h_images(const float* W1, const float* W2, unsigned short* img, hipStream_t s);
-int launch_mlp_fused_h(const float* x1, const float* scale, const float* shift, const float* resid,
-                       float* out, const unsigned short* img, const float* b1, const float* b2,
-                       int B, int64_t P, hipStream_t s);
-int launch_mlp_fused2(const float* x1, const float* scale, const float* shift, const float* resid,
-                      float* out, const unsigned short* img, const float* b1, const float* b2,
-                      int B, int64_t P, hipStream_t s);
+int launch_mlp_fused_h_images(const float* W1, const float* b1, const float* W2,
+                              unsigned short* img, hipStream_t s);
+int launch_mlp_fused_h(const float* x1, const float* scale, const float* shift,
+                       const float* abound, const float* resid, float* out,
+                       const unsigned short* img, const float* b1, const float* b2, int B,
+                       int64_t P, hipStream_t s);
 // ---- cgemm.hip -----------------------------------------------------------------
 // complex (Ci,Co,2) weight -> Ar, Ai (Co x Ci) row-major (Ar[o][i] = Re w[i][o])
 int launch_split_complex_weight(const float* w, float* Ar, float* Ai, int Ci, int Co,

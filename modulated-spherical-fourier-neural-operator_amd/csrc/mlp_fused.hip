@@ -735,11 +735,11 @@ size_t mlp_fused_image_bytes() {
   return std::max((size_t)2 * MF_HB * 2 * MF_SLICE_ELEMS * 2, mlp_fused_h_image_bytes());
 }
 
-int launch_mlp_fused_images(const float* W1, const float* W2, unsigned short* img, hipStream_t s) {
+int launch_mlp_fused_images(const float* W1, const float* b1, const float* W2,
+                            unsigned short* img, hipStream_t s) {
   MSFNO_REQUIRE(W1 && W2 && img && (reinterpret_cast<uintptr_t>(img) & 15) == 0, MSFNO_EINVAL,
                 "mlp_fused: bad weight image arguments");
-  if (mlp_fused_h_env()) return launch_mlp_fused_h_images(W1, W2, img, s);
-  if (mlp_fused2_env()) return launch_mlp_fused2_images(W1, W2, img, s);
+  if (mlp_fused_h_env()) return launch_mlp_fused_h_images(W1, b1, W2, img, s);
   unsigned short* w2img = img + (int64_t)MF_HB * 2 * MF_SLICE_ELEMS;
   hipLaunchKernelGGL(mf_w1_image_kernel, dim3(256), dim3(256), 0, s, W1, img);
   MSFNO_TRY(launch_check("mf_w1_image"));
@@ -747,17 +747,15 @@ int launch_mlp_fused_images(const float* W1, const float* W2, unsigned short* im
   return launch_check("mf_w2_image");
 }
 
-int launch_mlp_fused(const float* x1, const float* scale, const float* shift, const float* resid,
-                     float* out, const unsigned short* img, const float* b1, const float* b2,
-                     int B, int64_t P, hipStream_t s) {
+int launch_mlp_fused(const float* x1, const float* scale, const float* shift, const float* abound,
+                     const float* resid, float* out, const unsigned short* img, const float* b1,
+                     const float* b2, int B, int64_t P, hipStream_t s) {
   MSFNO_REQUIRE(x1 && scale && shift && out && img && b1 && B > 0 && P >= 4 && P % 4 == 0,
                 MSFNO_EINVAL, "mlp_fused: bad arguments");
   MSFNO_REQUIRE(((reinterpret_cast<uintptr_t>(x1) | reinterpret_cast<uintptr_t>(resid)) & 15) == 0,
                 MSFNO_EINVAL, "mlp_fused: x1 / resid must be 16-B aligned");
   if (mlp_fused_h_env())
-    return launch_mlp_fused_h(x1, scale, shift, resid, out, img, b1, b2, B, P, s);
-  if (mlp_fused2_env())
-    return launch_mlp_fused2(x1, scale, shift, resid, out, img, b1, b2, B, P, s);
+    return launch_mlp_fused_h(x1, scale, shift, abound, resid, out, img, b1, b2, B, P, s);
   MlpFusedParams p{};
   p.x1 = x1; p.scale = scale; p.shift = shift; p.resid = resid; p.out = out;
   p.w1img = img;

@@ -1,6 +1,6 @@
 // Fused block MLP on the "x3h" engine (gfx950): out = W2·GELU(W1·(a ⊙ x1 + t) + b1)
 // + b2 + resid, C = 256, H = 512, hidden activation on-chip — the tiling of
-// mlp_fused2.hip (16x16x32 MFMAs, 16 pixels per wave, 64 per workgroup, two
+// the round-2 MLP re-tiled (16x16x32 MFMAs, 16 pixels per wave, 64 per workgroup, two
 // workgroups per CU, x1 straight from global memory into registers) with fp32
 // emulated by TWO fp16 terms instead of three bf16 ones:
 //
@@ -18,19 +18,26 @@
 // DESIGN.md §8), two planes instead of three (a third less weight stream and
 // register image).
 //
-// Range: fp16 holds |v| < 65504.  Every weight row is scaled by a power of two so
-// that its largest entry lies in [2^14, 2^15) (exact; undone in fp32 after the
-// contraction: the fc1 rows before bias + GELU, the fc2 rows in the epilogue), so
-// no weight term is subnormal unless it is < 2^-24 of its row's maximum.  The
-// activations (the InstanceNorm output a ⊙ x1 + t, |.| <= sqrt(P) |a| + |t|, and
-// the GELU outputs) are used unscaled; a low term below 2^-14 is subnormal and then
-// carries 2^-24 absolute precision.
+// Range: fp16 holds |v| < 65504.  Every operand is scaled by exact powers of two chosen
+// from a bound, so nothing overflows whatever the weights or the data:
+//   - weights: every W1 row and every row of W2' = W2 · diag(1 / eta) (below) so that
+//     its largest entry lies in [2^14, 2^15), undone in fp32 after the contraction;
+//   - fc1 input x^ = a ⊙ x1 + t: per field by xi_b = 2^(14 - e), where
+//     B_b = max_c abound[b][c] = f 2^e and abound = |a| sqrt(M2) + |a mu + t| >= |x^|
+//     (chan_affine, from the norm1 statistics: |x1 - mu| <= sqrt(M2));
+//   - hidden h_j = GELU(z_j), |h_j| <= |z_j| <= ||W1_j||_1 B_b + |b1_j|
+//     <= L_j (B_b + 1), L_j = max(||W1_j||_1, |b1_j|): h is multiplied by
+//     eta_j = 2^-ceil(log2 L_j) (from the weights, folded into W2's columns) and by
+//     eta_b = 2^(14 - e'), B_b + 1 = f' 2^e' (per field), so |h'| < 2^14; the output
+//     is unscaled by 1 / eta_b with W2's row scales.
+// A term far below its bound keeps the bound's absolute precision (2^-38 of it), far
+// under the fp32 rounding of the sums it enters.
 //
-// Slices (24-KB slices of mlp_fused2.hip become 16 KB):
+// Slices (the 24-KB bf16x3 slices of mlp_fused.hip become 16 KB):
 //   W1(j,kh): hidden rows 32j..+31, channels 128kh..+127: [pl 2][ks 4][t 2][r 16][32]
 //   W2(j,oh): out rows 128oh..+127, hidden block j:       [pl 2][ot 8][r 16][32 (perm)]
 // ring of four 16-KB slots; image = 64 slices, then the row scales (inverse) of W1
-// (512) and W2 (256) as fp32.
+// (512) and W2' (256), then eta (512), as fp32.
 #include "dma.h"
 #include "gemm_common.h"
 #include "kernels.h"
@@ -66,12 +73,21 @@ struct MlpHParams {
   const unsigned short* w2img;  // [HB][2 oh] slices
   const float* inv_s1;  // [H] 1 / (W1 row scale)
   const float* inv_s2;  // [C] 1 / (W2 row scale)
+  const float* eta;     // [H] hidden-row scales eta_j (folded into W2's columns)
+  const float* abound;  // [B][C] bound of |a ⊙ x1 + t| per channel
   const float* b1;      // [H]
   const float* b2;      // [C] or null
   int64_t P;
   int tiles_per_field;
-  int stagger;  // s_sleep 127 rounds for the first tile of the second slot per CU
 };
+
+// 2^(t - e) for v = f 2^e (f in [0.5, 1)): maps v below 2^t; 1 for v = 0 / non-finite
+__device__ __forceinline__ float pow2_below(float v, int t) {
+  if (!(v > 0.f) || !isfinite(v)) return 1.f;
+  int e;
+  frexpf(v, &e);
+  return ldexpf(1.f, min(max(t - e, -120), 120));
+}
 
 __host__ __device__ __forceinline__ int mh_swz(int r) { return ((r >> 2) & 1) << 1; }
 
@@ -94,16 +110,36 @@ __device__ __forceinline__ half8 mh_frag(uint32_t a, uint32_t b, uint32_t c, uin
   return __builtin_bit_cast(half8, make_uint4(a, b, c, d));
 }
 
-// row scales: 2^(15 - e) with max |row| = f 2^e, f in [0.5, 1) -> max scaled in [2^14, 2^15)
+// eta_j = 2^-ceil(log2 L_j), L_j = max(||W1_j||_1, |b1_j|): L_j eta_j <= 1
+__global__ void mh_eta_kernel(const float* __restrict__ W1, const float* __restrict__ b1,
+                              float* __restrict__ eta) {
+  const int r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= MH_H) return;
+  const float* row = W1 + (int64_t)r * MH_C;
+  double l1 = 0.0;
+  for (int k = 0; k < MH_C; ++k) l1 += fabs((double)row[k]);
+  const double L = fmax(l1, b1 ? fabs((double)b1[r]) : 0.0) * (1.0 + 1e-6);
+  float e = 1.f;
+  if (L > 0.0 && L < 1e30) {
+    int x;
+    frexp(L, &x);  // L = f 2^x, f in [0.5, 1): L 2^-x < 1
+    e = (float)ldexp(1.0, min(max(-x, -120), 120));
+  }
+  eta[r] = e;
+}
+
+// row scales: 2^(15 - e) with max |row| = f 2^e, f in [0.5, 1) -> max scaled in [2^14, 2^15);
+// the W2 rows taken as W2' = W2 diag(1 / eta)
 __global__ void mh_scale_kernel(const float* __restrict__ W1, const float* __restrict__ W2,
-                                float* __restrict__ s1, float* __restrict__ s2) {
+                                const float* __restrict__ eta, float* __restrict__ s1,
+                                float* __restrict__ s2) {
   const int r = blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= MH_H + MH_C) return;
   const bool first = r < MH_H;
   const float* row = first ? W1 + (int64_t)r * MH_C : W2 + (int64_t)(r - MH_H) * MH_H;
   const int n = first ? MH_C : MH_H;
   float m = 0.f;
-  for (int k = 0; k < n; ++k) m = fmaxf(m, fabsf(row[k]));
+  for (int k = 0; k < n; ++k) m = fmaxf(m, fabsf(first ? row[k] : row[k] / eta[k]));
   float sc = 1.f;
   if (m > 0.f && isfinite(m)) {
     int e;
@@ -140,9 +176,10 @@ __global__ void mh_w1_image_kernel(const float* __restrict__ W1, const float* __
   }
 }
 
-// W2 (C x H fp32) · row scales -> [j][oh][pl][ot][r][32], hidden index permuted by mh_perm
-__global__ void mh_w2_image_kernel(const float* __restrict__ W2, const float* __restrict__ s2,
-                                   unsigned short* __restrict__ img) {
+// W2' (C x H fp32, W2 diag(1 / eta)) · row scales -> [j][oh][pl][ot][r][32], hidden index
+// permuted by mh_perm
+__global__ void mh_w2_image_kernel(const float* __restrict__ W2, const float* __restrict__ eta,
+                                   const float* __restrict__ s2, unsigned short* __restrict__ img) {
   constexpr int64_t PAIRS = (int64_t)MH_HB * 2 * 8 * 16 * 16;
   for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < PAIRS;
        e += (int64_t)gridDim.x * blockDim.x) {
@@ -155,9 +192,11 @@ __global__ void mh_w2_image_kernel(const float* __restrict__ W2, const float* __
     const int kap = 8 * ((kk >> 3) ^ mh_swz(r)) + (kk & 7);
     const int orow = 128 * oh + 16 * ot + r;
     const float* row = W2 + (int64_t)orow * MH_H + 32 * j;
+    const float* er = eta + 32 * j;
     const float sc = s2[orow];
+    const int k0 = mh_perm(kap), k1 = mh_perm(kap + 1);
     uint32_t t0, t1;
-    split2h(row[mh_perm(kap)] * sc, row[mh_perm(kap + 1)] * sc, t0, t1);
+    split2h(row[k0] / er[k0] * sc, row[k1] / er[k1] * sc, t0, t1);
     uint32_t* o = reinterpret_cast<uint32_t*>(
         img + (int64_t)(j * 2 + oh) * MH_SLICE + (ot * 16 + r) * 32 + kk);
     o[0] = t0;
@@ -201,56 +240,35 @@ __device__ __forceinline__ void glds16x4(uint64_t sbase, const uint32_t (&voff)[
       : "memory", "scc");
 }
 
-// NG: 16-pixel groups per wave (1: two workgroups of 64 pixels per CU; 2: one
-// workgroup of 128 pixels per CU, a wave's A fragment feeding both groups — half the
-// LDS fragment reads and half the weight stream per pixel, 1 wave per SIMD with the
-// output accumulators in AGPRs).  NS: ring slots (NS - 2 slices in flight while one
-// is consumed).  DBG (diagnostic timing builds only, wrong results; MSFNO_MH_DBG):
-// 1 no weight slices streamed after the first NS (stale ring), 2 no MFMAs, 4 no LDS
-// fragment reads (A from registers)
-// W waves per workgroup: 4 (two workgroups per CU) or 8 (one workgroup of 128 pixels
-// per CU sharing one weight stream: half the L2 -> LDS slice traffic per pixel)
-// two pieces (as glds16x4)
-template <int LDS_STEP>
-__device__ __forceinline__ void glds16x2(uint64_t sbase, const uint32_t (&voff)[4], uint32_t lds) {
-  unsigned keep;
-  sbase = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(sbase >> 32)) << 32) |
-          (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)sbase);
-  lds = (uint32_t)__builtin_amdgcn_readfirstlane((int)lds);
-  asm volatile(
-      "s_mov_b32 %0, m0\n\t"
-      "s_mov_b32 m0, %4\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %2, %1\n\t"
-      "s_add_u32 m0, m0, %5\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %3, %1\n\t"
-      "s_mov_b32 m0, %0"
-      : "=&s"(keep)
-      : "s"(sbase), "v"(voff[0]), "v"(voff[1]), "s"(lds), "i"(LDS_STEP)
-      : "memory", "scc");
-}
-
-template <int AHEAD, int DBG = 0, int NG = 1, int NS = MH_NS, int W = MH_WAVES>
-__global__ __launch_bounds__(64 * W, (NG == 1 && W == 4) ? 2 : 1) void mlp_fused_h_kernel(MlpHParams p) {
-  static_assert(W == 4 || W == 8, "4 or 8 waves");
-  constexpr int PPW = 16 / W;  // 1-KB DMA pieces per wave and slice
+// The block MLP for one tile of 64 pixels (4 waves of 16; two workgroups per CU).
+// Prologue: the weight slices 0..3 go in flight by LDS-DMA; the field's range scalars
+// (xi_b from max_c abound, eta_b from B_b + 1) are reduced over the workgroup; x1 of the
+// wave's 16 pixels is normalised (a ⊙ x1 + t, times xi_b) and split into fp16x2 B
+// fragments kept in registers.  Then 64 slice steps: W1(j, 0..1) into the fc1
+// accumulator of block j while block j - 1 is unscaled, + b1, GELU'd, scaled by
+// eta_j eta_b and split into fc2's B fragment (in place: mf_perm orders W2's columns),
+// W2(j - 1, 0..1) into the 256 x 16 output accumulators.  Epilogue: unscale + b2 +
+// residual, one store per output.
+template <int AHEAD>
+__global__ __launch_bounds__(256, 2) void mlp_fused_h_kernel(MlpHParams p) {
+  constexpr int W = MH_WAVES, NS = MH_NS;
   constexpr int RING_BYTES = NS * MH_SLICE * 2;
-  constexpr int TPX = 16 * NG * W;  // pixels per workgroup tile
-  __shared__ __attribute__((aligned(16))) char lds_raw[RING_BYTES + 2 * (MH_H + MH_C) * 4];
+  constexpr int TPX = 16 * W;  // pixels per workgroup tile
+  __shared__ __attribute__((aligned(16))) char lds_raw[RING_BYTES + (3 * MH_H + 2 * MH_C + 8) * 4];
   unsigned short* const ring = reinterpret_cast<unsigned short*>(lds_raw);
   float* const b1s = reinterpret_cast<float*>(lds_raw + RING_BYTES);
   float* const is1s = b1s + MH_H;
-  float* const b2s = is1s + MH_H;  // the epilogue's vectors (no global loads there)
+  float* const hss = is1s + MH_H;  // eta_j eta_b
+  float* const b2s = hss + MH_H;   // the epilogue's vectors (no global loads there)
   float* const is2s = b2s + MH_C;
+  float* const red = is2s + MH_C;  // per-wave maxima of abound
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r16 = lane & 15, g = lane >> 4;
-  // phase shift: the workgroups that take the second slot of every CU first start
-  // about half a tile late, so the two co-resident tiles' memory phases (x1 in,
-  // output out) fall under each other's MFMA phases instead of all CUs loading at once
-  if (p.stagger && blockIdx.x >= 256 && blockIdx.x < 512)
-    for (int i = 0; i < p.stagger; ++i) __builtin_amdgcn_s_sleep(127);
   const int lin = xcd_remap(blockIdx.x, gridDim.x);
   const int z = lin / p.tiles_per_field;
   const int64_t P = p.P;
-  const int64_t px0 = (int64_t)(lin - z * p.tiles_per_field) * TPX + 16 * NG * wave + r16;
+  const int64_t px = (int64_t)(lin - z * p.tiles_per_field) * TPX + 16 * wave + r16;
 
   // ---- slices 0..NS-1 in flight --------------------------------------------------------
   const uint32_t ring_lds = lds_addr(ring);
@@ -260,131 +278,112 @@ __global__ __launch_bounds__(64 * W, (NG == 1 && W == 4) ? 2 : 1) void mlp_fused
   for (int i = 0; i < 4; ++i) piece_off[i] = (uint32_t)(i * W * 1024 + lane * 16);
   auto issue = [&](int q) {
     const uint64_t src = reinterpret_cast<uint64_t>(mh_slice_src(p, q)) + (uint64_t)wave_u * 1024;
-    const uint32_t base = ring_lds + (uint32_t)((q % NS) * MH_SLICE * 2 + wave_u * 1024);
-    if constexpr (PPW == 4)
-      glds16x4<W * 1024>(src, piece_off, base);
-    else
-      glds16x2<W * 1024>(src, piece_off, base);
+    glds16x4<W * 1024>(src, piece_off, ring_lds + (uint32_t)((q % NS) * MH_SLICE * 2 + wave_u * 1024));
   };
 #pragma unroll
   for (int q = 0; q < NS; ++q) issue(q);
 
-  // ---- x1 -> normalised fp16x2 B fragments (k-step ks: channels 32 ks + 8 g + 0..7) --
+  // ---- x1 loads, the field's bound B_b = max_c abound (thread tid: channel tid) ------
+  const float* xcol = p.x1 + (int64_t)z * MH_C * P + (px < P ? px : P - 1);
+  float xv[8][8];
+#pragma unroll
+  for (int ks = 0; ks < 8; ++ks)
+#pragma unroll
+    for (int e = 0; e < 8; ++e)
+      xv[ks][e] = __builtin_nontemporal_load(xcol + (int64_t)(32 * ks + 8 * g + e) * P);
+  float bm = p.abound[(int64_t)z * MH_C + tid];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) bm = fmaxf(bm, __shfl_xor(bm, o));
+  if (lane == 0) red[wave] = bm;
+  __syncthreads();  // (also: the first NS slices and the x1 loads landed)
+  const float Bb = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+  const float xi = pow2_below(Bb, 14);          // |x^ xi| < 2^14
+  const float etab = pow2_below(Bb + 1.f, 14);  // |h eta_j eta_b| < 2^14
+
+  // ---- normalised x1 -> fp16x2 B fragments (k-step ks: channels 32 ks + 8 g + 0..7) ----
   const float* sc = p.scale + (int64_t)z * MH_C;
   const float* sh = p.shift + (int64_t)z * MH_C;
-  half8 xf[NG][8][2];
+  half8 xf[8][2];
 #pragma unroll
-  for (int gr = 0; gr < NG; ++gr) {
-    const int64_t px = px0 + 16 * gr;
-    const float* xcol = p.x1 + (int64_t)z * MH_C * P + (px < P ? px : P - 1);
+  for (int ks = 0; ks < 8; ++ks) {
+    const int c0 = 32 * ks + 8 * g;
+    const float4 sa = *reinterpret_cast<const float4*>(sc + c0);
+    const float4 sb = *reinterpret_cast<const float4*>(sc + c0 + 4);
+    const float4 ta = *reinterpret_cast<const float4*>(sh + c0);
+    const float4 tb = *reinterpret_cast<const float4*>(sh + c0 + 4);
+    const float sv[8] = {sa.x * xi, sa.y * xi, sa.z * xi, sa.w * xi,
+                         sb.x * xi, sb.y * xi, sb.z * xi, sb.w * xi};
+    const float tv[8] = {ta.x * xi, ta.y * xi, ta.z * xi, ta.w * xi,
+                         tb.x * xi, tb.y * xi, tb.z * xi, tb.w * xi};
+    uint32_t t[2][4];
 #pragma unroll
-    for (int ks = 0; ks < 8; ++ks) {
-      const int c0 = 32 * ks + 8 * g;
-      float xv[8];
+    for (int e = 0; e < 4; ++e)
+      split2h(fmaf(sv[2 * e], xv[ks][2 * e], tv[2 * e]),
+              fmaf(sv[2 * e + 1], xv[ks][2 * e + 1], tv[2 * e + 1]), t[0][e], t[1][e]);
 #pragma unroll
-      for (int e = 0; e < 8; ++e) xv[e] = __builtin_nontemporal_load(xcol + (int64_t)(c0 + e) * P);
-      const float4 sa = *reinterpret_cast<const float4*>(sc + c0);
-      const float4 sb = *reinterpret_cast<const float4*>(sc + c0 + 4);
-      const float4 ta = *reinterpret_cast<const float4*>(sh + c0);
-      const float4 tb = *reinterpret_cast<const float4*>(sh + c0 + 4);
-      const float sv[8] = {sa.x, sa.y, sa.z, sa.w, sb.x, sb.y, sb.z, sb.w};
-      const float tv[8] = {ta.x, ta.y, ta.z, ta.w, tb.x, tb.y, tb.z, tb.w};
-      uint32_t t[2][4];
-#pragma unroll
-      for (int e = 0; e < 4; ++e)
-        split2h(fmaf(sv[2 * e], xv[2 * e], tv[2 * e]), fmaf(sv[2 * e + 1], xv[2 * e + 1], tv[2 * e + 1]),
-                t[0][e], t[1][e]);
-#pragma unroll
-      for (int pl = 0; pl < 2; ++pl) xf[gr][ks][pl] = mh_frag(t[pl][0], t[pl][1], t[pl][2], t[pl][3]);
-    }
+    for (int pl = 0; pl < 2; ++pl) xf[ks][pl] = mh_frag(t[pl][0], t[pl][1], t[pl][2], t[pl][3]);
   }
-  floatx4 oacc[NG][16];
+  floatx4 oacc[16];
 #pragma unroll
-  for (int gr = 0; gr < NG; ++gr)
-#pragma unroll
-    for (int ot = 0; ot < 16; ++ot) oacc[gr][ot] = floatx4{0.f, 0.f, 0.f, 0.f};
+  for (int ot = 0; ot < 16; ++ot) oacc[ot] = floatx4{0.f, 0.f, 0.f, 0.f};
+  const float ixi = 1.f / xi, ietab = 1.f / etab;
   for (int i = tid; i < MH_H; i += 64 * W) {
     b1s[i] = p.b1[i];
-    is1s[i] = p.inv_s1[i];
+    is1s[i] = p.inv_s1[i] * ixi;
+    hss[i] = p.eta[i] * etab;
   }
   for (int i = tid; i < MH_C; i += 64 * W) {
     b2s[i] = p.b2 ? p.b2[i] : 0.f;
-    is2s[i] = p.inv_s2[i];
+    is2s[i] = p.inv_s2[i] * ietab;
   }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the first NS slices and every load landed
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
-  floatx4 hacc[2][2][NG];  // [parity][tile][group]
+  floatx4 hacc[2][2];  // [parity][tile]
 #pragma unroll
   for (int a = 0; a < 2; ++a)
 #pragma unroll
-    for (int t = 0; t < 2; ++t)
-#pragma unroll
-      for (int gr = 0; gr < NG; ++gr) hacc[a][t][gr] = floatx4{0.f, 0.f, 0.f, 0.f};
-  uint32_t hfu[NG][2][4];  // fc2 B fragment of the converted block [group][plane][pair]
+    for (int t = 0; t < 2; ++t) hacc[a][t] = floatx4{0.f, 0.f, 0.f, 0.f};
+  uint32_t hfu[2][4];  // fc2 B fragment of the converted block [plane][pair]
 
   const int a_lane = r16 * 32 + 8 * (g ^ mh_swz(r16));
-  // A fragment read (DBG & 4: from registers instead of LDS, diagnostic)
-  auto afrag = [&](const unsigned short* q, int u, int pl) -> half8 {
-    if constexpr ((DBG & 4) != 0) return xf[0][u & 7][pl];
+  auto afrag = [&](const unsigned short* q) -> half8 {
     return *reinterpret_cast<const half8*>(q);
   };
 
   // step q: slice q landed for every wave (slices up to q + NS - 2 may stay in flight);
   // the slot of slice q - 1 is free and takes slice q + NS - 1
   auto step_begin = [&](int q) {
-    const int after = (DBG & 1) ? 0 : min(NS - 2, MH_NSLICE - 1 - q);
-    if constexpr (PPW != 4) {
-      wait_vmcnt(after * PPW);
-    } else if constexpr (NS >= 8) {
-      if (after >= 6) asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
-      else if (after == 5) asm volatile("s_waitcnt vmcnt(20)" ::: "memory");
-      else if (after == 4) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-      else if (after == 3) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
-      else if (after == 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-      else if (after == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    } else {
-      if (after >= 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-      else if (after == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
+    const int after = min(NS - 2, MH_NSLICE - 1 - q);
+    if (after >= 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else if (after == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     return ring + (q % NS) * MH_SLICE;
   };
   auto refill = [&](int q) {
-    if ((DBG & 1) == 0 && q >= 1 && q + NS - 1 < MH_NSLICE) issue(q + NS - 1);
+    if (q >= 1 && q + NS - 1 < MH_NSLICE) issue(q + NS - 1);
   };
 
-  // c[gr] += a (x) b[gr], three fp16 MFMAs each, the groups interleaved
-  auto mfma3 = [](const half8 (&a)[2], const half8 (&b)[NG][2], floatx4 (&c)[NG]) {
-    if constexpr ((DBG & 2) != 0) {  // keep the fragment reads alive
-#pragma unroll
-      for (int gr = 0; gr < NG; ++gr) c[gr][0] += (float)a[0][0] + (float)a[1][0] + (float)b[gr][0][0];
-      return;
-    }
-#pragma unroll
-    for (int gr = 0; gr < NG; ++gr) c[gr] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[1], b[gr][0], c[gr], 0, 0, 0);
-#pragma unroll
-    for (int gr = 0; gr < NG; ++gr) c[gr] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[0], b[gr][1], c[gr], 0, 0, 0);
-#pragma unroll
-    for (int gr = 0; gr < NG; ++gr) c[gr] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[0], b[gr][0], c[gr], 0, 0, 0);
+  // c += a (x) b, three fp16 MFMAs
+  auto mfma3 = [](const half8 (&a)[2], const half8 (&b)[2], floatx4& c) {
+    c = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[1], b[0], c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[0], b[1], c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[0], b[0], c, 0, 0, 0);
   };
 
-  // pair e2 (0..3) of hidden block j in hacc[PAR]: unscale, + b1, GELU(erf), split -> hfu
+  // pair e2 (0..3) of hidden block j in hacc[PAR]: unscale, + b1, GELU(erf), scale, split
   auto conv_pair = [&](int j, int e2, auto par_c) {
     constexpr int PAR = decltype(par_c)::value;
     const int t = e2 >> 1, i = 2 * (e2 & 1);
     const int row = 32 * j + 16 * t + 4 * g + i;
     const float2 b = *reinterpret_cast<const float2*>(b1s + row);
     const float2 is = *reinterpret_cast<const float2*>(is1s + row);
-#pragma unroll
-    for (int gr = 0; gr < NG; ++gr) {
-      f32x2 v = {fmaf(hacc[PAR][t][gr][i], is.x, b.x), fmaf(hacc[PAR][t][gr][i + 1], is.y, b.y)};
-      v = gelu_erf2(v);
-      split2h(v.x, v.y, hfu[gr][0][e2], hfu[gr][1][e2]);
-    }
+    const float2 hs = *reinterpret_cast<const float2*>(hss + row);
+    f32x2 v = {fmaf(hacc[PAR][t][i], is.x, b.x), fmaf(hacc[PAR][t][i + 1], is.y, b.y)};
+    v = gelu_erf2(v) * f32x2{hs.x, hs.y};
+    split2h(v.x, v.y, hfu[0][e2], hfu[1][e2]);
   };
 
   auto fc1_step = [&](const unsigned short* slot, int q, auto kh_c, auto par_c, auto conv_c,
@@ -397,22 +396,15 @@ __global__ __launch_bounds__(64 * W, (NG == 1 && W == 4) ? 2 : 1) void mlp_fused
 #pragma unroll
     for (int k = 0; k < AHEAD; ++k)
 #pragma unroll
-      for (int pl = 0; pl < 2; ++pl) a[k][pl] = afrag(slot + aoff(k, pl), k, pl);
-    if constexpr (AHEAD >= 8) __builtin_amdgcn_sched_barrier(0);  // every read issued first
+      for (int pl = 0; pl < 2; ++pl) a[k][pl] = afrag(slot + aoff(k, pl));
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
       if (u + AHEAD < 8) {
 #pragma unroll
         for (int pl = 0; pl < 2; ++pl)
-          a[(u + AHEAD) % (AHEAD + 1)][pl] = afrag(slot + aoff(u + AHEAD, pl), u + AHEAD, pl);
+          a[(u + AHEAD) % (AHEAD + 1)][pl] = afrag(slot + aoff(u + AHEAD, pl));
       }
-      half8 xb[NG][2];
-#pragma unroll
-      for (int gr = 0; gr < NG; ++gr) {
-        xb[gr][0] = xf[gr][KH * 4 + (u >> 1)][0];
-        xb[gr][1] = xf[gr][KH * 4 + (u >> 1)][1];
-      }
-      mfma3(a[u % (AHEAD + 1)], xb, hacc[PAR][u & 1]);
+      mfma3(a[u % (AHEAD + 1)], xf[KH * 4 + (u >> 1)], hacc[PAR][u & 1]);
       if (u == 0) refill(q);
       if constexpr (CONV) {
         if (u == 2 || u == 6) conv_pair(jc, 2 * KH + (u >> 2), PPrev{});
@@ -420,39 +412,27 @@ __global__ __launch_bounds__(64 * W, (NG == 1 && W == 4) ? 2 : 1) void mlp_fused
     }
     if constexpr (CONV && KH == 1) {
 #pragma unroll
-      for (int t = 0; t < 2; ++t)
-#pragma unroll
-        for (int gr = 0; gr < NG; ++gr) hacc[PAR ^ 1][t][gr] = floatx4{0.f, 0.f, 0.f, 0.f};
+      for (int t = 0; t < 2; ++t) hacc[PAR ^ 1][t] = floatx4{0.f, 0.f, 0.f, 0.f};
     }
   };
   auto fc2_step = [&](const unsigned short* slot, int q, auto oh_c) {
     constexpr int OH = decltype(oh_c)::value;
     auto aoff = [&](int u, int pl) { return (pl * 8 + u) * 512 + a_lane; };
-    half8 hb[NG][2];
-#pragma unroll
-    for (int gr = 0; gr < NG; ++gr) {
-      hb[gr][0] = mh_frag(hfu[gr][0][0], hfu[gr][0][1], hfu[gr][0][2], hfu[gr][0][3]);
-      hb[gr][1] = mh_frag(hfu[gr][1][0], hfu[gr][1][1], hfu[gr][1][2], hfu[gr][1][3]);
-    }
+    const half8 hb[2] = {mh_frag(hfu[0][0], hfu[0][1], hfu[0][2], hfu[0][3]),
+                         mh_frag(hfu[1][0], hfu[1][1], hfu[1][2], hfu[1][3])};
     half8 a[AHEAD + 1][2];
 #pragma unroll
     for (int k = 0; k < AHEAD; ++k)
 #pragma unroll
-      for (int pl = 0; pl < 2; ++pl) a[k][pl] = afrag(slot + aoff(k, pl), k, pl);
-    if constexpr (AHEAD >= 8) __builtin_amdgcn_sched_barrier(0);  // every read issued first
+      for (int pl = 0; pl < 2; ++pl) a[k][pl] = afrag(slot + aoff(k, pl));
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
       if (u + AHEAD < 8) {
 #pragma unroll
         for (int pl = 0; pl < 2; ++pl)
-          a[(u + AHEAD) % (AHEAD + 1)][pl] = afrag(slot + aoff(u + AHEAD, pl), u + AHEAD, pl);
+          a[(u + AHEAD) % (AHEAD + 1)][pl] = afrag(slot + aoff(u + AHEAD, pl));
       }
-      floatx4 c[NG];
-#pragma unroll
-      for (int gr = 0; gr < NG; ++gr) c[gr] = oacc[gr][OH * 8 + u];
-      mfma3(a[u % (AHEAD + 1)], hb, c);
-#pragma unroll
-      for (int gr = 0; gr < NG; ++gr) oacc[gr][OH * 8 + u] = c[gr];
+      mfma3(a[u % (AHEAD + 1)], hb, oacc[OH * 8 + u]);
       if (u == 0) refill(q);
     }
   };
@@ -478,45 +458,34 @@ __global__ __launch_bounds__(64 * W, (NG == 1 && W == 4) ? 2 : 1) void mlp_fused
   for (int e2 = 0; e2 < 4; ++e2) conv_pair(MH_HB - 1, e2, I1{});
   // the residual of every output row, all loads in flight at once and under the last
   // two steps' MFMAs (the x1 fragments are dead: their registers take it)
-  float rv[NG][16][4];
+  float rv[16][4];
   if (p.resid) {
+    const float* rs = p.resid + (int64_t)z * MH_C * P + (px < P ? px : P - 1);
 #pragma unroll
-    for (int gr = 0; gr < NG; ++gr) {
-      const int64_t px = px0 + 16 * gr;
-      const float* rs = p.resid + (int64_t)z * MH_C * P + (px < P ? px : P - 1);
+    for (int ot = 0; ot < 16; ++ot)
 #pragma unroll
-      for (int ot = 0; ot < 16; ++ot)
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-          rv[gr][ot][i] = __builtin_nontemporal_load(rs + (int64_t)(16 * ot + 4 * g + i) * P);
-    }
+      for (int i = 0; i < 4; ++i)
+        rv[ot][i] = __builtin_nontemporal_load(rs + (int64_t)(16 * ot + 4 * g + i) * P);
   } else {
 #pragma unroll
-    for (int gr = 0; gr < NG; ++gr)
+    for (int ot = 0; ot < 16; ++ot)
 #pragma unroll
-      for (int ot = 0; ot < 16; ++ot)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) rv[gr][ot][i] = 0.f;
+      for (int i = 0; i < 4; ++i) rv[ot][i] = 0.f;
   }
   fc2_step(step_begin(MH_NSLICE - 2), MH_NSLICE - 2, I0{});
   fc2_step(step_begin(MH_NSLICE - 1), MH_NSLICE - 1, I1{});
 
   // ---- epilogue: unscale + b2 + residual, store (rows 16 ot + 4 g + i) ----------------
+  if (px >= P) return;
+  float* o = p.out + (int64_t)z * MH_C * P + px;
 #pragma unroll
-  for (int gr = 0; gr < NG; ++gr) {
-    const int64_t px = px0 + 16 * gr;
-    if (px >= P) continue;
-    float* o = p.out + (int64_t)z * MH_C * P + px;
+  for (int ot = 0; ot < 16; ++ot) {
+    const int r0 = 16 * ot + 4 * g;
+    const float4 is = *reinterpret_cast<const float4*>(is2s + r0);
+    const float4 b = *reinterpret_cast<const float4*>(b2s + r0);
+    const float isv[4] = {is.x, is.y, is.z, is.w}, bv[4] = {b.x, b.y, b.z, b.w};
 #pragma unroll
-    for (int ot = 0; ot < 16; ++ot) {
-      const int r0 = 16 * ot + 4 * g;
-      const float4 is = *reinterpret_cast<const float4*>(is2s + r0);
-      const float4 b = *reinterpret_cast<const float4*>(b2s + r0);
-      const float isv[4] = {is.x, is.y, is.z, is.w}, bv[4] = {b.x, b.y, b.z, b.w};
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-        o[(int64_t)(r0 + i) * P] = fmaf(oacc[gr][ot][i], isv[i], bv[i]) + rv[gr][ot][i];
-    }
+    for (int i = 0; i < 4; ++i) o[(int64_t)(r0 + i) * P] = fmaf(oacc[ot][i], isv[i], bv[i]) + rv[ot][i];
   }
 }
 
@@ -749,7 +718,25 @@ __global__ __launch_bounds__(256, 2) void skip_h_kernel(SkipHParams p) {
   }
 }
 
+__global__ void debug_cmp_kernel(const uint32_t* __restrict__ a, const uint32_t* __restrict__ b,
+                                 int64_t n, unsigned long long* res) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    if (a[i] != b[i]) {
+      atomicAdd(res, 1ull);
+      atomicMin(res + 1, (unsigned long long)i);
+    }
+  }
+}
+
 }  // namespace
+
+int launch_debug_cmp(const void* a, const void* b, int64_t nwords, unsigned long long* res,
+                     hipStream_t s) {
+  hipLaunchKernelGGL(debug_cmp_kernel, dim3(1024), dim3(256), 0, s,
+                     static_cast<const uint32_t*>(a), static_cast<const uint32_t*>(b), nwords, res);
+  return launch_check("debug_cmp");
+}
 
 size_t skip_h_workspace(int B) {
   return (size_t)B * SK_NSLICE * MH_SLICE * 2 + (size_t)B * MH_C * 4 * 2 + 256;
@@ -814,88 +801,47 @@ bool mlp_fused_h_env() {
 }
 
 size_t mlp_fused_h_image_bytes() {
-  return (size_t)MH_IMG_ELEMS * 2 + (size_t)(MH_H + MH_C) * 4;
+  return (size_t)MH_IMG_ELEMS * 2 + (size_t)(2 * MH_H + MH_C) * 4;
 }
 
-int launch_mlp_fused_h_images(const float* W1, const float* W2, unsigned short* img, hipStream_t s) {
+int launch_mlp_fused_h_images(const float* W1, const float* b1, const float* W2,
+                              unsigned short* img, hipStream_t s) {
   float* sc = reinterpret_cast<float*>(img + MH_IMG_ELEMS);
-  hipLaunchKernelGGL(mh_scale_kernel, dim3((MH_H + MH_C + 255) / 256), dim3(256), 0, s, W1, W2, sc,
-                     sc + MH_H);
+  float* eta = sc + MH_H + MH_C;
+  hipLaunchKernelGGL(mh_eta_kernel, dim3(MH_H / 256), dim3(256), 0, s, W1, b1, eta);
+  MSFNO_TRY(launch_check("mh_eta"));
+  hipLaunchKernelGGL(mh_scale_kernel, dim3((MH_H + MH_C + 255) / 256), dim3(256), 0, s, W1, W2, eta,
+                     sc, sc + MH_H);
   MSFNO_TRY(launch_check("mh_scale"));
   hipLaunchKernelGGL(mh_w1_image_kernel, dim3(256), dim3(256), 0, s, W1, sc, img);
   MSFNO_TRY(launch_check("mh_w1_image"));
-  hipLaunchKernelGGL(mh_w2_image_kernel, dim3(256), dim3(256), 0, s, W2, sc + MH_H,
+  hipLaunchKernelGGL(mh_w2_image_kernel, dim3(256), dim3(256), 0, s, W2, eta, sc + MH_H,
                      img + (int64_t)MH_HB * 2 * MH_SLICE);
   MSFNO_TRY(launch_check("mh_w2_image"));
   hipLaunchKernelGGL(mh_invert_kernel, dim3((MH_H + MH_C + 255) / 256), dim3(256), 0, s, sc);
   return launch_check("mh_invert");
 }
 
-int launch_mlp_fused_h(const float* x1, const float* scale, const float* shift, const float* resid,
-                       float* out, const unsigned short* img, const float* b1, const float* b2,
-                       int B, int64_t P, hipStream_t s) {
-  MSFNO_REQUIRE(x1 && scale && shift && out && img && b1 && B > 0 && P >= 1, MSFNO_EINVAL,
-                "mlp_fused_h: bad arguments");
+int launch_mlp_fused_h(const float* x1, const float* scale, const float* shift,
+                       const float* abound, const float* resid, float* out,
+                       const unsigned short* img, const float* b1, const float* b2, int B,
+                       int64_t P, hipStream_t s) {
+  MSFNO_REQUIRE(x1 && scale && shift && abound && out && img && b1 && B > 0 && P >= 1,
+                MSFNO_EINVAL, "mlp_fused_h: bad arguments");
   MlpHParams p{};
   p.x1 = x1; p.scale = scale; p.shift = shift; p.resid = resid; p.out = out;
+  p.abound = abound;
   p.w1img = img;
   p.w2img = img + (int64_t)MH_HB * 2 * MH_SLICE;
   const float* sc = reinterpret_cast<const float*>(img + MH_IMG_ELEMS);
   p.inv_s1 = sc;
   p.inv_s2 = sc + MH_H;
+  p.eta = sc + MH_H + MH_C;
   p.b1 = b1; p.b2 = b2; p.P = P;
-  static const int stagger = [] {  // MSFNO_MH_STAGGER: s_sleep 127 rounds (A/B)
-    const char* e = getenv("MSFNO_MH_STAGGER");
-    return e ? atoi(e) : 0;
-  }();
-  p.stagger = stagger;
-  // MSFNO_MH_NG: 16-pixel groups per wave (1 or 2); MSFNO_MH_W: waves per workgroup
-  // (4: two workgroups per CU, 8: one workgroup of 128 pixels per CU)
-  static const int ng = [] {
-    const char* e = getenv("MSFNO_MH_NG");
-    return (e && atoi(e) == 2) ? 2 : 1;
-  }();
-  static const int nw = [] {
-    const char* e = getenv("MSFNO_MH_W");
-    return (e && atoi(e) == 8) ? 8 : 4;
-  }();
-  static const int ahead = [] {  // MSFNO_MH_AHEAD: fragment reads in flight (u steps)
-    const char* e = getenv("MSFNO_MH_AHEAD");
-    return e ? atoi(e) : 2;
-  }();
-  static const int dbg = [] {
-    const char* e = getenv("MSFNO_MH_DBG");
-    return e ? atoi(e) : 0;
-  }();
-  const int waves = ng == 2 ? 4 : nw;
-  p.tiles_per_field = (int)cdiv(P, 16 * ng * waves);
+  p.tiles_per_field = (int)cdiv(P, 16 * MH_WAVES);
   const int64_t tiles = (int64_t)B * p.tiles_per_field;
   MSFNO_REQUIRE(tiles < (1LL << 31), MSFNO_EINVAL, "mlp_fused_h: grid too large");
-  void (*kern)(MlpHParams);
-  if (ng == 2)
-    kern = dbg == 1 ? mlp_fused_h_kernel<2, 1, 2, 8>
-         : dbg == 2 ? mlp_fused_h_kernel<2, 2, 2, 8>
-         : dbg == 3 ? mlp_fused_h_kernel<2, 3, 2, 8> : mlp_fused_h_kernel<2, 0, 2, 8>;
-  else if (nw == 8)
-    kern = dbg == 1 ? mlp_fused_h_kernel<2, 1, 1, 8, 8>
-         : dbg == 7 ? mlp_fused_h_kernel<2, 7, 1, 8, 8> : mlp_fused_h_kernel<2, 0, 1, 8, 8>;
-  else if (ahead == 3)
-    kern = mlp_fused_h_kernel<3>;
-  else if (ahead == 4)
-    kern = mlp_fused_h_kernel<4>;
-  else if (ahead == 6)
-    kern = mlp_fused_h_kernel<6>;
-  else if (ahead == 8)
-    kern = mlp_fused_h_kernel<8>;
-  else
-    kern = dbg == 1 ? mlp_fused_h_kernel<2, 1>
-         : dbg == 2 ? mlp_fused_h_kernel<2, 2>
-         : dbg == 3 ? mlp_fused_h_kernel<2, 3>
-         : dbg == 4 ? mlp_fused_h_kernel<2, 4>
-         : dbg == 5 ? mlp_fused_h_kernel<2, 5>
-         : dbg == 6 ? mlp_fused_h_kernel<2, 6>
-         : dbg == 7 ? mlp_fused_h_kernel<2, 7> : mlp_fused_h_kernel<2>;
-  hipLaunchKernelGGL(kern, dim3((unsigned)tiles), dim3(64 * waves), 0, s, p);
+  hipLaunchKernelGGL(mlp_fused_h_kernel<2>, dim3((unsigned)tiles), dim3(64 * MH_WAVES), 0, s, p);
   return launch_check("mlp_fused_h");
 }
 

@@ -812,12 +812,19 @@ __device__ __forceinline__ float x3_bound_scale(double mu, double m2) {
   return (float)ldexp(1.0, min(max(14 - e, -100), 100));
 }
 
+// a bound of |sc x + sh| over a channel with mean mu and sum of squared deviations m2
+// (|x - mu| <= sqrt(m2)), with 0.1 % headroom for the fp32 evaluation
+__device__ __forceinline__ float affine_bound(double sc, double sh, double mu, double m2) {
+  const double b = (fabs(sc) * sqrt(m2) + fabs(sc * mu + sh)) * (1.0 + 1e-3);
+  return (float)fmin(b, 3.0e38);
+}
+
 __global__ __launch_bounds__(256) void chan_affine_kernel(
     const float2* __restrict__ part, int64_t np, int64_t cnt, int64_t cnt_last, int C,
     const float* __restrict__ w, const float* __restrict__ bsh, float eps,
     const float* __restrict__ gamma, const float* __restrict__ beta, float film_scale,
     float* __restrict__ scale, float* __restrict__ shift, float* __restrict__ xscale,
-    float* __restrict__ lsig) {
+    float* __restrict__ lsig, float* __restrict__ abound) {
   __shared__ double sn[256], smean[256], sm2[256];
   const int bc = blockIdx.x;
   const int c = bc % C;
@@ -857,6 +864,7 @@ __global__ __launch_bounds__(256) void chan_affine_kernel(
     scale[bc] = (float)sc;
     shift[bc] = (float)sh;
     if (xscale) xscale[bc] = x3_bound_scale(mu, sm2[0]);
+    if (abound) abound[bc] = affine_bound(sc, sh, mu, sm2[0]);
     if (lsig) {  // transpose_fwd_sym4h_kernel's sigma: |x^| <= |sc| sqrt(M2) + |sc mu + sh|,
                  // |X^_m| <= 2 pi max |x^|, folded x 2
       const double bound = 2.0 * 6.283185307179586 *
@@ -875,9 +883,10 @@ __global__ __launch_bounds__(256) void chan_affine_kernel(
 int launch_chan_affine(const float2* partials, int64_t np, int64_t cnt, int64_t cnt_last, int B,
                        int C, const float* w, const float* b, float eps, const float* gamma,
                        const float* beta, float film_scale, float* scale, float* shift,
-                       hipStream_t s, float* xscale, float* lsig) {
+                       hipStream_t s, float* xscale, float* lsig, float* abound) {
   hipLaunchKernelGGL(chan_affine_kernel, dim3(B * C), dim3(256), 0, s, partials, np, cnt,
-                     cnt_last, C, w, b, eps, gamma, beta, film_scale, scale, shift, xscale, lsig);
+                     cnt_last, C, w, b, eps, gamma, beta, film_scale, scale, shift, xscale, lsig,
+                     abound);
   return launch_check("chan_affine");
 }
 
@@ -934,7 +943,7 @@ __global__ void chan_affine_parts_kernel(const double* __restrict__ parts, int n
                                          const float* __restrict__ gamma,
                                          const float* __restrict__ beta, float film_scale,
                                          float* __restrict__ scale, float* __restrict__ shift,
-                                         float* __restrict__ xscale) {
+                                         float* __restrict__ xscale, float* __restrict__ abound) {
   const int bc = blockIdx.x * blockDim.x + threadIdx.x;
   if (bc >= BC) return;
   const int c = bc % C;
@@ -955,16 +964,17 @@ __global__ void chan_affine_parts_kernel(const double* __restrict__ parts, int n
   scale[bc] = (float)sc;
   shift[bc] = (float)sh;
   if (xscale) xscale[bc] = x3_bound_scale(acc.mean, acc.m2);
+  if (abound) abound[bc] = affine_bound(sc, sh, acc.mean, acc.m2);
 }
 
 int launch_chan_affine_parts(const double* parts, int nparts, int B, int C, const float* w,
                              const float* b, float eps, const float* gamma, const float* beta,
                              float film_scale, float* scale, float* shift, hipStream_t s,
-                             float* xscale) {
+                             float* xscale, float* abound) {
   const int BC = B * C;
   hipLaunchKernelGGL(chan_affine_parts_kernel, dim3((unsigned)cdiv(BC, 256)), dim3(256), 0, s,
                      parts, nparts, BC, C, w, b, eps, gamma, beta, film_scale, scale, shift,
-                     xscale);
+                     xscale, abound);
   return launch_check("chan_affine_parts");
 }
 
