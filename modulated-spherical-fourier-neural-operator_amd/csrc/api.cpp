@@ -641,128 +641,6 @@ int transpose_inv_plan(const msfno_sht_plan_s* p, const float* Yt, float2* Yn, i
   return launch_transpose_inv(Yt, Yn, B, C, p->nlat, p->mmax, p->spec.mact, p->ldk, s);
 }
 
-// ---- x6 Legendre (symmetric plans) -----------------------------------------------
-// The per-(m, parity) problems of DESIGN.md §3 on the x6 engine: the plan's table
-// image in bf16x3 planes (rows zero-padded to 16) is built once at load; A is the
-// slab (forward, written as planes by transpose_fwd_sym_planes) or the S
-// coefficients (inverse, written as planes by the spectral MLP's output layer).
-// Off by default: measured slower than the fp32-MFMA descriptor GEMM at 721x1440
-// (forward 0.44 vs 0.38 ms, inverse 0.68 vs 0.54 ms, side stream off): the
-// per-(m, parity) problems are narrow (N ~ 90, or K <= 180), so the six-MFMA
-// k-steps of a 128 x 64 tile are too short to amortise the per-k-tile barrier
-// and DMA waits.  MSFNO_LEG_X6=1 enables it.
-bool leg_x6_enabled() {
-  static const bool on = [] {
-    const char* e = getenv("MSFNO_LEG_X6");
-    return e && e[0] == '1';
-  }();
-  return on && spec_use_x6();
-}
-
-int build_table_x6(msfno_sht_plan_s* p, const float* table, hipStream_t s) {
-  const SpecLayout& L = p->spec;
-  const int64_t ke16 = round_up(p->Ke, 16), ko16 = round_up(p->Ko, 16);
-  p->tabx_offe.assign(p->mmax, 0);
-  p->tabx_offo.assign(p->mmax, 0);
-  int64_t acc = 0;
-  for (int m = 0; m < p->mmax; ++m) {
-    const int64_t lpe = L.Lpe[m], lpo = L.Lp[m] - L.Lpe[m];
-    p->tabx_offe[m] = acc;
-    if (L.L[m] == 0) { p->tabx_offo[m] = acc; continue; }
-    acc += p->inverse ? round_up(lpe, 16) * p->ldke : ke16 * lpe;
-    p->tabx_offo[m] = acc;
-    acc += p->inverse ? round_up(lpo, 16) * ko16 : ko16 * lpo;
-  }
-  p->tabx_plane = round_up(std::max<int64_t>(acc, 8), 8);
-  if (p->tabx) (void)hipFree(p->tabx);
-  if (!p->d_tabx_offe) MSFNO_CHECK_HIP(hipMalloc(&p->d_tabx_offe, p->mmax * sizeof(int64_t)));
-  if (!p->d_tabx_offo) MSFNO_CHECK_HIP(hipMalloc(&p->d_tabx_offo, p->mmax * sizeof(int64_t)));
-  MSFNO_CHECK_HIP(hipMalloc(&p->tabx, 3 * p->tabx_plane * sizeof(unsigned short)));
-  MSFNO_CHECK_HIP(hipMemsetAsync(p->tabx, 0, 3 * p->tabx_plane * sizeof(unsigned short), s));
-  MSFNO_CHECK_HIP(hipMemcpy(p->d_tabx_offe, p->tabx_offe.data(), p->mmax * sizeof(int64_t),
-                            hipMemcpyHostToDevice));
-  MSFNO_CHECK_HIP(hipMemcpy(p->d_tabx_offo, p->tabx_offo.data(), p->mmax * sizeof(int64_t),
-                            hipMemcpyHostToDevice));
-  return launch_relayout_table_x6(*p, table, s);
-}
-
-// descriptors of the x6 problems (offsets per plane; A and C layouts as in
-// ensure_desc, B = the table image)
-int ensure_descx(msfno_sht_plan_s* p, int R, int64_t ldT) {
-  if (p->descx_R == R && p->d_descx) return MSFNO_OK;
-  MSFNO_REQUIRE(p->sym && p->tabx, MSFNO_EINVAL, "x6 Legendre needs a symmetric plan");
-  const SpecLayout& L = p->spec;
-  const int ke16 = (int)round_up(p->Ke, 16), ko16 = (int)round_up(p->Ko, 16);
-  std::vector<GemmDesc> d;
-  int tiles = 0;
-  auto push = [&](GemmDesc g) {
-    g.tiles_m = (int)cdiv(g.M, X6D_TILE_M);
-    g.tiles_n = (int)cdiv(g.N, X6D_TILE_N);
-    if (g.tiles_m * g.tiles_n == 0) return;
-    g.tile_start = tiles;
-    tiles += g.tiles_m * g.tiles_n;
-    d.push_back(g);
-  };
-  for (int m = 0; m < L.mact; ++m) {
-    if (L.L[m] == 0) continue;
-    const int64_t slab = (int64_t)p->slab[m] * R * p->ldk;
-    const int lpe = L.Lpe[m], lpo = L.Lp[m] - L.Lpe[m];
-    const int le = (L.L[m] + 1) / 2, lo = L.L[m] / 2;
-    GemmDesc g{};
-    g.M = R;
-    if (!p->inverse) {
-      GemmDesc e = g;  // even: Xs (R x Ke) . We (Ke x Lpe) -> S[:, off]
-      e.N = lpe; e.K = p->Ke; e.lda = p->ldk; e.ldb = lpe; e.ldc = (int)ldT;
-      e.offA = slab; e.offB = p->tabx_offe[m]; e.offC = L.off[m];
-      push(e);
-      if (lo > 0) {
-        GemmDesc o = g;  // odd: Xa (R x Ko) . Wo (Ko x Lpo) -> S[:, off + Lpe]
-        o.N = lpo; o.K = p->Ko; o.lda = p->ldk; o.ldb = lpo; o.ldc = (int)ldT;
-        o.offA = slab + p->ldke; o.offB = p->tabx_offo[m]; o.offC = L.off[m] + lpe;
-        push(o);
-      }
-    } else {
-      GemmDesc e = g;  // even: E (R x Ke) = S_e (R x Le) . Pe (Le x Ke)
-      e.N = p->Ke; e.K = le; e.lda = (int)ldT; e.ldb = ke16; e.ldc = p->ldk;
-      e.offA = L.off[m]; e.offB = p->tabx_offe[m]; e.offC = slab;
-      push(e);
-      GemmDesc o = g;  // odd: O (R x Ko) = S_o (R x Lo) . Po (Lo x Ko); K = 0 writes zeros
-      o.N = p->Ko; o.K = lo; o.lda = (int)ldT; o.ldb = ko16; o.ldc = p->ldk;
-      o.offA = L.off[m] + lpe; o.offB = p->tabx_offo[m]; o.offC = slab + p->ldke;
-      push(o);
-    }
-  }
-  for (const GemmDesc& g : d)
-    MSFNO_REQUIRE(g.lda % 8 == 0 && g.ldb % 8 == 0 && g.ldc % 4 == 0 && g.offA % 8 == 0 &&
-                      g.offB % 8 == 0 && g.offC % 4 == 0,
-                  MSFNO_EINVAL, "x6 Legendre: misaligned problem layout");
-  if (p->d_descx) MSFNO_CHECK_HIP(hipFree(p->d_descx));
-  p->d_descx = nullptr;
-  MSFNO_CHECK_HIP(hipMalloc(&p->d_descx, std::max<size_t>(1, d.size()) * sizeof(GemmDesc)));
-  if (!d.empty())
-    MSFNO_CHECK_HIP(hipMemcpy(p->d_descx, d.data(), d.size() * sizeof(GemmDesc), hipMemcpyHostToDevice));
-  p->ndescx = (int)d.size();
-  p->descx_tiles = tiles;
-  p->descx_R = R;
-  return MSFNO_OK;
-}
-
-// forward: Xtp (slab planes, plane stride xstride) -> S fp32 (ld ldT)
-int legendre_fwd_x6(msfno_sht_plan_s* f, const unsigned short* Xtp, int64_t xstride, float* S,
-                    int R, hipStream_t s) {
-  MSFNO_TRY(ensure_descx(f, R, f->spec.ldT));
-  return gemm_x6d(Xtp, xstride, f->tabx, f->tabx_plane, S, f->d_descx, f->ndescx,
-                  f->descx_tiles, s);
-}
-
-// inverse: Sp (coefficient planes [plane][R][ldT]) -> Yt fp32 slabs
-int legendre_inv_x6(msfno_sht_plan_s* g, const unsigned short* Sp, float* Yt, int R,
-                    hipStream_t s) {
-  MSFNO_TRY(ensure_descx(g, R, g->spec.ldT));
-  return gemm_x6d(Sp, (int64_t)R * g->spec.ldT, g->tabx, g->tabx_plane, Yt, g->d_descx,
-                  g->ndescx, g->descx_tiles, s);
-}
-
 int legendre_fwd(msfno_sht_plan_s* f, const float* Xt, float* S, int R, hipStream_t s,
                  const float* rowscale, int C) {
   if (leg_x3_enabled() && !rowscale) {
@@ -853,12 +731,6 @@ void carve_block(Carve& cv, BlockBufs& b, const msfno_block_desc* d,
   } else {
     b.xt = cv.take<float>(BC * L.T * 2);
     b.yt = cv.take<float>(BC * L.T * 2);
-  }
-  b.Xtp = b.Sp = nullptr;
-  if (d->filter_type == MSFNO_FILTER_NONLINEAR && leg_x6_enabled()) {
-    // used when both plans turn out symmetric (known once their tables are loaded)
-    b.Xtp = cv.take<unsigned short>(3LL * f->nslab * R * f->ldk);
-    b.Sp = cv.take<unsigned short>(3LL * R * L.ldT);
   }
   b.Yt = cv.take<float>((int64_t)g->mmax * R * g->ldk);
   b.Yn = cv.take<float2>(BC * g->nlat * g->mmax);
@@ -997,7 +869,7 @@ int check_pair(const msfno_block_desc* d, const msfno_sht_plan_s* f,
 }
 
 int run_filter(const msfno_block_desc* d, msfno_sht_plan_s* f, msfno_sht_plan_s* g,
-                      const BlockBufs& b, int B, hipStream_t s, unsigned short* Sp) {
+                      const BlockBufs& b, int B, hipStream_t s) {
   const int64_t C = d->C;
   const SpecLayout& L = f->spec;
   if (d->filter_type == MSFNO_FILTER_NONLINEAR) {
@@ -1006,7 +878,7 @@ int run_filter(const msfno_block_desc* d, msfno_sht_plan_s* f, msfno_sht_plan_s*
     prof(ST_SPEC_PREP, s);
     const bool x6 = spec_use_x6() && b.dw.spec[0];
     const bool c3m = !x6 && use_c3m();
-    if (x6 && spec_use_3m() && !Sp && C <= Hs) {
+    if (x6 && spec_use_3m() && C <= Hs) {
       // Gauss 3M complex GEMMs (gemm_x6c.hip): weights Wr, Wi, Wr+Wi of all layers in
       // one launch; layer 0's input split into 3M planes in Sc (free until layer 1)
       SpecWeightsX6p sw{};
@@ -1054,41 +926,6 @@ int run_filter(const msfno_block_desc* d, msfno_sht_plan_s* f, msfno_sht_plan_s*
         return !(e && e[0] == '0');
       }();
       const bool f32b = l0f32 && nl >= 1 && L.ldT % 4 == 0;
-      // MSFNO_SPEC_HF32=1: the hidden activations stay fp32 rows (8 B per complex value
-      // instead of 18 B of 3M planes); every layer splits its input while staging
-      static const bool hf32 = [] {
-        const char* e = getenv("MSFNO_SPEC_HF32");
-        return e && e[0] == '1';
-      }();
-      // MSFNO_SPEC_HF32T=1: fp32 hidden activations in the tiled layout (8 B per complex
-      // value, 16-KB contiguous stages), every layer splitting its input while staging
-      static const bool hf32t = [] {
-        const char* e = getenv("MSFNO_SPEC_HF32T");
-        return e && e[0] == '1';
-      }();
-      if (f32b && hf32t) {
-        const float* in = b.Sa;
-        for (int l = 0; l <= nl; ++l) {
-          prof(l == nl ? ST_SPEC_OUT : ST_SPEC_L0 + std::min(l, 3), s);
-          float* out = l == nl ? b.Sa : ((l & 1) ? b.Sc : b.Sb);
-          MSFNO_TRY(gemm_x6c_f32t(sw.out[l], sw.co[l], sw.ci[l], in, (int)L.ldT, l > 0, (int)L.Tp,
-                                  l < nl ? out : nullptr, l < nl ? nullptr : out, (int)L.ldT, l < nl,
-                                  B, s));
-          in = out;
-        }
-        return MSFNO_OK;
-      }
-      if (f32b && hf32) {
-        const float* in = b.Sa;
-        for (int l = 0; l <= nl; ++l) {
-          prof(l == nl ? ST_SPEC_OUT : ST_SPEC_L0 + std::min(l, 3), s);
-          float* out = l == nl ? b.Sa : ((l & 1) ? b.Sc : b.Sb);
-          MSFNO_TRY(gemm_x6c_f32b(sw.out[l], sw.co[l], sw.ci[l], in, (int)L.ldT, (int)L.Tp,
-                                  nullptr, 0, out, (int)L.ldT, l < nl, B, s));
-          in = out;
-        }
-        return MSFNO_OK;
-      }
       // hidden activations in the tiled layout (gemm_x6c.hip; spectral MLP 8 % faster
       // at config 2); MSFNO_X6C_TILED=0: row layout [b][mat][plane][c][ld]
       static const bool tiled = [] {
@@ -1173,10 +1010,6 @@ int run_filter(const msfno_block_desc* d, msfno_sht_plan_s* f, msfno_sht_plan_s*
         }
         const int ldc = l < nl ? (int)ldTx : (int)L.ldT;
         const int64_t sC = l < nl ? 3 * 2LL * co * ldTx : 2LL * co * L.ldT;
-        if (l == nl && Sp) {  // S for the x6 inverse Legendre: planes [plane][R][ldT]
-          e.c_planes = Sp;
-          e.c_plane_stride = 2LL * B * co * L.ldT;
-        }
         if (l > 0 || split_l0) e.a_planes = static_cast<const unsigned short*>(b.dw.spec[l]);
         if (l == 0 && split_l0) {  // Sc is free during layer 0
           // layer 0's fp32 input (the forward Legendre output) -> planes in Sc: one
@@ -1240,9 +1073,6 @@ int run_spectral(const msfno_block_desc* d, msfno_sht_plan_s* f, msfno_sht_plan_
                  const std::function<int()>& after_leg = std::function<int()>(),
                  const std::function<int()>& before_inv = std::function<int()>()) {
   const int64_t C = d->C, BC = (int64_t)B * C, R = 2 * BC;
-  // x6 Legendre: symmetric plans, slab / coefficient planes carved, row path
-  const bool lx6 = b.Xtp && b.Sp && f->sym && g->sym && !use_fft_tile(f) &&
-                   f->spec.ldT == g->spec.ldT;
   prof(ST_FFT_FWD, s);
   const float scale = (float)(2.0 * M_PI / f->nlon);
   if (use_fft_tile(f)) {
@@ -1271,20 +1101,13 @@ int run_spectral(const msfno_block_desc* d, msfno_sht_plan_s* f, msfno_sht_plan_
       if (after_norm0) MSFNO_TRY(after_norm0());
     }
     prof(ST_TRANSPOSE_FWD, s);
-    if (!lx6 && norm0 && b.lsig && b.isr && x3f_usable(f)) {
+    if (norm0 && b.lsig && b.isr && x3f_usable(f)) {
       // slab as x3h fp16 pairs in the Xt buffer (the fp32 bytes)
       unsigned short* Xp = reinterpret_cast<unsigned short*>(b.Xt);
       MSFNO_TRY(launch_transpose_fwd_sym_h(b.Xn, Xp, B, (int)C, f->geom(), f->mmax, b.sc0, b.sh0,
                                            b.lsig, b.isr, s));
       prof(ST_LEG_FWD, s);
       MSFNO_TRY(legendre_fwd_x3f(f, Xp, b.isr, b.Sa, (int)R, s));
-    } else if (lx6) {
-      const int64_t xstride = (int64_t)f->nslab * R * f->ldk;
-      MSFNO_TRY(launch_transpose_fwd_sym_planes(b.Xn, b.Xtp, xstride, B, (int)C, f->geom(),
-                                                f->mmax, norm0 ? b.sc0 : nullptr,
-                                                norm0 ? b.sh0 : nullptr, s));
-      prof(ST_LEG_FWD, s);
-      MSFNO_TRY(legendre_fwd_x6(f, b.Xtp, xstride, b.Sa, (int)R, s));
     } else {
       MSFNO_TRY(transpose_fwd_plan(f, b.Xn, b.Xt, B, (int)C, norm0 ? b.sc0 : nullptr,
                                    norm0 ? b.sh0 : nullptr, s));
@@ -1293,13 +1116,10 @@ int run_spectral(const msfno_block_desc* d, msfno_sht_plan_s* f, msfno_sht_plan_
     }
   }
   if (after_leg) MSFNO_TRY(after_leg());
-  MSFNO_TRY(run_filter(d, f, g, b, B, s, lx6 ? b.Sp : nullptr));
+  MSFNO_TRY(run_filter(d, f, g, b, B, s));
   if (before_inv) MSFNO_TRY(before_inv());
   prof(ST_LEG_INV, s);
-  if (lx6)
-    MSFNO_TRY(legendre_inv_x6(g, b.Sp, b.Yt, (int)R, s));
-  else
-    MSFNO_TRY(legendre_inv(g, b.Sa, b.Yt, (int)R, s));
+  MSFNO_TRY(legendre_inv(g, b.Sa, b.Yt, (int)R, s));
   return MSFNO_OK;
 }
 
@@ -1618,10 +1438,6 @@ int msfno_sht_plan_destroy(msfno_sht_plan_t p) {
   if (p->d_tril_local) (void)hipFree(p->d_tril_local);
   if (p->d_Lpe) (void)hipFree(p->d_Lpe);
   if (p->d_desc) (void)hipFree(p->d_desc);
-  if (p->tabx) (void)hipFree(p->tabx);
-  if (p->d_tabx_offe) (void)hipFree(p->d_tabx_offe);
-  if (p->d_tabx_offo) (void)hipFree(p->d_tabx_offo);
-  if (p->d_descx) (void)hipFree(p->d_descx);
   if (p->d_desc3) (void)hipFree(p->d_desc3);
   if (p->d_desc3f) (void)hipFree(p->d_desc3f);
   if (p->d_tile3f) (void)hipFree(p->d_tile3f);
@@ -1672,12 +1488,9 @@ int msfno_sht_plan_load_table(msfno_sht_plan_t p, const float* table, void* stre
                             hipMemcpyHostToDevice));
   p->desc_R = -1;  // descriptors depend on the layout
   MSFNO_TRY(launch_relayout_table(*p, table, s));
-  p->descx_R = -1;
   p->desc3_R = -1;
   p->desc3f_R = -1;
   p->tab3_valid = 0;  // the x3h image is rebuilt from the new table on first use
-  // the bf16x3 table image only feeds the x6 Legendre GEMMs (MSFNO_LEG_X6=1)
-  if (sym && leg_x6_enabled() && !p->band_world) MSFNO_TRY(build_table_x6(p, table, s));
   p->table_loaded = 1;
   return MSFNO_OK;
 }
@@ -1830,7 +1643,30 @@ int msfno_block_forward(const msfno_block_desc* d, msfno_sht_plan_t f, msfno_sht
     prof(ST_SKIP, ss);
     GemmEpi e;
     e.bias = d->skip_b;
-    if (b.xs && C == 256 && skip_h_env()) {
+    // MSFNO_PX_SIDEK (diagnostic, PX mode): what the side stream runs at the block start
+    // instead: "ones" = skip_h with per-channel scales 1 (x1 wrong), "fft" = a second
+    // forward row FFT of x into scratch (x1 not computed)
+    static const int sidek = [] {
+      const char* e = getenv("MSFNO_PX_SIDEK");
+      return !e ? 0 : std::string(e) == "ones" ? 1 : std::string(e) == "fft" ? 2 : 0;
+    }();
+    static float* dbg_ones = nullptr;
+    static float2* dbg_xn = nullptr;
+    if (skip_px && sidek == 1) {
+      if (!dbg_ones) {
+        std::vector<float> ones((size_t)BC * 4, 1.f);
+        MSFNO_CHECK_HIP(hipMalloc(&dbg_ones, ones.size() * sizeof(float)));
+        MSFNO_CHECK_HIP(hipMemcpy(dbg_ones, ones.data(), ones.size() * sizeof(float),
+                                  hipMemcpyHostToDevice));
+      }
+      MSFNO_TRY(launch_skip_h(d->skip_w, dbg_ones, x, x1, d->skip_b, B, P, b.dw.skip,
+                              b.dw.skip_b, ss));
+    } else if (skip_px && sidek == 2) {
+      if (!dbg_xn)
+        MSFNO_CHECK_HIP(hipMalloc(&dbg_xn, (BC * f->nlat * f->mmax + BC * f->nlat) * sizeof(float2)));
+      MSFNO_TRY(launch_fft_r2c_rows(f->fft, x, dbg_xn, dbg_xn + BC * f->nlat * f->mmax,
+                                    BC * f->nlat, f->mmax, (float)(2.0 * M_PI / f->nlon), ss));
+    } else if (b.xs && C == 256 && skip_h_env()) {
       MSFNO_TRY(launch_skip_h(d->skip_w, skip_px ? nullptr : b.xs, x, x1, d->skip_b, B, P,
                               b.dw.skip, b.dw.skip_b, ss));
     } else if (b.xs) {
@@ -1863,7 +1699,13 @@ int msfno_block_forward(const msfno_block_desc* d, msfno_sht_plan_t f, msfno_sht
   }();
   static float* dbg_x = nullptr;
   static int dbg_call = 0;
-  const bool pxc = px_check && skip_px && d->inner_skip == MSFNO_SKIP_LINEAR;
+  float2* px_snap = nullptr;  // PX check: the forward FFT output right after the FFT
+  const bool pxc = px_check && b.xs && C == 256 && d->inner_skip == MSFNO_SKIP_LINEAR;
+  // MSFNO_PX_AT=fft (diagnostic): the PX skip forked after the forward FFT
+  static const bool px_at_fft = [] {
+    const char* e = getenv("MSFNO_PX_AT");
+    return e && std::string(e) == "fft";
+  }();
   if (pxc) {
     if (!dbg_x) {
       MSFNO_CHECK_HIP(hipMalloc(&dbg_x, BC * P * sizeof(float)));
@@ -1874,7 +1716,7 @@ int msfno_block_forward(const msfno_block_desc* d, msfno_sht_plan_t f, msfno_sht
   if (d->inner_skip == MSFNO_SKIP_LINEAR) {
     MSFNO_REQUIRE(d->skip_w, MSFNO_EINVAL, "missing inner_skip weight");
     MSFNO_TRY(side_ctx(&side, s));
-    if ((!xpl && !b.xs) || skip_px) MSFNO_TRY(launch_skip());
+    if ((!xpl && !b.xs) || (skip_px && !px_at_fft)) MSFNO_TRY(launch_skip());
     if (pxc && px_check == 2 && side) MSFNO_CHECK_HIP(hipStreamSynchronize(side->side));
   }
   // MSFNO_SKIP_AT=leg: fork the x3h skip after the forward Legendre instead of right
@@ -1885,7 +1727,25 @@ int msfno_block_forward(const msfno_block_desc* d, msfno_sht_plan_t f, msfno_sht
     return !e ? 0 : std::string(e) == "leg" ? 1 : std::string(e) == "inv" ? 2 : 0;
   }();
   const std::function<int()> none;
-  if (skip_px)
+  if (skip_px && px_at_fft)
+    MSFNO_TRY(run_spectral(d, f, g, b, x, B, true, s, nullptr, launch_skip));
+  else if (skip_px && pxc) {
+    // diagnostic: snapshot the forward FFT's output as soon as it is complete (stream
+    // order), to tell a wrong FFT from a later overwrite of its output
+    static float2* dbg_xn = nullptr;
+    static size_t dbg_xn_b = 0;
+    const size_t xnb = (size_t)BC * f->nlat * f->mmax * sizeof(float2);
+    if (xnb > dbg_xn_b) {
+      if (dbg_xn) MSFNO_CHECK_HIP(hipFree(dbg_xn));
+      MSFNO_CHECK_HIP(hipMalloc(&dbg_xn, xnb));
+      dbg_xn_b = xnb;
+    }
+    px_snap = dbg_xn;
+    MSFNO_TRY(run_spectral(d, f, g, b, x, B, true, s, nullptr, [&]() -> int {
+      MSFNO_CHECK_HIP(hipMemcpyAsync(dbg_xn, b.Xn, xnb, hipMemcpyDeviceToDevice, s));
+      return MSFNO_OK;
+    }));
+  } else if (skip_px)
     MSFNO_TRY(run_spectral(d, f, g, b, x, B, true, s));
   else if (b.xs && skip_at == 1)
     MSFNO_TRY(run_spectral(d, f, g, b, x, B, true, s, nullptr, none, none, launch_skip));
@@ -1902,19 +1762,22 @@ int msfno_block_forward(const msfno_block_desc* d, msfno_sht_plan_t f, msfno_sht
     // serial recomputation: the skip, and the whole spectral path into a second
     // workspace; every intermediate compared bit for bit with this call's
     static void* dbg_ws2 = nullptr;
+    static size_t dbg_ws2_b = 0;
     static unsigned long long* dbg_r = nullptr;
     const size_t wsb = msfno_block_workspace_size(d, f, g, B);
-    if (!dbg_ws2) {
+    if (wsb > dbg_ws2_b) {
+      if (dbg_ws2) MSFNO_CHECK_HIP(hipFree(dbg_ws2));
       MSFNO_CHECK_HIP(hipMalloc(&dbg_ws2, wsb));
-      MSFNO_CHECK_HIP(hipMalloc(&dbg_r, 32 * sizeof(unsigned long long)));
+      dbg_ws2_b = wsb;
     }
+    if (!dbg_r) MSFNO_CHECK_HIP(hipMalloc(&dbg_r, 32 * sizeof(unsigned long long)));
     Carve cv2;
     cv2.base = static_cast<char*>(dbg_ws2);
     BlockBufs b2;
     carve_block(cv2, b2, d, f, g, B, true);
     MSFNO_TRY(run_spectral(d, f, g, b2, x, B, true, s));
-    MSFNO_TRY(launch_skip_h(d->skip_w, nullptr, x, b2.x1, d->skip_b, B, P, b2.dw.skip,
-                            b2.dw.skip_b, s));
+    MSFNO_TRY(launch_skip_h(d->skip_w, skip_px ? nullptr : b2.xs, x, b2.x1, d->skip_b, B, P,
+                            b2.dw.skip, b2.dw.skip_b, s));
     const int64_t R = 2 * BC;
     struct Cmp { const char* name; const void* a; const void* b2; int64_t words; };
     const Cmp cmps[] = {
@@ -1922,6 +1785,8 @@ int msfno_block_forward(const msfno_block_desc* d, msfno_sht_plan_t f, msfno_sht
         {"x1", b.x1, b2.x1, BC * P},
         {"skipimg", b.dw.skip, b2.dw.skip, (int64_t)(skip_h_workspace(B) - 256) / 4},
         {"Xn", b.Xn, b2.Xn, BC * f->nlat * f->mmax * 2},
+        {"XnSnap", px_snap, b2.Xn, px_snap ? BC * f->nlat * f->mmax * 2 : 0},
+        {"XnLate", px_snap, b.Xn, px_snap ? BC * f->nlat * f->mmax * 2 : 0},
         {"rs0", b.rs0, b2.rs0, BC * f->nlat * 2},
         {"sc0", b.sc0, b2.sc0, BC},
         {"sh0", b.sh0, b2.sh0, BC},
@@ -1932,21 +1797,43 @@ int msfno_block_forward(const msfno_block_desc* d, msfno_sht_plan_t f, msfno_sht
         {"Yt", b.Yt, b2.Yt, (int64_t)g->mmax * R * g->ldk},
     };
     const int nc = (int)(sizeof(cmps) / sizeof(cmps[0]));
+    constexpr int RW = 3 + 3 * 16;  // per compare: count, first, log flag, 16 log entries
+    static unsigned long long* dbg_log = nullptr;
+    if (!dbg_log) MSFNO_CHECK_HIP(hipMalloc(&dbg_log, nc * RW * sizeof(unsigned long long)));
+    (void)dbg_r;
+    std::vector<unsigned long long> init((size_t)nc * RW, 0ull);
     for (int i = 0; i < nc; ++i) {
-      MSFNO_CHECK_HIP(hipMemsetAsync(dbg_r + 2 * i, 0, sizeof(unsigned long long), s));
-      MSFNO_CHECK_HIP(hipMemsetAsync(dbg_r + 2 * i + 1, 0xff, sizeof(unsigned long long), s));
-      if (cmps[i].words > 0)
-        MSFNO_TRY(launch_debug_cmp(cmps[i].a, cmps[i].b2, cmps[i].words, dbg_r + 2 * i, s));
+      init[(size_t)i * RW + 1] = ~0ull;
+      init[(size_t)i * RW + 2] = 1;
     }
-    unsigned long long h[32];
-    MSFNO_CHECK_HIP(hipMemcpyAsync(h, dbg_r, 2 * nc * sizeof(unsigned long long),
+    MSFNO_CHECK_HIP(hipMemcpyAsync(dbg_log, init.data(), init.size() * sizeof(unsigned long long),
+                                   hipMemcpyHostToDevice, s));
+    for (int i = 0; i < nc; ++i)
+      if (cmps[i].words > 0)
+        MSFNO_TRY(launch_debug_cmp(cmps[i].a, cmps[i].b2, cmps[i].words, dbg_log + i * RW, s));
+    std::vector<unsigned long long> h((size_t)nc * RW);
+    MSFNO_CHECK_HIP(hipMemcpyAsync(h.data(), dbg_log, h.size() * sizeof(unsigned long long),
                                    hipMemcpyDeviceToHost, s));
     MSFNO_CHECK_HIP(hipStreamSynchronize(s));
     std::string line = "PX_CHECK call " + std::to_string(dbg_call++) + ":";
-    for (int i = 0; i < nc; ++i)
-      line += std::string(" ") + cmps[i].name + "=" + std::to_string(h[2 * i]) +
-              (h[2 * i] ? "@" + std::to_string((long long)h[2 * i + 1]) : std::string());
+    for (int i = 0; i < nc; ++i) {
+      const unsigned long long* r = &h[(size_t)i * RW];
+      line += std::string(" ") + cmps[i].name + "=" + std::to_string(r[0]) +
+              (r[0] ? "@" + std::to_string((long long)r[1]) : std::string());
+    }
     fprintf(stderr, "%s\n", line.c_str());
+    static const bool logv = getenv("MSFNO_PX_LOG") != nullptr;
+    for (int i = 0; logv && i < nc; ++i) {
+      const unsigned long long* r = &h[(size_t)i * RW];
+      if (!r[0] || std::string(cmps[i].name) == "Yt" || std::string(cmps[i].name) == "S") continue;
+      for (int k = 0; k < (int)std::min<unsigned long long>(r[0], 16); ++k) {
+        float fa, fb;
+        const uint32_t ua = (uint32_t)r[3 + 3 * k + 1], ub = (uint32_t)r[3 + 3 * k + 2];
+        std::memcpy(&fa, &ua, 4);
+        std::memcpy(&fb, &ub, 4);
+        fprintf(stderr, "  %s[%llu] = %.9g (serial %.9g)\n", cmps[i].name, r[3 + 3 * k], fa, fb);
+      }
+    }
   }
   // ---- filter output + skip (+ GELU for the linear filter) -> x1, norm1 partials ---
   const float* skip_src = d->inner_skip == MSFNO_SKIP_LINEAR ? x1

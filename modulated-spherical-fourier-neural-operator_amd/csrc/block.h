@@ -55,8 +55,6 @@ struct BlockBufs {
   float* ab1 = nullptr;  // norm1 output bound per (b, c) (chan_affine abound; fused x3h MLP)
   float* W1f; float* b1f; float* h;
   unsigned short* x1p;  // x1 as bf16x3 planes for fc1 (x6 engine), else null
-  unsigned short* Xtp;  // x6 Legendre: forward slabs as bf16x3 planes, else null
-  unsigned short* Sp;   // x6 Legendre: filter output S as planes [plane][R][ldT]
   unsigned short* mfimg;  // fused MLP weight image (mlp_fused), else null
   float* cs;  // x3h spectral MLP: per-(b, column) input scale and its inverse [2][B][ld]
   float* xs = nullptr;  // x3h inner skip: per-(b, c) power-of-two scale of x (B-row scales)
@@ -78,7 +76,7 @@ int legendre_fwd(msfno_sht_plan_s* f, const float* Xt, float* S, int R, hipStrea
 int legendre_inv(msfno_sht_plan_s* g, const float* S, float* Yt, int R, hipStream_t s);
 // spectral filter on S (f->spec layout) in b.Sa (in place)
 int run_filter(const msfno_block_desc* d, msfno_sht_plan_s* f, msfno_sht_plan_s* g,
-               const BlockBufs& b, int B, hipStream_t s, unsigned short* Sp = nullptr);
+               const BlockBufs& b, int B, hipStream_t s);
 bool use_fft_tile(const msfno_sht_plan_s* p);
 bool use_c3m();
 int c3m_tile();
@@ -107,7 +105,6 @@ int64_t mlp_chunk(int64_t P);
 int64_t mlp_h_floats(int B, int64_t Hd, int64_t P);
 bool x1_planes(const msfno_block_desc* d, const msfno_sht_plan_s* g);
 bool skip_planes(const msfno_block_desc* d, const msfno_sht_plan_s* f, const BlockBufs& b);
-bool leg_x6_enabled();
 // the inner-skip GEMM on the x3h engine (gemm_x3), forked after the norm0 statistics
 bool skip_x3(const msfno_block_desc* d);
 // plan construction (mask: optional m-set, see SpecLayout::build)

@@ -232,12 +232,6 @@ struct SpecWeightsX6p {
 };
 size_t spec_weights_x6p_layout(SpecWeightsX6p& a);
 int launch_spec_weights_x6p(const SpecWeightsX6p& a, hipStream_t s);
-// descriptor-mode x6 GEMM (gemm_x6p.hip): every problem's A (M x K, lda) and B
-// (K x N, ldb; rows zero-padded to a multiple of 16) in bf16x3 planes (plane
-// strides sAxp, sBxp; descriptor offsets per plane), fp32 C; tiles 128 x 64
-constexpr int X6D_TILE_M = 128, X6D_TILE_N = 64;
-int gemm_x6d(const unsigned short* Ax, int64_t sAxp, const unsigned short* Bx, int64_t sBxp,
-             float* C, const GemmDesc* descs, int ndesc, int total_tiles, hipStream_t s);
 // spectral-MLP layer as a Gauss 3M complex GEMM on the x6 engine (gemm_x6c.hip);
 // activations in "3M planes" [b][re, im, re+im][plane][rows][ld]
 size_t gemm_x6c_weight_bytes(int co, int ci);
@@ -249,9 +243,6 @@ int gemm_x6c_f32b(const unsigned short* Aw, int co, int ci, const float* Sin, in
                   unsigned short* Y, int ldy, float* Sout, int ldSout, bool relu, int B,
                   hipStream_t s, bool tiled_out = false);
 int64_t x6c_tiled_elems(int rows, int N);
-int gemm_x6c_f32t(const unsigned short* Aw, int co, int ci, const float* Sin, int ldSin,
-                  bool tiled_in, int N, float* Tout, float* Sout, int ldSout, bool relu, int B,
-                  hipStream_t s);
 int gemm_x6c(const unsigned short* Aw, int co, int ci, const unsigned short* X, int N, int ldx,
              unsigned short* Y, float* S, int ldS, bool relu, int B, hipStream_t s, int lay = 0);
 // the same chain on the x3h engine (two fp16 terms, three MFMAs per product; tiled
@@ -315,16 +306,6 @@ struct msfno_sht_plan_s {
   int desc_R = -1;
   msfno::GemmDesc* d_desc = nullptr;
   int ndesc = 0, desc_tiles = 0;
-  // x6 Legendre (symmetric plans): table image in bf16x3 planes (gemm_x6d's B),
-  // per-m even / odd block offsets within a plane, and its descriptor cache
-  unsigned short* tabx = nullptr;
-  int64_t tabx_plane = 0;
-  std::vector<int64_t> tabx_offe, tabx_offo;
-  int64_t* d_tabx_offe = nullptr;
-  int64_t* d_tabx_offo = nullptr;
-  int descx_R = -1;
-  msfno::GemmDesc* d_descx = nullptr;
-  int ndescx = 0, descx_tiles = 0;
   // x3h Legendre (legendre_x3.hip): descriptor cache, the table image (two fp16
   // planes per problem, column-scaled) and the inverse column scales
   int desc3_R = -1;

@@ -403,19 +403,14 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_x6c_kernel(X6CParams p) {
         csb[e] = p.colscale[z * p.cs_b + min(n0 + bcol_f + e, N - 1)];
     }
   }
+  static_assert(!BF32 || (LAY & 1) == 0, "BF32: fp32 rows in");
   auto load_bf = [&](int kt) {
-    if constexpr ((LAY & 1) != 0) {  // tiled fp32: [tn][kt][re/im][16][128], 16 KB per stage
-      const float* r = Xf + ((int64_t)tn * p.kt_in + kt) * 2 * B_PLANE + brow_f * BN + bcol_f;
-      fre = *reinterpret_cast<const float4*>(r);
-      fim = *reinterpret_cast<const float4*>(r + B_PLANE);
-    } else {
-      const int k = kt * BK + brow_f;
-      const int kc = min(k, K - 1);
-      const int col = min(n0 + bcol_f, (N - 1) & ~3);
-      const float* r = Xf + (int64_t)kc * p.ldxf + col;
-      fre = *reinterpret_cast<const float4*>(r);
-      fim = *reinterpret_cast<const float4*>(r + p.xf_im);
-    }
+    const int k = kt * BK + brow_f;
+    const int kc = min(k, K - 1);
+    const int col = min(n0 + bcol_f, (N - 1) & ~3);
+    const float* r = Xf + (int64_t)kc * p.ldxf + col;
+    fre = *reinterpret_cast<const float4*>(r);
+    fim = *reinterpret_cast<const float4*>(r + p.xf_im);
   };
   auto store_bf = [&](int kt, int st) {
     const int k = kt * BK + brow_f;
@@ -605,32 +600,6 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_x6c_kernel(X6CParams p) {
       }
       __syncthreads();
     }
-  } else if constexpr (!PLANES_OUT && (LAY & 2) != 0) {
-    // tiled fp32 rows (Re, Im) for a BF32 consumer: [b][tn][kt][re/im][16][128]
-    constexpr int CS_LD = BN + 8;
-    float* St = p.S + z * p.s_b + (int64_t)tn * p.kt_out * 2 * B_PLANE;
-#pragma unroll
-    for (int mat = 0; mat < 2; ++mat) {
-#pragma unroll
-      for (int i = 0; i < MT; ++i)
-#pragma unroll
-        for (int j = 0; j < NT; ++j)
-#pragma unroll
-          for (int r = 0; r < 16; ++r)
-            lds[(wm * WM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * half) * CS_LD + wn * WN + j * 32 +
-                l32] = acc[mat][i][j][r];
-      __syncthreads();
-      constexpr int NQ = BM * BN / 4 / (64 * NW);
-#pragma unroll
-      for (int qq = 0; qq < NQ; ++qq) {
-        const int idx = tid + 64 * NW * qq;
-        const int lr = idx / (BN / 4), c = 4 * (idx % (BN / 4));
-        const int m = m0 + lr;
-        *reinterpret_cast<float4*>(St + ((int64_t)(m >> 4) * 2 + mat) * B_PLANE + (m & 15) * BN + c) =
-            *reinterpret_cast<const float4*>(lds + lr * CS_LD + c);
-      }
-      __syncthreads();
-    }
   } else if constexpr (PLANES_OUT) {
 #pragma unroll
     for (int mat = 0; mat < 3; ++mat) {
@@ -739,53 +708,6 @@ int gemm_x6c_f32b(const unsigned short* Aw, int co, int ci, const float* Sin, in
   else
     hipLaunchKernelGGL((gemm_x6c_kernel<false, 4, 2, true>), grid, dim3(512), 0, s, p);
   return launch_check("gemm_x6c_f32b");
-}
-
-// a layer of the fp32-tiled chain (MSFNO_SPEC_HF32T): input fp32 rows of S (lay_in 0,
-// ld ldSin) or tiled fp32 (lay_in 1); output tiled fp32 (Tout) or fp32 rows of Sout
-int gemm_x6c_f32t(const unsigned short* Aw, int co, int ci, const float* Sin, int ldSin,
-                  bool tiled_in, int N, float* Tout, float* Sout, int ldSout, bool relu, int B,
-                  hipStream_t s) {
-  if (co <= 0 || N <= 0 || B <= 0) return MSFNO_OK;
-  MSFNO_REQUIRE((Tout != nullptr) != (Sout != nullptr), MSFNO_EINVAL, "gemm_x6c_f32t: one output");
-  MSFNO_REQUIRE(tiled_in || (ldSin % 4 == 0 && ldSin >= N), MSFNO_EINVAL,
-                "gemm_x6c_f32t: fp32 rows need ld % 4 == 0");
-  X6CParams p{};
-  p.Mp = (int)round_up(co, X6C_BM);
-  const int KT = (int)cdiv(ci, X6C_BK);
-  p.Aw = Aw;
-  p.a_plane = (int64_t)p.Mp * KT * 16;
-  p.a_mat = 3 * p.a_plane;
-  p.Xf = Sin;
-  p.kt_in = (int)round_up(ci, X6C_BM) / 16;
-  p.xf_b = tiled_in ? x6c_tiled_elems(ci, N) * 2 / 9 : 2LL * ci * ldSin;
-  p.xf_im = (int64_t)ci * ldSin;
-  p.ldxf = ldSin;
-  p.ldx = 8;
-  p.kt_out = p.Mp / 16;
-  if (Tout) {
-    p.S = Tout;
-    p.s_b = x6c_tiled_elems(co, N) * 2 / 9;
-  } else {
-    p.S = Sout;
-    p.s_b = 2LL * co * ldSout;
-    p.s_im = (int64_t)co * ldSout;
-    p.ldS = ldSout;
-  }
-  p.co = co; p.ci = ci; p.N = N;
-  p.tiles_m = p.Mp / X6C_BM;
-  p.tiles_n = (int)cdiv(N, X6C_BN);
-  p.relu = relu ? 1 : 0;
-  const dim3 grid(p.tiles_m * p.tiles_n, 1, B);
-  if (tiled_in && Tout)
-    hipLaunchKernelGGL((gemm_x6c_kernel<false, 4, 2, true, 0, 3>), grid, dim3(512), 0, s, p);
-  else if (tiled_in)
-    hipLaunchKernelGGL((gemm_x6c_kernel<false, 4, 2, true, 0, 1>), grid, dim3(512), 0, s, p);
-  else if (Tout)
-    hipLaunchKernelGGL((gemm_x6c_kernel<false, 4, 2, true, 0, 2>), grid, dim3(512), 0, s, p);
-  else
-    hipLaunchKernelGGL((gemm_x6c_kernel<false, 4, 2, true, 0, 0>), grid, dim3(512), 0, s, p);
-  return launch_check("gemm_x6c_f32t");
 }
 
 // elements of one field's tiled 3M activation with `rows` channel rows, N columns

@@ -481,184 +481,7 @@ __global__ __launch_bounds__(512) void gemm_x6q_kernel(GemmParams p) {
       p, acc, reinterpret_cast<float*>(lds_raw), bias_s, C, addend, M, N, ldc, m0, n0, 0);
 }
 
-// ---- descriptor mode: the per-(m, parity) Legendre GEMMs --------------------------
-// All problems of one transform in one launch (binary search over tile starts).
-// Both operands bf16x3 planes, row-major: A (M x K, lda; the latitude slab or the
-// S coefficients), B (K x N, ldb; the plan's table image, rows zero-padded to a
-// multiple of 16).  Offsets in the descriptors are per plane; plane strides
-// sAxp / sBxp.  Tile 128 x 64 x 16, 4 waves (2 x 2, each 64 x 32), a ring of
-// four 18-KB stages (three k-tiles in flight), two workgroups per CU.
-// A k-chunk past K is clamped to the last valid chunk: its (finite) values meet
-// the zero rows of B.  LDS images: A as in gemm_x6p_kernel; B [plane][16][64]
-// with the 16-B units of row r XORed by 4 ((r >> 1) & 1).
-constexpr int X6D_BM = X6D_TILE_M, X6D_BN = X6D_TILE_N;
-
-__global__ __launch_bounds__(256) void gemm_x6d_kernel(GemmParams p) {
-  constexpr int BM = X6D_BM, BN = X6D_BN, BK = 16;
-  constexpr int WGM = 2, WGN = 2;
-  constexpr int WM = BM / WGM, WN = BN / WGN;  // 64 x 32
-  constexpr int MT = WM / 32, NT = WN / 32;
-  constexpr int A_PLANE = BM * BK, B_PLANE = BK * BN;
-  constexpr int STAGE = 3 * (A_PLANE + B_PLANE);  // 18 KB
-  constexpr int NSTAGE = 4;
-  constexpr int RING_BYTES = NSTAGE * STAGE * 2;
-  constexpr int EPI_BYTES = 32 * WGM * (BN + 8) * 4;
-  constexpr int LDS_BYTES = RING_BYTES > EPI_BYTES ? RING_BYTES : EPI_BYTES;
-  static_assert(STAGE * 2 == 18 * 1024, "stage = 12 A + 6 B pieces of 1 KB");
-  __shared__ __attribute__((aligned(16))) char lds_raw[LDS_BYTES];
-  unsigned short* const ring = reinterpret_cast<unsigned short*>(lds_raw);
-
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wave = tid >> 6;
-  const int wm = wave / WGN, wn = wave % WGN;
-  const int half = lane >> 5, l32 = lane & 31;
-
-  const int lin = xcd_remap(blockIdx.x, gridDim.x);
-  int lo = 0, hi = p.ndesc - 1;
-  while (lo < hi) {  // last descriptor with tile_start <= lin
-    const int mid = (lo + hi + 1) >> 1;
-    if (p.descs[mid].tile_start <= lin) lo = mid; else hi = mid - 1;
-  }
-  const GemmDesc d = p.descs[lo];
-  const int local = lin - d.tile_start;
-  const int tm = local % d.tiles_m, tn = local / d.tiles_m;
-  const int M = d.M, N = d.N, K = d.K, lda = d.lda, ldb = d.ldb;
-  const int m0 = tm * BM, n0 = tn * BN;
-  const int nk = (K + BK - 1) / BK;
-  const unsigned short* Ax = p.Ax + d.offA;
-  const unsigned short* Bx = p.Bx + d.offB;
-  float* C = p.C + d.offC;
-
-  // LDS-DMA pieces: A piece a = wave + 4 q (q < 3): plane a / 4, rows 32 (a % 4)..;
-  // B piece b = wave (+ 4 for waves 0, 1): plane b / 2, k rows 8 (b % 2)..+7
-  const int kmax8 = (K - 1) & ~7;
-  const unsigned short* a_row[3];
-  int a_h[3], a_dst[3];
-#pragma unroll
-  for (int q = 0; q < 3; ++q) {
-    const int a = wave + 4 * q;
-    const int pl = a >> 2, mb = a & 3;
-    const int m = 32 * mb + (lane >> 1);
-    a_h[q] = (lane & 1) ^ ((m >> 3) & 1);
-    a_row[q] = Ax + (int64_t)pl * p.sAxp + (int64_t)min(m0 + m, M - 1) * lda;
-    a_dst[q] = pl * A_PLANE + mb * 32 * BK;
-  }
-  const int nbp = wave < 2 ? 2 : 1;  // B pieces of this wave
-  const unsigned short* b_src[2];
-  int b_dst[2];
-#pragma unroll
-  for (int q = 0; q < 2; ++q) {
-    const int b = wave + 4 * q;  // valid when q < nbp
-    const int pl = b >> 1, rb = b & 1;
-    const int row = 8 * rb + (lane >> 3);
-    const int gu = (lane & 7) ^ (4 * ((row >> 1) & 1));
-    b_src[q] = Bx + (int64_t)pl * p.sBxp + (int64_t)row * ldb + min(n0 + 8 * gu, ldb - 8);
-    b_dst[q] = 3 * A_PLANE + pl * B_PLANE + rb * 8 * BN;
-  }
-  const uint32_t ring_lds = (uint32_t)(uintptr_t)(lds_void*)ring;
-  auto issue = [&](int kt, int st) {
-    const uint32_t base = ring_lds + (uint32_t)(st * STAGE * 2);
-#pragma unroll
-    for (int q = 0; q < 3; ++q)
-      glds16(a_row[q] + min(kt * BK + 8 * a_h[q], kmax8),
-             __builtin_amdgcn_readfirstlane(base + (uint32_t)(a_dst[q] * 2)));
-#pragma unroll
-    for (int q = 0; q < 2; ++q)
-      if (q < nbp)
-        glds16(b_src[q] + (int64_t)kt * BK * ldb,
-               __builtin_amdgcn_readfirstlane(base + (uint32_t)(b_dst[q] * 2)));
-  };
-  const int lpt = 3 + nbp;  // LDS-DMA instructions of this wave per k-tile
-
-  floatx16 acc[MT][NT];
-#pragma unroll
-  for (int i = 0; i < MT; ++i)
-#pragma unroll
-    for (int j = 0; j < NT; ++j)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-  int a_off[MT];
-#pragma unroll
-  for (int i = 0; i < MT; ++i) {
-    const int row = wm * WM + i * 32 + l32;
-    a_off[i] = row * BK + 8 * (half ^ ((row >> 3) & 1));
-  }
-  const int li = lane & 15, g16 = (lane >> 4) & 1;
-  const int br = 8 * half + (li >> 2);
-  int b_off[NT];
-#pragma unroll
-  for (int j = 0; j < NT; ++j) {
-    const int c = wn * WN + j * 32 + 16 * g16 + 4 * (li & 3);
-    b_off[j] = 3 * A_PLANE + br * BN + (((c >> 3) ^ (4 * ((br >> 1) & 1))) << 3) + (c & 7);
-  }
-  auto mfma_tile = [&](int st) {
-    typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
-    const unsigned short* base = ring + st * STAGE;
-    bf16x8 a[MT][3];
-#pragma unroll
-    for (int i = 0; i < MT; ++i)
-#pragma unroll
-      for (int pl = 0; pl < 3; ++pl)
-        a[i][pl] = *reinterpret_cast<const bf16x8*>(base + pl * A_PLANE + a_off[i]);
-#pragma unroll
-    for (int j = 0; j < NT; ++j) {
-      bf16x8 b[3];
-#pragma unroll
-      for (int pl = 0; pl < 3; ++pl) {
-        const unsigned short* q = base + pl * B_PLANE + b_off[j];
-        const s16x4 lo4 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-            (lds_s16x4*)((__attribute__((address_space(3))) unsigned short*)q));
-        const s16x4 hi4 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-            (lds_s16x4*)((__attribute__((address_space(3))) unsigned short*)(q + 4 * BN)));
-        const s16x8 v = {lo4[0], lo4[1], lo4[2], lo4[3], hi4[0], hi4[1], hi4[2], hi4[3]};
-        b[pl] = __builtin_bit_cast(bf16x8, v);
-      }
-#pragma unroll
-      for (int i = 0; i < MT; ++i) {
-        floatx16 c = acc[i][j];
-        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i][2], b[0], c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i][1], b[1], c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i][0], b[2], c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i][1], b[0], c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i][0], b[1], c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i][0], b[0], c, 0, 0, 0);
-        acc[i][j] = c;
-      }
-    }
-  };
-
-  for (int t = 0; t < NSTAGE - 1 && t < nk; ++t) issue(t, t);
-  for (int kt = 0; kt < nk; ++kt) {
-    // k-tiles kt+1 .. kt+2 (those issued) may stay in flight
-    wait_vmcnt(lpt * min(NSTAGE - 2, nk - 1 - kt));
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    if (kt + NSTAGE - 1 < nk) issue(kt + NSTAGE - 1, (kt + NSTAGE - 1) % NSTAGE);
-    __builtin_amdgcn_s_setprio(1);
-    mfma_tile(kt % NSTAGE);
-    __builtin_amdgcn_s_setprio(0);
-  }
-  __syncthreads();  // all DMA retired (the last wait was vmcnt(0)); the ring is free
-  gemm_epilogue<BM, BN, 0, WGM, WGN>(p, acc, reinterpret_cast<float*>(lds_raw), nullptr, C,
-                                     nullptr, M, N, d.ldc, m0, n0, 0);
-}
-
 // ---- host ---------------------------------------------------------------------
-
-int gemm_x6d(const unsigned short* Ax, int64_t sAxp, const unsigned short* Bx, int64_t sBxp,
-             float* C, const GemmDesc* descs, int ndesc, int total_tiles, hipStream_t s) {
-  if (ndesc <= 0 || total_tiles <= 0) return MSFNO_OK;
-  GemmParams p{};
-  p.Ax = Ax; p.sAxp = sAxp;
-  p.Bx = Bx; p.sBxp = sBxp;
-  p.C = C;
-  p.descs = descs; p.ndesc = ndesc;
-  // every problem's offC and ldc are multiples of 4 (checked where the descriptors are built)
-  p.vecC = (reinterpret_cast<uintptr_t>(C) & 15) == 0;
-  hipLaunchKernelGGL(gemm_x6d_kernel, dim3(total_tiles), dim3(256), 0, s, p);
-  return launch_check("gemm_x6d");
-}
 
 size_t gemm_x6p_workspace(int M, int K, int batch_a) {
   // k padded to 32: covers the 16-deep (x6p) and 32-deep (x6q) A images

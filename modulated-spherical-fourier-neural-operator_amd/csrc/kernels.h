@@ -140,13 +140,6 @@ int launch_gelu_grad_mul(float* dh, const float* pre, int64_t n, hipStream_t s);
 int launch_film_grad_reduce(const float* du, const float* x1, const float* an, const float* tn,
                             float scale, int BC, int64_t P, float* dgamma, float* dbeta,
                             hipStream_t s);
-// x6 Legendre table image (bf16x3 planes, rows padded to 16; gemm_x6d's B)
-int launch_relayout_table_x6(const msfno_sht_plan_s& p, const float* table, hipStream_t s);
-// symmetric forward transpose writing Xt as bf16x3 planes (plane stride pstride),
-// zero pads (gemm_x6d's A)
-int launch_transpose_fwd_sym_planes(const float2* Xn, unsigned short* Xtp, int64_t pstride, int B,
-                                    int C, const LatGeom& g, int mmax, const float* nscale,
-                                    const float* nshift, hipStream_t s);
 // *d_flag |= 1 unless table[m][l][nlat-1-k] = (-1)^(l-m) table[m][l][k] (rel. 1e-5)
 int launch_check_symmetry(const float* table, int mmax, int lmax, int nlat, int* d_flag,
                           hipStream_t s);

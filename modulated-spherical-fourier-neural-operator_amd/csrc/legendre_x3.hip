@@ -368,19 +368,11 @@ __device__ float x3r_sink[256];
 
 __device__ __forceinline__ int x3r_swz(int n) { return (n >> 3) & 1; }
 
-// TR: the accumulator holds C^T (the table as the MFMA A operand): a lane keeps one
-// slab row and 4 consecutive latitudes per register group, stored as 16-B vectors
-// (4 stores per chunk instead of 16; unsegmented C, ldc and offC multiples of 4; the
-// last vector of a row may write up to 3 pad columns, which nothing reads)
-// DEEP: the ring holds as many stages of this problem's size as fit the 72 KB
-// (six for Kp <= 96, four for 128, three above): short-K problems are latency-bound
-// (a chunk's MFMAs are a few hundred cycles against one DMA round trip)
-template <int NK, bool TR, bool DEEP>
+template <int NK>
 __device__ __forceinline__ void x3r_body(const X3DParams& p, const GemmDesc& d, int m0,
                                          unsigned char* ring, float* tau_s) {
-  constexpr int STG = DEEP ? 4 * NK * 1024 : X3R_STAGE;  // bytes per stage
-  constexpr int NST = !DEEP ? X3R_NSTG : NK <= 3 ? 6 : NK == 4 ? 4 : 3;
-  static_assert(NST * STG <= X3R_NSTG * X3R_STAGE, "ring");
+  constexpr int STG = X3R_STAGE;  // bytes per stage
+  constexpr int NST = X3R_NSTG;
   constexpr int KS = 2 * NK;       // 16-deep k-steps
   constexpr int KP = 32 * NK;      // padded K of the image
   constexpr int NI = KP / 32;      // DMA wave-instructions per wave and stage (= NK)
@@ -456,8 +448,8 @@ __device__ __forceinline__ void x3r_body(const X3DParams& p, const GemmDesc& d, 
   // 1 / sigma of the 16 rows this lane's accumulator holds: (r & 3) + 8 (r >> 2) + 4 half
   float isv[16];
 #pragma unroll
-  for (int r = 0; r < 16; ++r) isv[r] = TR ? 1.f / sg : __shfl(1.f / sg, (r & 3) + 8 * (r >> 2) + 4 * half);
-  constexpr int NSTORE = TR ? 4 : 16;  // store instructions per chunk
+  for (int r = 0; r < 16; ++r) isv[r] = __shfl(1.f / sg, (r & 3) + 8 * (r >> 2) + 4 * half);
+  constexpr int NSTORE = 16;  // store instructions per chunk
 
   const int rbase = m0 + 32 * wave + 4 * half;
   float* Cb = p.C + d.offC;
@@ -481,28 +473,9 @@ __device__ __forceinline__ void x3r_body(const X3DParams& p, const GemmDesc& d, 
       const int off = ks * 1024 + l32 * 32 + 16 * (half ^ x3r_swz(l32));
       const h8 b0 = *reinterpret_cast<const h8*>(st + off);
       const h8 b1 = *reinterpret_cast<const h8*>(st + KS * 1024 + off);
-      if constexpr (TR) {
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(b0, a[ks][1], acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(b1, a[ks][0], acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(b0, a[ks][0], acc, 0, 0, 0);
-      } else {
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[ks][1], b0, acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[ks][0], b1, acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[ks][0], b0, acc, 0, 0, 0);
-      }
-    }
-    if constexpr (TR) {
-      const int row = m0 + 32 * wave + l32;
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int lat0 = 32 * j + 8 * g + 4 * half;
-        const float4 t4 = *reinterpret_cast<const float4*>(tau_s + lat0);
-        const float4 v = make_float4(acc[4 * g] * isv[0] * t4.x, acc[4 * g + 1] * isv[0] * t4.y,
-                                     acc[4 * g + 2] * isv[0] * t4.z, acc[4 * g + 3] * isv[0] * t4.w);
-        float* dst = (row < M && lat0 < N) ? Cb + (int64_t)row * d.ldc + lat0 : x3r_sink + 4 * lane;
-        *reinterpret_cast<float4*>(dst) = v;
-      }
-      continue;
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[ks][1], b0, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[ks][0], b1, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[ks][0], b0, acc, 0, 0, 0);
     }
     const int col = 32 * j + l32;
     const float it = tau_s[min(col, N - 1)];
@@ -525,7 +498,6 @@ __device__ __forceinline__ void x3r_zero(const X3DParams& p, const GemmDesc& d, 
   }
 }
 
-template <bool TR, bool DEEP>
 __global__ __launch_bounds__(256) void legendre_x3r_kernel(X3DParams p) {
   __shared__ __attribute__((aligned(16))) unsigned char ring[X3R_NSTG * X3R_STAGE];
   __shared__ __attribute__((aligned(16))) float tau_s[X3R_NMAX + 32];
@@ -534,12 +506,12 @@ __global__ __launch_bounds__(256) void legendre_x3r_kernel(X3DParams p) {
   const int m0 = (lin - d.tile_start) * X3D_BM;
   switch ((d.K + 31) / 32) {
     case 0: x3r_zero(p, d, m0); break;
-    case 1: x3r_body<1, TR, DEEP>(p, d, m0, ring, tau_s); break;
-    case 2: x3r_body<2, TR, DEEP>(p, d, m0, ring, tau_s); break;
-    case 3: x3r_body<3, TR, DEEP>(p, d, m0, ring, tau_s); break;
-    case 4: x3r_body<4, TR, DEEP>(p, d, m0, ring, tau_s); break;
-    case 5: x3r_body<5, TR, DEEP>(p, d, m0, ring, tau_s); break;
-    default: x3r_body<6, TR, DEEP>(p, d, m0, ring, tau_s); break;
+    case 1: x3r_body<1>(p, d, m0, ring, tau_s); break;
+    case 2: x3r_body<2>(p, d, m0, ring, tau_s); break;
+    case 3: x3r_body<3>(p, d, m0, ring, tau_s); break;
+    case 4: x3r_body<4>(p, d, m0, ring, tau_s); break;
+    case 5: x3r_body<5>(p, d, m0, ring, tau_s); break;
+    default: x3r_body<6>(p, d, m0, ring, tau_s); break;
   }
 }
 
@@ -694,21 +666,7 @@ int legendre_x3r(const float* A, const unsigned short* img, const float* invs, f
   p.A = A; p.img = img; p.invs = invs; p.C = C;
   p.descs = descs; p.tile_desc = tile_desc; p.ndesc = ndesc;
   p.segC_w = e.segC_w; p.segC_stride = e.segC_stride;
-  // MSFNO_X3R_T=1: C^T accumulators, 16-B stores (unsegmented C only)
-  static const bool tr_env = [] {
-    const char* e = getenv("MSFNO_X3R_T");
-    return e && e[0] == '1';
-  }();
-  const bool tr = tr_env && !e.segC_w && (reinterpret_cast<uintptr_t>(C) & 15) == 0;
-  // MSFNO_X3R_DEEP=1: as many stages of the problem's own size as fit (measured equal:
-  // 0.285 vs 0.285 ms in-block — the kernel is not bound by DMA depth)
-  static const bool deep = [] {
-    const char* e = getenv("MSFNO_X3R_DEEP");
-    return e && e[0] == '1';
-  }();
-  void (*kern)(X3DParams) = tr ? (deep ? legendre_x3r_kernel<true, true> : legendre_x3r_kernel<true, false>)
-                                : (deep ? legendre_x3r_kernel<false, true> : legendre_x3r_kernel<false, false>);
-  hipLaunchKernelGGL(kern, dim3(tiles), dim3(256), 0, s, p);
+  hipLaunchKernelGGL(legendre_x3r_kernel, dim3(tiles), dim3(256), 0, s, p);
   return launch_check("legendre_x3r");
 }
 

@@ -417,22 +417,10 @@ int launch_transpose_fwd_sym_h(const float2* Xn, unsigned short* Xp, int B, int 
                                hipStream_t s) {
   if (!nscale || !nshift || !lsig || !isr || !g.sym || (g.ldke & 7) || (g.ldk & 7) ||
       std::max(g.ldke, g.ldk - g.ldke) > cdiv(g.Ke, 64) * 64)
-    return MSFNO_EINVAL;  // (a 128-row tile grid covers at least the 64-row one)
-  // MSFNO_TRH=128: 128 x 32 tiles (256-B plane segments, 67 KB of LDS; measured slower:
-  // 0.386 vs 0.33 ms in-block) instead of 64 x 32
-  static const int tk = [] {
-    const char* e = getenv("MSFNO_TRH");
-    return (e && atoi(e) == 128) ? 128 : 64;
-  }();
-  if (tk == 64) {
-    dim3 grid((unsigned)cdiv(g.Ke, 64), (unsigned)cdiv(mmax, 32), (unsigned)(B * C));
-    hipLaunchKernelGGL((transpose_fwd_sym4h_kernel<64, 32>), grid, dim3(256), 0, s, Xn, Xp,
-                       B, C, g, mmax, nscale, nshift, lsig, isr);
-  } else {
-    dim3 grid((unsigned)cdiv(g.Ke, 128), (unsigned)cdiv(mmax, 32), (unsigned)(B * C));
-    hipLaunchKernelGGL((transpose_fwd_sym4h_kernel<128, 32>), grid, dim3(256), 0, s, Xn, Xp,
-                       B, C, g, mmax, nscale, nshift, lsig, isr);
-  }
+    return MSFNO_EINVAL;
+  dim3 grid((unsigned)cdiv(g.Ke, 64), (unsigned)cdiv(mmax, 32), (unsigned)(B * C));
+  hipLaunchKernelGGL((transpose_fwd_sym4h_kernel<64, 32>), grid, dim3(256), 0, s, Xn, Xp, B, C,
+                     g, mmax, nscale, nshift, lsig, isr);
   return launch_check("transpose_fwd_sym_h");
 }
 
@@ -563,143 +551,6 @@ int launch_band_pack(const float2* Xn, float* send, int B, int C, const LatGeom&
   return launch_check("band_pack");
 }
 
-// The same fold + affine, written as bf16x3 planes Xtp[plane][m][R][ldk] (the A
-// operand of the x6 Legendre GEMM, gemm_x6d).  Every slab column of the grid's
-// k range is written, pads (Xs: k in [Ke, ldke), Xa: k in [nh, ldk - ldke)) as
-// zeros: the GEMM's last k-chunk reads them.  Threads own k pairs (4-B stores).
-__global__ __launch_bounds__(256) void transpose_fwd_sym_planes_kernel(
-    const float2* __restrict__ Xn, unsigned short* __restrict__ Xtp, int64_t pstride, int B,
-    int C, LatGeom g, int mmax, const float* __restrict__ nscale,
-    const float* __restrict__ nshift) {
-  __shared__ float2 tn[TMM][TK + 1], ts[TMM][TK + 1];
-  const int k0 = blockIdx.x * TK, m0 = blockIdx.y * TMM;
-  const int bc = blockIdx.z;
-  const int b = bc / C, c = bc - b * C;
-  const float2* src = Xn + (int64_t)bc * g.nlat * mmax;
-  for (int i = threadIdx.x; i < TK * TMM; i += 256) {
-    const int kk = i / TMM, mm = i - kk * TMM;
-    const int k = k0 + kk, m = m0 + mm;
-    float2 vn = make_float2(0.f, 0.f), vs = vn;
-    if (k < g.Ke && m < mmax) {
-      vn = src[(int64_t)k * mmax + m];
-      if (k < g.nh) vs = src[(int64_t)(g.nlat - 1 - k) * mmax + m];
-    }
-    tn[mm][kk] = vn;
-    ts[mm][kk] = vs;
-  }
-  __syncthreads();
-  const float sc = nscale ? nscale[bc] : 1.f;
-  const float sh = nshift ? nshift[bc] * kTwoPi : 0.f;
-  const int64_t R = 2LL * B * C;
-  const int64_t rre = (int64_t)(b * 2 + 0) * C + c;
-  const int64_t rim = (int64_t)(b * 2 + 1) * C + c;
-  const int ko = g.ldk - g.ldke;  // width of the Xa block
-  for (int i = threadIdx.x; i < TK / 2 * TMM; i += 256) {
-    const int mm = i / (TK / 2), kk = 2 * (i - mm * (TK / 2));
-    const int k = k0 + kk, m = m0 + mm;
-    if (k >= g.ldke || m >= mmax) continue;
-    const float shm = (m == 0) ? sh : 0.f;
-    float sre[2], sim[2], are[2], aim[2];
-#pragma unroll
-    for (int t = 0; t < 2; ++t) {
-      const int kt = k + t;
-      const float2 n = tn[mm][kk + t], q = ts[mm][kk + t];
-      const bool pair = kt < g.nh;
-      // affine per row, then fold: s(N + S) + 2t  /  s(N - S); zeros in the pads
-      sre[t] = kt < g.Ke ? (pair ? fmaf(sc, n.x + q.x, 2.f * shm) : fmaf(sc, n.x, shm)) : 0.f;
-      sim[t] = kt < g.Ke ? (pair ? sc * (n.y + q.y) : sc * n.y) : 0.f;
-      are[t] = pair ? sc * (n.x - q.x) : 0.f;
-      aim[t] = pair ? sc * (n.y - q.y) : 0.f;
-    }
-    unsigned short* dst = Xtp + (int64_t)m * R * g.ldk + k;
-    uint32_t t0, t1, t2;
-    split2(sre[0], sre[1], t0, t1, t2);
-    uint32_t* o = reinterpret_cast<uint32_t*>(dst + rre * g.ldk);
-    o[0] = t0; o[pstride / 2] = t1; o[pstride] = t2;
-    split2(sim[0], sim[1], t0, t1, t2);
-    o = reinterpret_cast<uint32_t*>(dst + rim * g.ldk);
-    o[0] = t0; o[pstride / 2] = t1; o[pstride] = t2;
-    if (k < ko) {
-      split2(are[0], are[1], t0, t1, t2);
-      o = reinterpret_cast<uint32_t*>(dst + rre * g.ldk + g.ldke);
-      o[0] = t0; o[pstride / 2] = t1; o[pstride] = t2;
-      split2(aim[0], aim[1], t0, t1, t2);
-      o = reinterpret_cast<uint32_t*>(dst + rim * g.ldk + g.ldke);
-      o[0] = t0; o[pstride / 2] = t1; o[pstride] = t2;
-    }
-  }
-}
-
-int launch_transpose_fwd_sym_planes(const float2* Xn, unsigned short* Xtp, int64_t pstride, int B,
-                                    int C, const LatGeom& g, int mmax, const float* nscale,
-                                    const float* nshift, hipStream_t s) {
-  MSFNO_REQUIRE(g.sym && g.ldke % 16 == 0 && g.ldk % 16 == 0 && pstride % 2 == 0, MSFNO_EINVAL,
-                "transpose_fwd_sym_planes: needs a symmetric plan with 16-aligned slab columns");
-  dim3 grid((unsigned)cdiv(g.ldke, TK), (unsigned)cdiv(mmax, TMM), (unsigned)(B * C));
-  hipLaunchKernelGGL(transpose_fwd_sym_planes_kernel, grid, dim3(256), 0, s, Xn, Xtp, pstride, B,
-                     C, g, mmax, nscale, nshift);
-  return launch_check("transpose_fwd_sym_planes");
-}
-
-// x6 Legendre table image (gemm_x6d's B operand): per m an even-parity and an
-// odd-parity block, row-major, rows zero-padded to a multiple of 16, split into
-// three bf16 planes (plane stride `plane`).
-//   forward: even (Ke x Lpe):  B[k][c] = weights[m][m + 2c][k];    odd (Ko x Lpo): m + 2c + 1
-//   inverse: even (Lpe x ldke): B[c][k] = pct[m][m + 2c][k] (k < Ke); odd (Lpo x ldko16)
-// (values 0 outside the triangle l < lmax, as in relayout_table_kernel)
-__global__ void relayout_table_x6_kernel(const float* __restrict__ tab, unsigned short* __restrict__ out,
-                                         int64_t plane, const int64_t* __restrict__ offe,
-                                         const int64_t* __restrict__ offo,
-                                         const int* __restrict__ Lp, const int* __restrict__ Lpe,
-                                         int lmax, LatGeom g, int inverse) {
-  const int m = blockIdx.y;
-  const int L = lmax - m;
-  const int lp = Lp[m], lpe = Lpe[m], lpo = lp - lpe;
-  if (L <= 0 || lp == 0) return;
-  const float* t = tab + (int64_t)m * lmax * g.nlat;
-  auto at = [&](int j, int k) -> float {
-    return (j < L) ? t[(int64_t)(m + j) * g.nlat + k] : 0.f;
-  };
-  auto r16 = [](int v) { return (v + 15) & ~15; };
-  const int ldko = r16(g.Ko);
-  // block geometry: rows x ld, and the value of (row, col)
-  int rows_e, ld_e, rows_o, ld_o;
-  if (!inverse) { rows_e = r16(g.Ke); ld_e = lpe; rows_o = r16(g.Ko); ld_o = lpo; }
-  else { rows_e = r16(lpe); ld_e = g.ldke; rows_o = r16(lpo); ld_o = ldko; }
-  const int64_t ne = (int64_t)rows_e * ld_e / 2, no = (int64_t)rows_o * ld_o / 2;  // pairs
-  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < ne + no;
-       e += (int64_t)gridDim.x * blockDim.x) {
-    const bool odd = e >= ne;
-    const int64_t idx = 2 * (odd ? e - ne : e);
-    const int ld = odd ? ld_o : ld_e;
-    const int r = (int)(idx / ld), c0 = (int)(idx - (int64_t)r * ld);
-    float v[2];
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      const int c = c0 + q;
-      float x = 0.f;
-      if (!inverse) {  // row = latitude k, column = coefficient c
-        const int kmax = odd ? g.Ko : g.Ke;
-        if (r < kmax && c < (odd ? lpo : lpe)) x = at(2 * c + (odd ? 1 : 0), r);
-      } else {         // row = coefficient, column = latitude
-        const int kmax = odd ? g.Ko : g.Ke;
-        if (r < (odd ? lpo : lpe) && c < kmax) x = at(2 * r + (odd ? 1 : 0), c);
-      }
-      v[q] = x;
-    }
-    uint32_t t0, t1, t2;
-    split2(v[0], v[1], t0, t1, t2);
-    uint32_t* o = reinterpret_cast<uint32_t*>(out + (odd ? offo[m] : offe[m]) + idx);
-    o[0] = t0; o[plane / 2] = t1; o[plane] = t2;
-  }
-}
-
-int launch_relayout_table_x6(const msfno_sht_plan_s& p, const float* table, hipStream_t s) {
-  dim3 grid(64, (unsigned)p.mmax);
-  hipLaunchKernelGGL(relayout_table_x6_kernel, grid, dim3(256), 0, s, table, p.tabx, p.tabx_plane,
-                     p.d_tabx_offe, p.d_tabx_offo, p.d_Lp, p.d_Lpe, p.lmax, p.geom(), p.inverse);
-  return launch_check("relayout_table_x6");
-}
 
 template <int TKx, int TMx>
 __global__ __launch_bounds__(256) void transpose_inv_sym_kernel(const float* __restrict__ Yt,

@@ -36,9 +36,7 @@ VARIANTS = [
     {"MSFNO_CONTRACT_NS": "3"},
     {"MSFNO_CX16": "0"},
     {"MSFNO_SPEC_L0F32": "0"},
-    {"MSFNO_SPEC_HF32": "1"},
     {"MSFNO_X6C_TILED": "0"},
-    {"MSFNO_SPEC_HF32T": "1"},
     {"MSFNO_MF_XS": "1"},
     {"MSFNO_X6C_WAVES": "24", "MSFNO_X6C_TILED": "0"},
     {"MSFNO_X6C_WAVES": "4", "MSFNO_X6C_TILED": "0"},
@@ -47,15 +45,12 @@ VARIANTS = [
     {"MSFNO_SIDE_CUSTRIDE": "3"},
     {"MSFNO_LEG_X3R": "0"},
     {"MSFNO_LEG_X3F": "0"},
-    {"MSFNO_TRH": "128"},
     {"MSFNO_X3F_NS": "2"},
     {"MSFNO_SKIP_H": "0"},
     {"MSFNO_SKIP_AT": "leg"},
     {"MSFNO_SKIP_AT": "inv"},
-    {"MSFNO_MH_STAGGER": "4"},
-    {"MSFNO_X3R_T": "1"},
-    {"MSFNO_X3R_DEEP": "1"},
     {"MSFNO_SKIP_PX": "1"},
+    {"MSFNO_MH_PERSIST": "0"},
 ]
 
 
