@@ -223,13 +223,11 @@ static hipError_t create_side_stream(hipStream_t* s, int dev) {
   return e;
 }
 
-int side_ctx(SideCtx** out, hipStream_t caller) {
-  static int enabled = -1;
-  if (enabled < 0) {
-    const char* e = getenv("MSFNO_SIDE_STREAM");
-    enabled = (e && e[0] == '0') ? 0 : 1;
-  }
-  *out = nullptr;
+int side_ctx(std::shared_ptr<SideCtx>* out, hipStream_t caller) {
+  // (read at every call: tests switch it inside one process)
+  const char* se = getenv("MSFNO_SIDE_STREAM");
+  const bool enabled = !(se && se[0] == '0');
+  out->reset();
   if (!enabled) return MSFNO_OK;
   // no fork while the caller's stream is being captured into a HIP graph: the
   // captured fork/join made a 12-block network step 19.0 ms instead of 12.4 ms
@@ -243,13 +241,13 @@ int side_ctx(SideCtx** out, hipStream_t caller) {
   // it) + one fork/join event pair per (device, caller stream).  The device comes
   // from the caller's stream (not the thread's current device); two caller streams
   // never share fork/join events.  The per-caller map is bounded (LRU, kMaxCallers):
-  // a caller that creates and destroys many streams recycles the oldest pair
-  // instead of leaking events (an evicted pair is destroyed; HIP releases an event
-  // whose recorded work is still pending once it completes).
+  // the oldest pair is dropped from the map, and its events are destroyed when the
+  // last holder releases it (HIP releases an event whose recorded work is still
+  // pending once it completes)
   static std::mutex mu;
   static std::map<int, hipStream_t> side_of_dev;
   struct Entry {
-    SideCtx c;
+    std::shared_ptr<SideCtx> c;
     uint64_t used = 0;
   };
   static std::map<std::pair<int, hipStream_t>, Entry> ctx;
@@ -264,30 +262,30 @@ int side_ctx(SideCtx** out, hipStream_t caller) {
     auto lru = ctx.begin();
     for (auto j = ctx.begin(); j != ctx.end(); ++j)
       if (j->second.used < lru->second.used) lru = j;
-    (void)hipEventDestroy(lru->second.c.fork);
-    (void)hipEventDestroy(lru->second.c.join);
     ctx.erase(lru);
   }
   Entry& en = ctx[{dev, caller}];
   en.used = ++tick;
-  SideCtx& c = en.c;
-  if (!c.side || !c.fork || !c.join) {
+  if (!en.c) {
+    auto c = std::make_shared<SideCtx>();
     int cur = 0;
     MSFNO_CHECK_HIP(hipGetDevice(&cur));
     if (cur != dev) MSFNO_CHECK_HIP(hipSetDevice(dev));
     hipError_t e = hipSuccess;
     hipStream_t& pooled = side_of_dev[dev];
     if (!pooled) e = create_side_stream(&pooled, dev);
-    c.side = pooled;
-    if (e == hipSuccess && !c.fork) e = hipEventCreateWithFlags(&c.fork, hipEventDisableTiming);
-    if (e == hipSuccess && !c.join) e = hipEventCreateWithFlags(&c.join, hipEventDisableTiming);
+    c->side = pooled;
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&c->fork, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&c->join, hipEventDisableTiming);
     if (cur != dev) (void)hipSetDevice(cur);
     if (e != hipSuccess) {
+      ctx.erase({dev, caller});
       set_error(std::string("side stream creation failed: ") + hipGetErrorString(e));
       return MSFNO_EHIP;
     }
+    en.c = std::move(c);
   }
-  *out = &c;
+  *out = en.c;
   return MSFNO_OK;
 }
 
@@ -393,8 +391,48 @@ static void leg_problems(const msfno_sht_plan_s* p, int R, int64_t ldT,
   }
 }
 
-int ensure_desc(msfno_sht_plan_s* p, int R, int other_ld, int64_t ldT) {
+// descriptor and image builds allocate and copy synchronously: refused while the
+// stream is being captured into a HIP graph (run the call once before capturing)
+static int require_not_capturing(hipStream_t s, const char* what) {
+  if (!s) return MSFNO_OK;
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(s, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone) {
+    set_error(std::string(what) + ": first use of this row count or table under HIP graph "
+              "capture; run the call once before capturing");
+    return MSFNO_EINVAL;
+  }
+  return MSFNO_OK;
+}
+
+// device copies of a descriptor list and its tile -> descriptor map
+static int upload_descs(const std::vector<GemmDesc>& d, int tiles, bool tile_map,
+                        msfno_sht_plan_s::DescSet* set) {
+  MSFNO_CHECK_HIP(hipMalloc(&set->d, std::max<size_t>(1, d.size()) * sizeof(GemmDesc)));
+  if (!d.empty())
+    MSFNO_CHECK_HIP(hipMemcpy(set->d, d.data(), d.size() * sizeof(GemmDesc), hipMemcpyHostToDevice));
+  if (tile_map) {
+    std::vector<int> t2d((size_t)std::max(tiles, 1), 0);
+    for (size_t i = 0; i < d.size(); ++i)
+      for (int t = 0; t < d[i].tiles_m * d[i].tiles_n; ++t) t2d[d[i].tile_start + t] = (int)i;
+    MSFNO_CHECK_HIP(hipMalloc(&set->tile, t2d.size() * sizeof(int)));
+    MSFNO_CHECK_HIP(hipMemcpy(set->tile, t2d.data(), t2d.size() * sizeof(int), hipMemcpyHostToDevice));
+  }
+  set->n = (int)d.size();
+  set->tiles = tiles;
+  return MSFNO_OK;
+}
+
+int ensure_desc(msfno_sht_plan_s* p, int R, int other_ld, int64_t ldT, hipStream_t s) {
   if (p->desc_R == R && p->d_desc) return MSFNO_OK;
+  auto hit = p->desc_sets.find(R);
+  if (hit != p->desc_sets.end()) {
+    p->d_desc = hit->second.d;
+    p->ndesc = hit->second.n;
+    p->desc_tiles = hit->second.tiles;
+    p->desc_R = R;
+    return MSFNO_OK;
+  }
+  MSFNO_TRY(require_not_capturing(s, "Legendre descriptors"));
   int bm, bn;
   gemm_tile_dims(leg_tile(p->inverse), &bm, &bn);
   std::vector<GemmDesc> d;
@@ -426,13 +464,12 @@ int ensure_desc(msfno_sht_plan_s* p, int R, int other_ld, int64_t ldT) {
     d.push_back(g);
   });
   (void)other_ld;
-  if (p->d_desc) MSFNO_CHECK_HIP(hipFree(p->d_desc));
-  p->d_desc = nullptr;
-  MSFNO_CHECK_HIP(hipMalloc(&p->d_desc, std::max<size_t>(1, d.size()) * sizeof(GemmDesc)));
-  if (!d.empty())
-    MSFNO_CHECK_HIP(hipMemcpy(p->d_desc, d.data(), d.size() * sizeof(GemmDesc), hipMemcpyHostToDevice));
-  p->ndesc = (int)d.size();
-  p->desc_tiles = tiles;
+  msfno_sht_plan_s::DescSet set;
+  MSFNO_TRY(upload_descs(d, tiles, false, &set));
+  p->desc_sets[R] = set;
+  p->d_desc = set.d;
+  p->ndesc = set.n;
+  p->desc_tiles = set.tiles;
   p->desc_R = R;
   return MSFNO_OK;
 }
@@ -462,8 +499,22 @@ static bool x3r_env() {
   return on;
 }
 
+static int build_tab3(msfno_sht_plan_s* p, int R, int64_t ldT, hipStream_t s);
+
 static int ensure_desc3(msfno_sht_plan_s* p, int R, int64_t ldT, hipStream_t s) {
   if (p->desc3_R == R && p->d_desc3 && p->tab3_valid) return MSFNO_OK;
+  auto hit = p->desc3_sets.find(R);
+  if (hit != p->desc3_sets.end()) {
+    p->d_desc3 = hit->second.d;
+    p->d_tile3 = hit->second.tile;
+    p->ndesc3 = hit->second.n;
+    p->desc3_tiles = hit->second.tiles;
+    p->desc3_res = hit->second.res;
+    p->desc3_R = R;
+    if (p->tab3_valid) return MSFNO_OK;
+  }
+  MSFNO_TRY(require_not_capturing(s, "x3h Legendre image"));
+  if (hit != p->desc3_sets.end()) return build_tab3(p, R, ldT, s);
   bool res = p->inverse && x3r_env();
   if (res)
     leg_problems(p, R, ldT, [&](GemmDesc g) {
@@ -486,21 +537,28 @@ static int ensure_desc3(msfno_sht_plan_s* p, int R, int64_t ldT, hipStream_t s) 
     tiles += g.tiles_m * g.tiles_n;
     d.push_back(g);
   });
-  if (p->d_desc3) MSFNO_CHECK_HIP(hipFree(p->d_desc3));
-  if (p->d_tile3) MSFNO_CHECK_HIP(hipFree(p->d_tile3));
-  p->d_desc3 = nullptr;
-  p->d_tile3 = nullptr;
-  MSFNO_CHECK_HIP(hipMalloc(&p->d_desc3, std::max<size_t>(1, d.size()) * sizeof(GemmDesc)));
-  if (!d.empty())
-    MSFNO_CHECK_HIP(hipMemcpy(p->d_desc3, d.data(), d.size() * sizeof(GemmDesc), hipMemcpyHostToDevice));
-  std::vector<int> t2d((size_t)std::max(tiles, 1), 0);
-  for (size_t i = 0; i < d.size(); ++i)
-    for (int t = 0; t < d[i].tiles_m * d[i].tiles_n; ++t) t2d[d[i].tile_start + t] = (int)i;
-  MSFNO_CHECK_HIP(hipMalloc(&p->d_tile3, t2d.size() * sizeof(int)));
-  MSFNO_CHECK_HIP(hipMemcpy(p->d_tile3, t2d.data(), t2d.size() * sizeof(int), hipMemcpyHostToDevice));
-  p->ndesc3 = (int)d.size();
-  p->desc3_tiles = tiles;
+  msfno_sht_plan_s::DescSet set;
+  MSFNO_TRY(upload_descs(d, tiles, true, &set));
+  set.res = p->desc3_res;
+  p->desc3_sets[R] = set;
+  p->d_desc3 = set.d;
+  p->d_tile3 = set.tile;
+  p->ndesc3 = set.n;
+  p->desc3_tiles = set.tiles;
   p->desc3_R = R;
+  (void)img;
+  (void)sc;
+  return build_tab3(p, R, ldT, s);
+}
+
+// the x3h table image and column scales (R-independent: every descriptor set gives the
+// same image offsets), rebuilt after a table load
+static int build_tab3(msfno_sht_plan_s* p, int R, int64_t ldT, hipStream_t s) {
+  int64_t img = 0, sc = 0;
+  leg_problems(p, R, ldT, [&](GemmDesc g) {
+    img += 2LL * g.N * round_up(std::max(g.K, 1), X3D_BK);
+    sc += g.N;
+  });
   if (!p->tab3_valid || img > p->tab3_elems || sc > p->tab3s_elems) {
     if (img > p->tab3_elems) {
       if (p->tab3) MSFNO_CHECK_HIP(hipFree(p->tab3));
@@ -542,6 +600,16 @@ bool x3f_usable(msfno_sht_plan_s* f) {
 static int ensure_desc3f(msfno_sht_plan_s* p, int R, int64_t ldT, hipStream_t s) {
   MSFNO_TRY(ensure_desc3(p, R, ldT, s));
   if (p->desc3f_R == R && p->d_desc3f) return MSFNO_OK;
+  auto hit = p->desc3f_sets.find(R);
+  if (hit != p->desc3f_sets.end()) {
+    p->d_desc3f = hit->second.d;
+    p->d_tile3f = hit->second.tile;
+    p->ndesc3f = hit->second.n;
+    p->desc3f_tiles = hit->second.tiles;
+    p->desc3f_R = R;
+    return MSFNO_OK;
+  }
+  MSFNO_TRY(require_not_capturing(s, "x3h forward Legendre descriptors"));
   std::vector<GemmDesc> d;
   int tiles = 0;
   int64_t img = 0, sc = 0;
@@ -557,20 +625,13 @@ static int ensure_desc3f(msfno_sht_plan_s* p, int R, int64_t ldT, hipStream_t s)
     tiles += g.tiles_m * g.tiles_n;
     d.push_back(g);
   });
-  if (p->d_desc3f) MSFNO_CHECK_HIP(hipFree(p->d_desc3f));
-  if (p->d_tile3f) MSFNO_CHECK_HIP(hipFree(p->d_tile3f));
-  p->d_desc3f = nullptr;
-  p->d_tile3f = nullptr;
-  MSFNO_CHECK_HIP(hipMalloc(&p->d_desc3f, std::max<size_t>(1, d.size()) * sizeof(GemmDesc)));
-  if (!d.empty())
-    MSFNO_CHECK_HIP(hipMemcpy(p->d_desc3f, d.data(), d.size() * sizeof(GemmDesc), hipMemcpyHostToDevice));
-  std::vector<int> t2d((size_t)std::max(tiles, 1), 0);
-  for (size_t i = 0; i < d.size(); ++i)
-    for (int t = 0; t < d[i].tiles_m * d[i].tiles_n; ++t) t2d[d[i].tile_start + t] = (int)i;
-  MSFNO_CHECK_HIP(hipMalloc(&p->d_tile3f, t2d.size() * sizeof(int)));
-  MSFNO_CHECK_HIP(hipMemcpy(p->d_tile3f, t2d.data(), t2d.size() * sizeof(int), hipMemcpyHostToDevice));
-  p->ndesc3f = (int)d.size();
-  p->desc3f_tiles = tiles;
+  msfno_sht_plan_s::DescSet set;
+  MSFNO_TRY(upload_descs(d, tiles, true, &set));
+  p->desc3f_sets[R] = set;
+  p->d_desc3f = set.d;
+  p->d_tile3f = set.tile;
+  p->ndesc3f = set.n;
+  p->desc3f_tiles = set.tiles;
   p->desc3f_R = R;
   return MSFNO_OK;
 }
@@ -653,7 +714,7 @@ int legendre_fwd(msfno_sht_plan_s* f, const float* Xt, float* S, int R, hipStrea
     return legendre_x3(Xt, f->tab3, f->tab3s, S, f->d_desc3, f->d_tile3, f->ndesc3,
                        f->desc3_tiles, x3d_bn(0), e, s);
   }
-  MSFNO_TRY(ensure_desc(f, R, 0, f->spec.ldT));
+  MSFNO_TRY(ensure_desc(f, R, 0, f->spec.ldT, s));
   GemmEpi e;
   e.rowscale = rowscale;
   e.rs_C = C;
@@ -679,7 +740,7 @@ int legendre_inv(msfno_sht_plan_s* g, const float* S, float* Yt, int R, hipStrea
     return legendre_x3(S, g->tab3, g->tab3s, Yt, g->d_desc3, g->d_tile3, g->ndesc3,
                        g->desc3_tiles, x3d_bn(1), e, s);
   }
-  MSFNO_TRY(ensure_desc(g, R, 0, g->spec.ldT));
+  MSFNO_TRY(ensure_desc(g, R, 0, g->spec.ldT, s));
   GemmEpi e;
   if (g->band_world) {  // Yt is the phase-1 send buffer: one block per destination rank
     e.segC_w = g->band_seg();
@@ -729,8 +790,12 @@ void carve_block(Carve& cv, BlockBufs& b, const msfno_block_desc* d,
       carve_spec_ws(cv, b.dw, d);
     }
   } else {
-    b.xt = cv.take<float>(BC * L.T * 2);
-    b.yt = cv.take<float>(BC * L.T * 2);
+    // one region for either form of the linear filter: the gathered copies xt, yt, or
+    // (batch 1, full plans: launch_contract_spec) the filter's output S in Sb
+    float* r = cv.take<float>(std::max<int64_t>(4 * BC * L.T, R * L.ldT));
+    b.xt = r;
+    b.yt = r + 2 * BC * L.T;
+    b.Sb = r;
   }
   b.Yt = cv.take<float>((int64_t)g->mmax * R * g->ldk);
   b.Yn = cv.take<float2>(BC * g->nlat * g->mmax);
@@ -1051,6 +1116,10 @@ int run_filter(const msfno_block_desc* d, msfno_sht_plan_s* f, msfno_sht_plan_s*
     }
   } else {
     MSFNO_REQUIRE(d->lin_w, MSFNO_EINVAL, "missing linear spectral weight");
+    if (contract_spec_ok(*f, d->lin_w, B)) {  // on S itself: Sa -> Sb (read by the inverse)
+      prof(ST_LIN_CONTRACT, s);
+      return launch_contract_spec(*f, b.Sa, d->lin_w, b.Sb, (int)C, s);
+    }
     prof(ST_LIN_GATHER, s);
     MSFNO_TRY(launch_spec_to_tril(*f, b.Sa, b.xt, B, (int)C, s));
     prof(ST_LIN_CONTRACT, s);
@@ -1119,7 +1188,9 @@ int run_spectral(const msfno_block_desc* d, msfno_sht_plan_s* f, msfno_sht_plan_
   MSFNO_TRY(run_filter(d, f, g, b, B, s));
   if (before_inv) MSFNO_TRY(before_inv());
   prof(ST_LEG_INV, s);
-  MSFNO_TRY(legendre_inv(g, b.Sa, b.Yt, (int)R, s));
+  // (the linear filter on S writes its output to Sb)
+  const bool lin_s = d->filter_type != MSFNO_FILTER_NONLINEAR && contract_spec_ok(*f, d->lin_w, B);
+  MSFNO_TRY(legendre_inv(g, lin_s ? b.Sb : b.Sa, b.Yt, (int)R, s));
   return MSFNO_OK;
 }
 
@@ -1221,6 +1292,28 @@ int plan_create(int nlat, int nlon, int lmax, int mmax, int inverse,
     e = hipMalloc(&p->d_tril_local, std::max<size_t>(loc.size(), 1) * sizeof(int));
     if (e == hipSuccess)
       e = hipMemcpy(p->d_tril_local, loc.data(), loc.size() * sizeof(int), hipMemcpyHostToDevice);
+  }
+  if (e == hipSuccess && !mask) {
+    const SpecLayout& L = p->spec;
+    std::vector<int> tcol;
+    tcol.reserve((size_t)L.T);
+    std::vector<char> used((size_t)L.Tp, 0);
+    for (int l = 0; l < lmax; ++l)
+      for (int m = 0; m <= std::min(l, mmax - 1); ++m) {
+        const int64_t t = L.col(m, l);
+        tcol.push_back((int)t);
+        used[(size_t)t] = 1;
+      }
+    std::vector<int> pad;
+    for (int64_t t = 0; t < L.Tp; ++t)
+      if (!used[(size_t)t]) pad.push_back((int)t);
+    p->npad = (int)pad.size();
+    e = hipMalloc(&p->d_tcol, std::max<size_t>(tcol.size(), 1) * sizeof(int));
+    if (e == hipSuccess)
+      e = hipMemcpy(p->d_tcol, tcol.data(), tcol.size() * sizeof(int), hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMalloc(&p->d_tpad, std::max<size_t>(pad.size(), 1) * sizeof(int));
+    if (e == hipSuccess && !pad.empty())
+      e = hipMemcpy(p->d_tpad, pad.data(), pad.size() * sizeof(int), hipMemcpyHostToDevice);
   }
   if (e != hipSuccess) {
     set_error(std::string("plan allocation failed: ") + hipGetErrorString(e));
@@ -1436,12 +1529,14 @@ int msfno_sht_plan_destroy(msfno_sht_plan_t p) {
   if (p->d_Lp) (void)hipFree(p->d_Lp);
   if (p->d_off) (void)hipFree(p->d_off);
   if (p->d_tril_local) (void)hipFree(p->d_tril_local);
+  if (p->d_tcol) (void)hipFree(p->d_tcol);
+  if (p->d_tpad) (void)hipFree(p->d_tpad);
   if (p->d_Lpe) (void)hipFree(p->d_Lpe);
-  if (p->d_desc) (void)hipFree(p->d_desc);
-  if (p->d_desc3) (void)hipFree(p->d_desc3);
-  if (p->d_desc3f) (void)hipFree(p->d_desc3f);
-  if (p->d_tile3f) (void)hipFree(p->d_tile3f);
-  if (p->d_tile3) (void)hipFree(p->d_tile3);
+  for (auto* sets : {&p->desc_sets, &p->desc3_sets, &p->desc3f_sets})
+    for (auto& kv : *sets) {
+      if (kv.second.d) (void)hipFree(kv.second.d);
+      if (kv.second.tile) (void)hipFree(kv.second.tile);
+    }
   if (p->tab3) (void)hipFree(p->tab3);
   if (p->tab3s) (void)hipFree(p->tab3s);
   if (p->d_kmap) (void)hipFree(p->d_kmap);
@@ -1486,7 +1581,18 @@ int msfno_sht_plan_load_table(msfno_sht_plan_t p, const float* table, void* stre
   }
   MSFNO_CHECK_HIP(hipMemcpy(p->d_tab_off, p->tab_off.data(), p->mmax * sizeof(int64_t),
                             hipMemcpyHostToDevice));
-  p->desc_R = -1;  // descriptors depend on the layout
+  // descriptors depend on the layout (symmetric or not): every cached set goes
+  MSFNO_CHECK_HIP(hipStreamSynchronize(s));
+  for (auto* sets : {&p->desc_sets, &p->desc3_sets, &p->desc3f_sets}) {
+    for (auto& kv : *sets) {
+      if (kv.second.d) MSFNO_CHECK_HIP(hipFree(kv.second.d));
+      if (kv.second.tile) MSFNO_CHECK_HIP(hipFree(kv.second.tile));
+    }
+    sets->clear();
+  }
+  p->d_desc = p->d_desc3 = p->d_desc3f = nullptr;
+  p->d_tile3 = p->d_tile3f = nullptr;
+  p->desc_R = -1;
   MSFNO_TRY(launch_relayout_table(*p, table, s));
   p->desc3_R = -1;
   p->desc3f_R = -1;
@@ -1628,7 +1734,7 @@ int msfno_block_forward(const msfno_block_desc* d, msfno_sht_plan_t f, msfno_sht
   // GEMM is forked after the forward FFT and stages B by LDS-DMA (gemm_x6p) instead
   // of splitting fp32 x in-kernel.
   float* x1 = b.x1;
-  SideCtx* side = nullptr;
+  std::shared_ptr<SideCtx> side;
   const bool xpl = skip_planes(d, f, b);
   const C2RPlanes xp{b.x1p, (int)C, f->nlat};
   // skip_h with per-pixel scales needs no norm0 statistics: forked at the block start

@@ -406,7 +406,7 @@ int msfno_band_block_stage(const msfno_block_desc* d, msfno_band_plan_t p, int s
   const bool xpl = skip_planes(d, p->fwd, b.fb);
   const int64_t Pl = (int64_t)p->rows_in * p->nlon_in;
   auto launch_skip = [&]() -> int {
-    SideCtx* side = nullptr;
+    std::shared_ptr<SideCtx> side;
     MSFNO_TRY(side_ctx(&side, s));
     hipStream_t ss = s;
     hipEvent_t join = side ? slot_event(p, io->slot) : nullptr;
@@ -497,7 +497,7 @@ int msfno_band_block_stage(const msfno_block_desc* d, msfno_band_plan_t p, int s
                                    p->mmax, p->mact, p->d_perm, s));
       const float* skip_src = nullptr;
       if (d->inner_skip == MSFNO_SKIP_LINEAR) {
-        SideCtx* side = nullptr;
+        std::shared_ptr<SideCtx> side;
         MSFNO_TRY(side_ctx(&side, s));
         if (side) {
           hipEvent_t join = slot_event(p, io->slot);

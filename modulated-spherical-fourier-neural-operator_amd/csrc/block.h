@@ -1,6 +1,7 @@
 // Internal block-orchestration helpers shared by api.cpp (single-GPU block)
 // and band.cpp (latitude-band sharded block).  Not part of the C-ABI.
 #pragma once
+#include <memory>
 #include "kernels.h"
 
 namespace msfno {
@@ -26,12 +27,21 @@ struct Carve {
   }
 };
 
-// per-device side stream for the inner-skip GEMM (fork/join through events)
+// per-device side stream for the inner-skip GEMM (fork/join through events).  Handed out
+// reference-counted: a context evicted from side_ctx's per-caller LRU map stays alive
+// (its events undestroyed) until the last call holding it has finished with it
 struct SideCtx {
-  hipStream_t side = nullptr;
+  hipStream_t side = nullptr;  // (pooled per device, never destroyed)
   hipEvent_t fork = nullptr, join = nullptr;
+  SideCtx() = default;
+  SideCtx(const SideCtx&) = delete;
+  SideCtx& operator=(const SideCtx&) = delete;
+  ~SideCtx() {
+    if (fork) (void)hipEventDestroy(fork);
+    if (join) (void)hipEventDestroy(join);
+  }
 };
-int side_ctx(SideCtx** out, hipStream_t caller);
+int side_ctx(std::shared_ptr<SideCtx>* out, hipStream_t caller);
 
 // split-A workspaces of the dense GEMMs (gemm_dense): one per call site, the
 // skip GEMM runs on the side stream concurrently with the spectral path
@@ -66,7 +76,7 @@ struct BlockBufs {
 void carve_block(Carve& cv, BlockBufs& b, const msfno_block_desc* d, const msfno_sht_plan_s* f,
                  const msfno_sht_plan_s* g, int B, bool with_norms);
 int check_pair(const msfno_block_desc* d, const msfno_sht_plan_s* f, const msfno_sht_plan_s* g);
-int ensure_desc(msfno_sht_plan_s* p, int R, int other_ld, int64_t ldT);
+int ensure_desc(msfno_sht_plan_s* p, int R, int other_ld, int64_t ldT, hipStream_t s = nullptr);
 int transpose_fwd_plan(const msfno_sht_plan_s* p, const float2* Xn, float* Xt, int B, int C,
                        const float* nscale, const float* nshift, hipStream_t s);
 int transpose_inv_plan(const msfno_sht_plan_s* p, const float* Yt, float2* Yn, int B, int C,

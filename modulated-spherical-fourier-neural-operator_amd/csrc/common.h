@@ -5,6 +5,7 @@
 #include <cstdint>
 #include <cstdio>
 #include <string>
+#include <map>
 #include <vector>
 
 #include "../../include/msfno.h"
@@ -290,6 +291,12 @@ struct msfno_sht_plan_s {
   // -1 for modes of other ranks; null for full plans.  lin_modes: the inverse map.
   int* d_tril_local = nullptr;
   std::vector<long long> lin_modes;
+  // full plans: S column of every tril mode n (torch.tril_indices order), and the S
+  // columns no mode maps to (block pads): the linear filter reads and writes S in place
+  // of a gathered copy (launch_contract_spec)
+  int* d_tcol = nullptr;
+  int* d_tpad = nullptr;
+  int npad = 0;
   int table_loaded = 0;
   // equatorial symmetry: the grid is symmetric (table[m][l][nlat-1-k] =
   // (-1)^(l-m) table[m][l][k], checked at load).  Then the Legendre GEMMs run
@@ -308,6 +315,15 @@ struct msfno_sht_plan_s {
   int ndesc = 0, desc_tiles = 0;
   // x3h Legendre (legendre_x3.hip): descriptor cache, the table image (two fp16
   // planes per problem, column-scaled) and the inverse column scales
+  // descriptor sets per row count R (the band pipeline's uneven sub-batches alternate
+  // R): built once each, freed with the plan; the fields below are the set of the
+  // last R used
+  struct DescSet {
+    msfno::GemmDesc* d = nullptr;
+    int* tile = nullptr;
+    int n = 0, tiles = 0, res = 0;
+  };
+  std::map<int, DescSet> desc_sets, desc3_sets, desc3f_sets;
   int desc3_R = -1;
   msfno::GemmDesc* d_desc3 = nullptr;
   int* d_tile3 = nullptr;  // tile -> descriptor index

@@ -589,7 +589,7 @@ __device__ __forceinline__ void quad_transpose(float (&v)[4], int qb) {
   }
 }
 
-// s_waitcnt vmcnt(n) for a run-time n in 0..63 (exact)
+// s_waitcnt vmcnt(n) for a run-time n in 0..63 (exact; vmcnt is six bits)
 __device__ __forceinline__ void wait_vmcnt_exact(int n) {
   switch (n) {
 #define HP_W_CASE(k) case k: asm volatile("s_waitcnt vmcnt(" #k ")" ::: "memory"); break;
@@ -597,8 +597,15 @@ __device__ __forceinline__ void wait_vmcnt_exact(int n) {
     HP_W_CASE(7) HP_W_CASE(8) HP_W_CASE(9) HP_W_CASE(10) HP_W_CASE(11) HP_W_CASE(12)
     HP_W_CASE(13) HP_W_CASE(14) HP_W_CASE(15) HP_W_CASE(16) HP_W_CASE(17) HP_W_CASE(18)
     HP_W_CASE(19) HP_W_CASE(20) HP_W_CASE(21) HP_W_CASE(22) HP_W_CASE(23) HP_W_CASE(24)
+    HP_W_CASE(25) HP_W_CASE(26) HP_W_CASE(27) HP_W_CASE(28) HP_W_CASE(29) HP_W_CASE(30)
+    HP_W_CASE(31) HP_W_CASE(32) HP_W_CASE(33) HP_W_CASE(34) HP_W_CASE(35) HP_W_CASE(36)
+    HP_W_CASE(37) HP_W_CASE(38) HP_W_CASE(39) HP_W_CASE(40) HP_W_CASE(41) HP_W_CASE(42)
+    HP_W_CASE(43) HP_W_CASE(44) HP_W_CASE(45) HP_W_CASE(46) HP_W_CASE(47) HP_W_CASE(48)
+    HP_W_CASE(49) HP_W_CASE(50) HP_W_CASE(51) HP_W_CASE(52) HP_W_CASE(53) HP_W_CASE(54)
+    HP_W_CASE(55) HP_W_CASE(56) HP_W_CASE(57) HP_W_CASE(58) HP_W_CASE(59) HP_W_CASE(60)
+    HP_W_CASE(61) HP_W_CASE(62) HP_W_CASE(63)
 #undef HP_W_CASE
-    default: asm volatile("s_waitcnt vmcnt(24)" ::: "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
   }
 }
 
@@ -981,14 +988,17 @@ __global__ __launch_bounds__(512, 1) void mlp_fused_hp_kernel(MlpHPParams p) {
         }
       }
     }
-    auto res_in = [&](auto o0_c) {  // residual rows -> accumulator layout, times s2 eta_b
+    // residual rows -> accumulator layout, times s2 eta_b: at the tile's first half-period
+    // only (a select: the accumulators of a second half-period pass through)
+    auto res_in = [&](auto o0_c) {
       constexpr int O0 = decltype(o0_c)::value;
 #pragma unroll
       for (int ot = O0; ot < O0 + 8; ++ot) {
         float v[4] = {oacc[ot][0], oacc[ot][1], oacc[ot][2], oacc[ot][3]};
         quad_transpose(v, qb);
 #pragma unroll
-        for (int i = 0; i < 4; ++i) oacc[ot][i] = v[i] * (s2s[16 * ot + 4 * g + i] * cur_etab);
+        for (int i = 0; i < 4; ++i)
+          oacc[ot][i] = first ? v[i] * (s2s[16 * ot + 4 * g + i] * cur_etab) : oacc[ot][i];
       }
     };
 
@@ -1319,6 +1329,212 @@ __global__ __launch_bounds__(256, 2) void skip_h_kernel(SkipHParams p) {
   }
 }
 
+// ---- weight-stationary inner skip (C = 256): skip_ws_kernel -----------------------------
+// One 512-thread workgroup per CU, persistent over 32-pixel chunks of x.  Wave w keeps
+// output rows 32 w .. 32 w + 31 of the field's weight image W' (skip_h's image: rs_c
+// W[c][k] / xs_k, two fp16 planes) as MFMA A fragments in registers (128 VGPRs), loaded
+// once per field, so the 256 x 256 weight never streams again: the kernel moves x in
+// and the skip out and nothing else (skip_h re-read the 256-KB image per 64 pixels:
+// 4 GB of L2 traffic at config 2).  Per chunk: x (256 channels x 32 pixels fp32, 32 KB)
+// arrives by LDS-DMA into one of three raw buffers (two chunks in flight), is scaled
+// per channel (xs) and split into the fp16x2 B fragments of one conversion buffer
+// ([pixel tile][k-step][plane][16 px][32 k], skip_h's swizzle), then 96 MFMAs per wave
+// and 16-B stores of the quad-transposed accumulators (x inv_rs + bias).
+constexpr int SW_PX = 32;                      // pixels per chunk
+constexpr int SW_RAW = MH_C * SW_PX * 4;       // 32 KB: fp32 [256][32]
+constexpr int SW_CONV = 2 * 8 * 2 * 16 * 64;   // 32 KB: fp16 [2][8][2][16][32]
+constexpr int SW_NRAW = 3;
+__device__ float4 sw_sink[64];
+
+struct SkipWSParams {
+  const float* x;
+  const float* xs;
+  float* out;
+  const unsigned short* img;  // [B][16 slices]
+  const float* inv_rs;        // [B][C]
+  const float* bias;          // [C] or null
+  int64_t P;
+  int chunks_per_field;
+  int nchunks;
+};
+
+__global__ __launch_bounds__(512, 1) void skip_ws_kernel(SkipWSParams p) {
+  __shared__ __attribute__((aligned(16))) char lds[SW_NRAW * SW_RAW + SW_CONV + 3 * MH_C * 4];
+  char* const conv = lds + SW_NRAW * SW_RAW;
+  float* const xs_s = reinterpret_cast<float*>(conv + SW_CONV);
+  float* const irs_s = xs_s + MH_C;
+  float* const bias_s = irs_s + MH_C;
+  const int tid = threadIdx.x;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  // lane-dependent values, re-laundered through an empty asm operand every chunk: hipcc
+  // would otherwise hoist every address of the loop body out of the chunk loop and spill
+  int lane = tid & 63;
+  int r16 = lane & 15, gq = lane >> 4, qb = lane & 3, qa = r16 >> 2;
+  const int64_t P = p.P;
+  const int64_t CP = (int64_t)MH_C * P;
+  // this workgroup's chunks [q0, q1)
+  const int G = gridDim.x;
+  const int q0 = (int)((int64_t)p.nchunks * blockIdx.x / G);
+  const int q1 = (int)((int64_t)p.nchunks * (blockIdx.x + 1) / G);
+  const int n = q1 - q0;
+  if (n <= 0) return;
+  const uint32_t raw_lds = lds_addr(lds);
+
+  // chunk q's x: piece pc (channels 8 pc .. + 7, 1 KB) from wave pc % 8; lane: channel
+  // 8 pc + (lane >> 3), pixels 4 (lane & 7) .. + 3 (clamped into the field)
+  auto issue = [&](int q, int buf) {
+    const int z = q / p.chunks_per_field;
+    int64_t px = (int64_t)(q - z * p.chunks_per_field) * SW_PX + 4 * (lane & 7);
+    if (px > P - 4) px = P - 4;
+    const float* base = p.x + (int64_t)z * CP + (int64_t)(lane >> 3) * P + px;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int pc = wave + 8 * j;
+      glds16(base + (int64_t)(8 * pc) * P, raw_lds + (uint32_t)(buf * SW_RAW + pc * 1024));
+    }
+  };
+  // the field's weight fragments: slice (wave, kh), [pl][ksl][t][r][32] (skip_h's image)
+  half8 A[8][2][2];  // [ks][t][pl]
+  int cur_z = -1;
+  auto load_field = [&](int z) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    for (int i = tid; i < MH_C; i += 512) {
+      xs_s[i] = p.xs[(int64_t)z * MH_C + i];
+      irs_s[i] = p.inv_rs[(int64_t)z * MH_C + i];
+      bias_s[i] = p.bias ? p.bias[i] : 0.f;
+    }
+    const unsigned short* img = p.img + (int64_t)z * SK_NSLICE * MH_SLICE;
+    const int a_lane = r16 * 32 + 8 * (gq ^ mh_swz(r16));
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks)
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int pl = 0; pl < 2; ++pl)
+          A[ks][t][pl] = *reinterpret_cast<const half8*>(
+              img + (int64_t)(2 * wave + (ks >> 2)) * MH_SLICE +
+              ((pl * 4 + (ks & 3)) * 2 + t) * 512 + a_lane);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  };
+
+  // prologue: chunks q0 .. q0 + 2 in flight
+#pragma unroll
+  for (int j = 0; j < SW_NRAW; ++j)
+    if (j < n) issue(q0 + j, j);
+
+  for (int i = 0; i < n; ++i) {
+    asm volatile("" : "+v"(lane), "+v"(r16), "+v"(gq), "+v"(qb), "+v"(qa));
+    const int h = lane >> 5, pt_c = (lane >> 4) & 1, r_c = lane & 15;
+    const int q = q0 + i;
+    const int z = q / p.chunks_per_field;
+    const int64_t px0 = (int64_t)(q - z * p.chunks_per_field) * SW_PX;
+    if (z != cur_z) {  // (uniform) new field: drains everything in flight, then reloads
+      load_field(z);
+      cur_z = z;
+    } else {
+      // chunk i's pieces landed: after them this wave issued the pieces of chunks i + 1,
+      // i + 2 (if any) and the stores of chunks i - 3 .. i - 1
+      const int cnt = 4 * ((i + 1 < n) + (i + 2 < n) + min(i, 3));
+      if (cnt >= 20) asm volatile("s_waitcnt vmcnt(20)" ::: "memory");
+      else if (cnt >= 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+      else if (cnt >= 12) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+      else if (cnt >= 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      else if (cnt >= 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      // every wave's pieces landed; the conversion buffer's last reads (MFMA of chunk
+      // i - 1) returned
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+    }
+    // ---- convert: wave w takes k-step ks = w; lane: pixel 16 pt + r, channel group
+    // g = 2 j + h (the two lane halves read rows of opposite parity: no bank conflict)
+    {
+      const float* raw = reinterpret_cast<const float*>(lds + (i % SW_NRAW) * SW_RAW);
+      const int pxl = 16 * pt_c + r_c;
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int g = 2 * j + h;
+        const int c0 = 32 * wave + 8 * g;
+        float tv[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) tv[e] = raw[(c0 + (e ^ h)) * SW_PX + pxl];
+        float xv[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) xv[e] = h ? tv[e ^ 1] : tv[e];
+        const float4 sa = *reinterpret_cast<const float4*>(xs_s + c0);
+        const float4 sb = *reinterpret_cast<const float4*>(xs_s + c0 + 4);
+        const float sv[8] = {sa.x, sa.y, sa.z, sa.w, sb.x, sb.y, sb.z, sb.w};
+        uint32_t t2[2][4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          split2h(sv[2 * e] * xv[2 * e], sv[2 * e + 1] * xv[2 * e + 1], t2[0][e], t2[1][e]);
+#pragma unroll
+        for (int pl = 0; pl < 2; ++pl)
+          *reinterpret_cast<uint4*>(conv + ((pt_c * 8 + wave) * 2 + pl) * 1024 + r_c * 64 +
+                                    16 * (g ^ mh_swz(r_c))) =
+              make_uint4(t2[pl][0], t2[pl][1], t2[pl][2], t2[pl][3]);
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    // the raw buffer of chunk i is free: chunk i + 3 into it
+    if (i + SW_NRAW < n) issue(q + SW_NRAW, i % SW_NRAW);
+    // ---- 96 MFMAs: rows 32 w + 16 t .., pixels 16 pt ..
+    floatx4 acc[2][2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int pt = 0; pt < 2; ++pt) acc[t][pt] = floatx4{0.f, 0.f, 0.f, 0.f};
+    // B fragments one k-step ahead (two sets live; a sched barrier per k-step keeps
+    // hipcc from hoisting all eight sets next to the 128 weight registers)
+    const char* cb = conv + r16 * 64 + 16 * (gq ^ mh_swz(r16));
+    auto ldb = [&](int ks, half8 (&b)[2][2]) {
+#pragma unroll
+      for (int pt = 0; pt < 2; ++pt)
+#pragma unroll
+        for (int pl = 0; pl < 2; ++pl)
+          b[pt][pl] = *reinterpret_cast<const half8*>(cb + ((pt * 8 + ks) * 2 + pl) * 1024);
+    };
+    half8 bb[2][2][2];
+    ldb(0, bb[0]);
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks) {
+      if (ks + 1 < 8) ldb(ks + 1, bb[(ks + 1) & 1]);
+      const half8 (&b)[2][2] = bb[ks & 1];
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int pt = 0; pt < 2; ++pt) {
+          acc[t][pt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A[ks][t][1], b[pt][0], acc[t][pt], 0, 0, 0);
+          acc[t][pt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A[ks][t][0], b[pt][1], acc[t][pt], 0, 0, 0);
+          acc[t][pt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A[ks][t][0], b[pt][0], acc[t][pt], 0, 0, 0);
+        }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    // ---- out = acc / rs_c + b_c: quad-transposed, 16-B stores (4 pixels of one row)
+    float* ob = p.out + (int64_t)z * CP;
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int pt = 0; pt < 2; ++pt) {
+        float v[4] = {acc[t][pt][0], acc[t][pt][1], acc[t][pt][2], acc[t][pt][3]};
+        quad_transpose(v, qb);
+        const int c = 32 * wave + 16 * t + 4 * gq + qb;
+        const float is = irs_s[c], bb = bias_s[c];
+        const int64_t px = px0 + 16 * pt + 4 * qa;
+        // (pixels past P go to a sink: every wave issues exactly 4 stores per chunk, the
+        // count the waits above assume)
+        float4* dst = px < P ? reinterpret_cast<float4*>(ob + (int64_t)c * P + px) : sw_sink + lane;
+        *dst = make_float4(fmaf(v[0], is, bb), fmaf(v[1], is, bb), fmaf(v[2], is, bb),
+                           fmaf(v[3], is, bb));
+      }
+    // (the chunk's stores stay in this iteration: the counted waits assume the order)
+    asm volatile("" ::: "memory");
+  }
+}
+
 __global__ void debug_cmp_kernel(const uint32_t* __restrict__ a, const uint32_t* __restrict__ b,
                                  int64_t n, unsigned long long* res) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
@@ -1372,6 +1588,24 @@ bool skip_h_env() {
   return on;
 }
 
+// MSFNO_SKIP_WS=0 keeps the per-tile skip_h kernel (A/B) instead of the weight-stationary one
+static bool skip_ws_env() {
+  static const bool on = [] {
+    const char* e = getenv("MSFNO_SKIP_WS");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
+static int device_cus() {
+  int dev = 0, cus = 0;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+      cus <= 0)
+    cus = 256;
+  return cus;
+}
+
 int launch_skip_h(const float* W, const float* xs, const float* x, float* out, const float* bias,
                   int B, int64_t P, void* ws, size_t ws_bytes, hipStream_t s) {
   MSFNO_REQUIRE(W && x && out && ws && B > 0 && P >= 1 && ws_bytes >= skip_h_workspace(B),
@@ -1390,6 +1624,18 @@ int launch_skip_h(const float* W, const float* xs, const float* x, float* out, c
   p.tiles_per_field = (int)cdiv(P, 64);
   const int64_t tiles = (int64_t)B * p.tiles_per_field;
   MSFNO_REQUIRE(tiles < (1LL << 31), MSFNO_EINVAL, "skip_h: grid too large");
+  if (xs && P % 4 == 0 && skip_ws_env()) {
+    SkipWSParams w{};
+    w.x = x; w.xs = xs; w.out = out; w.img = img; w.inv_rs = inv_rs; w.bias = bias; w.P = P;
+    w.chunks_per_field = (int)cdiv(P, SW_PX);
+    const int64_t nch = (int64_t)B * w.chunks_per_field;
+    MSFNO_REQUIRE(nch < (1LL << 31), MSFNO_EINVAL, "skip_ws: too many chunks");
+    w.nchunks = (int)nch;
+    static const int cus = device_cus();
+    const int grid = (int)std::min<int64_t>(cus, nch);
+    hipLaunchKernelGGL(skip_ws_kernel, dim3((unsigned)grid), dim3(512), 0, s, w);
+    return launch_check("skip_ws");
+  }
   if (xs)
     hipLaunchKernelGGL(skip_h_kernel<false>, dim3((unsigned)tiles), dim3(256), 0, s, p);
   else
@@ -1437,15 +1683,6 @@ static bool mh_persist_env() {
     return e && e[0] == '1';
   }();
   return on;
-}
-
-static int device_cus() {
-  int dev = 0, cus = 0;
-  if (hipGetDevice(&dev) != hipSuccess ||
-      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-      cus <= 0)
-    cus = 256;
-  return cus;
 }
 
 int launch_mlp_fused_h(const float* x1, const float* scale, const float* shift,

@@ -213,6 +213,11 @@ class FourierNeuralOperatorBlock(nn.Module):
             return None
         buf = getattr(self, "_wcache_buf", None)
         if buf is None or buf.device != device or buf.numel() < nbytes:
+            old_ev = getattr(self, "_wcache_event", None)
+            if buf is not None and old_ev is not None:
+                # the old buffer's last user may be another stream: the allocator must
+                # not hand its memory out before that stream's work is done
+                buf.record_stream(torch.cuda.ExternalStream(old_ev[0], device=buf.device))
             buf = self._wcache_buf = torch.empty(nbytes, dtype=torch.uint8, device=device)
             self._wcache_key = None
             self._wcache_event = None
