@@ -197,6 +197,9 @@ def parse(argv=None):
     ap.add_argument("--band-chunks", type=int, default=0,
                     help="latband: sub-batches pipelined so exchanges overlap compute "
                          "(0: one sub-batch per field, at most 4)")
+    ap.add_argument("--band-inner", default="shard", choices=["shard", "replicate"],
+                    help="--workload net, latband: shard every block, or replicate the inner "
+                         "(h, w) blocks on every rank after one all-gather (SURVEY 8(e))")
     ap.add_argument("--replicas-check", type=int, default=1,
                     help="latband, N>1: also time the replica mode (comm-free upper bound)")
     ap.add_argument("--linear-check", type=int, default=1,
@@ -389,7 +392,7 @@ def run_net(args, rank, world, dev, dist, backend):
         # network latitude-band sharded over the ranks (LatBandNet; strong scaling)
         from msfno_amd.sfno import LatBandNet, TorchComm
         shard = LatBandNet(net, rank, world, device=dev,
-                           comm=TorchComm() if dist else None)
+                           comm=TorchComm() if dist else None, inner=args.band_inner)
         g = torch.Generator(device=dev).manual_seed(0)
         x = shard.take(torch.randn(B, 73, args.nlat, args.nlon, generator=g, device=dev))
         film = 0.1 * torch.randn(B, 2, 1, args.C, generator=g, device=dev)
@@ -404,7 +407,9 @@ def run_net(args, rank, world, dev, dist, backend):
         if dist:
             torch.distributed.barrier()
 
-    use_graph = args.graph != 0 and not band  # collectives are not captured
+    # the sharded step is captured too when its exchanges run on RCCL (recorded into
+    # the graph); gloo collectives are host calls
+    use_graph = args.graph != 0 and (not band or (dist and backend == "nccl"))
     with torch.no_grad():
         for _ in range(max(args.warmup, 1)):
             y = run(x, film, 1.0)
@@ -413,11 +418,20 @@ def run_net(args, rank, world, dev, dist, backend):
             # one 6 h step as a HIP graph: removes the host cost of ~300 launches and
             # the per-call module bookkeeping (the 120x240 blocks are launch-bound)
             graph = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(graph):
-                y = net(x, film, 1.0)
-            graph.replay()
-            torch.cuda.synchronize()
+            try:
+                with torch.cuda.graph(graph):
+                    y = run(x, film, 1.0)
+                graph.replay()
+                torch.cuda.synchronize()
+            except RuntimeError as e:
+                if not band:
+                    raise
+                print(f"bench: sharded step not capturable ({e}); eager", file=sys.stderr)
+                use_graph = False
+                torch.cuda.synchronize()
+                y = run(x, film, 1.0)
 
+        if use_graph:
             def step():
                 graph.replay()
         else:
@@ -446,6 +460,18 @@ def run_net(args, rank, world, dev, dist, backend):
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         elapsed = t.item()
     assert torch.isfinite(y).all()
+    roof = None
+    if rank == 0 and not band:
+        # roofline of the step's dominant kernel: one more (untimed, eager) step with
+        # the stage profiler on (the graph replay above cannot be split into kernels)
+        from msfno_amd import _native as N
+        with torch.no_grad():
+            N.profile_collect()
+            N.profile_enable(True)
+            run(x, film, 1.0)
+            torch.cuda.synchronize()
+            N.profile_enable(False)
+            roof = net_roofline(N.profile_collect(), args, B)
     if rank == 0:
         print(json.dumps({
             "metric": "FourierNeuralOperatorNet_Filmed 6h steps/sec (12 blocks, 73 ch, 721x1440)",
@@ -455,13 +481,42 @@ def run_net(args, rank, world, dev, dist, backend):
             "ms_per_step": round(1000.0 * elapsed / args.steps, 3), "higher_is_better": True,
             "scaling": "strong" if band else "weak", "vs_baseline": None, "dtype": "f32",
             "data": "synthetic (x~N(0,1), FiLM modulation ~0.1 N(0,1), random-init weights)",
+            "roofline": roof,
             "config": {"workload": f"sfno_net12_filmed_{args.nlat}x{args.nlon}_C{args.C}_73ch",
                        "batch_per_gpu": B, "filter": args.filter, "hip_graph": use_graph,
+                       "band_inner": args.band_inner if band else None,
                        "parallelism": (f"latband{world}" if band else
                                        (f"replicas{world}" if world > 1 else "single"))}}),
               flush=True)
     if dist:
         torch.distributed.destroy_process_group()
+
+
+def net_roofline(stages, args, B):
+    """Config 3's dominant kernel: of the profiled stages whose work is known for the
+    network (the encoder + decoder fc1 / fc2 GEMMs, 73 -> 256 -> 256 and 329 -> 256 ->
+    73 at the full grid; the 12 block MLPs, 11 on the 120x240 grid and the last at the
+    full grid), the one with the most device time per step; work and time summed over
+    the step's launches of it."""
+    C, P = args.C, args.nlat * args.nlon
+    P_in = 120 * 240
+    work = {
+        "mlp_fc1": 2 * B * P * C * (73 + (C + 73)),
+        "mlp_fc2": 2 * B * P * C * (C + 73),
+        "mlp_fused": 4 * B * C * (2 * C) * (11 * P_in + P),
+    }
+    known = {k: v for k, v in stages.items() if k in work}
+    if not known:
+        return None
+    name, (ms, cnt) = max(known.items(), key=lambda kv: kv[1][0])
+    ach = work[name] / (ms / 1000.0) / 1e12
+    peak, engine = mfma_peak(name)
+    return {"bound": "mfma", "achieved": round(ach, 2), "peak": round(peak, 1),
+            "unit": "TFLOP/s", "frac": round(ach / peak, 4), "traffic": None,
+            "kernel": name, "engine": engine, "launches_per_step": cnt,
+            "ms_per_step": round(ms, 4), "work_per_step": f"{work[name] / 1e9:.1f} GFLOP",
+            "all_stages_ms": {k: round(v[0], 3) for k, v in
+                              sorted(stages.items(), key=lambda kv: -kv[1][0])[:8]}}
 
 
 def launch(args):
@@ -788,6 +843,7 @@ def main():
                                    f"{args.filter}_filmed",
                        "batch_per_gpu": args.batch, "global_batch": B if band else B * world,
                        "filter": args.filter,
+                       "band_inner": args.band_inner if band else None,
                        "parallelism": (f"latband{world}" if band else
                                        (f"replicas{world}" if world > 1 else "single"))},
             "ranks_seen": ranks_seen,

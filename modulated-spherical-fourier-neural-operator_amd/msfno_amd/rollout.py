@@ -141,14 +141,19 @@ class Rollout:
     ``means`` / ``stds`` broadcast against the (B, C, H, W) state (the
     reference's global statistics, model.py:190-204: per channel, so they apply to
     a rank's rows unchanged).  ``film`` is the FiLM modulation passed to Filmed
-    networks every step (or None).  A sharded network with more than one rank
-    steps eagerly (its exchanges are collectives; no graph capture)."""
+    networks every step (or None).  A sharded network with more than one rank is
+    captured too when its exchanges run on RCCL (a ``TorchComm`` over the nccl
+    backend: the collectives are recorded into the graph, model.py:327-331's
+    per-step cost without the host launches); over gloo (host collectives) it steps
+    eagerly, and a capture that fails falls back to eager stepping."""
 
     def __init__(self, model, means=None, stds=None, film=None, scale=1.0, graph=True):
         self.model = model
         self.means, self.stds = means, stds
         self.film, self.scale = film, scale
-        self.use_graph = graph and getattr(model, "world", 1) == 1
+        comm = getattr(model, "comm", None)
+        device_comm = comm is not None and not getattr(comm, "host", True)
+        self.use_graph = graph and (getattr(model, "world", 1) == 1 or device_comm)
         self._graph = None
 
     def normalise(self, data, reverse=False):
@@ -179,9 +184,17 @@ class Rollout:
         6 h steps starting from ``x0`` (raw fields unless ``normalised_input``)."""
         x = x0 if normalised_input else self.normalise(x0)
         x = x.contiguous()
-        if self.use_graph and x.is_cuda:
-            if self._graph is None or self._state.shape != x.shape:
+        if self.use_graph and x.is_cuda and (self._graph is None or self._state.shape != x.shape):
+            if getattr(self.model, "world", 1) == 1:
                 self._capture(x)
+            else:
+                try:
+                    self._capture(x)
+                except RuntimeError:  # (a collective the backend cannot record)
+                    self._graph = None
+                    self.use_graph = False
+                    torch.cuda.synchronize()
+        if self.use_graph and x.is_cuda:
             self._state.copy_(x)
             for i in range(steps):
                 self._graph.replay()

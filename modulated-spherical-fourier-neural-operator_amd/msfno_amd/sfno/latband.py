@@ -557,14 +557,39 @@ class LatBandNet:
     are this rank's rows of the full grid (``take`` / ``LatBandBlock.assemble``
     conventions); ``forward(x_local, sst, scale)`` returns its rows of the output."""
 
-    def __init__(self, net, rank: int, world: int, device=None, comm=None, chunks=1):
+    def __init__(self, net, rank: int, world: int, device=None, comm=None, chunks=1,
+                 inner="shard"):
+        """``inner``: "shard" (every block latitude-band sharded: four collectives per
+        block) or "replicate" (the first and last blocks, which carry the
+        full grid, stay sharded; the inner blocks run unsharded on every rank on the
+        whole (h, w) state, gathered once after block 0: one all-gather instead of four
+        collectives per inner block, at the price of computing the small inner blocks
+        on every rank)."""
+        if inner not in ("shard", "replicate"):
+            raise ValueError(f"inner must be 'shard' or 'replicate', not {inner!r}")
         self.net = net
         self.rank, self.world = rank, world
         self.comm = comm
         self.chunks = chunks
-        self.shards = [LatBandBlock(blk, rank, world, device=device) for blk in net.blocks]
-        for a, b in zip(self.shards, self.shards[1:]):
-            assert a.rows_out == b.rows, "block band partitions do not chain"
+        self.inner = inner
+        nb = len(net.blocks)
+        replicate = inner == "replicate" and nb > 2
+        self._replicate = replicate
+        sharded = [0, nb - 1] if replicate else list(range(nb))
+        self._shard_of = {i: LatBandBlock(net.blocks[i], rank, world, device=device)
+                          for i in sharded}
+        self.shards = [self._shard_of[i] for i in sharded]
+        if replicate:
+            first, last = self._shard_of[0], self._shard_of[nb - 1]
+            # every rank's rows of block 0's output grid (the gather's layout)
+            self._gather_rows = [local_rows(world, r, first.nlat_out, first.row_start_out)
+                                 for r in range(world)]
+            self._gather_nlat = first.nlat_out
+            self._gather_idx = {}
+            assert last.nlat == first.nlat_out, "inner blocks must keep block 0's output grid"
+        else:
+            for a, b in zip(self.shards, self.shards[1:]):
+                assert a.rows_out == b.rows, "block band partitions do not chain"
         self.rows = self.shards[0].rows
         self.rows_out = self.shards[-1].rows_out
         self.nlat_out = self.shards[-1].nlat_out
@@ -594,13 +619,41 @@ class LatBandNet:
         residual = x
         h = net.encoder.native_forward(x, addend=self._pos_local(x.device))
         h = net.pos_drop(h)  # sfnonet.py:674 / 827 (identity in eval)
-        for i, s in enumerate(self.shards):
+
+        def film_args(i):
             if filmed is not None and filmed(i):
                 k = i - (net.num_layers - net.film_layers)
-                h = yield from s.stages(h, gamma[:, k], beta[:, k], scale, slot=slot)
-            else:
-                h = yield from s.stages(h, slot=slot)
+                return (gamma[:, k], beta[:, k], scale)
+            return ()
+
+        if not self._replicate:
+            for i, s in enumerate(self.shards):
+                h = yield from s.stages(h, *film_args(i), slot=slot)
+            return net.decode(h, residual)
+        nb = len(net.blocks)
+        h = yield from self._shard_of[0].stages(h, *film_args(0), slot=slot)
+        h = yield from self._gather(h)
+        for i in range(1, nb - 1):  # sfnonet.py:838-844, unsharded on every rank
+            h = net.blocks[i](h, *film_args(i))
+        last = self._shard_of[nb - 1]
+        h = yield from last.stages(last.take(h), *film_args(nb - 1), slot=slot)
         return net.decode(h, residual)
+
+    def _gather(self, h):
+        """The whole (h, w) state from every rank's rows of it: the rows padded to the
+        largest band, one all-gather, placed by each rank's row list."""
+        B, C, n, W = h.shape
+        pad = max(len(r) for r in self._gather_rows)
+        buf = h.new_zeros(B, C, pad, W)
+        buf[:, :, :n].copy_(h)
+        parts = yield ("all_gather", buf)
+        full = h.new_empty(B, C, self._gather_nlat, W)
+        for r, rows in enumerate(self._gather_rows):
+            key = (r, str(h.device))
+            if key not in self._gather_idx:
+                self._gather_idx[key] = torch.tensor(rows, dtype=torch.long, device=h.device)
+            full.index_copy_(2, self._gather_idx[key], parts[r][:, :, :len(rows)])
+        return full
 
     def chunk_stages(self, x, sst=None, scale=1.0, chunks=1):
         """Generators of ``chunks`` sub-batches (fields are independent), each with its

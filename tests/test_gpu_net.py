@@ -74,12 +74,43 @@ def test_native_mlp_concat_and_broadcast_addend():
     assert (got - want).abs().max().item() < 1e-5 * max(1.0, want.abs().max().item())
 
 
-def _sharded_net(net, x, world, sst=None, scale=1.0):
+def _sharded_net(net, x, world, sst=None, scale=1.0, inner="shard"):
     from msfno_amd.sfno import LatBandBlock, LatBandNet, LocalGroup
-    shards = [LatBandNet(net, r, world) for r in range(world)]
+    shards = [LatBandNet(net, r, world, inner=inner) for r in range(world)]
     gens = [s.stages(s.take(x), sst, scale) for s in shards]
     outs = LocalGroup.run(gens)
     return LatBandBlock.assemble([s.shards[-1] for s in shards], outs)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("path", NET_FIXTURES, ids=lambda p: os.path.basename(p)[:-4])
+def test_latband_net_replicated_inner_blocks(path, world):
+    """LatBandNet(inner="replicate") (the first and last blocks sharded,
+    the inner blocks run unsharded on every rank after one all-gather of block 0's
+    output rows) against the reference network's output and the all-sharded form."""
+    meta, params, x, y, _ = load_net(path)
+    net = _build(meta, params)
+    x = x.to(DEV)
+    with torch.no_grad():
+        got = _sharded_net(net, x, world, inner="replicate").cpu()
+        sh = _sharded_net(net, x, world).cpu()
+    assert (got - y).abs().max().item() < 1e-4 * max(1.0, y.abs().max().item())
+    assert (got - sh).abs().max().item() < 2e-5 * max(1.0, y.abs().max().item())
+
+
+def test_latband_filmed_net_replicated_inner_blocks_matches_unsharded():
+    path = NET_FIXTURES[0]
+    meta, params, x, y, _ = load_net(path)
+    net = _build(meta, params, filmed=True, film_layers=2)
+    g = torch.Generator().manual_seed(5)
+    B, C = x.shape[0], meta["C"]
+    film = torch.stack((0.1 * torch.randn(B, 2, C, generator=g),
+                        0.1 * torch.randn(B, 2, C, generator=g)), dim=1).to(DEV)
+    x = x.to(DEV)
+    with torch.no_grad():
+        want = net(x, film, 0.8)
+        got = _sharded_net(net, x, 3, film, 0.8, inner="replicate")
+    assert (got - want).abs().max().item() < 2e-5 * max(1.0, want.abs().max().item())
 
 
 @pytest.mark.parametrize("world", [2, 3, 4])
