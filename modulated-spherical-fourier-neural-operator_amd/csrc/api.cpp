@@ -591,7 +591,9 @@ bool x3f_env() {
 }
 
 bool x3f_usable(msfno_sht_plan_s* f) {
-  if (!x3f_env() || !leg_x3_enabled() || !f->sym || f->band_world || f->inverse) return false;
+  if (!x3f_env() || !leg_x3_enabled() || !f->sym || f->inverse) return false;
+  if (f->band_world)  // the receive buffer, segmented by source rank (W % 8 == 0)
+    return f->band_W % 8 == 0 && f->band_K() <= X3F_KMAX;
   if (f->nslab != f->mmax) return false;
   return f->Ke <= X3F_KMAX && f->Ko <= X3F_KMAX && f->ldke % 8 == 0 && f->ldk % 8 == 0 &&
          std::max(f->ldke, f->ldk - f->ldke) <= cdiv(f->Ke, 64) * 64;
@@ -641,8 +643,10 @@ static int ensure_desc3f(msfno_sht_plan_s* p, int R, int64_t ldT, hipStream_t s)
 int legendre_fwd_x3f(msfno_sht_plan_s* f, const unsigned short* Xp, const float* isr, float* S,
                      int R, hipStream_t s) {
   MSFNO_TRY(ensure_desc3f(f, R, f->spec.ldT, s));
+  const int segw = f->band_world ? f->band_seg() : 0;
+  const int64_t segs = f->band_world ? (int64_t)f->nslab * R * 2 * f->band_W : 0;
   return legendre_x3f(Xp, isr, f->tab3, f->tab3s, S, f->d_desc3f, f->d_tile3f,
-                      f->ndesc3f, f->desc3f_tiles, s);
+                      f->ndesc3f, f->desc3f_tiles, s, segw, segs);
 }
 
 // spectral MLP: Gauss 3M complex GEMM by default (MSFNO_SPEC_4M=1: the real-ified

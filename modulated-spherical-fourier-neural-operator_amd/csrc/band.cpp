@@ -193,6 +193,13 @@ void carve_band(Carve& cv, BandBufs& b, const msfno_block_desc* d, const msfno_b
                  ? cv.take<unsigned short>(BC * 3 * std::max(Pin, Pout))
                  : nullptr;
   b.fb.xs = skip_x3(d) ? cv.take<float>((int64_t)B * d->C) : nullptr;
+  // forward Legendre on legendre_x3f: the exchange carries x3h pairs, the channel's
+  // sigma (stage 1) and 1 / sigma per slab row (read in stage 2)
+  b.fb.lsig = b.fb.isr = nullptr;
+  if (x3f_usable(p->fwd)) {
+    b.fb.lsig = cv.take<float>(BC);
+    b.fb.isr = cv.take<float>(R);
+  }
   carve_dense_ws(cv, b.fb.dw, d, B);
 }
 
@@ -465,15 +472,20 @@ int msfno_band_block_stage(const msfno_block_desc* d, msfno_band_plan_t p, int s
       prof(ST_NORM0, s);
       MSFNO_TRY(launch_chan_affine_parts(io->stats_all, p->world, B, (int)C, d->norm0_w,
                                          d->norm0_b, d->norm_eps, nullptr, nullptr, 0.f, b.sc0,
-                                         b.sh0, s, b.fb.xs));
+                                         b.sh0, s, b.fb.xs, nullptr, b.fb.lsig));
       if (b.fb.xs && d->inner_skip == MSFNO_SKIP_LINEAR) {
         MSFNO_REQUIRE(io->x && d->skip_w, MSFNO_EINVAL, "stage 1 needs x for the x3h skip");
         MSFNO_TRY(launch_skip());
       }
       prof(ST_BAND_PACK, s);
       const BandRows o = band_rows(p->nlat_in, p->row_in.data(), p->rank);
-      MSFNO_TRY(launch_band_pack(b.Xn, io->send, B, (int)C, band_geom(p->fwd, o, p->W_in),
-                                 p->mmax, b.sc0, b.sh0, p->d_perm, p->W_in, s));
+      if (b.fb.lsig)  // x3h pairs for legendre_x3f (every rank decides alike: plan geometry)
+        MSFNO_TRY(launch_band_pack_h(b.Xn, reinterpret_cast<unsigned short*>(io->send), B,
+                                     (int)C, band_geom(p->fwd, o, p->W_in), p->mmax, b.sc0,
+                                     b.sh0, b.fb.lsig, b.fb.isr, p->d_perm, p->W_in, s));
+      else
+        MSFNO_TRY(launch_band_pack(b.Xn, io->send, B, (int)C, band_geom(p->fwd, o, p->W_in),
+                                   p->mmax, b.sc0, b.sh0, p->d_perm, p->W_in, s));
       prof(ST_END, s);
       break;
     }
@@ -482,7 +494,11 @@ int msfno_band_block_stage(const msfno_block_desc* d, msfno_band_plan_t p, int s
       if (p->nm == 0) break;  // this rank owns no zonal wavenumber
       // the GEMMs read the phase-0 receive buffer and write the phase-1 send buffer
       prof(ST_LEG_FWD, s);
-      MSFNO_TRY(legendre_fwd(p->fwd, io->recv, b.fb.Sa, (int)R, s));
+      if (b.fb.isr)
+        MSFNO_TRY(legendre_fwd_x3f(p->fwd, reinterpret_cast<const unsigned short*>(io->recv),
+                                   b.fb.isr, b.fb.Sa, (int)R, s));
+      else
+        MSFNO_TRY(legendre_fwd(p->fwd, io->recv, b.fb.Sa, (int)R, s));
       MSFNO_TRY(run_filter(d, p->fwd, p->inv, b.fb, B, s));
       prof(ST_LEG_INV, s);
       MSFNO_TRY(legendre_inv(p->inv, b.fb.Sa, io->send, (int)R, s));

@@ -85,6 +85,9 @@ int legendre_fwd(msfno_sht_plan_s* f, const float* Xt, float* S, int R, hipStrea
                  const float* rowscale = nullptr, int C = 0);
 int legendre_inv(msfno_sht_plan_s* g, const float* S, float* Yt, int R, hipStream_t s);
 // spectral filter on S (f->spec layout) in b.Sa (in place)
+bool x3f_usable(msfno_sht_plan_s* f);
+int legendre_fwd_x3f(msfno_sht_plan_s* f, const unsigned short* Xp, const float* isr, float* S,
+                     int R, hipStream_t s);
 int run_filter(const msfno_block_desc* d, msfno_sht_plan_s* f, msfno_sht_plan_s* g,
                const BlockBufs& b, int B, hipStream_t s);
 bool use_fft_tile(const msfno_sht_plan_s* p);

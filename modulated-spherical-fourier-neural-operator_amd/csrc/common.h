@@ -199,7 +199,8 @@ int legendre_x3(const float* A, const unsigned short* img, const float* invs, fl
                 const GemmEpi& e, hipStream_t s);
 int legendre_x3f(const unsigned short* Ap, const float* isr,
                  const unsigned short* img, const float* invs, float* C, const GemmDesc* descs,
-                 const int* tile_desc, int ndesc, int tiles, hipStream_t s);
+                 const int* tile_desc, int ndesc, int tiles, hipStream_t s, int segA_w = 0,
+                 int64_t segA_stride = 0);
 int legendre_x3r(const float* A, const unsigned short* img, const float* invs, float* C,
                  const GemmDesc* descs, const int* tile_desc, int ndesc, int tiles,
                  const GemmEpi& e, hipStream_t s);

@@ -72,7 +72,8 @@ int launch_stats_partial(const float2* rowstats, int64_t np, int64_t cnt, int64_
 int launch_chan_affine_parts(const double* parts, int nparts, int B, int C, const float* w,
                              const float* b, float eps, const float* gamma, const float* beta,
                              float film_scale, float* scale, float* shift, hipStream_t s,
-                             float* xscale = nullptr, float* abound = nullptr);
+                             float* xscale = nullptr, float* abound = nullptr,
+                             float* lsig = nullptr);
 // the all-to-all buffers are the Legendre GEMMs' own operands: [p][slab][R][2W]
 // blocks (common.h msfno_sht_plan_s band fields).  g: the rank's local rows as a
 // small symmetric grid (Ke = its band, nh = the band rows that have a mirror row,
@@ -154,6 +155,9 @@ int launch_transpose_fwd_sym_h(const float2* Xn, unsigned short* Xp, int B, int 
                                const LatGeom& g, int mmax, const float* nscale,
                                const float* nshift, const float* lsig, float* isr,
                                hipStream_t s);
+int launch_band_pack_h(const float2* Xn, unsigned short* send, int B, int C, const LatGeom& g,
+                       int mmax, const float* nscale, const float* nshift, const float* lsig,
+                       float* isr, const int* perm, int W, hipStream_t s);
 // S layout <-> reference (bc, lmax, mmax) complex dense
 int launch_spec_to_ref(const msfno_sht_plan_s& p, const float* S, float2* out, int B, int C,
                        const int* d_off, hipStream_t s);

@@ -110,6 +110,10 @@ struct X3FParams {
   float* C;
   const GemmDesc* descs;
   const int* tile_desc;
+  // segmented A (latitude-band plans: the all-to-all receive buffer, one block per
+  // source rank): k -> k + (k / segA_w) (segA_stride - segA_w); segA_w % 8 == 0
+  int segA_w;
+  int64_t segA_stride;
 };
 
 constexpr int BM = X3D_BM, BK = X3D_BK;
@@ -555,7 +559,8 @@ __device__ __forceinline__ void x3f_body(const X3FParams& p, const GemmDesc& d, 
       if (i < NP) {
         const int pl = i & 1, ks = i >> 1;
         const int k = 32 * ks + 8 * kg;
-        glds16(rowp + 2 * (k < K ? k : 0) + 8 * pl, ring_lds + s * X3F_STAGE + i * 1024);
+        glds16(rowp + 2 * seg_k(k < K ? k : 0, p.segA_w, p.segA_stride) + 8 * pl,
+               ring_lds + s * X3F_STAGE + i * 1024);
       }
     }
   };
@@ -634,14 +639,18 @@ __global__ __launch_bounds__(256) void legendre_x3f_kernel(X3FParams p) {
 
 int legendre_x3f(const unsigned short* Ap, const float* isr,
                  const unsigned short* img, const float* invs, float* C, const GemmDesc* descs,
-                 const int* tile_desc, int ndesc, int tiles, hipStream_t s) {
+                 const int* tile_desc, int ndesc, int tiles, hipStream_t s, int segA_w,
+                 int64_t segA_stride) {
   if (ndesc <= 0 || tiles <= 0) return MSFNO_OK;
   MSFNO_REQUIRE(Ap && isr && img && invs && C && descs && tile_desc, MSFNO_EINVAL,
                 "legendre_x3f: null operand");
+  MSFNO_REQUIRE(segA_w % 8 == 0 && segA_w >= 0, MSFNO_EINVAL,
+                "legendre_x3f: segments must hold whole 8-k groups");
   X3FParams p{};
   p.Ap = Ap; p.isr = isr;
   p.img = img; p.invs = invs; p.C = C;
   p.descs = descs; p.tile_desc = tile_desc;
+  p.segA_w = segA_w; p.segA_stride = segA_stride;
   // MSFNO_X3F_NS=2: two LDS stages (49 KB, three workgroups per CU) instead of three
   static const int ns = [] {
     const char* e = getenv("MSFNO_X3F_NS");

@@ -356,7 +356,7 @@ template <int TKx, int TMx>
 __global__ __launch_bounds__(256) void transpose_fwd_sym4h_kernel(
     const float2* __restrict__ Xn, unsigned short* __restrict__ Xp, int B, int C,
     LatGeom g, int mmax, const float* __restrict__ nscale, const float* __restrict__ nshift,
-    const float* __restrict__ lsig, float* __restrict__ isr) {
+    const float* __restrict__ lsig, float* __restrict__ isr, const int* __restrict__ slab) {
   constexpr int LD = TKx + 4;
   __shared__ __attribute__((aligned(16))) float tile[4 * TMx * LD];  // [h][c][m][k]
   const int k0 = blockIdx.x * TKx, m0 = blockIdx.y * TMx;
@@ -396,6 +396,8 @@ __global__ __launch_bounds__(256) void transpose_fwd_sym4h_kernel(
     const int h = hc >> 1, ri = hc & 1;
     const int k = k0 + 8 * kv, m = m0 + mm;
     if (m >= mmax || k >= (h ? kend_a : kend_s)) continue;
+    const int sl = slab ? slab[m] : m;  // (band pack: the slab of m in the send order)
+    if (sl < 0) continue;
     const float4 v = *reinterpret_cast<const float4*>(tile + row * LD + 8 * kv);
     const float4 w = *reinterpret_cast<const float4*>(tile + row * LD + 8 * kv + 4);
     uint4 hi, lo;
@@ -404,7 +406,7 @@ __global__ __launch_bounds__(256) void transpose_fwd_sym4h_kernel(
     split_h2(w.x, w.y, hi.z, lo.z);
     split_h2(w.z, w.w, hi.w, lo.w);
     // interleaved planes: 8 k of the high plane, then the same 8 k of the low plane
-    unsigned short* dst = Xp + 2 * ((int64_t)m * R * g.ldk +
+    unsigned short* dst = Xp + 2 * ((int64_t)sl * R * g.ldk +
                                     ((int64_t)(b * 2 + ri) * C + c) * g.ldk + (h ? g.ldke : 0) + k);
     *reinterpret_cast<uint4*>(dst) = hi;
     *reinterpret_cast<uint4*>(dst + 8) = lo;
@@ -420,8 +422,24 @@ int launch_transpose_fwd_sym_h(const float2* Xn, unsigned short* Xp, int B, int 
     return MSFNO_EINVAL;
   dim3 grid((unsigned)cdiv(g.Ke, 64), (unsigned)cdiv(mmax, 32), (unsigned)(B * C));
   hipLaunchKernelGGL((transpose_fwd_sym4h_kernel<64, 32>), grid, dim3(256), 0, s, Xn, Xp, B, C,
-                     g, mmax, nscale, nshift, lsig, isr);
+                     g, mmax, nscale, nshift, lsig, isr, nullptr);
   return launch_check("transpose_fwd_sym_h");
+}
+
+// the latitude-band pack on x3h pairs (band.cpp stage 1, symmetric plans): this rank's
+// spectra -> the phase-0 send buffer as launch_band_pack lays it out (slab perm[m], rows
+// of 2W: [Xs | Xa], pads zero), each value as the two fp16 terms of
+// transpose_fwd_sym4h_kernel under the channel's sigma; 1 / sigma to isr (every row)
+int launch_band_pack_h(const float2* Xn, unsigned short* send, int B, int C, const LatGeom& g,
+                       int mmax, const float* nscale, const float* nshift, const float* lsig,
+                       float* isr, const int* perm, int W, hipStream_t s) {
+  MSFNO_REQUIRE(g.sym && nscale && nshift && lsig && isr && perm && W % 8 == 0 &&
+                    g.ldke == W && g.ldk == 2 * W,
+                MSFNO_EINVAL, "band_pack_h: symmetric band geometry with W % 8 == 0");
+  dim3 grid((unsigned)cdiv(std::max(g.Ke, W), 64), (unsigned)cdiv(mmax, 32), (unsigned)(B * C));
+  hipLaunchKernelGGL((transpose_fwd_sym4h_kernel<64, 32>), grid, dim3(256), 0, s, Xn, send, B, C,
+                     g, mmax, nscale, nshift, lsig, isr, perm);
+  return launch_check("band_pack_h");
 }
 
 template <int TKx, int TMx>
@@ -670,6 +688,20 @@ __device__ __forceinline__ float affine_bound(double sc, double sh, double mu, d
   return (float)fmin(b, 3.0e38);
 }
 
+// transpose_fwd_sym4h_kernel's sigma: |x^| <= |sc| sqrt(M2) + |sc mu + sh|, |X^_m| <= 2 pi
+// max |x^|, folded x 2; mapped into [2^14, 2^15)
+__device__ __forceinline__ float slab_sigma(double sc, double sh, double mu, double m2) {
+  const double bound = 2.0 * 6.283185307179586 * (fabs(sc) * sqrt(m2) + fabs(sc * mu + sh)) *
+                       (1.0 + 1e-3);
+  float sig = 1.f;
+  if (bound > 0.0 && bound < 1e300) {
+    int e;
+    frexp(bound, &e);
+    sig = (float)ldexp(1.0, min(max(15 - e, -100), 100));
+  }
+  return sig;
+}
+
 __global__ __launch_bounds__(256) void chan_affine_kernel(
     const float2* __restrict__ part, int64_t np, int64_t cnt, int64_t cnt_last, int C,
     const float* __restrict__ w, const float* __restrict__ bsh, float eps,
@@ -716,18 +748,7 @@ __global__ __launch_bounds__(256) void chan_affine_kernel(
     shift[bc] = (float)sh;
     if (xscale) xscale[bc] = x3_bound_scale(mu, sm2[0]);
     if (abound) abound[bc] = affine_bound(sc, sh, mu, sm2[0]);
-    if (lsig) {  // transpose_fwd_sym4h_kernel's sigma: |x^| <= |sc| sqrt(M2) + |sc mu + sh|,
-                 // |X^_m| <= 2 pi max |x^|, folded x 2
-      const double bound = 2.0 * 6.283185307179586 *
-                           (fabs(sc) * sqrt(sm2[0]) + fabs(sc * mu + sh)) * (1.0 + 1e-3);
-      float sig = 1.f;
-      if (bound > 0.0 && bound < 1e300) {
-        int e;
-        frexp(bound, &e);
-        sig = (float)ldexp(1.0, min(max(15 - e, -100), 100));
-      }
-      lsig[bc] = sig;
-    }
+    if (lsig) lsig[bc] = slab_sigma(sc, sh, mu, sm2[0]);
   }
 }
 
@@ -794,7 +815,8 @@ __global__ void chan_affine_parts_kernel(const double* __restrict__ parts, int n
                                          const float* __restrict__ gamma,
                                          const float* __restrict__ beta, float film_scale,
                                          float* __restrict__ scale, float* __restrict__ shift,
-                                         float* __restrict__ xscale, float* __restrict__ abound) {
+                                         float* __restrict__ xscale, float* __restrict__ abound,
+                                         float* __restrict__ lsig) {
   const int bc = blockIdx.x * blockDim.x + threadIdx.x;
   if (bc >= BC) return;
   const int c = bc % C;
@@ -816,16 +838,17 @@ __global__ void chan_affine_parts_kernel(const double* __restrict__ parts, int n
   shift[bc] = (float)sh;
   if (xscale) xscale[bc] = x3_bound_scale(acc.mean, acc.m2);
   if (abound) abound[bc] = affine_bound(sc, sh, acc.mean, acc.m2);
+  if (lsig) lsig[bc] = slab_sigma(sc, sh, acc.mean, acc.m2);
 }
 
 int launch_chan_affine_parts(const double* parts, int nparts, int B, int C, const float* w,
                              const float* b, float eps, const float* gamma, const float* beta,
                              float film_scale, float* scale, float* shift, hipStream_t s,
-                             float* xscale, float* abound) {
+                             float* xscale, float* abound, float* lsig) {
   const int BC = B * C;
   hipLaunchKernelGGL(chan_affine_parts_kernel, dim3((unsigned)cdiv(BC, 256)), dim3(256), 0, s,
                      parts, nparts, BC, C, w, b, eps, gamma, beta, film_scale, scale, shift,
-                     xscale, abound);
+                     xscale, abound, lsig);
   return launch_check("chan_affine_parts");
 }
 
