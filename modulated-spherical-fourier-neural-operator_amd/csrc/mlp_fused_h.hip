@@ -240,23 +240,6 @@ __device__ __forceinline__ void glds16x4(uint64_t sbase, const uint32_t (&voff)[
       : "memory", "scc");
 }
 
-// two pieces (as glds16x4): lane l copies 16 B from sbase + voff[i] to LDS byte
-// lds + i * LDS_STEP + 16 l, i = 0, 1
-template <int LDS_STEP>
-__device__ __forceinline__ void glds16x2(uint64_t sbase, const uint32_t (&voff)[4], uint32_t lds) {
-  unsigned keep;
-  sbase = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(sbase >> 32)) << 32) |
-          (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)sbase);
-  lds = (uint32_t)__builtin_amdgcn_readfirstlane((int)lds);
-  asm volatile(
-      "s_mov_b32 %0, m0\n\t"
-      "s_mov_b32 m0, %4\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %2, %1\n\t"
-      "s_add_u32 m0, m0, %5\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %3, %1\n\t"
-      "s_mov_b32 m0, %0"
-      : "=&s"(keep)
-      : "s"(sbase), "v"(voff[0]), "v"(voff[1]), "s"(lds), "i"(LDS_STEP)
-      : "memory", "scc");
-}
 
 // The block MLP for one tile of 64 pixels (4 waves of 16; two workgroups per CU).
 // Prologue: the weight slices 0..3 go in flight by LDS-DMA; the field's range scalars
@@ -507,64 +490,7 @@ __global__ __launch_bounds__(256, 2) void mlp_fused_h_kernel(MlpHParams p) {
   }
 }
 
-// ---- persistent two-phase form (mlp_fused_hp_kernel, MSFNO_MH_PERSIST=1) -----------------------
-// One 512-thread workgroup per CU, persistent over 64-pixel tiles.  Its two halves of four
-// waves (16 pixels each) consume ONE weight-slice stream through a four-slot LDS ring:
-// every 16-KB slice feeds 8 waves (half the L2 -> LDS traffic of two 4-wave workgroups).
-// The stream is periodic, 64 slices per period; each half-period (32 slices) runs fc1
-// and fc2 of eight hidden blocks, fc2 two blocks behind fc1, so a tile is any 64
-// consecutive slices that start at a half-period boundary.  Half A's tiles start at even
-// half-periods, half B's at odd ones: one half's memory work (the next tile's x1 staged
-// by LDS-DMA and rebuilt into fragments, the output stores, the residual loads) runs
-// beside the other half's MFMAs instead of every wave of the chip loading at once.
-//   - x1 of the next tile: 16 KB per wave, LDS-DMA'd into the wave's stage (shared with
-//     the other half's wave, whose use falls in the other half-periods) at steps 4..7 of
-//     the current tile's second half-period, rebuilt into fp16x2 fragments at 26..30
-//     (the current tile's last fc1 is at step 25);
-//   - output: at steps 0..3 of the next tile's first half-period, quad-transposed
-//     (4 pixels of one row per lane: 16-B stores); the residual of the new tile is loaded
-//     into the freed accumulators the same way and scaled in at steps 4, 5, ahead of the
-//     first fc2 (step 6): out = acc / (s2 eta_b) + b2 with acc started at resid s2 eta_b.
-constexpr int HP_W = 8;                  // waves per workgroup
-constexpr int HP_NS = 4;                 // ring slots (slices q + 1, q + 2 in flight)
-constexpr int HP_STG = 16 * 1024;        // one local wave's x1 stage: 256 rows x 16 px fp32
-constexpr int HP_SMALL = 3 * MH_C;       // per half: scale, shift, abound of the staged tile
-
-struct MlpHPParams {
-  const float* x1;
-  const float* scale;
-  const float* shift;
-  const float* abound;
-  const float* resid;
-  float* out;
-  const unsigned short* w1img;
-  const unsigned short* w2img;
-  const float* inv_s1;
-  const float* inv_s2;
-  const float* eta;
-  const float* b1;
-  const float* b2;
-  int64_t P;
-  int tiles_per_field;
-  int ntiles;
-};
-
-// stage row of channel c: the low two bits XOR bits 3..4, so the four lane groups of a
-// rebuild read (channels 8 g + e) fall in four different bank quarters (an involution)
-__device__ __forceinline__ int hp_row(int c) { return (c & ~3) | ((c ^ (c >> 3)) & 3); }
-
-// slice s (0..63) of the periodic stream: half-period b0 = 8 (s >> 5), pair pr = (s & 31) >> 1,
-// element e = s & 1 (kh / oh): pr 0: W1(b0); odd pr: W1(b0 + (pr + 1) / 2); even pr 2..14:
-// W2(b0 + pr / 2 - 1); 15: W2(b0 + 7)
-__device__ __forceinline__ const unsigned short* hp_slice_src(const unsigned short* w1img,
-                                                              const unsigned short* w2img, int s) {
-  const int b0 = (s >> 5) * 8, pr = (s & 31) >> 1, e = s & 1;
-  const bool w2 = pr > 0 && !(pr & 1);
-  const int j = pr == 15 ? 7 : (pr & 1) ? (pr + 1) >> 1 : (pr == 0 ? 0 : (pr >> 1) - 1);
-  const bool w2b = w2 || pr == 15;
-  return (w2b ? w2img : w1img) + (int64_t)(2 * (b0 + j) + e) * MH_SLICE;
-}
-
+// ---- quad-lane helpers (skip_ws_kernel's epilogue) ---------------------------------------
 __device__ __forceinline__ float dpp_xor1(float v) {
   return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v),
                                                                0xB1, 0xF, 0xF, false));
@@ -587,517 +513,6 @@ __device__ __forceinline__ void quad_transpose(float (&v)[4], int qb) {
     const float r0 = dpp_xor1(od ? v[0] : v[1]), r1 = dpp_xor1(od ? v[2] : v[3]);
     if (od) { v[0] = r0; v[2] = r1; } else { v[1] = r0; v[3] = r1; }
   }
-}
-
-// s_waitcnt vmcnt(n) for a run-time n in 0..63 (exact; vmcnt is six bits)
-__device__ __forceinline__ void wait_vmcnt_exact(int n) {
-  switch (n) {
-#define HP_W_CASE(k) case k: asm volatile("s_waitcnt vmcnt(" #k ")" ::: "memory"); break;
-    HP_W_CASE(0) HP_W_CASE(1) HP_W_CASE(2) HP_W_CASE(3) HP_W_CASE(4) HP_W_CASE(5) HP_W_CASE(6)
-    HP_W_CASE(7) HP_W_CASE(8) HP_W_CASE(9) HP_W_CASE(10) HP_W_CASE(11) HP_W_CASE(12)
-    HP_W_CASE(13) HP_W_CASE(14) HP_W_CASE(15) HP_W_CASE(16) HP_W_CASE(17) HP_W_CASE(18)
-    HP_W_CASE(19) HP_W_CASE(20) HP_W_CASE(21) HP_W_CASE(22) HP_W_CASE(23) HP_W_CASE(24)
-    HP_W_CASE(25) HP_W_CASE(26) HP_W_CASE(27) HP_W_CASE(28) HP_W_CASE(29) HP_W_CASE(30)
-    HP_W_CASE(31) HP_W_CASE(32) HP_W_CASE(33) HP_W_CASE(34) HP_W_CASE(35) HP_W_CASE(36)
-    HP_W_CASE(37) HP_W_CASE(38) HP_W_CASE(39) HP_W_CASE(40) HP_W_CASE(41) HP_W_CASE(42)
-    HP_W_CASE(43) HP_W_CASE(44) HP_W_CASE(45) HP_W_CASE(46) HP_W_CASE(47) HP_W_CASE(48)
-    HP_W_CASE(49) HP_W_CASE(50) HP_W_CASE(51) HP_W_CASE(52) HP_W_CASE(53) HP_W_CASE(54)
-    HP_W_CASE(55) HP_W_CASE(56) HP_W_CASE(57) HP_W_CASE(58) HP_W_CASE(59) HP_W_CASE(60)
-    HP_W_CASE(61) HP_W_CASE(62) HP_W_CASE(63)
-#undef HP_W_CASE
-    default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
-  }
-}
-
-template <int AHEAD>
-__global__ __launch_bounds__(512, 1) void mlp_fused_hp_kernel(MlpHPParams p) {
-  constexpr int NS = HP_NS;
-  constexpr int RING = NS * MH_SLICE * 2;  // bytes
-  __shared__ __attribute__((aligned(16)))
-  char lds[RING + 4 * HP_STG + 2 * HP_SMALL * 4 + (3 * MH_H + 3 * MH_C) * 4];
-  unsigned short* const ring = reinterpret_cast<unsigned short*>(lds);
-  char* const stage = lds + RING;
-  float* const small = reinterpret_cast<float*>(lds + RING + 4 * HP_STG);
-  float* const b1s = small + 2 * HP_SMALL;
-  float* const is1s = b1s + MH_H;
-  float* const ets = is1s + MH_H;
-  float* const b2s = ets + MH_H;
-  float* const is2s = b2s + MH_C;
-  float* const s2s = is2s + MH_C;
-
-  const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int half = wave >> 2, lw = wave & 3;  // (wave-uniform: SGPRs)
-  // lane-dependent values (re-laundered every half-period, see the loop)
-  int lane = tid & 63;
-  int r16 = lane & 15, g = lane >> 4, qb = lane & 3, qa = r16 >> 2;
-  const int64_t P = p.P;
-  const int64_t CP = (int64_t)MH_C * P;
-  const int G = gridDim.x;
-  // tiles: half h of workgroup b takes tiles 2 b + h + k 2G, k = 0 .. n_h - 1
-  const int base0 = 2 * blockIdx.x, base1 = base0 + 1;
-  const int n0 = base0 < p.ntiles ? (p.ntiles - 1 - base0) / (2 * G) + 1 : 0;
-  const int n1 = base1 < p.ntiles ? (p.ntiles - 1 - base1) / (2 * G) + 1 : 0;
-  if (n0 == 0 && n1 == 0) return;  // (never with the launcher's grid)
-  const int nh = half ? n1 : n0;
-  const int baseh = half ? base1 : base0;
-  // half-periods: the later half's last tile ends at 2 n_h + h; one more for its epilogue
-  const int HPE = max(2 * n0, 2 * n1 + 1) + 1;
-  // steps: every half-period but the last, whose start only stores the later half's last
-  // tile (the boundary block below)
-  const int Q = 32 * (HPE - 1);
-
-  for (int i = tid; i < MH_H; i += 512) {
-    b1s[i] = p.b1[i];
-    is1s[i] = p.inv_s1[i];
-    ets[i] = p.eta[i];
-  }
-  for (int i = tid; i < MH_C; i += 512) {
-    b2s[i] = p.b2 ? p.b2[i] : 0.f;
-    is2s[i] = p.inv_s2[i];
-    s2s[i] = 1.f / p.inv_s2[i];
-  }
-
-  // values every step derives its addresses from; re-laundered through empty asm operands
-  // at every half-period (below), so hipcc cannot hoist the 32 steps' addresses (64 slice
-  // sources, every fragment address) out of the loop and spill them
-  uint32_t ring_lds = (uint32_t)__builtin_amdgcn_readfirstlane((int)lds_addr(ring));
-  const unsigned short* w1i = p.w1img;
-  const unsigned short* w2i = p.w2img;
-  const int wave_u = __builtin_amdgcn_readfirstlane(wave);
-  uint32_t voff2[4] = {(uint32_t)(lane * 16), (uint32_t)(1024 + lane * 16), 0u, 0u};
-  auto issue_slice = [&](int qq) {
-    const uint64_t src = reinterpret_cast<uint64_t>(hp_slice_src(w1i, w2i, qq & 63)) + (uint64_t)wave_u * 2048;
-    glds16x2<1024>(src, voff2, ring_lds + (uint32_t)((qq % NS) * MH_SLICE * 2 + wave_u * 2048));
-  };
-  // tile t -> (field, first pixel)
-  auto tile_z = [&](int t) { return t / p.tiles_per_field; };
-  // (this wave's 16 pixels of the tile's 64)
-  auto tile_px = [&](int t) {
-    return (int64_t)(t - (t / p.tiles_per_field) * p.tiles_per_field) * 64 + 16 * lw;
-  };
-
-  // x1 of tile t, pieces i0 .. i0 + n - 1 of 16 (rows 16 i .. 16 i + 15 of the stage)
-  char* const my_stage = stage + lw * HP_STG;
-  const uint32_t my_stage_lds = lds_addr(my_stage);
-  auto stage_x1 = [&](int t, int i0, int n) {
-    const int z = tile_z(t);
-    const int64_t px0 = tile_px(t);
-    int64_t pc = px0 + 4 * (lane & 3);
-    if (pc >= P) pc = P - 4;
-    const float* base = p.x1 + (int64_t)z * CP + pc;
-    for (int i = i0; i < i0 + n; ++i) {
-      const int c = hp_row(16 * i + (lane >> 2));
-      glds16(base + (int64_t)c * P, my_stage_lds + (uint32_t)(i * 1024));
-    }
-  };
-  float* const my_small = small + half * HP_SMALL;
-  auto stage_small = [&](int t) {  // scale, shift, abound of tile t's field (one wave)
-    const int z = tile_z(t);
-    const uint32_t d = lds_addr(my_small);
-    glds16(p.scale + (int64_t)z * MH_C + lane * 4, d);
-    glds16(p.shift + (int64_t)z * MH_C + lane * 4, d + 1024);
-    glds16(p.abound + (int64_t)z * MH_C + lane * 4, d + 2048);
-  };
-
-  half8 xf[8][2];
-  floatx4 oacc[16];
-  floatx4 hacc[2][2];
-  uint32_t hfu[2][4];  // fc2 B fragment of the converted block [plane][pair]
-#pragma unroll
-  for (int a = 0; a < 2; ++a)
-#pragma unroll
-    for (int t = 0; t < 2; ++t) hacc[a][t] = floatx4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-  for (int ot = 0; ot < 16; ++ot) oacc[ot] = floatx4{0.f, 0.f, 0.f, 0.f};
-  // per-tile range scalars: the current tile's (conversions) and the staged one's
-  float cur_ixi = 1.f, cur_etab = 1.f, nxt_xi = 1.f, nxt_etab = 1.f;
-
-  auto rebuild_scalars = [&](bool dor) {
-    const float4 ab = *reinterpret_cast<const float4*>(my_small + 2 * MH_C + 4 * lane);
-    float m = fmaxf(fmaxf(ab.x, ab.y), fmaxf(ab.z, ab.w));
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
-    nxt_xi = dor ? pow2_below(m, 14) : nxt_xi;
-    nxt_etab = dor ? pow2_below(m + 1.f, 14) : nxt_etab;
-  };
-  auto rebuild_ks = [&](int ks, bool dor) {
-    const int c0 = 32 * ks + 8 * g;
-    const float4 sa = *reinterpret_cast<const float4*>(my_small + c0);
-    const float4 sb = *reinterpret_cast<const float4*>(my_small + c0 + 4);
-    const float4 ta = *reinterpret_cast<const float4*>(my_small + MH_C + c0);
-    const float4 tb = *reinterpret_cast<const float4*>(my_small + MH_C + c0 + 4);
-    const float xi = nxt_xi;
-    const float sv[8] = {sa.x * xi, sa.y * xi, sa.z * xi, sa.w * xi, sb.x * xi, sb.y * xi, sb.z * xi, sb.w * xi};
-    const float tv[8] = {ta.x * xi, ta.y * xi, ta.z * xi, ta.w * xi, tb.x * xi, tb.y * xi, tb.z * xi, tb.w * xi};
-    float xv[8];
-#pragma unroll
-    for (int e = 0; e < 8; ++e)
-      xv[e] = *reinterpret_cast<const float*>(my_stage + hp_row(c0 + e) * 64 + r16 * 4);
-    uint32_t t2[2][4];
-#pragma unroll
-    for (int e = 0; e < 4; ++e)
-      split2h(fmaf(sv[2 * e], xv[2 * e], tv[2 * e]), fmaf(sv[2 * e + 1], xv[2 * e + 1], tv[2 * e + 1]),
-              t2[0][e], t2[1][e]);
-#pragma unroll
-    for (int pl = 0; pl < 2; ++pl) {
-      const half8 nf = mh_frag(t2[pl][0], t2[pl][1], t2[pl][2], t2[pl][3]);
-      xf[ks][pl] = dor ? nf : xf[ks][pl];  // (a select: no branch, no phi of xf)
-    }
-  };
-
-  // ---- prologue: slices 0 .. NS - 2 in flight; half A stages and rebuilds its first tile
-#pragma unroll
-  for (int qq = 0; qq < NS - 1; ++qq)
-    if (qq < Q) issue_slice(qq);
-  if (half == 0 && n0 > 0) {
-    stage_x1(base0, 0, 16);
-    if (lw == 0) stage_small(base0);
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (half == 0 && n0 > 0) {
-    rebuild_scalars(true);
-#pragma unroll
-    for (int ks = 0; ks < 8; ++ks) rebuild_ks(ks, true);
-  }
-
-  int a_lane = r16 * 32 + 8 * (g ^ mh_swz(r16));
-  // vm operations this wave issued after its slice pieces in the last three steps, and
-  // its slice pieces of the last two (the counted wait of a step: everything the wave
-  // issued after the pieces of the slice it consumes)
-  int X1 = 0, X2 = 0, X3 = 0;
-  int PP1 = (Q > 2) ? 2 : 0, PP2 = (Q > 1) ? 2 : 0;
-
-  auto mfma3 = [](const half8 (&a)[2], const half8 (&b)[2], floatx4& c) {
-    c = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[1], b[0], c, 0, 0, 0);
-    c = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[0], b[1], c, 0, 0, 0);
-    c = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[0], b[0], c, 0, 0, 0);
-  };
-  // pair e2 (0..3) of hidden block j from hacc[HI] -> fc2 fragment hfu
-  auto conv_pair = [&](int j, int e2, auto hi_c) {
-    constexpr int HI = decltype(hi_c)::value;
-    const int t = e2 >> 1, i = 2 * (e2 & 1);
-    const int row = 32 * j + 16 * t + 4 * g + i;
-    const float2 b = *reinterpret_cast<const float2*>(b1s + row);
-    const float2 is = *reinterpret_cast<const float2*>(is1s + row);
-    const float2 hs = *reinterpret_cast<const float2*>(ets + row);
-    f32x2 v = {fmaf(hacc[HI][t][i], is.x * cur_ixi, b.x), fmaf(hacc[HI][t][i + 1], is.y * cur_ixi, b.y)};
-    v = gelu_erf2(v) * f32x2{hs.x * cur_etab, hs.y * cur_etab};
-    split2h(v.x, v.y, hfu[0][e2], hfu[1][e2]);
-  };
-  using I0 = std::integral_constant<int, 0>;
-  using I1 = std::integral_constant<int, 1>;
-  // fc1 of one slice (kh KH) into hacc[HA]; with CONV: block jc's pairs from hacc[HA ^ 1]
-  // -> hfu[FC] at u = 2, 6 (and hacc[HA ^ 1] zeroed after the kh = 1 slice)
-  auto fc1_step = [&](const unsigned short* slot, auto kh_c, auto ha_c, auto conv_c, int jc) {
-    constexpr int KH = decltype(kh_c)::value, HA = decltype(ha_c)::value;
-    constexpr bool CONV = decltype(conv_c)::value;
-    using HB = std::integral_constant<int, HA ^ 1>;
-    auto aoff = [&](int u, int pl) { return ((pl * 4 + (u >> 1)) * 2 + (u & 1)) * 512 + a_lane; };
-    half8 a[AHEAD + 1][2];
-#pragma unroll
-    for (int k = 0; k < AHEAD; ++k)
-#pragma unroll
-      for (int pl = 0; pl < 2; ++pl) a[k][pl] = *reinterpret_cast<const half8*>(slot + aoff(k, pl));
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      if (u + AHEAD < 8) {
-#pragma unroll
-        for (int pl = 0; pl < 2; ++pl)
-          a[(u + AHEAD) % (AHEAD + 1)][pl] = *reinterpret_cast<const half8*>(slot + aoff(u + AHEAD, pl));
-      }
-      mfma3(a[u % (AHEAD + 1)], xf[KH * 4 + (u >> 1)], hacc[HA][u & 1]);
-#ifndef HP_NO_CONV
-      if constexpr (CONV) {
-        if (u == 2 || u == 6) conv_pair(jc, 2 * KH + (u >> 2), HB{});
-      }
-#endif
-    }
-    if constexpr (CONV && KH == 1) {
-#pragma unroll
-      for (int t = 0; t < 2; ++t) hacc[HA ^ 1][t] = floatx4{0.f, 0.f, 0.f, 0.f};
-    }
-  };
-  // fc2 of one slice (oh OH) from hfu; with CONV (the last block of a half-period, after its
-  // fragment has been taken for this slice): block jc from hacc[1] -> hfu, hacc[1] zeroed
-  auto fc2_step = [&](const unsigned short* slot, auto oh_c, auto conv_c, int jc) {
-    constexpr int OH = decltype(oh_c)::value;
-    constexpr bool CONV = decltype(conv_c)::value;
-    auto aoff = [&](int u, int pl) { return (pl * 8 + u) * 512 + a_lane; };
-    const half8 hb[2] = {mh_frag(hfu[0][0], hfu[0][1], hfu[0][2], hfu[0][3]),
-                         mh_frag(hfu[1][0], hfu[1][1], hfu[1][2], hfu[1][3])};
-    half8 a[AHEAD + 1][2];
-#pragma unroll
-    for (int k = 0; k < AHEAD; ++k)
-#pragma unroll
-      for (int pl = 0; pl < 2; ++pl) a[k][pl] = *reinterpret_cast<const half8*>(slot + aoff(k, pl));
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      if (u + AHEAD < 8) {
-#pragma unroll
-        for (int pl = 0; pl < 2; ++pl)
-          a[(u + AHEAD) % (AHEAD + 1)][pl] = *reinterpret_cast<const half8*>(slot + aoff(u + AHEAD, pl));
-      }
-      mfma3(a[u % (AHEAD + 1)], hb, oacc[OH * 8 + u]);
-      if constexpr (CONV) {
-        if (u & 1) conv_pair(jc, u >> 1, I1{});
-      }
-    }
-    if constexpr (CONV) {
-#pragma unroll
-      for (int t = 0; t < 2; ++t) hacc[1][t] = floatx4{0.f, 0.f, 0.f, 0.f};
-    }
-  };
-
-  // tile bookkeeping of this half: the tile whose output is pending (epilogue)
-  int64_t prev_zoff = 0;  // z C P of the previous tile
-  int64_t prev_px0 = 0;
-  float prev_ietab = 1.f;
-  int q = 0;
-  for (int HPi = 0; HPi < HPE; ++HPi) {
-    const bool last_hp = HPi == HPE - 1;
-    {
-      uint32_t rl = ring_lds;
-      uint64_t w1v = reinterpret_cast<uint64_t>(w1i), w2v = reinterpret_cast<uint64_t>(w2i);
-      asm volatile("" : "+v"(a_lane), "+v"(voff2[0]), "+v"(voff2[1]), "+v"(rl), "+v"(w1v), "+v"(w2v),
-                   "+v"(lane), "+v"(r16), "+v"(g), "+v"(qb), "+v"(qa));
-      ring_lds = (uint32_t)__builtin_amdgcn_readfirstlane((int)rl);
-      w1i = reinterpret_cast<const unsigned short*>(
-          ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(w1v >> 32)) << 32) |
-          (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)w1v));
-      w2i = reinterpret_cast<const unsigned short*>(
-          ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(w2v >> 32)) << 32) |
-          (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)w2v));
-    }
-    const int rel = HPi - half;
-    const int k = rel >= 0 ? (rel >> 1) : -1;
-    const bool first = rel >= 0 && (rel & 1) == 0;
-    const bool cur = k >= 0 && k < nh;
-    const bool prev = first && k >= 1 && k - 1 < nh;
-    const bool load_res = first && cur;
-    const bool stage_next = !first && k + 1 < nh;
-    const int b0 = (HPi & 1) * 8;
-    const int tk = baseh + k * 2 * G;  // this tile (when cur)
-    if (first) {  // tile boundary: the staged tile becomes current
-      if (prev) prev_ietab = 1.f / cur_etab;
-      if (cur) {
-        cur_ixi = 1.f / nxt_xi;
-        cur_etab = nxt_etab;
-      }
-    }
-    const int64_t cur_px0 = cur ? tile_px(tk) : 0;
-    const int64_t cur_zoff = cur ? (int64_t)tile_z(tk) * CP : 0;
-    const int tn = baseh + (k + 1) * 2 * G;  // the next tile (staged in the second half)
-
-    // one step: counted wait + barrier, refill, extra vm work, then the slice's compute
-    auto step = [&](auto t_c, auto body) {
-      constexpr int T = decltype(t_c)::value;
-#ifdef HP_FIXED_WAIT
-      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-#else
-      wait_vmcnt_exact(X3 + PP2 + X2 + PP1 + X1);
-#endif
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      // (the slot offset laundered through an asm operand: q % NS is the same at every
-      // half-period, and hipcc would otherwise hoist every fragment address of the 32
-      // steps out of the half-period loop and spill)
-      int qs = (q % NS) * MH_SLICE;
-      asm volatile("" : "+s"(qs));
-      const unsigned short* slot = ring + qs;
-      int P0 = 0, X0 = 0;
-      if (q + NS - 1 < Q) {
-        issue_slice(q + NS - 1);
-        P0 = 2;
-      }
-      if constexpr (T >= 4 && T < 8) {
-        if (stage_next) {
-          stage_x1(tn, 4 * (T - 4), 4);
-          X0 += 4;
-          if (T == 4 && lw == 0) {
-            stage_small(tn);
-            X0 += 3;
-          }
-        }
-      }
-#ifdef HP_SCHED_BARRIER
-      __builtin_amdgcn_sched_barrier(0);
-#endif
-      body(slot);
-#ifdef HP_SCHED_BARRIER
-      __builtin_amdgcn_sched_barrier(0);
-#endif
-      X3 = X2; X2 = X1; X1 = X0;
-      PP2 = PP1; PP1 = P0;
-      ++q;
-    };
-
-    // tile boundary (first half-period, before its step 0): the previous tile's output
-    // (quad-transposed, 16-B buffer stores; pixels past P go to an out-of-range offset
-    // the buffer's range check drops), then the residual of this tile into the freed
-    // accumulators (buffer loads), scaled in at steps 4, 5.  Counted with the last step.
-    if (first && (prev || load_res)) {
-#ifndef HP_NO_STORE
-      if (prev) {
-        const uint64_t ob = reinterpret_cast<uint64_t>(p.out + prev_zoff);
-        const __amdgpu_buffer_rsrc_t rout = __builtin_amdgcn_make_buffer_rsrc(
-            reinterpret_cast<void*>(
-                ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(ob >> 32)) << 32) |
-                (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)ob)),
-            0, (int)(CP * 4), 0x00020000);
-        const bool okp = prev_px0 + 4 * qa < P;
-#pragma unroll
-        for (int ot = 0; ot < 16; ++ot) {
-          float v[4];
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const int row = 16 * ot + 4 * g + i;
-            v[i] = fmaf(oacc[ot][i], is2s[row] * prev_ietab, b2s[row]);
-          }
-          quad_transpose(v, qb);
-          const int rowb = 16 * ot + 4 * g + qb;
-          const uint32_t vo = okp ? (uint32_t)(((int64_t)rowb * P + prev_px0 + 4 * qa) * 4) : 0xFFFFFFF0u;
-          __builtin_amdgcn_raw_buffer_store_b128(
-              __builtin_bit_cast(__attribute__((ext_vector_type(4))) int,
-                                 make_float4(v[0], v[1], v[2], v[3])),
-              rout, (int)vo, 0, 0);
-        }
-        X1 += 16;
-      }
-#endif
-      {  // (every accumulator reassigned: the previous tile's values die at the stores)
-        if (load_res && p.resid) {
-          const uint64_t rb = reinterpret_cast<uint64_t>(p.resid + cur_zoff);
-          const __amdgpu_buffer_rsrc_t rres = __builtin_amdgcn_make_buffer_rsrc(
-              reinterpret_cast<void*>(
-                  ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(rb >> 32)) << 32) |
-                  (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)rb)),
-              0, (int)(CP * 4), 0x00020000);
-          const bool okc = cur_px0 + 4 * qa < P;
-#pragma unroll
-          for (int ot = 0; ot < 16; ++ot) {
-            const int rowb = 16 * ot + 4 * g + qb;
-            const uint32_t vo = okc ? (uint32_t)(((int64_t)rowb * P + cur_px0 + 4 * qa) * 4) : 0xFFFFFFF0u;
-            const auto r = __builtin_amdgcn_raw_buffer_load_b128(rres, (int)vo, 0, 0);
-            oacc[ot] = __builtin_bit_cast(floatx4, r);
-          }
-          X1 += 16;
-        } else {
-#pragma unroll
-          for (int ot = 0; ot < 16; ++ot) oacc[ot] = floatx4{0.f, 0.f, 0.f, 0.f};
-        }
-      }
-    }
-    // residual rows -> accumulator layout, times s2 eta_b: at the tile's first half-period
-    // only (a select: the accumulators of a second half-period pass through)
-    auto res_in = [&](auto o0_c) {
-      constexpr int O0 = decltype(o0_c)::value;
-#pragma unroll
-      for (int ot = O0; ot < O0 + 8; ++ot) {
-        float v[4] = {oacc[ot][0], oacc[ot][1], oacc[ot][2], oacc[ot][3]};
-        quad_transpose(v, qb);
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-          oacc[ot][i] = first ? v[i] * (s2s[16 * ot + 4 * g + i] * cur_etab) : oacc[ot][i];
-      }
-    };
-
-    using F = std::false_type;
-    using T = std::true_type;
-    // ---- the 32 steps of this half-period (pair pr, element e = kh / oh) ------------------
-    // pr 0: W1(b0) | 1: W1(b0+1), conv b0 | 2: W1(b0+2), conv b0+1 | 3: W2(b0)
-    // 4: W1(b0+3), conv b0+2 | 5: W2(b0+1) | 6: W1(b0+4), conv b0+3 | 7: W2(b0+2)
-    // 8: W1(b0+5), conv b0+4 | 9: W2(b0+3) | 10: W1(b0+6), conv b0+5 | 11: W2(b0+4)
-    // 12: W1(b0+7), conv b0+6 | 13: W2(b0+5) | 14: W2(b0+6), conv b0+7 | 15: W2(b0+7)
-    auto run_hp = [&](auto cur_c) {
-    auto w1 = [&](auto t_c, auto kh_c, auto ha_c, auto conv_c, int jc) {
-      step(t_c, [&](const unsigned short* slot) {
-        constexpr int TT = decltype(t_c)::value;
-#ifndef HP_NO_EPI
-        if constexpr (TT == 3) res_in(I0{});
-        if constexpr (TT == 4) res_in(std::integral_constant<int, 8>{});
-#endif
-#ifndef HP_NO_REBUILD
-        // (unconditional: without a staged tile the fragments are garbage and unused,
-        // and the previous fragments die here instead of living on in a phi)
-        if constexpr (TT == 28) rebuild_scalars(!first);
-        if constexpr (TT >= 28) {
-          rebuild_ks(2 * (TT - 28), !first);
-          rebuild_ks(2 * (TT - 28) + 1, !first);
-        }
-#endif
-        if constexpr (decltype(cur_c)::value) fc1_step(slot, kh_c, ha_c, conv_c, jc);
-      });
-    };
-    auto w2 = [&](auto t_c, auto oh_c, auto conv_c, int jc) {
-      step(t_c, [&](const unsigned short* slot) {
-        constexpr int TT = decltype(t_c)::value;
-#ifndef HP_NO_EPI
-        if constexpr (TT == 3) res_in(I0{});
-        if constexpr (TT == 4) res_in(std::integral_constant<int, 8>{});
-#endif
-#ifndef HP_NO_REBUILD
-        // (unconditional: without a staged tile the fragments are garbage and unused,
-        // and the previous fragments die here instead of living on in a phi)
-        if constexpr (TT == 28) rebuild_scalars(!first);
-        if constexpr (TT >= 28) {
-          rebuild_ks(2 * (TT - 28), !first);
-          rebuild_ks(2 * (TT - 28) + 1, !first);
-        }
-#endif
-        if constexpr (decltype(cur_c)::value) fc2_step(slot, oh_c, conv_c, jc);
-      });
-    };
-#define HP_C(n) std::integral_constant<int, n>{}
-    w1(HP_C(0), I0{}, I0{}, F{}, 0);
-    w1(HP_C(1), I1{}, I0{}, F{}, 0);
-    w1(HP_C(2), I0{}, I1{}, T{}, b0 + 0);
-    w1(HP_C(3), I1{}, I1{}, T{}, b0 + 0);
-    w2(HP_C(4), I0{}, F{}, 0);
-    w2(HP_C(5), I1{}, F{}, 0);
-    w1(HP_C(6), I0{}, I0{}, T{}, b0 + 1);
-    w1(HP_C(7), I1{}, I0{}, T{}, b0 + 1);
-    w2(HP_C(8), I0{}, F{}, 0);
-    w2(HP_C(9), I1{}, F{}, 0);
-    w1(HP_C(10), I0{}, I1{}, T{}, b0 + 2);
-    w1(HP_C(11), I1{}, I1{}, T{}, b0 + 2);
-    w2(HP_C(12), I0{}, F{}, 0);
-    w2(HP_C(13), I1{}, F{}, 0);
-    w1(HP_C(14), I0{}, I0{}, T{}, b0 + 3);
-    w1(HP_C(15), I1{}, I0{}, T{}, b0 + 3);
-    w2(HP_C(16), I0{}, F{}, 0);
-    w2(HP_C(17), I1{}, F{}, 0);
-    w1(HP_C(18), I0{}, I1{}, T{}, b0 + 4);
-    w1(HP_C(19), I1{}, I1{}, T{}, b0 + 4);
-    w2(HP_C(20), I0{}, F{}, 0);
-    w2(HP_C(21), I1{}, F{}, 0);
-    w1(HP_C(22), I0{}, I0{}, T{}, b0 + 5);
-    w1(HP_C(23), I1{}, I0{}, T{}, b0 + 5);
-    w2(HP_C(24), I0{}, F{}, 0);
-    w2(HP_C(25), I1{}, F{}, 0);
-    w1(HP_C(26), I0{}, I1{}, T{}, b0 + 6);
-    w1(HP_C(27), I1{}, I1{}, T{}, b0 + 6);
-    w2(HP_C(28), I0{}, F{}, 0);
-    w2(HP_C(29), I1{}, T{}, b0 + 7);
-    w2(HP_C(30), I0{}, F{}, 0);
-    w2(HP_C(31), I1{}, F{}, 0);
-    };  // run_hp
-    if (last_hp) break;
-#ifdef HP_SPLIT_CUR
-    if (cur) run_hp(T{}); else run_hp(F{});
-#else
-    run_hp(T{});  // (an idle half computes on stale registers; nothing of it is stored)
-#endif
-#undef HP_C
-    if (first && cur) {  // the epilogue of this tile runs at the start of its next-but-one half
-      prev_zoff = cur_zoff;
-      prev_px0 = cur_px0;
-    }
-  }
-#ifdef HP_SINK
-  for (int ot = 0; ot < 16; ++ot)
-    for (int i = 0; i < 4; ++i) p.out[ot * 1024 + i * 256 + tid] = oacc[ot][i];
-#endif
 }
 
 // ---- inner skip (1x1 conv, C = 256) on the same tiling: out = Ws·x + bs -------------
@@ -1588,13 +1003,13 @@ bool skip_h_env() {
   return on;
 }
 
-// MSFNO_SKIP_WS=0 keeps the per-tile skip_h kernel (A/B) instead of the weight-stationary one
+// MSFNO_SKIP_WS=1: the weight-stationary skip_ws_kernel instead of the per-tile skip_h.
+// Opt-in: bitwise equal, but in-block with the side stream its one 134-KB workgroup per CU
+// keeps the forward Legendre (legendre_x3f) from co-residing: legendre_fwd 0.66 -> 1.01 ms,
+// 159.6 -> 155.7 fields/s (profiles/r04_v4)
 static bool skip_ws_env() {
-  static const bool on = [] {
-    const char* e = getenv("MSFNO_SKIP_WS");
-    return !(e && e[0] == '0');
-  }();
-  return on;
+  const char* e = getenv("MSFNO_SKIP_WS");
+  return e && e[0] == '1';
 }
 
 static int device_cus() {
@@ -1675,43 +1090,10 @@ int launch_mlp_fused_h_images(const float* W1, const float* b1, const float* W2,
   return launch_check("mh_invert");
 }
 
-// MSFNO_MH_PERSIST=1: the persistent two-phase kernel (mlp_fused_hp_kernel) instead of
-// one workgroup per 64-pixel tile (mlp_fused_h_kernel, the default)
-static bool mh_persist_env() {
-  static const bool on = [] {
-    const char* e = getenv("MSFNO_MH_PERSIST");
-    return e && e[0] == '1';
-  }();
-  return on;
-}
-
 int launch_mlp_fused_h(const float* x1, const float* scale, const float* shift,
                        const float* abound, const float* resid, float* out,
                        const unsigned short* img, const float* b1, const float* b2, int B,
                        int64_t P, hipStream_t s) {
-  // (16-B pixel groups: P a multiple of 4, and 32-bit buffer offsets; otherwise the
-  // per-tile kernel)
-  if (mh_persist_env() && P % 4 == 0 && (int64_t)MH_C * P * 4 < (1LL << 31)) {
-    MSFNO_REQUIRE(x1 && scale && shift && abound && out && img && b1 && B > 0 && P >= 4,
-                  MSFNO_EINVAL, "mlp_fused_hp: bad arguments");
-    MlpHPParams p{};
-    p.x1 = x1; p.scale = scale; p.shift = shift; p.abound = abound; p.resid = resid; p.out = out;
-    p.w1img = img;
-    p.w2img = img + (int64_t)MH_HB * 2 * MH_SLICE;
-    const float* sc = reinterpret_cast<const float*>(img + MH_IMG_ELEMS);
-    p.inv_s1 = sc;
-    p.inv_s2 = sc + MH_H;
-    p.eta = sc + MH_H + MH_C;
-    p.b1 = b1; p.b2 = b2; p.P = P;
-    p.tiles_per_field = (int)cdiv(P, 64);
-    const int64_t tiles = (int64_t)B * p.tiles_per_field;
-    MSFNO_REQUIRE(tiles < (1LL << 30), MSFNO_EINVAL, "mlp_fused_hp: grid too large");
-    p.ntiles = (int)tiles;
-    static const int cus = device_cus();
-    const int grid = (int)std::min<int64_t>(cus, cdiv(tiles, 2));
-    hipLaunchKernelGGL(mlp_fused_hp_kernel<0>, dim3((unsigned)grid), dim3(512), 0, s, p);
-    return launch_check("mlp_fused_hp");
-  }
   MSFNO_REQUIRE(x1 && scale && shift && abound && out && img && b1 && B > 0 && P >= 1,
                 MSFNO_EINVAL, "mlp_fused_h: bad arguments");
   MlpHParams p{};

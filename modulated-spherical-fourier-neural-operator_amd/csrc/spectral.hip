@@ -1230,9 +1230,113 @@ __global__ void tril_to_spec_kernel(const float* __restrict__ yt, float* __restr
   }
 }
 
+// the S columns no mode maps to, zeroed in every row of the output S
+__global__ void zero_spec_pads_kernel(float* __restrict__ Y, const int* __restrict__ tpad,
+                                      int npad, int rows, int64_t ldT) {
+  const int64_t n = (int64_t)rows * npad;
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < n;
+       e += (int64_t)gridDim.x * blockDim.x)
+    Y[(e / npad) * ldT + tpad[e % npad]] = 0.f;
+}
+
+// Tiled form of the two re-layouts for full plans: the (l, m) triangle in tiles of
+// 64 l x 16 m through LDS, so both sides move whole runs (S: per m the even and odd
+// j = l - m of the tile, 32 contiguous floats each in the Re and in the Im row; tril:
+// per l the tile's 16 m, 128 contiguous bytes).  The scattered 8-B writes of the
+// per-element kernels above cost 0.38 / 0.17 ms at config 2 for 0.27 GB.
+constexpr int TT_L = 64, TT_M = 16;
+
+template <bool TO_TRIL>
+__global__ __launch_bounds__(256) void spec_tril_tiled_kernel(
+    const float* __restrict__ S, float* __restrict__ Sout, const float2* __restrict__ tin,
+    float2* __restrict__ tout, int C, int lmax, int mmax, int64_t T, int64_t ldT,
+    const int* __restrict__ off, const int* __restrict__ Lpe) {
+  __shared__ float2 tile[TT_L][TT_M + 1];
+  const int l0 = blockIdx.x * TT_L, m0 = blockIdx.y * TT_M;
+  const int64_t bc = blockIdx.z;
+  const int b = (int)(bc / C), c = (int)(bc - (int64_t)b * C);
+  if (m0 > l0 + TT_L - 1 || m0 >= mmax || l0 >= lmax) return;
+  const int tid = threadIdx.x;
+  const int64_t rre = ((int64_t)(b * 2 + 0) * C + c) * ldT;
+  const int64_t rim = ((int64_t)(b * 2 + 1) * C + c) * ldT;
+  // S side: thread (ml = tid >> 4, q = tid & 15): m = m0 + ml; for each parity the
+  // j = l - m of the tile's l range are a run of 32 (u = j >> 1 consecutive)
+  auto s_side = [&](auto store_c) {
+    constexpr bool STORE = decltype(store_c)::value;
+    const int ml = tid >> 4, q = tid & 15;
+    const int m = m0 + ml;
+    if (m >= mmax || m >= lmax) return;
+    const int lpe = Lpe[m];
+    const int64_t base = off[m];
+#pragma unroll
+    for (int par = 0; par < 2; ++par) {
+      // first j >= l0 - m of this parity (j >= 0)
+      int j0 = max(l0 - m, 0);
+      if ((j0 & 1) != par) ++j0;
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        const int j = j0 + 2 * (q + 16 * k);
+        const int l = m + j;
+        if (l >= l0 + TT_L || l >= lmax) continue;
+        const int64_t t = base + (par ? lpe : 0) + (j >> 1);
+        if constexpr (STORE) {
+          const float2 v = tile[l - l0][ml];
+          Sout[rre + t] = v.x;
+          Sout[rim + t] = v.y;
+        } else {
+          tile[l - l0][ml] = make_float2(S[rre + t], S[rim + t]);
+        }
+      }
+    }
+  };
+  // tril side: thread (ll = tid >> 2, mq = tid & 3): l = l0 + ll, m = m0 + 4 mq .. + 3
+  auto t_side = [&](auto store_c) {
+    constexpr bool STORE = decltype(store_c)::value;
+    const int ll = tid >> 2, mq = tid & 3;
+    const int l = l0 + ll;
+    if (l >= lmax) return;
+    const int64_t row = (l <= mmax) ? (int64_t)l * (l + 1) / 2
+                                    : (int64_t)mmax * (mmax + 1) / 2 + (int64_t)(l - mmax) * mmax;
+    const int mend = min(l + 1, mmax);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int m = m0 + 4 * mq + e;
+      if (m >= mend) continue;
+      if constexpr (STORE)
+        tout[bc * T + row + m] = tile[ll][4 * mq + e];
+      else
+        tile[ll][4 * mq + e] = tin[bc * T + row + m];
+    }
+  };
+  using F = std::false_type;
+  using Tt = std::true_type;
+  if constexpr (TO_TRIL) {
+    s_side(F{});
+    __syncthreads();
+    t_side(Tt{});
+  } else {
+    t_side(F{});
+    __syncthreads();
+    s_side(Tt{});
+  }
+}
+
+static bool tril_tiled(const msfno_sht_plan_s& p) { return p.d_tcol != nullptr; }
+
+static dim3 tril_grid(const SpecLayout& L, int B, int C) {
+  return dim3((unsigned)cdiv(L.lmax, TT_L), (unsigned)cdiv(std::min(L.mmax, L.lmax), TT_M),
+              (unsigned)(B * C));
+}
+
 int launch_spec_to_tril(const msfno_sht_plan_s& p, const float* S, float* xt, int B, int C,
                         hipStream_t s) {
   const SpecLayout& L = p.spec;
+  if (tril_tiled(p)) {  // full plans (the m-set plans of the band path map through tmap)
+    hipLaunchKernelGGL((spec_tril_tiled_kernel<true>), tril_grid(L, B, C), dim3(256), 0, s, S,
+                       nullptr, nullptr, reinterpret_cast<float2*>(xt), C, L.lmax, L.mmax, L.T,
+                       L.ldT, p.d_off, p.d_Lpe);
+    return launch_check("spec_to_tril_tiled");
+  }
   const int64_t n = (int64_t)B * C * L.Tp;
   hipLaunchKernelGGL(spec_to_tril_kernel, dim3((unsigned)std::min<int64_t>(cdiv(n, 256), 65535)),
                      dim3(256), 0, s, S, xt, B, C, L.lmax, L.mmax, L.mact, L.Tp, L.T, L.ldT,
@@ -1243,6 +1347,19 @@ int launch_spec_to_tril(const msfno_sht_plan_s& p, const float* S, float* xt, in
 int launch_tril_to_spec(const msfno_sht_plan_s& p, const float* yt, float* S, int B, int C,
                         hipStream_t s) {
   const SpecLayout& L = p.spec;
+  if (tril_tiled(p)) {
+    hipLaunchKernelGGL((spec_tril_tiled_kernel<false>), tril_grid(L, B, C), dim3(256), 0, s,
+                       nullptr, S, reinterpret_cast<const float2*>(yt), nullptr, C, L.lmax,
+                       L.mmax, L.T, L.ldT, p.d_off, p.d_Lpe);
+    MSFNO_TRY(launch_check("tril_to_spec_tiled"));
+    if (p.npad > 0) {  // the pad columns of every row, zero (as tril_to_spec_kernel wrote)
+      const int64_t n = 2LL * B * C * p.npad;
+      hipLaunchKernelGGL(zero_spec_pads_kernel, dim3((unsigned)std::min<int64_t>(cdiv(n, 256), 4096)),
+                         dim3(256), 0, s, S, p.d_tpad, p.npad, 2 * B * C, L.ldT);
+      MSFNO_TRY(launch_check("zero_spec_pads"));
+    }
+    return MSFNO_OK;
+  }
   const int64_t n = (int64_t)B * C * L.Tp;
   hipLaunchKernelGGL(tril_to_spec_kernel, dim3((unsigned)std::min<int64_t>(cdiv(n, 256), 65535)),
                      dim3(256), 0, s, yt, S, B, C, L.lmax, L.mmax, L.mact, L.Tp, L.T, L.ldT,
@@ -1505,15 +1622,6 @@ __global__ __launch_bounds__(256) void compl_contract_spec_kernel(
   }
 }
 
-// the S columns no mode maps to, zeroed in every row of the output S
-__global__ void zero_spec_pads_kernel(float* __restrict__ Y, const int* __restrict__ tpad,
-                                      int npad, int rows, int64_t ldT) {
-  const int64_t n = (int64_t)rows * npad;
-  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < n;
-       e += (int64_t)gridDim.x * blockDim.x)
-    Y[(e / npad) * ldT + tpad[e % npad]] = 0.f;
-}
-
 // MSFNO_CONTRACT_DMA=0 keeps the register-load kernel at batch 1 (A/B)
 static bool contract_dma() {
   static const bool on = [] {
@@ -1563,11 +1671,14 @@ int launch_compl_contract(const float* a, const float* w, float* y, int B, int C
               : launch_contract_t<1, 16, 1>(a, w, y, B, Ci, Co, T, s);
 }
 
-// MSFNO_LIN_DIRECT=0 keeps the gathered copies (spec_to_tril / tril_to_spec) at batch 1
-// (read at every call: the workspace carve covers both forms; tests switch it in-process)
+// MSFNO_LIN_DIRECT=1: the contraction on S itself (bitwise equal to the gathered form,
+// tests/test_gpu_linear_direct.py) instead of spec_to_tril -> contract -> tril_to_spec.
+// Opt-in: its 4-B activation gathers fetch a 64-B line per mode per channel, as many
+// line requests as the weight stream itself: 10.31 ms vs 5.66 ms per field
+// (profiles/r04_v4).  Read at every call (the carve covers both forms).
 static bool lin_direct_env() {
   const char* e = getenv("MSFNO_LIN_DIRECT");
-  return !(e && e[0] == '0');
+  return e && e[0] == '1';
 }
 
 bool contract_spec_ok(const msfno_sht_plan_s& p, const float* w, int B) {

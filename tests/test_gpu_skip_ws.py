@@ -1,6 +1,6 @@
-"""The weight-stationary inner skip (mlp_fused_h.hip: skip_ws_kernel, the default for
+"""The weight-stationary inner skip (mlp_fused_h.hip: skip_ws_kernel, MSFNO_SKIP_WS=1, for
 C = 256 with per-channel scales and P % 4 == 0) against the per-tile skip_h kernel
-(MSFNO_SKIP_WS=0), each in a child process (the switch is read once per process).
+(the default), each in a child process (the switch is read once per process).
 
 Both run the same x3h arithmetic (skip_h's per-field weight image, the same three fp16
 MFMAs per k-step in the same order, the same epilogue), so the block outputs must agree

@@ -50,7 +50,7 @@ VARIANTS = [
     {"MSFNO_SKIP_AT": "leg"},
     {"MSFNO_SKIP_AT": "inv"},
     {"MSFNO_SKIP_PX": "1"},
-    {"MSFNO_MH_PERSIST": "0"},
+    {"MSFNO_LIN_DIRECT": "1"},
 ]
 
 
