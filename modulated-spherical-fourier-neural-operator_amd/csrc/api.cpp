@@ -1741,8 +1741,6 @@ int msfno_block_forward(const msfno_block_desc* d, msfno_sht_plan_t f, msfno_sht
   std::shared_ptr<SideCtx> side;
   const bool xpl = skip_planes(d, f, b);
   const C2RPlanes xp{b.x1p, (int)C, f->nlat};
-  // skip_h with per-pixel scales needs no norm0 statistics: forked at the block start
-  const bool skip_px = b.xs && C == 256 && skip_h_env() && skip_px_env();
   auto launch_skip = [&]() -> int {
     hipStream_t ss = s;
     if (side) {  // fork
@@ -1753,32 +1751,9 @@ int msfno_block_forward(const msfno_block_desc* d, msfno_sht_plan_t f, msfno_sht
     prof(ST_SKIP, ss);
     GemmEpi e;
     e.bias = d->skip_b;
-    // MSFNO_PX_SIDEK (diagnostic, PX mode): what the side stream runs at the block start
-    // instead: "ones" = skip_h with per-channel scales 1 (x1 wrong), "fft" = a second
-    // forward row FFT of x into scratch (x1 not computed)
-    static const int sidek = [] {
-      const char* e = getenv("MSFNO_PX_SIDEK");
-      return !e ? 0 : std::string(e) == "ones" ? 1 : std::string(e) == "fft" ? 2 : 0;
-    }();
-    static float* dbg_ones = nullptr;
-    static float2* dbg_xn = nullptr;
-    if (skip_px && sidek == 1) {
-      if (!dbg_ones) {
-        std::vector<float> ones((size_t)BC * 4, 1.f);
-        MSFNO_CHECK_HIP(hipMalloc(&dbg_ones, ones.size() * sizeof(float)));
-        MSFNO_CHECK_HIP(hipMemcpy(dbg_ones, ones.data(), ones.size() * sizeof(float),
-                                  hipMemcpyHostToDevice));
-      }
-      MSFNO_TRY(launch_skip_h(d->skip_w, dbg_ones, x, x1, d->skip_b, B, P, b.dw.skip,
-                              b.dw.skip_b, ss));
-    } else if (skip_px && sidek == 2) {
-      if (!dbg_xn)
-        MSFNO_CHECK_HIP(hipMalloc(&dbg_xn, (BC * f->nlat * f->mmax + BC * f->nlat) * sizeof(float2)));
-      MSFNO_TRY(launch_fft_r2c_rows(f->fft, x, dbg_xn, dbg_xn + BC * f->nlat * f->mmax,
-                                    BC * f->nlat, f->mmax, (float)(2.0 * M_PI / f->nlon), ss));
-    } else if (b.xs && C == 256 && skip_h_env()) {
-      MSFNO_TRY(launch_skip_h(d->skip_w, skip_px ? nullptr : b.xs, x, x1, d->skip_b, B, P,
-                              b.dw.skip, b.dw.skip_b, ss));
+    if (b.xs && C == 256 && skip_h_env()) {
+      MSFNO_TRY(launch_skip_h(d->skip_w, b.xs, x, x1, d->skip_b, B, P, b.dw.skip, b.dw.skip_b,
+                              ss));
     } else if (b.xs) {
       MSFNO_TRY(gemm_x3(d->skip_w, (int)C, b.xs, x, x1, (int)C, (int)P, (int)C, (int)P, (int)P,
                         C * P, C * P, B, e, b.dw.skip, b.dw.skip_b, ss));
@@ -1798,153 +1773,22 @@ int msfno_block_forward(const msfno_block_desc* d, msfno_sht_plan_t f, msfno_sht
     }
     return MSFNO_OK;
   };
-  // MSFNO_PX_CHECK (diagnostic, PX mode only): 1 = snapshot x before the fork, and
-  // after the join recompute the skip serially and compare x1, the weight image and x
-  // bit for bit; 2 = also wait for the side stream on the host right after the skip is
-  // enqueued (nothing of this block overlaps it); 3 = wait for the caller's stream on
-  // the host before the fork
-  static const int px_check = [] {
-    const char* e = getenv("MSFNO_PX_CHECK");
-    return e ? atoi(e) : 0;
-  }();
-  static float* dbg_x = nullptr;
-  static int dbg_call = 0;
-  float2* px_snap = nullptr;  // PX check: the forward FFT output right after the FFT
-  const bool pxc = px_check && b.xs && C == 256 && d->inner_skip == MSFNO_SKIP_LINEAR;
-  // MSFNO_PX_AT=fft (diagnostic): the PX skip forked after the forward FFT
-  static const bool px_at_fft = [] {
-    const char* e = getenv("MSFNO_PX_AT");
-    return e && std::string(e) == "fft";
-  }();
-  if (pxc) {
-    if (!dbg_x) {
-      MSFNO_CHECK_HIP(hipMalloc(&dbg_x, BC * P * sizeof(float)));
-    }
-    MSFNO_CHECK_HIP(hipMemcpyAsync(dbg_x, x, BC * P * sizeof(float), hipMemcpyDeviceToDevice, s));
-    if (px_check == 3) MSFNO_CHECK_HIP(hipStreamSynchronize(s));
-  }
   if (d->inner_skip == MSFNO_SKIP_LINEAR) {
     MSFNO_REQUIRE(d->skip_w, MSFNO_EINVAL, "missing inner_skip weight");
     MSFNO_TRY(side_ctx(&side, s));
-    if ((!xpl && !b.xs) || (skip_px && !px_at_fft)) MSFNO_TRY(launch_skip());
-    if (pxc && px_check == 2 && side) MSFNO_CHECK_HIP(hipStreamSynchronize(side->side));
+    if (!xpl && !b.xs) MSFNO_TRY(launch_skip());
   }
-  // MSFNO_SKIP_AT=leg: fork the x3h skip after the forward Legendre instead of right
-  // after the norm0 statistics (A/B of the overlap window)
-  // (inv: after the spectral filter, before the inverse Legendre)
-  static const int skip_at = [] {
-    const char* e = getenv("MSFNO_SKIP_AT");
-    return !e ? 0 : std::string(e) == "leg" ? 1 : std::string(e) == "inv" ? 2 : 0;
-  }();
-  const std::function<int()> none;
-  if (skip_px && px_at_fft)
-    MSFNO_TRY(run_spectral(d, f, g, b, x, B, true, s, nullptr, launch_skip));
-  else if (skip_px && pxc) {
-    // diagnostic: snapshot the forward FFT's output as soon as it is complete (stream
-    // order), to tell a wrong FFT from a later overwrite of its output
-    static float2* dbg_xn = nullptr;
-    static size_t dbg_xn_b = 0;
-    const size_t xnb = (size_t)BC * f->nlat * f->mmax * sizeof(float2);
-    if (xnb > dbg_xn_b) {
-      if (dbg_xn) MSFNO_CHECK_HIP(hipFree(dbg_xn));
-      MSFNO_CHECK_HIP(hipMalloc(&dbg_xn, xnb));
-      dbg_xn_b = xnb;
-    }
-    px_snap = dbg_xn;
-    MSFNO_TRY(run_spectral(d, f, g, b, x, B, true, s, nullptr, [&]() -> int {
-      MSFNO_CHECK_HIP(hipMemcpyAsync(dbg_xn, b.Xn, xnb, hipMemcpyDeviceToDevice, s));
-      return MSFNO_OK;
-    }));
-  } else if (skip_px)
-    MSFNO_TRY(run_spectral(d, f, g, b, x, B, true, s));
-  else if (b.xs && skip_at == 1)
-    MSFNO_TRY(run_spectral(d, f, g, b, x, B, true, s, nullptr, none, none, launch_skip));
-  else if (b.xs && skip_at == 2)
-    MSFNO_TRY(run_spectral(d, f, g, b, x, B, true, s, nullptr, none, none, none, launch_skip));
-  else if (b.xs)  // x3h: the skip needs x's per-channel bounds (norm0 statistics) first
+  // The skip is forked after the norm0 statistics (x3h: its per-channel scales come from
+  // them), so it never shares the GPU with this block's forward FFT: skip_h co-resident
+  // with a row FFT (a fork at the block start, retired MSFNO_SKIP_PX) corrupted real parts
+  // of single FFT bins
+  if (b.xs)
     MSFNO_TRY(run_spectral(d, f, g, b, x, B, true, s, nullptr, std::function<int()>(), launch_skip));
   else if (xpl)
     MSFNO_TRY(run_spectral(d, f, g, b, x, B, true, s, &xp, launch_skip));
   else
     MSFNO_TRY(run_spectral(d, f, g, b, x, B, true, s));
   if (side) MSFNO_CHECK_HIP(hipStreamWaitEvent(s, side->join, 0));  // join
-  if (pxc) {
-    // serial recomputation: the skip, and the whole spectral path into a second
-    // workspace; every intermediate compared bit for bit with this call's
-    static void* dbg_ws2 = nullptr;
-    static size_t dbg_ws2_b = 0;
-    static unsigned long long* dbg_r = nullptr;
-    const size_t wsb = msfno_block_workspace_size(d, f, g, B);
-    if (wsb > dbg_ws2_b) {
-      if (dbg_ws2) MSFNO_CHECK_HIP(hipFree(dbg_ws2));
-      MSFNO_CHECK_HIP(hipMalloc(&dbg_ws2, wsb));
-      dbg_ws2_b = wsb;
-    }
-    if (!dbg_r) MSFNO_CHECK_HIP(hipMalloc(&dbg_r, 32 * sizeof(unsigned long long)));
-    Carve cv2;
-    cv2.base = static_cast<char*>(dbg_ws2);
-    BlockBufs b2;
-    carve_block(cv2, b2, d, f, g, B, true);
-    MSFNO_TRY(run_spectral(d, f, g, b2, x, B, true, s));
-    MSFNO_TRY(launch_skip_h(d->skip_w, skip_px ? nullptr : b2.xs, x, b2.x1, d->skip_b, B, P,
-                            b2.dw.skip, b2.dw.skip_b, s));
-    const int64_t R = 2 * BC;
-    struct Cmp { const char* name; const void* a; const void* b2; int64_t words; };
-    const Cmp cmps[] = {
-        {"x", dbg_x, x, BC * P},
-        {"x1", b.x1, b2.x1, BC * P},
-        {"skipimg", b.dw.skip, b2.dw.skip, (int64_t)(skip_h_workspace(B) - 256) / 4},
-        {"Xn", b.Xn, b2.Xn, BC * f->nlat * f->mmax * 2},
-        {"XnSnap", px_snap, b2.Xn, px_snap ? BC * f->nlat * f->mmax * 2 : 0},
-        {"XnLate", px_snap, b.Xn, px_snap ? BC * f->nlat * f->mmax * 2 : 0},
-        {"rs0", b.rs0, b2.rs0, BC * f->nlat * 2},
-        {"sc0", b.sc0, b2.sc0, BC},
-        {"sh0", b.sh0, b2.sh0, BC},
-        {"lsig", b.lsig, b2.lsig, b.lsig ? BC : 0},
-        {"isr", b.isr, b2.isr, b.isr ? R : 0},
-        {"Xt", b.Xt, b2.Xt, (int64_t)f->mmax * R * f->ldk},
-        {"S", b.Sa, b2.Sa, R * f->spec.ldT},
-        {"Yt", b.Yt, b2.Yt, (int64_t)g->mmax * R * g->ldk},
-    };
-    const int nc = (int)(sizeof(cmps) / sizeof(cmps[0]));
-    constexpr int RW = 3 + 3 * 16;  // per compare: count, first, log flag, 16 log entries
-    static unsigned long long* dbg_log = nullptr;
-    if (!dbg_log) MSFNO_CHECK_HIP(hipMalloc(&dbg_log, nc * RW * sizeof(unsigned long long)));
-    (void)dbg_r;
-    std::vector<unsigned long long> init((size_t)nc * RW, 0ull);
-    for (int i = 0; i < nc; ++i) {
-      init[(size_t)i * RW + 1] = ~0ull;
-      init[(size_t)i * RW + 2] = 1;
-    }
-    MSFNO_CHECK_HIP(hipMemcpyAsync(dbg_log, init.data(), init.size() * sizeof(unsigned long long),
-                                   hipMemcpyHostToDevice, s));
-    for (int i = 0; i < nc; ++i)
-      if (cmps[i].words > 0)
-        MSFNO_TRY(launch_debug_cmp(cmps[i].a, cmps[i].b2, cmps[i].words, dbg_log + i * RW, s));
-    std::vector<unsigned long long> h((size_t)nc * RW);
-    MSFNO_CHECK_HIP(hipMemcpyAsync(h.data(), dbg_log, h.size() * sizeof(unsigned long long),
-                                   hipMemcpyDeviceToHost, s));
-    MSFNO_CHECK_HIP(hipStreamSynchronize(s));
-    std::string line = "PX_CHECK call " + std::to_string(dbg_call++) + ":";
-    for (int i = 0; i < nc; ++i) {
-      const unsigned long long* r = &h[(size_t)i * RW];
-      line += std::string(" ") + cmps[i].name + "=" + std::to_string(r[0]) +
-              (r[0] ? "@" + std::to_string((long long)r[1]) : std::string());
-    }
-    fprintf(stderr, "%s\n", line.c_str());
-    static const bool logv = getenv("MSFNO_PX_LOG") != nullptr;
-    for (int i = 0; logv && i < nc; ++i) {
-      const unsigned long long* r = &h[(size_t)i * RW];
-      if (!r[0] || std::string(cmps[i].name) == "Yt" || std::string(cmps[i].name) == "S") continue;
-      for (int k = 0; k < (int)std::min<unsigned long long>(r[0], 16); ++k) {
-        float fa, fb;
-        const uint32_t ua = (uint32_t)r[3 + 3 * k + 1], ub = (uint32_t)r[3 + 3 * k + 2];
-        std::memcpy(&fa, &ua, 4);
-        std::memcpy(&fb, &ub, 4);
-        fprintf(stderr, "  %s[%llu] = %.9g (serial %.9g)\n", cmps[i].name, r[3 + 3 * k], fa, fb);
-      }
-    }
-  }
   // ---- filter output + skip (+ GELU for the linear filter) -> x1, norm1 partials ---
   const float* skip_src = d->inner_skip == MSFNO_SKIP_LINEAR ? x1
                           : (d->inner_skip == MSFNO_SKIP_IDENTITY ? x : nullptr);

@@ -21,7 +21,6 @@ namespace msfno {
 
 struct FFTArgs {
   int N, H, packed, nrad, inplace, codelet;
-  int outdbg;  // diagnostic: r2c output-stage variant (MSFNO_FFT_OUTDBG)
   int radices[kMaxRadices];
   const float2* twH;
   const float2* twN;
@@ -195,7 +194,7 @@ __device__ __forceinline__ void apply_twiddles(float2 (&v)[R], const float2* tw,
 // belongs to exactly one wave.
 template <int R, int IT, bool INV>
 __device__ __forceinline__ void stockham_pass_inplace(float2* buf, int H, int Ns,
-                                                      const float2* tw, int lane, int sync = 0) {
+                                                      const float2* tw, int lane) {
   const int nb = H / R;
   const int step = H / (Ns * R);
   float2 v[IT][R];
@@ -217,7 +216,6 @@ __device__ __forceinline__ void stockham_pass_inplace(float2* buf, int H, int Ns
     }
   }
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  if (sync) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // diagnostic (MSFNO_FFT_OUTDBG=3)
 #pragma unroll
   for (int it = 0; it < IT; ++it) {
     const int j = lane + 64 * it;
@@ -237,7 +235,6 @@ __device__ __forceinline__ void stockham_pass_inplace(float2* buf, int H, int Ns
       }
     }
   }
-  if (sync) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
@@ -281,8 +278,7 @@ struct FixedFFT {
   __device__ __forceinline__ static void run(float2* buf, float2*, const struct FFTArgs& f, const float2* tw,
                              int lane) {
     int Ns = 1;
-    const int sync = f.outdbg == 3;
-    ((stockham_pass_inplace<Rs, pass_iters(H, Rs), INV>(buf, H, Ns, tw, lane, sync), Ns *= Rs), ...);
+    ((stockham_pass_inplace<Rs, pass_iters(H, Rs), INV>(buf, H, Ns, tw, lane), Ns *= Rs), ...);
   }
 };
 
@@ -703,22 +699,8 @@ __global__ __launch_bounds__(64 * WV) void fft_r2c_dma_kernel(const float* __res
       const float2 X = cadd(E, cmul(twN[k], O));
       return make_float2(scale * X.x, scale * X.y);
     };
-    if (f.outdbg == 1) {  // every bin computed first (clamped), then one store per 64 bins
-      constexpr int ITS = (H + 1 + 63) / 64;
-      float2 res[ITS];
-#pragma unroll
-      for (int it = 0; it < ITS; ++it) res[it] = bin(min(lane + 64 * it, mmax - 1));
-#pragma unroll
-      for (int it = 0; it < ITS; ++it)
-        if (lane + 64 * it < mmax) o[lane + 64 * it] = res[it];
-    } else if (f.outdbg == 2) {
-      for (int k = lane; k < mmax; k += 64) {
-        o[k] = bin(k);
-        asm volatile("s_waitcnt expcnt(0)" ::: "memory");
-      }
-    } else {
-      for (int k = lane; k < mmax; k += 64) o[k] = bin(k);
-    }
+    for (int k = lane; k < mmax; k += 64) o[k] = bin(k);
+
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
     if constexpr (NS == 1) {
       // every read of the slot has returned: refill it with the next row
@@ -1112,11 +1094,6 @@ __global__ __launch_bounds__(256) void fft_c2r_tile_kernel(const float* __restri
 
 static FFTArgs make_args(const FFTPlan& p) {
   FFTArgs a{};
-  static const int outdbg = [] {
-    const char* e = getenv("MSFNO_FFT_OUTDBG");
-    return e ? atoi(e) : 0;
-  }();
-  a.outdbg = outdbg;
   a.N = p.N; a.H = p.H; a.packed = p.packed; a.nrad = p.nrad; a.inplace = p.inplace;
   a.codelet = p.codelet;
   for (int i = 0; i < kMaxRadices; ++i) a.radices[i] = p.radices[i];

@@ -927,19 +927,6 @@ int gemm_x3c(const unsigned short* Aw, int co, int ci, const float* Sin, int ldS
     const char* e = getenv("MSFNO_X3C_NS");
     return (e && e[0] == '2') ? 2 : 3;
   }();
-  // MSFNO_X3C_WAVES=4 (A/B): 2 x 2 waves of 64 x 64 (one wave per SIMD, 512 registers:
-  // a third fewer LDS fragment reads per MFMA) instead of 4 x 2 of 32 x 64
-  static const int w4 = [] {
-    const char* e = getenv("MSFNO_X3C_WAVES");
-    return e && atoi(e) == 4;
-  }();
-  if (w4 && ns == 3 && !Sin) {  // (the fp32-input layer 0 stages one float4 per thread of 8 waves)
-    if (Y)
-      hipLaunchKernelGGL((gemm_x6c_kernel<true, 2, 2, false, 0, 3, 2, 3>), grid, dim3(256), 0, s, p);
-    else
-      hipLaunchKernelGGL((gemm_x6c_kernel<false, 2, 2, false, 0, 1, 2, 3>), grid, dim3(256), 0, s, p);
-    return launch_check("gemm_x3c");
-  }
   if (Sin)
     hipLaunchKernelGGL((gemm_x6c_kernel<true, 4, 2, true, 0, 2, 2>), grid, dim3(512), 0, s, p);
   else if (Y && ns == 3)

@@ -109,13 +109,9 @@ bool mlp_fused_h_env();
 // power-of-two channel scales xs (|xs x| < 2^14), or per pixel in-kernel when xs is null;
 // ws >= skip_h_workspace(B)
 bool skip_h_env();
-bool skip_px_env();  // skip_h with per-pixel scales (xs = null) at the block start
 size_t skip_h_workspace(int B);
 int launch_skip_h(const float* W, const float* xs, const float* x, float* out, const float* bias,
                   int B, int64_t P, void* ws, size_t ws_bytes, hipStream_t s);
-// diagnostics: res[0] += #words where a != b, res[1] = min index of such a word
-int launch_debug_cmp(const void* a, const void* b, int64_t nwords, unsigned long long* res,
-                     hipStream_t s);
 size_t mlp_fused_h_image_bytes();
 int launch_mlp_fused_h_images(const float* W1, const float* b1, const float* W2,
                               unsigned short* img, hipStream_t s);

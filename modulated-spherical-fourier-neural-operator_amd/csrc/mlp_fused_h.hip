@@ -490,30 +490,6 @@ __global__ __launch_bounds__(256, 2) void mlp_fused_h_kernel(MlpHParams p) {
   }
 }
 
-// ---- quad-lane helpers (skip_ws_kernel's epilogue) ---------------------------------------
-__device__ __forceinline__ float dpp_xor1(float v) {
-  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v),
-                                                               0xB1, 0xF, 0xF, false));
-}
-__device__ __forceinline__ float dpp_xor2(float v) {
-  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v),
-                                                               0x4E, 0xF, 0xF, false));
-}
-
-// 4 x 4 transpose inside each quad of lanes: lane b of the quad ends with element j =
-// element b of quad lane j
-__device__ __forceinline__ void quad_transpose(float (&v)[4], int qb) {
-  {
-    const bool hi = (qb & 2) != 0;
-    const float r0 = dpp_xor2(hi ? v[0] : v[2]), r1 = dpp_xor2(hi ? v[1] : v[3]);
-    if (hi) { v[0] = r0; v[1] = r1; } else { v[2] = r0; v[3] = r1; }
-  }
-  {
-    const bool od = (qb & 1) != 0;
-    const float r0 = dpp_xor1(od ? v[0] : v[1]), r1 = dpp_xor1(od ? v[2] : v[3]);
-    if (od) { v[0] = r0; v[2] = r1; } else { v[1] = r0; v[3] = r1; }
-  }
-}
 
 // ---- inner skip (1x1 conv, C = 256) on the same tiling: out = Ws·x + bs -------------
 // The fc1 half of mlp_fused_h_kernel with 256 output rows and no hidden layer:
@@ -595,12 +571,6 @@ __global__ void sk_image_kernel(const float* __restrict__ W, const float* __rest
   }
 }
 
-// PX: x scaled per pixel instead of per channel (xs null): the lane's 64 values and
-// those of the three other lanes of its pixel give max_c |x[c][px]| = f 2^e, the column
-// is split under 2^(15 - e) and the output column multiplied back by 2^(e - 15) — exact
-// powers of two, so no dependence on the norm0 statistics (the skip can start with the
-// block) and a batch-independent weight image
-template <bool PX>
 __global__ __launch_bounds__(256, 2) void skip_h_kernel(SkipHParams p) {
   constexpr int NS = MH_NS, W = 4;
   constexpr int RING_BYTES = NS * MH_SLICE * 2;
@@ -615,8 +585,7 @@ __global__ __launch_bounds__(256, 2) void skip_h_kernel(SkipHParams p) {
   const int z = lin / p.tiles_per_field;
   const int64_t P = p.P;
   const int64_t px = (int64_t)(lin - z * p.tiles_per_field) * 64 + 16 * wave + r16;
-  const int zi = PX ? 0 : z;  // per-pixel scales: one image for every batch
-  const unsigned short* img = p.img + (int64_t)zi * SK_NSLICE * MH_SLICE;
+  const unsigned short* img = p.img + (int64_t)z * SK_NSLICE * MH_SLICE;
 
   const uint32_t ring_lds = lds_addr(ring);
   const int wave_u = __builtin_amdgcn_readfirstlane(wave);
@@ -633,38 +602,7 @@ __global__ __launch_bounds__(256, 2) void skip_h_kernel(SkipHParams p) {
   // x -> scaled fp16x2 B fragments (k-step ks: channels 32 ks + 8 g + 0..7)
   const float* xcol = p.x + (int64_t)z * MH_C * P + (px < P ? px : P - 1);
   half8 xf[8][2];
-  float ipx = 1.f;  // PX: 1 / the pixel's scale
-  if constexpr (PX) {
-    float xv[8][8];
-#pragma unroll
-    for (int ks = 0; ks < 8; ++ks)
-#pragma unroll
-      for (int e = 0; e < 8; ++e)
-        xv[ks][e] = __builtin_nontemporal_load(xcol + (int64_t)(32 * ks + 8 * g + e) * P);
-    float m = 0.f;
-#pragma unroll
-    for (int ks = 0; ks < 8; ++ks)
-#pragma unroll
-      for (int e = 0; e < 8; ++e) m = fmaxf(m, fabsf(xv[ks][e]));
-    m = fmaxf(m, __shfl_xor(m, 16));
-    m = fmaxf(m, __shfl_xor(m, 32));
-    float sp = 1.f;
-    if (m > 0.f && isfinite(m)) {
-      int e;
-      frexpf(m, &e);
-      sp = ldexpf(1.f, 15 - e);
-      ipx = ldexpf(1.f, e - 15);
-    }
-#pragma unroll
-    for (int ks = 0; ks < 8; ++ks) {
-      uint32_t t[2][4];
-#pragma unroll
-      for (int e = 0; e < 4; ++e)
-        split2h(sp * xv[ks][2 * e], sp * xv[ks][2 * e + 1], t[0][e], t[1][e]);
-#pragma unroll
-      for (int pl = 0; pl < 2; ++pl) xf[ks][pl] = mh_frag(t[pl][0], t[pl][1], t[pl][2], t[pl][3]);
-    }
-  } else {
+  {
     const float* xsb = p.xs + (int64_t)z * MH_C;
 #pragma unroll
     for (int ks = 0; ks < 8; ++ks) {
@@ -684,7 +622,7 @@ __global__ __launch_bounds__(256, 2) void skip_h_kernel(SkipHParams p) {
     }
   }
   for (int i = tid; i < MH_C; i += 256) {
-    irs[i] = p.inv_rs[(int64_t)zi * MH_C + i];
+    irs[i] = p.inv_rs[(int64_t)z * MH_C + i];
     bs[i] = p.bias ? p.bias[i] : 0.f;
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -737,261 +675,17 @@ __global__ __launch_bounds__(256, 2) void skip_h_kernel(SkipHParams p) {
     const int r0 = 16 * ot + 4 * g;
     const float4 is = *reinterpret_cast<const float4*>(irs + r0);
     const float4 b = *reinterpret_cast<const float4*>(bs + r0);
-    const float isv[4] = {is.x * ipx, is.y * ipx, is.z * ipx, is.w * ipx};
+    const float isv[4] = {is.x, is.y, is.z, is.w};
     const float bv[4] = {b.x, b.y, b.z, b.w};
 #pragma unroll
     for (int i = 0; i < 4; ++i) o[(int64_t)(r0 + i) * P] = fmaf(oacc[ot][i], isv[i], bv[i]);
   }
 }
 
-// ---- weight-stationary inner skip (C = 256): skip_ws_kernel -----------------------------
-// One 512-thread workgroup per CU, persistent over 32-pixel chunks of x.  Wave w keeps
-// output rows 32 w .. 32 w + 31 of the field's weight image W' (skip_h's image: rs_c
-// W[c][k] / xs_k, two fp16 planes) as MFMA A fragments in registers (128 VGPRs), loaded
-// once per field, so the 256 x 256 weight never streams again: the kernel moves x in
-// and the skip out and nothing else (skip_h re-read the 256-KB image per 64 pixels:
-// 4 GB of L2 traffic at config 2).  Per chunk: x (256 channels x 32 pixels fp32, 32 KB)
-// arrives by LDS-DMA into one of three raw buffers (two chunks in flight), is scaled
-// per channel (xs) and split into the fp16x2 B fragments of one conversion buffer
-// ([pixel tile][k-step][plane][16 px][32 k], skip_h's swizzle), then 96 MFMAs per wave
-// and 16-B stores of the quad-transposed accumulators (x inv_rs + bias).
-constexpr int SW_PX = 32;                      // pixels per chunk
-constexpr int SW_RAW = MH_C * SW_PX * 4;       // 32 KB: fp32 [256][32]
-constexpr int SW_CONV = 2 * 8 * 2 * 16 * 64;   // 32 KB: fp16 [2][8][2][16][32]
-constexpr int SW_NRAW = 3;
-__device__ float4 sw_sink[64];
-
-struct SkipWSParams {
-  const float* x;
-  const float* xs;
-  float* out;
-  const unsigned short* img;  // [B][16 slices]
-  const float* inv_rs;        // [B][C]
-  const float* bias;          // [C] or null
-  int64_t P;
-  int chunks_per_field;
-  int nchunks;
-};
-
-__global__ __launch_bounds__(512, 1) void skip_ws_kernel(SkipWSParams p) {
-  __shared__ __attribute__((aligned(16))) char lds[SW_NRAW * SW_RAW + SW_CONV + 3 * MH_C * 4];
-  char* const conv = lds + SW_NRAW * SW_RAW;
-  float* const xs_s = reinterpret_cast<float*>(conv + SW_CONV);
-  float* const irs_s = xs_s + MH_C;
-  float* const bias_s = irs_s + MH_C;
-  const int tid = threadIdx.x;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  // lane-dependent values, re-laundered through an empty asm operand every chunk: hipcc
-  // would otherwise hoist every address of the loop body out of the chunk loop and spill
-  int lane = tid & 63;
-  int r16 = lane & 15, gq = lane >> 4, qb = lane & 3, qa = r16 >> 2;
-  const int64_t P = p.P;
-  const int64_t CP = (int64_t)MH_C * P;
-  // this workgroup's chunks [q0, q1)
-  const int G = gridDim.x;
-  const int q0 = (int)((int64_t)p.nchunks * blockIdx.x / G);
-  const int q1 = (int)((int64_t)p.nchunks * (blockIdx.x + 1) / G);
-  const int n = q1 - q0;
-  if (n <= 0) return;
-  const uint32_t raw_lds = lds_addr(lds);
-
-  // chunk q's x: piece pc (channels 8 pc .. + 7, 1 KB) from wave pc % 8; lane: channel
-  // 8 pc + (lane >> 3), pixels 4 (lane & 7) .. + 3 (clamped into the field)
-  auto issue = [&](int q, int buf) {
-    const int z = q / p.chunks_per_field;
-    int64_t px = (int64_t)(q - z * p.chunks_per_field) * SW_PX + 4 * (lane & 7);
-    if (px > P - 4) px = P - 4;
-    const float* base = p.x + (int64_t)z * CP + (int64_t)(lane >> 3) * P + px;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int pc = wave + 8 * j;
-      glds16(base + (int64_t)(8 * pc) * P, raw_lds + (uint32_t)(buf * SW_RAW + pc * 1024));
-    }
-  };
-  // the field's weight fragments: slice (wave, kh), [pl][ksl][t][r][32] (skip_h's image)
-  half8 A[8][2][2];  // [ks][t][pl]
-  int cur_z = -1;
-  auto load_field = [&](int z) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    for (int i = tid; i < MH_C; i += 512) {
-      xs_s[i] = p.xs[(int64_t)z * MH_C + i];
-      irs_s[i] = p.inv_rs[(int64_t)z * MH_C + i];
-      bias_s[i] = p.bias ? p.bias[i] : 0.f;
-    }
-    const unsigned short* img = p.img + (int64_t)z * SK_NSLICE * MH_SLICE;
-    const int a_lane = r16 * 32 + 8 * (gq ^ mh_swz(r16));
-#pragma unroll
-    for (int ks = 0; ks < 8; ++ks)
-#pragma unroll
-      for (int t = 0; t < 2; ++t)
-#pragma unroll
-        for (int pl = 0; pl < 2; ++pl)
-          A[ks][t][pl] = *reinterpret_cast<const half8*>(
-              img + (int64_t)(2 * wave + (ks >> 2)) * MH_SLICE +
-              ((pl * 4 + (ks & 3)) * 2 + t) * 512 + a_lane);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-  };
-
-  // prologue: chunks q0 .. q0 + 2 in flight
-#pragma unroll
-  for (int j = 0; j < SW_NRAW; ++j)
-    if (j < n) issue(q0 + j, j);
-
-  for (int i = 0; i < n; ++i) {
-    asm volatile("" : "+v"(lane), "+v"(r16), "+v"(gq), "+v"(qb), "+v"(qa));
-    const int h = lane >> 5, pt_c = (lane >> 4) & 1, r_c = lane & 15;
-    const int q = q0 + i;
-    const int z = q / p.chunks_per_field;
-    const int64_t px0 = (int64_t)(q - z * p.chunks_per_field) * SW_PX;
-    if (z != cur_z) {  // (uniform) new field: drains everything in flight, then reloads
-      load_field(z);
-      cur_z = z;
-    } else {
-      // chunk i's pieces landed: after them this wave issued the pieces of chunks i + 1,
-      // i + 2 (if any) and the stores of chunks i - 3 .. i - 1
-      const int cnt = 4 * ((i + 1 < n) + (i + 2 < n) + min(i, 3));
-      if (cnt >= 20) asm volatile("s_waitcnt vmcnt(20)" ::: "memory");
-      else if (cnt >= 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-      else if (cnt >= 12) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
-      else if (cnt >= 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-      else if (cnt >= 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      // every wave's pieces landed; the conversion buffer's last reads (MFMA of chunk
-      // i - 1) returned
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-    }
-    // ---- convert: wave w takes k-step ks = w; lane: pixel 16 pt + r, channel group
-    // g = 2 j + h (the two lane halves read rows of opposite parity: no bank conflict)
-    {
-      const float* raw = reinterpret_cast<const float*>(lds + (i % SW_NRAW) * SW_RAW);
-      const int pxl = 16 * pt_c + r_c;
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const int g = 2 * j + h;
-        const int c0 = 32 * wave + 8 * g;
-        float tv[8];
-#pragma unroll
-        for (int e = 0; e < 8; ++e) tv[e] = raw[(c0 + (e ^ h)) * SW_PX + pxl];
-        float xv[8];
-#pragma unroll
-        for (int e = 0; e < 8; ++e) xv[e] = h ? tv[e ^ 1] : tv[e];
-        const float4 sa = *reinterpret_cast<const float4*>(xs_s + c0);
-        const float4 sb = *reinterpret_cast<const float4*>(xs_s + c0 + 4);
-        const float sv[8] = {sa.x, sa.y, sa.z, sa.w, sb.x, sb.y, sb.z, sb.w};
-        uint32_t t2[2][4];
-#pragma unroll
-        for (int e = 0; e < 4; ++e)
-          split2h(sv[2 * e] * xv[2 * e], sv[2 * e + 1] * xv[2 * e + 1], t2[0][e], t2[1][e]);
-#pragma unroll
-        for (int pl = 0; pl < 2; ++pl)
-          *reinterpret_cast<uint4*>(conv + ((pt_c * 8 + wave) * 2 + pl) * 1024 + r_c * 64 +
-                                    16 * (g ^ mh_swz(r_c))) =
-              make_uint4(t2[pl][0], t2[pl][1], t2[pl][2], t2[pl][3]);
-      }
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    // the raw buffer of chunk i is free: chunk i + 3 into it
-    if (i + SW_NRAW < n) issue(q + SW_NRAW, i % SW_NRAW);
-    // ---- 96 MFMAs: rows 32 w + 16 t .., pixels 16 pt ..
-    floatx4 acc[2][2];
-#pragma unroll
-    for (int t = 0; t < 2; ++t)
-#pragma unroll
-      for (int pt = 0; pt < 2; ++pt) acc[t][pt] = floatx4{0.f, 0.f, 0.f, 0.f};
-    // B fragments one k-step ahead (two sets live; a sched barrier per k-step keeps
-    // hipcc from hoisting all eight sets next to the 128 weight registers)
-    const char* cb = conv + r16 * 64 + 16 * (gq ^ mh_swz(r16));
-    auto ldb = [&](int ks, half8 (&b)[2][2]) {
-#pragma unroll
-      for (int pt = 0; pt < 2; ++pt)
-#pragma unroll
-        for (int pl = 0; pl < 2; ++pl)
-          b[pt][pl] = *reinterpret_cast<const half8*>(cb + ((pt * 8 + ks) * 2 + pl) * 1024);
-    };
-    half8 bb[2][2][2];
-    ldb(0, bb[0]);
-#pragma unroll
-    for (int ks = 0; ks < 8; ++ks) {
-      if (ks + 1 < 8) ldb(ks + 1, bb[(ks + 1) & 1]);
-      const half8 (&b)[2][2] = bb[ks & 1];
-#pragma unroll
-      for (int t = 0; t < 2; ++t)
-#pragma unroll
-        for (int pt = 0; pt < 2; ++pt) {
-          acc[t][pt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A[ks][t][1], b[pt][0], acc[t][pt], 0, 0, 0);
-          acc[t][pt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A[ks][t][0], b[pt][1], acc[t][pt], 0, 0, 0);
-          acc[t][pt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A[ks][t][0], b[pt][0], acc[t][pt], 0, 0, 0);
-        }
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    // ---- out = acc / rs_c + b_c: quad-transposed, 16-B stores (4 pixels of one row)
-    float* ob = p.out + (int64_t)z * CP;
-#pragma unroll
-    for (int t = 0; t < 2; ++t)
-#pragma unroll
-      for (int pt = 0; pt < 2; ++pt) {
-        float v[4] = {acc[t][pt][0], acc[t][pt][1], acc[t][pt][2], acc[t][pt][3]};
-        quad_transpose(v, qb);
-        const int c = 32 * wave + 16 * t + 4 * gq + qb;
-        const float is = irs_s[c], bb = bias_s[c];
-        const int64_t px = px0 + 16 * pt + 4 * qa;
-        // (pixels past P go to a sink: every wave issues exactly 4 stores per chunk, the
-        // count the waits above assume)
-        float4* dst = px < P ? reinterpret_cast<float4*>(ob + (int64_t)c * P + px) : sw_sink + lane;
-        *dst = make_float4(fmaf(v[0], is, bb), fmaf(v[1], is, bb), fmaf(v[2], is, bb),
-                           fmaf(v[3], is, bb));
-      }
-    // (the chunk's stores stay in this iteration: the counted waits assume the order)
-    asm volatile("" ::: "memory");
-  }
-}
-
-__global__ void debug_cmp_kernel(const uint32_t* __restrict__ a, const uint32_t* __restrict__ b,
-                                 int64_t n, unsigned long long* res) {
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
-       i += (int64_t)gridDim.x * blockDim.x) {
-    if (a[i] != b[i]) {
-      const unsigned long long slot = atomicAdd(res, 1ull);
-      atomicMin(res + 1, (unsigned long long)i);
-      if (res[2] && slot < 16) {  // res[2] != 0: a log of [index, a, b] after res[3]
-        unsigned long long* log = res + 3 + 3 * slot;
-        log[0] = (unsigned long long)i;
-        log[1] = a[i];
-        log[2] = b[i];
-      }
-    }
-  }
-}
-
 }  // namespace
-
-int launch_debug_cmp(const void* a, const void* b, int64_t nwords, unsigned long long* res,
-                     hipStream_t s) {
-  hipLaunchKernelGGL(debug_cmp_kernel, dim3(1024), dim3(256), 0, s,
-                     static_cast<const uint32_t*>(a), static_cast<const uint32_t*>(b), nwords, res);
-  return launch_check("debug_cmp");
-}
 
 size_t skip_h_workspace(int B) {
   return (size_t)B * SK_NSLICE * MH_SLICE * 2 + (size_t)B * MH_C * 4 * 2 + 256;
-}
-
-// MSFNO_SKIP_PX=1: per-pixel scales (the skip starts with the block) instead of
-// per-channel scales from the norm0 statistics.  Opt-in: equal speed (160.5 vs 160.2
-// fields/s), and with the side stream the 12-block config-3 network drifted to 5.3e-4
-// against the oracle (bar 2.1e-4; per-channel: 2.7e-6) while the same test passes with
-// MSFNO_SIDE_STREAM=0 — an ordering problem of the fork at the block start in the
-// network, not yet found, so the mode stays off by default
-bool skip_px_env() {
-  static const bool on = [] {
-    const char* e = getenv("MSFNO_SKIP_PX");
-    return e && e[0] == '1';
-  }();
-  return on;
 }
 
 // MSFNO_SKIP_H=0 keeps gemm_x3 for the inner skip
@@ -1003,58 +697,24 @@ bool skip_h_env() {
   return on;
 }
 
-// MSFNO_SKIP_WS=1: the weight-stationary skip_ws_kernel instead of the per-tile skip_h.
-// Opt-in: bitwise equal, but in-block with the side stream its one 134-KB workgroup per CU
-// keeps the forward Legendre (legendre_x3f) from co-residing: legendre_fwd 0.66 -> 1.01 ms,
-// 159.6 -> 155.7 fields/s (profiles/r04_v4)
-static bool skip_ws_env() {
-  const char* e = getenv("MSFNO_SKIP_WS");
-  return e && e[0] == '1';
-}
-
-static int device_cus() {
-  int dev = 0, cus = 0;
-  if (hipGetDevice(&dev) != hipSuccess ||
-      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-      cus <= 0)
-    cus = 256;
-  return cus;
-}
 
 int launch_skip_h(const float* W, const float* xs, const float* x, float* out, const float* bias,
                   int B, int64_t P, void* ws, size_t ws_bytes, hipStream_t s) {
-  MSFNO_REQUIRE(W && x && out && ws && B > 0 && P >= 1 && ws_bytes >= skip_h_workspace(B),
+  MSFNO_REQUIRE(W && xs && x && out && ws && B > 0 && P >= 1 && ws_bytes >= skip_h_workspace(B),
                 MSFNO_EINVAL, "skip_h: bad arguments");
-  // xs null: per-pixel scales, one batch-independent weight image
-  const int nimg = xs ? B : 1;
   unsigned short* img = static_cast<unsigned short*>(ws);
   float* rs = reinterpret_cast<float*>(img + (int64_t)B * SK_NSLICE * MH_SLICE);
   float* inv_rs = rs + (int64_t)B * MH_C;
-  hipLaunchKernelGGL(sk_scale_kernel, dim3(MH_C, nimg), dim3(256), 0, s, W, xs, rs, inv_rs);
+  hipLaunchKernelGGL(sk_scale_kernel, dim3(MH_C, B), dim3(256), 0, s, W, xs, rs, inv_rs);
   MSFNO_TRY(launch_check("sk_scale"));
-  hipLaunchKernelGGL(sk_image_kernel, dim3(64, nimg), dim3(256), 0, s, W, xs, rs, img);
+  hipLaunchKernelGGL(sk_image_kernel, dim3(64, B), dim3(256), 0, s, W, xs, rs, img);
   MSFNO_TRY(launch_check("sk_image"));
   SkipHParams p{};
   p.x = x; p.xs = xs; p.out = out; p.img = img; p.inv_rs = inv_rs; p.bias = bias; p.P = P;
   p.tiles_per_field = (int)cdiv(P, 64);
   const int64_t tiles = (int64_t)B * p.tiles_per_field;
   MSFNO_REQUIRE(tiles < (1LL << 31), MSFNO_EINVAL, "skip_h: grid too large");
-  if (xs && P % 4 == 0 && skip_ws_env()) {
-    SkipWSParams w{};
-    w.x = x; w.xs = xs; w.out = out; w.img = img; w.inv_rs = inv_rs; w.bias = bias; w.P = P;
-    w.chunks_per_field = (int)cdiv(P, SW_PX);
-    const int64_t nch = (int64_t)B * w.chunks_per_field;
-    MSFNO_REQUIRE(nch < (1LL << 31), MSFNO_EINVAL, "skip_ws: too many chunks");
-    w.nchunks = (int)nch;
-    static const int cus = device_cus();
-    const int grid = (int)std::min<int64_t>(cus, nch);
-    hipLaunchKernelGGL(skip_ws_kernel, dim3((unsigned)grid), dim3(512), 0, s, w);
-    return launch_check("skip_ws");
-  }
-  if (xs)
-    hipLaunchKernelGGL(skip_h_kernel<false>, dim3((unsigned)tiles), dim3(256), 0, s, p);
-  else
-    hipLaunchKernelGGL(skip_h_kernel<true>, dim3((unsigned)tiles), dim3(256), 0, s, p);
+  hipLaunchKernelGGL(skip_h_kernel, dim3((unsigned)tiles), dim3(256), 0, s, p);
   return launch_check("skip_h");
 }
 

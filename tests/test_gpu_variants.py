@@ -47,9 +47,6 @@ VARIANTS = [
     {"MSFNO_LEG_X3F": "0"},
     {"MSFNO_X3F_NS": "2"},
     {"MSFNO_SKIP_H": "0"},
-    {"MSFNO_SKIP_AT": "leg"},
-    {"MSFNO_SKIP_AT": "inv"},
-    {"MSFNO_SKIP_PX": "1"},
     {"MSFNO_LIN_DIRECT": "1"},
 ]
 
