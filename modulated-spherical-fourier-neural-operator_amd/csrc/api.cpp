@@ -794,12 +794,9 @@ void carve_block(Carve& cv, BlockBufs& b, const msfno_block_desc* d,
       carve_spec_ws(cv, b.dw, d);
     }
   } else {
-    // one region for either form of the linear filter: the gathered copies xt, yt, or
-    // (batch 1, full plans: launch_contract_spec) the filter's output S in Sb
-    float* r = cv.take<float>(std::max<int64_t>(4 * BC * L.T, R * L.ldT));
-    b.xt = r;
-    b.yt = r + 2 * BC * L.T;
-    b.Sb = r;
+    // the gathered copies of the linear filter's input and output (tril order)
+    b.xt = cv.take<float>(2 * BC * L.T);
+    b.yt = cv.take<float>(2 * BC * L.T);
   }
   b.Yt = cv.take<float>((int64_t)g->mmax * R * g->ldk);
   b.Yn = cv.take<float2>(BC * g->nlat * g->mmax);
@@ -1120,10 +1117,6 @@ int run_filter(const msfno_block_desc* d, msfno_sht_plan_s* f, msfno_sht_plan_s*
     }
   } else {
     MSFNO_REQUIRE(d->lin_w, MSFNO_EINVAL, "missing linear spectral weight");
-    if (contract_spec_ok(*f, d->lin_w, B)) {  // on S itself: Sa -> Sb (read by the inverse)
-      prof(ST_LIN_CONTRACT, s);
-      return launch_contract_spec(*f, b.Sa, d->lin_w, b.Sb, (int)C, s);
-    }
     prof(ST_LIN_GATHER, s);
     MSFNO_TRY(launch_spec_to_tril(*f, b.Sa, b.xt, B, (int)C, s));
     prof(ST_LIN_CONTRACT, s);
@@ -1193,8 +1186,7 @@ int run_spectral(const msfno_block_desc* d, msfno_sht_plan_s* f, msfno_sht_plan_
   if (before_inv) MSFNO_TRY(before_inv());
   prof(ST_LEG_INV, s);
   // (the linear filter on S writes its output to Sb)
-  const bool lin_s = d->filter_type != MSFNO_FILTER_NONLINEAR && contract_spec_ok(*f, d->lin_w, B);
-  MSFNO_TRY(legendre_inv(g, lin_s ? b.Sb : b.Sa, b.Yt, (int)R, s));
+  MSFNO_TRY(legendre_inv(g, b.Sa, b.Yt, (int)R, s));
   return MSFNO_OK;
 }
 

@@ -293,8 +293,8 @@ struct msfno_sht_plan_s {
   int* d_tril_local = nullptr;
   std::vector<long long> lin_modes;
   // full plans: S column of every tril mode n (torch.tril_indices order), and the S
-  // columns no mode maps to (block pads): the linear filter reads and writes S in place
-  // of a gathered copy (launch_contract_spec)
+  // columns no mode maps to (block pads): the tiled S <-> tril re-layouts of the linear
+  // filter (spec_tril_tiled_kernel, zero_spec_pads_kernel)
   int* d_tcol = nullptr;
   int* d_tpad = nullptr;
   int npad = 0;

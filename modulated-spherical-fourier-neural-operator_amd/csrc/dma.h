@@ -32,18 +32,6 @@ __device__ __forceinline__ void glds16(const void* gsrc, uint32_t lds) {
       : "memory");
 }
 
-// one wave-instruction: lane l copies 4 B from its own gsrc (a gather) to LDS byte
-// (lds + 4 l); lds must be wave-uniform
-__device__ __forceinline__ void glds4(const void* gsrc, uint32_t lds) {
-  unsigned keep;
-  asm volatile(
-      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\t"
-      "s_mov_b32 m0, %0"
-      : "=&s"(keep)
-      : "v"(gsrc), "s"(__builtin_amdgcn_readfirstlane(lds))
-      : "memory");
-}
-
 // six wave-instructions in one block (one m0 save / restore): lane l copies 16 B
 // from sbase + voff[i] to LDS byte lds + i * lds_step + 16 l.  sbase and lds must be
 // wave-uniform (SGPR operands); voff[i] are the lane's byte offsets (SADDR + VADDR

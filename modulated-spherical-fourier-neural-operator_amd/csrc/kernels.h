@@ -164,11 +164,6 @@ int launch_spec_to_tril(const msfno_sht_plan_s& p, const float* S, float* xt, in
                         hipStream_t s);
 int launch_tril_to_spec(const msfno_sht_plan_s& p, const float* yt, float* S, int B, int C,
                         hipStream_t s);
-// the linear filter on S directly (batch 1, full plans; layers.py:408-413): S (2 C rows
-// of ldT) -> Y (same layout, pad columns zeroed), no gathered copies
-bool contract_spec_ok(const msfno_sht_plan_s& p, const float* w, int B);
-int launch_contract_spec(const msfno_sht_plan_s& p, const float* S, const float* w, float* Y,
-                         int C, hipStream_t s);
 // compl_contract_fwd_c: a (B,Ci,T,2), w (Co,Ci,T,2) -> y (B,Co,T,2)
 int launch_compl_contract(const float* a, const float* w, float* y, int B, int Ci, int Co,
                           int64_t T, hipStream_t s);

@@ -1544,84 +1544,6 @@ __global__ __launch_bounds__(256) void compl_contract_dma_kernel(const float* __
   }
 }
 
-// The same contraction on S itself (batch 1, full plans): no gathered copy of the
-// coefficients.  Mode n of the weight (tril order, layers.py:408-413) lives in S column
-// tcol[n]; a workgroup's 256 modes are scattered over S's m blocks, so the activation
-// of each input channel arrives by two 4-B gather LDS-DMAs per wave (Re and Im rows of
-// S, one lane per mode) beside the 32 weight pieces, and the outputs are stored to the
-// Re / Im rows of the output S (4-B stores).  Out of place: the workgroups of one mode
-// tile write channels the others still read.
-template <int NS>
-__global__ __launch_bounds__(256) void compl_contract_spec_kernel(
-    const float* __restrict__ S, const float* __restrict__ w, float* __restrict__ Y,
-    const int* __restrict__ tcol, int Ci, int Co, int64_t T, int64_t ldT, int nkc) {
-  constexpr int STAGE = CDMA_SEG * CDMA_NT * 8;  // bytes: 16 weight rows, then Re[256], Im[256]
-  constexpr int NQ = 2 * CDMA_KC / 4;            // weight pieces per wave and stage (8)
-  __shared__ __attribute__((aligned(16))) char lds[NS * STAGE];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int kc = blockIdx.x % nkc, mt = blockIdx.x / nkc;
-  const int k0 = kc * CDMA_KC;
-  const int64_t n0 = (int64_t)mt * CDMA_NT;
-  const int64_t rowb = T * 8;  // bytes per (k, i) weight row
-  const char* src[NQ];
-  uint32_t dst[NQ];
-#pragma unroll
-  for (int q = 0; q < NQ; ++q) {
-    const int pc = wave + 4 * q;  // weight piece: segment pc / 2, half pc % 2
-    const int seg = pc >> 1, half = pc & 1;
-    const int64_t off = min(n0 * 8 + half * 1024 + lane * 16, rowb - 16);
-    const int k = min(k0 + seg, Co - 1);
-    src[q] = reinterpret_cast<const char*>(w) + (int64_t)k * Ci * rowb + off;
-    dst[q] = (uint32_t)(seg * CDMA_NT * 8 + half * 1024);
-  }
-  // this thread's mode (lane of wave w: mode n0 + 64 w + lane = n0 + tid)
-  const int64_t n = n0 + tid;
-  const int t = tcol[n < T ? n : T - 1];
-  const float* are = S + t;             // + i ldT: Re of input channel i
-  const float* aim = S + Ci * ldT + t;  // + i ldT: Im
-  const uint32_t act = (uint32_t)(CDMA_KC * CDMA_NT * 8 + wave * 256);
-  const uint32_t lds0 = lds_addr(lds);
-  auto issue = [&](int i, int slot) {
-    const uint32_t base = lds0 + (uint32_t)(slot * STAGE);
-#pragma unroll
-    for (int q = 0; q < NQ; ++q) glds16(src[q] + i * rowb, base + dst[q]);
-    glds4(are + (int64_t)i * ldT, base + act);
-    glds4(aim + (int64_t)i * ldT, base + act + CDMA_NT * 4);
-  };
-  constexpr int PER = NQ + 2;  // vm instructions per wave and stage
-#pragma unroll
-  for (int j = 0; j < NS - 1; ++j)
-    if (j < Ci) issue(j, j);
-  float2 acc[CDMA_KC];
-#pragma unroll
-  for (int k = 0; k < CDMA_KC; ++k) acc[k] = make_float2(0.f, 0.f);
-  for (int i = 0; i < Ci; ++i) {
-    const int ahead = min(NS - 2, Ci - 1 - i);
-    wait_vmcnt(ahead * PER);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    if (i + NS - 1 < Ci) issue(i + NS - 1, (i + NS - 1) % NS);
-    const char* st = lds + (i % NS) * STAGE;
-    const float* ar = reinterpret_cast<const float*>(st + CDMA_KC * CDMA_NT * 8);
-    const float2 av = make_float2(ar[tid], ar[CDMA_NT + tid]);
-    const float2* ws = reinterpret_cast<const float2*>(st);
-#pragma unroll
-    for (int k = 0; k < CDMA_KC; ++k) {
-      const float2 wv = ws[k * CDMA_NT + tid];
-      acc[k].x = fmaf(av.x, wv.x, fmaf(-av.y, wv.y, acc[k].x));
-      acc[k].y = fmaf(av.x, wv.y, fmaf(av.y, wv.x, acc[k].y));
-    }
-  }
-  if (n < T) {
-#pragma unroll
-    for (int k = 0; k < CDMA_KC; ++k)
-      if (k0 + k < Co) {
-        Y[(int64_t)(k0 + k) * ldT + t] = acc[k].x;
-        Y[(int64_t)(Co + k0 + k) * ldT + t] = acc[k].y;
-      }
-  }
-}
-
 // MSFNO_CONTRACT_DMA=0 keeps the register-load kernel at batch 1 (A/B)
 static bool contract_dma() {
   static const bool on = [] {
@@ -1669,41 +1591,6 @@ int launch_compl_contract(const float* a, const float* w, float* y, int B, int C
   }
   return even ? launch_contract_t<1, 16, 2>(a, w, y, B, Ci, Co, T, s)
               : launch_contract_t<1, 16, 1>(a, w, y, B, Ci, Co, T, s);
-}
-
-// MSFNO_LIN_DIRECT=1: the contraction on S itself (bitwise equal to the gathered form,
-// tests/test_gpu_linear_direct.py) instead of spec_to_tril -> contract -> tril_to_spec.
-// Opt-in: its 4-B activation gathers fetch a 64-B line per mode per channel, as many
-// line requests as the weight stream itself: 10.31 ms vs 5.66 ms per field
-// (profiles/r04_v4).  Read at every call (the carve covers both forms).
-static bool lin_direct_env() {
-  const char* e = getenv("MSFNO_LIN_DIRECT");
-  return e && e[0] == '1';
-}
-
-bool contract_spec_ok(const msfno_sht_plan_s& p, const float* w, int B) {
-  return B == 1 && p.d_tcol && p.spec.T % 2 == 0 && p.spec.T >= 8 && contract_dma() &&
-         lin_direct_env() && (reinterpret_cast<uintptr_t>(w) & 15) == 0;
-}
-
-int launch_contract_spec(const msfno_sht_plan_s& p, const float* S, const float* w, float* Y,
-                         int C, hipStream_t s) {
-  const SpecLayout& L = p.spec;
-  MSFNO_REQUIRE(contract_spec_ok(p, w, 1) && S != Y, MSFNO_EINVAL,
-                "contract_spec: batch 1, a full plan, even T, 16-B aligned weight, out of place");
-  const int nkc = (int)cdiv(C, CDMA_KC);
-  const int64_t nmt = cdiv(L.T, CDMA_NT);
-  MSFNO_REQUIRE(nmt * nkc < (1LL << 31), MSFNO_EINVAL, "contract grid too large");
-  hipLaunchKernelGGL(compl_contract_spec_kernel<2>, dim3((unsigned)(nmt * nkc)), dim3(256), 0, s,
-                     S, w, Y, p.d_tcol, C, C, L.T, L.ldT, nkc);
-  MSFNO_TRY(launch_check("compl_contract_spec"));
-  if (p.npad > 0) {
-    const int64_t n = 2LL * C * p.npad;
-    hipLaunchKernelGGL(zero_spec_pads_kernel, dim3((unsigned)std::min<int64_t>(cdiv(n, 256), 4096)),
-                       dim3(256), 0, s, Y, p.d_tpad, p.npad, 2 * C, L.ldT);
-    MSFNO_TRY(launch_check("zero_spec_pads"));
-  }
-  return MSFNO_OK;
 }
 
 // compl_mul2d_fwd_c in reference layout (standalone op, not on the fused path):

@@ -47,7 +47,6 @@ VARIANTS = [
     {"MSFNO_LEG_X3F": "0"},
     {"MSFNO_X3F_NS": "2"},
     {"MSFNO_SKIP_H": "0"},
-    {"MSFNO_LIN_DIRECT": "1"},
 ]
 
 
