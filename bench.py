@@ -100,7 +100,7 @@ STAGE_KERNEL_LINEAR = {
 }
 X6_STAGES = {"mlp_fc1", "mlp_fc2", "inner_skip", "mlp_fused"}
 X6_SPEC_STAGES = {"spectral_l0", "spectral_l1", "spectral_l2", "spectral_out"}
-X3H_STAGES = {"inner_skip", "mlp_fused"} | X6_SPEC_STAGES
+X3H_STAGES = {"inner_skip", "mlp_fused", "mlp_gen"} | X6_SPEC_STAGES
 
 
 def leg_x3h():
@@ -494,13 +494,16 @@ def run_net(args, rank, world, dev, dist, backend):
 
 def net_roofline(stages, args, B):
     """Config 3's dominant kernel: of the profiled stages whose work is known for the
-    network (the encoder + decoder fc1 / fc2 GEMMs, 73 -> 256 -> 256 and 329 -> 256 ->
+    network (the fused encoder + decoder MLPs or their fc1 / fc2 GEMMs, 73 -> 256 -> 256 and 329 -> 256 ->
     73 at the full grid; the 12 block MLPs, 11 on the 120x240 grid and the last at the
     full grid), the one with the most device time per step; work and time summed over
     the step's launches of it."""
     C, P = args.C, args.nlat * args.nlon
     P_in = 120 * 240
     work = {
+        # encoder 73 -> C -> C and decoder (C + 73) -> C -> 73, each one fused x3h launch
+        # (csrc/mlp_gen_h.hip; MSFNO_MLP_GEN_H=0: the fc1 / fc2 GEMM pairs below)
+        "mlp_gen": 2 * B * P * C * ((73 + C) + (C + 73 + 73)),
         "mlp_fc1": 2 * B * P * C * (73 + (C + 73)),
         "mlp_fc2": 2 * B * P * C * (C + 73),
         "mlp_fused": 4 * B * C * (2 * C) * (11 * P_in + P),

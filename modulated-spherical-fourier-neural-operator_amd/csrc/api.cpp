@@ -157,7 +157,7 @@ static const char* kStageNames[MSFNO_PROF_NSTAGES] = {
     "spectral_l1", "spectral_l2", "spectral_l3", "spectral_out", "linear_gather",
     "linear_contract", "linear_scatter", "legendre_inv", "transpose_inv", "fft_inv",
     "inner_skip", "norm1_film_fold", "mlp_fc1", "mlp_fc2", "out_affine", "band_pack",
-    "band_exchange", "mlp_fused", "end"};
+    "band_exchange", "mlp_fused", "mlp_gen", "end"};
 
 struct Profiler {
   bool on = false;
@@ -1847,6 +1847,8 @@ extern "C" {
 
 size_t msfno_mlp_workspace_size(const msfno_mlp_desc* d, int B, long long P) {
   if (!d || B <= 0 || P <= 0) return 0;
+  if (mlp_gen_h_supported(d->Cin + d->Cin2, d->Hid, d->Cout))
+    return mlp_gen_h_workspace(d->Cin + d->Cin2, d->Hid, d->Cout);
   Carve cv;
   cv.take<float>(std::max<int64_t>((int64_t)B * d->Hid * P, mlp_h_floats(B, d->Hid, P)));  // h
   // first half of fc1 (two-GEMM concatenation on the fp32 engine only)
@@ -1870,6 +1872,14 @@ int msfno_mlp_forward(const msfno_mlp_desc* d, const float* x, const float* x2,
   MSFNO_REQUIRE(ws_bytes >= msfno_mlp_workspace_size(d, B, P), MSFNO_EWORKSPACE,
                 "workspace too small");
   hipStream_t s = (hipStream_t)stream;
+  if (mlp_gen_h_supported(d->Cin + d->Cin2, d->Hid, d->Cout)) {
+    // one fused x3h launch, the hidden activation on-chip (mlp_gen_h.hip)
+    prof(ST_MLP_GEN, s);
+    MSFNO_TRY(launch_mlp_gen_h(x, x2, d->Cin, d->Cin2, d->fc1_w, d->fc1_b, d->fc2_w, d->fc2_b,
+                               d->Hid, d->Cout, addend, add_bstride, out, B, P, ws, ws_bytes, s));
+    prof(ST_END, s);
+    return MSFNO_OK;
+  }
   Carve cv;
   cv.base = (char*)ws;
   const int64_t Hd = d->Hid, Ct = d->Cin + d->Cin2;

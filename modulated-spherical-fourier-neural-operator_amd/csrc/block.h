@@ -11,7 +11,7 @@ enum Stage {
   ST_FFT_FWD = 0, ST_NORM0, ST_TRANSPOSE_FWD, ST_LEG_FWD, ST_SPEC_PREP, ST_SPEC_L0, ST_SPEC_L1,
   ST_SPEC_L2, ST_SPEC_L3, ST_SPEC_OUT, ST_LIN_GATHER, ST_LIN_CONTRACT, ST_LIN_SCATTER, ST_LEG_INV,
   ST_TRANSPOSE_INV, ST_FFT_INV, ST_SKIP, ST_NORM1, ST_FC1, ST_FC2, ST_OUT_AFFINE, ST_BAND_PACK,
-  ST_BAND_EXCHANGE, ST_MLP_FUSED, ST_END
+  ST_BAND_EXCHANGE, ST_MLP_FUSED, ST_MLP_GEN, ST_END
 };
 void prof(int stage, hipStream_t s);
 

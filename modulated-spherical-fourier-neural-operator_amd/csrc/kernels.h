@@ -105,6 +105,14 @@ int launch_mlp_fused(const float* x1, const float* scale, const float* shift, co
 // mlp_fused_h.hip: the MLP on the x3h engine (fp32 as two fp16 terms, three fp16
 // MFMAs per product, row-scaled weights); default (MSFNO_ENGINE=x6 selects the x6 engine)
 bool mlp_fused_h_env();
+// mlp_gen_h.hip: the standalone MLP (network encoder / decoder) fused on the x3h engine,
+// per-pixel range scales; widths (Cin + Cin2, Cout) of the instantiated kernels only
+bool mlp_gen_h_supported(int Ct, int H, int Cout);
+size_t mlp_gen_h_workspace(int Ct, int H, int Cout);
+int launch_mlp_gen_h(const float* x, const float* x2, int Cin, int Cin2, const float* W1,
+                     const float* b1, const float* W2, const float* b2, int H, int Cout,
+                     const float* addend, int64_t add_bstride, float* out, int B, int64_t P,
+                     void* ws, size_t ws_bytes, hipStream_t s);
 // inner skip at C = 256 on the mlp_fused_h tiling (x3h): out = Ws·x + bs, x scaled by the
 // power-of-two channel scales xs (|xs x| < 2^14), or per pixel in-kernel when xs is null;
 // ws >= skip_h_workspace(B)
