@@ -148,6 +148,17 @@ size_t msfno_block_workspace_size(const msfno_block_desc* d, msfno_sht_plan_t fw
 int msfno_block_forward(const msfno_block_desc* d, msfno_sht_plan_t fwd, msfno_sht_plan_t inv,
                         const float* x, const float* gamma, const float* beta, float film_scale,
                         float* out, int B, void* ws, size_t ws_bytes, void* stream);
+/* The same block stopped before its output affine (blocks without MLP and outer skip:
+ * the network's last block, sfnonet.py:838-846): x1_out (B,C,nlat_out,nlon_out) gets the
+ * block's pre-norm1 state and affine_out (2*B*C) the per-(b,c) norm1 (+ FiLM) affine as
+ * [scale (B*C)][shift (B*C)]; out = scale * x1 + shift.  The network hands both to
+ * msfno_mlp_forward_affine (the decoder), so the affine pass over the full grid is
+ * folded into the decoder's input loads.  Workspace: msfno_block_workspace_size. */
+int msfno_block_forward_deferred(const msfno_block_desc* d, msfno_sht_plan_t fwd,
+                                 msfno_sht_plan_t inv, const float* x, const float* gamma,
+                                 const float* beta, float film_scale, float* x1_out,
+                                 float* affine_out, int B, void* ws, size_t ws_bytes,
+                                 void* stream);
 /* SpectralFilterLayer.forward alone (sfnonet.py:132-133): SHT -> filter -> ISHT,
  * no norms.  x (B,C,nlat_in,nlon_in) -> y (B,C,nlat_out,nlon_out). */
 int msfno_filter_forward(const msfno_block_desc* d, msfno_sht_plan_t fwd, msfno_sht_plan_t inv,
@@ -171,6 +182,16 @@ typedef struct msfno_mlp_desc {
 } msfno_mlp_desc;
 
 size_t msfno_mlp_workspace_size(const msfno_mlp_desc* d, int B, long long P);
+/* 1 when the widths (Cin + Cin2, Hid, Cout) have the one-launch fused x3h kernel
+ * (the encoder 73 -> 256 -> 256 and decoder 329 -> 256 -> 73 of the reference config). */
+int msfno_mlp_fused_supported(const msfno_mlp_desc* d);
+/* msfno_mlp_forward with x replaced by x_scale[b][c] * x + x_shift[b][c] (c < Cin; the
+ * affine_out of msfno_block_forward_deferred); fused widths only (MSFNO_EUNSUPPORTED
+ * otherwise).  Workspace: msfno_mlp_workspace_size. */
+int msfno_mlp_forward_affine(const msfno_mlp_desc* d, const float* x, const float* x_scale,
+                             const float* x_shift, const float* x2, const float* addend,
+                             long long add_bstride, float* out, int B, long long P, void* ws,
+                             size_t ws_bytes, void* stream);
 int msfno_mlp_forward(const msfno_mlp_desc* d, const float* x, const float* x2,
                       const float* addend, long long add_bstride, float* out, int B,
                       long long P, void* ws, size_t ws_bytes, void* stream);

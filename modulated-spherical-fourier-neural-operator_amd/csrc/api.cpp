@@ -1702,9 +1702,15 @@ int msfno_filter_forward(const msfno_block_desc* d, msfno_sht_plan_t f, msfno_sh
   return MSFNO_OK;
 }
 
-int msfno_block_forward(const msfno_block_desc* d, msfno_sht_plan_t f, msfno_sht_plan_t g,
-                        const float* x, const float* gamma, const float* beta, float film_scale,
-                        float* out, int B, void* ws, size_t ws_bytes, void* stream) {
+}  // extern "C"
+
+// x1_ext / aff_out (both or neither; blocks without MLP and outer skip): the block stops
+// before its output affine, leaving x1 in x1_ext and the per-(b,c) norm1 (+ FiLM) affine
+// in aff_out = [scale (B*C)][shift (B*C)] for the consumer to apply (the decoder MLP)
+static int block_forward_impl(const msfno_block_desc* d, msfno_sht_plan_t f, msfno_sht_plan_t g,
+                              const float* x, const float* gamma, const float* beta,
+                              float film_scale, float* out, float* x1_ext, float* aff_out, int B,
+                              void* ws, size_t ws_bytes, void* stream) {
   MSFNO_TRY(check_pair(d, f, g));
   MSFNO_REQUIRE(ws_bytes >= msfno_block_workspace_size(d, f, g, B), MSFNO_EWORKSPACE,
                 "workspace too small");
@@ -1729,7 +1735,7 @@ int msfno_block_forward(const msfno_block_desc* d, msfno_sht_plan_t f, msfno_sht
   // buffer (dead until the inverse FFT, which runs after the skip GEMM): the skip
   // GEMM is forked after the forward FFT and stages B by LDS-DMA (gemm_x6p) instead
   // of splitting fp32 x in-kernel.
-  float* x1 = b.x1;
+  float* x1 = x1_ext ? x1_ext : b.x1;
   std::shared_ptr<SideCtx> side;
   const bool xpl = skip_planes(d, f, b);
   const C2RPlanes xp{b.x1p, (int)C, f->nlat};
@@ -1793,7 +1799,11 @@ int msfno_block_forward(const msfno_block_desc* d, msfno_sht_plan_t f, msfno_sht
                                d->norm_eps, gamma, beta, film_scale, b.sc1, b.sh1, s, nullptr,
                                nullptr, b.ab1));
   const float* resid = d->outer_skip == MSFNO_SKIP_IDENTITY ? x : nullptr;
-  if (d->has_mlp) {
+  if (aff_out) {
+    MSFNO_CHECK_HIP(hipMemcpyAsync(aff_out, b.sc1, BC * sizeof(float), hipMemcpyDeviceToDevice, s));
+    MSFNO_CHECK_HIP(
+        hipMemcpyAsync(aff_out + BC, b.sh1, BC * sizeof(float), hipMemcpyDeviceToDevice, s));
+  } else if (d->has_mlp) {
     MSFNO_TRY(run_block_mlp(d, x1, x1p, b.sc1, b.sh1, b.ab1, b.W1f, b.b1f, b.h, b.mfimg, out, resid, B,
                             P, b.dw, s));
   } else {
@@ -1802,6 +1812,27 @@ int msfno_block_forward(const msfno_block_desc* d, msfno_sht_plan_t f, msfno_sht
   }
   prof(ST_END, s);
   return MSFNO_OK;
+}
+
+extern "C" {
+
+int msfno_block_forward(const msfno_block_desc* d, msfno_sht_plan_t f, msfno_sht_plan_t g,
+                        const float* x, const float* gamma, const float* beta, float film_scale,
+                        float* out, int B, void* ws, size_t ws_bytes, void* stream) {
+  return block_forward_impl(d, f, g, x, gamma, beta, film_scale, out, nullptr, nullptr, B, ws,
+                            ws_bytes, stream);
+}
+
+int msfno_block_forward_deferred(const msfno_block_desc* d, msfno_sht_plan_t f,
+                                 msfno_sht_plan_t g, const float* x, const float* gamma,
+                                 const float* beta, float film_scale, float* x1_out,
+                                 float* affine_out, int B, void* ws, size_t ws_bytes,
+                                 void* stream) {
+  MSFNO_REQUIRE(d && x1_out && affine_out, MSFNO_EINVAL, "block_forward_deferred: null output");
+  MSFNO_REQUIRE(!d->has_mlp && d->outer_skip == MSFNO_SKIP_NONE, MSFNO_EUNSUPPORTED,
+                "block_forward_deferred: blocks without MLP and outer skip only");
+  return block_forward_impl(d, f, g, x, gamma, beta, film_scale, nullptr, x1_out, affine_out, B,
+                            ws, ws_bytes, stream);
 }
 
 int msfno_profile_mark(int stage, void* stream) {
@@ -1859,6 +1890,30 @@ size_t msfno_mlp_workspace_size(const msfno_mlp_desc* d, int B, long long P) {
   return cv.off;
 }
 
+int msfno_mlp_fused_supported(const msfno_mlp_desc* d) {
+  return d && mlp_gen_h_supported(d->Cin + d->Cin2, d->Hid, d->Cout) ? 1 : 0;
+}
+
+int msfno_mlp_forward_affine(const msfno_mlp_desc* d, const float* x, const float* x_scale,
+                             const float* x_shift, const float* x2, const float* addend,
+                             long long add_bstride, float* out, int B, long long P, void* ws,
+                             size_t ws_bytes, void* stream) {
+  MSFNO_REQUIRE(d && x && x_scale && x_shift && out && d->fc1_w && d->fc1_b && d->fc2_w,
+                MSFNO_EINVAL, "mlp_forward_affine: missing tensors");
+  MSFNO_REQUIRE(msfno_mlp_fused_supported(d), MSFNO_EUNSUPPORTED,
+                "mlp_forward_affine: widths without the fused x3h kernel");
+  MSFNO_REQUIRE((d->Cin2 > 0) == (x2 != nullptr) && B > 0 && P > 0 &&
+                    ws_bytes >= msfno_mlp_workspace_size(d, B, P),
+                MSFNO_EINVAL, "mlp_forward_affine: bad arguments");
+  hipStream_t s = (hipStream_t)stream;
+  prof(ST_MLP_GEN, s);
+  MSFNO_TRY(launch_mlp_gen_h(x, x_scale, x_shift, x2, d->Cin, d->Cin2, d->fc1_w, d->fc1_b, d->fc2_w,
+                             d->fc2_b, d->Hid, d->Cout, addend, add_bstride, out, B, P, ws,
+                             ws_bytes, s));
+  prof(ST_END, s);
+  return MSFNO_OK;
+}
+
 int msfno_mlp_forward(const msfno_mlp_desc* d, const float* x, const float* x2,
                       const float* addend, long long add_bstride, float* out, int B,
                       long long P, void* ws, size_t ws_bytes, void* stream) {
@@ -1875,7 +1930,7 @@ int msfno_mlp_forward(const msfno_mlp_desc* d, const float* x, const float* x2,
   if (mlp_gen_h_supported(d->Cin + d->Cin2, d->Hid, d->Cout)) {
     // one fused x3h launch, the hidden activation on-chip (mlp_gen_h.hip)
     prof(ST_MLP_GEN, s);
-    MSFNO_TRY(launch_mlp_gen_h(x, x2, d->Cin, d->Cin2, d->fc1_w, d->fc1_b, d->fc2_w, d->fc2_b,
+    MSFNO_TRY(launch_mlp_gen_h(x, nullptr, nullptr, x2, d->Cin, d->Cin2, d->fc1_w, d->fc1_b, d->fc2_w, d->fc2_b,
                                d->Hid, d->Cout, addend, add_bstride, out, B, P, ws, ws_bytes, s));
     prof(ST_END, s);
     return MSFNO_OK;

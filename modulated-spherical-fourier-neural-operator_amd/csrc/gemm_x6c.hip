@@ -302,14 +302,19 @@ __global__ void split3m_kernel(const float* __restrict__ S, unsigned short* __re
 // for the k-tile DMA, 2 no DMA in the loop at all (stale stages), 4 no MFMAs
 // LAY: bit 1 = B planes read in the tiled layout, bit 2 = planes written tiled
 // NS: LDS stages (2; 3 for the x3h DMA-fed layers: two k-tiles in flight, 144 KB)
+// BM_: tile rows (128, or 64 for grids that would not fill the chip: the 120 x 240
+// blocks of the network, N = 7,260 modes, 57 column tiles)
 template <bool PLANES_OUT, int WGM = 4, int WGN = 2, bool BF32 = false, int DBG = 0, int LAY = 0,
-          int NP = 3, int NS = 2>
+          int NP = 3, int NS = 2, int BM_ = X6C_BM>
 __global__ __launch_bounds__(64 * WGM * WGN) void gemm_x6c_kernel(X6CParams p) {
-  constexpr int BM = X6C_BM, BN = X6C_BN, BK = X6C_BK;
+  constexpr int BM = BM_, BN = X6C_BN, BK = X6C_BK;
   constexpr int NW = WGM * WGN;
   constexpr int NMP = 3 * NP;                 // matrix-planes per operand
-  constexpr int APC = 4 * NMP;                // A pieces (1 KB) per k-tile
-  constexpr int NPC = BF32 ? (APC + NW - 1) / NW : 2 * APC / NW;  // DMA pieces per wave and k-tile
+  constexpr int APC = (BM / 32) * NMP;        // A pieces (1 KB: 32 rows x 16 k) per k-tile
+  constexpr int BPC = 4 * NMP;                // B pieces (1 KB: 4 k rows x 128) per k-tile
+  static_assert(BM % 32 == 0 && X6C_BM % BM == 0, "tile rows");
+  static_assert(BF32 || (APC + BPC) % NW == 0, "DMA pieces per wave");
+  constexpr int NPC = BF32 ? (APC + NW - 1) / NW : (APC + BPC) / NW;  // DMA pieces per wave and k-tile
   constexpr int WM = BM / WGM, WN = BN / WGN;
   constexpr int MT = WM / 32, NT = WN / 32;
   constexpr int A_PLANE = BM * BK, B_PLANE = BK * BN;  // 16-bit elements per matrix plane
@@ -320,7 +325,7 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_x6c_kernel(X6CParams p) {
   constexpr int RING_BYTES = NSTAGE * STAGE * 2;
   constexpr int EPI_BYTES = 32 * WGM * (BN + 8) * 4;
   constexpr int LDS_BYTES = RING_BYTES > EPI_BYTES ? RING_BYTES : EPI_BYTES;
-  static_assert(STAGE * 2 == 2 * APC * 1024, "stage = A + B pieces of 1 KB");
+  static_assert(STAGE * 2 == (APC + BPC) * 1024, "stage = A + B pieces of 1 KB");
   // the x3h engine writes hidden planes in the tiled layout only
   static_assert(NP == 3 || !PLANES_OUT || (LAY & 2) != 0, "x3h: tiled plane output only");
   typedef typename X6CEng<NP>::frag Frag;
@@ -354,7 +359,7 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_x6c_kernel(X6CParams p) {
       dst[q] = 0;
       brow[q] = -2;
     } else if (c < APC) {
-      const int mp = c >> 2, mb = c & 3;
+      const int mp = c / (BM / 32), mb = c % (BM / 32);
       const int mat = mp / NP, pl = mp - NP * mat;
       const int m = 32 * mb + (lane >> 1);
       const int h = (lane & 1) ^ ((m >> 3) & 1);
@@ -927,6 +932,22 @@ int gemm_x3c(const unsigned short* Aw, int co, int ci, const float* Sin, int ldS
     const char* e = getenv("MSFNO_X3C_NS");
     return (e && e[0] == '2') ? 2 : 3;
   }();
+  // grids that would not fill the chip twice (the network's 120 x 240 blocks: 57 column
+  // tiles) take 64-row tiles of four waves, two stages, two workgroups per CU
+  // (MSFNO_X3C_BM64=0 keeps the 128-row tiles)
+  static const bool bm64_on = [] {
+    const char* e = getenv("MSFNO_X3C_BM64");
+    return !(e && e[0] == '0');
+  }();
+  if (!Sin && bm64_on && (int64_t)p.tiles_m * p.tiles_n * B < 2 * 256) {
+    p.tiles_m = p.Mp / 64;
+    const dim3 g64(p.tiles_m * p.tiles_n, 1, B);
+    if (Y)
+      hipLaunchKernelGGL((gemm_x6c_kernel<true, 2, 2, false, 0, 3, 2, 2, 64>), g64, dim3(256), 0, s, p);
+    else
+      hipLaunchKernelGGL((gemm_x6c_kernel<false, 2, 2, false, 0, 1, 2, 2, 64>), g64, dim3(256), 0, s, p);
+    return launch_check("gemm_x3c");
+  }
   if (Sin)
     hipLaunchKernelGGL((gemm_x6c_kernel<true, 4, 2, true, 0, 2, 2>), grid, dim3(512), 0, s, p);
   else if (Y && ns == 3)

@@ -109,7 +109,10 @@ bool mlp_fused_h_env();
 // per-pixel range scales; widths (Cin + Cin2, Cout) of the instantiated kernels only
 bool mlp_gen_h_supported(int Ct, int H, int Cout);
 size_t mlp_gen_h_workspace(int Ct, int H, int Cout);
-int launch_mlp_gen_h(const float* x, const float* x2, int Cin, int Cin2, const float* W1,
+// xa, xt (both or neither): [B][Cin] per-channel affine applied to x first (a deferred
+// norm / FiLM of the producing block)
+int launch_mlp_gen_h(const float* x, const float* xa, const float* xt, const float* x2, int Cin,
+                     int Cin2, const float* W1,
                      const float* b1, const float* W2, const float* b2, int H, int Cout,
                      const float* addend, int64_t add_bstride, float* out, int B, int64_t P,
                      void* ws, size_t ws_bytes, hipStream_t s);

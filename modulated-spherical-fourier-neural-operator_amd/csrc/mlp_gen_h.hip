@@ -50,7 +50,7 @@ constexpr int MG_TILE = 1024;   // fp16 per 2-KB tile (two 512-element planes)
 constexpr int MG_SLICE = 8;     // tiles per 16-KB slice
 constexpr int MG_NS = 4;        // ring slots
 constexpr int MG_WAVES = 4;
-constexpr int MG_H_MAX = 512;
+constexpr int MG_H_MAX = 256;
 
 __host__ __device__ constexpr int mg_round8(int n) { return (n + 7) & ~7; }
 
@@ -99,15 +99,24 @@ __device__ __forceinline__ void mg_for(F&& f) {
 }
 
 // ---- weight image ------------------------------------------------------------------
-// eta_j = 2^-ceil(log2 L_j), L_j = max(||W1_j||_1, |b1_j|); W1 (H x Ct)
-__global__ void mg_eta_kernel(const float* __restrict__ W1, const float* __restrict__ b1, int H,
-                              int Ct, float* __restrict__ eta) {
-  const int r = blockIdx.x * blockDim.x + threadIdx.x;
-  if (r >= H) return;
+// eta_j = 2^-ceil(log2 L_j), L_j = max(||W1_j||_1, |b1_j|); W1 (H x Ct).  One 256-thread
+// workgroup per row (the row sum in fp64, a fixed reduction order)
+__global__ __launch_bounds__(256) void mg_eta_kernel(const float* __restrict__ W1,
+                                                     const float* __restrict__ b1, int Ct,
+                                                     float* __restrict__ eta) {
+  __shared__ double red[256];
+  const int r = blockIdx.x, t = threadIdx.x;
   const float* row = W1 + (int64_t)r * Ct;
   double l1 = 0.0;
-  for (int k = 0; k < Ct; ++k) l1 += fabs((double)row[k]);
-  const double L = fmax(l1, fabs((double)b1[r])) * (1.0 + 1e-6);
+  for (int k = t; k < Ct; k += 256) l1 += fabs((double)row[k]);
+  red[t] = l1;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (t < o) red[t] += red[t + o];
+    __syncthreads();
+  }
+  if (t != 0) return;
+  const double L = fmax(red[0], fabs((double)b1[r])) * (1.0 + 1e-6);
   float e = 1.f;
   if (L > 0.0 && L < 1e30) {
     int x;
@@ -118,23 +127,30 @@ __global__ void mg_eta_kernel(const float* __restrict__ W1, const float* __restr
 }
 
 // row scales 2^(15 - e), max |row| = f 2^e (W2 rows taken as W2 diag(1 / eta)); inverses
-// into is1 [H] / is2 [16 OT] (0 past Cout)
-__global__ void mg_scale_kernel(const float* __restrict__ W1, const float* __restrict__ W2,
-                                const float* __restrict__ eta, int H, int Ct, int Cout, int Cp,
-                                float* __restrict__ s1, float* __restrict__ s2,
-                                float* __restrict__ is1, float* __restrict__ is2) {
-  const int r = blockIdx.x * blockDim.x + threadIdx.x;
-  if (r >= H + Cp) return;
+// into is1 [H] / is2 [16 OT] (0 past Cout).  One 256-thread workgroup per row
+__global__ __launch_bounds__(256) void mg_scale_kernel(
+    const float* __restrict__ W1, const float* __restrict__ W2, const float* __restrict__ eta,
+    int H, int Ct, int Cout, float* __restrict__ s1, float* __restrict__ s2,
+    float* __restrict__ is1, float* __restrict__ is2) {
+  __shared__ float red[256];
+  const int r = blockIdx.x, t = threadIdx.x;
   const bool first = r < H;
   if (!first && r - H >= Cout) {
-    s2[r - H] = 0.f;
-    is2[r - H] = 0.f;
+    if (t == 0) { s2[r - H] = 0.f; is2[r - H] = 0.f; }
     return;
   }
   const float* row = first ? W1 + (int64_t)r * Ct : W2 + (int64_t)(r - H) * H;
   const int n = first ? Ct : H;
   float m = 0.f;
-  for (int k = 0; k < n; ++k) m = fmaxf(m, fabsf(first ? row[k] : row[k] / eta[k]));
+  for (int k = t; k < n; k += 256) m = fmaxf(m, fabsf(first ? row[k] : row[k] / eta[k]));
+  red[t] = m;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (t < o) red[t] = fmaxf(red[t], red[t + o]);
+    __syncthreads();
+  }
+  if (t != 0) return;
+  m = red[0];
   float sc = 1.f;
   if (m > 0.f && isfinite(m)) {
     int e;
@@ -196,6 +212,8 @@ __global__ void mg_image_kernel(const float* __restrict__ W1, const float* __res
 struct MlpGParams {
   const float* x;       // [B][Cin][P]
   const float* x2;      // [B][Cin2][P] or null
+  const float* xa;      // [B][Cin] per-channel affine of x (x -> xa x + xt) or null
+  const float* xt;      // [B][Cin]
   const float* addend;  // [.][Cout][P] (batch stride add_bstride) or null
   float* out;           // [B][Cout][P]
   const unsigned short* img;
@@ -238,13 +256,15 @@ __global__ __launch_bounds__(256, 2) void mlp_gen_h_kernel(MlpGParams p) {
   constexpr int NU = mg_round8(NT1 + NT2);       // tiles per middle unit
   constexpr int N0 = mg_round8(NT1);
   constexpr int CP = 16 * OT;
-  __shared__ __attribute__((aligned(16))) char lds_raw[RING_BYTES + (3 * MG_H_MAX + 2 * CP) * 4];
+  __shared__ __attribute__((aligned(16))) char lds_raw[RING_BYTES + (3 * MG_H_MAX + 2 * CP + 64 * KS) * 4];
   unsigned short* const ring = reinterpret_cast<unsigned short*>(lds_raw);
   float* const b1s = reinterpret_cast<float*>(lds_raw + RING_BYTES);
   float* const is1s = b1s + MG_H_MAX;
   float* const etas = is1s + MG_H_MAX;
   float* const b2s = etas + MG_H_MAX;
   float* const is2s = b2s + CP;
+  float* const xas = is2s + CP;  // deferred input affine [32 KS]
+  float* const xts = xas + 32 * KS;
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r16 = lane & 15, g = lane >> 4;
@@ -283,6 +303,7 @@ __global__ __launch_bounds__(256, 2) void mlp_gen_h_kernel(MlpGParams p) {
       else if (c - p.Cin < p.Cin2) v = __builtin_nontemporal_load(x2b + (int64_t)(c - p.Cin) * P);
       xv[ks][e] = v;
     }
+
   for (int i = tid; i < H; i += 64 * W) {
     b1s[i] = p.b1[i];
     is1s[i] = p.is1[i];
@@ -291,6 +312,26 @@ __global__ __launch_bounds__(256, 2) void mlp_gen_h_kernel(MlpGParams p) {
   for (int i = tid; i < CP; i += 64 * W) {
     b2s[i] = (p.b2 && i < p.Cout) ? p.b2[i] : 0.f;
     is2s[i] = p.is2[i];
+  }
+  if (p.xa) {  // the producer's deferred per-channel affine (channels < Cin, 0 beyond)
+    for (int i = tid; i < 32 * KS; i += 64 * W) {
+      const bool in = i < p.Cin;
+      xas[i] = in ? p.xa[(int64_t)z * p.Cin + i] : 1.f;
+      xts[i] = in ? p.xt[(int64_t)z * p.Cin + i] : 0.f;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      const int c0 = 32 * ks + 8 * g;
+      const float4 a0 = *reinterpret_cast<const float4*>(xas + c0);
+      const float4 a1 = *reinterpret_cast<const float4*>(xas + c0 + 4);
+      const float4 t0 = *reinterpret_cast<const float4*>(xts + c0);
+      const float4 t1 = *reinterpret_cast<const float4*>(xts + c0 + 4);
+      const float av[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+      const float tv[8] = {t0.x, t0.y, t0.z, t0.w, t1.x, t1.y, t1.z, t1.w};
+#pragma unroll
+      for (int e = 0; e < 8; ++e) xv[ks][e] = fmaf(av[e], xv[ks][e], tv[e]);
+    }
   }
   // the pixel's bound M over all its channels (the four lanes r16, r16 + 16, ...)
   float m = 0.f;
@@ -410,7 +451,9 @@ __global__ __launch_bounds__(256, 2) void mlp_gen_h_kernel(MlpGParams p) {
 #pragma unroll
   for (int e2 = 0; e2 < 4; ++e2) conv_pair(HB - 1, e2, I1{});
   make_hb();
-  // the addend of every output row, in flight under the last unit's MFMAs
+  // the addend of every output row, in flight under the last unit's MFMAs (three
+  // workgroups per CU with half of it issued after that unit measured slower: 1.55 vs
+  // 1.33 ms for the encoder)
   float rv[OT][4];
   if (p.addend) {
     const float* ad = p.addend + (int64_t)z * p.add_bstride + pxc;
@@ -481,13 +524,14 @@ size_t mlp_gen_h_workspace(int Ct, int H, int Cout) {
   return (size_t)round_up(tiles * MG_TILE * 2, 256) + (size_t)(3 * H + 4 * 16 * ot) * 4 + 256;
 }
 
-int launch_mlp_gen_h(const float* x, const float* x2, int Cin, int Cin2, const float* W1,
+int launch_mlp_gen_h(const float* x, const float* xa, const float* xt, const float* x2, int Cin,
+                     int Cin2, const float* W1,
                      const float* b1, const float* W2, const float* b2, int H, int Cout,
                      const float* addend, int64_t add_bstride, float* out, int B, int64_t P,
                      void* ws, size_t ws_bytes, hipStream_t s) {
   const int Ct = Cin + Cin2;
   int KS, OT;
-  MSFNO_REQUIRE(x && W1 && b1 && W2 && out && B > 0 && P >= 1 && Cin > 0 && Cin2 >= 0 &&
+  MSFNO_REQUIRE((xa == nullptr) == (xt == nullptr) && x && W1 && b1 && W2 && out && B > 0 && P >= 1 && Cin > 0 && Cin2 >= 0 &&
                     (Cin2 == 0) == (x2 == nullptr) && mlp_gen_h_supported(Ct, H, Cout) &&
                     mg_shape(Ct, Cout, &KS, &OT) && ws && ws_bytes >= mlp_gen_h_workspace(Ct, H, Cout),
                 MSFNO_EINVAL, "mlp_gen_h: bad arguments");
@@ -504,16 +548,16 @@ int launch_mlp_gen_h(const float* x, const float* x2, int Cin, int Cin2, const f
     set_error("mlp_gen_h: image clear failed");
     return MSFNO_EHIP;
   }
-  hipLaunchKernelGGL(mg_eta_kernel, dim3(cdiv(H, 256)), dim3(256), 0, s, W1, b1, H, Ct, eta);
+  hipLaunchKernelGGL(mg_eta_kernel, dim3(H), dim3(256), 0, s, W1, b1, Ct, eta);
   MSFNO_TRY(launch_check("mg_eta"));
-  hipLaunchKernelGGL(mg_scale_kernel, dim3(cdiv(H + Cp, 256)), dim3(256), 0, s, W1, W2, eta, H, Ct,
-                     Cout, Cp, s1, s2, is1, is2);
+  hipLaunchKernelGGL(mg_scale_kernel, dim3(H + Cp), dim3(256), 0, s, W1, W2, eta, H, Ct, Cout, s1,
+                     s2, is1, is2);
   MSFNO_TRY(launch_check("mg_scale"));
   hipLaunchKernelGGL(mg_image_kernel, dim3(256), dim3(256), 0, s, W1, W2, eta, s1, s2, H, Ct, Cout,
                      KS, OT, img);
   MSFNO_TRY(launch_check("mg_image"));
   MlpGParams p{};
-  p.x = x; p.x2 = x2; p.addend = addend; p.out = out; p.img = img;
+  p.x = x; p.xa = xa; p.xt = xt; p.x2 = x2; p.addend = addend; p.out = out; p.img = img;
   p.is1 = is1; p.is2 = is2; p.eta = eta; p.b1 = b1; p.b2 = b2;
   p.P = P; p.add_bstride = add_bstride;
   p.Cin = Cin; p.Cin2 = Cin2; p.Cout = Cout; p.H = H;

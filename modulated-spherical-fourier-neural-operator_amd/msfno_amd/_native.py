@@ -89,9 +89,15 @@ SIGNATURES = [
     ("msfno_block_wcache_size", _sz, [ctypes.POINTER(BlockDesc)]),
     ("msfno_block_forward", _i, [ctypes.POINTER(BlockDesc), _vp, _vp, _vp, _vp, _vp, _f, _vp,
                                  _i, _vp, _sz, _vp]),
+    ("msfno_block_forward_deferred", _i, [ctypes.POINTER(BlockDesc), _vp, _vp, _vp, _vp, _vp, _f,
+                                          _vp, _vp, _i, _vp, _sz, _vp]),
     ("msfno_filter_forward", _i, [ctypes.POINTER(BlockDesc), _vp, _vp, _vp, _vp, _i, _vp, _sz,
                                   _vp]),
     ("msfno_mlp_workspace_size", _sz, [ctypes.POINTER(MlpDesc), _i, ctypes.c_longlong]),
+    ("msfno_mlp_fused_supported", _i, [ctypes.POINTER(MlpDesc)]),
+    ("msfno_mlp_forward_affine", _i, [ctypes.POINTER(MlpDesc), _vp, _vp, _vp, _vp, _vp,
+                                      ctypes.c_longlong, _vp, _i, ctypes.c_longlong, _vp, _sz,
+                                      _vp]),
     ("msfno_mlp_forward", _i, [ctypes.POINTER(MlpDesc), _vp, _vp, _vp, ctypes.c_longlong, _vp, _i,
                                ctypes.c_longlong, _vp, _sz, _vp]),
     ("msfno_block_film_backward_workspace_size", _sz, [ctypes.POINTER(BlockDesc), _vp, _vp, _i]),

@@ -135,6 +135,40 @@ class MLP(nn.Module):
         return out.to(dtype)
 
     @N.on_input_device
+    def native_forward_affine(self, x, x_scale, x_shift, x2=None, addend=None):
+        """native_forward of (x_scale * x + x_shift) per (batch, channel) — the deferred
+        output affine of the block that produced x (msfno_mlp_forward_affine; fused widths
+        only)."""
+        x = N.require_device_f32(x, "MLP input")
+        B, Cin, H, W = x.shape
+        xa = x_scale.detach().float().reshape(B, Cin).contiguous()
+        xt = x_shift.detach().float().reshape(B, Cin).contiguous()
+        cin2 = 0
+        if x2 is not None:
+            x2 = N.require_device_f32(x2, "MLP second input")
+            assert x2.shape[0] == B and x2.shape[2:] == x.shape[2:]
+            cin2 = x2.shape[1]
+        d, keep = self.native_desc(cin2)
+        if d.Cin != Cin:
+            raise ValueError(f"MLP expects {d.Cin} (+{cin2}) input channels, got {Cin}")
+        bstride = 0
+        if addend is not None:
+            addend = N.require_device_f32(addend, "MLP addend")
+            assert addend.shape[1:] == (d.Cout, H, W)
+            bstride = 0 if addend.shape[0] == 1 else d.Cout * H * W
+        L = N.lib()
+        P = H * W
+        nbytes = L.msfno_mlp_workspace_size(d, B, P)
+        ws = torch.empty(nbytes, dtype=torch.uint8, device=x.device)
+        out = torch.empty(B, d.Cout, H, W, dtype=torch.float32, device=x.device)
+        N.check(L.msfno_mlp_forward_affine(d, x.data_ptr(), xa.data_ptr(), xt.data_ptr(),
+                                           N.ptr(x2), N.ptr(addend), bstride, out.data_ptr(), B,
+                                           P, ws.data_ptr(), nbytes, N.stream_of(x.device)),
+                "MLP.forward_affine")
+        del keep
+        return out
+
+    @N.on_input_device
     def native_backward_input(self, x, dy, x2=None):
         """dL/dx of fc2(GELU(fc1(cat(x, x2)))) for frozen weights
         (msfno_mlp_backward_input): the decoder's backward in FiLM fine-tuning."""

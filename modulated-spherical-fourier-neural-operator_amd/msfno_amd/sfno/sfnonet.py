@@ -274,6 +274,42 @@ class FourierNeuralOperatorBlock(nn.Module):
     def forward(self, x, *overflow):
         return self._native_forward(x)
 
+    def defers_output_affine(self):
+        """True for blocks whose output is one per-channel affine of x1 (no MLP, no outer
+        skip: the network's last block), which msfno_block_forward_deferred can leave
+        to the consumer."""
+        d, _ = self.native_desc()
+        return d.has_mlp == 0 and d.outer_skip == N.SKIP_NONE
+
+    @N.on_input_device
+    def native_forward_deferred(self, x, gamma=None, beta=None, scale=1.0):
+        """(x1, affine) with out = affine[0] * x1 + affine[1] per (b, c): the block without
+        its output affine pass (msfno_block_forward_deferred)."""
+        x = N.require_device_f32(x, "block input")
+        B, C, H, W = x.shape
+        fwd, inv = self._transforms()
+        assert H == fwd.nlat and W == fwd.nlon and C == self.embed_dim_sfno
+        pf = fwd._plan(x.device)
+        pi = inv._plan(x.device)
+        d, keep = self.native_desc()
+        if gamma is not None:
+            gamma = gamma.detach().float().reshape(B, C).contiguous()
+            beta = beta.detach().float().reshape(B, C).contiguous()
+        L = N.lib()
+        wkey = self.wcache_attach(d, keep, x.device)
+        nbytes = L.msfno_block_workspace_size(d, pf.handle, pi.handle, B)
+        ws = torch.empty(nbytes, dtype=torch.uint8, device=x.device)
+        x1 = torch.empty(B, C, inv.nlat, inv.nlon, dtype=torch.float32, device=x.device)
+        aff = torch.empty(2, B, C, dtype=torch.float32, device=x.device)
+        N.check(L.msfno_block_forward_deferred(d, pf.handle, pi.handle, x.data_ptr(),
+                                               N.ptr(gamma), N.ptr(beta), float(scale),
+                                               x1.data_ptr(), aff.data_ptr(), B, ws.data_ptr(),
+                                               nbytes, N.stream_of(x.device)),
+                type(self).__name__ + ".forward_deferred")
+        self.wcache_commit(wkey)
+        del keep
+        return x1, aff
+
 
 class FourierNeuralOperatorBlock_Filmed(FourierNeuralOperatorBlock):
     _filmed = True
@@ -482,6 +518,23 @@ class FourierNeuralOperatorNet(nn.Module):
             return _MLPFn.apply(x, x2, None, self.decoder)
         return self.decoder.native_forward(x, x2=x2)
 
+    def _fuse_last_affine(self, x):
+        """Whether the last block's output affine can ride in the decoder's input loads
+        (inference, a last block without MLP / outer skip, a fused decoder); x is the
+        network input (the decoder's second input, the big skip)."""
+        if torch.is_grad_enabled() or not self.big_skip:
+            return False
+        blk = self.blocks[-1]
+        if not blk.defers_output_affine():
+            return False
+        d, _ = self.decoder.native_desc(cin2=x.shape[1])
+        return bool(N.lib().msfno_mlp_fused_supported(d))
+
+    def decode_deferred(self, x1, aff, residual):
+        """decoder(cat(aff[0] * x1 + aff[1], residual)) with the affine applied as the
+        decoder loads x1 (msfno_mlp_forward_affine)."""
+        return self.decoder.native_forward_affine(x1, aff[0], aff[1], x2=residual)
+
     def forward_features(self, x):
         x = self.pos_drop(x)
         for blk in self.blocks:
@@ -491,6 +544,12 @@ class FourierNeuralOperatorNet(nn.Module):
     def forward(self, x):
         residual = x
         x = self.encode(x)
+        if self._fuse_last_affine(residual):
+            x = self.pos_drop(x)
+            for blk in self.blocks[:-1]:
+                x = blk(x)
+            x1, aff = self.blocks[-1].native_forward_deferred(x)
+            return self.decode_deferred(x1, aff, residual)
         x = self.forward_features(x)
         return self.decode(x, residual)
 
@@ -527,10 +586,15 @@ class FourierNeuralOperatorNet_Filmed(FourierNeuralOperatorNet):
             self.gamma, self.beta = gamma, beta
         residual = x
         x = self.pos_drop(self.encode(x))
+        fuse = self._fuse_last_affine(residual)
+        nb = len(self.blocks)
         for i, blk in enumerate(self.blocks):
+            film = ()
             if self._filmed(i):
                 film_idx = i - (self.num_layers - self.film_layers)
-                x = blk(x, gamma[:, film_idx], beta[:, film_idx], scale)
-            else:
-                x = blk(x)
+                film = (gamma[:, film_idx], beta[:, film_idx], scale)
+            if fuse and i == nb - 1:
+                x1, aff = blk.native_forward_deferred(x, *film)
+                return self.decode_deferred(x1, aff, residual)
+            x = blk(x, *film)
         return self.decode(x, residual)
