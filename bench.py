@@ -86,11 +86,11 @@ STAGE_KERNEL_X3H = dict(STAGE_KERNEL_X6, **{
     # inner skip at C = 256 on the fused-MLP tiling (MSFNO_SKIP_H=0: gemm_x3)
     "inner_skip": "msfno::(anonymous namespace)::skip_h_kernel("
                   "msfno::(anonymous namespace)::SkipHParams)",
-    "mlp_fused": "void msfno::(anonymous namespace)::mlp_fused_h_kernel<2, 0, 1, 4, 4>"
+    "mlp_fused": "void msfno::(anonymous namespace)::mlp_fused_h_kernel<2>"
                  "(msfno::(anonymous namespace)::MlpHParams)",
     "legendre_fwd": "void msfno::(anonymous namespace)::legendre_x3f_kernel<3>("
                     "msfno::(anonymous namespace)::X3FParams)",
-    "legendre_inv": "void msfno::(anonymous namespace)::legendre_x3r_kernel<false, false>("
+    "legendre_inv": "msfno::(anonymous namespace)::legendre_x3r_kernel("
                     "msfno::(anonymous namespace)::X3DParams)",
 })
 # the linear filter's weight stream at batch 1 (any engine)
