@@ -231,8 +231,13 @@ int side_ctx(std::shared_ptr<SideCtx>* out, hipStream_t caller) {
   if (!enabled) return MSFNO_OK;
   // no fork while the caller's stream is being captured into a HIP graph: the
   // captured fork/join made a 12-block network step 19.0 ms instead of 12.4 ms
-  // (replayed, config 3); the graph runs the skip GEMM in line
-  if (caller) {
+  // (replayed, config 3, round 2); the graph runs the skip GEMM in line.
+  // MSFNO_GRAPH_FORK=1 captures the fork / join as graph branches (A/B)
+  static const bool graph_fork = [] {
+    const char* e = getenv("MSFNO_GRAPH_FORK");
+    return e && e[0] == '1';
+  }();
+  if (caller && !graph_fork) {
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
     if (hipStreamIsCapturing(caller, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone)
       return MSFNO_OK;
