@@ -1785,7 +1785,18 @@ static int block_forward_impl(const msfno_block_desc* d, msfno_sht_plan_t f, msf
   // them), so it never shares the GPU with this block's forward FFT: skip_h co-resident
   // with a row FFT (a fork at the block start, retired MSFNO_SKIP_PX) corrupted real parts
   // of single FFT bins
-  if (b.xs)
+  // linear filter: MSFNO_LIN_SKIP_AT=inv forks the skip after the HBM-bound per-mode
+  // contraction instead (its 2.1 GB then do not share HBM with the 34 GB weight stream;
+  // A/B)
+  static const bool lin_skip_late = [] {
+    const char* e = getenv("MSFNO_LIN_SKIP_AT");
+    return e && std::string(e) == "inv";
+  }();
+  const bool skip_late = lin_skip_late && d->filter_type != MSFNO_FILTER_NONLINEAR;
+  if (b.xs && skip_late)
+    MSFNO_TRY(run_spectral(d, f, g, b, x, B, true, s, nullptr, std::function<int()>(),
+                           std::function<int()>(), std::function<int()>(), launch_skip));
+  else if (b.xs)
     MSFNO_TRY(run_spectral(d, f, g, b, x, B, true, s, nullptr, std::function<int()>(), launch_skip));
   else if (xpl)
     MSFNO_TRY(run_spectral(d, f, g, b, x, B, true, s, &xp, launch_skip));

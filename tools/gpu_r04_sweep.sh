@@ -20,6 +20,14 @@ for i in 1 2; do
   run skipx3_$i MSFNO_SKIP_H=0 || exit $?
   run side0_$i MSFNO_SIDE_STREAM=0 || exit $?
 done
+# the linear filter: skip forked after the contraction (A/B)
+for i in 1 2; do
+  for v in "MSFNO_NONE=1" "MSFNO_LIN_SKIP_AT=inv"; do
+    tag=lin_${v%%=*}_$i
+    env $v timeout -k 10 240 python bench.py --filter linear --linear-check 0 --cpu-baseline 0 > $O/$tag.json 2> $O/$tag.err || exit $?
+    python3 -c "import json;print('$tag', json.loads(open('$O/$tag.json').readline())['value'])" | tee -a $O/summary.txt
+  done
+done
 # the network step: the side-stream fork captured into the graph (A/B)
 for i in 1 2; do
   for v in "MSFNO_NONE=1" "MSFNO_GRAPH_FORK=1"; do
