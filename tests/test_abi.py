@@ -87,3 +87,27 @@ def test_cpu_tensor_is_rejected_loudly():
     s = RealSHT(8, 16, lmax=8, mmax=9)
     with pytest.raises(ValueError):
         s(torch.zeros(1, 8, 16))
+
+
+@pytest.mark.parametrize("cin,cin2,hid,cout,fused", [
+    (73, 0, 256, 256, True),     # the encoder (sfnonet.py:513-523)
+    (256, 73, 256, 73, True),    # the decoder over cat(x, residual) (:617-629)
+    (5, 0, 16, 16, False),       # fixture-sized nets: the x6 GEMM pair
+    (256, 73, 512, 73, False),   # hidden wider than the fused kernel's LDS vectors
+    (256, 0, 256, 256, False),   # widths without an instantiated kernel
+])
+def test_mlp_fused_widths_and_workspace(cin, cin2, hid, cout, fused):
+    """Host-side dispatch of the standalone MLP (no GPU call): which widths take the
+    one-launch x3h kernel, and that its workspace is the weight image only (no hidden
+    activation through HBM), far below the two-GEMM path's."""
+    from msfno_amd import _native as N
+    lib = N.lib()
+    d = N.MlpDesc()
+    d.Cin, d.Cin2, d.Hid, d.Cout = cin, cin2, hid, cout
+    assert bool(lib.msfno_mlp_fused_supported(ctypes.byref(d))) == fused
+    P = 721 * 1440
+    ws = lib.msfno_mlp_workspace_size(ctypes.byref(d), 1, P)
+    if fused:
+        assert ws < 4 << 20        # the image and scale vectors
+    else:
+        assert ws >= hid * P * 4   # the hidden activation
