@@ -47,6 +47,8 @@ VARIANTS = [
     {"MSFNO_LEG_X3F": "0"},
     {"MSFNO_X3F_NS": "2"},
     {"MSFNO_SKIP_H": "0"},
+    {"MSFNO_X3C_BM64": "0"},
+    {"MSFNO_LIN_SKIP_AT": "inv"},
 ]
 
 
