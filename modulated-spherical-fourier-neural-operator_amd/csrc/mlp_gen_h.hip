@@ -23,10 +23,9 @@
 //   unit 0:        fc1 tiles of hidden block 0                   (2 KS tiles)
 //   unit j (1..HB-1): fc1 tiles of block j, then fc2 tiles of block j - 1 (2 KS + OT)
 //   unit HB:       fc2 tiles of block HB - 1                     (OT)
-// back to back (the hidden width is a compile-time HB blocks of 32, so every tile's
-// position in the stream — and every 16-KB slice boundary, 8 tiles — is known at compile
-// time; only the stream's end is padded to a whole slice).  The slices stream through a
-// four-slot LDS ring by LDS-DMA exactly as in mlp_fused_h.hip.
+// each unit padded to whole 16-KB slices (8 tiles; the pad tiles are streamed, never
+// multiplied) so every slice boundary falls at a compile-time tile position.  The slices
+// stream through a four-slot LDS ring by LDS-DMA exactly as in mlp_fused_h.hip.
 // fc1 tile (ks, t) of block j: W1 rows 32 j + 16 t + r, columns 32 ks + k;
 // fc2 tile ot of block j: W2' rows 16 ot + r, hidden columns 32 j + mh_perm(k) (the C
 // layout of the fc1 accumulators becomes fc2's B fragment in place).
@@ -55,12 +54,12 @@ constexpr int MG_H_MAX = 256;
 
 __host__ __device__ constexpr int mg_round8(int n) { return (n + 7) & ~7; }
 
-// unit u's first tile in the stream; the image's tiles (the stream padded to 8)
+// unit u's first tile (units of the padded stream)
 __host__ __device__ constexpr int mg_unit_tile(int u, int KS, int OT) {
-  return u == 0 ? 0 : 2 * KS + (u - 1) * (2 * KS + OT);
+  return u == 0 ? 0 : mg_round8(2 * KS) + (u - 1) * mg_round8(2 * KS + OT);
 }
 __host__ __device__ constexpr int mg_tiles(int HB, int KS, int OT) {
-  return mg_round8(HB * (2 * KS + OT));
+  return mg_unit_tile(HB, KS, OT) + mg_round8(OT);
 }
 
 __host__ __device__ __forceinline__ int mg_swz(int r) { return ((r >> 2) & 1) << 1; }
@@ -248,13 +247,14 @@ __device__ __forceinline__ void mg_glds16x4(uint64_t sbase, const uint32_t (&vof
       : "memory", "scc");
 }
 
-template <int KS, int OT, int HB>
+template <int KS, int OT>
 __global__ __launch_bounds__(256, 2) void mlp_gen_h_kernel(MlpGParams p) {
   constexpr int W = MG_WAVES, NS = MG_NS;
   constexpr int SLICE_E = MG_SLICE * MG_TILE;    // fp16 per slice
   constexpr int RING_BYTES = NS * SLICE_E * 2;
   constexpr int NT1 = 2 * KS, NT2 = OT;
-  constexpr int NSLICE = mg_tiles(HB, KS, OT) / MG_SLICE;
+  constexpr int NU = mg_round8(NT1 + NT2);       // tiles per middle unit
+  constexpr int N0 = mg_round8(NT1);
   constexpr int CP = 16 * OT;
   __shared__ __attribute__((aligned(16))) char lds_raw[RING_BYTES + (3 * MG_H_MAX + 2 * CP + 64 * KS) * 4];
   unsigned short* const ring = reinterpret_cast<unsigned short*>(lds_raw);
@@ -273,8 +273,7 @@ __global__ __launch_bounds__(256, 2) void mlp_gen_h_kernel(MlpGParams p) {
   const int64_t P = p.P;
   const int64_t px = (int64_t)(lin - z * p.tiles_per_field) * (16 * W) + 16 * wave + r16;
   const int64_t pxc = px < P ? px : P - 1;
-  const int H = p.H;
-  constexpr int nslice = NSLICE;
+  const int H = p.H, HB = H >> 5, nslice = p.nslice;
 
   // ---- slices 0..NS-1 in flight ------------------------------------------------------
   const uint32_t ring_lds = lds_addr(ring);
@@ -406,19 +405,17 @@ __global__ __launch_bounds__(256, 2) void mlp_gen_h_kernel(MlpGParams p) {
 
   // one unit: FC1 -> fc1 tiles of block j into hacc[PAR] (converting block j - 1 from
   // hacc[PAR ^ 1] on the way when FC2), FC2 -> fc2 tiles of block j - 1
-  const unsigned short* slot = ring;  // the current slice's slot (units share slices)
-  auto unit = [&](auto j_c, auto fc1_c, auto fc2_c) {
-    constexpr int j = decltype(j_c)::value, PAR = j & 1;
+  auto unit = [&](int j, int s0, auto par_c, auto fc1_c, auto fc2_c) {
+    constexpr int PAR = decltype(par_c)::value;
     constexpr bool FC1 = decltype(fc1_c)::value, FC2 = decltype(fc2_c)::value;
     constexpr int n1 = FC1 ? NT1 : 0;
     constexpr int NTOT = n1 + (FC2 ? NT2 : 0);
-    constexpr int T0 = mg_unit_tile(j, KS, OT);
     using PPrev = std::integral_constant<int, PAR ^ 1>;
+    const unsigned short* slot = ring;
     mg_for<NTOT>([&](auto pc) {
       constexpr int pos = decltype(pc)::value;
-      constexpr int tg = T0 + pos;  // the tile's place in the stream
-      if constexpr (tg % MG_SLICE == 0) slot = step_begin(tg / MG_SLICE);
-      const unsigned short* tp = slot + (tg % MG_SLICE) * MG_TILE + a_lane;
+      if constexpr (pos % MG_SLICE == 0) slot = step_begin(s0 + pos / MG_SLICE);
+      const unsigned short* tp = slot + (pos % MG_SLICE) * MG_TILE + a_lane;
       const half8 a[2] = {*reinterpret_cast<const half8*>(tp),
                           *reinterpret_cast<const half8*>(tp + 512)};
       if constexpr (pos < n1) {
@@ -445,9 +442,11 @@ __global__ __launch_bounds__(256, 2) void mlp_gen_h_kernel(MlpGParams p) {
   using I1 = std::integral_constant<int, 1>;
   using F = std::false_type;
   using T = std::true_type;
-  static_assert(HB % 2 == 0, "block HB - 1 in hacc[1]");
-  unit(I0{}, T{}, F{});
-  mg_for<HB - 1>([&](auto jm) { unit(std::integral_constant<int, decltype(jm)::value + 1>{}, T{}, T{}); });
+  unit(0, 0, I0{}, T{}, F{});
+  for (int j = 1; j < HB; j += 2) {
+    unit(j, (N0 + (j - 1) * NU) / MG_SLICE, I1{}, T{}, T{});
+    if (j + 1 < HB) unit(j + 1, (N0 + j * NU) / MG_SLICE, I0{}, T{}, T{});
+  }
   // HB is even: block HB - 1 sits in hacc[1]
 #pragma unroll
   for (int e2 = 0; e2 < 4; ++e2) conv_pair(HB - 1, e2, I1{});
@@ -471,7 +470,7 @@ __global__ __launch_bounds__(256, 2) void mlp_gen_h_kernel(MlpGParams p) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) rv[ot][i] = 0.f;
   }
-  unit(std::integral_constant<int, HB>{}, F{}, T{});
+  unit(HB, (N0 + (HB - 1) * NU) / MG_SLICE, I0{}, F{}, T{});
 
   // ---- epilogue: unscale + b2 + addend, store (rows 16 ot + 4 g + i) -------------------
   if (px >= P) return;
@@ -514,7 +513,7 @@ static bool mlp_gen_h_env() {
 
 bool mlp_gen_h_supported(int Ct, int H, int Cout) {
   int ks, ot;
-  return mlp_gen_h_env() && mlp_fused_h_env() && gemm_use_x6() && H == MG_H_MAX &&
+  return mlp_gen_h_env() && mlp_fused_h_env() && gemm_use_x6() && H > 0 && H % 64 == 0 && H <= MG_H_MAX &&
          mg_shape(Ct, Cout, &ks, &ot);
 }
 
@@ -567,11 +566,9 @@ int launch_mlp_gen_h(const float* x, const float* xa, const float* xt, const flo
   const int64_t grid = (int64_t)B * p.tiles_per_field;
   MSFNO_REQUIRE(grid < (1LL << 31), MSFNO_EINVAL, "mlp_gen_h: grid too large");
   if (KS == 3)
-    hipLaunchKernelGGL((mlp_gen_h_kernel<3, 16, MG_H_MAX / 32>), dim3((unsigned)grid), dim3(64 * MG_WAVES),
-                       0, s, p);
+    hipLaunchKernelGGL((mlp_gen_h_kernel<3, 16>), dim3((unsigned)grid), dim3(64 * MG_WAVES), 0, s, p);
   else
-    hipLaunchKernelGGL((mlp_gen_h_kernel<11, 5, MG_H_MAX / 32>), dim3((unsigned)grid), dim3(64 * MG_WAVES),
-                       0, s, p);
+    hipLaunchKernelGGL((mlp_gen_h_kernel<11, 5>), dim3((unsigned)grid), dim3(64 * MG_WAVES), 0, s, p);
   return launch_check("mlp_gen_h");
 }
 
