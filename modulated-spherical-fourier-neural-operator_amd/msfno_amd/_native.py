@@ -12,7 +12,8 @@ import os
 import torch  # noqa: F401  (loads the HIP runtime (libamdhip64.so.7) that libmsfno shares)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libmsfno.so")
+# MSFNO_LIB: another in-tree build of the same library (A/B of two builds in one run)
+LIB_PATH = os.environ.get("MSFNO_LIB") or os.path.join(_HERE, "libmsfno.so")
 
 MSFNO_OK = 0
 MSFNO_EINVAL = 1
