@@ -48,7 +48,6 @@ VARIANTS = [
     {"MSFNO_X3F_NS": "2"},
     {"MSFNO_SKIP_H": "0"},
     {"MSFNO_X3C_BM64": "0"},
-    {"MSFNO_LIN_SKIP_AT": "inv"},
 ]
 
 

@@ -3,7 +3,8 @@
 # unit with exact waits, libmsfno_addw.so (MSFNO_LIB A/B) — parity, then interleaved
 # network benches;
 # (2) this round's new A/B switches (graph-captured skip fork, late linear skip fork) —
-# variant parity and interleaved benches; (3) a kernel trace of each network build
+# variant parity and interleaved benches.  Build the two variant libraries first, on the
+# CPU: bash tools/build_ab_variants.sh
 set -o pipefail
 cd /root/repo
 O=gpurun_out/r04_v16
