@@ -205,6 +205,12 @@ def parse(argv=None):
     ap.add_argument("--linear-check", type=int, default=1,
                     help="N=1, non-linear headline: also time config 2's linear filter (the "
                          "per-mode weight stream) and print it as the line's 'linear' object")
+    ap.add_argument("--net-check", type=int, default=1,
+                    help="N=1 block headline: also time config 3 (the 12-block filmed net, "
+                         "one 6 h step) and print it as the line's 'net' object")
+    ap.add_argument("--band-check", type=int, default=1,
+                    help="latband, N>1: after the timed region compare field 0's sharded "
+                         "output with the whole-field block on rank 0 (max-abs in the line)")
     ap.add_argument("--dry-run", action="store_true",
                     help="launcher / process-group check only (gloo, no GPU): ranks report in")
     return ap.parse_args(argv)
@@ -418,17 +424,25 @@ def run_net(args, rank, world, dev, dist, backend):
             # one 6 h step as a HIP graph: removes the host cost of ~300 launches and
             # the per-call module bookkeeping (the 120x240 blocks are launch-bound)
             graph = torch.cuda.CUDAGraph()
+            ok = True
             try:
                 with torch.cuda.graph(graph):
                     y = run(x, film, 1.0)
-                graph.replay()
-                torch.cuda.synchronize()
             except RuntimeError as e:
                 if not band:
                     raise
-                print(f"bench: sharded step not capturable ({e}); eager", file=sys.stderr)
-                use_graph = False
+                print(f"bench: sharded step not capturable on rank {rank} ({e})", file=sys.stderr)
+                ok = False
                 torch.cuda.synchronize()
+            if band and dist:
+                # every rank replays, or every rank steps eagerly (no replayed collective
+                # may meet an eager one)
+                ok = run.comm.all_agree(ok)
+            if ok:
+                graph.replay()
+                torch.cuda.synchronize()
+            else:
+                use_graph = False
                 y = run(x, film, 1.0)
 
         if use_graph:
@@ -472,8 +486,9 @@ def run_net(args, rank, world, dev, dist, backend):
             torch.cuda.synchronize()
             N.profile_enable(False)
             roof = net_roofline(N.profile_collect(), args, B)
+    line = None
     if rank == 0:
-        print(json.dumps({
+        line = {
             "metric": "FourierNeuralOperatorNet_Filmed 6h steps/sec (12 blocks, 73 ch, 721x1440)",
             "value": round((1 if band else world) * B * args.steps / elapsed, 3),
             "unit": "steps/s",
@@ -486,18 +501,75 @@ def run_net(args, rank, world, dev, dist, backend):
                        "batch_per_gpu": B, "filter": args.filter, "hip_graph": use_graph,
                        "band_inner": args.band_inner if band else None,
                        "parallelism": (f"latband{world}" if band else
-                                       (f"replicas{world}" if world > 1 else "single"))}}),
-              flush=True)
-    if dist:
-        torch.distributed.destroy_process_group()
+                                       (f"replicas{world}" if world > 1 else "single"))}}
+    del run, x, y
+    if not band:
+        del net
+    torch.cuda.empty_cache()
+    return line
+
+
+def net_cpu_baseline(args):
+    """Config 3 on the host: oracle.sfno_ref.net_forward (the torch-CPU restatement of
+    FourierNeuralOperatorNet_Filmed.forward, sfnonet.py:787-860) on ONE 6 h step after
+    one warm-up step (a bounded sample: ~5 s per step on 16 cores), same shapes and
+    default parameter recipe as the GPU line."""
+    from msfno_amd.sfno import FourierNeuralOperatorNet_Filmed
+    from oracle import sfno_ref
+    auto, desc = host_cores()
+    threads = args.cpu_threads if args.cpu_threads > 0 else auto
+    torch.set_num_threads(threads)
+    torch.manual_seed(1)
+    net = FourierNeuralOperatorNet_Filmed("cpu", None, film_layers=1, advanced_logging=False,
+                                          model_depth=None, img_size=(args.nlat, args.nlon),
+                                          in_chans=73, out_chans=73, embed_dim_sfno=args.C,
+                                          num_layers=12, filter_type=args.filter,
+                                          spectral_layers=3)
+    params = {k: v.detach() for k, v in net.state_dict().items()
+              if not k.endswith((".weights", ".pct"))}
+    del net
+    ncfg = sfno_ref.NetCfg(img_size=(args.nlat, args.nlon), scale_factor=6, num_layers=12,
+                           filter_type=args.filter)
+    tr = sfno_ref.make_net_transforms(ncfg)
+    g = torch.Generator().manual_seed(0)
+    x = torch.randn(1, 73, args.nlat, args.nlon, generator=g)
+    gamma = 0.1 * torch.randn(1, 1, args.C, generator=g)
+    beta = 0.1 * torch.randn(1, 1, args.C, generator=g)
+    times = []
+    with torch.no_grad():
+        for rep in range(2):
+            t0 = time.perf_counter()
+            sfno_ref.net_forward(params, x, ncfg, transforms=tr, film=(gamma, beta), scale=1.0)
+            times.append(time.perf_counter() - t0)
+    dt = times[-1]
+    return {"value": 1.0 / dt, "unit": "steps/s", "cores": threads, "kind": "port", "cpu": desc,
+            "sample": f"1 step of the 12-block filmed net ({args.nlat}x{args.nlon}, C={args.C}, "
+                      f"73 ch) after 1 warm-up; oracle/sfno_ref.py net_forward, {threads} "
+                      f"threads; s/step {times[0]:.2f} (warm-up), {times[1]:.2f}"}
+
+
+def net_line(args, dev):
+    """Config 3 beside the N = 1 block line (the driver runs bench.py --gpus 1 only):
+    one 6 h step of the 12-block filmed network at 721 x 1440, HIP-graph replayed, its
+    roofline and CPU baseline."""
+    import copy
+    na = copy.copy(args)
+    na.workload = "net"
+    na.graph = -1
+    torch.cuda.empty_cache()
+    line = run_net(na, 0, 1, dev, False, "nccl")
+    if args.cpu_baseline:
+        line["cpu_baseline"] = net_cpu_baseline(na)
+    return {k: line[k] for k in ("metric", "value", "unit", "ms_per_step", "roofline", "config",
+                                 "cpu_baseline") if k in line}
 
 
 def net_roofline(stages, args, B):
     """Config 3's dominant kernel: of the profiled stages whose work is known for the
     network (the fused encoder + decoder MLPs or their fc1 / fc2 GEMMs, 73 -> 256 -> 256 and 329 -> 256 ->
-    73 at the full grid; the 12 block MLPs, 11 on the 120x240 grid and the last at the
-    full grid), the one with the most device time per step; work and time summed over
-    the step's launches of it."""
+    73 at the full grid; the block MLPs of blocks 0..10 on the 120x240 grid, the last
+    block having none), the one with the most device time per step; work and time
+    summed over the step's launches of it."""
     C, P = args.C, args.nlat * args.nlon
     P_in = 120 * 240
     work = {
@@ -506,7 +578,9 @@ def net_roofline(stages, args, B):
         "mlp_gen": 2 * B * P * C * ((73 + C) + (C + 73 + 73)),
         "mlp_fc1": 2 * B * P * C * (73 + (C + 73)),
         "mlp_fc2": 2 * B * P * C * (C + 73),
-        "mlp_fused": 4 * B * C * (2 * C) * (11 * P_in + P),
+        # blocks 0..10 (block 0's MLP runs on its 120x240 output grid); the last block
+        # has none (mlp_mode="none", sfnonet.py:583/729)
+        "mlp_fused": 4 * B * C * (2 * C) * 11 * P_in,
     }
     known = {k: v for k, v in stages.items() if k in work}
     if not known:
@@ -679,6 +753,39 @@ def linear_line(args, dev):
                         "linear_filmed", "roofline": roof, "cpu_baseline": cpu}
 
 
+def band_check(shard, blk, y, gamma, beta, args, rank, world, dev, backend):
+    """Correctness of the sharded step (config 4): field 0's output rows from every
+    rank, assembled on rank 0, against the whole-field block on rank 0 (the same
+    module, unsharded) on the same input field.  Returns the check for the line."""
+    C, nlon = args.C, args.nlon
+    rows_all = [None] * world
+    torch.distributed.all_gather_object(rows_all, list(shard.rows_out))
+    maxr = max(len(r) for r in rows_all)
+    mine = torch.zeros(1, C, maxr, nlon, device=dev)
+    mine[:, :, :len(shard.rows_out)] = y[:1]
+    if backend != "nccl":
+        mine = mine.cpu()
+    parts = [torch.empty_like(mine) for _ in range(world)]
+    torch.distributed.all_gather(parts, mine)
+    if rank != 0:
+        return None
+    full = torch.empty(1, C, args.nlat, nlon, device=dev)
+    for r, t in enumerate(parts):
+        idx = torch.tensor(rows_all[r], dtype=torch.long, device=dev)
+        full.index_copy_(2, idx, t[:, :, :len(rows_all[r])].to(dev))
+    gd = torch.Generator(device=dev).manual_seed(0)  # field 0 is the first draw (main)
+    x0 = torch.randn(1, C, args.nlat, nlon, generator=gd, device=dev)
+    with torch.no_grad():
+        ref = blk(x0, gamma[:1].contiguous(), beta[:1].contiguous(), 1.0)
+    err = (full - ref).abs().max().item()
+    scale = ref.abs().max().item()
+    del full, ref, x0
+    torch.cuda.empty_cache()
+    return {"field": 0, "max_abs": err, "max_ref": round(scale, 4),
+            "ok": bool(err <= 2e-5 * max(1.0, scale)),
+            "against": "the whole-field block (same module, unsharded) on rank 0"}
+
+
 def dry_run(rank, world):
     """Process-group check without a GPU (tests/test_bench_launch.py): gloo."""
     import socket
@@ -735,7 +842,12 @@ def main():
         gpus_seen = len({(h, u) for _, h, u in seen})
 
     if args.workload == "net":
-        return run_net(args, rank, world, dev, dist, backend)
+        line = run_net(args, rank, world, dev, dist, backend)
+        if rank == 0:
+            print(json.dumps(line), flush=True)
+        if dist:
+            torch.distributed.destroy_process_group()
+        return
     blk, p, cfg = build_block(args, dev)
     C = args.C
     parallel = args.parallel
@@ -785,6 +897,10 @@ def main():
         print_stages(stages, args, B_launch, C, rows, mset, tag=f"rank{rank} ")
     assert torch.isfinite(y).all()
 
+    check = None
+    if band and dist and args.band_check:
+        check = band_check(shard, blk, y, gamma, beta, args, rank, world, dev, backend)
+
     replicas = None
     if band and dist and args.replicas_check:
         # the comm-free upper bound: every rank runs its own batch fields whole
@@ -827,6 +943,9 @@ def main():
     linear = None
     if world == 1 and args.linear_check and args.filter == "non-linear" and not band:
         linear = linear_line(args, dev)
+    net = None
+    if world == 1 and args.net_check and not band and (args.nlat, args.nlon) == (721, 1440):
+        net = net_line(args, dev)
 
     if rank == 0:
         out = {
@@ -862,6 +981,10 @@ def main():
             out["replicas_upper_bound"] = replicas
         if linear:
             out["linear"] = linear
+        if net:
+            out["net"] = net
+        if check:
+            out["latband_check"] = check
         print(json.dumps(out), flush=True)
     if dist:
         torch.distributed.destroy_process_group()

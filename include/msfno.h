@@ -95,6 +95,15 @@ int msfno_compl_contract_fwd_c(const float* a, const float* w, float* y, int B, 
 int msfno_compl_mul2d_fwd_c(const float* a, const float* w, float* y, int B, int Ci, int Co,
                             long long XY, int relu_real, void* stream);
 
+/* 1x1 convolution, the block's inner skip as a standalone op (nn.Conv2d(C, C, 1) at
+ * sfnonet.py:304-307, applied at :366-371):  out[b] = W x[b] + bias (per pixel)
+ *   w (Cout, Cin, 1, 1), bias (Cout) or NULL, x (B, Cin, P), out (B, Cout, P); fp32 in and
+ *   out, computed on the x3h engine (fp32 as two fp16 terms, three MFMAs per product)
+ *   under per-(b, channel) power-of-two scales from max |x| (as accurate as fp32). */
+size_t msfno_conv1x1_workspace_size(int B, int Cin, int Cout);
+int msfno_conv1x1(const float* w, const float* bias, const float* x, float* out, int B, int Cin,
+                  int Cout, long long P, void* ws, size_t ws_bytes, void* stream);
+
 /* ---------------------------------------------------------------------------
  * Fused SFNO-Block forward.
  * Replaces FourierNeuralOperatorBlock.forward (sfnonet.py:221-251) and
@@ -159,6 +168,14 @@ int msfno_block_forward_deferred(const msfno_block_desc* d, msfno_sht_plan_t fwd
                                  const float* beta, float film_scale, float* x1_out,
                                  float* affine_out, int B, void* ws, size_t ws_bytes,
                                  void* stream);
+/* FourierNeuralOperatorBlock_Filmed.global_conv(x, residual) (sfnonet.py:341-356): the
+ * block up to norm1 -- norm0(x) -> filter -> + inner_skip(residual) (+ GELU for the
+ * linear filter) -> norm1 -- without FiLM, MLP or outer skip.  residual may be NULL
+ * (= x).  x, residual (B,C,nlat_in,nlon_in) -> out (B,C,nlat_out,nlon_out).
+ * Workspace: msfno_block_workspace_size. */
+int msfno_block_global_conv(const msfno_block_desc* d, msfno_sht_plan_t fwd, msfno_sht_plan_t inv,
+                            const float* x, const float* residual, float* out, int B, void* ws,
+                            size_t ws_bytes, void* stream);
 /* SpectralFilterLayer.forward alone (sfnonet.py:132-133): SHT -> filter -> ISHT,
  * no norms.  x (B,C,nlat_in,nlon_in) -> y (B,C,nlat_out,nlon_out). */
 int msfno_filter_forward(const msfno_block_desc* d, msfno_sht_plan_t fwd, msfno_sht_plan_t inv,
@@ -179,8 +196,14 @@ typedef struct msfno_mlp_desc {
   int Cin, Cin2, Hid, Cout;
   const float* fc1_w; const float* fc1_b;   /* (Hid, Cin+Cin2, 1, 1), (Hid)  */
   const float* fc2_w; const float* fc2_b;   /* (Cout, Hid, 1, 1), (Cout) or NULL */
+  /* Prepared-weight cache of the fused widths (as msfno_block_desc.wcache): NULL, or a
+   * device buffer of msfno_mlp_wcache_size(d) bytes owned by the caller (one per
+   * module) holding the x3h weight image; wcache_valid = 1 skips its preparation. */
+  void* wcache;
+  int wcache_valid;
 } msfno_mlp_desc;
 
+size_t msfno_mlp_wcache_size(const msfno_mlp_desc* d);
 size_t msfno_mlp_workspace_size(const msfno_mlp_desc* d, int B, long long P);
 /* 1 when the widths (Cin + Cin2, Hid, Cout) have the one-launch fused x3h kernel
  * (the encoder 73 -> 256 -> 256 and decoder 329 -> 256 -> 73 of the reference config). */

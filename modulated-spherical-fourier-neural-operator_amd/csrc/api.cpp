@@ -1500,7 +1500,7 @@ using namespace msfno;
 extern "C" {
 
 const char* msfno_last_error(void) { return g_last_error.c_str(); }
-int msfno_abi_version(void) { return 4; }
+int msfno_abi_version(void) { return 5; }
 
 int msfno_quadrature(int nlat, int grid, double* nodes, double* weights) {
   std::vector<double> x, w;
@@ -1674,6 +1674,33 @@ int msfno_compl_mul2d_fwd_c(const float* a, const float* w, float* y, int B, int
   return launch_compl_mul2d(a, w, y, B, Ci, Co, XY, relu_real, (hipStream_t)stream);
 }
 
+// 1x1 convolution (the block's inner skip as a standalone op): x3h engine, B rows scaled
+// per (b, channel) by the power of two below its max |x| (no norm statistics here)
+size_t msfno_conv1x1_workspace_size(int B, int Cin, int Cout) {
+  if (B <= 0 || Cin <= 0 || Cout <= 0) return 0;
+  const size_t xs = round_up((int64_t)B * Cin * 4, 256);
+  return xs + (Cin == 256 && Cout == 256 ? skip_h_workspace(B) : gemm_x3_workspace(Cout, Cin, B));
+}
+
+int msfno_conv1x1(const float* w, const float* bias, const float* x, float* out, int B, int Cin,
+                  int Cout, long long P, void* ws, size_t ws_bytes, void* stream) {
+  MSFNO_REQUIRE(w && x && out && ws && B > 0 && Cin > 0 && Cout > 0 && P > 0 && P < (1LL << 31),
+                MSFNO_EINVAL, "bad conv1x1 arguments");
+  MSFNO_REQUIRE(ws_bytes >= msfno_conv1x1_workspace_size(B, Cin, Cout), MSFNO_EWORKSPACE,
+                "conv1x1: workspace too small");
+  hipStream_t s = (hipStream_t)stream;
+  float* xs = static_cast<float*>(ws);
+  const size_t xs_bytes = round_up((int64_t)B * Cin * 4, 256);
+  void* rest = static_cast<char*>(ws) + xs_bytes;
+  MSFNO_TRY(launch_chan_pow2_scale(x, (int64_t)B * Cin, P, xs, s));
+  if (Cin == 256 && Cout == 256 && skip_h_env())
+    return launch_skip_h(w, xs, x, out, bias, B, P, rest, ws_bytes - xs_bytes, s);
+  GemmEpi e;
+  e.bias = bias;
+  return gemm_x3(w, Cin, xs, x, out, Cout, (int)P, Cin, (int)P, (int)P, (int64_t)Cin * P,
+                 (int64_t)Cout * P, B, e, rest, ws_bytes - xs_bytes, s);
+}
+
 size_t msfno_block_wcache_size(const msfno_block_desc* d) {
   if (!d) return 0;
   msfno_block_desc t = *d;
@@ -1712,10 +1739,13 @@ int msfno_filter_forward(const msfno_block_desc* d, msfno_sht_plan_t f, msfno_sh
 // x1_ext / aff_out (both or neither; blocks without MLP and outer skip): the block stops
 // before its output affine, leaving x1 in x1_ext and the per-(b,c) norm1 (+ FiLM) affine
 // in aff_out = [scale (B*C)][shift (B*C)] for the consumer to apply (the decoder MLP)
+// skip_x (or null = x): the inner skip's input (global_conv's `residual`); norm_only: stop
+// after norm1 (no FiLM, MLP or outer skip: FourierNeuralOperatorBlock_Filmed.global_conv)
 static int block_forward_impl(const msfno_block_desc* d, msfno_sht_plan_t f, msfno_sht_plan_t g,
                               const float* x, const float* gamma, const float* beta,
                               float film_scale, float* out, float* x1_ext, float* aff_out, int B,
-                              void* ws, size_t ws_bytes, void* stream) {
+                              void* ws, size_t ws_bytes, void* stream,
+                              const float* skip_x = nullptr, bool norm_only = false) {
   MSFNO_TRY(check_pair(d, f, g));
   MSFNO_REQUIRE(ws_bytes >= msfno_block_workspace_size(d, f, g, B), MSFNO_EWORKSPACE,
                 "workspace too small");
@@ -1741,8 +1771,9 @@ static int block_forward_impl(const msfno_block_desc* d, msfno_sht_plan_t f, msf
   // GEMM is forked after the forward FFT and stages B by LDS-DMA (gemm_x6p) instead
   // of splitting fp32 x in-kernel.
   float* x1 = x1_ext ? x1_ext : b.x1;
+  const float* sx = skip_x ? skip_x : x;
   std::shared_ptr<SideCtx> side;
-  const bool xpl = skip_planes(d, f, b);
+  const bool xpl = skip_planes(d, f, b) && sx == x;  // the FFT writes planes of x
   const C2RPlanes xp{b.x1p, (int)C, f->nlat};
   auto launch_skip = [&]() -> int {
     hipStream_t ss = s;
@@ -1754,11 +1785,13 @@ static int block_forward_impl(const msfno_block_desc* d, msfno_sht_plan_t f, msf
     prof(ST_SKIP, ss);
     GemmEpi e;
     e.bias = d->skip_b;
+    // a separate skip input has no norm0 statistics: its x3h B-row scales from its max
+    if (b.xs && sx != x) MSFNO_TRY(launch_chan_pow2_scale(sx, (int64_t)B * C, P, b.xs, ss));
     if (b.xs && C == 256 && skip_h_env()) {
-      MSFNO_TRY(launch_skip_h(d->skip_w, b.xs, x, x1, d->skip_b, B, P, b.dw.skip, b.dw.skip_b,
+      MSFNO_TRY(launch_skip_h(d->skip_w, b.xs, sx, x1, d->skip_b, B, P, b.dw.skip, b.dw.skip_b,
                               ss));
     } else if (b.xs) {
-      MSFNO_TRY(gemm_x3(d->skip_w, (int)C, b.xs, x, x1, (int)C, (int)P, (int)C, (int)P, (int)P,
+      MSFNO_TRY(gemm_x3(d->skip_w, (int)C, b.xs, sx, x1, (int)C, (int)P, (int)C, (int)P, (int)P,
                         C * P, C * P, B, e, b.dw.skip, b.dw.skip_b, ss));
     } else if (xpl) {
       e.b_planes = b.x1p;
@@ -1805,8 +1838,9 @@ static int block_forward_impl(const msfno_block_desc* d, msfno_sht_plan_t f, msf
   if (side) MSFNO_CHECK_HIP(hipStreamWaitEvent(s, side->join, 0));  // join
   // ---- filter output + skip (+ GELU for the linear filter) -> x1, norm1 partials ---
   const float* skip_src = d->inner_skip == MSFNO_SKIP_LINEAR ? x1
-                          : (d->inner_skip == MSFNO_SKIP_IDENTITY ? x : nullptr);
-  unsigned short* x1p = x1_planes(d, g) ? b.x1p : nullptr;  // irfft writes x1 as planes
+                          : (d->inner_skip == MSFNO_SKIP_IDENTITY ? sx : nullptr);
+  // irfft writes x1 as planes (the unfused MLP's fc1 operand; global_conv reads fp32 x1)
+  unsigned short* x1p = !norm_only && x1_planes(d, g) ? b.x1p : nullptr;
   MSFNO_TRY(run_inverse_fft(g, b, B, (int)C, x1, skip_src, b.st1, act, s, x1p));
   const int64_t np = g->nlat, cnt = g->nlon, cnt_last = g->nlon;
   // ---- norm1 (+ FiLM) as a per-(b,c) affine --------------------------------------
@@ -1815,7 +1849,10 @@ static int block_forward_impl(const msfno_block_desc* d, msfno_sht_plan_t f, msf
                                d->norm_eps, gamma, beta, film_scale, b.sc1, b.sh1, s, nullptr,
                                nullptr, b.ab1));
   const float* resid = d->outer_skip == MSFNO_SKIP_IDENTITY ? x : nullptr;
-  if (aff_out) {
+  if (norm_only) {
+    prof(ST_OUT_AFFINE, s);
+    MSFNO_TRY(launch_affine_rows(x1, b.sc1, b.sh1, nullptr, out, BC, P, 0, nullptr, 0, s));
+  } else if (aff_out) {
     MSFNO_CHECK_HIP(hipMemcpyAsync(aff_out, b.sc1, BC * sizeof(float), hipMemcpyDeviceToDevice, s));
     MSFNO_CHECK_HIP(
         hipMemcpyAsync(aff_out + BC, b.sh1, BC * sizeof(float), hipMemcpyDeviceToDevice, s));
@@ -1837,6 +1874,14 @@ int msfno_block_forward(const msfno_block_desc* d, msfno_sht_plan_t f, msfno_sht
                         float* out, int B, void* ws, size_t ws_bytes, void* stream) {
   return block_forward_impl(d, f, g, x, gamma, beta, film_scale, out, nullptr, nullptr, B, ws,
                             ws_bytes, stream);
+}
+
+int msfno_block_global_conv(const msfno_block_desc* d, msfno_sht_plan_t f, msfno_sht_plan_t g,
+                            const float* x, const float* residual, float* out, int B, void* ws,
+                            size_t ws_bytes, void* stream) {
+  MSFNO_REQUIRE(x && out, MSFNO_EINVAL, "global_conv: missing tensors");
+  return block_forward_impl(d, f, g, x, nullptr, nullptr, 0.f, out, nullptr, nullptr, B, ws,
+                            ws_bytes, stream, residual, true);
 }
 
 int msfno_block_forward_deferred(const msfno_block_desc* d, msfno_sht_plan_t f,
@@ -1910,6 +1955,10 @@ int msfno_mlp_fused_supported(const msfno_mlp_desc* d) {
   return d && mlp_gen_h_supported(d->Cin + d->Cin2, d->Hid, d->Cout) ? 1 : 0;
 }
 
+size_t msfno_mlp_wcache_size(const msfno_mlp_desc* d) {
+  return msfno_mlp_fused_supported(d) ? mlp_gen_h_workspace(d->Cin + d->Cin2, d->Hid, d->Cout) : 0;
+}
+
 int msfno_mlp_forward_affine(const msfno_mlp_desc* d, const float* x, const float* x_scale,
                              const float* x_shift, const float* x2, const float* addend,
                              long long add_bstride, float* out, int B, long long P, void* ws,
@@ -1925,7 +1974,7 @@ int msfno_mlp_forward_affine(const msfno_mlp_desc* d, const float* x, const floa
   prof(ST_MLP_GEN, s);
   MSFNO_TRY(launch_mlp_gen_h(x, x_scale, x_shift, x2, d->Cin, d->Cin2, d->fc1_w, d->fc1_b, d->fc2_w,
                              d->fc2_b, d->Hid, d->Cout, addend, add_bstride, out, B, P, ws,
-                             ws_bytes, s));
+                             ws_bytes, s, d->wcache, d->wcache_valid));
   prof(ST_END, s);
   return MSFNO_OK;
 }
@@ -1947,7 +1996,8 @@ int msfno_mlp_forward(const msfno_mlp_desc* d, const float* x, const float* x2,
     // one fused x3h launch, the hidden activation on-chip (mlp_gen_h.hip)
     prof(ST_MLP_GEN, s);
     MSFNO_TRY(launch_mlp_gen_h(x, nullptr, nullptr, x2, d->Cin, d->Cin2, d->fc1_w, d->fc1_b, d->fc2_w, d->fc2_b,
-                               d->Hid, d->Cout, addend, add_bstride, out, B, P, ws, ws_bytes, s));
+                               d->Hid, d->Cout, addend, add_bstride, out, B, P, ws, ws_bytes, s,
+                               d->wcache, d->wcache_valid));
     prof(ST_END, s);
     return MSFNO_OK;
   }

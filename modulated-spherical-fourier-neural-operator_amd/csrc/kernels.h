@@ -110,12 +110,15 @@ bool mlp_fused_h_env();
 bool mlp_gen_h_supported(int Ct, int H, int Cout);
 size_t mlp_gen_h_workspace(int Ct, int H, int Cout);
 // xa, xt (both or neither): [B][Cin] per-channel affine applied to x first (a deferred
-// norm / FiLM of the producing block)
+// norm / FiLM of the producing block).  cache (or null): mlp_gen_h_workspace bytes holding
+// the prepared weight image across calls, rebuilt only when cache_valid is 0 (ws is then
+// unused)
 int launch_mlp_gen_h(const float* x, const float* xa, const float* xt, const float* x2, int Cin,
                      int Cin2, const float* W1,
                      const float* b1, const float* W2, const float* b2, int H, int Cout,
                      const float* addend, int64_t add_bstride, float* out, int B, int64_t P,
-                     void* ws, size_t ws_bytes, hipStream_t s);
+                     void* ws, size_t ws_bytes, hipStream_t s, void* cache = nullptr,
+                     int cache_valid = 0);
 // inner skip at C = 256 on the mlp_fused_h tiling (x3h): out = Ws·x + bs, x scaled by the
 // power-of-two channel scales xs (|xs x| < 2^14), or per pixel in-kernel when xs is null;
 // ws >= skip_h_workspace(B)
@@ -123,6 +126,9 @@ bool skip_h_env();
 size_t skip_h_workspace(int B);
 int launch_skip_h(const float* W, const float* xs, const float* x, float* out, const float* bias,
                   int B, int64_t P, void* ws, size_t ws_bytes, hipStream_t s);
+// xs[r] = the power of two 2^(14 - e) with max_p |x[r][p]| = f 2^e (rows of P values): the
+// x3h B-row scales of a 1x1 conv whose input carries no norm statistics
+int launch_chan_pow2_scale(const float* x, int64_t rows, int64_t P, float* xs, hipStream_t s);
 size_t mlp_fused_h_image_bytes();
 int launch_mlp_fused_h_images(const float* W1, const float* b1, const float* W2,
                               unsigned short* img, hipStream_t s);

@@ -682,7 +682,31 @@ __global__ __launch_bounds__(256, 2) void skip_h_kernel(SkipHParams p) {
   }
 }
 
+// xs[r] = 2^(14 - e), max_p |x[r][p]| = f 2^e (f in [0.5, 1)): every |xs x| < 2^14 (the
+// x3h B-row scale of a standalone 1x1 conv, whose input has no norm statistics); one
+// 256-thread workgroup per row r
+__global__ __launch_bounds__(256) void chan_pow2_scale_kernel(const float* __restrict__ x,
+                                                              int64_t P, float* __restrict__ xs) {
+  __shared__ float wmax[4];
+  const float* row = x + (int64_t)blockIdx.x * P;
+  float m = 0.f;
+  for (int64_t p = threadIdx.x; p < P; p += 256) m = fmaxf(m, fabsf(row[p]));
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+  if ((threadIdx.x & 63) == 0) wmax[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0)
+    xs[blockIdx.x] = pow2_below(fmaxf(fmaxf(wmax[0], wmax[1]), fmaxf(wmax[2], wmax[3])), 14);
+}
+
 }  // namespace
+
+int launch_chan_pow2_scale(const float* x, int64_t rows, int64_t P, float* xs, hipStream_t s) {
+  MSFNO_REQUIRE(x && xs && rows > 0 && rows < (1LL << 31) && P >= 1, MSFNO_EINVAL,
+                "chan_pow2_scale: bad arguments");
+  hipLaunchKernelGGL(chan_pow2_scale_kernel, dim3((unsigned)rows), dim3(256), 0, s, x, P, xs);
+  return launch_check("chan_pow2_scale");
+}
 
 size_t skip_h_workspace(int B) {
   return (size_t)B * SK_NSLICE * MH_SLICE * 2 + (size_t)B * MH_C * 4 * 2 + 256;

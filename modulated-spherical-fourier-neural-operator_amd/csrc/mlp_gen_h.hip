@@ -528,34 +528,40 @@ int launch_mlp_gen_h(const float* x, const float* xa, const float* xt, const flo
                      int Cin2, const float* W1,
                      const float* b1, const float* W2, const float* b2, int H, int Cout,
                      const float* addend, int64_t add_bstride, float* out, int B, int64_t P,
-                     void* ws, size_t ws_bytes, hipStream_t s) {
+                     void* ws, size_t ws_bytes, hipStream_t s, void* cache, int cache_valid) {
   const int Ct = Cin + Cin2;
   int KS, OT;
   MSFNO_REQUIRE((xa == nullptr) == (xt == nullptr) && x && W1 && b1 && W2 && out && B > 0 && P >= 1 && Cin > 0 && Cin2 >= 0 &&
                     (Cin2 == 0) == (x2 == nullptr) && mlp_gen_h_supported(Ct, H, Cout) &&
-                    mg_shape(Ct, Cout, &KS, &OT) && ws && ws_bytes >= mlp_gen_h_workspace(Ct, H, Cout),
+                    mg_shape(Ct, Cout, &KS, &OT) &&
+                    (cache || (ws && ws_bytes >= mlp_gen_h_workspace(Ct, H, Cout))),
                 MSFNO_EINVAL, "mlp_gen_h: bad arguments");
   const int HB = H / 32, Cp = 16 * OT;
   const int64_t tiles = mg_tiles(HB, KS, OT);
-  unsigned short* img = static_cast<unsigned short*>(ws);
-  float* eta = reinterpret_cast<float*>(static_cast<char*>(ws) + round_up(tiles * MG_TILE * 2, 256));
+  // the weight image and its scale vectors: in the caller's prepared-weight cache when
+  // given (rebuilt only when cache_valid is 0), else in the workspace on every call
+  char* base = static_cast<char*>(cache ? cache : ws);
+  unsigned short* img = reinterpret_cast<unsigned short*>(base);
+  float* eta = reinterpret_cast<float*>(base + round_up(tiles * MG_TILE * 2, 256));
   float* s1 = eta + H;
   float* is1 = s1 + H;
   float* s2 = is1 + H;
   float* is2 = s2 + Cp;
-  // the pad tiles are streamed (never multiplied): keep them finite
-  if (hipMemsetAsync(img, 0, tiles * MG_TILE * 2, s) != hipSuccess) {
-    set_error("mlp_gen_h: image clear failed");
-    return MSFNO_EHIP;
+  if (!(cache && cache_valid)) {
+    // the pad tiles are streamed (never multiplied): keep them finite
+    if (hipMemsetAsync(img, 0, tiles * MG_TILE * 2, s) != hipSuccess) {
+      set_error("mlp_gen_h: image clear failed");
+      return MSFNO_EHIP;
+    }
+    hipLaunchKernelGGL(mg_eta_kernel, dim3(H), dim3(256), 0, s, W1, b1, Ct, eta);
+    MSFNO_TRY(launch_check("mg_eta"));
+    hipLaunchKernelGGL(mg_scale_kernel, dim3(H + Cp), dim3(256), 0, s, W1, W2, eta, H, Ct, Cout,
+                       s1, s2, is1, is2);
+    MSFNO_TRY(launch_check("mg_scale"));
+    hipLaunchKernelGGL(mg_image_kernel, dim3(256), dim3(256), 0, s, W1, W2, eta, s1, s2, H, Ct,
+                       Cout, KS, OT, img);
+    MSFNO_TRY(launch_check("mg_image"));
   }
-  hipLaunchKernelGGL(mg_eta_kernel, dim3(H), dim3(256), 0, s, W1, b1, Ct, eta);
-  MSFNO_TRY(launch_check("mg_eta"));
-  hipLaunchKernelGGL(mg_scale_kernel, dim3(H + Cp), dim3(256), 0, s, W1, W2, eta, H, Ct, Cout, s1,
-                     s2, is1, is2);
-  MSFNO_TRY(launch_check("mg_scale"));
-  hipLaunchKernelGGL(mg_image_kernel, dim3(256), dim3(256), 0, s, W1, W2, eta, s1, s2, H, Ct, Cout,
-                     KS, OT, img);
-  MSFNO_TRY(launch_check("mg_image"));
   MlpGParams p{};
   p.x = x; p.xa = xa; p.xt = xt; p.x2 = x2; p.addend = addend; p.out = out; p.img = img;
   p.is1 = is1; p.is2 = is2; p.eta = eta; p.b1 = b1; p.b2 = b2;

@@ -56,6 +56,7 @@ class MlpDesc(ctypes.Structure):
     _fields_ = [
         ("Cin", _i), ("Cin2", _i), ("Hid", _i), ("Cout", _i),
         ("fc1_w", _vp), ("fc1_b", _vp), ("fc2_w", _vp), ("fc2_b", _vp),
+        ("wcache", _vp), ("wcache_valid", _i),
     ]
 
 
@@ -86,14 +87,19 @@ SIGNATURES = [
     ("msfno_sht_inverse", _i, [_vp, _vp, _vp, _i, _vp, _sz, _vp]),
     ("msfno_compl_contract_fwd_c", _i, [_vp, _vp, _vp, _i, _i, _i, _i, _vp]),
     ("msfno_compl_mul2d_fwd_c", _i, [_vp, _vp, _vp, _i, _i, _i, ctypes.c_longlong, _i, _vp]),
+    ("msfno_conv1x1_workspace_size", _sz, [_i, _i, _i]),
+    ("msfno_conv1x1", _i, [_vp, _vp, _vp, _vp, _i, _i, _i, ctypes.c_longlong, _vp, _sz, _vp]),
     ("msfno_block_workspace_size", _sz, [ctypes.POINTER(BlockDesc), _vp, _vp, _i]),
     ("msfno_block_wcache_size", _sz, [ctypes.POINTER(BlockDesc)]),
     ("msfno_block_forward", _i, [ctypes.POINTER(BlockDesc), _vp, _vp, _vp, _vp, _vp, _f, _vp,
                                  _i, _vp, _sz, _vp]),
     ("msfno_block_forward_deferred", _i, [ctypes.POINTER(BlockDesc), _vp, _vp, _vp, _vp, _vp, _f,
                                           _vp, _vp, _i, _vp, _sz, _vp]),
+    ("msfno_block_global_conv", _i, [ctypes.POINTER(BlockDesc), _vp, _vp, _vp, _vp, _vp, _i, _vp,
+                                     _sz, _vp]),
     ("msfno_filter_forward", _i, [ctypes.POINTER(BlockDesc), _vp, _vp, _vp, _vp, _i, _vp, _sz,
                                   _vp]),
+    ("msfno_mlp_wcache_size", _sz, [ctypes.POINTER(MlpDesc)]),
     ("msfno_mlp_workspace_size", _sz, [ctypes.POINTER(MlpDesc), _i, ctypes.c_longlong]),
     ("msfno_mlp_fused_supported", _i, [ctypes.POINTER(MlpDesc)]),
     ("msfno_mlp_forward_affine", _i, [ctypes.POINTER(MlpDesc), _vp, _vp, _vp, _vp, _vp,

@@ -145,7 +145,8 @@ class Rollout:
     captured too when its exchanges run on RCCL (a ``TorchComm`` over the nccl
     backend: the collectives are recorded into the graph, model.py:327-331's
     per-step cost without the host launches); over gloo (host collectives) it steps
-    eagerly, and a capture that fails falls back to eager stepping."""
+    eagerly, and a capture that fails on any rank makes every rank step eagerly
+    (``TorchComm.all_agree``)."""
 
     def __init__(self, model, means=None, stds=None, film=None, scale=1.0, graph=True):
         self.model = model
@@ -188,12 +189,21 @@ class Rollout:
             if getattr(self.model, "world", 1) == 1:
                 self._capture(x)
             else:
+                # capture-or-eager is decided by all ranks together: a rank whose
+                # capture failed (a collective the backend cannot record) must not step
+                # eagerly while its peers replay recorded collectives
+                ok = True
                 try:
                     self._capture(x)
-                except RuntimeError:  # (a collective the backend cannot record)
+                except RuntimeError:
+                    ok = False
+                    torch.cuda.synchronize()
+                agree = getattr(getattr(self.model, "comm", None), "all_agree", None)
+                if agree is not None:
+                    ok = agree(ok)
+                if not ok:
                     self._graph = None
                     self.use_graph = False
-                    torch.cuda.synchronize()
         if self.use_graph and x.is_cuda:
             self._state.copy_(x)
             for i in range(steps):

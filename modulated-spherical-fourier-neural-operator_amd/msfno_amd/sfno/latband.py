@@ -112,6 +112,15 @@ class TorchComm:
         self.rank = dist.get_rank(group)
         self.host = dist.get_backend(group) == "gloo"
 
+    def all_agree(self, ok: bool) -> bool:
+        """True on every rank iff `ok` on every rank (a MIN all-reduce): collective
+        decisions such as capture-or-eager, so no rank replays recorded collectives
+        while a peer steps eagerly."""
+        dev = "cpu" if self.host else torch.device("cuda", torch.cuda.current_device())
+        t = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MIN, group=self.group)
+        return bool(t.item())
+
     def all_gather(self, t):
         src = t.cpu() if self.host else t
         parts = [torch.empty_like(src) for _ in range(self.world)]

@@ -10,6 +10,7 @@ weight-streaming contraction (linear)."""
 from __future__ import annotations
 
 import math
+import os
 import warnings
 
 import torch
@@ -41,6 +42,78 @@ def trunc_normal_(tensor, mean=0.0, std=1.0, a=-2.0, b=2.0):
     return _no_grad_trunc_normal_(tensor, mean, std, a, b)
 
 
+# MSFNO_WCACHE=0: rebuild the weight images on every call (A/B of the prepared-weight cache)
+_WCACHE = not os.environ.get("MSFNO_WCACHE", "").startswith("0")
+
+
+class WeightCache:
+    """Prepared-weight cache of a module whose native call consumes its weights as
+    x3h / bf16x3 images (msfno_block_desc.wcache, msfno_mlp_desc.wcache): a device
+    buffer per module, rebuilt by the native call only when a weight changed.
+    Subclasses give the buffer size of a descriptor (``_wcache_bytes``)."""
+
+    def _wcache_bytes(self, d):
+        raise NotImplementedError
+
+    def _wcache_key_of(self, device, nbytes):
+        """The prepared images depend only on the module's own weights: key on the
+        Parameters themselves (data_ptr, _version, dtype), not on the fp32 copies the
+        descriptor points at (those are fresh tensors, version 0, often at a reused
+        address)."""
+        return (str(device), nbytes) + tuple(
+            (p.data_ptr(), p._version, p.dtype) for p in self.parameters())
+
+    def wcache_attach(self, d, keep, device):
+        """Point the descriptor at this module's prepared-weight cache (bf16x3 weight
+        images, the descriptor's wcache) and mark it valid when the weights are
+        unchanged since it was filled.  Returns the key to pass to wcache_commit once
+        the native call has been issued.  In-place weight updates bump _version, so
+        the next call rebuilds the images; a HIP graph captured with a valid cache
+        replays without the preparation (weights frozen, as in Rollout).
+
+        Stream safety: the images were written (and last read) on the stream of the
+        previous committed call; a call on another stream first waits for that call's
+        completion event, so it neither reads unwritten images nor rebuilds them under
+        a reader."""
+        nbytes = self._wcache_bytes(d)
+        if nbytes == 0 or not _WCACHE:
+            return None
+        buf = getattr(self, "_wcache_buf", None)
+        if buf is None or buf.device != device or buf.numel() < nbytes:
+            old_ev = getattr(self, "_wcache_event", None)
+            if buf is not None and old_ev is not None:
+                # the old buffer's last user may be another stream: the allocator must
+                # not hand its memory out before that stream's work is done
+                buf.record_stream(torch.cuda.ExternalStream(old_ev[0], device=buf.device))
+            buf = self._wcache_buf = torch.empty(nbytes, dtype=torch.uint8, device=device)
+            self._wcache_key = None
+            self._wcache_event = None
+        cur = torch.cuda.current_stream(device)
+        ev = getattr(self, "_wcache_event", None)
+        if ev is not None and ev[0] != cur.cuda_stream \
+                and not torch.cuda.is_current_stream_capturing():
+            cur.wait_event(ev[1])
+        key = self._wcache_key_of(device, nbytes)
+        d.wcache = buf.data_ptr()
+        d.wcache_valid = int(key == getattr(self, "_wcache_key", None))
+        return key
+
+    def wcache_commit(self, key):
+        """Mark the images valid after the native call that (re)built them.  Never
+        while the stream is being captured: the preparation then lives only in the
+        graph, and the buffer has not been written yet (a capture that found the
+        images valid leaves the key as it was)."""
+        if key is None or torch.cuda.is_current_stream_capturing():
+            return
+        dev = self._wcache_buf.device
+        cur = torch.cuda.current_stream(dev)
+        e = torch.cuda.Event()
+        e.record(cur)
+        self._wcache_event = (cur.cuda_stream, e)
+        self._wcache_key = key
+
+
+
 class DropPath(nn.Module):
     """Stochastic depth; identity at inference (the only mode of the fused path)."""
 
@@ -57,7 +130,7 @@ class DropPath(nn.Module):
         return x.div(keep) * mask
 
 
-class MLP(nn.Module):
+class MLP(WeightCache, nn.Module):
     """Conv1x1 → act → Conv1x1 (state-dict keys fwd.0.*, fwd.2.*).  Inside a
     block it is executed by the fused native block (two MFMA GEMMs with the
     norm1/FiLM affine folded into fc1 and GELU / bias / residual in epilogues);
@@ -102,6 +175,9 @@ class MLP(nn.Module):
         d.fc1_w, d.fc1_b, d.fc2_w, d.fc2_b = w1.data_ptr(), b1.data_ptr(), w2.data_ptr(), N.ptr(b2)
         return d, keep
 
+    def _wcache_bytes(self, d):
+        return N.lib().msfno_mlp_wcache_size(d)
+
     @N.on_input_device
     def native_forward(self, x, x2=None, addend=None):
         """out = fc2(GELU(fc1(cat(x, x2)))) (+ addend, broadcast over the batch when its
@@ -125,12 +201,14 @@ class MLP(nn.Module):
             bstride = 0 if addend.shape[0] == 1 else d.Cout * H * W
         L = N.lib()
         P = H * W
+        wkey = self.wcache_attach(d, keep, x.device)
         nbytes = L.msfno_mlp_workspace_size(d, B, P)
         ws = torch.empty(nbytes, dtype=torch.uint8, device=x.device)
         out = torch.empty(B, d.Cout, H, W, dtype=torch.float32, device=x.device)
         N.check(L.msfno_mlp_forward(d, x.data_ptr(), N.ptr(x2), N.ptr(addend), bstride,
                                     out.data_ptr(), B, P, ws.data_ptr(), nbytes,
                                     N.stream_of(x.device)), "MLP.forward")
+        self.wcache_commit(wkey)
         del keep
         return out.to(dtype)
 
@@ -139,6 +217,7 @@ class MLP(nn.Module):
         """native_forward of (x_scale * x + x_shift) per (batch, channel) — the deferred
         output affine of the block that produced x (msfno_mlp_forward_affine; fused widths
         only)."""
+        dtype = x.dtype
         x = N.require_device_f32(x, "MLP input")
         B, Cin, H, W = x.shape
         xa = x_scale.detach().float().reshape(B, Cin).contiguous()
@@ -158,6 +237,7 @@ class MLP(nn.Module):
             bstride = 0 if addend.shape[0] == 1 else d.Cout * H * W
         L = N.lib()
         P = H * W
+        wkey = self.wcache_attach(d, keep, x.device)
         nbytes = L.msfno_mlp_workspace_size(d, B, P)
         ws = torch.empty(nbytes, dtype=torch.uint8, device=x.device)
         out = torch.empty(B, d.Cout, H, W, dtype=torch.float32, device=x.device)
@@ -165,8 +245,9 @@ class MLP(nn.Module):
                                            N.ptr(x2), N.ptr(addend), bstride, out.data_ptr(), B,
                                            P, ws.data_ptr(), nbytes, N.stream_of(x.device)),
                 "MLP.forward_affine")
+        self.wcache_commit(wkey)
         del keep
-        return out
+        return out.to(dtype)
 
     @N.on_input_device
     def native_backward_input(self, x, dy, x2=None):

@@ -13,14 +13,13 @@ residual adds live in GEMM epilogues.  Inference semantics (no autograd graph).
 """
 from __future__ import annotations
 
-import os
 
 import torch
 import torch.nn as nn
 
 from .. import _native as N
 from ..harmonics import RealSHT, adopt
-from .layers import MLP, DropPath, SpectralAttentionS2, SpectralConvS2
+from .layers import MLP, DropPath, SpectralAttentionS2, SpectralConvS2, WeightCache
 
 
 def _is_real_sht(t):
@@ -71,11 +70,9 @@ def _is_exact_gelu(m):
     return isinstance(m, nn.GELU) and getattr(m, "approximate", "none") == "none"
 
 
-# MSFNO_WCACHE=0: rebuild the weight images on every call (A/B of the prepared-weight cache)
-_WCACHE = not os.environ.get("MSFNO_WCACHE", "").startswith("0")
 
 
-class FourierNeuralOperatorBlock(nn.Module):
+class FourierNeuralOperatorBlock(WeightCache, nn.Module):
     _filmed = False
 
     def __init__(self, forward_transform, inverse_transform, embed_dim_sfno, filter_type="linear",
@@ -187,63 +184,8 @@ class FourierNeuralOperatorBlock(nn.Module):
     def _transforms(self):
         return self.filter_layer.filter._transforms()
 
-    def _wcache_key_of(self, device, nbytes):
-        """The prepared images depend only on the module's own weights: key on the
-        Parameters themselves (data_ptr, _version, dtype), not on the fp32 copies the
-        descriptor points at (those are fresh tensors, version 0, often at a reused
-        address)."""
-        return (str(device), nbytes) + tuple(
-            (p.data_ptr(), p._version, p.dtype) for p in self.parameters())
-
-    def wcache_attach(self, d, keep, device):
-        """Point the descriptor at this module's prepared-weight cache (bf16x3 weight
-        images, msfno_block_desc.wcache) and mark it valid when the weights are
-        unchanged since it was filled.  Returns the key to pass to wcache_commit once
-        the native call has been issued.  In-place weight updates bump _version, so
-        the next call rebuilds the images; a HIP graph captured with a valid cache
-        replays without the preparation (weights frozen, as in Rollout).
-
-        Stream safety: the images were written (and last read) on the stream of the
-        previous committed call; a call on another stream first waits for that call's
-        completion event, so it neither reads unwritten images nor rebuilds them under
-        a reader."""
-        L = N.lib()
-        nbytes = L.msfno_block_wcache_size(d)
-        if nbytes == 0 or not _WCACHE:
-            return None
-        buf = getattr(self, "_wcache_buf", None)
-        if buf is None or buf.device != device or buf.numel() < nbytes:
-            old_ev = getattr(self, "_wcache_event", None)
-            if buf is not None and old_ev is not None:
-                # the old buffer's last user may be another stream: the allocator must
-                # not hand its memory out before that stream's work is done
-                buf.record_stream(torch.cuda.ExternalStream(old_ev[0], device=buf.device))
-            buf = self._wcache_buf = torch.empty(nbytes, dtype=torch.uint8, device=device)
-            self._wcache_key = None
-            self._wcache_event = None
-        cur = torch.cuda.current_stream(device)
-        ev = getattr(self, "_wcache_event", None)
-        if ev is not None and ev[0] != cur.cuda_stream \
-                and not torch.cuda.is_current_stream_capturing():
-            cur.wait_event(ev[1])
-        key = self._wcache_key_of(device, nbytes)
-        d.wcache = buf.data_ptr()
-        d.wcache_valid = int(key == getattr(self, "_wcache_key", None))
-        return key
-
-    def wcache_commit(self, key):
-        """Mark the images valid after the native call that (re)built them.  Never
-        while the stream is being captured: the preparation then lives only in the
-        graph, and the buffer has not been written yet (a capture that found the
-        images valid leaves the key as it was)."""
-        if key is None or torch.cuda.is_current_stream_capturing():
-            return
-        dev = self._wcache_buf.device
-        cur = torch.cuda.current_stream(dev)
-        e = torch.cuda.Event()
-        e.record(cur)
-        self._wcache_event = (cur.cuda_stream, e)
-        self._wcache_key = key
+    def _wcache_bytes(self, d):
+        return N.lib().msfno_block_wcache_size(d)
 
     @N.on_input_device
     def _native_forward(self, x, gamma=None, beta=None, scale=1.0):
@@ -319,6 +261,35 @@ class FourierNeuralOperatorBlock_Filmed(FourierNeuralOperatorBlock):
                                         or x.requires_grad):
             return _FilmedBlockFn.apply(x, gamma, beta, float(scale), self)
         return self._native_forward(x, gamma, beta, scale)
+
+    @N.on_input_device
+    def global_conv(self, x, residual):
+        """sfnonet.py:341-356: norm0(x) -> filter -> + inner_skip(residual) (+ GELU for
+        the linear filter) -> norm1, without FiLM, MLP or outer skip
+        (msfno_block_global_conv; inference only)."""
+        dtype = x.dtype
+        x = N.require_device_f32(x, "global_conv input")
+        residual = N.require_device_f32(residual, "global_conv residual")
+        B, C, H, W = x.shape
+        fwd, inv = self._transforms()
+        assert H == fwd.nlat and W == fwd.nlon and C == self.embed_dim_sfno
+        if hasattr(self, "inner_skip"):
+            assert residual.shape == x.shape
+        pf = fwd._plan(x.device)
+        pi = inv._plan(x.device)
+        d, keep = self.native_desc()
+        L = N.lib()
+        wkey = self.wcache_attach(d, keep, x.device)
+        nbytes = L.msfno_block_workspace_size(d, pf.handle, pi.handle, B)
+        ws = torch.empty(nbytes, dtype=torch.uint8, device=x.device)
+        out = torch.empty(B, C, inv.nlat, inv.nlon, dtype=torch.float32, device=x.device)
+        N.check(L.msfno_block_global_conv(d, pf.handle, pi.handle, x.data_ptr(),
+                                          residual.data_ptr(), out.data_ptr(), B, ws.data_ptr(),
+                                          nbytes, N.stream_of(x.device)),
+                "FourierNeuralOperatorBlock_Filmed.global_conv")
+        self.wcache_commit(wkey)
+        del keep
+        return out.to(dtype)
 
     @N.on_input_device
     def native_film_backward(self, x, gamma, beta, scale, dout):
@@ -431,10 +402,14 @@ class FourierNeuralOperatorNet(nn.Module):
         self.pos_drop = nn.Dropout(p=drop_rate) if drop_rate > 0.0 else nn.Identity()
         self.dpr = [x.item() for x in torch.linspace(0, drop_path_rate, self.num_layers)]
         if self.normalization_layer == "layer_norm":
-            self.norm_layer0 = partial(nn.LayerNorm, normalized_shape=(img_size[0], img_size[1]),
-                                       eps=1e-6)
-            self.norm_layer1 = partial(nn.LayerNorm, normalized_shape=(self.h, self.w), eps=1e-6)
-        elif self.normalization_layer == "instance_norm":
+            # sfnonet.py:482-490 builds nn.LayerNorm over (H, W) with a per-pixel affine;
+            # the fused block folds its norms into per-(batch, channel) affines (norm0 into
+            # the spectral transpose, norm1 into the MLP's input loads), which a per-pixel
+            # affine does not fit.  Refused here, at construction, not at the first forward.
+            raise NotImplementedError(
+                "normalization_layer='layer_norm' is not on the MI355X path (the fused block "
+                "implements the reference default 'instance_norm')")
+        if self.normalization_layer == "instance_norm":
             self.norm_layer0 = partial(nn.InstanceNorm2d, num_features=embed_dim_sfno, eps=1e-6,
                                        affine=True, track_running_stats=False)
             self.norm_layer1 = self.norm_layer0

@@ -109,9 +109,9 @@ class BlockCfg:
     eps: float = 1e-6
 
 
-def block_forward(p, x, sht, isht, cfg: BlockCfg, gamma=None, beta=None, scale=1.0):
-    """SFNO-Block forward; FiLM applied iff gamma is not None (Filmed block)."""
-    residual = x
+def global_conv(p, x, residual, sht, isht, cfg: BlockCfg):
+    """FourierNeuralOperatorBlock_Filmed.global_conv(x, residual) (sfnonet.py:341-356):
+    the block up to norm1, the inner skip applied to `residual`."""
     x = instance_norm(x, p["norm0.weight"], p["norm0.bias"], cfg.eps)
     if cfg.filter_type == "non-linear":
         ws = [p[f"filter_layer.filter.w.{i}"] for i in range(cfg.spectral_layers)]
@@ -126,7 +126,14 @@ def block_forward(p, x, sht, isht, cfg: BlockCfg, gamma=None, beta=None, scale=1
         x = x + residual
     if cfg.filter_type == "linear":
         x = F.gelu(x)
-    x = instance_norm(x, p["norm1.weight"], p["norm1.bias"], cfg.eps)
+    return instance_norm(x, p["norm1.weight"], p["norm1.bias"], cfg.eps)
+
+
+def block_forward(p, x, sht, isht, cfg: BlockCfg, gamma=None, beta=None, scale=1.0):
+    """SFNO-Block forward (sfnonet.py:221-251, 359-393); FiLM applied iff gamma is not
+    None (Filmed block)."""
+    residual = x
+    x = global_conv(p, x, residual, sht, isht, cfg)
     if gamma is not None:
         x = film(x, gamma, beta, scale)
     if cfg.has_mlp:

@@ -20,7 +20,8 @@ Every other line executed (SpectralFilterLayer, SpectralAttentionS2,
 SpectralConvS2, contractions, ComplexReLU, MLP, InstanceNorm, FiLM, block
 wiring, the ×1e5 rescale recipe) is the reference's own code.
 
-Usage:  python tests/golden/make_golden.py [--net]   (--net: only the network fixtures)
+Usage:  python tests/golden/make_golden.py [--net | --gconv]   (only the network /
+        global_conv fixtures)
 """
 from __future__ import annotations
 
@@ -218,9 +219,46 @@ def main_net():
         print("wrote", path, tuple(y.shape), float(y.abs().max()))
 
 
+def main_global_conv():
+    """FourierNeuralOperatorBlock_Filmed.global_conv(x, residual) (sfnonet.py:341-356)
+    with residual != x, both filters, config-1 shapes, middle-block wiring."""
+    mods = load_reference()
+    sfnonet = mods["sfnonet"]
+    for filter_type in ("non-linear", "linear"):
+        seed = 777
+        torch.manual_seed(seed)
+        blk, sht, isht = build_ref_block(sfnonet, 32, 64, 32, 33, 8, filter_type, True,
+                                         "equiangular")
+        gen = torch.Generator().manual_seed(seed + 1)
+        randomize_(blk, gen)
+        blk.eval()
+        x = torch.randn(2, 8, 32, 64, generator=gen)
+        residual = 3.0 * torch.randn(2, 8, 32, 64, generator=gen)
+        with torch.no_grad():
+            y = blk.global_conv(x, residual)
+            y_self = blk.global_conv(x, x)
+        full_sd = blk.state_dict()
+        ft = "nl" if filter_type == "non-linear" else "lin"
+        out = {"meta_kind": "global_conv", "meta_filter": filter_type, "meta_nlat": 32,
+               "meta_nlon": 64, "meta_lmax": 32, "meta_mmax": 33, "meta_C": 8,
+               "meta_grid": "equiangular", "x": x.numpy(), "residual": residual.numpy(),
+               "y": y.numpy(), "y_self": y_self.numpy(),
+               "state_dict_keys": np.array(sorted(full_sd.keys()))}
+        for k, v in full_sd.items():
+            if not k.endswith((".weights", ".pct")):
+                out["p__" + k] = v.numpy()
+        path = os.path.join(HERE, "gconv", f"gconv_{ft}.npz")
+        os.makedirs(os.path.dirname(path), exist_ok=True)
+        np.savez_compressed(path, **out)
+        print("wrote", path, tuple(y.shape), float(y.abs().max()))
+
+
 if __name__ == "__main__":
     if "--net" in sys.argv:
         main_net()
+    elif "--gconv" in sys.argv:
+        main_global_conv()
     else:
         main()
         main_net()
+        main_global_conv()

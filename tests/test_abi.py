@@ -32,7 +32,7 @@ def test_library_exports_every_declared_symbol():
         assert hasattr(lib, s), s
     # and the ctypes binding covers all of them
     assert {n for n, _, _ in N.SIGNATURES} == set(_declared_symbols())
-    assert lib.msfno_abi_version() == 4
+    assert lib.msfno_abi_version() == 5
 
 
 def test_block_desc_struct_layout():

@@ -70,3 +70,15 @@ def test_torch_harmonics_style_transforms_are_adopted():
     bad.norm = "schmidt"
     with pytest.raises(NotImplementedError):
         SpectralFilterLayer(bad, g, 8, "linear").filter._transforms()
+
+
+def test_layer_norm_network_is_refused_at_construction():
+    """normalization_layer='layer_norm' (sfnonet.py:482-490, a per-pixel LayerNorm affine)
+    is not fused: the mirror refuses it when the network is built, not at its first
+    forward."""
+    import pytest
+    from msfno_amd.sfno import FourierNeuralOperatorNet
+    with pytest.raises(NotImplementedError, match="layer_norm"):
+        FourierNeuralOperatorNet("cpu", None, img_size=(33, 64), scale_factor=4, in_chans=5,
+                                 out_chans=5, embed_dim_sfno=16, num_layers=4,
+                                 normalization_layer="layer_norm")

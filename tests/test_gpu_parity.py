@@ -261,3 +261,23 @@ def test_block_over_torch_harmonics_style_transforms():
     with torch.no_grad():
         ya, yb = a(x, gm, bt, 0.7), b(x, gm, bt, 0.7)
     assert (ya - yb).abs().max().item() < 1e-5 * max(1.0, ya.abs().max().item())
+
+
+@pytest.mark.parametrize("ft", ["nl", "lin"])
+def test_global_conv_matches_reference_golden(ft):
+    """FourierNeuralOperatorBlock_Filmed.global_conv(x, residual) (sfnonet.py:341-356) on
+    the native block (msfno_block_global_conv), residual != x (its x3h scales from its
+    own max) and residual == x, against the reference's own output."""
+    from golden_util import GOLDEN
+    meta, params, arrays, _ = load(os.path.join(GOLDEN, "gconv", f"gconv_{ft}.npz"))
+    meta = dict(meta, filmed=1, wiring="middle")
+    blk, _, _ = make_block(meta, params)
+    blk = blk.to(DEV)
+    x, r = arrays["x"].to(DEV), arrays["residual"].to(DEV)
+    with torch.no_grad():
+        y = blk.global_conv(x, r).cpu()
+        y_self = blk.global_conv(x, x).cpu()
+    for got, want in ((y, arrays["y"]), (y_self, arrays["y_self"])):
+        err = (got - want).abs().max().item()
+        assert got.shape == want.shape
+        assert err < 1e-4, f"max-abs {err:.3e}"

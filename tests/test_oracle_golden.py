@@ -45,3 +45,18 @@ def test_oracle_block_matches_reference(path):
     # state-dict names the oracle consumes exist in the reference module
     for k in p:
         assert k in keys
+
+
+@pytest.mark.parametrize("ft", ["nl", "lin"])
+def test_oracle_global_conv_matches_reference(ft):
+    """FourierNeuralOperatorBlock_Filmed.global_conv(x, residual) (sfnonet.py:341-356),
+    residual != x and residual == x, against the reference (make_golden.py --gconv)."""
+    meta, p, a, keys = load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden",
+                                         "gconv", f"gconv_{ft}.npz"))
+    sht, isht = _transforms(meta)
+    cfg = sfno_ref.BlockCfg(filter_type=meta["filter"])
+    with torch.no_grad():
+        y = sfno_ref.global_conv(p, a["x"], a["residual"], sht, isht, cfg)
+        y_self = sfno_ref.global_conv(p, a["x"], a["x"], sht, isht, cfg)
+    assert (y - a["y"]).abs().max().item() < 1e-5
+    assert (y_self - a["y_self"]).abs().max().item() < 1e-5
