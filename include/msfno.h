@@ -246,6 +246,26 @@ int msfno_block_film_backward(const msfno_block_desc* d, msfno_sht_plan_t fwd,
                               float* dgamma, float* dbeta, int B, void* ws, size_t ws_bytes,
                               void* stream);
 
+/* Full backward of the block, SFNO weights frozen: dx = dL/dx (and dgamma / dbeta for a
+ * filmed block) for dout = dL/d(out) of msfno_block_forward -- what --film-layers k
+ * (main.py:1083-1087) and --repeat-film (main.py:1133-1136) need, whose filmed blocks
+ * run back to back with autograd (sfnonet.py:838-844).  The forward is recomputed.  Two
+ * adjoint transform plans (built once by the caller):
+ *   fwd_adj: a FORWARD plan on inv's grid, table pct[m,l,k] c_m nlon_out / (2 pi) with
+ *            c_m = 1 for m = 0 and m = nlon_out / 2, else 2   (the adjoint of inv);
+ *   inv_adj: an INVERSE plan on fwd's grid, table weights[m,l,k] d_m (2 pi) / nlon_in with
+ *            d_m = 1 for m = 0 and m = nlon_in / 2, else 1/2  (the adjoint of fwd).
+ * dx (B,C,nlat_in,nlon_in), dgamma / dbeta (B,C) may each be NULL; gamma / beta NULL for an
+ * unfilmed block. */
+size_t msfno_block_backward_workspace_size(const msfno_block_desc* d, msfno_sht_plan_t fwd,
+                                           msfno_sht_plan_t inv, msfno_sht_plan_t fwd_adj,
+                                           msfno_sht_plan_t inv_adj, int B);
+int msfno_block_backward(const msfno_block_desc* d, msfno_sht_plan_t fwd, msfno_sht_plan_t inv,
+                         msfno_sht_plan_t fwd_adj, msfno_sht_plan_t inv_adj, const float* x,
+                         const float* gamma, const float* beta, float film_scale,
+                         const float* dout, float* dx, float* dgamma, float* dbeta, int B,
+                         void* ws, size_t ws_bytes, void* stream);
+
 /* Backward of the channel MLP (layers.py:145-178) to its first input, weights
  * frozen: the decoder over cat(x, residual) (sfnonet.py:679-686) when the loss
  * gradient dy = dL/dy reaches it.

@@ -231,13 +231,9 @@ int side_ctx(std::shared_ptr<SideCtx>* out, hipStream_t caller) {
   if (!enabled) return MSFNO_OK;
   // no fork while the caller's stream is being captured into a HIP graph: the
   // captured fork/join made a 12-block network step 19.0 ms instead of 12.4 ms
-  // (replayed, config 3, round 2); the graph runs the skip GEMM in line.
-  // MSFNO_GRAPH_FORK=1 captures the fork / join as graph branches (A/B)
-  static const bool graph_fork = [] {
-    const char* e = getenv("MSFNO_GRAPH_FORK");
-    return e && e[0] == '1';
-  }();
-  if (caller && !graph_fork) {
+  // (replayed, config 3, round 2) and still 8.16 vs 8.10 ms in round 5 (profiles/r05_b);
+  // the graph runs the skip GEMM in line
+  if (caller) {
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
     if (hipStreamIsCapturing(caller, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone)
       return MSFNO_OK;
@@ -1815,17 +1811,12 @@ static int block_forward_impl(const msfno_block_desc* d, msfno_sht_plan_t f, msf
     if (!xpl && !b.xs) MSFNO_TRY(launch_skip());
   }
   // The skip is forked after the norm0 statistics (x3h: its per-channel scales come from
-  // them), so it never shares the GPU with this block's forward FFT: skip_h co-resident
-  // with a row FFT (a fork at the block start, retired MSFNO_SKIP_PX) corrupted real parts
-  // of single FFT bins
-  // linear filter: MSFNO_LIN_SKIP_AT=inv forks the skip after the HBM-bound per-mode
-  // contraction instead (its 2.1 GB then do not share HBM with the 34 GB weight stream;
-  // A/B)
-  static const bool lin_skip_late = [] {
-    const char* e = getenv("MSFNO_LIN_SKIP_AT");
-    return e && std::string(e) == "inv";
-  }();
-  const bool skip_late = lin_skip_late && d->filter_type != MSFNO_FILTER_NONLINEAR;
+  // them).  It slows whatever it overlaps by about its own length: forked after the forward
+  // Legendre instead (overlapping only the MFMA-bound spectral layers) measured equal
+  // (160.8 / 159.9 vs 160.7 / 159.9 fields/s, round 5).  The linear filter forks it after
+  // the per-mode contraction, so its 2.1 GB do not share HBM with the 34 GB weight stream:
+  // 94.0 / 94.2 vs 92.2 / 92.3 fields/s (profiles/r05_b)
+  const bool skip_late = d->filter_type != MSFNO_FILTER_NONLINEAR;
   if (b.xs && skip_late)
     MSFNO_TRY(run_spectral(d, f, g, b, x, B, true, s, nullptr, std::function<int()>(),
                            std::function<int()>(), std::function<int()>(), launch_skip));

@@ -426,11 +426,13 @@ int msfno_band_block_stage(const msfno_block_desc* d, msfno_band_plan_t p, int s
     prof(ST_SKIP, ss);
     GemmEpi e;
     e.bias = d->skip_b;
-    // x3h: B-row scales from the global norm0 statistics (stage 1).  Always gemm_x3 here,
-    // never skip_h: the pipelined sub-batches put this side-stream skip beside other
-    // sub-batches' row FFTs, and skip_h co-resident with a row FFT corrupts the FFT's
-    // output (gemm_x3 beside it measured clean)
-    if (b.fb.xs) {
+    // x3h: B-row scales from the global norm0 statistics (stage 1).  The pipelined
+    // sub-batches put this side-stream skip beside other sub-batches' row FFTs: safe since
+    // the FFT units carry no packed-FP32 op_sel:[0,1] forms
+    if (b.fb.xs && C == 256 && skip_h_env()) {
+      MSFNO_TRY(launch_skip_h(d->skip_w, b.fb.xs, io->x, b.x1, d->skip_b, B, Pl, b.fb.dw.skip,
+                              b.fb.dw.skip_b, ss));
+    } else if (b.fb.xs) {
       MSFNO_TRY(gemm_x3(d->skip_w, (int)C, b.fb.xs, io->x, b.x1, (int)C, (int)Pl, (int)C,
                         (int)Pl, (int)Pl, C * Pl, C * Pl, B, e, b.fb.dw.skip, b.fb.dw.skip_b,
                         ss));

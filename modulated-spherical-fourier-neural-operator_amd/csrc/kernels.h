@@ -154,6 +154,24 @@ int launch_gelu_grad_mul(float* dh, const float* pre, int64_t n, hipStream_t s);
 int launch_film_grad_reduce(const float* du, const float* x1, const float* an, const float* tn,
                             float scale, int BC, int64_t P, float* dgamma, float* dbeta,
                             hipStream_t s);
+// full block backward (block_bwd.cpp): per-row InstanceNorm moments and affine,
+// InstanceNorm backward (with the FiLM factor 1 + gamma s and up to two addends),
+// ComplexReLU(real) mask, complex conjugate transposes, tril <-> dense spectra, fill
+int launch_row_moments(const float* x, int64_t rows, int C, int64_t P, const float* w,
+                       const float* b, float eps, float* mean, float* rstd, float* scale,
+                       float* shift, hipStream_t s);
+int launch_inorm_backward(const float* x, const float* mean, const float* rstd, const float* w,
+                          const float* gamma, float film_scale, const float* g, const float* add1,
+                          const float* add2, float* dx, int64_t rows, int C, int64_t P,
+                          hipStream_t s);
+int launch_relu_real_mask(float* dh, const float* h, int64_t n, hipStream_t s);
+int launch_conj_swap01(const float* w, int I, int K, int64_t T, float* wt, hipStream_t s);
+int launch_tril_map(const float* src, float* dst, int64_t rows, int lmax, int mmax, int64_t T,
+                    bool gather, hipStream_t s);
+int launch_fill(float* p, int64_t n, float v, hipStream_t s);
+// sc = (1 + gamma s) an, sh = (1 + gamma s) tn + beta s (n = B*C)
+int launch_film_affine(const float* an, const float* tn, const float* gamma, const float* beta,
+                       float film_scale, float* sc, float* sh, int64_t n, hipStream_t s);
 // *d_flag |= 1 unless table[m][l][nlat-1-k] = (-1)^(l-m) table[m][l][k] (rel. 1e-5)
 int launch_check_symmetry(const float* table, int mmax, int lmax, int nlat, int* d_flag,
                           hipStream_t s);

@@ -110,6 +110,10 @@ SIGNATURES = [
     ("msfno_block_film_backward_workspace_size", _sz, [ctypes.POINTER(BlockDesc), _vp, _vp, _i]),
     ("msfno_block_film_backward", _i, [ctypes.POINTER(BlockDesc), _vp, _vp, _vp, _vp, _vp, _f,
                                        _vp, _vp, _vp, _i, _vp, _sz, _vp]),
+    ("msfno_block_backward_workspace_size", _sz, [ctypes.POINTER(BlockDesc), _vp, _vp, _vp, _vp,
+                                                   _i]),
+    ("msfno_block_backward", _i, [ctypes.POINTER(BlockDesc), _vp, _vp, _vp, _vp, _vp, _vp, _vp, _f,
+                                  _vp, _vp, _vp, _vp, _i, _vp, _sz, _vp]),
     ("msfno_mlp_backward_input_workspace_size", _sz, [ctypes.POINTER(MlpDesc), _i,
                                                        ctypes.c_longlong]),
     ("msfno_mlp_backward_input", _i, [ctypes.POINTER(MlpDesc), _vp, _vp, _vp, _vp, _i,

@@ -9,10 +9,11 @@ inverse SHT, inner skip (+GELU for the linear filter), norm1, FiLM, MLP and the
 outer skip — as ONE native call (``msfno_block_forward``) on the current HIP
 stream: the FFT kernel emits the norm0 statistics, norm0 is folded into the
 spectrum transpose, norm1+FiLM are folded into fc1's weights, and GELU / bias /
-residual adds live in GEMM epilogues.  Inference semantics (no autograd graph).
+residual adds live in GEMM epilogues.  Autograd (SFNO weights frozen, as MSFNO's FiLM
+fine-tuning): gradients to the FiLM modulation and to the block input through native
+backward calls (msfno_block_film_backward, msfno_block_backward).
 """
 from __future__ import annotations
-
 
 import torch
 import torch.nn as nn
@@ -68,8 +69,6 @@ class FiLM(nn.Module):
 
 def _is_exact_gelu(m):
     return isinstance(m, nn.GELU) and getattr(m, "approximate", "none") == "none"
-
-
 
 
 class FourierNeuralOperatorBlock(WeightCache, nn.Module):
@@ -214,7 +213,76 @@ class FourierNeuralOperatorBlock(WeightCache, nn.Module):
         return out.to(dtype)
 
     def forward(self, x, *overflow):
+        if torch.is_grad_enabled() and x.requires_grad:
+            return _BlockFn.apply(x, self)
         return self._native_forward(x)
+
+    def _adjoint_plans(self, device):
+        """The two adjoint transform plans of msfno_block_backward (include/msfno.h): a
+        forward plan on the output grid with table pct c_m nlon_out / 2pi (the adjoint of
+        the inverse SHT: irfft(norm="forward") weighs bin m by c_m = 2 but the DC and
+        Nyquist bins) and an inverse plan on the input grid with table weights d_m 2pi /
+        nlon_in (the adjoint of 2pi rfft(norm="forward"): d_m = 1/2 but DC and Nyquist).
+        Rebuilt only when a transform table tensor changes."""
+        import math
+        fwd, inv = self._transforms()
+        idx = device.index if device.index is not None else torch.cuda.current_device()
+        key = (idx,) + tuple((t.data_ptr(), t._version, t.dtype, str(t.device))
+                             for t in (fwd.weights, inv.pct))
+        cache = getattr(self, "_adj", None)
+        if cache is not None and cache[0] == key:
+            return cache[1], cache[2]
+        mmax = fwd.mmax
+        m = torch.arange(mmax, dtype=torch.float64)
+
+        def weights(n, inner, edge):
+            w = torch.full((mmax,), inner, dtype=torch.float64)
+            w[(m == 0) | (2 * m == n)] = edge
+            return w[:, None, None]
+        t1 = (inv.pct.detach().double().cpu() * weights(inv.nlon, 2.0, 1.0)
+              * (inv.nlon / (2 * math.pi))).float().to(device).contiguous()
+        t2 = (fwd.weights.detach().double().cpu() * weights(fwd.nlon, 0.5, 1.0)
+              * (2 * math.pi / fwd.nlon)).float().to(device).contiguous()
+        fa = N.SHTPlan(inv.nlat, inv.nlon, inv.lmax, inv.mmax, False, idx)
+        fa.load(t1, key)
+        ga = N.SHTPlan(fwd.nlat, fwd.nlon, fwd.lmax, fwd.mmax, True, idx)
+        ga.load(t2, key)
+        self._adj = (key, fa, ga)
+        return fa, ga
+
+    @N.on_input_device
+    def native_backward(self, x, dout, gamma=None, beta=None, scale=1.0, need_dx=True):
+        """(dL/dx, dL/dgamma, dL/dbeta) for dout = dL/d(out), the SFNO weights frozen
+        (msfno_block_backward; the forward is recomputed).  dgamma / dbeta are None for an
+        unfilmed call; dx is None unless need_dx."""
+        x = N.require_device_f32(x, "block input")
+        dout = N.require_device_f32(dout, "block output gradient")
+        B, C, H, W = x.shape
+        fwd, inv = self._transforms()
+        assert H == fwd.nlat and W == fwd.nlon and C == self.embed_dim_sfno
+        assert dout.shape == (B, C, inv.nlat, inv.nlon)
+        pf = fwd._plan(x.device)
+        pi = inv._plan(x.device)
+        fa, ga = self._adjoint_plans(x.device)
+        d, keep = self.native_desc()
+        g = b = dg = db = None
+        if gamma is not None:
+            g = gamma.detach().float().reshape(B, C).contiguous()
+            b = beta.detach().float().reshape(B, C).contiguous()
+            dg = torch.empty(B, C, dtype=torch.float32, device=x.device)
+            db = torch.empty(B, C, dtype=torch.float32, device=x.device)
+        dx = torch.empty_like(x) if need_dx else None
+        L = N.lib()
+        nbytes = L.msfno_block_backward_workspace_size(d, pf.handle, pi.handle, fa.handle,
+                                                        ga.handle, B)
+        ws = torch.empty(nbytes, dtype=torch.uint8, device=x.device)
+        N.check(L.msfno_block_backward(d, pf.handle, pi.handle, fa.handle, ga.handle, x.data_ptr(),
+                                       N.ptr(g), N.ptr(b), float(scale), dout.data_ptr(),
+                                       N.ptr(dx), N.ptr(dg), N.ptr(db), B, ws.data_ptr(), nbytes,
+                                       N.stream_of(x.device)),
+                type(self).__name__ + ".backward")
+        del keep
+        return dx, dg, db
 
     def defers_output_affine(self):
         """True for blocks whose output is one per-channel affine of x1 (no MLP, no outer
@@ -332,12 +400,31 @@ class _FilmedBlockFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dout):
         x, gamma, beta = ctx.saved_tensors
+        dx = None
         if ctx.needs_input_grad[0]:
-            raise NotImplementedError(
-                "dL/dx through a filmed block is not on the MI355X path (film_layers > 1)")
-        dg, db = ctx.blk.native_film_backward(x, gamma, beta, ctx.scale, dout)
-        return None, dg.reshape(gamma.shape).to(gamma.dtype), \
+            # dL/dx too (film_layers > 1, repeat_film: filmed blocks back to back)
+            dx, dg, db = ctx.blk.native_backward(x, dout, gamma, beta, ctx.scale)
+            dx = dx.to(x.dtype)
+        else:
+            dg, db = ctx.blk.native_film_backward(x, gamma, beta, ctx.scale, dout)
+        return dx, dg.reshape(gamma.shape).to(gamma.dtype), \
             db.reshape(beta.shape).to(beta.dtype), None, None
+
+
+class _BlockFn(torch.autograd.Function):
+    """Native unfilmed block forward with dL/dx (weights frozen; msfno_block_backward)."""
+
+    @staticmethod
+    def forward(ctx, x, blk):
+        ctx.blk = blk
+        ctx.save_for_backward(x)
+        return blk._native_forward(x)
+
+    @staticmethod
+    def backward(ctx, dout):
+        (x,) = ctx.saved_tensors
+        dx, _, _ = ctx.blk.native_backward(x, dout)
+        return dx.to(x.dtype), None
 
 
 def _trunc_normal_init(m):
