@@ -241,6 +241,21 @@ __device__ __forceinline__ void glds16x4(uint64_t sbase, const uint32_t (&voff)[
 }
 
 
+// one wave-instruction, SADDR form: lane l copies 16 B from sbase + voff (lane's 32-bit
+// byte offset) to LDS byte lds + 16 l (sbase, lds wave-uniform)
+__device__ __forceinline__ void glds16s(uint64_t sbase, uint32_t voff, uint32_t lds) {
+  unsigned keep;
+  sbase = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(sbase >> 32)) << 32) |
+          (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)sbase);
+  lds = (uint32_t)__builtin_amdgcn_readfirstlane((int)lds);
+  asm volatile(
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %2, %1\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "s"(sbase), "v"(voff), "s"(lds)
+      : "memory");
+}
+
 // The block MLP for one tile of 64 pixels (4 waves of 16; two workgroups per CU).
 // Prologue: the weight slices 0..3 go in flight by LDS-DMA; the field's range scalars
 // (xi_b from max_c abound, eta_b from B_b + 1) are reduced over the workgroup; x1 of the
@@ -571,8 +586,9 @@ __global__ void sk_image_kernel(const float* __restrict__ W, const float* __rest
   }
 }
 
-__global__ __launch_bounds__(256, 2) void skip_h_kernel(SkipHParams p) {
-  constexpr int NS = MH_NS, W = 4;
+template <int NS, int MINB>
+__global__ __launch_bounds__(256, MINB) void skip_h_kernel(SkipHParams p) {
+  constexpr int W = 4;
   constexpr int RING_BYTES = NS * MH_SLICE * 2;
   __shared__ __attribute__((aligned(16))) char lds_raw[RING_BYTES + 2 * MH_C * 4];
   unsigned short* const ring = reinterpret_cast<unsigned short*>(lds_raw);
@@ -682,6 +698,295 @@ __global__ __launch_bounds__(256, 2) void skip_h_kernel(SkipHParams p) {
   }
 }
 
+// Persistent, pipelined form of skip_h_kernel (one workgroup of 4 waves per CU, one
+// wave per SIMD with the whole register file: 32 pixels per wave as two 16-pixel
+// groups, 128 per tile; a contiguous range of tiles per workgroup).  skip_h_kernel
+// runs one tile per workgroup: its x loads, its 16 slice steps and its 64 four-byte
+// stores per lane are three phases that every CU enters at the same time, so HBM idles
+// while the MFMAs run and the MFMAs idle while x streams in.  Here one ring carries,
+// per slice step, the weight slice of this tile AND one 16-channel piece of the NEXT
+// tile's x (8 KB, LDS-DMA), which the step converts into the next tile's B fragments
+// in registers; the outputs leave through a per-wave LDS transpose as 16-B stores
+// (whole 128-B lines, 32 per lane instead of 128).  HBM then streams x and out under
+// the MFMAs, and each A fragment read from LDS feeds both pixel groups.
+//
+// vmcnt accounting (each wave, in issue order): group n = 6 LDS-DMAs (four 1-KB weight
+// pieces + two x-piece rows pairs), issued at step n - (NS - 1); a tile's 32 output
+// stores come after its step 15.  The wait for group n at step n leaves NS - 2 younger
+// groups in flight, plus the previous tile's stores when n is one of the first NS - 1
+// steps of a tile (tile 0: those groups were drained in the prologue).  The tail
+// issues dummy groups (the last tile again) so the counts stay exact, and the kernel
+// drains every DMA before it exits.
+constexpr int SP_NS = 5, SP_W = 4, SP_PX = 32 * SP_W;
+constexpr int SP_XPAIR = 1024 + 32;                  // two 512-B x rows + bank pad
+constexpr int SP_WBYTES = MH_SLICE * 2;              // 16 KB of weights
+constexpr int SP_SLOT = SP_WBYTES + 8 * SP_XPAIR;    // 24,832 B
+constexpr int SP_ERS = 36;                           // epilogue row stride (floats)
+constexpr int SP_EPI = 32 * SP_ERS * 4;              // per wave: 32 channels x 32 pixels
+constexpr int SP_LDS = SP_NS * SP_SLOT + SP_W * SP_EPI + 3 * MH_C * 4;
+constexpr int SP_GROUP = 6;                          // DMAs per wave and step
+static_assert(SP_LDS <= 160 * 1024, "skip_hp LDS");
+static_assert(SP_SLOT % 16 == 0 && SP_EPI % 16 == 0, "skip_hp LDS alignment");
+static_assert(SP_GROUP * (SP_NS - 2) + 32 <= 63, "skip_hp vmcnt range");
+
+struct SkipHPParams {
+  const float* x;
+  const float* xs;
+  float* out;
+  const unsigned short* img;
+  const float* inv_rs;
+  const float* bias;
+  int64_t P;
+  int tiles_per_field;
+  int tiles;
+};
+
+__global__ __launch_bounds__(64 * SP_W, 1) void skip_hp_kernel(SkipHPParams p) {
+  constexpr int NS = SP_NS;
+  __shared__ __attribute__((aligned(16))) char lds[SP_LDS];
+  float* const epi_all = reinterpret_cast<float*>(lds + NS * SP_SLOT);
+  float* const xsl = reinterpret_cast<float*>(lds + NS * SP_SLOT + SP_W * SP_EPI);
+  float* const irsl = xsl + MH_C;
+  float* const bl = irsl + MH_C;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int r16 = lane & 15, g = lane >> 4;
+  const int64_t P = p.P;
+  const int t0 = (int)((int64_t)blockIdx.x * p.tiles / gridDim.x);
+  const int t1 = (int)((int64_t)(blockIdx.x + 1) * p.tiles / gridDim.x);
+  const int ntile = t1 - t0;  // >= 1: the host launches at most `tiles` workgroups
+  const int tpf = p.tiles_per_field;
+  const uint32_t ring_lds = lds_addr(lds);
+  const int wave_u = __builtin_amdgcn_readfirstlane(wave);
+
+  // x piece of step q: 16 channels 32 (q >> 1) + 8 g' + 4 (q & 1) + e (g' 0..3, e 0..3),
+  // piece row i = 4 g' + e, rows (2k, 2k + 1) at k * SP_XPAIR.  This wave's two DMAs move
+  // rows 4 wave + 2 h2 + (lane >> 5), pixels 4 (lane & 31) .. + 3 of the tile.
+  const uint32_t w_voff = (uint32_t)lane * 16;
+  uint32_t x_voff_row[2];
+#pragma unroll
+  for (int h2 = 0; h2 < 2; ++h2) {
+    const int xrow = 4 * wave + 2 * h2 + (lane >> 5);
+    x_voff_row[h2] = (uint32_t)(8 * (xrow >> 2) + (xrow & 3)) * (uint32_t)P * 4;
+  }
+  const int xcol = 4 * (lane & 31);
+
+  // per-tile DMA sources (uniform): the tile's weight image, the x base of the tile
+  // after it (or of itself at the end: never read) and that tile's pixel limit
+  struct Src {
+    uint64_t w, x;
+    uint32_t xo[2];
+  };
+  auto src_of = [&](int tl) {
+    if (tl >= ntile) tl = ntile - 1;  // tail: dummy groups
+    const int t = t0 + tl;
+    const int z = t / tpf;
+    const int tn = tl + 1 < ntile ? t + 1 : t;
+    const int zn = tn / tpf;
+    const int64_t pxt = (int64_t)(tn - zn * tpf) * SP_PX;
+    const int64_t room = P - 4 - pxt;  // >= 0: P % 4 == 0 and pxt < P
+    const int lim = room < SP_PX - 4 ? (int)room : SP_PX - 4;
+    Src r;
+    r.w = reinterpret_cast<uint64_t>(p.img + (int64_t)z * SK_NSLICE * MH_SLICE) + (uint64_t)(wave_u * 1024);
+    r.x = reinterpret_cast<uint64_t>(p.x + (int64_t)zn * MH_C * P + pxt);
+    const uint32_t c4 = (uint32_t)min(xcol, lim) * 4;
+    r.xo[0] = x_voff_row[0] + c4;
+    r.xo[1] = x_voff_row[1] + c4;
+    return r;
+  };
+  auto issue = [&](const Src& sr, int n, int q) {
+    // opaque copies: keep the per-step address arithmetic at the step (hoisted to the
+    // tile start, 16 steps of addresses overflow the SGPRs)
+    uint64_t wb = sr.w, xb0 = sr.x, p4 = (uint64_t)P * 4;
+    asm volatile("" : "+s"(wb), "+s"(xb0), "+s"(p4));
+    const uint32_t slot = ring_lds + (uint32_t)((n % NS) * SP_SLOT);
+    const uint64_t wq = wb + (uint64_t)q * MH_SLICE * 2;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      glds16s(wq + (uint64_t)(i * 4096), w_voff, slot + (uint32_t)(i * 4096 + wave_u * 1024));
+    const uint64_t xq = xb0 + (uint64_t)(32 * (q >> 1) + 4 * (q & 1)) * p4;
+#pragma unroll
+    for (int h2 = 0; h2 < 2; ++h2)
+      glds16s(xq, sr.xo[h2], slot + (uint32_t)(SP_WBYTES + (2 * wave_u + h2) * SP_XPAIR));
+  };
+
+  int zc = t0 / tpf, zx = (ntile > 1 ? t0 + 1 : t0) / tpf;
+  for (int i = tid; i < MH_C; i += 64 * SP_W) {
+    bl[i] = p.bias ? p.bias[i] : 0.f;
+    irsl[i] = p.inv_rs[(int64_t)zc * MH_C + i];
+    xsl[i] = p.xs[(int64_t)zx * MH_C + i];
+  }
+  {
+    const Src s0 = src_of(0);
+#pragma unroll
+    for (int n = 0; n < NS - 1; ++n) issue(s0, n, n);
+  }
+
+  // the first tile's x -> B fragments (plain loads, once per workgroup)
+  half8 xf[2][8][2];
+  {
+    const float* xsb = p.xs + (int64_t)zc * MH_C;
+#pragma unroll
+    for (int pg = 0; pg < 2; ++pg) {
+      int64_t px = (int64_t)(t0 - zc * tpf) * SP_PX + 32 * wave + 16 * pg + r16;
+      if (px > P - 1) px = P - 1;  // past the field's end (never stored)
+      const float* xw = p.x + (int64_t)zc * MH_C * P;
+      const uint32_t lo = (uint32_t)(8 * g) * (uint32_t)P + (uint32_t)px;
+#pragma unroll
+      for (int ks = 0; ks < 8; ++ks) {
+        const int c0 = 32 * ks + 8 * g;
+        float xv[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+          xv[e] = __builtin_nontemporal_load(xw + (int64_t)(32 * ks + e) * P + lo);
+        const float4 sa = *reinterpret_cast<const float4*>(xsb + c0);
+        const float4 sb = *reinterpret_cast<const float4*>(xsb + c0 + 4);
+        const float sv[8] = {sa.x, sa.y, sa.z, sa.w, sb.x, sb.y, sb.z, sb.w};
+        uint32_t t[2][4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          split2h(sv[2 * e] * xv[2 * e], sv[2 * e + 1] * xv[2 * e + 1], t[0][e], t[1][e]);
+#pragma unroll
+        for (int pl = 0; pl < 2; ++pl) xf[pg][ks][pl] = mh_frag(t[pl][0], t[pl][1], t[pl][2], t[pl][3]);
+      }
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  const int a_lane = r16 * 32 + 8 * (g ^ mh_swz(r16));
+  float* const ep = epi_all + wave * 32 * SP_ERS;
+  uint32_t xn[2][8][2][4];
+
+  for (int tl = 0; tl < ntile; ++tl) {
+    const int t = t0 + tl;
+    if (tl > 0) {
+      const int zc2 = t / tpf, zx2 = (tl + 1 < ntile ? t + 1 : t) / tpf;
+      if (zc2 != zc || zx2 != zx) {  // a field boundary: new scale tables (drains the ring)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        for (int i = tid; i < MH_C; i += 64 * SP_W) {
+          irsl[i] = p.inv_rs[(int64_t)zc2 * MH_C + i];
+          xsl[i] = p.xs[(int64_t)zx2 * MH_C + i];
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        zc = zc2;
+        zx = zx2;
+      }
+    }
+    const Src s_cur = src_of(tl), s_nxt = src_of(tl + 1);
+    floatx4 oacc[2][16];
+#pragma unroll
+    for (int pg = 0; pg < 2; ++pg)
+#pragma unroll
+      for (int ot = 0; ot < 16; ++ot) oacc[pg][ot] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+#pragma unroll
+    for (int q = 0; q < SK_NSLICE; ++q) {
+      const int n = tl * SK_NSLICE + q;
+      if (q < NS - 1) asm volatile("s_waitcnt vmcnt(50)" ::: "memory");  // 6 (NS-2) + 32
+      else asm volatile("s_waitcnt vmcnt(18)" ::: "memory");              // 6 (NS-2)
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      const char* slot = lds + (n % NS) * SP_SLOT;
+      // the next tile's x piece -> its B fragments (channels 32 ks + 8 g + 4 h + 0..3)
+      {
+        const int ks = q >> 1, h = q & 1;
+        const float4 sv = *reinterpret_cast<const float4*>(xsl + 32 * ks + 8 * g + 4 * h);
+#pragma unroll
+        for (int pg = 0; pg < 2; ++pg) {
+          const char* xb = slot + SP_WBYTES + 4 * (32 * wave + 16 * pg + r16);
+          float v[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            v[e] = *reinterpret_cast<const float*>(xb + (2 * g + (e >> 1)) * SP_XPAIR + (e & 1) * 512);
+          split2h(sv.x * v[0], sv.y * v[1], xn[pg][ks][0][2 * h], xn[pg][ks][1][2 * h]);
+          split2h(sv.z * v[2], sv.w * v[3], xn[pg][ks][0][2 * h + 1], xn[pg][ks][1][2 * h + 1]);
+        }
+      }
+      const unsigned short* ws = reinterpret_cast<const unsigned short*>(slot);
+      const int j = q >> 1, kh = q & 1;
+      auto aoff = [&](int u, int pl) { return ((pl * 4 + (u >> 1)) * 2 + (u & 1)) * 512 + a_lane; };
+      half8 a[3][2];
+#pragma unroll
+      for (int k = 0; k < 2; ++k)
+#pragma unroll
+        for (int pl = 0; pl < 2; ++pl) a[k][pl] = *reinterpret_cast<const half8*>(ws + aoff(k, pl));
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        if (u + 2 < 8) {
+#pragma unroll
+          for (int pl = 0; pl < 2; ++pl)
+            a[(u + 2) % 3][pl] = *reinterpret_cast<const half8*>(ws + aoff(u + 2, pl));
+        }
+        const half8* av = a[u % 3];
+#pragma unroll
+        for (int pg = 0; pg < 2; ++pg) {
+          const half8* xb = xf[pg][kh * 4 + (u >> 1)];
+          floatx4& c = oacc[pg][2 * j + (u & 1)];
+          c = __builtin_amdgcn_mfma_f32_16x16x32_f16(av[1], xb[0], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_f16(av[0], xb[1], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_f16(av[0], xb[0], c, 0, 0, 0);
+        }
+        if (u == 0) {
+          if (q + NS - 1 < SK_NSLICE) issue(s_cur, n + NS - 1, q + NS - 1);
+          else issue(s_nxt, n + NS - 1, q + NS - 1 - SK_NSLICE);
+        }
+      }
+    }
+
+    // epilogue: row 16 ot + 4 g + i, pixel 32 wave + 16 pg + r16; 32 rows per round
+    // through the wave's LDS patch, out as 16-B stores (a row's 32 pixels = one line)
+    {
+      const int64_t px0 = (int64_t)(t - zc * tpf) * SP_PX + 32 * wave;
+      float* const ob = p.out + (int64_t)zc * MH_C * P + px0;
+      const uint32_t so = (uint32_t)(lane >> 3) * (uint32_t)P + 4u * (uint32_t)(lane & 7);
+      const bool in = px0 + 4 * (lane & 7) < P;
+#pragma unroll
+      for (int c = 0; c < 8; ++c) {
+#pragma unroll
+        for (int o2 = 0; o2 < 2; ++o2) {
+          const int r0 = 16 * (2 * c + o2) + 4 * g;
+          const float4 is = *reinterpret_cast<const float4*>(irsl + r0);
+          const float4 bb = *reinterpret_cast<const float4*>(bl + r0);
+#pragma unroll
+          for (int pg = 0; pg < 2; ++pg) {
+            const floatx4 acc = oacc[pg][2 * c + o2];
+            float* e0 = ep + (16 * o2 + 4 * g) * SP_ERS + 16 * pg + r16;
+            e0[0] = fmaf(acc[0], is.x, bb.x);
+            e0[SP_ERS] = fmaf(acc[1], is.y, bb.y);
+            e0[2 * SP_ERS] = fmaf(acc[2], is.z, bb.z);
+            e0[3 * SP_ERS] = fmaf(acc[3], is.w, bb.w);
+          }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const int row = 8 * k + (lane >> 3), col = 4 * (lane & 7);
+          const floatx4 v = *reinterpret_cast<const floatx4*>(ep + row * SP_ERS + col);
+          if (in)
+            __builtin_nontemporal_store(
+                v, reinterpret_cast<floatx4*>(ob + (int64_t)(32 * c + 8 * k) * P + so));
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      }
+    }
+#pragma unroll
+    for (int pg = 0; pg < 2; ++pg)
+#pragma unroll
+      for (int ks = 0; ks < 8; ++ks)
+#pragma unroll
+        for (int pl = 0; pl < 2; ++pl)
+          xf[pg][ks][pl] = mh_frag(xn[pg][ks][pl][0], xn[pg][ks][pl][1], xn[pg][ks][pl][2], xn[pg][ks][pl][3]);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the tail's dummy DMAs land before exit
+}
+
 // xs[r] = 2^(14 - e), max_p |x[r][p]| = f 2^e (f in [0.5, 1)): every |xs x| < 2^14 (the
 // x3h B-row scale of a standalone 1x1 conv, whose input has no norm statistics); one
 // 256-thread workgroup per row r
@@ -738,7 +1043,38 @@ int launch_skip_h(const float* W, const float* xs, const float* x, float* out, c
   p.tiles_per_field = (int)cdiv(P, 64);
   const int64_t tiles = (int64_t)B * p.tiles_per_field;
   MSFNO_REQUIRE(tiles < (1LL << 31), MSFNO_EINVAL, "skip_h: grid too large");
-  hipLaunchKernelGGL(skip_h_kernel, dim3((unsigned)tiles), dim3(256), 0, s, p);
+  // the persistent pipelined kernel (MSFNO_SKIP_P=0: one tile per workgroup, read on
+  // every call so one process can run both); its x pieces and output stores move 4
+  // pixels per lane (P % 4 == 0)
+  const char* pe = getenv("MSFNO_SKIP_P");
+  const bool persist = !(pe && pe[0] == '0');
+  if (persist && P % 4 == 0) {
+    static const int cus = [] {
+      int dev = 0, n = 0;
+      if (hipGetDevice(&dev) != hipSuccess ||
+          hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+        n = 256;
+      return n;
+    }();
+    SkipHPParams q{};
+    q.x = x; q.xs = xs; q.out = out; q.img = img; q.inv_rs = inv_rs; q.bias = bias; q.P = P;
+    q.tiles_per_field = (int)cdiv(P, SP_PX);
+    const int64_t t = (int64_t)B * q.tiles_per_field;
+    MSFNO_REQUIRE(t < (1LL << 31), MSFNO_EINVAL, "skip_hp: grid too large");
+    q.tiles = (int)t;
+    const int grid = (int)std::min<int64_t>(t, cus);
+    hipLaunchKernelGGL(skip_hp_kernel, dim3((unsigned)grid), dim3(64 * SP_W), 0, s, q);
+    return launch_check("skip_hp");
+  }
+  // MSFNO_SKIP_NS=3: three ring slots, three workgroups per CU (A/B)
+  static const int ns = [] {
+    const char* e = getenv("MSFNO_SKIP_NS");
+    return e && e[0] == '3' ? 3 : 4;
+  }();
+  if (ns == 3)
+    hipLaunchKernelGGL((skip_h_kernel<3, 3>), dim3((unsigned)tiles), dim3(256), 0, s, p);
+  else
+    hipLaunchKernelGGL((skip_h_kernel<MH_NS, 2>), dim3((unsigned)tiles), dim3(256), 0, s, p);
   return launch_check("skip_h");
 }
 

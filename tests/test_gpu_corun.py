@@ -7,10 +7,9 @@ whenever skip_h_kernel ran beside it.  The cause: on gfx950 a packed-FP32 VALU o
 returns wrong low results in lanes 48..63 while another wave's MFMAs execute on the CU
 (tools/pk_opsel_sweep.cpp, profiles/r05_pk/).  The FFT and spectral units are built
 without packed FP32 (csrc/Makefile) and tests/test_isa_audit.py keeps the form out of
-the library; this test launches the inner-skip conv (skip_h_kernel, 2 workgroups per CU
-with room for a 24-KB FFT workgroup beside them) on one stream and the SHT of the
-network's 120 x 240 blocks on another, and requires the SHT outputs to equal their solo
-run bit for bit.  Reference: sfnonet.py:366-371 (inner skip), torch-harmonics RealSHT /
+the library; this test launches the inner-skip conv (both skip kernels) on one stream
+and the SHT of the network's 120 x 240 blocks on another, and requires the SHT outputs
+to equal their solo run bit for bit.  Reference: sfnonet.py:366-371 (inner skip), torch-harmonics RealSHT /
 InverseRealSHT as called at layers.py:629,638.
 """
 import ctypes
@@ -36,10 +35,14 @@ def _conv(w, b, x, stream=None):
 
 
 @pytest.mark.parametrize("B,Cin,Cout,P", [(2, 256, 256, 120 * 240), (1, 64, 32, 4000),
-                                          (3, 256, 256, 1000)])
+                                          (3, 256, 256, 1000), (3, 256, 256, 50000),
+                                          (1, 256, 256, 1038)])
 def test_conv1x1_matches_fp64(B, Cin, Cout, P):
     """The standalone 1x1 conv against fp64; channel magnitudes spread over 1e-3 .. 1e3
-    (the per-channel power-of-two scales keep every fp16 term in range)."""
+    (the per-channel power-of-two scales keep every fp16 term in range).  C = 256 runs
+    the persistent skip kernel when P % 4 == 0: P = 50000 gives each workgroup several
+    128-pixel tiles that cross field boundaries and end in a partial tile; P = 1038 takes
+    the one-tile-per-workgroup kernel."""
     g = torch.Generator(device=DEV).manual_seed(5)
     x = torch.randn(B, Cin, P, generator=g, device=DEV)
     x *= torch.logspace(-3, 3, Cin, device=DEV)[None, :, None]
@@ -73,8 +76,13 @@ def _sht_call(plan, fn, src, dst, bc, ws, stream):
                stream.cuda_stream), "sht")
 
 
+@pytest.mark.parametrize("persist", ["0", "1"])
 @pytest.mark.parametrize("inverse", [False, True])
-def test_sht_beside_skip_conv_is_bitwise(inverse):
+def test_sht_beside_skip_conv_is_bitwise(inverse, persist, monkeypatch):
+    """persist "0": skip_h_kernel (two 66-KB workgroups per CU, room for an FFT workgroup
+    beside them on the same CU); "1": the persistent skip_hp_kernel (the block's default,
+    one 142-KB workgroup per CU).  MSFNO_SKIP_P is read on every call."""
+    monkeypatch.setenv("MSFNO_SKIP_P", persist)
     from msfno_amd import _native as N
     from msfno_amd.harmonics import InverseRealSHT, RealSHT
     nlat, nlon, lmax = 120, 240, 120
@@ -94,7 +102,7 @@ def test_sht_beside_skip_conv_is_bitwise(inverse):
         fn = N.lib().msfno_sht_forward
     ws = torch.empty(N.lib().msfno_sht_workspace_size(plan.handle, bc), dtype=torch.uint8,
                      device=DEV)
-    # the aggressor: the block's inner skip at C = 256 (skip_h_kernel) on 8 fields
+    # the aggressor: the block's inner skip at C = 256 on 8 fields
     P = nlat * nlon
     x = torch.randn(8, 256, P, generator=g, device=DEV)
     w = torch.randn(256, 256, generator=g, device=DEV) / 16
