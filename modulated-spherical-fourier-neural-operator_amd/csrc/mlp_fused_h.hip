@@ -265,12 +265,13 @@ __device__ __forceinline__ void glds16s(uint64_t sbase, uint32_t voff, uint32_t 
 // eta_j eta_b and split into fc2's B fragment (in place: mf_perm orders W2's columns),
 // W2(j - 1, 0..1) into the 256 x 16 output accumulators.  Epilogue: unscale + b2 +
 // residual, one store per output.
-template <int AHEAD>
-__global__ __launch_bounds__(256, 2) void mlp_fused_h_kernel(MlpHParams p) {
+constexpr int MH_LDS = MH_NS * MH_SLICE * 2 + (3 * MH_H + 2 * MH_C + 8) * 4;
+
+template <int AHEAD, bool EPI16>
+__device__ __forceinline__ void mlp_fused_h_tile(const MlpHParams& p, int lin, char* lds_raw) {
   constexpr int W = MH_WAVES, NS = MH_NS;
   constexpr int RING_BYTES = NS * MH_SLICE * 2;
   constexpr int TPX = 16 * W;  // pixels per workgroup tile
-  __shared__ __attribute__((aligned(16))) char lds_raw[RING_BYTES + (3 * MH_H + 2 * MH_C + 8) * 4];
   unsigned short* const ring = reinterpret_cast<unsigned short*>(lds_raw);
   float* const b1s = reinterpret_cast<float*>(lds_raw + RING_BYTES);
   float* const is1s = b1s + MH_H;
@@ -281,7 +282,6 @@ __global__ __launch_bounds__(256, 2) void mlp_fused_h_kernel(MlpHParams p) {
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r16 = lane & 15, g = lane >> 4;
-  const int lin = xcd_remap(blockIdx.x, gridDim.x);
   const int z = lin / p.tiles_per_field;
   const int64_t P = p.P;
   const int64_t px = (int64_t)(lin - z * p.tiles_per_field) * TPX + 16 * wave + r16;
@@ -472,6 +472,67 @@ __global__ __launch_bounds__(256, 2) void mlp_fused_h_kernel(MlpHParams p) {
   }
 #pragma unroll
   for (int e2 = 0; e2 < 4; ++e2) conv_pair(MH_HB - 1, e2, I1{});
+  if constexpr (EPI16) {
+    // EPI16 (P % 4 == 0): the outputs leave through a per-wave LDS transpose (the ring is
+    // idle after the last step) as 16-B stores, a row's 16 pixels = 64 contiguous bytes,
+    // 16 stores per lane instead of 64; the residual comes in the same layout as 16 float4
+    // loads, issued under the last two steps' MFMAs
+    const int64_t px0 = px - r16;
+    const int c4 = 4 * (lane & 3);
+    const bool in4 = px0 + c4 < P;
+    floatx4 rv4[8][2];
+    if (p.resid && in4) {
+      const float* rs = p.resid + (int64_t)z * MH_C * P + px0 + c4;
+#pragma unroll
+      for (int c = 0; c < 8; ++c)
+#pragma unroll
+        for (int k = 0; k < 2; ++k)
+          rv4[c][k] = __builtin_nontemporal_load(
+              reinterpret_cast<const floatx4*>(rs + (int64_t)(32 * c + 16 * k + (lane >> 2)) * P));
+    } else {
+#pragma unroll
+      for (int c = 0; c < 8; ++c)
+#pragma unroll
+        for (int k = 0; k < 2; ++k) rv4[c][k] = floatx4{0.f, 0.f, 0.f, 0.f};
+    }
+    fc2_step(step_begin(MH_NSLICE - 2), MH_NSLICE - 2, I0{});
+    fc2_step(step_begin(MH_NSLICE - 1), MH_NSLICE - 1, I1{});
+    // every wave's last fragment reads are done before the ring becomes transpose patches
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    constexpr int ERS = 20;
+    float* const ep = reinterpret_cast<float*>(lds_raw) + wave * 32 * ERS;
+    float* const ob = p.out + (int64_t)z * MH_C * P + px0 + c4;
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+#pragma unroll
+      for (int o2 = 0; o2 < 2; ++o2) {
+        const int r0 = 16 * (2 * c + o2) + 4 * g;
+        const float4 is = *reinterpret_cast<const float4*>(is2s + r0);
+        const float4 b = *reinterpret_cast<const float4*>(b2s + r0);
+        const floatx4 acc = oacc[2 * c + o2];
+        float* e0 = ep + (16 * o2 + 4 * g) * ERS + r16;
+        e0[0] = fmaf(acc[0], is.x, b.x);
+        e0[ERS] = fmaf(acc[1], is.y, b.y);
+        e0[2 * ERS] = fmaf(acc[2], is.z, b.z);
+        e0[3 * ERS] = fmaf(acc[3], is.w, b.w);
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        const int row = 16 * k + (lane >> 2);
+        const floatx4 v = *reinterpret_cast<const floatx4*>(ep + row * ERS + c4) + rv4[c][k];
+        if (in4)
+          __builtin_nontemporal_store(v, reinterpret_cast<floatx4*>(ob + (int64_t)(32 * c + row) * P));
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+    return;
+  }
   // the residual of every output row, all loads in flight at once and under the last
   // two steps' MFMAs (the x1 fragments are dead: their registers take it)
   float rv[16][4];
@@ -505,8 +566,13 @@ __global__ __launch_bounds__(256, 2) void mlp_fused_h_kernel(MlpHParams p) {
   }
 }
 
+// EPI16 (MSFNO_MH_EPI16=1, A/B): the transposed 16-B output stores of mlp_fused_h_tile
+template <int AHEAD, bool EPI16>
+__global__ __launch_bounds__(256, 2) void mlp_fused_h_kernel(MlpHParams p) {
+  __shared__ __attribute__((aligned(16))) char lds_raw[MH_LDS];
+  mlp_fused_h_tile<AHEAD, EPI16>(p, xcd_remap(blockIdx.x, gridDim.x), lds_raw);
+}
 
-// ---- inner skip (1x1 conv, C = 256) on the same tiling: out = Ws·x + bs -------------
 // The fc1 half of mlp_fused_h_kernel with 256 output rows and no hidden layer:
 // a wave's 16 pixels of x, scaled per channel by the power of two xs (chan_affine's
 // norm0 bound, |xs x| < 2^14) and split into fp16x2 B fragments in registers; the
@@ -1062,7 +1128,13 @@ int launch_skip_h(const float* W, const float* xs, const float* x, float* out, c
     const int64_t t = (int64_t)B * q.tiles_per_field;
     MSFNO_REQUIRE(t < (1LL << 31), MSFNO_EINVAL, "skip_hp: grid too large");
     q.tiles = (int)t;
-    const int grid = (int)std::min<int64_t>(t, cus);
+    // MSFNO_SKIP_GRID = workgroups per CU (default 2: each CU holds one 142-KB workgroup
+    // at a time, so the second half of the grid starts as the first retires, and the
+    // main stream's kernels get CUs in between; 1 and 0.5 measured 1 % slower in-block)
+    const char* ge = getenv("MSFNO_SKIP_GRID");
+    const double per_cu = ge ? atof(ge) : 2.0;
+    const int64_t want = std::max<int64_t>(1, (int64_t)(per_cu * cus + 0.5));
+    const int grid = (int)std::min<int64_t>(t, want);
     hipLaunchKernelGGL(skip_hp_kernel, dim3((unsigned)grid), dim3(64 * SP_W), 0, s, q);
     return launch_check("skip_hp");
   }
@@ -1129,7 +1201,12 @@ int launch_mlp_fused_h(const float* x1, const float* scale, const float* shift,
   p.tiles_per_field = (int)cdiv(P, 16 * MH_WAVES);
   const int64_t tiles = (int64_t)B * p.tiles_per_field;
   MSFNO_REQUIRE(tiles < (1LL << 31), MSFNO_EINVAL, "mlp_fused_h: grid too large");
-  hipLaunchKernelGGL(mlp_fused_h_kernel<2>, dim3((unsigned)tiles), dim3(64 * MH_WAVES), 0, s, p);
+  // MSFNO_MH_EPI16=1: transposed 16-B output stores (A/B)
+  const char* ee = getenv("MSFNO_MH_EPI16");
+  if (ee && ee[0] == '1' && P % 4 == 0)
+    hipLaunchKernelGGL((mlp_fused_h_kernel<2, true>), dim3((unsigned)tiles), dim3(64 * MH_WAVES), 0, s, p);
+  else
+    hipLaunchKernelGGL((mlp_fused_h_kernel<2, false>), dim3((unsigned)tiles), dim3(64 * MH_WAVES), 0, s, p);
   return launch_check("mlp_fused_h");
 }
 
