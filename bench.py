@@ -420,6 +420,8 @@ def run_net(args, rank, world, dev, dist, backend):
         for _ in range(max(args.warmup, 1)):
             y = run(x, film, 1.0)
         torch.cuda.synchronize()
+        if use_graph and band and dist:
+            run.comm.quiesce()  # RCCL watchdog: nothing pending while the capture runs
         if use_graph:
             # one 6 h step as a HIP graph: removes the host cost of ~300 launches and
             # the per-call module bookkeeping (the 120x240 blocks are launch-bound)

@@ -1795,7 +1795,8 @@ static int block_forward_impl(const msfno_block_desc* d, msfno_sht_plan_t f, msf
       MSFNO_TRY(gemm_x6p(d->skip_w, x1, (int)C, (int)P, (int)C, (int)C, (int)P, (int)P, 0,
                          3 * C * P, C * P, B, e, b.dw.skip, b.dw.skip_b, ss));
     } else {
-      MSFNO_TRY(gemm_dense(ROLE_SKIP, TILE_128x256, d->skip_w, x, x1, (int)C, (int)P, (int)C,
+      // sx: global_conv's skip input is the residual, not the filter input x
+      MSFNO_TRY(gemm_dense(ROLE_SKIP, TILE_128x256, d->skip_w, sx, x1, (int)C, (int)P, (int)C,
                            (int)C, (int)P, (int)P, 0, C * P, C * P, B, e, b.dw.skip, b.dw.skip_b,
                            ss));
     }

@@ -154,7 +154,10 @@ class Rollout:
         self.film, self.scale = film, scale
         comm = getattr(model, "comm", None)
         device_comm = comm is not None and not getattr(comm, "host", True)
-        self.use_graph = graph and (getattr(model, "world", 1) == 1 or device_comm)
+        # capture-or-eager must be one decision for all ranks (all_agree); a multi-rank
+        # comm that cannot agree steps eagerly on every rank
+        agreeable = device_comm and callable(getattr(comm, "all_agree", None))
+        self.use_graph = graph and (getattr(model, "world", 1) == 1 or agreeable)
         self._graph = None
 
     def normalise(self, data, reverse=False):
@@ -173,6 +176,9 @@ class Rollout:
     def _capture(self, x):
         self._state = x.clone()
         self._step(self._state)  # warm-up: plans, descriptors, allocator pools
+        quiesce = getattr(getattr(self.model, "comm", None), "quiesce", None)
+        if callable(quiesce):
+            quiesce()  # no RCCL work of the warm-up left for the watchdog to poll
         torch.cuda.synchronize()
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
@@ -198,9 +204,7 @@ class Rollout:
                 except RuntimeError:
                     ok = False
                     torch.cuda.synchronize()
-                agree = getattr(getattr(self.model, "comm", None), "all_agree", None)
-                if agree is not None:
-                    ok = agree(ok)
+                ok = self.model.comm.all_agree(ok)
                 if not ok:
                     self._graph = None
                     self.use_graph = False

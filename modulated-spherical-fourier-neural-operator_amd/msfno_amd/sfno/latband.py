@@ -121,6 +121,20 @@ class TorchComm:
         self.dist.all_reduce(t, op=self.dist.ReduceOp.MIN, group=self.group)
         return bool(t.item())
 
+    def quiesce(self):
+        """Before a HIP-graph capture of this group's collectives: drain the device and
+        let torch's ProcessGroupNCCL watchdog reap its completed work.  The watchdog
+        polls each pending work's end event; on HIP a query of an event whose stream
+        (RCCL's internal stream, which joins the capture) is capturing fails with
+        hipErrorCapturedEvent and the watchdog aborts the process.  Works issued during
+        capture are not handed to the watchdog, so an empty list before capture_begin
+        avoids the race."""
+        if self.host:
+            return
+        import time
+        torch.cuda.synchronize()
+        time.sleep(0.35)  # > 3 watchdog polling periods (100 ms)
+
     def all_gather(self, t):
         src = t.cpu() if self.host else t
         parts = [torch.empty_like(src) for _ in range(self.world)]
@@ -218,6 +232,15 @@ class LocalGroup:
     """Lock-step execution of several virtual ranks in one process (the
     exchanges become device copies).  Used by the parity tests to run the
     sharded path on one GPU, and by world-size-1 runs."""
+
+    @staticmethod
+    def all_agree(ok: bool) -> bool:
+        """Every virtual rank lives in this process and decides with it."""
+        return bool(ok)
+
+    @staticmethod
+    def quiesce():
+        torch.cuda.synchronize()
 
     @staticmethod
     def _exchange(reqs):

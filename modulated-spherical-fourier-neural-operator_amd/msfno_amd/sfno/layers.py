@@ -273,28 +273,35 @@ class MLP(WeightCache, nn.Module):
         return dx
 
     def forward(self, x):
-        if torch.is_grad_enabled() and x.requires_grad:
-            return _MLPFn.apply(x, None, None, self)
+        if torch.is_grad_enabled():
+            params = tuple(p for p in self.parameters() if p.requires_grad)
+            if x.requires_grad or params:
+                return _MLPFn.apply(x, None, None, self, *params)
         return self.native_forward(x)
 
 
 class _MLPFn(torch.autograd.Function):
     """Native MLP forward; backward to the first input only (weights frozen, as in
-    MSFNO's FiLM fine-tuning, sfnonet.py:787-860)."""
+    MSFNO's FiLM fine-tuning, sfnonet.py:787-860).  Trainable parameters ride along
+    as trailing inputs so that asking for their gradient raises."""
 
     @staticmethod
-    def forward(ctx, x, x2, addend, mlp):
-        ctx.mlp = mlp
+    def forward(ctx, x, x2, addend, mlp, *params):
+        ctx.mlp, ctx.nparams = mlp, len(params)
         ctx.save_for_backward(x, x2)
         return mlp.native_forward(x, x2=x2, addend=addend)
 
     @staticmethod
     def backward(ctx, dy):
+        from .sfnonet import refuse_param_grads
+        refuse_param_grads(ctx, 4, "MLP.backward")
         x, x2 = ctx.saved_tensors
         if ctx.needs_input_grad[1] or ctx.needs_input_grad[2]:
             raise NotImplementedError("MLP backward: gradients only to the first input")
-        dx = ctx.mlp.native_backward_input(x, dy, x2=x2)
-        return dx.to(x.dtype), None, None, None
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = ctx.mlp.native_backward_input(x, dy, x2=x2).to(x.dtype)
+        return (dx, None, None, None) + (None,) * ctx.nparams
 
 
 def _check_transforms(fwd, inv):

@@ -212,9 +212,16 @@ class FourierNeuralOperatorBlock(WeightCache, nn.Module):
         del keep
         return out.to(dtype)
 
+    def trainable(self):
+        """The parameters that require grad (passed to autograd so a backward into them
+        raises instead of leaving .grad None)."""
+        return tuple(p for p in self.parameters() if p.requires_grad)
+
     def forward(self, x, *overflow):
-        if torch.is_grad_enabled() and x.requires_grad:
-            return _BlockFn.apply(x, self)
+        if torch.is_grad_enabled():
+            params = self.trainable()
+            if x.requires_grad or params:
+                return _BlockFn.apply(x, self, *params)
         return self._native_forward(x)
 
     def _adjoint_plans(self, device):
@@ -325,9 +332,10 @@ class FourierNeuralOperatorBlock_Filmed(FourierNeuralOperatorBlock):
     _filmed = True
 
     def forward(self, x, gamma, beta, scale=1):
-        if torch.is_grad_enabled() and (gamma.requires_grad or beta.requires_grad
-                                        or x.requires_grad):
-            return _FilmedBlockFn.apply(x, gamma, beta, float(scale), self)
+        if torch.is_grad_enabled():
+            params = self.trainable()
+            if gamma.requires_grad or beta.requires_grad or x.requires_grad or params:
+                return _FilmedBlockFn.apply(x, gamma, beta, float(scale), self, *params)
         return self._native_forward(x, gamma, beta, scale)
 
     @N.on_input_device
@@ -386,19 +394,35 @@ class FourierNeuralOperatorBlock_Filmed(FourierNeuralOperatorBlock):
         return dg, db
 
 
+def refuse_param_grads(ctx, first, what):
+    """Raise when autograd asks for a gradient of a module parameter (inputs ``first``
+    onwards of the Function).  The native backward gives dL/dx and dL/d(gamma, beta) only;
+    the reference's --retrain-film (main.py:958-960) makes the decoder and the last
+    film_layers blocks trainable (MSFNO/Models/sfno/model.py:922-923, 1016-1019), whose
+    weight gradients are not implemented natively.  Raising keeps them from being
+    silently left at None."""
+    if any(ctx.needs_input_grad[first:]):
+        raise NotImplementedError(
+            f"{what}: gradients of the module's own parameters are not implemented on the "
+            "MI355X path (dL/dx and FiLM dL/dgamma, dL/dbeta only); freeze them with "
+            "requires_grad_(False) (MSFNO trains the FiLM generator, model.py:1016-1023)")
+
+
 class _FilmedBlockFn(torch.autograd.Function):
-    """Native filmed-block forward; backward to (gamma, beta) with the SFNO weights
+    """Native filmed-block forward; backward to (x, gamma, beta) with the SFNO weights
     frozen (sfnonet.py:787-860 runs the filmed blocks with autograd and every
-    earlier block under no_grad)."""
+    earlier block under no_grad).  The block's trainable parameters ride along as
+    trailing inputs so that asking for their gradient raises (refuse_param_grads)."""
 
     @staticmethod
-    def forward(ctx, x, gamma, beta, scale, blk):
-        ctx.blk, ctx.scale = blk, scale
+    def forward(ctx, x, gamma, beta, scale, blk, *params):
+        ctx.blk, ctx.scale, ctx.nparams = blk, scale, len(params)
         ctx.save_for_backward(x, gamma, beta)
         return blk._native_forward(x, gamma, beta, scale)
 
     @staticmethod
     def backward(ctx, dout):
+        refuse_param_grads(ctx, 5, type(ctx.blk).__name__ + ".backward")
         x, gamma, beta = ctx.saved_tensors
         dx = None
         if ctx.needs_input_grad[0]:
@@ -407,24 +431,29 @@ class _FilmedBlockFn(torch.autograd.Function):
             dx = dx.to(x.dtype)
         else:
             dg, db = ctx.blk.native_film_backward(x, gamma, beta, ctx.scale, dout)
-        return dx, dg.reshape(gamma.shape).to(gamma.dtype), \
-            db.reshape(beta.shape).to(beta.dtype), None, None
+        return (dx, dg.reshape(gamma.shape).to(gamma.dtype),
+                db.reshape(beta.shape).to(beta.dtype), None, None) + (None,) * ctx.nparams
 
 
 class _BlockFn(torch.autograd.Function):
-    """Native unfilmed block forward with dL/dx (weights frozen; msfno_block_backward)."""
+    """Native unfilmed block forward with dL/dx (weights frozen; msfno_block_backward).
+    Trainable parameters ride along so that asking for their gradient raises."""
 
     @staticmethod
-    def forward(ctx, x, blk):
-        ctx.blk = blk
+    def forward(ctx, x, blk, *params):
+        ctx.blk, ctx.nparams = blk, len(params)
         ctx.save_for_backward(x)
         return blk._native_forward(x)
 
     @staticmethod
     def backward(ctx, dout):
+        refuse_param_grads(ctx, 2, type(ctx.blk).__name__ + ".backward")
         (x,) = ctx.saved_tensors
-        dx, _, _ = ctx.blk.native_backward(x, dout)
-        return dx.to(x.dtype), None
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx, _, _ = ctx.blk.native_backward(x, dout)
+            dx = dx.to(x.dtype)
+        return (dx, None) + (None,) * ctx.nparams
 
 
 def _trunc_normal_init(m):
@@ -575,9 +604,11 @@ class FourierNeuralOperatorNet(nn.Module):
         """decoder(cat(x, residual)) (sfnonet.py:679-686) without materialising the concat;
         with autograd (FiLM fine-tuning) the gradient reaches x through the frozen decoder."""
         x2 = residual if self.big_skip else None
-        if torch.is_grad_enabled() and x.requires_grad:
-            from .layers import _MLPFn
-            return _MLPFn.apply(x, x2, None, self.decoder)
+        if torch.is_grad_enabled():
+            params = tuple(p for p in self.decoder.parameters() if p.requires_grad)
+            if x.requires_grad or (x2 is not None and x2.requires_grad) or params:
+                from .layers import _MLPFn
+                return _MLPFn.apply(x, x2, None, self.decoder, *params)
         return self.decoder.native_forward(x, x2=x2)
 
     def _fuse_last_affine(self, x):
@@ -647,7 +678,8 @@ class FourierNeuralOperatorNet_Filmed(FourierNeuralOperatorNet):
         if self.advanced_logging:
             self.gamma, self.beta = gamma, beta
         residual = x
-        x = self.pos_drop(self.encode(x))
+        with torch.no_grad():  # sfnonet.py:816-827: encoder and pos_embed without autograd
+            x = self.pos_drop(self.encode(x))
         fuse = self._fuse_last_affine(residual)
         nb = len(self.blocks)
         for i, blk in enumerate(self.blocks):
@@ -658,5 +690,9 @@ class FourierNeuralOperatorNet_Filmed(FourierNeuralOperatorNet):
             if fuse and i == nb - 1:
                 x1, aff = blk.native_forward_deferred(x, *film)
                 return self.decode_deferred(x1, aff, residual)
-            x = blk(x, *film)
+            if film:
+                x = blk(x, *film)
+            else:  # sfnonet.py:838-844: unfilmed blocks under no_grad
+                with torch.no_grad():
+                    x = blk(x)
         return self.decode(x, residual)

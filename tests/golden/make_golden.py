@@ -20,8 +20,8 @@ Every other line executed (SpectralFilterLayer, SpectralAttentionS2,
 SpectralConvS2, contractions, ComplexReLU, MLP, InstanceNorm, FiLM, block
 wiring, the ×1e5 rescale recipe) is the reference's own code.
 
-Usage:  python tests/golden/make_golden.py [--net | --gconv]   (only the network /
-        global_conv fixtures)
+Usage:  python tests/golden/make_golden.py [--net | --gconv | --large]   (only the
+        network / global_conv / large-size fixtures)
 """
 from __future__ import annotations
 
@@ -38,6 +38,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(os.path.dirname(HERE))
 REF = "/root/reference/MSFNO/Models"
 sys.path.insert(0, REPO)
+sys.path.insert(0, os.path.dirname(HERE))
 
 from oracle import sht_ref  # noqa: E402
 
@@ -253,12 +254,77 @@ def main_global_conv():
         print("wrote", path, tuple(y.shape), float(y.abs().max()))
 
 
+LARGE_CASES = [
+    # tag, nlat, nlon, lmax, mmax, C, grid, filter, filmed, rows kept, channels kept
+    # (SURVEY §8(c) "What pins results": mid-size LG C=64, the default network's inner
+    # block, config 2 full size)
+    ("lg121_c64_nl", 121, 240, 60, 61, 64, "legendre-gauss", "non-linear", True,
+     (0, 30, 60, 90, 120), tuple(range(64))),
+    ("lg121_c64_lin", 121, 240, 60, 61, 64, "legendre-gauss", "linear", True,
+     (0, 30, 60, 90, 120), tuple(range(64))),
+    ("inner120_c256_nl", 120, 240, 120, 121, 256, "legendre-gauss", "non-linear", False,
+     (0, 40, 80, 119), tuple(range(8))),
+    ("c2_721_c256_nl", 721, 1440, 360, 361, 256, "equiangular", "non-linear", True,
+     (0, 180, 360, 540, 720), tuple(range(8))),
+]
+
+
+def main_large(only=None):
+    """Reference blocks at the sizes that matter, built from a committed recipe
+    (golden_util.param_recipe / recipe_normal) and stored as output rows x channels
+    plus per-channel moments: middle-block wiring, B=1, scale 1."""
+    from golden_util import moments, param_recipe, recipe_normal
+    mods = load_reference()
+    sfnonet = mods["sfnonet"]
+    for (tag, nlat, nlon, lmax, mmax, C, grid, ft, filmed, rows, chans) in LARGE_CASES:
+        if only and only not in tag:
+            continue
+        torch.manual_seed(0)
+        blk, sht, isht = build_ref_block(sfnonet, nlat, nlon, lmax, mmax, C, ft, filmed, grid)
+        out = {"meta_kind": "large", "meta_nlat": nlat, "meta_nlon": nlon, "meta_lmax": lmax,
+               "meta_mmax": mmax, "meta_C": C, "meta_B": 1, "meta_grid": grid,
+               "meta_filter": ft, "meta_filmed": int(filmed), "meta_scale": 1.0,
+               "meta_wiring": "middle", "meta_x_seed": 9000 + C + nlat}
+        names = sorted(n for n, _ in blk.named_parameters())
+        with torch.no_grad():
+            for i, (n, p) in enumerate(sorted(blk.named_parameters())):
+                sigma, offset = param_recipe(n, tuple(p.shape), ft)
+                seed = 100 + i
+                p.copy_(recipe_normal(seed, p.shape, sigma, offset))
+                out["r__" + n] = np.array([seed, sigma, offset], dtype=np.float64)
+                out["s__" + n] = np.array(p.shape, dtype=np.int64)
+        blk.eval()
+        x = recipe_normal(out["meta_x_seed"], (1, C, nlat, nlon))
+        gen = torch.Generator().manual_seed(77)
+        gamma = 0.1 * torch.randn(1, C, generator=gen)
+        beta = 0.1 * torch.randn(1, C, generator=gen)
+        with torch.no_grad():
+            y = blk(x, gamma, beta, 1.0) if filmed else blk(x)
+        mean, std, mx = moments(y)
+        r = torch.tensor(rows)
+        c = torch.tensor(chans)
+        out.update({"x_probe": x.reshape(-1)[:4096].numpy(), "gamma": gamma.numpy(),
+                    "beta": beta.numpy(), "rows": r.numpy(), "chans": c.numpy(),
+                    "rows_y": y[0][c][:, r].numpy(), "mom_mean": mean.numpy(),
+                    "mom_std": std.numpy(), "mom_maxabs": mx.numpy(),
+                    "state_dict_keys": np.array(sorted(blk.state_dict().keys()))})
+        assert set(names) == {k[3:] for k in out if k.startswith("r__")}
+        path = os.path.join(HERE, "large", tag + ".npz")
+        os.makedirs(os.path.dirname(path), exist_ok=True)
+        np.savez_compressed(path, **out)
+        print("wrote", path, tuple(y.shape), "max|y|", float(y.abs().max()),
+              "std", float(y.std()))
+
+
 if __name__ == "__main__":
     if "--net" in sys.argv:
         main_net()
     elif "--gconv" in sys.argv:
         main_global_conv()
+    elif "--large" in sys.argv:
+        main_large(sys.argv[sys.argv.index("--large") + 1] if len(sys.argv) > 2 else None)
     else:
         main()
         main_net()
         main_global_conv()
+        main_large()

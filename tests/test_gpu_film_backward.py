@@ -42,7 +42,7 @@ def _oracle_transforms(meta):
 def test_block_film_grads_match_oracle_autograd(path):
     meta, params, arrays, _ = load(path)
     blk, _, _ = make_block(meta, params)
-    blk = blk.to(DEV)
+    blk = blk.to(DEV).requires_grad_(False)  # SFNO frozen (model.py:1016-1023)
     x, scale = arrays["x"], float(meta["scale"])
     g = torch.Generator().manual_seed(11)
     gamma0, beta0 = arrays["gamma"], arrays["beta"]
@@ -75,7 +75,7 @@ def test_filmed_net_film_grads_match_oracle_autograd(path):
     of the last block through the frozen decoder over cat(x, residual)."""
     from test_gpu_net import _build
     meta, params, x, _, _ = load_net(path)
-    net = _build(meta, params, filmed=True, film_layers=1)
+    net = _build(meta, params, filmed=True, film_layers=1).requires_grad_(False)
     B, C = x.shape[0], meta["C"]
     g = torch.Generator().manual_seed(5)
     film0 = 0.1 * torch.randn(B, 2, 1, C, generator=g)
@@ -104,7 +104,7 @@ def test_block_input_grad_matches_oracle_autograd(path):
     against fp64 autograd through the oracle.  Tolerance: max-abs < 1e-4 x max|grad|."""
     meta, params, arrays, _ = load(path)
     blk, _, _ = make_block(meta, params)
-    blk = blk.to(DEV)
+    blk = blk.to(DEV).requires_grad_(False)  # SFNO frozen (model.py:1016-1023)
     scale = float(meta["scale"])
     filmed = bool(meta["filmed"])
     g = torch.Generator().manual_seed(13)
@@ -199,7 +199,7 @@ def test_filmed_net_multi_layer_film_grads(path, film_layers):
                                           model_depth=None, **kw)
     missing, unexpected = net.load_state_dict(params, strict=False)
     assert not unexpected and all(m.endswith((".weights", ".pct")) for m in missing)
-    net = net.eval().to(DEV)
+    net = net.eval().to(DEV).requires_grad_(False)  # model.py:1016-1023
     B, C = x.shape[0], meta["C"]
     cfg = net_cfg(meta)
     pd = {kk: (v.double() if v.is_floating_point() else v) for kk, v in params.items()}
@@ -220,3 +220,37 @@ def test_filmed_net_multi_layer_film_grads(path, film_layers):
     assert err < 1e-4 * want.abs().max().item()
     # every filmed block's modulation gets a gradient
     assert (want.abs().amax(dim=(0, 1, 3)) > 0).all()
+
+
+@pytest.mark.parametrize("which", ["filter_layer", "norm0", "decoder"])
+def test_trainable_sfno_weights_raise_not_none(which):
+    """--retrain-film makes the decoder and the last blocks trainable
+    (MSFNO/Models/sfno/model.py:922-923, 1016-1019).  The native backward has no
+    weight gradients: asking for one raises instead of leaving .grad None."""
+    from test_gpu_net import _build
+    meta, params, x, _, _ = load_net(NET_FIXTURES[0])
+    net = _build(meta, params, filmed=True, film_layers=1).requires_grad_(False)
+    owner = net.decoder if which == "decoder" else net.blocks[-1]
+    name, p = next((n, q) for n, q in owner.named_parameters()
+                   if which == "decoder" or n.startswith(which))
+    p.requires_grad_(True)
+    film = (0.1 * torch.randn(x.shape[0], 2, 1, meta["C"])).to(DEV).requires_grad_()
+    y = net(x.to(DEV), film, 1.0)
+    with pytest.raises(NotImplementedError, match="parameters are not implemented"):
+        y.sum().backward()
+    assert p.grad is None, name
+
+
+def test_block_trainable_weight_raises_without_input_grad():
+    """A block whose input needs no gradient but whose fc1 weight does still builds
+    an autograd node, and backward raises (no silent None)."""
+    path = [p for p in FILM_CASES if "_nl_" in os.path.basename(p)][0]
+    meta, params, arrays, _ = load(path)
+    blk, _, _ = make_block(meta, params)
+    blk = blk.to(DEV).requires_grad_(False)
+    blk.mlp.fwd[0].weight.requires_grad_(True)
+    y = blk(arrays["x"].to(DEV), arrays["gamma"].to(DEV), arrays["beta"].to(DEV), 1.0)
+    assert y.requires_grad
+    with pytest.raises(NotImplementedError):
+        y.sum().backward()
+    assert blk.mlp.fwd[0].weight.grad is None

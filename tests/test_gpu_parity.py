@@ -281,3 +281,30 @@ def test_global_conv_matches_reference_golden(ft):
         err = (got - want).abs().max().item()
         assert got.shape == want.shape
         assert err < 1e-4, f"max-abs {err:.3e}"
+
+
+@pytest.mark.parametrize("env", ["MSFNO_SKIP_X3H=0", "MSFNO_ENGINE=x6", "MSFNO_SKIP_PLANES=1"])
+@pytest.mark.parametrize("ft", ["nl", "lin"])
+def test_global_conv_skip_engines(ft, env):
+    """global_conv's inner skip multiplies the residual on every skip engine (the x3h
+    default, the x6 fp32 split, the x6 planes path and the dense fallback), not the filter
+    input x.  The engines are chosen once per process from the environment, so each
+    runs in a child process (this file as a script)."""
+    import subprocess
+    import sys
+    from conftest import PKG_DIR, REPO
+    k, v = env.split("=")
+    r = subprocess.run([sys.executable, os.path.abspath(__file__), "gconv", ft],
+                       env=dict(os.environ, PYTHONPATH=os.pathsep.join([REPO, PKG_DIR]), **{k: v}),
+                       cwd=os.path.dirname(__file__),
+                       capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    print(r.stdout.strip())
+
+
+if __name__ == "__main__":
+    import sys
+    if sys.argv[1] == "gconv":
+        test_global_conv_matches_reference_golden(sys.argv[2])
+        print(f"global_conv {sys.argv[2]} ok under "
+              f"{[k + '=' + v for k, v in os.environ.items() if k.startswith('MSFNO_')]}")

@@ -72,7 +72,7 @@ def test_band_net_step_graph_over_rccl(rccl):
     film = 0.1 * torch.randn(2, 2, 1, 16, device=DEV)
     with torch.no_grad():
         eager = shard(x, film, 1.0).clone()
-        torch.cuda.synchronize()
+        TorchComm().quiesce()  # the watchdog has reaped the eager step's works
         graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(graph):
             y = shard(x, film, 1.0)
