@@ -83,10 +83,11 @@ STAGE_KERNEL_F32 = {
 # x3h engine: the fused MLP, the inner skip (fp32 x, bias epilogue) and the spectral
 # MLP chain; the unfused fc1 / fc2 pair stays on x6
 STAGE_KERNEL_X3H = dict(STAGE_KERNEL_X6, **{
-    # inner skip at C = 256 on the fused-MLP tiling (MSFNO_SKIP_H=0: gemm_x3)
-    "inner_skip": "msfno::(anonymous namespace)::skip_h_kernel("
-                  "msfno::(anonymous namespace)::SkipHParams)",
-    "mlp_fused": "void msfno::(anonymous namespace)::mlp_fused_h_kernel<2>"
+    # inner skip at C = 256: the persistent pipelined skip (skip_h for P % 4 != 0,
+    # MSFNO_SKIP_H=0: gemm_x3)
+    "inner_skip": "msfno::(anonymous namespace)::skip_hp_kernel("
+                  "msfno::(anonymous namespace)::SkipHPParams)",
+    "mlp_fused": "void msfno::(anonymous namespace)::mlp_fused_h_kernel<2, false>"
                  "(msfno::(anonymous namespace)::MlpHParams)",
     "legendre_fwd": "void msfno::(anonymous namespace)::legendre_x3f_kernel<3>("
                     "msfno::(anonymous namespace)::X3FParams)",

@@ -265,6 +265,15 @@ int msfno_block_backward(const msfno_block_desc* d, msfno_sht_plan_t fwd, msfno_
                          const float* gamma, const float* beta, float film_scale,
                          const float* dout, float* dx, float* dgamma, float* dbeta, int B,
                          void* ws, size_t ws_bytes, void* stream);
+/* Introspection of msfno_block_backward's workspace: the byte offsets of the recomputed
+ * non-linear filter's hidden activations h_l = ComplexReLU(...) (B, spec_hidden, lmax,
+ * mmax) complex, l < spectral_layers, whose ReLU(real) masks the backward applies.  Writes
+ * at most n offsets and the number of hidden layers (0 for the linear filter) to *nlayers.
+ * Lets a test compare the masks the GPU actually used with an oracle's. */
+int msfno_block_backward_hidden_offsets(const msfno_block_desc* d, msfno_sht_plan_t fwd,
+                                        msfno_sht_plan_t inv, msfno_sht_plan_t fwd_adj,
+                                        msfno_sht_plan_t inv_adj, int B, size_t* offsets, int n,
+                                        int* nlayers);
 
 /* Backward of the channel MLP (layers.py:145-178) to its first input, weights
  * frozen: the decoder over cat(x, residual) (sfnonet.py:679-686) when the loss

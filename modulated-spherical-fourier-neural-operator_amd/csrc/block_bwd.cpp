@@ -164,6 +164,26 @@ size_t msfno_block_backward_workspace_size(const msfno_block_desc* d, msfno_sht_
   return cv.off;
 }
 
+int msfno_block_backward_hidden_offsets(const msfno_block_desc* d, msfno_sht_plan_t f,
+                                        msfno_sht_plan_t g, msfno_sht_plan_t fa,
+                                        msfno_sht_plan_t ga, int B, size_t* offsets, int n,
+                                        int* nlayers) {
+  using namespace msfno;
+  MSFNO_TRY(check_adjoint(d, f, g, fa, ga));
+  MSFNO_REQUIRE(B > 0 && nlayers && (n == 0 || offsets), MSFNO_EINVAL,
+                "hidden offsets: bad arguments");
+  // carve against a non-null base so take() hands out addresses; subtract it again
+  static char anchor alignas(256)[256];
+  Carve cv;
+  cv.base = anchor;
+  BwdBufs r;
+  carve_bwd(cv, r, d, f, g, fa, ga, B);
+  const int L = d->filter_type == MSFNO_FILTER_LINEAR ? 0 : d->spectral_layers;
+  for (int l = 0; l < L && l < n; ++l) offsets[l] = (size_t)((char*)r.h[l] - anchor);
+  *nlayers = L;
+  return MSFNO_OK;
+}
+
 int msfno_block_backward(const msfno_block_desc* d, msfno_sht_plan_t f, msfno_sht_plan_t g,
                          msfno_sht_plan_t fa, msfno_sht_plan_t ga, const float* x,
                          const float* gamma, const float* beta, float film_scale,

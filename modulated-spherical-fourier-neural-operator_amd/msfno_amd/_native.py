@@ -114,6 +114,9 @@ SIGNATURES = [
                                                    _i]),
     ("msfno_block_backward", _i, [ctypes.POINTER(BlockDesc), _vp, _vp, _vp, _vp, _vp, _vp, _vp, _f,
                                   _vp, _vp, _vp, _vp, _i, _vp, _sz, _vp]),
+    ("msfno_block_backward_hidden_offsets", _i, [ctypes.POINTER(BlockDesc), _vp, _vp, _vp, _vp,
+                                                 _i, ctypes.POINTER(_sz), _i,
+                                                 ctypes.POINTER(_i)]),
     ("msfno_mlp_backward_input_workspace_size", _sz, [ctypes.POINTER(MlpDesc), _i,
                                                        ctypes.c_longlong]),
     ("msfno_mlp_backward_input", _i, [ctypes.POINTER(MlpDesc), _vp, _vp, _vp, _vp, _i,

@@ -258,10 +258,13 @@ class FourierNeuralOperatorBlock(WeightCache, nn.Module):
         return fa, ga
 
     @N.on_input_device
-    def native_backward(self, x, dout, gamma=None, beta=None, scale=1.0, need_dx=True):
+    def native_backward(self, x, dout, gamma=None, beta=None, scale=1.0, need_dx=True,
+                        hidden_tap=None):
         """(dL/dx, dL/dgamma, dL/dbeta) for dout = dL/d(out), the SFNO weights frozen
         (msfno_block_backward; the forward is recomputed).  dgamma / dbeta are None for an
-        unfilmed call; dx is None unless need_dx."""
+        unfilmed call; dx is None unless need_dx.  ``hidden_tap`` (tests) receives the
+        non-linear filter's recomputed hidden activations, (B, hidden, lmax, mmax) complex
+        per layer, whose ReLU(real) masks this backward applied."""
         x = N.require_device_f32(x, "block input")
         dout = N.require_device_f32(dout, "block output gradient")
         B, C, H, W = x.shape
@@ -288,6 +291,17 @@ class FourierNeuralOperatorBlock(WeightCache, nn.Module):
                                        N.ptr(dx), N.ptr(dg), N.ptr(db), B, ws.data_ptr(), nbytes,
                                        N.stream_of(x.device)),
                 type(self).__name__ + ".backward")
+        if hidden_tap is not None:
+            import ctypes
+            offs = (ctypes.c_size_t * 8)()
+            nl = ctypes.c_int(0)
+            N.check(L.msfno_block_backward_hidden_offsets(d, pf.handle, pi.handle, fa.handle,
+                                                          ga.handle, B, offs, 8, ctypes.byref(nl)),
+                    "hidden offsets")
+            n = B * d.spec_hidden * fwd.lmax * fwd.mmax * 2
+            hs = [ws[offs[l]:offs[l] + 4 * n].view(torch.float32)
+                  .view(B, d.spec_hidden, fwd.lmax, fwd.mmax, 2) for l in range(nl.value)]
+            hidden_tap([torch.view_as_complex(h.clone()) for h in hs])
         del keep
         return dx, dg, db
 
