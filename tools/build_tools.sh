@@ -9,4 +9,5 @@ mkdir -p tools/bin
   -L $LIB -lmsfno -Wl,-rpath,'$ORIGIN/../../'$LIB -o tools/bin/gemm_x6_bench
 /opt/rocm/bin/hipcc -O3 --offload-arch=gfx950 -std=c++17 -Wno-unused-result -I $CS tools/corun_probe.cpp \
   -L $LIB -lmsfno -Wl,-rpath,'$ORIGIN/../../'$LIB -o tools/bin/corun_probe
-/opt/rocm/bin/hipcc -O2 --offload-arch=gfx950 -std=c++17 tools/pk_opsel_sweep.cpp -o tools/bin/pk_opsel_sweep
+python3 tools/gen_pk_opsel_sweep.py tools/bin/pk_opsel_sweep.cpp
+/opt/rocm/bin/hipcc -O2 --offload-arch=gfx950 -std=c++17 tools/bin/pk_opsel_sweep.cpp -o tools/bin/pk_opsel_sweep
