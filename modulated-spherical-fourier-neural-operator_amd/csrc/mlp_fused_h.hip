@@ -42,7 +42,9 @@
 #include "gemm_common.h"
 #include "kernels.h"
 
+#include <cstdio>
 #include <string>
+#include <vector>
 #include <type_traits>
 
 namespace msfno {
@@ -79,6 +81,7 @@ struct MlpHParams {
   const float* b2;      // [C] or null
   int64_t P;
   int tiles_per_field;
+  uint64_t* trace;      // MSFNO_MH_TRACE: 5 words per workgroup, or null
 };
 
 // 2^(t - e) for v = f 2^e (f in [0.5, 1)): maps v below 2^t; 1 for v = 0 / non-finite
@@ -267,7 +270,7 @@ __device__ __forceinline__ void glds16s(uint64_t sbase, uint32_t voff, uint32_t 
 // residual, one store per output.
 constexpr int MH_LDS = MH_NS * MH_SLICE * 2 + (3 * MH_H + 2 * MH_C + 8) * 4;
 
-template <int AHEAD, bool EPI16>
+template <int AHEAD, bool TRACE>
 __device__ __forceinline__ void mlp_fused_h_tile(const MlpHParams& p, int lin, char* lds_raw) {
   constexpr int W = MH_WAVES, NS = MH_NS;
   constexpr int RING_BYTES = NS * MH_SLICE * 2;
@@ -283,6 +286,8 @@ __device__ __forceinline__ void mlp_fused_h_tile(const MlpHParams& p, int lin, c
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r16 = lane & 15, g = lane >> 4;
   const int z = lin / p.tiles_per_field;
+  uint64_t tr[3] = {0, 0, 0};
+  if constexpr (TRACE) tr[0] = __builtin_amdgcn_s_memrealtime();
   const int64_t P = p.P;
   const int64_t px = (int64_t)(lin - z * p.tiles_per_field) * TPX + 16 * wave + r16;
 
@@ -354,6 +359,7 @@ __device__ __forceinline__ void mlp_fused_h_tile(const MlpHParams& p, int lin, c
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
+  if constexpr (TRACE) tr[1] = __builtin_amdgcn_s_memrealtime();
 
   floatx4 hacc[2][2];  // [parity][tile]
 #pragma unroll
@@ -472,67 +478,6 @@ __device__ __forceinline__ void mlp_fused_h_tile(const MlpHParams& p, int lin, c
   }
 #pragma unroll
   for (int e2 = 0; e2 < 4; ++e2) conv_pair(MH_HB - 1, e2, I1{});
-  if constexpr (EPI16) {
-    // EPI16 (P % 4 == 0): the outputs leave through a per-wave LDS transpose (the ring is
-    // idle after the last step) as 16-B stores, a row's 16 pixels = 64 contiguous bytes,
-    // 16 stores per lane instead of 64; the residual comes in the same layout as 16 float4
-    // loads, issued under the last two steps' MFMAs
-    const int64_t px0 = px - r16;
-    const int c4 = 4 * (lane & 3);
-    const bool in4 = px0 + c4 < P;
-    floatx4 rv4[8][2];
-    if (p.resid && in4) {
-      const float* rs = p.resid + (int64_t)z * MH_C * P + px0 + c4;
-#pragma unroll
-      for (int c = 0; c < 8; ++c)
-#pragma unroll
-        for (int k = 0; k < 2; ++k)
-          rv4[c][k] = __builtin_nontemporal_load(
-              reinterpret_cast<const floatx4*>(rs + (int64_t)(32 * c + 16 * k + (lane >> 2)) * P));
-    } else {
-#pragma unroll
-      for (int c = 0; c < 8; ++c)
-#pragma unroll
-        for (int k = 0; k < 2; ++k) rv4[c][k] = floatx4{0.f, 0.f, 0.f, 0.f};
-    }
-    fc2_step(step_begin(MH_NSLICE - 2), MH_NSLICE - 2, I0{});
-    fc2_step(step_begin(MH_NSLICE - 1), MH_NSLICE - 1, I1{});
-    // every wave's last fragment reads are done before the ring becomes transpose patches
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    constexpr int ERS = 20;
-    float* const ep = reinterpret_cast<float*>(lds_raw) + wave * 32 * ERS;
-    float* const ob = p.out + (int64_t)z * MH_C * P + px0 + c4;
-#pragma unroll
-    for (int c = 0; c < 8; ++c) {
-#pragma unroll
-      for (int o2 = 0; o2 < 2; ++o2) {
-        const int r0 = 16 * (2 * c + o2) + 4 * g;
-        const float4 is = *reinterpret_cast<const float4*>(is2s + r0);
-        const float4 b = *reinterpret_cast<const float4*>(b2s + r0);
-        const floatx4 acc = oacc[2 * c + o2];
-        float* e0 = ep + (16 * o2 + 4 * g) * ERS + r16;
-        e0[0] = fmaf(acc[0], is.x, b.x);
-        e0[ERS] = fmaf(acc[1], is.y, b.y);
-        e0[2 * ERS] = fmaf(acc[2], is.z, b.z);
-        e0[3 * ERS] = fmaf(acc[3], is.w, b.w);
-      }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-#pragma unroll
-      for (int k = 0; k < 2; ++k) {
-        const int row = 16 * k + (lane >> 2);
-        const floatx4 v = *reinterpret_cast<const floatx4*>(ep + row * ERS + c4) + rv4[c][k];
-        if (in4)
-          __builtin_nontemporal_store(v, reinterpret_cast<floatx4*>(ob + (int64_t)(32 * c + row) * P));
-      }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    }
-    return;
-  }
   // the residual of every output row, all loads in flight at once and under the last
   // two steps' MFMAs (the x1 fragments are dead: their registers take it)
   float rv[16][4];
@@ -551,6 +496,21 @@ __device__ __forceinline__ void mlp_fused_h_tile(const MlpHParams& p, int lin, c
   }
   fc2_step(step_begin(MH_NSLICE - 2), MH_NSLICE - 2, I0{});
   fc2_step(step_begin(MH_NSLICE - 1), MH_NSLICE - 1, I1{});
+  if constexpr (TRACE) {
+    // diagnostic (MSFNO_MH_TRACE): per workgroup the CU it ran on and the real-time
+    // clock (100 MHz) at entry, after the prologue's loads, after the last MFMA step
+    // and once its stores are issued
+    tr[2] = __builtin_amdgcn_s_memrealtime();
+    const uint32_t hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);    // HW_REG_HW_ID
+    const uint32_t xcc = __builtin_amdgcn_s_getreg((31 << 11) | 20);  // HW_REG_XCC_ID
+    if (tid == 0) {
+      uint64_t* t = p.trace + 5 * (int64_t)blockIdx.x;
+      t[0] = ((uint64_t)xcc << 32) | hw;
+      t[1] = tr[0];
+      t[2] = tr[1];
+      t[3] = tr[2];
+    }
+  }
 
   // ---- epilogue: unscale + b2 + residual, store (rows 16 ot + 4 g + i) ----------------
   if (px >= P) return;
@@ -564,13 +524,16 @@ __device__ __forceinline__ void mlp_fused_h_tile(const MlpHParams& p, int lin, c
 #pragma unroll
     for (int i = 0; i < 4; ++i) o[(int64_t)(r0 + i) * P] = fmaf(oacc[ot][i], isv[i], bv[i]) + rv[ot][i];
   }
+  if constexpr (TRACE) {
+    if (tid == 0) p.trace[5 * (int64_t)blockIdx.x + 4] = __builtin_amdgcn_s_memrealtime();
+  }
 }
 
-// EPI16 (MSFNO_MH_EPI16=1, A/B): the transposed 16-B output stores of mlp_fused_h_tile
-template <int AHEAD, bool EPI16>
+// TRACE (MSFNO_MH_TRACE, diagnostic): per-workgroup CU id and phase timestamps
+template <int AHEAD, bool TRACE>
 __global__ __launch_bounds__(256, 2) void mlp_fused_h_kernel(MlpHParams p) {
   __shared__ __attribute__((aligned(16))) char lds_raw[MH_LDS];
-  mlp_fused_h_tile<AHEAD, EPI16>(p, xcd_remap(blockIdx.x, gridDim.x), lds_raw);
+  mlp_fused_h_tile<AHEAD, TRACE>(p, xcd_remap(blockIdx.x, gridDim.x), lds_raw);
 }
 
 // The fc1 half of mlp_fused_h_kernel with 256 output rows and no hidden layer:
@@ -1128,11 +1091,14 @@ int launch_skip_h(const float* W, const float* xs, const float* x, float* out, c
     const int64_t t = (int64_t)B * q.tiles_per_field;
     MSFNO_REQUIRE(t < (1LL << 31), MSFNO_EINVAL, "skip_hp: grid too large");
     q.tiles = (int)t;
-    // MSFNO_SKIP_GRID = workgroups per CU (default 2: each CU holds one 142-KB workgroup
-    // at a time, so the second half of the grid starts as the first retires, and the
-    // main stream's kernels get CUs in between; 1 and 0.5 measured 1 % slower in-block)
+    // MSFNO_SKIP_GRID = workgroups per CU.  A workgroup fills its CU (142 KB of LDS, the
+    // whole register file), so the grid size is the share of CUs the side stream takes
+    // from the main stream's SHT kernels while the skip runs.  Default 0.25 (64 of 256
+    // CUs, the skip spans 2.35 ms under the SHT): 166.9 / 165.4 / 166.1 fields/s against
+    // 163.6 / 164.3 / 162.8 for 2 per CU, 158.7 / 156.1 / 158.9 for 0.1875 and
+    // 164.4 / 162.6 / 163.9 for 0.3125, three interleaved rounds (profiles/r06_f)
     const char* ge = getenv("MSFNO_SKIP_GRID");
-    const double per_cu = ge ? atof(ge) : 2.0;
+    const double per_cu = ge ? atof(ge) : 0.25;
     const int64_t want = std::max<int64_t>(1, (int64_t)(per_cu * cus + 0.5));
     const int grid = (int)std::min<int64_t>(t, want);
     hipLaunchKernelGGL(skip_hp_kernel, dim3((unsigned)grid), dim3(64 * SP_W), 0, s, q);
@@ -1201,12 +1167,29 @@ int launch_mlp_fused_h(const float* x1, const float* scale, const float* shift,
   p.tiles_per_field = (int)cdiv(P, 16 * MH_WAVES);
   const int64_t tiles = (int64_t)B * p.tiles_per_field;
   MSFNO_REQUIRE(tiles < (1LL << 31), MSFNO_EINVAL, "mlp_fused_h: grid too large");
-  // MSFNO_MH_EPI16=1: transposed 16-B output stores (A/B)
-  const char* ee = getenv("MSFNO_MH_EPI16");
-  if (ee && ee[0] == '1' && P % 4 == 0)
+  // MSFNO_MH_TRACE=<file> (diagnostic): each launch's per-workgroup CU ids and phase
+  // timestamps are appended to <file> (synchronous; tools/mh_trace.py reads it)
+  const char* te = getenv("MSFNO_MH_TRACE");
+  if (te && te[0]) {
+    uint64_t* tb = nullptr;
+    MSFNO_CHECK_HIP(hipMalloc(&tb, (size_t)tiles * 5 * 8));
+    MSFNO_CHECK_HIP(hipMemsetAsync(tb, 0, (size_t)tiles * 5 * 8, s));
+    p.trace = tb;
     hipLaunchKernelGGL((mlp_fused_h_kernel<2, true>), dim3((unsigned)tiles), dim3(64 * MH_WAVES), 0, s, p);
-  else
-    hipLaunchKernelGGL((mlp_fused_h_kernel<2, false>), dim3((unsigned)tiles), dim3(64 * MH_WAVES), 0, s, p);
+    MSFNO_TRY(launch_check("mlp_fused_h"));
+    std::vector<uint64_t> h((size_t)tiles * 5);
+    MSFNO_CHECK_HIP(hipMemcpyAsync(h.data(), tb, h.size() * 8, hipMemcpyDeviceToHost, s));
+    MSFNO_CHECK_HIP(hipStreamSynchronize(s));
+    MSFNO_CHECK_HIP(hipFree(tb));
+    if (FILE* f = fopen(te, "ab")) {
+      const uint64_t n = (uint64_t)tiles;
+      fwrite(&n, 8, 1, f);
+      fwrite(h.data(), 8, h.size(), f);
+      fclose(f);
+    }
+    return MSFNO_OK;
+  }
+  hipLaunchKernelGGL((mlp_fused_h_kernel<2, false>), dim3((unsigned)tiles), dim3(64 * MH_WAVES), 0, s, p);
   return launch_check("mlp_fused_h");
 }
 
