@@ -1785,7 +1785,7 @@ static int block_forward_impl(const msfno_block_desc* d, msfno_sht_plan_t f, msf
     if (b.xs && sx != x) MSFNO_TRY(launch_chan_pow2_scale(sx, (int64_t)B * C, P, b.xs, ss));
     if (b.xs && C == 256 && skip_h_env()) {
       MSFNO_TRY(launch_skip_h(d->skip_w, b.xs, sx, x1, d->skip_b, B, P, b.dw.skip, b.dw.skip_b,
-                              ss));
+                              ss, side != nullptr));
     } else if (b.xs) {
       MSFNO_TRY(gemm_x3(d->skip_w, (int)C, b.xs, sx, x1, (int)C, (int)P, (int)C, (int)P, (int)P,
                         C * P, C * P, B, e, b.dw.skip, b.dw.skip_b, ss));

@@ -124,8 +124,11 @@ int launch_mlp_gen_h(const float* x, const float* xa, const float* xt, const flo
 // ws >= skip_h_workspace(B)
 bool skip_h_env();
 size_t skip_h_workspace(int B);
+// side_share: the persistent kernel's workgroups per CU when it runs on the block's side
+// stream beside the SHT (0: the default for a kernel that runs alone)
 int launch_skip_h(const float* W, const float* xs, const float* x, float* out, const float* bias,
-                  int B, int64_t P, void* ws, size_t ws_bytes, hipStream_t s);
+                  int B, int64_t P, void* ws, size_t ws_bytes, hipStream_t s,
+                  bool side = false);
 // xs[r] = the power of two 2^(14 - e) with max_p |x[r][p]| = f 2^e (rows of P values): the
 // x3h B-row scales of a 1x1 conv whose input carries no norm statistics
 int launch_chan_pow2_scale(const float* x, int64_t rows, int64_t P, float* xs, hipStream_t s);

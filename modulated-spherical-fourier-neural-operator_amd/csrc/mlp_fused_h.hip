@@ -1057,7 +1057,7 @@ bool skip_h_env() {
 
 
 int launch_skip_h(const float* W, const float* xs, const float* x, float* out, const float* bias,
-                  int B, int64_t P, void* ws, size_t ws_bytes, hipStream_t s) {
+                  int B, int64_t P, void* ws, size_t ws_bytes, hipStream_t s, bool side) {
   MSFNO_REQUIRE(W && xs && x && out && ws && B > 0 && P >= 1 && ws_bytes >= skip_h_workspace(B),
                 MSFNO_EINVAL, "skip_h: bad arguments");
   unsigned short* img = static_cast<unsigned short*>(ws);
@@ -1091,14 +1091,16 @@ int launch_skip_h(const float* W, const float* xs, const float* x, float* out, c
     const int64_t t = (int64_t)B * q.tiles_per_field;
     MSFNO_REQUIRE(t < (1LL << 31), MSFNO_EINVAL, "skip_hp: grid too large");
     q.tiles = (int)t;
-    // MSFNO_SKIP_GRID = workgroups per CU.  A workgroup fills its CU (142 KB of LDS, the
-    // whole register file), so the grid size is the share of CUs the side stream takes
-    // from the main stream's SHT kernels while the skip runs.  Default 0.25 (64 of 256
-    // CUs, the skip spans 2.35 ms under the SHT): 166.9 / 165.4 / 166.1 fields/s against
-    // 163.6 / 164.3 / 162.8 for 2 per CU, 158.7 / 156.1 / 158.9 for 0.1875 and
-    // 164.4 / 162.6 / 163.9 for 0.3125, three interleaved rounds (profiles/r06_f)
+    // Workgroups per CU.  A workgroup fills its CU (142 KB of LDS, the whole register
+    // file).  Alone (inline, or in a graph): 2 per CU, the second half of the grid starting
+    // as the first retires.  On the block's side stream the grid size is the share of CUs
+    // taken from the main stream's SHT kernels while the skip runs: 0.25 (64 of 256 CUs;
+    // the skip then spans 2.35 ms under the SHT) measured 166.9 / 165.4 / 166.1 fields/s
+    // against 163.6 / 164.3 / 162.8 for 2 per CU, 158.7 / 156.1 / 158.9 for 0.1875 and
+    // 164.4 / 162.6 / 163.9 for 0.3125, three interleaved rounds (profiles/r06_f).
+    // MSFNO_SKIP_GRID overrides both.
     const char* ge = getenv("MSFNO_SKIP_GRID");
-    const double per_cu = ge ? atof(ge) : 0.25;
+    const double per_cu = ge ? atof(ge) : (side ? 0.25 : 2.0);
     const int64_t want = std::max<int64_t>(1, (int64_t)(per_cu * cus + 0.5));
     const int grid = (int)std::min<int64_t>(t, want);
     hipLaunchKernelGGL(skip_hp_kernel, dim3((unsigned)grid), dim3(64 * SP_W), 0, s, q);
