@@ -265,6 +265,40 @@ int msfno_block_backward(const msfno_block_desc* d, msfno_sht_plan_t fwd, msfno_
                          const float* gamma, const float* beta, float film_scale,
                          const float* dout, float* dx, float* dgamma, float* dbeta, int B,
                          void* ws, size_t ws_bytes, void* stream);
+/* Parameter gradients of the block (the reference's --retrain-film, main.py:958-960: the
+ * decoder and the last film_layers blocks train, MSFNO/Models/sfno/model.py:922-923,
+ * 1016-1019).  Device fp32 outputs, each laid out as the parameter it is the gradient of;
+ * NULL = not wanted.  Written (not accumulated). */
+typedef struct msfno_block_param_grads {
+  float* norm0_w;      /* (C)                     norm0.weight */
+  float* norm0_b;      /* (C)                     norm0.bias */
+  float* spec_w[8];    /* (Ci, Co, 2)             filter_layer.filter.w.l (non-linear) */
+  float* spec_wout;    /* (spec_hidden, C, 2)     filter_layer.filter.wout */
+  float* lin_w;        /* (C, C, T, 2)            filter_layer.filter.w (linear) */
+  float* skip_w;       /* (C, C)                  inner_skip.weight */
+  float* skip_b;       /* (C)                     inner_skip.bias */
+  float* norm1_w;      /* (C)                     norm1.weight */
+  float* norm1_b;      /* (C)                     norm1.bias */
+  float* fc1_w;        /* (mlp_hidden, C)         mlp.fwd.0.weight */
+  float* fc1_b;        /* (mlp_hidden)            mlp.fwd.0.bias */
+  float* fc2_w;        /* (C, mlp_hidden)         mlp.fwd.2.weight */
+  float* fc2_b;        /* (C)                     mlp.fwd.2.bias */
+} msfno_block_param_grads;
+
+/* msfno_block_backward plus the parameter gradients `pg` asks for (NULL pg: exactly
+ * msfno_block_backward).  Weight gradients reduce over pixels or spectral modes in fp32
+ * chunks combined in fp64. */
+size_t msfno_block_backward_params_workspace_size(const msfno_block_desc* d,
+                                                  msfno_sht_plan_t fwd, msfno_sht_plan_t inv,
+                                                  msfno_sht_plan_t fwd_adj,
+                                                  msfno_sht_plan_t inv_adj, int B);
+int msfno_block_backward_params(const msfno_block_desc* d, msfno_sht_plan_t fwd,
+                                msfno_sht_plan_t inv, msfno_sht_plan_t fwd_adj,
+                                msfno_sht_plan_t inv_adj, const float* x, const float* gamma,
+                                const float* beta, float film_scale, const float* dout, float* dx,
+                                float* dgamma, float* dbeta, const msfno_block_param_grads* pg,
+                                int B, void* ws, size_t ws_bytes, void* stream);
+
 /* Introspection of msfno_block_backward's workspace: the byte offsets of the recomputed
  * non-linear filter's hidden activations h_l = ComplexReLU(...) (B, spec_hidden, lmax,
  * mmax) complex, l < spectral_layers, whose ReLU(real) masks the backward applies.  Writes
@@ -280,6 +314,14 @@ int msfno_block_backward_hidden_offsets(const msfno_block_desc* d, msfno_sht_pla
  * gradient dy = dL/dy reaches it.
  *   dx = W1[:, :Cin]^T (GELU'(W1 [x ; x2] + b1) * (W2^T dy))
  * (dL/dx2 is not produced: x2 is the network input.) */
+/* The same backward with the parameter gradients (the decoder under --retrain-film):
+ *   dW1 = dpre [x ; x2]^T, db1 = sum dpre, dW2 = dy GELU(pre)^T, db2 = sum dy
+ * (summed over the batch and the P pixels).  dx and each gradient output may be NULL. */
+size_t msfno_mlp_backward_params_workspace_size(const msfno_mlp_desc* d, int B, long long P);
+int msfno_mlp_backward_params(const msfno_mlp_desc* d, const float* x, const float* x2,
+                              const float* dy, float* dx, float* dfc1_w, float* dfc1_b,
+                              float* dfc2_w, float* dfc2_b, int B, long long P, void* ws,
+                              size_t ws_bytes, void* stream);
 size_t msfno_mlp_backward_input_workspace_size(const msfno_mlp_desc* d, int B, long long P);
 int msfno_mlp_backward_input(const msfno_mlp_desc* d, const float* x, const float* x2,
                              const float* dy, float* dx, int B, long long P, void* ws,

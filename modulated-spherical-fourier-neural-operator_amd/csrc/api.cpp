@@ -1496,7 +1496,7 @@ using namespace msfno;
 extern "C" {
 
 const char* msfno_last_error(void) { return g_last_error.c_str(); }
-int msfno_abi_version(void) { return 5; }
+int msfno_abi_version(void) { return 6; }
 
 int msfno_quadrature(int nlat, int grid, double* nodes, double* weights) {
   std::vector<double> x, w;
@@ -2200,18 +2200,38 @@ size_t msfno_mlp_backward_input_workspace_size(const msfno_mlp_desc* d, int B, l
   return cv.off;
 }
 
+size_t msfno_mlp_backward_params_workspace_size(const msfno_mlp_desc* d, int B, long long P) {
+  using namespace msfno;
+  const size_t base = msfno_mlp_backward_input_workspace_size(d, B, P);
+  if (!base) return 0;
+  const int wide = std::max({d->Cin, d->Cin2, d->Hid, d->Cout});
+  return round_up((int64_t)base, 256) + round_up((int64_t)wgrad_nt_workspace(wide, wide, P, B), 256) +
+         norm_param_grad_workspace(B, wide);
+}
+
 int msfno_mlp_backward_input(const msfno_mlp_desc* d, const float* x, const float* x2,
                              const float* dy, float* dx, int B, long long P, void* ws,
                              size_t ws_bytes, void* stream) {
-  MSFNO_REQUIRE(d && x && dy && dx && d->fc1_w && d->fc2_w && d->fc1_b, MSFNO_EINVAL,
+  MSFNO_REQUIRE(dx, MSFNO_EINVAL, "mlp backward: missing tensors");
+  return msfno_mlp_backward_params(d, x, x2, dy, dx, nullptr, nullptr, nullptr, nullptr, B, P, ws,
+                                   ws_bytes, stream);
+}
+
+int msfno_mlp_backward_params(const msfno_mlp_desc* d, const float* x, const float* x2,
+                              const float* dy, float* dx, float* dfc1_w, float* dfc1_b,
+                              float* dfc2_w, float* dfc2_b, int B, long long P, void* ws,
+                              size_t ws_bytes, void* stream) {
+  const bool params = dfc1_w || dfc1_b || dfc2_w || dfc2_b;
+  MSFNO_REQUIRE(d && x && dy && d->fc1_w && d->fc2_w && d->fc1_b, MSFNO_EINVAL,
                 "mlp backward: missing tensors");
   MSFNO_REQUIRE(d->Cin > 0 && d->Hid > 0 && d->Cout > 0 && d->Cin2 >= 0 && B > 0 && P > 0 &&
                     P <= 0x7fffffff,
                 MSFNO_EINVAL, "mlp backward: bad sizes");
   MSFNO_REQUIRE((d->Cin2 > 0) == (x2 != nullptr), MSFNO_EINVAL,
                 "mlp backward: x2 must be given exactly when Cin2 > 0");
-  MSFNO_REQUIRE(ws_bytes >= msfno_mlp_backward_input_workspace_size(d, B, P), MSFNO_EWORKSPACE,
-                "workspace too small");
+  MSFNO_REQUIRE(ws_bytes >= (params ? msfno_mlp_backward_params_workspace_size(d, B, P)
+                                     : msfno_mlp_backward_input_workspace_size(d, B, P)),
+                MSFNO_EWORKSPACE, "workspace too small");
   hipStream_t s = (hipStream_t)stream;
   Carve cv;
   cv.base = (char*)ws;
@@ -2251,7 +2271,36 @@ int msfno_mlp_backward_input(const msfno_mlp_desc* d, const float* x, const floa
   float* dh = t;
   MSFNO_TRY(gemm_dense(ROLE_FC2, TILE_256x128, W2T, dy, dh, (int)Hd, Pi, d->Cout, d->Cout, Pi, Pi,
                        0, (int64_t)d->Cout * P, Hd * P, B, e0, w2, w2b, s));
-  MSFNO_TRY(launch_gelu_grad_mul(dh, pre, (int64_t)B * Hd * P, s));
+  if (params) {
+    // dW2 = dy GELU(pre)^T and db2 = sum dy, before dh overwrites pre's partner buffer
+    void* wg = cv.take<char>(wgrad_nt_workspace(std::max({d->Cin, d->Cin2, d->Hid, d->Cout}),
+                                                std::max({d->Cin, d->Cin2, d->Hid, d->Cout}), P, B));
+    const size_t wg_b = wgrad_nt_workspace(std::max({d->Cin, d->Cin2, d->Hid, d->Cout}),
+                                           std::max({d->Cin, d->Cin2, d->Hid, d->Cout}), P, B);
+    void* nr = cv.take<char>(norm_param_grad_workspace(B, std::max({d->Cin, d->Cin2, d->Hid, d->Cout})));
+    if (dfc2_w)
+      MSFNO_TRY(launch_wgrad_nt(dy, P, (int64_t)d->Cout * P, pre, P, Hd * P, d->Cout, (int)Hd, P, B,
+                                WGRAD_GELU, nullptr, nullptr, dfc2_w, Hd, 1, wg, wg_b, s));
+    if (dfc2_b)
+      MSFNO_TRY(launch_norm_param_grad(dy, nullptr, nullptr, nullptr, nullptr, 0.f, B, d->Cout, P,
+                                       nullptr, dfc2_b, nr, s));
+    MSFNO_TRY(launch_gelu_grad_mul(dh, pre, (int64_t)B * Hd * P, s));
+    // dW1 = dpre [x ; x2]^T (columns Cin.. from x2), db1 = sum dpre
+    if (dfc1_w) {
+      MSFNO_TRY(launch_wgrad_nt(dh, P, Hd * P, x, P, (int64_t)d->Cin * P, (int)Hd, d->Cin, P, B,
+                                WGRAD_PLAIN, nullptr, nullptr, dfc1_w, Ct, 1, wg, wg_b, s));
+      if (d->Cin2 > 0)
+        MSFNO_TRY(launch_wgrad_nt(dh, P, Hd * P, x2, P, (int64_t)d->Cin2 * P, (int)Hd, d->Cin2, P, B,
+                                  WGRAD_PLAIN, nullptr, nullptr, dfc1_w + d->Cin, Ct, 1, wg, wg_b,
+                                  s));
+    }
+    if (dfc1_b)
+      MSFNO_TRY(launch_norm_param_grad(dh, nullptr, nullptr, nullptr, nullptr, 0.f, B, (int)Hd, P,
+                                       nullptr, dfc1_b, nr, s));
+  } else {
+    MSFNO_TRY(launch_gelu_grad_mul(dh, pre, (int64_t)B * Hd * P, s));
+  }
+  if (!dx) return MSFNO_OK;
   MSFNO_TRY(launch_transpose_mat(d->fc1_w, (int)Hd, d->Cin, (int)Ct, W1T, s));
   return gemm_dense(ROLE_FC2, TILE_256x128, W1T, dh, dx, d->Cin, Pi, (int)Hd, (int)Hd, Pi, Pi, 0,
                     Hd * P, (int64_t)d->Cin * P, B, e0, w3, w3b, s);

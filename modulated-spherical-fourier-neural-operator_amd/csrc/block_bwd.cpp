@@ -49,6 +49,9 @@ struct BwdBufs {
   float *a_t, *y_t;  // linear filter: tril-gathered spectra
   void *sws, *skws, *skws2;
   size_t sws_b, skws_b;
+  // parameter gradients (msfno_block_backward_params)
+  void *wg, *nrows;
+  size_t wg_b;
 };
 
 int64_t tril_count(int lmax, int mmax) {
@@ -58,7 +61,8 @@ int64_t tril_count(int lmax, int mmax) {
 }
 
 void carve_bwd(Carve& cv, BwdBufs& r, const msfno_block_desc* d, msfno_sht_plan_t f,
-               msfno_sht_plan_t g, msfno_sht_plan_t fa, msfno_sht_plan_t ga, int B) {
+               msfno_sht_plan_t g, msfno_sht_plan_t fa, msfno_sht_plan_t ga, int B,
+               bool params = false) {
   const int64_t C = d->C, BC = (int64_t)B * C;
   const int64_t Pi = (int64_t)f->nlat * f->nlon, Po = (int64_t)g->nlat * g->nlon;
   const int64_t XY = (int64_t)f->lmax * f->mmax;
@@ -124,6 +128,17 @@ void carve_bwd(Carve& cv, BwdBufs& r, const msfno_block_desc* d, msfno_sht_plan_
   r.skws_b = gemm_dense_workspace((int)C, (int)C, 1);
   r.skws = r.skws_b ? cv.take<char>(r.skws_b) : nullptr;
   r.skws2 = r.skws_b ? cv.take<char>(r.skws_b) : nullptr;
+  r.wg = r.nrows = nullptr;
+  r.wg_b = 0;
+  if (params) {
+    // the largest weight-gradient GEMM: 1x1 convs over the output grid's pixels, the
+    // spectral layers over 2 lmax mmax real columns
+    const int64_t hd = d->has_mlp ? d->mlp_hidden : 0, wide = std::max<int64_t>({C, Hs, hd});
+    r.wg_b = std::max(wgrad_nt_workspace((int)wide, (int)wide, Po, B),
+                      wgrad_nt_workspace((int)wide, (int)wide, 2 * XY, B));
+    r.wg = cv.take<char>(r.wg_b);
+    r.nrows = cv.take<char>(norm_param_grad_workspace(B, (int)wide));
+  }
 }
 
 int check_adjoint(const msfno_block_desc* d, msfno_sht_plan_t f, msfno_sht_plan_t g,
@@ -184,18 +199,40 @@ int msfno_block_backward_hidden_offsets(const msfno_block_desc* d, msfno_sht_pla
   return MSFNO_OK;
 }
 
+size_t msfno_block_backward_params_workspace_size(const msfno_block_desc* d, msfno_sht_plan_t f,
+                                                  msfno_sht_plan_t g, msfno_sht_plan_t fa,
+                                                  msfno_sht_plan_t ga, int B) {
+  using namespace msfno;
+  if (B <= 0 || check_adjoint(d, f, g, fa, ga) != MSFNO_OK) return 0;
+  Carve cv;
+  BwdBufs r;
+  carve_bwd(cv, r, d, f, g, fa, ga, B, true);
+  return cv.off;
+}
+
 int msfno_block_backward(const msfno_block_desc* d, msfno_sht_plan_t f, msfno_sht_plan_t g,
                          msfno_sht_plan_t fa, msfno_sht_plan_t ga, const float* x,
                          const float* gamma, const float* beta, float film_scale,
                          const float* dout, float* dx, float* dgamma, float* dbeta, int B,
                          void* ws, size_t ws_bytes, void* stream) {
+  return msfno_block_backward_params(d, f, g, fa, ga, x, gamma, beta, film_scale, dout, dx,
+                                     dgamma, dbeta, nullptr, B, ws, ws_bytes, stream);
+}
+
+int msfno_block_backward_params(const msfno_block_desc* d, msfno_sht_plan_t f,
+                                msfno_sht_plan_t g, msfno_sht_plan_t fa, msfno_sht_plan_t ga,
+                                const float* x, const float* gamma, const float* beta,
+                                float film_scale, const float* dout, float* dx, float* dgamma,
+                                float* dbeta, const msfno_block_param_grads* pg, int B, void* ws,
+                                size_t ws_bytes, void* stream) {
   using namespace msfno;
   MSFNO_TRY(check_adjoint(d, f, g, fa, ga));
   MSFNO_REQUIRE(x && dout && B > 0, MSFNO_EINVAL, "block backward: missing tensors");
   MSFNO_REQUIRE((gamma == nullptr) == (beta == nullptr) &&
                     (dgamma == nullptr) == (dbeta == nullptr) && (!dgamma || gamma),
                 MSFNO_EINVAL, "block backward: gamma / beta / dgamma / dbeta mismatch");
-  MSFNO_REQUIRE(ws_bytes >= msfno_block_backward_workspace_size(d, f, g, fa, ga, B),
+  MSFNO_REQUIRE(ws_bytes >= (pg ? msfno_block_backward_params_workspace_size(d, f, g, fa, ga, B)
+                                 : msfno_block_backward_workspace_size(d, f, g, fa, ga, B)),
                 MSFNO_EWORKSPACE, "workspace too small");
   const bool resample = f->nlat != g->nlat || f->nlon != g->nlon;
   MSFNO_REQUIRE(!resample || (d->inner_skip == MSFNO_SKIP_NONE && d->outer_skip == MSFNO_SKIP_NONE),
@@ -204,7 +241,7 @@ int msfno_block_backward(const msfno_block_desc* d, msfno_sht_plan_t f, msfno_sh
   Carve cv;
   cv.base = (char*)ws;
   BwdBufs r;
-  carve_bwd(cv, r, d, f, g, fa, ga, B);
+  carve_bwd(cv, r, d, f, g, fa, ga, B, pg != nullptr);
   const int C = d->C;
   const int64_t BC = (int64_t)B * C;
   const int64_t Pi = (int64_t)f->nlat * f->nlon, Po = (int64_t)g->nlat * g->nlon;
@@ -290,22 +327,61 @@ int msfno_block_backward(const msfno_block_desc* d, msfno_sht_plan_t f, msfno_sh
     MSFNO_TRY(gemm_dense(ROLE_FC2, TILE_256x128, r.W1T, r.dh, r.du, C, Pi2, Hd, Hd, Pi2, Pi2, 0,
                          (int64_t)Hd * Po, (int64_t)C * Po, B, e0, r.wsc, r.wsc_b, s));
     du = r.du;
+    if (pg) {
+      // fc2: dW2 = dout GELU(pre)^T, db2 = sum dout;  fc1: dW1 = dpre u^T with the MLP input
+      // u = sc1 x1 + sh1 (norm1 + FiLM), db1 = sum dpre   (layers.py:161-168)
+      if (pg->fc2_w)
+        MSFNO_TRY(launch_wgrad_nt(dout, Po, (int64_t)C * Po, r.pre, Po, (int64_t)Hd * Po, C, Hd, Po,
+                                  B, WGRAD_GELU, nullptr, nullptr, pg->fc2_w, Hd, 1, r.wg, r.wg_b,
+                                  s));
+      if (pg->fc2_b)
+        MSFNO_TRY(launch_norm_param_grad(dout, nullptr, nullptr, nullptr, nullptr, 0.f, B, C, Po,
+                                         nullptr, pg->fc2_b, r.nrows, s));
+      if (pg->fc1_w)
+        MSFNO_TRY(launch_wgrad_nt(r.dh, Po, (int64_t)Hd * Po, r.x1, Po, (int64_t)C * Po, Hd, C, Po,
+                                  B, WGRAD_AFFINE, r.sc1, r.sh1, pg->fc1_w, C, 1, r.wg, r.wg_b,
+                                  s));
+      if (pg->fc1_b)
+        MSFNO_TRY(launch_norm_param_grad(r.dh, nullptr, nullptr, nullptr, nullptr, 0.f, B, Hd, Po,
+                                         nullptr, pg->fc1_b, r.nrows, s));
+    }
   }
+  // norm1 affine: dw1 = sum_b (1 + gamma s) sum_p du xhat1, db1 = sum_b (1 + gamma s) sum_p du
+  if (pg && (pg->norm1_w || pg->norm1_b))
+    MSFNO_TRY(launch_norm_param_grad(du, r.x1, r.mean1, r.rstd1, gamma, film_scale, B, C, Po,
+                                     pg->norm1_w, pg->norm1_b, r.nrows, s));
   // ---- FiLM: dgamma = s sum du xhat1, dbeta = s sum du -------------------------------
   if (dgamma) MSFNO_TRY(launch_film_grad_reduce(du, r.x1, r.an1, r.tn1, film_scale, (int)BC, Po,
                                                 dgamma, dbeta, s));
-  if (!dx) return MSFNO_OK;
+  bool spec_params = false;
+  if (pg) {
+    spec_params = pg->norm0_w || pg->norm0_b || pg->spec_wout || pg->lin_w || pg->skip_w ||
+                  pg->skip_b;
+    for (int l = 0; l < 8; ++l) spec_params = spec_params || pg->spec_w[l];
+  }
+  if (!dx && !spec_params) return MSFNO_OK;
 
   // ---- norm1 (and FiLM) backward: dx1 ------------------------------------------------
   MSFNO_TRY(launch_inorm_backward(r.x1, r.mean1, r.rstd1, d->norm1_w, gamma, film_scale, du,
                                   nullptr, nullptr, r.dx1, BC, C, Po, s));
   if (lin) MSFNO_TRY(launch_gelu_grad_mul(r.dx1, r.x1pre, BC * Po, s));
+  // inner skip: x1pre = F + Ws x + bs -> dWs = dx1pre x^T, dbs = sum dx1pre (sfnonet.py:366-371)
+  if (pg && d->inner_skip == MSFNO_SKIP_LINEAR) {
+    if (pg->skip_w)
+      MSFNO_TRY(launch_wgrad_nt(r.dx1, Po, (int64_t)C * Po, x, Pi, (int64_t)C * Pi, C, C, Po, B,
+                                WGRAD_PLAIN, nullptr, nullptr, pg->skip_w, C, 1, r.wg, r.wg_b, s));
+    if (pg->skip_b)
+      MSFNO_TRY(launch_norm_param_grad(r.dx1, nullptr, nullptr, nullptr, nullptr, 0.f, B, C, Po,
+                                       nullptr, pg->skip_b, r.nrows, s));
+  }
   // ---- ISHT^T, filter^T, SHT^T --------------------------------------------------------
   MSFNO_TRY(msfno_sht_forward(fa, r.dx1, r.dZ, (int)BC, r.sws, r.sws_b, s));
   if (lin) {
     const int64_t T = tril_count(lmax, mmax);
     MSFNO_TRY(launch_conj_swap01(d->lin_w, C, C, T, r.wadj, s));  // (Co, Ci, T) -> (Ci, Co, T)
     MSFNO_TRY(launch_tril_map(r.dZ, r.y_t, BC, lmax, mmax, T, true, s));
+    // dw[k][i][t] = sum_b dy[b][k][t] conj(a[b][i][t]) (before a_t is reused below)
+    if (pg && pg->lin_w) MSFNO_TRY(launch_lin_wgrad(r.y_t, r.a_t, pg->lin_w, B, C, C, T, s));
     MSFNO_TRY(launch_compl_contract(r.y_t, r.wadj, r.a_t, B, C, C, T, s));
     MSFNO_TRY(launch_tril_map(r.a_t, r.dA, BC, lmax, mmax, T, false, s));
   } else {
@@ -320,6 +396,17 @@ int msfno_block_backward(const msfno_block_desc* d, msfno_sht_plan_t f, msfno_sh
     for (int l = L; l >= 0; --l) {
       // dh_l = dh_{l+1} w_l^H, then the mask of the forward's activation h_{l-1}
       const int ci = l == 0 ? C : Hs, co = l == L ? C : Hs;
+      // dW_l[i][o] = sum_n conj(in_l[i][n]) g_l[o][n]: real part on (re, im) rows, imaginary
+      // part against the pair-swapped gradient (layers.py:604-620, complex autograd)
+      float* dwl = pg ? (l == L ? pg->spec_wout : pg->spec_w[l]) : nullptr;
+      if (dwl) {
+        const float* in = l == 0 ? r.A : r.h[l - 1];
+        for (int part = 0; part < 2; ++part)
+          MSFNO_TRY(launch_wgrad_nt(in, 2 * XY, (int64_t)ci * 2 * XY, g_in, 2 * XY,
+                                    (int64_t)co * 2 * XY, ci, co, 2 * XY, B,
+                                    part ? WGRAD_CSWAP : WGRAD_PLAIN, nullptr, nullptr, dwl + part,
+                                    2 * co, 2, r.wg, r.wg_b, s));
+      }
       float* out = l == 0 ? r.dA : bufs[l & 1];
       MSFNO_TRY(launch_compl_mul2d(g_in, r.wadj + r.wadj_off[l], out, B, co, ci, XY, 0, s));
       if (l > 0) MSFNO_TRY(launch_relu_real_mask(out, r.h[l - 1], (int64_t)B * Hs * XY, s));
@@ -327,6 +414,11 @@ int msfno_block_backward(const msfno_block_desc* d, msfno_sht_plan_t f, msfno_sh
     }
   }
   MSFNO_TRY(msfno_sht_inverse(ga, r.dA, r.dxh0, (int)BC, r.sws, r.sws_b, s));
+  // norm0 affine: dw0 = sum dxhat0_out n0, db0 = sum dxhat0_out (sfnonet.py:363)
+  if (pg && (pg->norm0_w || pg->norm0_b))
+    MSFNO_TRY(launch_norm_param_grad(r.dxh0, x, r.mean0, r.rstd0, nullptr, 0.f, B, C, Pi,
+                                     pg->norm0_w, pg->norm0_b, r.nrows, s));
+  if (!dx) return MSFNO_OK;
   // ---- norm0 backward (+ dout through the identity outer skip, + dx1 through an identity
   // inner skip), then the linear inner skip's Ws^T dx1 --------------------------------------
   const float* add1 = d->outer_skip == MSFNO_SKIP_IDENTITY ? dout : nullptr;

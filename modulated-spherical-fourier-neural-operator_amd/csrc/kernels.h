@@ -175,6 +175,22 @@ int launch_fill(float* p, int64_t n, float v, hipStream_t s);
 // sc = (1 + gamma s) an, sh = (1 + gamma s) tn + beta s (n = B*C)
 int launch_film_affine(const float* an, const float* tn, const float* gamma, const float* beta,
                        float film_scale, float* sc, float* sh, int64_t n, hipStream_t s);
+// parameter gradients (param_bwd.hip): C[m * ldc + n * cs] = sum_b sum_k A_b[m][k] B'_b[n][k]
+// (B' by mode: B, per-(b, n) affine sc B + sh, GELU(B), complex pairs (re, im) -> (im, -re))
+enum { WGRAD_PLAIN = 0, WGRAD_AFFINE = 1, WGRAD_GELU = 2, WGRAD_CSWAP = 3 };
+size_t wgrad_nt_workspace(int M, int N, int64_t K, int batch);
+int launch_wgrad_nt(const float* A, int64_t lda, int64_t sA, const float* B, int64_t ldb,
+                    int64_t sB, int M, int N, int64_t K, int batch, int mode, const float* bsc,
+                    const float* bsh, float* C, int64_t ldc, int cs, void* ws, size_t ws_bytes,
+                    hipStream_t s);
+// dw[k][i][t] = sum_b g[b][k][t] conj(a[b][i][t]) (complex, the linear filter's weights)
+int launch_lin_wgrad(const float* g, const float* a, float* dw, int B, int Co, int Ci, int64_t T,
+                     hipStream_t s);
+// InstanceNorm affine gradients (x null: the bias / row-sum gradient db only)
+size_t norm_param_grad_workspace(int B, int C);
+int launch_norm_param_grad(const float* g, const float* x, const float* mean, const float* rstd,
+                           const float* gamma, float film_scale, int B, int C, int64_t P,
+                           float* dw, float* db, void* ws, hipStream_t s);
 // *d_flag |= 1 unless table[m][l][nlat-1-k] = (-1)^(l-m) table[m][l][k] (rel. 1e-5)
 int launch_check_symmetry(const float* table, int mmax, int lmax, int nlat, int* d_flag,
                           hipStream_t s);

@@ -50,6 +50,17 @@ class BlockDesc(ctypes.Structure):
     ]
 
 
+class BlockParamGrads(ctypes.Structure):
+    """Mirror of ``msfno_block_param_grads`` (include/msfno.h): output pointers of the
+    block's parameter gradients, NULL = not wanted."""
+
+    _fields_ = [
+        ("norm0_w", _vp), ("norm0_b", _vp), ("spec_w", _vp * 8), ("spec_wout", _vp),
+        ("lin_w", _vp), ("skip_w", _vp), ("skip_b", _vp), ("norm1_w", _vp), ("norm1_b", _vp),
+        ("fc1_w", _vp), ("fc1_b", _vp), ("fc2_w", _vp), ("fc2_b", _vp),
+    ]
+
+
 class MlpDesc(ctypes.Structure):
     """Mirror of ``msfno_mlp_desc`` (include/msfno.h)."""
 
@@ -114,6 +125,15 @@ SIGNATURES = [
                                                    _i]),
     ("msfno_block_backward", _i, [ctypes.POINTER(BlockDesc), _vp, _vp, _vp, _vp, _vp, _vp, _vp, _f,
                                   _vp, _vp, _vp, _vp, _i, _vp, _sz, _vp]),
+    ("msfno_block_backward_params_workspace_size", _sz, [ctypes.POINTER(BlockDesc), _vp, _vp,
+                                                          _vp, _vp, _i]),
+    ("msfno_block_backward_params", _i, [ctypes.POINTER(BlockDesc), _vp, _vp, _vp, _vp, _vp, _vp,
+                                         _vp, _f, _vp, _vp, _vp, _vp,
+                                         ctypes.POINTER(BlockParamGrads), _i, _vp, _sz, _vp]),
+    ("msfno_mlp_backward_params_workspace_size", _sz, [ctypes.POINTER(MlpDesc), _i,
+                                                        ctypes.c_longlong]),
+    ("msfno_mlp_backward_params", _i, [ctypes.POINTER(MlpDesc), _vp, _vp, _vp, _vp, _vp, _vp, _vp,
+                                       _vp, _i, ctypes.c_longlong, _vp, _sz, _vp]),
     ("msfno_block_backward_hidden_offsets", _i, [ctypes.POINTER(BlockDesc), _vp, _vp, _vp, _vp,
                                                  _i, ctypes.POINTER(_sz), _i,
                                                  ctypes.POINTER(_i)]),

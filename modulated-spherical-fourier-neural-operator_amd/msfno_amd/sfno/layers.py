@@ -250,9 +250,11 @@ class MLP(WeightCache, nn.Module):
         return out.to(dtype)
 
     @N.on_input_device
-    def native_backward_input(self, x, dy, x2=None):
-        """dL/dx of fc2(GELU(fc1(cat(x, x2)))) for frozen weights
-        (msfno_mlp_backward_input): the decoder's backward in FiLM fine-tuning."""
+    def native_backward_input(self, x, dy, x2=None, need_dx=True, params=()):
+        """dL/dx of fc2(GELU(fc1(cat(x, x2)))) (msfno_mlp_backward_params): the decoder's
+        backward in FiLM fine-tuning, plus the gradients of ``params`` (a subset of fc1 /
+        fc2 weight and bias: the decoder trains under --retrain-film, MSFNO/Models/sfno/
+        model.py:922-923).  Returns dx, or (dx, [dL/dp ...]) when params are given."""
         x = N.require_device_f32(x, "MLP input")
         dy = N.require_device_f32(dy, "MLP output gradient")
         B, Cin, H, W = x.shape
@@ -263,14 +265,28 @@ class MLP(WeightCache, nn.Module):
         d, keep = self.native_desc(cin2)
         L = N.lib()
         P = H * W
-        nbytes = L.msfno_mlp_backward_input_workspace_size(d, B, P)
+        fc1, fc2 = self.fwd[0], self.fwd[-1]
+        slots = {id(fc1.weight): 0, id(fc2.weight): 2}
+        if fc1.bias is not None:
+            slots[id(fc1.bias)] = 1
+        if fc2.bias is not None:
+            slots[id(fc2.bias)] = 3
+        outs, pgs = [None] * 4, []
+        for p in params:
+            if id(p) not in slots:
+                raise NotImplementedError(f"no native gradient for parameter {tuple(p.shape)}")
+            t = torch.empty(p.shape, dtype=torch.float32, device=x.device)
+            outs[slots[id(p)]] = t
+            pgs.append(t)
+        nbytes = (L.msfno_mlp_backward_params_workspace_size(d, B, P) if params
+                  else L.msfno_mlp_backward_input_workspace_size(d, B, P))
         ws = torch.empty(nbytes, dtype=torch.uint8, device=x.device)
-        dx = torch.empty(B, Cin, H, W, dtype=torch.float32, device=x.device)
-        N.check(L.msfno_mlp_backward_input(d, x.data_ptr(), N.ptr(x2), dy.data_ptr(),
-                                           dx.data_ptr(), B, P, ws.data_ptr(), nbytes,
-                                           N.stream_of(x.device)), "MLP.backward")
+        dx = torch.empty(B, Cin, H, W, dtype=torch.float32, device=x.device) if need_dx else None
+        N.check(L.msfno_mlp_backward_params(d, x.data_ptr(), N.ptr(x2), dy.data_ptr(), N.ptr(dx),
+                                            *[N.ptr(t) for t in outs], B, P, ws.data_ptr(),
+                                            nbytes, N.stream_of(x.device)), "MLP.backward")
         del keep
-        return dx
+        return (dx, pgs) if params else dx
 
     def forward(self, x):
         if torch.is_grad_enabled():
@@ -281,27 +297,37 @@ class MLP(WeightCache, nn.Module):
 
 
 class _MLPFn(torch.autograd.Function):
-    """Native MLP forward; backward to the first input only (weights frozen, as in
-    MSFNO's FiLM fine-tuning, sfnonet.py:787-860).  Trainable parameters ride along
-    as trailing inputs so that asking for their gradient raises."""
+    """Native MLP forward; backward to the first input (MSFNO's FiLM fine-tuning,
+    sfnonet.py:787-860) and to the MLP's trainable weights (the decoder under
+    --retrain-film), which ride along as trailing inputs."""
 
     @staticmethod
     def forward(ctx, x, x2, addend, mlp, *params):
-        ctx.mlp, ctx.nparams = mlp, len(params)
+        ctx.mlp, ctx.params = mlp, params
+        if addend is not None:
+            ctx.addend_shape, ctx.addend_dtype = addend.shape, addend.dtype
         ctx.save_for_backward(x, x2)
         return mlp.native_forward(x, x2=x2, addend=addend)
 
     @staticmethod
     def backward(ctx, dy):
-        from .sfnonet import refuse_param_grads
-        refuse_param_grads(ctx, 4, "MLP.backward")
+        from .sfnonet import _scatter, _wanted
         x, x2 = ctx.saved_tensors
-        if ctx.needs_input_grad[1] or ctx.needs_input_grad[2]:
-            raise NotImplementedError("MLP backward: gradients only to the first input")
-        dx = None
-        if ctx.needs_input_grad[0]:
-            dx = ctx.mlp.native_backward_input(x, dy, x2=x2).to(x.dtype)
-        return (dx, None, None, None) + (None,) * ctx.nparams
+        if ctx.needs_input_grad[1]:
+            raise NotImplementedError("MLP backward: no gradient to the second input (the "
+                                      "decoder's big skip is the network input)")
+        wanted = _wanted(ctx, 4, ctx.params)
+        dx, pgs = None, []
+        if ctx.needs_input_grad[0] or wanted:
+            res = ctx.mlp.native_backward_input(x, dy, x2=x2, need_dx=ctx.needs_input_grad[0],
+                                                params=wanted)
+            dx, pgs = res if wanted else (res, [])
+            dx = dx.to(x.dtype) if dx is not None else None
+        dadd = None
+        if ctx.needs_input_grad[2]:  # the encoder's pos_embed, broadcast over the batch
+            dadd = dy.sum(0, keepdim=True) if ctx.addend_shape[0] == 1 else dy
+            dadd = dadd.reshape(ctx.addend_shape).to(ctx.addend_dtype)
+        return (dx, None, dadd, None) + _scatter(ctx.params, wanted, pgs)
 
 
 def _check_transforms(fwd, inv):

@@ -213,9 +213,40 @@ class FourierNeuralOperatorBlock(WeightCache, nn.Module):
         return out.to(dtype)
 
     def trainable(self):
-        """The parameters that require grad (passed to autograd so a backward into them
-        raises instead of leaving .grad None)."""
+        """The parameters that require grad (passed to autograd, whose backward computes
+        their gradients natively: msfno_block_backward_params)."""
         return tuple(p for p in self.parameters() if p.requires_grad)
+
+    def param_grad_fields(self):
+        """(parameter, msfno_block_param_grads field, index) of every parameter the native
+        backward differentiates -- all of the block's parameters."""
+        out = []
+
+        def add(p, field, idx=None):
+            if p is not None:
+                out.append((p, field, idx))
+        for norm, tag in ((self.norm0, "norm0"), (self.norm1, "norm1")):
+            if norm.affine:
+                add(norm.weight, tag + "_w")
+                add(norm.bias, tag + "_b")
+        flt = self.filter_layer.filter
+        if isinstance(flt.w, nn.ParameterList):
+            for l, w in enumerate(flt.w):
+                add(w, "spec_w", l)
+            add(flt.wout, "spec_wout")
+        else:
+            add(flt.w, "lin_w")
+        if isinstance(getattr(self, "inner_skip", None), nn.Conv2d):
+            add(self.inner_skip.weight, "skip_w")
+            add(self.inner_skip.bias, "skip_b")
+        if hasattr(self, "mlp"):
+            seq = self.mlp.fwd
+            fc1, fc2 = seq[0], seq[-2] if len(seq) == 5 else seq[2]
+            add(fc1.weight, "fc1_w")
+            add(fc1.bias, "fc1_b")
+            add(fc2.weight, "fc2_w")
+            add(fc2.bias, "fc2_b")
+        return out
 
     def forward(self, x, *overflow):
         if torch.is_grad_enabled():
@@ -259,12 +290,13 @@ class FourierNeuralOperatorBlock(WeightCache, nn.Module):
 
     @N.on_input_device
     def native_backward(self, x, dout, gamma=None, beta=None, scale=1.0, need_dx=True,
-                        hidden_tap=None):
-        """(dL/dx, dL/dgamma, dL/dbeta) for dout = dL/d(out), the SFNO weights frozen
-        (msfno_block_backward; the forward is recomputed).  dgamma / dbeta are None for an
-        unfilmed call; dx is None unless need_dx.  ``hidden_tap`` (tests) receives the
-        non-linear filter's recomputed hidden activations, (B, hidden, lmax, mmax) complex
-        per layer, whose ReLU(real) masks this backward applied."""
+                        hidden_tap=None, params=()):
+        """(dL/dx, dL/dgamma, dL/dbeta) for dout = dL/d(out) (msfno_block_backward_params;
+        the forward is recomputed), plus a list of dL/dp for the parameters ``params``
+        (--retrain-film).  dgamma / dbeta are None for an unfilmed call; dx is None unless
+        need_dx.  ``hidden_tap`` (tests) receives the non-linear filter's recomputed hidden
+        activations, (B, hidden, lmax, mmax) complex per layer, whose ReLU(real) masks this
+        backward applied."""
         x = N.require_device_f32(x, "block input")
         dout = N.require_device_f32(dout, "block output gradient")
         B, C, H, W = x.shape
@@ -283,13 +315,31 @@ class FourierNeuralOperatorBlock(WeightCache, nn.Module):
             db = torch.empty(B, C, dtype=torch.float32, device=x.device)
         dx = torch.empty_like(x) if need_dx else None
         L = N.lib()
-        nbytes = L.msfno_block_backward_workspace_size(d, pf.handle, pi.handle, fa.handle,
-                                                        ga.handle, B)
+        pgs, pg = [], None
+        if params:
+            fields = {id(p): (f, i) for p, f, i in self.param_grad_fields()}
+            pg = N.BlockParamGrads()
+            for p in params:
+                if id(p) not in fields:
+                    raise NotImplementedError(f"no native gradient for parameter {tuple(p.shape)}")
+                f, i = fields[id(p)]
+                t = torch.empty(p.shape, dtype=torch.float32, device=x.device)
+                pgs.append(t)
+                if i is None:
+                    setattr(pg, f, t.data_ptr())
+                else:
+                    getattr(pg, f)[i] = t.data_ptr()
+            nbytes = L.msfno_block_backward_params_workspace_size(d, pf.handle, pi.handle,
+                                                                  fa.handle, ga.handle, B)
+        else:
+            nbytes = L.msfno_block_backward_workspace_size(d, pf.handle, pi.handle, fa.handle,
+                                                            ga.handle, B)
         ws = torch.empty(nbytes, dtype=torch.uint8, device=x.device)
-        N.check(L.msfno_block_backward(d, pf.handle, pi.handle, fa.handle, ga.handle, x.data_ptr(),
-                                       N.ptr(g), N.ptr(b), float(scale), dout.data_ptr(),
-                                       N.ptr(dx), N.ptr(dg), N.ptr(db), B, ws.data_ptr(), nbytes,
-                                       N.stream_of(x.device)),
+        N.check(L.msfno_block_backward_params(d, pf.handle, pi.handle, fa.handle, ga.handle,
+                                              x.data_ptr(), N.ptr(g), N.ptr(b), float(scale),
+                                              dout.data_ptr(), N.ptr(dx), N.ptr(dg), N.ptr(db),
+                                              pg, B, ws.data_ptr(), nbytes,
+                                              N.stream_of(x.device)),
                 type(self).__name__ + ".backward")
         if hidden_tap is not None:
             import ctypes
@@ -303,6 +353,8 @@ class FourierNeuralOperatorBlock(WeightCache, nn.Module):
                   .view(B, d.spec_hidden, fwd.lmax, fwd.mmax, 2) for l in range(nl.value)]
             hidden_tap([torch.view_as_complex(h.clone()) for h in hs])
         del keep
+        if params:
+            return dx, dg, db, pgs
         return dx, dg, db
 
     def defers_output_affine(self):
@@ -408,66 +460,66 @@ class FourierNeuralOperatorBlock_Filmed(FourierNeuralOperatorBlock):
         return dg, db
 
 
-def refuse_param_grads(ctx, first, what):
-    """Raise when autograd asks for a gradient of a module parameter (inputs ``first``
-    onwards of the Function).  The native backward gives dL/dx and dL/d(gamma, beta) only;
-    the reference's --retrain-film (main.py:958-960) makes the decoder and the last
-    film_layers blocks trainable (MSFNO/Models/sfno/model.py:922-923, 1016-1019), whose
-    weight gradients are not implemented natively.  Raising keeps them from being
-    silently left at None."""
-    if any(ctx.needs_input_grad[first:]):
-        raise NotImplementedError(
-            f"{what}: gradients of the module's own parameters are not implemented on the "
-            "MI355X path (dL/dx and FiLM dL/dgamma, dL/dbeta only); freeze them with "
-            "requires_grad_(False) (MSFNO trains the FiLM generator, model.py:1016-1023)")
+def _wanted(ctx, first, params):
+    """The trailing parameter inputs (from ``first``) whose gradient autograd asks for."""
+    return [p for p, need in zip(params, ctx.needs_input_grad[first:]) if need]
+
+
+def _scatter(params, wanted, grads):
+    """Gradients in the order of ``params`` (None where not wanted), cast to each dtype."""
+    by_id = {id(p): g for p, g in zip(wanted, grads)}
+    return tuple(by_id[id(p)].to(p.dtype) if id(p) in by_id else None for p in params)
 
 
 class _FilmedBlockFn(torch.autograd.Function):
-    """Native filmed-block forward; backward to (x, gamma, beta) with the SFNO weights
-    frozen (sfnonet.py:787-860 runs the filmed blocks with autograd and every
-    earlier block under no_grad).  The block's trainable parameters ride along as
-    trailing inputs so that asking for their gradient raises (refuse_param_grads)."""
+    """Native filmed-block forward; backward to (x, gamma, beta) and, for parameters that
+    require grad (--retrain-film: the last film_layers blocks train, MSFNO/Models/sfno/
+    model.py:922-923, 1016-1019), to the block's own weights (msfno_block_backward_params).
+    sfnonet.py:787-860 runs the filmed blocks with autograd and every earlier block under
+    no_grad; the trainable parameters ride along as trailing inputs."""
 
     @staticmethod
     def forward(ctx, x, gamma, beta, scale, blk, *params):
-        ctx.blk, ctx.scale, ctx.nparams = blk, scale, len(params)
+        ctx.blk, ctx.scale, ctx.params = blk, scale, params
         ctx.save_for_backward(x, gamma, beta)
         return blk._native_forward(x, gamma, beta, scale)
 
     @staticmethod
     def backward(ctx, dout):
-        refuse_param_grads(ctx, 5, type(ctx.blk).__name__ + ".backward")
         x, gamma, beta = ctx.saved_tensors
-        dx = None
-        if ctx.needs_input_grad[0]:
+        wanted = _wanted(ctx, 5, ctx.params)
+        dx, pgs = None, []
+        if ctx.needs_input_grad[0] or wanted:
             # dL/dx too (film_layers > 1, repeat_film: filmed blocks back to back)
-            dx, dg, db = ctx.blk.native_backward(x, dout, gamma, beta, ctx.scale)
-            dx = dx.to(x.dtype)
+            res = ctx.blk.native_backward(x, dout, gamma, beta, ctx.scale,
+                                          need_dx=ctx.needs_input_grad[0], params=wanted)
+            dx, dg, db = res[:3]
+            pgs = res[3] if wanted else []
+            dx = dx.to(x.dtype) if dx is not None else None
         else:
             dg, db = ctx.blk.native_film_backward(x, gamma, beta, ctx.scale, dout)
         return (dx, dg.reshape(gamma.shape).to(gamma.dtype),
-                db.reshape(beta.shape).to(beta.dtype), None, None) + (None,) * ctx.nparams
+                db.reshape(beta.shape).to(beta.dtype), None, None) + \
+            _scatter(ctx.params, wanted, pgs)
 
 
 class _BlockFn(torch.autograd.Function):
-    """Native unfilmed block forward with dL/dx (weights frozen; msfno_block_backward).
-    Trainable parameters ride along so that asking for their gradient raises."""
+    """Native unfilmed block forward with dL/dx and the gradients of its trainable
+    parameters (msfno_block_backward_params)."""
 
     @staticmethod
     def forward(ctx, x, blk, *params):
-        ctx.blk, ctx.nparams = blk, len(params)
+        ctx.blk, ctx.params = blk, params
         ctx.save_for_backward(x)
         return blk._native_forward(x)
 
     @staticmethod
     def backward(ctx, dout):
-        refuse_param_grads(ctx, 2, type(ctx.blk).__name__ + ".backward")
         (x,) = ctx.saved_tensors
-        dx = None
-        if ctx.needs_input_grad[0]:
-            dx, _, _ = ctx.blk.native_backward(x, dout)
-            dx = dx.to(x.dtype)
-        return (dx, None) + (None,) * ctx.nparams
+        wanted = _wanted(ctx, 2, ctx.params)
+        res = ctx.blk.native_backward(x, dout, need_dx=ctx.needs_input_grad[0], params=wanted)
+        dx = res[0].to(x.dtype) if res[0] is not None else None
+        return (dx, None) + _scatter(ctx.params, wanted, res[3] if wanted else [])
 
 
 def _trunc_normal_init(m):
@@ -611,7 +663,14 @@ class FourierNeuralOperatorNet(nn.Module):
         return {"pos_embed", "cls_token"}
 
     def encode(self, x):
-        """encoder(x) + pos_embed (sfnonet.py:667-674), pos_embed added in fc2's epilogue."""
+        """encoder(x) + pos_embed (sfnonet.py:667-674), pos_embed added in fc2's epilogue;
+        with autograd (a plain network in training) the gradients reach x, the encoder
+        weights and pos_embed natively (_MLPFn)."""
+        if torch.is_grad_enabled():
+            params = tuple(p for p in self.encoder.parameters() if p.requires_grad)
+            if x.requires_grad or self.pos_embed.requires_grad or params:
+                from .layers import _MLPFn
+                return _MLPFn.apply(x, None, self.pos_embed, self.encoder, *params)
         return self.encoder.native_forward(x, addend=self.pos_embed)
 
     def decode(self, x, residual):

@@ -32,7 +32,14 @@ def test_library_exports_every_declared_symbol():
         assert hasattr(lib, s), s
     # and the ctypes binding covers all of them
     assert {n for n, _, _ in N.SIGNATURES} == set(_declared_symbols())
-    assert lib.msfno_abi_version() == 5
+    assert lib.msfno_abi_version() == 6
+
+
+def test_block_param_grads_struct_layout():
+    from msfno_amd import _native as N
+    # 2 norm0, 8 spec_w, wout, lin_w, 2 skip, 2 norm1, 4 MLP pointers
+    assert ctypes.sizeof(N.BlockParamGrads) == (2 + 8 + 2 + 2 + 2 + 4) * 8
+    assert N.BlockParamGrads.fc2_b.offset == (2 + 8 + 2 + 2 + 2 + 3) * 8
 
 
 def test_block_desc_struct_layout():

@@ -222,38 +222,215 @@ def test_filmed_net_multi_layer_film_grads(path, film_layers):
     assert (want.abs().amax(dim=(0, 1, 3)) > 0).all()
 
 
-@pytest.mark.parametrize("which", ["filter_layer", "norm0", "decoder"])
-def test_trainable_sfno_weights_raise_not_none(which):
-    """--retrain-film makes the decoder and the last blocks trainable
-    (MSFNO/Models/sfno/model.py:922-923, 1016-1019).  The native backward has no
-    weight gradients: asking for one raises instead of leaving .grad None."""
+def _compare(tag, got, want, rel=1e-4, scale=0.0):
+    """max-abs < rel x max(max|want|, scale): `scale` is the matching weight's gradient
+    scale for a bias whose exact gradient vanishes (a per-channel constant that the next
+    InstanceNorm removes: the fp32 sum of a zero-mean gradient is noise at that scale)."""
+    got = got.detach().cpu().double()
+    assert got.shape == want.shape, (tag, got.shape, want.shape)
+    err = (got - want).abs().max().item()
+    tol = rel * max(want.abs().max().item(), scale, 1e-6)
+    print(f"{tag}: max-abs {err:.3e} (max|grad| {want.abs().max().item():.3e}, tol {tol:.2e})")
+    assert err < tol, (tag, err, tol)
+
+
+def _compare_params(tag, named, want_of):
+    """Every (name, parameter) of `named` against want_of(name); a bias is held to its
+    weight's gradient scale as well (_compare)."""
+    wants = {k: want_of(k) for k, _ in named}
+    n = 0
+    for k, p in named:
+        assert p.grad is not None, k
+        scale = 0.0
+        if k.endswith("bias") and k[:-4] + "weight" in wants:
+            scale = wants[k[:-4] + "weight"].abs().max().item()
+        _compare(f"{tag} d{k}", p.grad, wants[k], scale=scale)
+        n += 1
+    return n
+
+
+def _masked_oracle(taps, spectral_layers):
+    """A complex_relu_real for the oracle that applies the ComplexReLU(real) masks the GPU
+    backward used in the blocks it tapped (call order: block, then layer) and the oracle's
+    own elsewhere -- at a pre-activation within rounding of the kink the two sides may
+    legitimately differ (activations.py:42-46)."""
+    import oracle.sfno_ref as R
+    orig = R.complex_relu_real
+    calls = [0]
+
+    def relu(z):
+        blk, layer = divmod(calls[0], spectral_layers)
+        calls[0] += 1
+        if blk not in taps:
+            return orig(z)
+        m = (taps[blk][layer].real > 0).to(z.real.dtype)
+        return torch.complex(z.real * m, z.imag)
+    return relu
+
+
+def _tap_blocks(net, taps):
+    """Record every block backward's recomputed hidden activations into taps[block]."""
+    for i, blk in enumerate(net.blocks):
+        def tapped(*a, _i=i, _orig=blk.native_backward, **kwa):
+            return _orig(*a, hidden_tap=lambda hs: taps.__setitem__(_i, [h.cpu() for h in hs]),
+                         **kwa)
+        blk.native_backward = tapped
+
+
+PARAM_CASES = [p for p in golden_files()
+               if os.path.basename(p).startswith(("c1_", "c1b2_", "lg_", "down_", "up_"))]
+
+
+@pytest.mark.parametrize("path", PARAM_CASES, ids=lambda p: os.path.basename(p)[:-4])
+def test_block_param_grads_match_oracle_autograd(path):
+    """--retrain-film trains the last film_layers blocks (MSFNO/Models/sfno/model.py:922-923,
+    1016-1019): the gradient of every block parameter (norm affines, spectral weights of
+    either filter, inner skip, MLP) from msfno_block_backward_params, with dL/dx, against
+    fp64 autograd through the oracle.  Tolerance: max-abs < 1e-4 x max|grad| per tensor."""
+    import oracle.sfno_ref as R
+    meta, params, arrays, _ = load(path)
+    blk, _, _ = make_block(meta, params)
+    blk = blk.to(DEV)
+    taps = {}
+    _tap_blocks(type("OneBlock", (), {"blocks": [blk]}), taps)
+    scale = float(meta["scale"])
+    filmed = bool(meta["filmed"])
+    g = torch.Generator().manual_seed(17)
+    x0 = arrays["x"]
+    x = x0.clone().to(DEV).requires_grad_()
+    film = (arrays["gamma"].to(DEV), arrays["beta"].to(DEV), scale) if filmed else ()
+    y = blk(x, *film)
+    dout = torch.randn(y.shape, generator=g)
+    (y * dout.to(DEV)).sum().backward()
+    inner, outer, has_mlp = wiring_cfg(meta)
+    cfg = sfno_ref.BlockCfg(filter_type=meta["filter"], inner_skip=inner, outer_skip=outer,
+                            has_mlp=has_mlp)
+    pd = {k: (v.double().requires_grad_() if v.is_floating_point() else v)
+          for k, v in params.items()}
+    sht, isht = _oracle_transforms(meta)
+    xd = x0.double().requires_grad_()
+    orig = R.complex_relu_real
+    R.complex_relu_real = _masked_oracle(taps, cfg.spectral_layers)
+    try:
+        yd = sfno_ref.block_forward(pd, xd, sht, isht, cfg,
+                                    arrays["gamma"].double() if filmed else None,
+                                    arrays["beta"].double() if filmed else None, scale)
+        (yd * dout.double()).sum().backward()
+    finally:
+        R.complex_relu_real = orig
+    name = os.path.basename(path)[:-4]
+    _compare(f"{name} dx", x.grad, xd.grad)
+    n = _compare_params(name, list(blk.named_parameters()),
+                        lambda k: pd[k].grad if pd[k].grad is not None else torch.zeros_like(pd[k]))
+    assert n >= 5
+
+
+@pytest.mark.parametrize("path", NET_FIXTURES, ids=lambda p: os.path.basename(p)[:-4])
+def test_retrain_film_param_grads_match_oracle_autograd(path):
+    """--retrain-film on a FourierNeuralOperatorNet_Filmed (film_layers = 2): the decoder,
+    the last two blocks and the FiLM modulation get gradients (MSFNO/Models/sfno/model.py:
+    922-923, 1016-1019; the encoder and earlier blocks stay frozen, sfnonet.py:816-844),
+    against fp64 autograd through the oracle network."""
+    from types import SimpleNamespace
+
+    from msfno_amd.sfno import FourierNeuralOperatorNet_Filmed
+    meta, params, x, _, _ = load_net(path)
+    n, k = meta["num_layers"], 2
+    kw = dict(filter_type=meta["filter"], img_size=(meta["nlat"], meta["nlon"]),
+              scale_factor=meta["scale_factor"], in_chans=meta["in_chans"],
+              out_chans=meta["out_chans"], embed_dim_sfno=meta["C"], num_layers=n,
+              spectral_layers=3)
+    net = FourierNeuralOperatorNet_Filmed("cpu", SimpleNamespace(repeat_film=False),
+                                          film_layers=k, advanced_logging=False,
+                                          model_depth=None, **kw)
+    net.load_state_dict(params, strict=False)
+    net = net.eval().to(DEV)
+    grad_layers = ["decoder"] + [f"blocks.{n - 1 - i}." for i in range(k)]
+    for name, p in net.named_parameters():  # model.py:1014-1019
+        p.requires_grad_(any(name.startswith(gl) for gl in grad_layers))
+    B, C = x.shape[0], meta["C"]
+    g = torch.Generator().manual_seed(23)
+    film0 = 0.1 * torch.randn(B, 2, k, C, generator=g)
+    taps = {}
+    _tap_blocks(net, taps)
+    film = film0.clone().to(DEV).requires_grad_()
+    y = net(x.to(DEV), film, 0.8)
+    w = torch.randn(y.shape, generator=g)
+    (y * w.to(DEV)).sum().backward()
+    cfg = net_cfg(meta)
+    pd = {kk: (v.double() if v.is_floating_point() else v) for kk, v in params.items()}
+    for kk in pd:
+        if any(kk.startswith(gl) for gl in grad_layers) and pd[kk].is_floating_point():
+            pd[kk].requires_grad_()
+    tr64 = sfno_ref.make_net_transforms(cfg, torch.float64)
+    fd = film0.double().requires_grad_()
+    import oracle.sfno_ref as R
+    orig = R.complex_relu_real
+    R.complex_relu_real = _masked_oracle(taps, cfg.spectral_layers)  # the GPU's ReLU masks
+    try:
+        yd = sfno_ref.net_forward(pd, x.double(), cfg, tr64, film=(fd[:, 0], fd[:, 1]),
+                                  scale=0.8)
+        (yd * w.double()).sum().backward()
+    finally:
+        R.complex_relu_real = orig
+    tag = os.path.basename(path)[:-4]
+    _compare(f"{tag} dfilm", film.grad, fd.grad)
+    named = [(k, p) for k, p in net.named_parameters() if p.requires_grad]
+    for k, p in net.named_parameters():
+        if not p.requires_grad:
+            assert p.grad is None, k
+    trained = _compare_params(tag, named, lambda k: pd[k].grad if pd[k].grad is not None
+                              else torch.zeros_like(pd[k]))
+    assert trained >= 8
+
+
+@pytest.mark.parametrize("path", NET_FIXTURES, ids=lambda p: os.path.basename(p)[:-4])
+def test_plain_net_all_param_grads_match_oracle_autograd(path):
+    """A plain FourierNeuralOperatorNet in training (sfnonet.py:665-686, no no_grad
+    regions): every parameter -- encoder, pos_embed, all blocks, decoder -- and dL/dx
+    against fp64 autograd through the oracle network under the GPU's ReLU masks."""
+    import oracle.sfno_ref as R
     from test_gpu_net import _build
-    meta, params, x, _, _ = load_net(NET_FIXTURES[0])
-    net = _build(meta, params, filmed=True, film_layers=1).requires_grad_(False)
-    owner = net.decoder if which == "decoder" else net.blocks[-1]
-    name, p = next((n, q) for n, q in owner.named_parameters()
-                   if which == "decoder" or n.startswith(which))
-    p.requires_grad_(True)
-    film = (0.1 * torch.randn(x.shape[0], 2, 1, meta["C"])).to(DEV).requires_grad_()
-    y = net(x.to(DEV), film, 1.0)
-    with pytest.raises(NotImplementedError, match="parameters are not implemented"):
-        y.sum().backward()
-    assert p.grad is None, name
+    meta, params, x, _, _ = load_net(path)
+    net = _build(meta, params)
+    taps = {}
+    _tap_blocks(net, taps)
+    g = torch.Generator().manual_seed(29)
+    xg = x.clone().to(DEV).requires_grad_()
+    y = net(xg)
+    w = torch.randn(y.shape, generator=g)
+    (y * w.to(DEV)).sum().backward()
+    cfg = net_cfg(meta)
+    pd = {kk: (v.double().requires_grad_() if v.is_floating_point() else v)
+          for kk, v in params.items()}
+    tr64 = sfno_ref.make_net_transforms(cfg, torch.float64)
+    xd = x.double().requires_grad_()
+    orig = R.complex_relu_real
+    R.complex_relu_real = _masked_oracle(taps, cfg.spectral_layers)
+    try:
+        yd = sfno_ref.net_forward(pd, xd, cfg, tr64)
+        (yd * w.double()).sum().backward()
+    finally:
+        R.complex_relu_real = orig
+    tag = os.path.basename(path)[:-4]
+    _compare(f"{tag} dx", xg.grad, xd.grad)
+    n = _compare_params(tag, list(net.named_parameters()),
+                        lambda k: pd[k].grad if pd[k].grad is not None else torch.zeros_like(pd[k]))
+    assert n >= 20
 
 
-def test_block_trainable_weight_raises_without_input_grad():
-    """A block whose input needs no gradient but whose fc1 weight does still builds
-    an autograd node, and backward raises (no silent None)."""
+def test_block_weight_grad_without_input_grad():
+    """A block whose input needs no gradient but whose fc1 weight does (the first trained
+    block under --retrain-film) still builds an autograd node and fills .grad."""
     path = [p for p in FILM_CASES if "_nl_" in os.path.basename(p) and "_middle" in p][0]
     meta, params, arrays, _ = load(path)
     blk, _, _ = make_block(meta, params)
     blk = blk.to(DEV).requires_grad_(False)
-    blk.mlp.fwd[0].weight.requires_grad_(True)
+    w1 = blk.mlp.fwd[0].weight.requires_grad_(True)
     y = blk(arrays["x"].to(DEV), arrays["gamma"].to(DEV), arrays["beta"].to(DEV), 1.0)
     assert y.requires_grad
-    with pytest.raises(NotImplementedError):
-        y.sum().backward()
-    assert blk.mlp.fwd[0].weight.grad is None
+    y.sum().backward()
+    assert w1.grad is not None and torch.isfinite(w1.grad).all() and w1.grad.abs().max() > 0
 
 
 @pytest.mark.parametrize("film_layers", [4, "repeat"])
