@@ -314,14 +314,16 @@ int msfno_block_backward_hidden_offsets(const msfno_block_desc* d, msfno_sht_pla
  * gradient dy = dL/dy reaches it.
  *   dx = W1[:, :Cin]^T (GELU'(W1 [x ; x2] + b1) * (W2^T dy))
  * (dL/dx2 is not produced: x2 is the network input.) */
-/* The same backward with the parameter gradients (the decoder under --retrain-film):
- *   dW1 = dpre [x ; x2]^T, db1 = sum dpre, dW2 = dy GELU(pre)^T, db2 = sum dy
- * (summed over the batch and the P pixels).  dx and each gradient output may be NULL. */
+/* The same backward with the second input's and the parameter gradients (the decoder
+ * under --retrain-film; a plain network in training, whose big skip x2 is the network
+ * input):  dx2 = W1[:, Cin:]^T dpre,  dW1 = dpre [x ; x2]^T, db1 = sum dpre,
+ * dW2 = dy GELU(pre)^T, db2 = sum dy (summed over the batch and the P pixels).  dx, dx2
+ * and each gradient output may be NULL. */
 size_t msfno_mlp_backward_params_workspace_size(const msfno_mlp_desc* d, int B, long long P);
 int msfno_mlp_backward_params(const msfno_mlp_desc* d, const float* x, const float* x2,
-                              const float* dy, float* dx, float* dfc1_w, float* dfc1_b,
-                              float* dfc2_w, float* dfc2_b, int B, long long P, void* ws,
-                              size_t ws_bytes, void* stream);
+                              const float* dy, float* dx, float* dx2, float* dfc1_w,
+                              float* dfc1_b, float* dfc2_w, float* dfc2_b, int B, long long P,
+                              void* ws, size_t ws_bytes, void* stream);
 size_t msfno_mlp_backward_input_workspace_size(const msfno_mlp_desc* d, int B, long long P);
 int msfno_mlp_backward_input(const msfno_mlp_desc* d, const float* x, const float* x2,
                              const float* dy, float* dx, int B, long long P, void* ws,

@@ -2213,15 +2213,15 @@ int msfno_mlp_backward_input(const msfno_mlp_desc* d, const float* x, const floa
                              const float* dy, float* dx, int B, long long P, void* ws,
                              size_t ws_bytes, void* stream) {
   MSFNO_REQUIRE(dx, MSFNO_EINVAL, "mlp backward: missing tensors");
-  return msfno_mlp_backward_params(d, x, x2, dy, dx, nullptr, nullptr, nullptr, nullptr, B, P, ws,
-                                   ws_bytes, stream);
+  return msfno_mlp_backward_params(d, x, x2, dy, dx, nullptr, nullptr, nullptr, nullptr, nullptr,
+                                   B, P, ws, ws_bytes, stream);
 }
 
 int msfno_mlp_backward_params(const msfno_mlp_desc* d, const float* x, const float* x2,
-                              const float* dy, float* dx, float* dfc1_w, float* dfc1_b,
-                              float* dfc2_w, float* dfc2_b, int B, long long P, void* ws,
-                              size_t ws_bytes, void* stream) {
-  const bool params = dfc1_w || dfc1_b || dfc2_w || dfc2_b;
+                              const float* dy, float* dx, float* dx2, float* dfc1_w,
+                              float* dfc1_b, float* dfc2_w, float* dfc2_b, int B, long long P,
+                              void* ws, size_t ws_bytes, void* stream) {
+  const bool params = dfc1_w || dfc1_b || dfc2_w || dfc2_b || dx2;
   MSFNO_REQUIRE(d && x && dy && d->fc1_w && d->fc2_w && d->fc1_b, MSFNO_EINVAL,
                 "mlp backward: missing tensors");
   MSFNO_REQUIRE(d->Cin > 0 && d->Hid > 0 && d->Cout > 0 && d->Cin2 >= 0 && B > 0 && P > 0 &&
@@ -2299,6 +2299,14 @@ int msfno_mlp_backward_params(const msfno_mlp_desc* d, const float* x, const flo
                                        nullptr, dfc1_b, nr, s));
   } else {
     MSFNO_TRY(launch_gelu_grad_mul(dh, pre, (int64_t)B * Hd * P, s));
+  }
+  if (dx2) {
+    // dx2 = W1[:, Cin:]^T dpre (W1T holds the Cin2 x Hd transpose first, then dx's)
+    MSFNO_REQUIRE(x2 && d->Cin2 > 0 && d->Cin2 <= d->Cin, MSFNO_EINVAL,
+                  "mlp backward: dx2 needs x2 and Cin2 <= Cin");
+    MSFNO_TRY(launch_transpose_mat(d->fc1_w + d->Cin, (int)Hd, d->Cin2, (int)Ct, W1T, s));
+    MSFNO_TRY(gemm_dense(ROLE_FC2, TILE_256x128, W1T, dh, dx2, d->Cin2, Pi, (int)Hd, (int)Hd, Pi,
+                         Pi, 0, Hd * P, (int64_t)d->Cin2 * P, B, e0, w3, w3b, s));
   }
   if (!dx) return MSFNO_OK;
   MSFNO_TRY(launch_transpose_mat(d->fc1_w, (int)Hd, d->Cin, (int)Ct, W1T, s));

@@ -133,7 +133,7 @@ SIGNATURES = [
     ("msfno_mlp_backward_params_workspace_size", _sz, [ctypes.POINTER(MlpDesc), _i,
                                                         ctypes.c_longlong]),
     ("msfno_mlp_backward_params", _i, [ctypes.POINTER(MlpDesc), _vp, _vp, _vp, _vp, _vp, _vp, _vp,
-                                       _vp, _i, ctypes.c_longlong, _vp, _sz, _vp]),
+                                       _vp, _vp, _i, ctypes.c_longlong, _vp, _sz, _vp]),
     ("msfno_block_backward_hidden_offsets", _i, [ctypes.POINTER(BlockDesc), _vp, _vp, _vp, _vp,
                                                  _i, ctypes.POINTER(_sz), _i,
                                                  ctypes.POINTER(_i)]),

@@ -250,11 +250,12 @@ class MLP(WeightCache, nn.Module):
         return out.to(dtype)
 
     @N.on_input_device
-    def native_backward_input(self, x, dy, x2=None, need_dx=True, params=()):
+    def native_backward_input(self, x, dy, x2=None, need_dx=True, params=(), need_dx2=False):
         """dL/dx of fc2(GELU(fc1(cat(x, x2)))) (msfno_mlp_backward_params): the decoder's
         backward in FiLM fine-tuning, plus the gradients of ``params`` (a subset of fc1 /
         fc2 weight and bias: the decoder trains under --retrain-film, MSFNO/Models/sfno/
-        model.py:922-923).  Returns dx, or (dx, [dL/dp ...]) when params are given."""
+        model.py:922-923), and dL/dx2 when need_dx2.  Returns dx, or (dx, [dL/dp ...])
+        when params are given, with dx2 appended when asked for."""
         x = N.require_device_f32(x, "MLP input")
         dy = N.require_device_f32(dy, "MLP output gradient")
         B, Cin, H, W = x.shape
@@ -278,14 +279,18 @@ class MLP(WeightCache, nn.Module):
             t = torch.empty(p.shape, dtype=torch.float32, device=x.device)
             outs[slots[id(p)]] = t
             pgs.append(t)
-        nbytes = (L.msfno_mlp_backward_params_workspace_size(d, B, P) if params
+        nbytes = (L.msfno_mlp_backward_params_workspace_size(d, B, P) if params or need_dx2
                   else L.msfno_mlp_backward_input_workspace_size(d, B, P))
         ws = torch.empty(nbytes, dtype=torch.uint8, device=x.device)
         dx = torch.empty(B, Cin, H, W, dtype=torch.float32, device=x.device) if need_dx else None
+        dx2 = torch.empty_like(x2) if need_dx2 else None
         N.check(L.msfno_mlp_backward_params(d, x.data_ptr(), N.ptr(x2), dy.data_ptr(), N.ptr(dx),
-                                            *[N.ptr(t) for t in outs], B, P, ws.data_ptr(),
-                                            nbytes, N.stream_of(x.device)), "MLP.backward")
+                                            N.ptr(dx2), *[N.ptr(t) for t in outs], B, P,
+                                            ws.data_ptr(), nbytes, N.stream_of(x.device)),
+                "MLP.backward")
         del keep
+        if need_dx2:
+            return dx, pgs, dx2
         return (dx, pgs) if params else dx
 
     def forward(self, x):
@@ -313,21 +318,23 @@ class _MLPFn(torch.autograd.Function):
     def backward(ctx, dy):
         from .sfnonet import _scatter, _wanted
         x, x2 = ctx.saved_tensors
-        if ctx.needs_input_grad[1]:
-            raise NotImplementedError("MLP backward: no gradient to the second input (the "
-                                      "decoder's big skip is the network input)")
         wanted = _wanted(ctx, 4, ctx.params)
-        dx, pgs = None, []
-        if ctx.needs_input_grad[0] or wanted:
+        need2 = bool(ctx.needs_input_grad[1])  # the decoder's big skip (the network input)
+        dx, dx2, pgs = None, None, []
+        if ctx.needs_input_grad[0] or wanted or need2:
             res = ctx.mlp.native_backward_input(x, dy, x2=x2, need_dx=ctx.needs_input_grad[0],
-                                                params=wanted)
-            dx, pgs = res if wanted else (res, [])
+                                                params=wanted, need_dx2=need2)
+            if need2:
+                dx, pgs, dx2 = res
+                dx2 = dx2.to(x2.dtype)
+            else:
+                dx, pgs = res if wanted else (res, [])
             dx = dx.to(x.dtype) if dx is not None else None
         dadd = None
         if ctx.needs_input_grad[2]:  # the encoder's pos_embed, broadcast over the batch
             dadd = dy.sum(0, keepdim=True) if ctx.addend_shape[0] == 1 else dy
             dadd = dadd.reshape(ctx.addend_shape).to(ctx.addend_dtype)
-        return (dx, None, dadd, None) + _scatter(ctx.params, wanted, pgs)
+        return (dx, dx2, dadd, None) + _scatter(ctx.params, wanted, pgs)
 
 
 def _check_transforms(fwd, inv):

@@ -241,10 +241,14 @@ def _compare_params(tag, named, want_of):
     n = 0
     for k, p in named:
         assert p.grad is not None, k
-        scale = 0.0
+        scale, rel = 0.0, 1e-4
         if k.endswith("bias") and k[:-4] + "weight" in wants:
             scale = wants[k[:-4] + "weight"].abs().max().item()
-        _compare(f"{tag} d{k}", p.grad, wants[k], scale=scale)
+            if wants[k].abs().max().item() < 1e-6 * scale:
+                # exactly zero (a constant the next InstanceNorm removes): the fp32 sum of
+                # a zero-mean gradient over the grid, against the weight's scale
+                rel = 1e-3
+        _compare(f"{tag} d{k}", p.grad, wants[k], rel=rel, scale=scale)
         n += 1
     return n
 
