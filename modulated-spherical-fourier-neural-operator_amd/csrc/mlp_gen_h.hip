@@ -247,7 +247,7 @@ __device__ __forceinline__ void mg_glds16x4(uint64_t sbase, const uint32_t (&vof
       : "memory", "scc");
 }
 
-template <int KS, int OT>
+template <int KS, int OT, bool EARLY>
 __global__ __launch_bounds__(256, 2) void mlp_gen_h_kernel(MlpGParams p) {
   constexpr int W = MG_WAVES, NS = MG_NS;
   constexpr int SLICE_E = MG_SLICE * MG_TILE;    // fp16 per slice
@@ -357,6 +357,27 @@ __global__ __launch_bounds__(256, 2) void mlp_gen_h_kernel(MlpGParams p) {
   floatx4 oacc[OT];
 #pragma unroll
   for (int ot = 0; ot < OT; ++ot) oacc[ot] = floatx4{0.f, 0.f, 0.f, 0.f};
+  // the addend of every output row: with EARLY (the default) its loads are issued here and
+  // waited with x's, so the two latencies overlap; otherwise under the last unit's MFMAs
+  float rv[OT][4];
+  auto load_addend = [&]() {
+    if (p.addend) {
+      const float* ad = p.addend + (int64_t)z * p.add_bstride + pxc;
+#pragma unroll
+      for (int ot = 0; ot < OT; ++ot)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int r = 16 * ot + 4 * g + i;
+          rv[ot][i] = r < p.Cout ? __builtin_nontemporal_load(ad + (int64_t)r * P) : 0.f;
+        }
+    } else {
+#pragma unroll
+      for (int ot = 0; ot < OT; ++ot)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) rv[ot][i] = 0.f;
+    }
+  };
+  if constexpr (EARLY) load_addend();
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
@@ -451,25 +472,9 @@ __global__ __launch_bounds__(256, 2) void mlp_gen_h_kernel(MlpGParams p) {
 #pragma unroll
   for (int e2 = 0; e2 < 4; ++e2) conv_pair(HB - 1, e2, I1{});
   make_hb();
-  // the addend of every output row, in flight under the last unit's MFMAs (three
-  // workgroups per CU with half of it issued after that unit measured slower: 1.55 vs
-  // 1.33 ms for the encoder)
-  float rv[OT][4];
-  if (p.addend) {
-    const float* ad = p.addend + (int64_t)z * p.add_bstride + pxc;
-#pragma unroll
-    for (int ot = 0; ot < OT; ++ot)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int r = 16 * ot + 4 * g + i;
-        rv[ot][i] = r < p.Cout ? __builtin_nontemporal_load(ad + (int64_t)r * P) : 0.f;
-      }
-  } else {
-#pragma unroll
-    for (int ot = 0; ot < OT; ++ot)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) rv[ot][i] = 0.f;
-  }
+  // (not EARLY: in flight under the last unit's MFMAs; three workgroups per CU with half
+  // of it issued after that unit measured slower: 1.55 vs 1.33 ms for the encoder)
+  if constexpr (!EARLY) load_addend();
   unit(HB, (N0 + (HB - 1) * NU) / MG_SLICE, I0{}, F{}, T{});
 
   // ---- epilogue: unscale + b2 + addend, store (rows 16 ot + 4 g + i) -------------------
@@ -571,10 +576,18 @@ int launch_mlp_gen_h(const float* x, const float* xa, const float* xt, const flo
   p.tiles_per_field = (int)cdiv(P, 16 * MG_WAVES);
   const int64_t grid = (int64_t)B * p.tiles_per_field;
   MSFNO_REQUIRE(grid < (1LL << 31), MSFNO_EINVAL, "mlp_gen_h: grid too large");
-  if (KS == 3)
-    hipLaunchKernelGGL((mlp_gen_h_kernel<3, 16>), dim3((unsigned)grid), dim3(64 * MG_WAVES), 0, s, p);
+  // the encoder's addend (pos_embed) loads issued with x's: mlp_gen 2.48 / 2.51 / 2.46 ->
+  // 2.35 / 2.33 / 2.34 ms per 12-block step, net 124.5 / 124.0 / 123.9 -> 125.6 / 125.7 /
+  // 125.7 steps/s (three interleaved pairs, profiles/r06_h); MSFNO_MG_EARLY=0 restores
+  // the late form
+  const char* ee = getenv("MSFNO_MG_EARLY");
+  const bool early = !(ee && ee[0] == '0');
+  if (KS == 3 && early)
+    hipLaunchKernelGGL((mlp_gen_h_kernel<3, 16, true>), dim3((unsigned)grid), dim3(64 * MG_WAVES), 0, s, p);
+  else if (KS == 3)
+    hipLaunchKernelGGL((mlp_gen_h_kernel<3, 16, false>), dim3((unsigned)grid), dim3(64 * MG_WAVES), 0, s, p);
   else
-    hipLaunchKernelGGL((mlp_gen_h_kernel<11, 5>), dim3((unsigned)grid), dim3(64 * MG_WAVES), 0, s, p);
+    hipLaunchKernelGGL((mlp_gen_h_kernel<11, 5, false>), dim3((unsigned)grid), dim3(64 * MG_WAVES), 0, s, p);
   return launch_check("mlp_gen_h");
 }
 
