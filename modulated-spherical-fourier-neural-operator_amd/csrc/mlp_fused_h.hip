@@ -1191,14 +1191,8 @@ int launch_mlp_fused_h(const float* x1, const float* scale, const float* shift,
     }
     return MSFNO_OK;
   }
-  // MSFNO_MH_AHEAD=1|3 (A/B): A-fragment reads issued that many MFMA triples ahead
-  const char* ae = getenv("MSFNO_MH_AHEAD");
-  if (ae && ae[0] == '3')
-    hipLaunchKernelGGL((mlp_fused_h_kernel<3, false>), dim3((unsigned)tiles), dim3(64 * MH_WAVES), 0, s, p);
-  else if (ae && ae[0] == '1')
-    hipLaunchKernelGGL((mlp_fused_h_kernel<1, false>), dim3((unsigned)tiles), dim3(64 * MH_WAVES), 0, s, p);
-  else
-    hipLaunchKernelGGL((mlp_fused_h_kernel<2, false>), dim3((unsigned)tiles), dim3(64 * MH_WAVES), 0, s, p);
+  // A fragments read two MFMA triples ahead (one or three: equal within 1 %, profiles/r06_i)
+  hipLaunchKernelGGL((mlp_fused_h_kernel<2, false>), dim3((unsigned)tiles), dim3(64 * MH_WAVES), 0, s, p);
   return launch_check("mlp_fused_h");
 }
 
