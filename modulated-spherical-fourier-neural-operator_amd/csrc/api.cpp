@@ -1784,8 +1784,12 @@ static int block_forward_impl(const msfno_block_desc* d, msfno_sht_plan_t f, msf
     // a separate skip input has no norm0 statistics: its x3h B-row scales from its max
     if (b.xs && sx != x) MSFNO_TRY(launch_chan_pow2_scale(sx, (int64_t)B * C, P, b.xs, ss));
     if (b.xs && C == 256 && skip_h_env()) {
+      // the quarter-CU side grid only where the skip is forked at the block start and
+      // overlaps the whole SHT + spectral chain (non-linear filter); the other filters fork
+      // it after the contraction (skip_late below), where it is on the critical path (1.80 vs 0.79 ms,
+      // linear 85.9 vs 97.5 fields/s, profiles/r06_j)
       MSFNO_TRY(launch_skip_h(d->skip_w, b.xs, sx, x1, d->skip_b, B, P, b.dw.skip, b.dw.skip_b,
-                              ss, side != nullptr));
+                              ss, side != nullptr && d->filter_type == MSFNO_FILTER_NONLINEAR));
     } else if (b.xs) {
       MSFNO_TRY(gemm_x3(d->skip_w, (int)C, b.xs, sx, x1, (int)C, (int)P, (int)C, (int)P, (int)P,
                         C * P, C * P, B, e, b.dw.skip, b.dw.skip_b, ss));
