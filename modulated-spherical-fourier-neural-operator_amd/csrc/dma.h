@@ -32,6 +32,21 @@ __device__ __forceinline__ void glds16(const void* gsrc, uint32_t lds) {
       : "memory");
 }
 
+// one wave-instruction, SADDR form: lane l copies 16 B from sbase + voff (lane's 32-bit
+// byte offset) to LDS byte lds + 16 l (sbase, lds wave-uniform)
+__device__ __forceinline__ void glds16s(uint64_t sbase, uint32_t voff, uint32_t lds) {
+  unsigned keep;
+  sbase = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(sbase >> 32)) << 32) |
+          (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)sbase);
+  lds = (uint32_t)__builtin_amdgcn_readfirstlane((int)lds);
+  asm volatile(
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %2, %1\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "s"(sbase), "v"(voff), "s"(lds)
+      : "memory");
+}
+
 // six wave-instructions in one block (one m0 save / restore): lane l copies 16 B
 // from sbase + voff[i] to LDS byte lds + i * lds_step + 16 l.  sbase and lds must be
 // wave-uniform (SGPR operands); voff[i] are the lane's byte offsets (SADDR + VADDR

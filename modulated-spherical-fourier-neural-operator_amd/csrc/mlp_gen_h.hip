@@ -33,8 +33,11 @@
 #include "gemm_common.h"
 #include "kernels.h"
 
+#include <algorithm>
+#include <mutex>
 #include <string>
 #include <type_traits>
+#include <unordered_map>
 #include <utility>
 
 namespace msfno {
@@ -45,6 +48,7 @@ typedef _Float16 half8 __attribute__((ext_vector_type(8)));
 typedef _Float16 half2v __attribute__((ext_vector_type(2)));
 typedef float floatx4 __attribute__((ext_vector_type(4)));
 typedef float f2v __attribute__((ext_vector_type(2)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int MG_TILE = 1024;   // fp16 per 2-KB tile (two 512-element planes)
 constexpr int MG_SLICE = 8;     // tiles per 16-KB slice
@@ -162,10 +166,13 @@ __global__ __launch_bounds__(256) void mg_scale_kernel(
 }
 
 // one thread per fp16 pair of a real (non-pad) tile
+// layout 0: the unit stream above; layout 1 (mlp_gen_hp_kernel): all fc1 tiles first,
+// block-major (tile 2 KS j + i), then the fc2 tiles output-tile-major (tile 2 KS HB +
+// HB ot + j), no pad tiles
 __global__ void mg_image_kernel(const float* __restrict__ W1, const float* __restrict__ W2,
                                 const float* __restrict__ eta, const float* __restrict__ s1,
                                 const float* __restrict__ s2, int H, int Ct, int Cout, int KS,
-                                int OT, unsigned short* __restrict__ img) {
+                                int OT, int layout, unsigned short* __restrict__ img) {
   const int HB = H / 32;
   const int64_t n1 = (int64_t)HB * 2 * KS * 256, n2 = (int64_t)HB * OT * 256;
   for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < n1 + n2;
@@ -186,7 +193,7 @@ __global__ void mg_image_kernel(const float* __restrict__ W1, const float* __res
       const float* w = W1 + (int64_t)row * Ct;
       v0 = k < Ct ? w[k] * sc : 0.f;
       v1 = k + 1 < Ct ? w[k + 1] * sc : 0.f;
-      tile = mg_unit_tile(j, KS, OT) + i;
+      tile = layout ? 2 * KS * j + i : mg_unit_tile(j, KS, OT) + i;
     } else {
       const int j = (int)(tile_id / OT), ot = (int)(tile_id % OT);
       const int orow = 16 * ot + r;
@@ -199,7 +206,8 @@ __global__ void mg_image_kernel(const float* __restrict__ W1, const float* __res
       } else {
         v0 = v1 = 0.f;
       }
-      tile = mg_unit_tile(j + 1, KS, OT) + (j + 1 < HB ? 2 * KS : 0) + ot;
+      tile = layout ? (int64_t)2 * KS * HB + (int64_t)HB * ot + j
+                    : mg_unit_tile(j + 1, KS, OT) + (j + 1 < HB ? 2 * KS : 0) + ot;
     }
     uint32_t t0, t1;
     mg_split(v0, v1, t0, t1);
@@ -224,6 +232,7 @@ struct MlpGParams {
   const float* b2;      // [Cout] or null
   int64_t P, add_bstride;
   int Cin, Cin2, Cout, H, nslice, tiles_per_field;
+  int tiles;            // mlp_gen_hp_kernel: tiles of 128 pixels over all fields
 };
 
 // four wave-instructions (one m0 save / restore) of a 16-KB slice: lane l copies 16 B
@@ -493,6 +502,442 @@ __global__ __launch_bounds__(256, 2) void mlp_gen_h_kernel(MlpGParams p) {
   }
 }
 
+
+// ---- persistent, pipelined form (the encoder: Ct <= 96, H = 256, no second input) ------
+// mlp_gen_h_kernel runs one 64-pixel tile per workgroup: the x and addend loads, the
+// slice steps and the 4-byte output stores are three phases that every CU enters at
+// nearly the same time (PMC: MFMA busy 19 %, 56 % of wave cycles waiting on memory).
+// Here one workgroup of four waves per CU (one per SIMD, the whole register file) walks a
+// contiguous range of 128-pixel tiles, 32 pixels per wave as two 16-pixel groups, so each
+// A fragment read from LDS feeds two MFMA triples; and the loop order is changed so that
+// no HBM phase is left outside the slice steps:
+//   - fc1 for all 8 hidden blocks first (6 slices), the GELU'd hidden activation of the
+//     whole tile kept in registers as fc2 B fragments (fp16x2 pairs, 128 VGPRs);
+//   - then fc2 one 16-row output tile per slice (the slice holds W2' rows 16 ot..+15 for
+//     all 256 hidden channels), so an output tile is final after its own step: its
+//     epilogue runs in the next step (scaled, + b2, transposed through a per-wave LDS
+//     patch, + addend, 16-B stores of 128-B lines), under that step's MFMAs;
+//   - every ring slot carries, besides its 16-KB weight slice, one 2-KB piece per wave:
+//     in the fc1 steps 16 channels of the NEXT tile's x (raw fp32 into registers; split
+//     at the tile end, when the pixel's range scale over all its channels is known), in
+//     the fc2 steps the 16 addend rows of this tile's output tile (read back by the lane
+//     that stores them).  Each wave's pieces hold only its own pixels.
+// Arithmetic per output element is that of mlp_gen_h_kernel (same MFMA order, same
+// epilogue), so the two kernels agree bit for bit.
+//
+// vmcnt accounting (each wave, in issue order): group n = 4 weight DMAs + 2 piece DMAs
+// when step n has a piece, issued in step n - (NS - 1) after that step's epilogue stores
+// (2 per lane).  The wait for group n counts the stores and groups of the NS - 2 steps
+// in between (GpShape::younger, compile-time per step).  Groups 0..NS-2 are drained in
+// the prologue; the last tile issues dummy groups (its own slices and pieces again) and
+// the kernel drains every DMA before it exits.
+constexpr int GP_W = 4;                        // waves, one per SIMD
+constexpr int GP_PX = 32 * GP_W;               // 128 pixels per tile
+constexpr int GP_HB = 8;                       // hidden blocks of 32 (H = 256)
+constexpr int GP_WB = MG_SLICE * MG_TILE * 2;  // 16 KB of weight tiles per slice
+constexpr int GP_SLOT = GP_WB + GP_W * 2048;   // + one 2-KB piece per wave
+constexpr int GP_ERS = 36;                     // epilogue patch row stride (floats)
+constexpr int GP_EPI = 16 * GP_ERS * 4;        // per wave: 16 rows x 32 pixels
+
+template <int KS, int OT, bool ADD, int NS_>
+struct GpShape {
+  static constexpr int NS = NS_;  // ring slots
+  static constexpr int HB = GP_HB, NT1 = 2 * KS, NF = NT1 * HB;
+  static constexpr int NQ1 = NF / MG_SLICE;  // fc1 steps
+  static constexpr int NQ = NQ1 + OT;        // steps per tile
+  static constexpr int CP = 16 * OT;
+  // the next tile's x: 2 KS pieces (16 channels x 32 pixels per wave), carried by the
+  // groups of steps XS .. XS + 2 KS - 1 (issued in this tile's first steps, after the
+  // previous tile's x left the buffer) into a per-wave buffer read at the tile's end
+  static constexpr int XS = NS - 1, NXP = 2 * KS, XW = NXP * 2048;
+  static constexpr int LDS = NS * GP_SLOT + GP_W * XW + GP_W * GP_EPI + (3 * 32 * HB + 2 * CP) * 4;
+  static_assert(NF % MG_SLICE == 0 && XS + NXP < NQ, "x pieces land before the tile's end");
+  static_assert(OT % 2 == 0, "output tiles alternate between two accumulators");
+  static_assert(LDS <= 160 * 1024, "mlp_gen_hp LDS");
+  static_assert(NS >= 3, "ring depth");
+  __host__ __device__ static constexpr int md(int a) { return ((a % NQ) + NQ) % NQ; }
+  __host__ __device__ static constexpr bool xp(int q) { return q >= XS && q < XS + NXP; }
+  __host__ __device__ static constexpr bool ap(int q) { return ADD && q >= NQ1; }
+  __host__ __device__ static constexpr int grp(int q) { return 4 + (xp(q) ? 2 : 0) + (ap(q) ? 2 : 0); }
+  __host__ __device__ static constexpr int sto(int q) { return (q == 0 || q > NQ1) ? 2 : 0; }
+  // vector-memory instructions a wave issues after group q
+  __host__ __device__ static constexpr int younger(int q) {
+    int k = 0;
+    for (int d = 1; d <= NS - 2; ++d) k += sto(md(q - d)) + grp(md(q - d + NS - 1));
+    return k;
+  }
+};
+
+template <int N>
+__device__ __forceinline__ void gp_wait_vm() {
+  static_assert(N >= 0 && N <= 63, "vmcnt range");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"i"(N) : "memory");
+}
+
+template <int KS, int OT, bool ADD, int NS_>
+__global__ __launch_bounds__(64 * GP_W, 1) void mlp_gen_hp_kernel(MlpGParams p) {
+  using S = GpShape<KS, OT, ADD, NS_>;
+  constexpr int NS = S::NS, HB = S::HB, NT1 = S::NT1, NQ1 = S::NQ1, NQ = S::NQ, CP = S::CP;
+  __shared__ __attribute__((aligned(16))) char lds[S::LDS];
+  char* const xbuf = lds + NS * GP_SLOT;
+  float* const epi_all = reinterpret_cast<float*>(lds + NS * GP_SLOT + GP_W * S::XW);
+  float* const b1s = reinterpret_cast<float*>(lds + NS * GP_SLOT + GP_W * S::XW + GP_W * GP_EPI);
+  float* const is1s = b1s + 32 * HB;
+  float* const etas = is1s + 32 * HB;
+  float* const b2s = etas + 32 * HB;
+  float* const is2s = b2s + CP;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int r16 = lane & 15, g = lane >> 4;
+  const int64_t P = p.P;
+  const int tpf = p.tiles_per_field;
+  const int t0 = (int)((int64_t)blockIdx.x * p.tiles / gridDim.x);
+  const int t1 = (int)((int64_t)(blockIdx.x + 1) * p.tiles / gridDim.x);
+  const int ntile = t1 - t0;  // >= 1: the host launches at most `tiles` workgroups
+  const int wave_u = __builtin_amdgcn_readfirstlane(wave);
+  const uint32_t ring_lds = lds_addr(lds);
+  const uint32_t xbuf_lds = ring_lds + NS * GP_SLOT;
+
+  for (int i = tid; i < 32 * HB; i += 64 * GP_W) {
+    b1s[i] = p.b1[i];
+    is1s[i] = p.is1[i];
+    etas[i] = p.eta[i];
+  }
+  for (int i = tid; i < CP; i += 64 * GP_W) {
+    b2s[i] = (p.b2 && i < p.Cout) ? p.b2[i] : 0.f;
+    is2s[i] = p.is2[i];
+  }
+
+  // tile tl of this workgroup (clamped to its last tile: the tail's dummy groups)
+  struct Tile {
+    int z;
+    int64_t px0;
+  };
+  auto tile_of = [&](int tl) {
+    const int t = t0 + (tl < ntile ? tl : ntile - 1);
+    Tile r;
+    r.z = t / tpf;
+    r.px0 = (int64_t)(t - r.z * tpf) * GP_PX;
+    return r;
+  };
+
+  // ---- DMA groups ----------------------------------------------------------------------
+  uint32_t w_off[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) w_off[i] = (uint32_t)(i * GP_W * 1024 + lane * 16);
+  // piece DMA h2 of this wave: lane l -> LDS byte 16 l of the wave's 1-KB half h2, piece
+  // row R = 8 h2 + (l >> 3), pixel quad l & 7 (x pieces: quad (l & 7) ^ (R & 4), so the
+  // four lane groups reading a piece row hit distinct LDS banks)
+  const int prow0 = lane >> 3, pq = lane & 7;
+  auto issue = [&](uint32_t slot_off, const Tile& tw, const Tile& tx, auto qc) {
+    constexpr int Q = decltype(qc)::value;
+    // opaque copies: keep the per-step address arithmetic at the step (hoisted to the
+    // tile start, 22 steps of addresses overflow the SGPRs)
+    uint64_t img = reinterpret_cast<uint64_t>(p.img), xg = reinterpret_cast<uint64_t>(p.x),
+             ag = reinterpret_cast<uint64_t>(p.addend);
+    asm volatile("" : "+s"(img), "+s"(xg), "+s"(ag));
+    const uint32_t slot = ring_lds + slot_off;
+    const uint64_t wsrc = img + (uint64_t)Q * MG_SLICE * MG_TILE * 2 + (uint64_t)wave_u * 1024;
+    mg_glds16x4<GP_W * 1024>(wsrc, w_off, slot + (uint32_t)(wave_u * 1024));
+    const uint32_t pdst = slot + (uint32_t)(GP_WB + wave_u * 2048);
+    if constexpr (S::xp(Q)) {  // 16 channels of tile tx's x
+      constexpr int k = Q - S::XS, ks = k >> 1, h = k & 1;
+      const uint64_t base = xg + (uint64_t)((int64_t)tx.z * p.Cin * P * 4);
+      const uint32_t xdst = xbuf_lds + (uint32_t)(wave_u * S::XW + k * 2048);
+#pragma unroll
+      for (int h2 = 0; h2 < 2; ++h2) {
+        const int R = 8 * h2 + prow0;
+        const int c = min(32 * ks + 8 * (R >> 2) + 4 * h + (R & 3), p.Cin - 1);
+        const int64_t px = min(tx.px0 + 32 * wave + 4 * (pq ^ (R & 4)), P - 4);
+        glds16s(base, (uint32_t)(((int64_t)c * P + px) * 4), xdst + (uint32_t)(h2 * 1024));
+      }
+    }
+    if constexpr (S::ap(Q)) {  // addend rows 16 ot .. + 15 of tile tw
+      constexpr int ot = Q - NQ1;
+      const uint64_t base = ag + (uint64_t)((int64_t)tw.z * p.add_bstride * 4);
+#pragma unroll
+      for (int h2 = 0; h2 < 2; ++h2) {
+        const int r = min(16 * ot + 8 * h2 + prow0, p.Cout - 1);
+        const int64_t px = min(tw.px0 + 32 * wave + 4 * pq, P - 4);
+        glds16s(base, (uint32_t)(((int64_t)r * P + px) * 4), pdst + (uint32_t)(h2 * 1024));
+      }
+    }
+  };
+
+  // ---- register state --------------------------------------------------------------------
+  half8 xf[2][KS][2];          // this tile's x (B fragments of fc1) [pg][ks][plane]
+  uint32_t hf[HB][2][2][4];    // hidden activation: fc2 B fragments [j][pg][plane][pair]
+  floatx4 hacc[2][2][2];       // fc1 accumulators [block parity][pg][t]
+  floatx4 oacc[2][2];          // fc2 accumulators [output-tile parity][pg]
+  float ixi[2], etap[2], ietap[2], iet_prev[2];
+
+  // x (per pixel: the range scales, then the fp16x2 split); xv[pg][ks][e] raw, 0 past Cin
+  auto split_x = [&](const float (&xv)[2][KS][8]) {
+#pragma unroll
+    for (int pg = 0; pg < 2; ++pg) {
+      float m = 0.f;
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) m = fmaxf(m, fabsf(xv[pg][ks][e]));
+      m = fmaxf(m, __shfl_xor(m, 16));
+      m = fmaxf(m, __shfl_xor(m, 32));
+      const float xi = mg_pow2_below(m, 14);
+      etap[pg] = mg_pow2_below(m + 1.f, 14);
+      ixi[pg] = 1.f / xi;
+      ietap[pg] = 1.f / etap[pg];
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        uint32_t t[2][4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          mg_split(xv[pg][ks][2 * e] * xi, xv[pg][ks][2 * e + 1] * xi, t[0][e], t[1][e]);
+#pragma unroll
+        for (int pl = 0; pl < 2; ++pl) xf[pg][ks][pl] = mg_frag(t[pl][0], t[pl][1], t[pl][2], t[pl][3]);
+      }
+    }
+  };
+
+  // ---- prologue: groups 0..NS-2 in flight, the first tile's x by plain loads --------------
+  {
+    const Tile c0 = tile_of(0), c1 = tile_of(1);
+    mg_for<NS - 1>([&](auto qc) { issue((uint32_t)(decltype(qc)::value * GP_SLOT), c0, c1, qc); });
+    const float* xb = p.x + (int64_t)c0.z * p.Cin * P;
+    float xr[2][KS][8];
+#pragma unroll
+    for (int pg = 0; pg < 2; ++pg) {
+      const int64_t px = min(c0.px0 + 32 * wave + 16 * pg + r16, P - 1);
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const int c = 32 * ks + 8 * g + e;
+          xr[pg][ks][e] = c < p.Cin ? __builtin_nontemporal_load(xb + (int64_t)c * P + px) : 0.f;
+        }
+    }
+    split_x(xr);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int pg = 0; pg < 2; ++pg) {
+#pragma unroll
+      for (int t = 0; t < 2; ++t) hacc[a][pg][t] = floatx4{0.f, 0.f, 0.f, 0.f};
+      oacc[a][pg] = floatx4{0.f, 0.f, 0.f, 0.f};
+    }
+
+  const int a_lane = r16 * 32 + 8 * (g ^ mg_swz(r16));
+  float* const ep = epi_all + wave * 16 * GP_ERS;
+  auto mfma3 = [](const half8 (&a)[2], const half8 (&b)[2], floatx4& c) {
+    c = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[1], b[0], c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[0], b[1], c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[0], b[0], c, 0, 0, 0);
+  };
+  // pair e2 of hidden block j, pixel group pg (hacc[j & 1]): unscale, + b1, GELU, scale, split
+  auto conv = [&](auto jc, auto pgc, auto e2c) {
+    constexpr int j = decltype(jc)::value, pg = decltype(pgc)::value, e2 = decltype(e2c)::value;
+    constexpr int t = e2 >> 1, i = 2 * (e2 & 1);
+    const int row = 32 * j + 16 * t + 4 * g + i;
+    const float2 b = *reinterpret_cast<const float2*>(b1s + row);
+    const float2 is = *reinterpret_cast<const float2*>(is1s + row);
+    const float2 hs = *reinterpret_cast<const float2*>(etas + row);
+    const floatx4& h = hacc[j & 1][pg][t];
+    f32x2 v = {fmaf(h[i], is.x * ixi[pg], b.x), fmaf(h[i + 1], is.y * ixi[pg], b.y)};
+    v = gelu_erf2(v) * f32x2{hs.x * etap[pg], hs.y * etap[pg]};
+    mg_split(v.x, v.y, hf[j][pg][0][e2], hf[j][pg][1][e2]);
+  };
+  // step n's entry (run in step n - 1 under its last two tiles' MFMAs): group n landed
+  // for every wave, all reads of step n - 1's slot issued by now complete (so the group
+  // issued in step n may overwrite it), then the x piece and the first two A fragments
+  half8 a[4][2];  // A fragments of tiles u (mod 4); two tiles ahead
+  auto prep = [&](auto qc, uint32_t slot_off) {
+    constexpr int Q = decltype(qc)::value;
+    gp_wait_vm<S::younger(Q)>();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    const char* slot = lds + slot_off;
+    const unsigned short* ws = reinterpret_cast<const unsigned short*>(slot);
+#pragma unroll
+    for (int k = 0; k < 2; ++k)
+#pragma unroll
+      for (int pl = 0; pl < 2; ++pl)
+        a[k][pl] = *reinterpret_cast<const half8*>(ws + k * MG_TILE + pl * 512 + a_lane);
+  };
+
+  // epilogue in two halves: (1) unscale + b2 into the wave's patch, (2) rows back as 16-B
+  // vectors, + the addend piece of aslot, buffer stores
+  auto epi_patch = [&](int ot, const floatx4 (&acc)[2], const float (&iet)[2]) {
+    const int r0 = 16 * ot + 4 * g;
+    const float4 is = *reinterpret_cast<const float4*>(is2s + r0);
+    const float4 bb = *reinterpret_cast<const float4*>(b2s + r0);
+#pragma unroll
+    for (int pg = 0; pg < 2; ++pg) {
+      float* e0 = ep + (4 * g) * GP_ERS + 16 * pg + r16;
+      e0[0] = fmaf(acc[pg][0], is.x * iet[pg], bb.x);
+      e0[GP_ERS] = fmaf(acc[pg][1], is.y * iet[pg], bb.y);
+      e0[2 * GP_ERS] = fmaf(acc[pg][2], is.z * iet[pg], bb.z);
+      e0[3 * GP_ERS] = fmaf(acc[pg][3], is.w * iet[pg], bb.w);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  };
+  auto epi_store = [&](int ot, const Tile& tw, const char* aslot) {
+    // buffer stores: every wave issues both (the vmcnt counts stay exact); a lane past
+    // the field's last pixel or row points outside the field's range and is dropped
+    const int64_t pxl = tw.px0 + 32 * wave + 4 * pq;
+    const __amdgpu_buffer_rsrc_t orsrc = __builtin_amdgcn_make_buffer_rsrc(
+        p.out + (int64_t)tw.z * p.Cout * P, (short)0, (int)((int64_t)p.Cout * P * 4), 0x00020000);
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int row = 8 * k + prow0;
+      floatx4 v = *reinterpret_cast<const floatx4*>(ep + row * GP_ERS + 4 * pq);
+      if constexpr (ADD)
+        v += *reinterpret_cast<const floatx4*>(aslot + GP_WB + wave * 2048 + k * 1024 + lane * 16);
+      // (a row past Cout lies past the field's range by itself)
+      const uint32_t off = pxl < P ? (uint32_t)(((int64_t)(16 * ot + row) * P + pxl) * 4) : 0x80000000u;
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), orsrc, off, 0, 2 /* nt */);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  };
+
+  prep(std::integral_constant<int, 0>{}, 0u);
+  Tile prev = tile_of(0);
+  // byte offsets of the slots of the current and the previous step (a running pair,
+  // opaque to the compiler so that 22 steps of slot addresses are not precomputed)
+  uint32_t so = 0, so_prev = (NS - 1) * GP_SLOT;
+  for (int tl = 0; tl < ntile; ++tl) {
+    const Tile cur = tile_of(tl), nx1 = tile_of(tl + 1), nx2 = tile_of(tl + 2);
+    mg_for<NQ>([&](auto qc) {
+      constexpr int Q = decltype(qc)::value;
+      constexpr int QN = Q + NS - 1;  // the step whose group this step issues
+      asm volatile("" : "+s"(so), "+s"(so_prev));
+      const char* slot = lds + so;
+      const char* pslot = lds + so_prev;  // step n - 1
+      const uint32_t so_next = so + GP_SLOT == NS * GP_SLOT ? 0u : so + GP_SLOT;
+      const unsigned short* ws = reinterpret_cast<const unsigned short*>(slot);
+      // the previous output tile (this tile's, or the last of the previous tile)
+      constexpr bool EPI = Q > NQ1 || Q == 0;
+      const bool epi = Q > NQ1 || (Q == 0 && tl > 0);
+      if constexpr (Q == NQ1) {  // the last hidden block (its MFMAs ran in the last fc1 step)
+        mg_for<8>([&](auto cc) {
+          constexpr int c = decltype(cc)::value;
+          conv(std::integral_constant<int, HB - 1>{}, std::integral_constant<int, (c >> 2)>{},
+               std::integral_constant<int, (c & 3)>{});
+        });
+#pragma unroll
+        for (int pg = 0; pg < 2; ++pg)
+#pragma unroll
+          for (int t = 0; t < 2; ++t) hacc[(HB - 1) & 1][pg][t] = floatx4{0.f, 0.f, 0.f, 0.f};
+      }
+      mg_for<MG_SLICE>([&](auto uc) {
+        constexpr int u = decltype(uc)::value;
+        if constexpr (u + 2 < MG_SLICE) {
+#pragma unroll
+          for (int pl = 0; pl < 2; ++pl)
+            a[(u + 2) % 4][pl] = *reinterpret_cast<const half8*>(ws + (u + 2) * MG_TILE + pl * 512 + a_lane);
+        }
+        const half8(&av)[2] = a[u % 4];
+        if constexpr (Q < NQ1) {  // fc1 tile f: block j, k-step ks, row half t
+          constexpr int f = MG_SLICE * Q + u, j = f / NT1, i = f % NT1;
+#pragma unroll
+          for (int pg = 0; pg < 2; ++pg) mfma3(av, xf[pg][i >> 1], hacc[j & 1][pg][i & 1]);
+          if constexpr (j >= 1) {  // block j - 1 converted under block j's tiles
+            mg_for<8>([&](auto cc) {
+              constexpr int c = decltype(cc)::value;
+              if constexpr ((c * NT1) / 8 == i)
+                conv(std::integral_constant<int, j - 1>{}, std::integral_constant<int, (c >> 2)>{},
+                     std::integral_constant<int, (c & 3)>{});
+            });
+            if constexpr (i == (7 * NT1) / 8) {
+#pragma unroll
+              for (int pg = 0; pg < 2; ++pg)
+#pragma unroll
+                for (int t = 0; t < 2; ++t) hacc[(j - 1) & 1][pg][t] = floatx4{0.f, 0.f, 0.f, 0.f};
+            }
+          }
+        } else {  // fc2 of output tile ot, hidden block u
+          constexpr int ot = Q - NQ1;
+          if constexpr (u == 0) {
+#pragma unroll
+            for (int pg = 0; pg < 2; ++pg) oacc[ot & 1][pg] = floatx4{0.f, 0.f, 0.f, 0.f};
+          }
+#pragma unroll
+          for (int pg = 0; pg < 2; ++pg) {
+            const half8 hb[2] = {mg_frag(hf[u][pg][0][0], hf[u][pg][0][1], hf[u][pg][0][2], hf[u][pg][0][3]),
+                                 mg_frag(hf[u][pg][1][0], hf[u][pg][1][1], hf[u][pg][1][2], hf[u][pg][1][3])};
+            mfma3(av, hb, oacc[ot & 1][pg]);
+          }
+        }
+        if constexpr (EPI && u == 1) {
+          if (epi) {
+            if constexpr (Q == 0) epi_patch(OT - 1, oacc[(OT - 1) & 1], iet_prev);
+            else epi_patch(Q - NQ1 - 1, oacc[(Q - NQ1 - 1) & 1], ietap);
+          }
+        }
+        if constexpr (u == 3) {
+          // the epilogue's stores, then this step's group (into the slot of step n - 1,
+          // whose addend piece the stores have just read)
+          if constexpr (EPI) {
+            if (epi) {
+              if constexpr (Q == 0) epi_store(OT - 1, prev, pslot);
+              else epi_store(Q - NQ1 - 1, cur, pslot);
+            }
+          }
+          if constexpr (QN < NQ) issue(so_prev, cur, nx1, std::integral_constant<int, QN>{});
+          else issue(so_prev, nx1, nx2, std::integral_constant<int, QN - NQ>{});
+        }
+        if constexpr (u == 6) {
+          if constexpr (Q + 1 < NQ) {
+            prep(std::integral_constant<int, Q + 1>{}, so_next);
+          } else {
+            // the tile's end: the next tile's x (range scales, split; this tile's 1 / etap
+            // kept for its last output tile, whose epilogue runs in the next tile's first
+            // step), then the next tile's first step
+            iet_prev[0] = ietap[0];
+            iet_prev[1] = ietap[1];
+            if (tl + 1 < ntile) {
+              // the next tile's x from the wave's buffer (channels 32 ks + 8 g + e of
+              // piece 2 ks + e / 4, row 4 g + e % 4); channels past Cin read 0 (opaque:
+              // loop-invariant lane masks would be hoisted into SGPRs)
+              int cin = p.Cin;
+              asm volatile("" : "+s"(cin));
+              const char* xw = xbuf + wave * S::XW;
+              float xr[2][KS][8];
+#pragma unroll
+              for (int pg = 0; pg < 2; ++pg) {
+                const int px = 16 * pg + r16, quad = px >> 2;
+#pragma unroll
+                for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+                  for (int e8 = 0; e8 < 8; ++e8) {
+                    const int k = 2 * ks + (e8 >> 2), R = 4 * g + (e8 & 3);
+                    const float v = *reinterpret_cast<const float*>(
+                        xw + k * 2048 + (R >> 3) * 1024 + ((R & 7) * 8 + (quad ^ (R & 4))) * 16 + (px & 3) * 4);
+                    xr[pg][ks][e8] = 32 * ks + 8 * g + e8 < cin ? v : 0.f;
+                  }
+              }
+              split_x(xr);
+              prep(std::integral_constant<int, 0>{}, so_next);
+            }
+          }
+        }
+      });
+      so_prev = so;
+      so = so_next;
+    });
+    prev = cur;
+  }
+  // the last output tile of the last tile (its addend piece is in the last step's slot)
+  epi_patch(OT - 1, oacc[(OT - 1) & 1], iet_prev);
+  epi_store(OT - 1, prev, lds + so_prev);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the tail's dummy DMAs land before exit
+}
+
 // the instantiated widths: (KS, OT) = (3, 16): the encoder 73 -> 256 -> 256;
 // (11, 5): the decoder 329 -> 256 -> 73
 bool mg_shape(int Ct, int Cout, int* ks, int* ot) {
@@ -543,6 +988,17 @@ int launch_mlp_gen_h(const float* x, const float* xa, const float* xt, const flo
                 MSFNO_EINVAL, "mlp_gen_h: bad arguments");
   const int HB = H / 32, Cp = 16 * OT;
   const int64_t tiles = mg_tiles(HB, KS, OT);
+  // the persistent pipelined kernel (the encoder shape; MSFNO_MG_P=0 keeps one tile per
+  // workgroup).  Its pieces and stores move 4 pixels per lane (P % 4 == 0) with 32-bit
+  // byte offsets into a field
+  static const bool persist_env = [] {
+    const char* e = getenv("MSFNO_MG_P");
+    return !(e && e[0] == '0');
+  }();
+  const bool persist = persist_env && KS == 3 && OT == 16 && HB == GP_HB && !xa && !x2 &&
+                       P % 4 == 0 && P >= 4 && (int64_t)Cin * P * 4 < (1LL << 32) &&
+                       (int64_t)Cout * P * 4 < (1LL << 31);
+  const int layout = persist ? 1 : 0;
   // the weight image and its scale vectors: in the caller's prepared-weight cache when
   // given (rebuilt only when cache_valid is 0), else in the workspace on every call
   char* base = static_cast<char*>(cache ? cache : ws);
@@ -552,6 +1008,16 @@ int launch_mlp_gen_h(const float* x, const float* xa, const float* xt, const flo
   float* is1 = s1 + H;
   float* s2 = is1 + H;
   float* is2 = s2 + Cp;
+  // the image layout each cache was built with: a cached image of the other layout (a
+  // call of the same weights that the persistent kernel cannot take) is rebuilt
+  if (cache) {
+    static std::mutex mu;
+    static std::unordered_map<const void*, int> built;
+    std::lock_guard<std::mutex> lk(mu);
+    auto it = built.find(cache);
+    if (it == built.end() || it->second != layout) cache_valid = 0;
+    built[cache] = layout;
+  }
   if (!(cache && cache_valid)) {
     // the pad tiles are streamed (never multiplied): keep them finite
     if (hipMemsetAsync(img, 0, tiles * MG_TILE * 2, s) != hipSuccess) {
@@ -564,7 +1030,7 @@ int launch_mlp_gen_h(const float* x, const float* xa, const float* xt, const flo
                        s1, s2, is1, is2);
     MSFNO_TRY(launch_check("mg_scale"));
     hipLaunchKernelGGL(mg_image_kernel, dim3(256), dim3(256), 0, s, W1, W2, eta, s1, s2, H, Ct,
-                       Cout, KS, OT, img);
+                       Cout, KS, OT, layout, img);
     MSFNO_TRY(launch_check("mg_image"));
   }
   MlpGParams p{};
@@ -573,6 +1039,26 @@ int launch_mlp_gen_h(const float* x, const float* xa, const float* xt, const flo
   p.P = P; p.add_bstride = add_bstride;
   p.Cin = Cin; p.Cin2 = Cin2; p.Cout = Cout; p.H = H;
   p.nslice = (int)(tiles / MG_SLICE);
+  if (persist) {
+    static const int cus = [] {
+      int dev = 0, n = 0;
+      if (hipGetDevice(&dev) != hipSuccess ||
+          hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+        n = 256;
+      return n;
+    }();
+    p.tiles_per_field = (int)cdiv(P, GP_PX);
+    const int64_t t = (int64_t)B * p.tiles_per_field;
+    MSFNO_REQUIRE(t < (1LL << 31), MSFNO_EINVAL, "mlp_gen_hp: grid too large");
+    p.tiles = (int)t;
+    const int grid = (int)std::min<int64_t>(t, cus);  // one workgroup fills a CU
+    // ring depth 4 (5 and 6 measured equal with the x pieces in the ring slots,
+    // profiles/r06_l; with the x buffer only 4 fits)
+    const dim3 gd((unsigned)grid), bd(64 * GP_W);
+    if (addend) hipLaunchKernelGGL((mlp_gen_hp_kernel<3, 16, true, 4>), gd, bd, 0, s, p);
+    else hipLaunchKernelGGL((mlp_gen_hp_kernel<3, 16, false, 4>), gd, bd, 0, s, p);
+    return launch_check("mlp_gen_hp");
+  }
   p.tiles_per_field = (int)cdiv(P, 16 * MG_WAVES);
   const int64_t grid = (int64_t)B * p.tiles_per_field;
   MSFNO_REQUIRE(grid < (1LL << 31), MSFNO_EINVAL, "mlp_gen_h: grid too large");

@@ -31,10 +31,23 @@ CASES = [
     (73, 0, 256, 256, 3001, 2, "broadcast", True),   # encoder + pos_embed
     (256, 73, 256, 73, 2145, 2, None, False),        # decoder over cat(x, residual)
     (256, 73, 256, 73, 1000, 1, "batched", True),
+    # the persistent encoder kernel (P % 4 == 0): 301 128-pixel tiles per field, two
+    # fields -> more tiles than CUs, workgroup ranges crossing the field boundary, a
+    # 36-pixel last tile
+    (73, 0, 256, 256, 38436, 2, "broadcast", True),
+    (73, 0, 256, 256, 38436, 2, None, False),
+    (96, 0, 256, 256, 3000, 2, "batched", True),     # Ct = 96: no padded channels
 ]
+# the persistent kernel's cases (mlp_gen_hp_kernel vs mlp_gen_h_kernel, bitwise)
+PCASES = [c for c in CASES if c[1] == 0 and c[4] % 4 == 0]
 
 
 def _case(Cin, Cin2, Hid, Cout, P, B, addend, bias, seed):
+    got, y64, scale = _run(Cin, Cin2, Hid, Cout, P, B, addend, bias, seed)
+    return ((got - y64).abs() / scale).max().item(), (got - y64).abs().max().item()
+
+
+def _run(Cin, Cin2, Hid, Cout, P, B, addend, bias, seed):
     from msfno_amd.sfno import MLP
     torch.manual_seed(seed)
     m = MLP(in_features=Cin + Cin2, hidden_features=Hid, out_features=Cout,
@@ -70,7 +83,7 @@ def _case(Cin, Cin2, Hid, Cout, P, B, addend, bias, seed):
             x.to(DEV), x2=None if x2 is None else x2.to(DEV),
             addend=None if add is None else add.to(DEV)).double().cpu()[:, :, 0, :]
     assert torch.isfinite(got).all()
-    return ((got - y64).abs() / scale).max().item(), (got - y64).abs().max().item()
+    return got, y64, scale
 
 
 def _errors():
@@ -88,6 +101,23 @@ def test_fused_x3h_mlp_matches_fp64_like_x6():
         print(f"{c[:6]}: x3h fused rel {rg:.2e} abs {ag:.2e} | x6 two-GEMM rel {rx:.2e} abs {ax:.2e}")
         assert rg < 2e-6, c
         assert rg < 4 * rx + 1e-7, c
+
+
+def test_persistent_encoder_equals_tile_kernel_bitwise(tmp_path):
+    """mlp_gen_hp_kernel (persistent, pipelined; the default for the encoder shape) does
+    each output element's arithmetic in the order mlp_gen_h_kernel does: the two agree
+    bit for bit (MSFNO_MG_P=0 selects the one-tile-per-workgroup kernel, child process)."""
+    dump = tmp_path / "tile.pt"
+    env = dict(os.environ, MSFNO_MG_P="0")
+    out = subprocess.run([sys.executable, os.path.abspath(__file__), "--dump", str(dump)], env=env,
+                         cwd=HERE, capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr[-2000:]
+    ref = torch.load(dump, weights_only=True)
+    for i, c in enumerate(PCASES):
+        got = _run(*c, seed=CASES.index(c))[0]
+        nd = (got != ref[i]).sum().item()
+        print(f"{c[:6]}: {nd} of {got.numel()} differ, max-abs {(got - ref[i]).abs().max().item():.3e}")
+        assert nd == 0, c
 
 
 def test_fused_mlp_stage_is_the_fused_kernel():
@@ -143,4 +173,7 @@ def test_deferred_last_block_affine_equals_separate_pass():
 if __name__ == "__main__":
     sys.path.insert(0, HERE)
     import conftest  # noqa: F401  (puts the package on sys.path)
-    print(json.dumps(_errors()))
+    if len(sys.argv) > 2 and sys.argv[1] == "--dump":
+        torch.save([_run(*c, seed=CASES.index(c))[0] for c in PCASES], sys.argv[2])
+    else:
+        print(json.dumps(_errors()))
