@@ -87,8 +87,12 @@ STAGE_KERNEL_X3H = dict(STAGE_KERNEL_X6, **{
     # MSFNO_SKIP_H=0: gemm_x3)
     "inner_skip": "msfno::(anonymous namespace)::skip_hp_kernel("
                   "msfno::(anonymous namespace)::SkipHPParams)",
-    "mlp_fused": "void msfno::(anonymous namespace)::mlp_fused_h_kernel<2, false>"
-                 "(msfno::(anonymous namespace)::MlpHParams)",
+    # (raw-buffer addressing since round 6; the profiles before it name the same tiling
+    # with 64-bit addressing <2, false>, same HBM traffic)
+    "mlp_fused": ("void msfno::(anonymous namespace)::mlp_fused_h_kernel<2, false, true>"
+                  "(msfno::(anonymous namespace)::MlpHParams)",
+                  "void msfno::(anonymous namespace)::mlp_fused_h_kernel<2, false>"
+                  "(msfno::(anonymous namespace)::MlpHParams)"),
     "legendre_fwd": "void msfno::(anonymous namespace)::legendre_x3f_kernel<3>("
                     "msfno::(anonymous namespace)::X3FParams)",
     "legendre_inv": "msfno::(anonymous namespace)::legendre_x3r_kernel("
@@ -150,6 +154,7 @@ def pmc_traffic(stage):
         STAGE_KERNEL_X6 if x6_engine()[0] else STAGE_KERNEL_F32).get(stage)
     if sym is None:
         return None, None
+    syms = (sym,) if isinstance(sym, str) else sym
     import glob
     import re
 
@@ -161,11 +166,13 @@ def pmc_traffic(stage):
                     key=newest_first, reverse=True):
         try:
             with open(f) as fh:
-                k = json.load(fh)["kernels"].get(sym)
+                ks = json.load(fh)["kernels"]
         except (OSError, ValueError, KeyError):
             continue
-        if k and k.get("hbm_bytes"):
-            return round(k["hbm_bytes"]), os.path.relpath(f, REPO)
+        for sy in syms:
+            k = ks.get(sy)
+            if k and k.get("hbm_bytes"):
+                return round(k["hbm_bytes"]), os.path.relpath(f, REPO)
     return None, None
 
 

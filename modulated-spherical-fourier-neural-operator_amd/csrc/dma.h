@@ -47,6 +47,21 @@ __device__ __forceinline__ void glds16s(uint64_t sbase, uint32_t voff, uint32_t 
       : "memory");
 }
 
+// raw buffer access (stride 0) with a 32-bit lane offset and a wave-uniform SGPR offset:
+// a strided fp32 plane is then addressed with at most one VALU op per access, not a
+// 64-bit multiply-add; lanes whose LANE offset is past `bytes` (< 2^31) read 0 and drop
+// their stores (the range check does not include the SGPR offset).
+// aux 2 = nt (the nontemporal policy of __builtin_nontemporal_load / _store)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* p, int64_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ float buf_ld_nt(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, 2));
+}
+__device__ __forceinline__ void buf_st_nt(float v, __amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
+  __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), r, voff, soff, 2);
+}
+
 // six wave-instructions in one block (one m0 save / restore): lane l copies 16 B
 // from sbase + voff[i] to LDS byte lds + i * lds_step + 16 l.  sbase and lds must be
 // wave-uniform (SGPR operands); voff[i] are the lane's byte offsets (SADDR + VADDR

@@ -256,7 +256,9 @@ __device__ __forceinline__ void glds16x4(uint64_t sbase, const uint32_t (&voff)[
 // residual, one store per output.
 constexpr int MH_LDS = MH_NS * MH_SLICE * 2 + (3 * MH_H + 2 * MH_C + 8) * 4;
 
-template <int AHEAD, bool TRACE>
+// BUF: x1, residual and output addressed as raw buffers (32-bit lane offsets, SGPR row
+// offsets; the host takes it when a field's C x P fp32 plane is below 2 GB)
+template <int AHEAD, bool TRACE, bool BUF>
 __device__ __forceinline__ void mlp_fused_h_tile(const MlpHParams& p, int lin, char* lds_raw) {
   constexpr int W = MH_WAVES, NS = MH_NS;
   constexpr int RING_BYTES = NS * MH_SLICE * 2;
@@ -291,13 +293,24 @@ __device__ __forceinline__ void mlp_fused_h_tile(const MlpHParams& p, int lin, c
   for (int q = 0; q < NS; ++q) issue(q);
 
   // ---- x1 loads, the field's bound B_b = max_c abound (thread tid: channel tid) ------
-  const float* xcol = p.x1 + (int64_t)z * MH_C * P + (px < P ? px : P - 1);
+  const int64_t pxc = px < P ? px : P - 1;
+  const uint32_t P4 = (uint32_t)(P * 4);
   float xv[8][8];
+  if constexpr (BUF) {
+    const auto xr = buf_rsrc(p.x1 + (int64_t)z * MH_C * P, (int64_t)MH_C * P * 4);
+    const uint32_t vo = (uint32_t)(((int64_t)(8 * g) * P + pxc) * 4);
 #pragma unroll
-  for (int ks = 0; ks < 8; ++ks)
+    for (int ks = 0; ks < 8; ++ks)
 #pragma unroll
-    for (int e = 0; e < 8; ++e)
-      xv[ks][e] = __builtin_nontemporal_load(xcol + (int64_t)(32 * ks + 8 * g + e) * P);
+      for (int e = 0; e < 8; ++e) xv[ks][e] = buf_ld_nt(xr, vo, (uint32_t)(32 * ks + e) * P4);
+  } else {
+    const float* xcol = p.x1 + (int64_t)z * MH_C * P + pxc;
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks)
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+        xv[ks][e] = __builtin_nontemporal_load(xcol + (int64_t)(32 * ks + 8 * g + e) * P);
+  }
   float bm = p.abound[(int64_t)z * MH_C + tid];
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) bm = fmaxf(bm, __shfl_xor(bm, o));
@@ -467,8 +480,15 @@ __device__ __forceinline__ void mlp_fused_h_tile(const MlpHParams& p, int lin, c
   // the residual of every output row, all loads in flight at once and under the last
   // two steps' MFMAs (the x1 fragments are dead: their registers take it)
   float rv[16][4];
-  if (p.resid) {
-    const float* rs = p.resid + (int64_t)z * MH_C * P + (px < P ? px : P - 1);
+  if (p.resid && BUF) {
+    const auto rr = buf_rsrc(p.resid + (int64_t)z * MH_C * P, (int64_t)MH_C * P * 4);
+    const uint32_t vo = (uint32_t)(((int64_t)(4 * g) * P + pxc) * 4);
+#pragma unroll
+    for (int ot = 0; ot < 16; ++ot)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) rv[ot][i] = buf_ld_nt(rr, vo, (uint32_t)(16 * ot + i) * P4);
+  } else if (p.resid) {
+    const float* rs = p.resid + (int64_t)z * MH_C * P + pxc;
 #pragma unroll
     for (int ot = 0; ot < 16; ++ot)
 #pragma unroll
@@ -501,6 +521,8 @@ __device__ __forceinline__ void mlp_fused_h_tile(const MlpHParams& p, int lin, c
   // ---- epilogue: unscale + b2 + residual, store (rows 16 ot + 4 g + i) ----------------
   if (px >= P) return;
   float* o = p.out + (int64_t)z * MH_C * P + px;
+  const auto orr = buf_rsrc(p.out + (int64_t)z * MH_C * P, (int64_t)MH_C * P * 4);
+  const uint32_t vo = (uint32_t)(((int64_t)(4 * g) * P + px) * 4);
 #pragma unroll
   for (int ot = 0; ot < 16; ++ot) {
     const int r0 = 16 * ot + 4 * g;
@@ -508,7 +530,11 @@ __device__ __forceinline__ void mlp_fused_h_tile(const MlpHParams& p, int lin, c
     const float4 b = *reinterpret_cast<const float4*>(b2s + r0);
     const float isv[4] = {is.x, is.y, is.z, is.w}, bv[4] = {b.x, b.y, b.z, b.w};
 #pragma unroll
-    for (int i = 0; i < 4; ++i) o[(int64_t)(r0 + i) * P] = fmaf(oacc[ot][i], isv[i], bv[i]) + rv[ot][i];
+    for (int i = 0; i < 4; ++i) {
+      const float v = fmaf(oacc[ot][i], isv[i], bv[i]) + rv[ot][i];
+      if constexpr (BUF) buf_st_nt(v, orr, vo, (uint32_t)(16 * ot + i) * P4);
+      else o[(int64_t)(r0 + i) * P] = v;
+    }
   }
   if constexpr (TRACE) {
     if (tid == 0) p.trace[5 * (int64_t)blockIdx.x + 4] = __builtin_amdgcn_s_memrealtime();
@@ -516,10 +542,10 @@ __device__ __forceinline__ void mlp_fused_h_tile(const MlpHParams& p, int lin, c
 }
 
 // TRACE (MSFNO_MH_TRACE, diagnostic): per-workgroup CU id and phase timestamps
-template <int AHEAD, bool TRACE>
+template <int AHEAD, bool TRACE, bool BUF>
 __global__ __launch_bounds__(256, 2) void mlp_fused_h_kernel(MlpHParams p) {
   __shared__ __attribute__((aligned(16))) char lds_raw[MH_LDS];
-  mlp_fused_h_tile<AHEAD, TRACE>(p, xcd_remap(blockIdx.x, gridDim.x), lds_raw);
+  mlp_fused_h_tile<AHEAD, TRACE, BUF>(p, xcd_remap(blockIdx.x, gridDim.x), lds_raw);
 }
 
 // The fc1 half of mlp_fused_h_kernel with 256 output rows and no hidden layer:
@@ -1163,7 +1189,7 @@ int launch_mlp_fused_h(const float* x1, const float* scale, const float* shift,
     MSFNO_CHECK_HIP(hipMalloc(&tb, (size_t)tiles * 5 * 8));
     MSFNO_CHECK_HIP(hipMemsetAsync(tb, 0, (size_t)tiles * 5 * 8, s));
     p.trace = tb;
-    hipLaunchKernelGGL((mlp_fused_h_kernel<2, true>), dim3((unsigned)tiles), dim3(64 * MH_WAVES), 0, s, p);
+    hipLaunchKernelGGL((mlp_fused_h_kernel<2, true, false>), dim3((unsigned)tiles), dim3(64 * MH_WAVES), 0, s, p);
     MSFNO_TRY(launch_check("mlp_fused_h"));
     std::vector<uint64_t> h((size_t)tiles * 5);
     MSFNO_CHECK_HIP(hipMemcpyAsync(h.data(), tb, h.size() * 8, hipMemcpyDeviceToHost, s));
@@ -1177,8 +1203,17 @@ int launch_mlp_fused_h(const float* x1, const float* scale, const float* shift,
     }
     return MSFNO_OK;
   }
-  // A fragments read two MFMA triples ahead (one or three: equal within 1 %, profiles/r06_i)
-  hipLaunchKernelGGL((mlp_fused_h_kernel<2, false>), dim3((unsigned)tiles), dim3(64 * MH_WAVES), 0, s, p);
+  // A fragments read two MFMA triples ahead (one or three: equal within 1 %, profiles/r06_i).
+  // Raw-buffer addressing of x1 / residual / output when a field's plane is below 2 GB
+  // (MSFNO_MH_BUF=0: 64-bit addresses, A/B)
+  static const bool buf_env = [] {
+    const char* e = getenv("MSFNO_MH_BUF");
+    return !(e && e[0] == '0');
+  }();
+  if (buf_env && (int64_t)MH_C * P * 4 < (1LL << 31))
+    hipLaunchKernelGGL((mlp_fused_h_kernel<2, false, true>), dim3((unsigned)tiles), dim3(64 * MH_WAVES), 0, s, p);
+  else
+    hipLaunchKernelGGL((mlp_fused_h_kernel<2, false, false>), dim3((unsigned)tiles), dim3(64 * MH_WAVES), 0, s, p);
   return launch_check("mlp_fused_h");
 }
 

@@ -256,7 +256,11 @@ __device__ __forceinline__ void mg_glds16x4(uint64_t sbase, const uint32_t (&vof
       : "memory", "scc");
 }
 
-template <int KS, int OT, bool EARLY>
+// BUF: x, x2, addend and output addressed as raw buffers (32-bit lane offsets; channels
+// past Cin / Cin2 and rows past Cout fall outside the plane's range, which the buffer
+// range check (lane offset only: the SGPR offset is not checked) reads as 0 / drops); the
+// host takes it when every plane is below 2 GB and x2 starts on a k-step (Cin % 32 == 0)
+template <int KS, int OT, bool EARLY, bool BUF>
 __global__ __launch_bounds__(256, 2) void mlp_gen_h_kernel(MlpGParams p) {
   constexpr int W = MG_WAVES, NS = MG_NS;
   constexpr int SLICE_E = MG_SLICE * MG_TILE;    // fp16 per slice
@@ -302,16 +306,30 @@ __global__ __launch_bounds__(256, 2) void mlp_gen_h_kernel(MlpGParams p) {
   const float* xb = p.x + (int64_t)z * p.Cin * P + pxc;
   const float* x2b = p.x2 ? p.x2 + (int64_t)z * p.Cin2 * P + pxc : nullptr;
   float xv[KS][8];
+  const uint32_t P4 = (uint32_t)(P * 4);
+  if constexpr (BUF) {
+    const auto xr = buf_rsrc(p.x + (int64_t)z * p.Cin * P, (int64_t)p.Cin * P * 4);
+    const auto x2r = buf_rsrc(p.x2 ? p.x2 + (int64_t)z * p.Cin2 * P : p.x, (int64_t)p.Cin2 * P * 4);
+    const uint32_t vo = (uint32_t)(((int64_t)(8 * g) * P + pxc) * 4);
+    const int ks1 = p.Cin >> 5;  // k-steps of x (Cin % 32 == 0 when x2 is given)
 #pragma unroll
-  for (int ks = 0; ks < KS; ++ks)
+    for (int ks = 0; ks < KS; ++ks)
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const int c = 32 * ks + 8 * g + e;
-      float v = 0.f;
-      if (c < p.Cin) v = __builtin_nontemporal_load(xb + (int64_t)c * P);
-      else if (c - p.Cin < p.Cin2) v = __builtin_nontemporal_load(x2b + (int64_t)(c - p.Cin) * P);
-      xv[ks][e] = v;
-    }
+      for (int e = 0; e < 8; ++e)
+        xv[ks][e] = (p.x2 && ks >= ks1) ? buf_ld_nt(x2r, vo + (uint32_t)(32 * (ks - ks1) + e) * P4, 0)
+                                        : buf_ld_nt(xr, vo + (uint32_t)(32 * ks + e) * P4, 0);
+  } else {
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int c = 32 * ks + 8 * g + e;
+        float v = 0.f;
+        if (c < p.Cin) v = __builtin_nontemporal_load(xb + (int64_t)c * P);
+        else if (c - p.Cin < p.Cin2) v = __builtin_nontemporal_load(x2b + (int64_t)(c - p.Cin) * P);
+        xv[ks][e] = v;
+      }
+  }
 
   for (int i = tid; i < H; i += 64 * W) {
     b1s[i] = p.b1[i];
@@ -370,7 +388,14 @@ __global__ __launch_bounds__(256, 2) void mlp_gen_h_kernel(MlpGParams p) {
   // waited with x's, so the two latencies overlap; otherwise under the last unit's MFMAs
   float rv[OT][4];
   auto load_addend = [&]() {
-    if (p.addend) {
+    if (p.addend && BUF) {
+      const auto ar = buf_rsrc(p.addend + (int64_t)z * p.add_bstride, (int64_t)p.Cout * P * 4);
+      const uint32_t vo = (uint32_t)(((int64_t)(4 * g) * P + pxc) * 4);
+#pragma unroll
+      for (int ot = 0; ot < OT; ++ot)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) rv[ot][i] = buf_ld_nt(ar, vo + (uint32_t)(16 * ot + i) * P4, 0);
+    } else if (p.addend) {
       const float* ad = p.addend + (int64_t)z * p.add_bstride + pxc;
 #pragma unroll
       for (int ot = 0; ot < OT; ++ot)
@@ -489,6 +514,8 @@ __global__ __launch_bounds__(256, 2) void mlp_gen_h_kernel(MlpGParams p) {
   // ---- epilogue: unscale + b2 + addend, store (rows 16 ot + 4 g + i) -------------------
   if (px >= P) return;
   float* o = p.out + (int64_t)z * p.Cout * P + px;
+  const auto orr = buf_rsrc(p.out + (int64_t)z * p.Cout * P, (int64_t)p.Cout * P * 4);
+  const uint32_t vo = (uint32_t)(((int64_t)(4 * g) * P + px) * 4);
 #pragma unroll
   for (int ot = 0; ot < OT; ++ot) {
     const int r0 = 16 * ot + 4 * g;
@@ -497,8 +524,11 @@ __global__ __launch_bounds__(256, 2) void mlp_gen_h_kernel(MlpGParams p) {
     const float isv[4] = {is.x * ietap, is.y * ietap, is.z * ietap, is.w * ietap};
     const float bv[4] = {b.x, b.y, b.z, b.w};
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
-      if (r0 + i < p.Cout) o[(int64_t)(r0 + i) * P] = fmaf(oacc[ot][i], isv[i], bv[i]) + rv[ot][i];
+    for (int i = 0; i < 4; ++i) {
+      const float v = fmaf(oacc[ot][i], isv[i], bv[i]) + rv[ot][i];
+      if constexpr (BUF) buf_st_nt(v, orr, vo + (uint32_t)(16 * ot + i) * P4, 0);  // rows past Cout: out of range
+      else if (r0 + i < p.Cout) o[(int64_t)(r0 + i) * P] = v;
+    }
   }
 }
 
@@ -1068,12 +1098,20 @@ int launch_mlp_gen_h(const float* x, const float* xa, const float* xt, const flo
   // the late form
   const char* ee = getenv("MSFNO_MG_EARLY");
   const bool early = !(ee && ee[0] == '0');
-  if (KS == 3 && early)
-    hipLaunchKernelGGL((mlp_gen_h_kernel<3, 16, true>), dim3((unsigned)grid), dim3(64 * MG_WAVES), 0, s, p);
-  else if (KS == 3)
-    hipLaunchKernelGGL((mlp_gen_h_kernel<3, 16, false>), dim3((unsigned)grid), dim3(64 * MG_WAVES), 0, s, p);
-  else
-    hipLaunchKernelGGL((mlp_gen_h_kernel<11, 5, false>), dim3((unsigned)grid), dim3(64 * MG_WAVES), 0, s, p);
+  // raw-buffer addressing (MSFNO_MG_BUF=0: 64-bit addresses, A/B)
+  static const bool buf_env = [] {
+    const char* e = getenv("MSFNO_MG_BUF");
+    return !(e && e[0] == '0');
+  }();
+  const int64_t lim = 1LL << 31;
+  const bool buf = buf_env && (x2 == nullptr || Cin % 32 == 0) && (int64_t)Cin * P * 4 < lim &&
+                   (int64_t)Cin2 * P * 4 < lim && (int64_t)Cout * P * 4 < lim;
+  const dim3 gd((unsigned)grid), bd(64 * MG_WAVES);
+  if (KS == 3 && early && buf) hipLaunchKernelGGL((mlp_gen_h_kernel<3, 16, true, true>), gd, bd, 0, s, p);
+  else if (KS == 3 && early) hipLaunchKernelGGL((mlp_gen_h_kernel<3, 16, true, false>), gd, bd, 0, s, p);
+  else if (KS == 3) hipLaunchKernelGGL((mlp_gen_h_kernel<3, 16, false, false>), gd, bd, 0, s, p);
+  else if (buf) hipLaunchKernelGGL((mlp_gen_h_kernel<11, 5, false, true>), gd, bd, 0, s, p);
+  else hipLaunchKernelGGL((mlp_gen_h_kernel<11, 5, false, false>), gd, bd, 0, s, p);
   return launch_check("mlp_gen_h");
 }
 
