@@ -258,7 +258,7 @@ constexpr int MH_LDS = MH_NS * MH_SLICE * 2 + (3 * MH_H + 2 * MH_C + 8) * 4;
 
 // BUF: x1, residual and output addressed as raw buffers (32-bit lane offsets, SGPR row
 // offsets; the host takes it when a field's C x P fp32 plane is below 2 GB)
-template <int AHEAD, bool TRACE, bool BUF>
+template <int AHEAD, bool TRACE, bool BUF, bool ILV = false>
 __device__ __forceinline__ void mlp_fused_h_tile(const MlpHParams& p, int lin, char* lds_raw) {
   constexpr int W = MH_WAVES, NS = MH_NS;
   constexpr int RING_BYTES = NS * MH_SLICE * 2;
@@ -393,6 +393,20 @@ __device__ __forceinline__ void mlp_fused_h_tile(const MlpHParams& p, int lin, c
     c = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[0], b[1], c, 0, 0, 0);
     c = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[0], b[0], c, 0, 0, 0);
   };
+  // two tiles' triples interleaved (no MFMA reads the accumulator its predecessor writes;
+  // each accumulator sees the same three products in the same order as mfma3)
+  auto mfma3x2 = [](const half8 (&a)[2], const half8 (&b)[2], floatx4& c,
+                    const half8 (&a2)[2], const half8 (&b2)[2], floatx4& c2) {
+    c = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[1], b[0], c, 0, 0, 0);
+    c2 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a2[1], b2[0], c2, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[0], b[1], c, 0, 0, 0);
+    c2 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a2[0], b2[1], c2, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[0], b[0], c, 0, 0, 0);
+    c2 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a2[0], b2[0], c2, 0, 0, 0);
+  };
+  // ILV: the steps issue tile pairs through mfma3x2 (MLP 1.924 -> 1.905 ms in-block, three
+  // interleaved pairs, profiles/r06_p/ab_mfma_pairs.txt; MSFNO_MH_ILV=0 restores the single-tile order)
+  constexpr bool ilv = ILV;
 
   // pair e2 (0..3) of hidden block j in hacc[PAR]: unscale, + b1, GELU(erf), scale, split
   auto conv_pair = [&](int j, int e2, auto par_c) {
@@ -413,11 +427,29 @@ __device__ __forceinline__ void mlp_fused_h_tile(const MlpHParams& p, int lin, c
     constexpr bool CONV = decltype(conv_c)::value;
     using PPrev = std::integral_constant<int, PAR ^ 1>;
     auto aoff = [&](int u, int pl) { return ((pl * 4 + (u >> 1)) * 2 + (u & 1)) * 512 + a_lane; };
-    half8 a[AHEAD + 1][2];
+    half8 a[AHEAD + 2][2];  // (the pair path rotates over AHEAD + 2)
 #pragma unroll
     for (int k = 0; k < AHEAD; ++k)
 #pragma unroll
       for (int pl = 0; pl < 2; ++pl) a[k][pl] = afrag(slot + aoff(k, pl));
+    if constexpr (ilv) {  // tile pairs (u, u + 1): A fragments AHEAD = 2 ahead cover both
+#pragma unroll
+      for (int u = 0; u < 8; u += 2) {
+        mfma3x2(a[u % (AHEAD + 2)], xf[KH * 4 + (u >> 1)], hacc[PAR][0],
+                a[(u + 1) % (AHEAD + 2)], xf[KH * 4 + (u >> 1)], hacc[PAR][1]);
+#pragma unroll
+        for (int k = 0; k < 2; ++k)
+          if (u + k + AHEAD < 8) {
+#pragma unroll
+            for (int pl = 0; pl < 2; ++pl)
+              a[(u + k + AHEAD) % (AHEAD + 2)][pl] = afrag(slot + aoff(u + k + AHEAD, pl));
+          }
+        if (u == 0) refill(q);
+        if constexpr (CONV) {
+          if (u == 2 || u == 6) conv_pair(jc, 2 * KH + (u >> 2), PPrev{});
+        }
+      }
+    } else {
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
       if (u + AHEAD < 8) {
@@ -431,6 +463,7 @@ __device__ __forceinline__ void mlp_fused_h_tile(const MlpHParams& p, int lin, c
         if (u == 2 || u == 6) conv_pair(jc, 2 * KH + (u >> 2), PPrev{});
       }
     }
+    }
     if constexpr (CONV && KH == 1) {
 #pragma unroll
       for (int t = 0; t < 2; ++t) hacc[PAR ^ 1][t] = floatx4{0.f, 0.f, 0.f, 0.f};
@@ -441,11 +474,25 @@ __device__ __forceinline__ void mlp_fused_h_tile(const MlpHParams& p, int lin, c
     auto aoff = [&](int u, int pl) { return (pl * 8 + u) * 512 + a_lane; };
     const half8 hb[2] = {mh_frag(hfu[0][0], hfu[0][1], hfu[0][2], hfu[0][3]),
                          mh_frag(hfu[1][0], hfu[1][1], hfu[1][2], hfu[1][3])};
-    half8 a[AHEAD + 1][2];
+    half8 a[AHEAD + 2][2];  // (the pair path rotates over AHEAD + 2)
 #pragma unroll
     for (int k = 0; k < AHEAD; ++k)
 #pragma unroll
       for (int pl = 0; pl < 2; ++pl) a[k][pl] = afrag(slot + aoff(k, pl));
+    if constexpr (ilv) {
+#pragma unroll
+      for (int u = 0; u < 8; u += 2) {
+        mfma3x2(a[u % (AHEAD + 2)], hb, oacc[OH * 8 + u], a[(u + 1) % (AHEAD + 2)], hb, oacc[OH * 8 + u + 1]);
+#pragma unroll
+        for (int k = 0; k < 2; ++k)
+          if (u + k + AHEAD < 8) {
+#pragma unroll
+            for (int pl = 0; pl < 2; ++pl)
+              a[(u + k + AHEAD) % (AHEAD + 2)][pl] = afrag(slot + aoff(u + k + AHEAD, pl));
+          }
+        if (u == 0) refill(q);
+      }
+    } else {
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
       if (u + AHEAD < 8) {
@@ -455,6 +502,7 @@ __device__ __forceinline__ void mlp_fused_h_tile(const MlpHParams& p, int lin, c
       }
       mfma3(a[u % (AHEAD + 1)], hb, oacc[OH * 8 + u]);
       if (u == 0) refill(q);
+    }
     }
   };
 
@@ -542,10 +590,10 @@ __device__ __forceinline__ void mlp_fused_h_tile(const MlpHParams& p, int lin, c
 }
 
 // TRACE (MSFNO_MH_TRACE, diagnostic): per-workgroup CU id and phase timestamps
-template <int AHEAD, bool TRACE, bool BUF>
+template <int AHEAD, bool TRACE, bool BUF, bool ILV = false>
 __global__ __launch_bounds__(256, 2) void mlp_fused_h_kernel(MlpHParams p) {
   __shared__ __attribute__((aligned(16))) char lds_raw[MH_LDS];
-  mlp_fused_h_tile<AHEAD, TRACE, BUF>(p, xcd_remap(blockIdx.x, gridDim.x), lds_raw);
+  mlp_fused_h_tile<AHEAD, TRACE, BUF, ILV>(p, xcd_remap(blockIdx.x, gridDim.x), lds_raw);
 }
 
 // The fc1 half of mlp_fused_h_kernel with 256 output rows and no hidden layer:
@@ -1210,7 +1258,13 @@ int launch_mlp_fused_h(const float* x1, const float* scale, const float* shift,
     const char* e = getenv("MSFNO_MH_BUF");
     return !(e && e[0] == '0');
   }();
-  if (buf_env && (int64_t)MH_C * P * 4 < (1LL << 31))
+  static const bool ilv_env = [] {
+    const char* e = getenv("MSFNO_MH_ILV");
+    return !(e && e[0] == '0');
+  }();
+  if (buf_env && (int64_t)MH_C * P * 4 < (1LL << 31) && ilv_env)
+    hipLaunchKernelGGL((mlp_fused_h_kernel<2, false, true, true>), dim3((unsigned)tiles), dim3(64 * MH_WAVES), 0, s, p);
+  else if (buf_env && (int64_t)MH_C * P * 4 < (1LL << 31))
     hipLaunchKernelGGL((mlp_fused_h_kernel<2, false, true>), dim3((unsigned)tiles), dim3(64 * MH_WAVES), 0, s, p);
   else
     hipLaunchKernelGGL((mlp_fused_h_kernel<2, false, false>), dim3((unsigned)tiles), dim3(64 * MH_WAVES), 0, s, p);

@@ -896,12 +896,14 @@ __global__ __launch_bounds__(64 * GP_W, 1) void mlp_gen_hp_kernel(MlpGParams p) 
 #pragma unroll
             for (int pg = 0; pg < 2; ++pg) oacc[ot & 1][pg] = floatx4{0.f, 0.f, 0.f, 0.f};
           }
+          half8 hb[2][2];
 #pragma unroll
           for (int pg = 0; pg < 2; ++pg) {
-            const half8 hb[2] = {mg_frag(hf[u][pg][0][0], hf[u][pg][0][1], hf[u][pg][0][2], hf[u][pg][0][3]),
-                                 mg_frag(hf[u][pg][1][0], hf[u][pg][1][1], hf[u][pg][1][2], hf[u][pg][1][3])};
-            mfma3(av, hb, oacc[ot & 1][pg]);
+            hb[pg][0] = mg_frag(hf[u][pg][0][0], hf[u][pg][0][1], hf[u][pg][0][2], hf[u][pg][0][3]);
+            hb[pg][1] = mg_frag(hf[u][pg][1][0], hf[u][pg][1][1], hf[u][pg][1][2], hf[u][pg][1][3]);
           }
+#pragma unroll
+          for (int pg = 0; pg < 2; ++pg) mfma3(av, hb[pg], oacc[ot & 1][pg]);
         }
         if constexpr (EPI && u == 1) {
           if (epi) {
@@ -1085,6 +1087,8 @@ int launch_mlp_gen_h(const float* x, const float* xa, const float* xt, const flo
     // ring depth 4 (5 and 6 measured equal with the x pieces in the ring slots,
     // profiles/r06_l; with the x buffer only 4 fits)
     const dim3 gd((unsigned)grid), bd(64 * GP_W);
+    // (the two pixel groups' MFMA triples interleaved: equal, 132.0 / 132.0 vs 132.0 /
+    // 131.5 steps/s, profiles/r06_p/ab_mfma_pairs.txt)
     if (addend) hipLaunchKernelGGL((mlp_gen_hp_kernel<3, 16, true, 4>), gd, bd, 0, s, p);
     else hipLaunchKernelGGL((mlp_gen_hp_kernel<3, 16, false, 4>), gd, bd, 0, s, p);
     return launch_check("mlp_gen_hp");
