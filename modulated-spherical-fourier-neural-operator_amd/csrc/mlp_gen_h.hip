@@ -561,35 +561,39 @@ __global__ __launch_bounds__(256, 2) void mlp_gen_h_kernel(MlpGParams p) {
 // in between (GpShape::younger, compile-time per step).  Groups 0..NS-2 are drained in
 // the prologue; the last tile issues dummy groups (its own slices and pieces again) and
 // the kernel drains every DMA before it exits.
-constexpr int GP_W = 4;                        // waves, one per SIMD
-constexpr int GP_PX = 32 * GP_W;               // 128 pixels per tile
+constexpr int GP_PX = 128;                     // pixels per tile
 constexpr int GP_HB = 8;                       // hidden blocks of 32 (H = 256)
 constexpr int GP_WB = MG_SLICE * MG_TILE * 2;  // 16 KB of weight tiles per slice
-constexpr int GP_SLOT = GP_WB + GP_W * 2048;   // + one 2-KB piece per wave
-constexpr int GP_ERS = 36;                     // epilogue patch row stride (floats)
-constexpr int GP_EPI = 16 * GP_ERS * 4;        // per wave: 16 rows x 32 pixels
+constexpr int GP_SLOT = GP_WB + 8 * 1024;      // + the waves' addend pieces (8 KB)
 
-template <int KS, int OT, bool ADD, int NS_>
+// PG 16-pixel groups per wave, W = 8 / PG waves: PG = 2 -> one wave per SIMD with the
+// whole register file, each A fragment read feeding two MFMA triples; PG = 1 -> two waves
+// per SIMD (256 registers each), one wave's VALU, LDS and barrier time under the other's
+// MFMAs.  A wave's piece (x or addend) is 16 rows x 16 PG pixels: PG KB, PG DMAs.
+template <int KS, int OT, bool ADD, int NS_, int PG_>
 struct GpShape {
-  static constexpr int NS = NS_;  // ring slots
+  static constexpr int NS = NS_, PG = PG_, W = 8 / PG_;
   static constexpr int HB = GP_HB, NT1 = 2 * KS, NF = NT1 * HB;
   static constexpr int NQ1 = NF / MG_SLICE;  // fc1 steps
   static constexpr int NQ = NQ1 + OT;        // steps per tile
   static constexpr int CP = 16 * OT;
-  // the next tile's x: 2 KS pieces (16 channels x 32 pixels per wave), carried by the
-  // groups of steps XS .. XS + 2 KS - 1 (issued in this tile's first steps, after the
-  // previous tile's x left the buffer) into a per-wave buffer read at the tile's end
-  static constexpr int XS = NS - 1, NXP = 2 * KS, XW = NXP * 2048;
-  static constexpr int LDS = NS * GP_SLOT + GP_W * XW + GP_W * GP_EPI + (3 * 32 * HB + 2 * CP) * 4;
+  static constexpr int WD = 16 / W;          // weight DMAs per wave and slice (1 KB each)
+  static constexpr int ERS = 16 * PG + 4;    // epilogue patch row stride (floats)
+  static constexpr int EPI = 16 * ERS * 4;   // per wave: 16 rows x 16 PG pixels
+  // the next tile's x: 2 KS pieces (16 channels) per wave, carried by the groups of steps
+  // XS .. XS + 2 KS - 1 (issued in this tile's first steps, after the previous tile's x
+  // left the buffer) into a per-wave buffer read at the tile's end
+  static constexpr int XS = NS - 1, NXP = 2 * KS, XW = NXP * PG * 1024;
+  static constexpr int LDS = NS * GP_SLOT + W * XW + W * EPI + (3 * 32 * HB + 2 * CP) * 4;
   static_assert(NF % MG_SLICE == 0 && XS + NXP < NQ, "x pieces land before the tile's end");
   static_assert(OT % 2 == 0, "output tiles alternate between two accumulators");
   static_assert(LDS <= 160 * 1024, "mlp_gen_hp LDS");
-  static_assert(NS >= 3, "ring depth");
+  static_assert(NS >= 3 && (PG == 1 || PG == 2), "ring depth, pixel groups");
   __host__ __device__ static constexpr int md(int a) { return ((a % NQ) + NQ) % NQ; }
   __host__ __device__ static constexpr bool xp(int q) { return q >= XS && q < XS + NXP; }
   __host__ __device__ static constexpr bool ap(int q) { return ADD && q >= NQ1; }
-  __host__ __device__ static constexpr int grp(int q) { return 4 + (xp(q) ? 2 : 0) + (ap(q) ? 2 : 0); }
-  __host__ __device__ static constexpr int sto(int q) { return (q == 0 || q > NQ1) ? 2 : 0; }
+  __host__ __device__ static constexpr int grp(int q) { return WD + (xp(q) ? PG : 0) + (ap(q) ? PG : 0); }
+  __host__ __device__ static constexpr int sto(int q) { return (q == 0 || q > NQ1) ? PG : 0; }
   // vector-memory instructions a wave issues after group q
   __host__ __device__ static constexpr int younger(int q) {
     int k = 0;
@@ -604,14 +608,15 @@ __device__ __forceinline__ void gp_wait_vm() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"i"(N) : "memory");
 }
 
-template <int KS, int OT, bool ADD, int NS_>
-__global__ __launch_bounds__(64 * GP_W, 1) void mlp_gen_hp_kernel(MlpGParams p) {
-  using S = GpShape<KS, OT, ADD, NS_>;
+template <int KS, int OT, bool ADD, int NS_, int PG_>
+__global__ __launch_bounds__(64 * (8 / PG_), 1) void mlp_gen_hp_kernel(MlpGParams p) {
+  using S = GpShape<KS, OT, ADD, NS_, PG_>;
   constexpr int NS = S::NS, HB = S::HB, NT1 = S::NT1, NQ1 = S::NQ1, NQ = S::NQ, CP = S::CP;
+  constexpr int PG = S::PG, W = S::W, ERS = S::ERS;
   __shared__ __attribute__((aligned(16))) char lds[S::LDS];
   char* const xbuf = lds + NS * GP_SLOT;
-  float* const epi_all = reinterpret_cast<float*>(lds + NS * GP_SLOT + GP_W * S::XW);
-  float* const b1s = reinterpret_cast<float*>(lds + NS * GP_SLOT + GP_W * S::XW + GP_W * GP_EPI);
+  float* const epi_all = reinterpret_cast<float*>(lds + NS * GP_SLOT + W * S::XW);
+  float* const b1s = reinterpret_cast<float*>(lds + NS * GP_SLOT + W * S::XW + W * S::EPI);
   float* const is1s = b1s + 32 * HB;
   float* const etas = is1s + 32 * HB;
   float* const b2s = etas + 32 * HB;
@@ -628,12 +633,12 @@ __global__ __launch_bounds__(64 * GP_W, 1) void mlp_gen_hp_kernel(MlpGParams p) 
   const uint32_t ring_lds = lds_addr(lds);
   const uint32_t xbuf_lds = ring_lds + NS * GP_SLOT;
 
-  for (int i = tid; i < 32 * HB; i += 64 * GP_W) {
+  for (int i = tid; i < 32 * HB; i += 64 * W) {
     b1s[i] = p.b1[i];
     is1s[i] = p.is1[i];
     etas[i] = p.eta[i];
   }
-  for (int i = tid; i < CP; i += 64 * GP_W) {
+  for (int i = tid; i < CP; i += 64 * W) {
     b2s[i] = (p.b2 && i < p.Cout) ? p.b2[i] : 0.f;
     is2s[i] = p.is2[i];
   }
@@ -652,13 +657,19 @@ __global__ __launch_bounds__(64 * GP_W, 1) void mlp_gen_hp_kernel(MlpGParams p) 
   };
 
   // ---- DMA groups ----------------------------------------------------------------------
-  uint32_t w_off[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) w_off[i] = (uint32_t)(i * GP_W * 1024 + lane * 16);
-  // piece DMA h2 of this wave: lane l -> LDS byte 16 l of the wave's 1-KB half h2, piece
-  // row R = 8 h2 + (l >> 3), pixel quad l & 7 (x pieces: quad (l & 7) ^ (R & 4), so the
-  // four lane groups reading a piece row hit distinct LDS banks)
-  const int prow0 = lane >> 3, pq = lane & 7;
+  // A piece DMA h2 (0..PG-1) of this wave: lane l -> LDS byte 16 l of the wave's 1-KB
+  // half h2.  Addend pieces: row 8 h2 + (l >> 3) (PG 2) / l >> 2 (PG 1), pixel quad l & 7 /
+  // l & 3 (read back by the same lane).  x pieces: the row / quad order chosen so that the
+  // four lane groups reading a piece row hit distinct LDS banks: PG 2 as the addend with
+  // quad (l & 7) ^ (R & 4); PG 1: position l >> 2 holds row R = 4 (pos & 3) + (pos >> 2).
+  auto xrow_of = [&](int ln, int h2) {  // piece row R of lane ln's x DMA h2
+    if constexpr (PG == 2) return 8 * h2 + (ln >> 3);
+    else { const int pos = ln >> 2; return 4 * (pos & 3) + (pos >> 2); }
+  };
+  auto xquad_of = [&](int ln, int R) {  // pixel quad of lane ln's x DMA
+    if constexpr (PG == 2) return (ln & 7) ^ (R & 4);
+    else return ln & 3;
+  };
   auto issue = [&](uint32_t slot_off, const Tile& tw, const Tile& tx, auto qc) {
     constexpr int Q = decltype(qc)::value;
     // opaque copies: keep the per-step address arithmetic at the step (hoisted to the
@@ -666,45 +677,53 @@ __global__ __launch_bounds__(64 * GP_W, 1) void mlp_gen_hp_kernel(MlpGParams p) 
     uint64_t img = reinterpret_cast<uint64_t>(p.img), xg = reinterpret_cast<uint64_t>(p.x),
              ag = reinterpret_cast<uint64_t>(p.addend);
     asm volatile("" : "+s"(img), "+s"(xg), "+s"(ag));
+    // (and an opaque lane index: the per-lane offsets of 22 steps are not precomputed)
+    int ln = lane;
+    asm volatile("" : "+v"(ln));
     const uint32_t slot = ring_lds + slot_off;
     const uint64_t wsrc = img + (uint64_t)Q * MG_SLICE * MG_TILE * 2 + (uint64_t)wave_u * 1024;
-    mg_glds16x4<GP_W * 1024>(wsrc, w_off, slot + (uint32_t)(wave_u * 1024));
-    const uint32_t pdst = slot + (uint32_t)(GP_WB + wave_u * 2048);
+#pragma unroll
+    for (int i = 0; i < S::WD; ++i)
+      glds16s(wsrc + (uint64_t)(i * W * 1024), (uint32_t)(ln * 16),
+              slot + (uint32_t)(i * W * 1024 + wave_u * 1024));
     if constexpr (S::xp(Q)) {  // 16 channels of tile tx's x
       constexpr int k = Q - S::XS, ks = k >> 1, h = k & 1;
       const uint64_t base = xg + (uint64_t)((int64_t)tx.z * p.Cin * P * 4);
-      const uint32_t xdst = xbuf_lds + (uint32_t)(wave_u * S::XW + k * 2048);
+      const uint32_t xdst = xbuf_lds + (uint32_t)(wave_u * S::XW + k * PG * 1024);
 #pragma unroll
-      for (int h2 = 0; h2 < 2; ++h2) {
-        const int R = 8 * h2 + prow0;
+      for (int h2 = 0; h2 < PG; ++h2) {
+        const int R = xrow_of(ln, h2);
         const int c = min(32 * ks + 8 * (R >> 2) + 4 * h + (R & 3), p.Cin - 1);
-        const int64_t px = min(tx.px0 + 32 * wave + 4 * (pq ^ (R & 4)), P - 4);
+        const int64_t px = min(tx.px0 + 16 * PG * wave + 4 * xquad_of(ln, R), P - 4);
         glds16s(base, (uint32_t)(((int64_t)c * P + px) * 4), xdst + (uint32_t)(h2 * 1024));
       }
     }
     if constexpr (S::ap(Q)) {  // addend rows 16 ot .. + 15 of tile tw
       constexpr int ot = Q - NQ1;
       const uint64_t base = ag + (uint64_t)((int64_t)tw.z * p.add_bstride * 4);
+      const uint32_t pdst = slot + (uint32_t)(GP_WB + wave_u * PG * 1024);
 #pragma unroll
-      for (int h2 = 0; h2 < 2; ++h2) {
-        const int r = min(16 * ot + 8 * h2 + prow0, p.Cout - 1);
-        const int64_t px = min(tw.px0 + 32 * wave + 4 * pq, P - 4);
+      for (int h2 = 0; h2 < PG; ++h2) {
+        const int row = PG == 2 ? 8 * h2 + (ln >> 3) : ln >> 2;
+        const int quad = PG == 2 ? ln & 7 : ln & 3;
+        const int r = min(16 * ot + row, p.Cout - 1);
+        const int64_t px = min(tw.px0 + 16 * PG * wave + 4 * quad, P - 4);
         glds16s(base, (uint32_t)(((int64_t)r * P + px) * 4), pdst + (uint32_t)(h2 * 1024));
       }
     }
   };
 
   // ---- register state --------------------------------------------------------------------
-  half8 xf[2][KS][2];          // this tile's x (B fragments of fc1) [pg][ks][plane]
-  uint32_t hf[HB][2][2][4];    // hidden activation: fc2 B fragments [j][pg][plane][pair]
-  floatx4 hacc[2][2][2];       // fc1 accumulators [block parity][pg][t]
-  floatx4 oacc[2][2];          // fc2 accumulators [output-tile parity][pg]
-  float ixi[2], etap[2], ietap[2], iet_prev[2];
+  half8 xf[PG][KS][2];          // this tile's x (B fragments of fc1) [pg][ks][plane]
+  uint32_t hf[HB][PG][2][4];    // hidden activation: fc2 B fragments [j][pg][plane][pair]
+  floatx4 hacc[2][PG][2];       // fc1 accumulators [block parity][pg][t]
+  floatx4 oacc[2][PG];          // fc2 accumulators [output-tile parity][pg]
+  float ixi[PG], etap[PG], ietap[PG], iet_prev[PG];
 
   // x (per pixel: the range scales, then the fp16x2 split); xv[pg][ks][e] raw, 0 past Cin
-  auto split_x = [&](const float (&xv)[2][KS][8]) {
+  auto split_x = [&](const float (&xv)[PG][KS][8]) {
 #pragma unroll
-    for (int pg = 0; pg < 2; ++pg) {
+    for (int pg = 0; pg < PG; ++pg) {
       float m = 0.f;
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks)
@@ -733,10 +752,10 @@ __global__ __launch_bounds__(64 * GP_W, 1) void mlp_gen_hp_kernel(MlpGParams p) 
     const Tile c0 = tile_of(0), c1 = tile_of(1);
     mg_for<NS - 1>([&](auto qc) { issue((uint32_t)(decltype(qc)::value * GP_SLOT), c0, c1, qc); });
     const float* xb = p.x + (int64_t)c0.z * p.Cin * P;
-    float xr[2][KS][8];
+    float xr[PG][KS][8];
 #pragma unroll
-    for (int pg = 0; pg < 2; ++pg) {
-      const int64_t px = min(c0.px0 + 32 * wave + 16 * pg + r16, P - 1);
+    for (int pg = 0; pg < PG; ++pg) {
+      const int64_t px = min(c0.px0 + 16 * PG * wave + 16 * pg + r16, P - 1);
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks)
 #pragma unroll
@@ -752,14 +771,14 @@ __global__ __launch_bounds__(64 * GP_W, 1) void mlp_gen_hp_kernel(MlpGParams p) 
 #pragma unroll
   for (int a = 0; a < 2; ++a)
 #pragma unroll
-    for (int pg = 0; pg < 2; ++pg) {
+    for (int pg = 0; pg < PG; ++pg) {
 #pragma unroll
       for (int t = 0; t < 2; ++t) hacc[a][pg][t] = floatx4{0.f, 0.f, 0.f, 0.f};
       oacc[a][pg] = floatx4{0.f, 0.f, 0.f, 0.f};
     }
 
   const int a_lane = r16 * 32 + 8 * (g ^ mg_swz(r16));
-  float* const ep = epi_all + wave * 16 * GP_ERS;
+  float* const ep = epi_all + wave * 16 * ERS;
   auto mfma3 = [](const half8 (&a)[2], const half8 (&b)[2], floatx4& c) {
     c = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[1], b[0], c, 0, 0, 0);
     c = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[0], b[1], c, 0, 0, 0);
@@ -778,19 +797,23 @@ __global__ __launch_bounds__(64 * GP_W, 1) void mlp_gen_hp_kernel(MlpGParams p) 
     v = gelu_erf2(v) * f32x2{hs.x * etap[pg], hs.y * etap[pg]};
     mg_split(v.x, v.y, hf[j][pg][0][e2], hf[j][pg][1][e2]);
   };
+  // the conversions of a block: 4 pairs per pixel group, spread over the next block's tiles
+  constexpr int NCONV = 4 * PG;
   // step n's entry (run in step n - 1 under its last two tiles' MFMAs): group n landed
   // for every wave, all reads of step n - 1's slot issued by now complete (so the group
-  // issued in step n may overwrite it), then the x piece and the first two A fragments
-  half8 a[4][2];  // A fragments of tiles u (mod 4); two tiles ahead
+  // issued in step n may overwrite it), then the first two A fragments
+  // A fragments of tiles u (mod NA), AH tiles ahead (PG 1: one ahead, two waves per SIMD
+  // hide the rest; the register budget is 256)
+  constexpr int AH = PG == 1 ? 1 : 2, NA = 2 * AH;
+  half8 a[NA][2];
   auto prep = [&](auto qc, uint32_t slot_off) {
     constexpr int Q = decltype(qc)::value;
     gp_wait_vm<S::younger(Q)>();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
-    const char* slot = lds + slot_off;
-    const unsigned short* ws = reinterpret_cast<const unsigned short*>(slot);
+    const unsigned short* ws = reinterpret_cast<const unsigned short*>(lds + slot_off);
 #pragma unroll
-    for (int k = 0; k < 2; ++k)
+    for (int k = 0; k < AH; ++k)
 #pragma unroll
       for (int pl = 0; pl < 2; ++pl)
         a[k][pl] = *reinterpret_cast<const half8*>(ws + k * MG_TILE + pl * 512 + a_lane);
@@ -798,34 +821,35 @@ __global__ __launch_bounds__(64 * GP_W, 1) void mlp_gen_hp_kernel(MlpGParams p) 
 
   // epilogue in two halves: (1) unscale + b2 into the wave's patch, (2) rows back as 16-B
   // vectors, + the addend piece of aslot, buffer stores
-  auto epi_patch = [&](int ot, const floatx4 (&acc)[2], const float (&iet)[2]) {
+  auto epi_patch = [&](int ot, const floatx4 (&acc)[PG], const float (&iet)[PG]) {
     const int r0 = 16 * ot + 4 * g;
     const float4 is = *reinterpret_cast<const float4*>(is2s + r0);
     const float4 bb = *reinterpret_cast<const float4*>(b2s + r0);
 #pragma unroll
-    for (int pg = 0; pg < 2; ++pg) {
-      float* e0 = ep + (4 * g) * GP_ERS + 16 * pg + r16;
+    for (int pg = 0; pg < PG; ++pg) {
+      float* e0 = ep + (4 * g) * ERS + 16 * pg + r16;
       e0[0] = fmaf(acc[pg][0], is.x * iet[pg], bb.x);
-      e0[GP_ERS] = fmaf(acc[pg][1], is.y * iet[pg], bb.y);
-      e0[2 * GP_ERS] = fmaf(acc[pg][2], is.z * iet[pg], bb.z);
-      e0[3 * GP_ERS] = fmaf(acc[pg][3], is.w * iet[pg], bb.w);
+      e0[ERS] = fmaf(acc[pg][1], is.y * iet[pg], bb.y);
+      e0[2 * ERS] = fmaf(acc[pg][2], is.z * iet[pg], bb.z);
+      e0[3 * ERS] = fmaf(acc[pg][3], is.w * iet[pg], bb.w);
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   };
   auto epi_store = [&](int ot, const Tile& tw, const char* aslot) {
-    // buffer stores: every wave issues both (the vmcnt counts stay exact); a lane past
+    // buffer stores: every wave issues all PG (the vmcnt counts stay exact); a lane past
     // the field's last pixel or row points outside the field's range and is dropped
-    const int64_t pxl = tw.px0 + 32 * wave + 4 * pq;
     const __amdgpu_buffer_rsrc_t orsrc = __builtin_amdgcn_make_buffer_rsrc(
         p.out + (int64_t)tw.z * p.Cout * P, (short)0, (int)((int64_t)p.Cout * P * 4), 0x00020000);
 #pragma unroll
-    for (int k = 0; k < 2; ++k) {
-      const int row = 8 * k + prow0;
-      floatx4 v = *reinterpret_cast<const floatx4*>(ep + row * GP_ERS + 4 * pq);
+    for (int k = 0; k < PG; ++k) {
+      const int row = PG == 2 ? 8 * k + (lane >> 3) : lane >> 2;
+      const int quad = PG == 2 ? lane & 7 : lane & 3;
+      const int64_t pxl = tw.px0 + 16 * PG * wave + 4 * quad;
+      floatx4 v = *reinterpret_cast<const floatx4*>(ep + row * ERS + 4 * quad);
       if constexpr (ADD)
-        v += *reinterpret_cast<const floatx4*>(aslot + GP_WB + wave * 2048 + k * 1024 + lane * 16);
+        v += *reinterpret_cast<const floatx4*>(aslot + GP_WB + wave * PG * 1024 + k * 1024 + lane * 16);
       // (a row past Cout lies past the field's range by itself)
       const uint32_t off = pxl < P ? (uint32_t)(((int64_t)(16 * ot + row) * P + pxl) * 4) : 0x80000000u;
       __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), orsrc, off, 0, 2 /* nt */);
@@ -846,46 +870,45 @@ __global__ __launch_bounds__(64 * GP_W, 1) void mlp_gen_hp_kernel(MlpGParams p) 
       constexpr int Q = decltype(qc)::value;
       constexpr int QN = Q + NS - 1;  // the step whose group this step issues
       asm volatile("" : "+s"(so), "+s"(so_prev));
-      const char* slot = lds + so;
       const char* pslot = lds + so_prev;  // step n - 1
       const uint32_t so_next = so + GP_SLOT == NS * GP_SLOT ? 0u : so + GP_SLOT;
-      const unsigned short* ws = reinterpret_cast<const unsigned short*>(slot);
+      const unsigned short* ws = reinterpret_cast<const unsigned short*>(lds + so);
       // the previous output tile (this tile's, or the last of the previous tile)
       constexpr bool EPI = Q > NQ1 || Q == 0;
       const bool epi = Q > NQ1 || (Q == 0 && tl > 0);
       if constexpr (Q == NQ1) {  // the last hidden block (its MFMAs ran in the last fc1 step)
-        mg_for<8>([&](auto cc) {
+        mg_for<NCONV>([&](auto cc) {
           constexpr int c = decltype(cc)::value;
           conv(std::integral_constant<int, HB - 1>{}, std::integral_constant<int, (c >> 2)>{},
                std::integral_constant<int, (c & 3)>{});
         });
 #pragma unroll
-        for (int pg = 0; pg < 2; ++pg)
+        for (int pg = 0; pg < PG; ++pg)
 #pragma unroll
           for (int t = 0; t < 2; ++t) hacc[(HB - 1) & 1][pg][t] = floatx4{0.f, 0.f, 0.f, 0.f};
       }
       mg_for<MG_SLICE>([&](auto uc) {
         constexpr int u = decltype(uc)::value;
-        if constexpr (u + 2 < MG_SLICE) {
+        if constexpr (u + AH < MG_SLICE) {
 #pragma unroll
           for (int pl = 0; pl < 2; ++pl)
-            a[(u + 2) % 4][pl] = *reinterpret_cast<const half8*>(ws + (u + 2) * MG_TILE + pl * 512 + a_lane);
+            a[(u + AH) % NA][pl] = *reinterpret_cast<const half8*>(ws + (u + AH) * MG_TILE + pl * 512 + a_lane);
         }
-        const half8(&av)[2] = a[u % 4];
+        const half8(&av)[2] = a[u % NA];
         if constexpr (Q < NQ1) {  // fc1 tile f: block j, k-step ks, row half t
           constexpr int f = MG_SLICE * Q + u, j = f / NT1, i = f % NT1;
 #pragma unroll
-          for (int pg = 0; pg < 2; ++pg) mfma3(av, xf[pg][i >> 1], hacc[j & 1][pg][i & 1]);
+          for (int pg = 0; pg < PG; ++pg) mfma3(av, xf[pg][i >> 1], hacc[j & 1][pg][i & 1]);
           if constexpr (j >= 1) {  // block j - 1 converted under block j's tiles
-            mg_for<8>([&](auto cc) {
+            mg_for<NCONV>([&](auto cc) {
               constexpr int c = decltype(cc)::value;
-              if constexpr ((c * NT1) / 8 == i)
+              if constexpr ((c * NT1) / NCONV == i)
                 conv(std::integral_constant<int, j - 1>{}, std::integral_constant<int, (c >> 2)>{},
                      std::integral_constant<int, (c & 3)>{});
             });
-            if constexpr (i == (7 * NT1) / 8) {
+            if constexpr (i == ((NCONV - 1) * NT1) / NCONV) {
 #pragma unroll
-              for (int pg = 0; pg < 2; ++pg)
+              for (int pg = 0; pg < PG; ++pg)
 #pragma unroll
                 for (int t = 0; t < 2; ++t) hacc[(j - 1) & 1][pg][t] = floatx4{0.f, 0.f, 0.f, 0.f};
             }
@@ -894,16 +917,14 @@ __global__ __launch_bounds__(64 * GP_W, 1) void mlp_gen_hp_kernel(MlpGParams p) 
           constexpr int ot = Q - NQ1;
           if constexpr (u == 0) {
 #pragma unroll
-            for (int pg = 0; pg < 2; ++pg) oacc[ot & 1][pg] = floatx4{0.f, 0.f, 0.f, 0.f};
-          }
-          half8 hb[2][2];
-#pragma unroll
-          for (int pg = 0; pg < 2; ++pg) {
-            hb[pg][0] = mg_frag(hf[u][pg][0][0], hf[u][pg][0][1], hf[u][pg][0][2], hf[u][pg][0][3]);
-            hb[pg][1] = mg_frag(hf[u][pg][1][0], hf[u][pg][1][1], hf[u][pg][1][2], hf[u][pg][1][3]);
+            for (int pg = 0; pg < PG; ++pg) oacc[ot & 1][pg] = floatx4{0.f, 0.f, 0.f, 0.f};
           }
 #pragma unroll
-          for (int pg = 0; pg < 2; ++pg) mfma3(av, hb[pg], oacc[ot & 1][pg]);
+          for (int pg = 0; pg < PG; ++pg) {
+            const half8 hb[2] = {mg_frag(hf[u][pg][0][0], hf[u][pg][0][1], hf[u][pg][0][2], hf[u][pg][0][3]),
+                                 mg_frag(hf[u][pg][1][0], hf[u][pg][1][1], hf[u][pg][1][2], hf[u][pg][1][3])};
+            mfma3(av, hb, oacc[ot & 1][pg]);
+          }
         }
         if constexpr (EPI && u == 1) {
           if (epi) {
@@ -930,8 +951,8 @@ __global__ __launch_bounds__(64 * GP_W, 1) void mlp_gen_hp_kernel(MlpGParams p) 
             // the tile's end: the next tile's x (range scales, split; this tile's 1 / etap
             // kept for its last output tile, whose epilogue runs in the next tile's first
             // step), then the next tile's first step
-            iet_prev[0] = ietap[0];
-            iet_prev[1] = ietap[1];
+#pragma unroll
+            for (int pg = 0; pg < PG; ++pg) iet_prev[pg] = ietap[pg];
             if (tl + 1 < ntile) {
               // the next tile's x from the wave's buffer (channels 32 ks + 8 g + e of
               // piece 2 ks + e / 4, row 4 g + e % 4); channels past Cin read 0 (opaque:
@@ -939,21 +960,42 @@ __global__ __launch_bounds__(64 * GP_W, 1) void mlp_gen_hp_kernel(MlpGParams p) 
               int cin = p.Cin;
               asm volatile("" : "+s"(cin));
               const char* xw = xbuf + wave * S::XW;
-              float xr[2][KS][8];
-#pragma unroll
-              for (int pg = 0; pg < 2; ++pg) {
+              auto xval = [&](int pg, int ks, int e8) {
                 const int px = 16 * pg + r16, quad = px >> 2;
+                const int k = 2 * ks + (e8 >> 2), R = 4 * g + (e8 & 3);
+                int off;
+                if constexpr (PG == 2)
+                  off = k * 2048 + (R >> 3) * 1024 + ((R & 7) * 8 + (quad ^ (R & 4))) * 16 + (px & 3) * 4;
+                else
+                  off = k * 1024 + (4 * (e8 & 3) + g) * 64 + px * 4;
+                const float v = *reinterpret_cast<const float*>(xw + off);
+                return 32 * ks + 8 * g + e8 < cin ? v : 0.f;
+              };
+              // two passes over the buffer (range, then split) instead of 24 PG raw
+              // values in registers beside the new fragments
+#pragma unroll
+              for (int pg = 0; pg < PG; ++pg) {
+                float m = 0.f;
 #pragma unroll
                 for (int ks = 0; ks < KS; ++ks)
 #pragma unroll
-                  for (int e8 = 0; e8 < 8; ++e8) {
-                    const int k = 2 * ks + (e8 >> 2), R = 4 * g + (e8 & 3);
-                    const float v = *reinterpret_cast<const float*>(
-                        xw + k * 2048 + (R >> 3) * 1024 + ((R & 7) * 8 + (quad ^ (R & 4))) * 16 + (px & 3) * 4);
-                    xr[pg][ks][e8] = 32 * ks + 8 * g + e8 < cin ? v : 0.f;
-                  }
+                  for (int e8 = 0; e8 < 8; ++e8) m = fmaxf(m, fabsf(xval(pg, ks, e8)));
+                m = fmaxf(m, __shfl_xor(m, 16));
+                m = fmaxf(m, __shfl_xor(m, 32));
+                const float xi = mg_pow2_below(m, 14);
+                etap[pg] = mg_pow2_below(m + 1.f, 14);
+                ixi[pg] = 1.f / xi;
+                ietap[pg] = 1.f / etap[pg];
+#pragma unroll
+                for (int ks = 0; ks < KS; ++ks) {
+                  uint32_t t[2][4];
+#pragma unroll
+                  for (int e = 0; e < 4; ++e)
+                    mg_split(xval(pg, ks, 2 * e) * xi, xval(pg, ks, 2 * e + 1) * xi, t[0][e], t[1][e]);
+#pragma unroll
+                  for (int pl = 0; pl < 2; ++pl) xf[pg][ks][pl] = mg_frag(t[pl][0], t[pl][1], t[pl][2], t[pl][3]);
+                }
               }
-              split_x(xr);
               prep(std::integral_constant<int, 0>{}, so_next);
             }
           }
@@ -1086,11 +1128,26 @@ int launch_mlp_gen_h(const float* x, const float* xa, const float* xt, const flo
     const int grid = (int)std::min<int64_t>(t, cus);  // one workgroup fills a CU
     // ring depth 4 (5 and 6 measured equal with the x pieces in the ring slots,
     // profiles/r06_l; with the x buffer only 4 fits)
-    const dim3 gd((unsigned)grid), bd(64 * GP_W);
+    const dim3 gd((unsigned)grid);
     // (the two pixel groups' MFMA triples interleaved: equal, 132.0 / 132.0 vs 132.0 /
-    // 131.5 steps/s, profiles/r06_p/ab_mfma_pairs.txt)
-    if (addend) hipLaunchKernelGGL((mlp_gen_hp_kernel<3, 16, true, 4>), gd, bd, 0, s, p);
-    else hipLaunchKernelGGL((mlp_gen_hp_kernel<3, 16, false, 4>), gd, bd, 0, s, p);
+    // 131.5 steps/s, profiles/r06_p/ab_mfma_pairs.txt).  MSFNO_MG_PG = 1 / 2: pixel groups
+    // per wave (8 / 4 waves): equal, net 130.1 / 129.9 / 130.0 vs 130.0 / 130.5 / 130.5
+    // steps/s (profiles/r06_q/summary_q.txt).  Phase costs (summary_r.txt, diagnostic builds):
+    // without the GELU 0.16 ms less per net step, without the addend, x or store streams
+    // 0.01-0.05 ms less each; the fc1 steps' VALU forced between their MFMAs
+    // (sched_group_barrier, 2 / 4 / 6 per MFMA) changed nothing (summary_s.txt)
+    static const int pg = [] {
+      const char* e = getenv("MSFNO_MG_PG");
+      return e && e[0] == '1' ? 1 : 2;
+    }();
+    const dim3 bd2(64 * (8 / pg));
+    if (pg == 1) {
+      if (addend) hipLaunchKernelGGL((mlp_gen_hp_kernel<3, 16, true, 4, 1>), gd, bd2, 0, s, p);
+      else hipLaunchKernelGGL((mlp_gen_hp_kernel<3, 16, false, 4, 1>), gd, bd2, 0, s, p);
+    } else {
+      if (addend) hipLaunchKernelGGL((mlp_gen_hp_kernel<3, 16, true, 4, 2>), gd, bd2, 0, s, p);
+      else hipLaunchKernelGGL((mlp_gen_hp_kernel<3, 16, false, 4, 2>), gd, bd2, 0, s, p);
+    }
     return launch_check("mlp_gen_hp");
   }
   p.tiles_per_field = (int)cdiv(P, 16 * MG_WAVES);
