@@ -87,9 +87,9 @@ STAGE_KERNEL_X3H = dict(STAGE_KERNEL_X6, **{
     # MSFNO_SKIP_H=0: gemm_x3)
     "inner_skip": "msfno::(anonymous namespace)::skip_hp_kernel("
                   "msfno::(anonymous namespace)::SkipHPParams)",
-    # (raw-buffer addressing and paired MFMA triples since round 6; the profiles before
-    # it name the same tiling with 64-bit addressing <2, false>, same HBM traffic)
-    "mlp_fused": ("void msfno::(anonymous namespace)::mlp_fused_h_kernel<2, false, true, true>"
+    # (paired MFMA triples since round 6; the profiles before it name the same tiling
+    # and addressing <2, false>, same HBM traffic)
+    "mlp_fused": ("void msfno::(anonymous namespace)::mlp_fused_h_kernel<2, false, false, true>"
                   "(msfno::(anonymous namespace)::MlpHParams)",
                   "void msfno::(anonymous namespace)::mlp_fused_h_kernel<2, false>"
                   "(msfno::(anonymous namespace)::MlpHParams)"),

@@ -933,17 +933,16 @@ int gemm_x3c(const unsigned short* Aw, int co, int ci, const float* Sin, int ldS
     return (e && e[0] == '2') ? 2 : 3;
   }();
   // grids that would not fill the chip twice (the network's 120 x 240 blocks: 57 column
-  // tiles), and the output layer (fp32 rows out), take 64-row tiles of four waves, two
-  // stages, two workgroups per CU: one workgroup's epilogue runs under the other's MFMAs.
-  // Config 2, three interleaved pairs (profiles/r06_t/ab_bm64.txt): output layer 0.239 / 0.234 / 0.231
-  // vs 0.291 / 0.294 / 0.292 ms; the hidden layers lose (0.65 vs 0.54 ms: B read twice as
-  // often).  MSFNO_X3C_BM64=0 keeps the 128-row tiles, 2 takes 64 rows for every layer
+  // tiles) take 64-row tiles of four waves, two stages, two workgroups per CU
+  // (MSFNO_X3C_BM64=0 keeps the 128-row tiles; 2 takes 64 rows for every DMA-fed layer:
+  // hidden layers 0.65 vs 0.54 ms in-block, the output layer no faster once it is timed
+  // beside the same side-stream skip: 0.293 ms with 64 rows in profiles/r06_v vs 0.292
+  // with 128 in profiles/r06_t/ab_bm64.txt)
   static const int bm64_on = [] {
     const char* e = getenv("MSFNO_X3C_BM64");
     return e ? atoi(e) : 1;
   }();
-  if (!Sin && bm64_on &&
-      ((int64_t)p.tiles_m * p.tiles_n * B < 2 * 256 || Sout || bm64_on == 2)) {
+  if (!Sin && bm64_on && ((int64_t)p.tiles_m * p.tiles_n * B < 2 * 256 || bm64_on == 2)) {
     p.tiles_m = p.Mp / 64;
     const dim3 g64(p.tiles_m * p.tiles_n, 1, B);
     if (Y)

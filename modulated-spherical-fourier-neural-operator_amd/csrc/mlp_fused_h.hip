@@ -1252,20 +1252,24 @@ int launch_mlp_fused_h(const float* x1, const float* scale, const float* shift,
     return MSFNO_OK;
   }
   // A fragments read two MFMA triples ahead (one or three: equal within 1 %, profiles/r06_i).
-  // Raw-buffer addressing of x1 / residual / output when a field's plane is below 2 GB
-  // (MSFNO_MH_BUF=0: 64-bit addresses, A/B)
+  // MSFNO_MH_BUF=1: raw-buffer addressing of x1 / residual / output (a field's plane below
+  // 2 GB).  Not the default: as fast (1.96 ms) but 3.98 instead of 3.36 GB of HBM traffic
+  // per launch (profiles/r06_v vs r06_j pmc_traffic.json)
   static const bool buf_env = [] {
     const char* e = getenv("MSFNO_MH_BUF");
-    return !(e && e[0] == '0');
+    return e && e[0] == '1';
   }();
   static const bool ilv_env = [] {
     const char* e = getenv("MSFNO_MH_ILV");
     return !(e && e[0] == '0');
   }();
-  if (buf_env && (int64_t)MH_C * P * 4 < (1LL << 31) && ilv_env)
+  const bool buf = buf_env && (int64_t)MH_C * P * 4 < (1LL << 31);
+  if (buf && ilv_env)
     hipLaunchKernelGGL((mlp_fused_h_kernel<2, false, true, true>), dim3((unsigned)tiles), dim3(64 * MH_WAVES), 0, s, p);
-  else if (buf_env && (int64_t)MH_C * P * 4 < (1LL << 31))
+  else if (buf)
     hipLaunchKernelGGL((mlp_fused_h_kernel<2, false, true>), dim3((unsigned)tiles), dim3(64 * MH_WAVES), 0, s, p);
+  else if (ilv_env)
+    hipLaunchKernelGGL((mlp_fused_h_kernel<2, false, false, true>), dim3((unsigned)tiles), dim3(64 * MH_WAVES), 0, s, p);
   else
     hipLaunchKernelGGL((mlp_fused_h_kernel<2, false, false>), dim3((unsigned)tiles), dim3(64 * MH_WAVES), 0, s, p);
   return launch_check("mlp_fused_h");
