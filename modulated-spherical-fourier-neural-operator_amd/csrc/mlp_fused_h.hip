@@ -617,20 +617,26 @@ struct SkipHParams {
   int tiles_per_field;
 };
 
-// rs[b][c] = 2^(15 - e), max_k |Ws[c][k] / xs[b][k]| = f 2^e; inv_rs = 1 / rs
-// (one 256-thread workgroup per (row, batch): thread k, a max-reduction over the block)
-__global__ __launch_bounds__(256) void sk_scale_kernel(const float* __restrict__ W,
-                                                       const float* __restrict__ xs,
-                                                       float* __restrict__ rs,
-                                                       float* __restrict__ inv_rs) {
+// The per-batch skip weight image in one launch (it was two: the row scales, then the
+// image, 5.6 us each per block and batch at the network's 120 x 240 blocks): one
+// 256-thread workgroup per (row c, batch b).  rs[b][c] = 2^(15 - e) for
+// max_k |Ws[c][k] / xs[b][k]| = f 2^e, inv_rs = 1 / rs; then the row of
+// W' = rs Ws / xs split into fp16x2 in mh_w1_image_kernel's slice layout
+// [b][j][kh][pl][ks][t][r][32] (8 blocks j; thread k < 128 writes the pair 2k, 2k + 1)
+__global__ __launch_bounds__(256) void sk_prep_kernel(const float* __restrict__ W,
+                                                      const float* __restrict__ xs,
+                                                      float* __restrict__ rs,
+                                                      float* __restrict__ inv_rs,
+                                                      unsigned short* __restrict__ img) {
   __shared__ float wmax[4];
   const int b = blockIdx.y, c = blockIdx.x, k = threadIdx.x;
-  float m = fabsf(xs ? W[(int64_t)c * MH_C + k] / xs[(int64_t)b * MH_C + k] : W[(int64_t)c * MH_C + k]);
+  const float* row = W + (int64_t)c * MH_C;
+  const float* xsb = xs ? xs + (int64_t)b * MH_C : nullptr;
+  float m = fabsf(xsb ? row[k] / xsb[k] : row[k]);
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
   if ((k & 63) == 0) wmax[k >> 6] = m;
   __syncthreads();
-  if (k != 0) return;
   m = fmaxf(fmaxf(wmax[0], wmax[1]), fmaxf(wmax[2], wmax[3]));
   float sc = 1.f;
   if (m > 0.f && isfinite(m)) {
@@ -638,41 +644,24 @@ __global__ __launch_bounds__(256) void sk_scale_kernel(const float* __restrict__
     frexpf(m, &e);
     sc = ldexpf(1.f, 15 - e);
   }
-  rs[(int64_t)b * MH_C + c] = sc;
-  inv_rs[(int64_t)b * MH_C + c] = 1.f / sc;
-}
-
-// W' -> [b][j][kh][pl][ks][t][r][32] (mh_w1_image_kernel's slice layout, 8 blocks j)
-__global__ void sk_image_kernel(const float* __restrict__ W, const float* __restrict__ xs,
-                                const float* __restrict__ rs, unsigned short* __restrict__ img) {
-  constexpr int64_t PAIRS = (int64_t)8 * 2 * 4 * 2 * 16 * 16;
-  const int b = blockIdx.y;
-  const float* xsb = xs ? xs + (int64_t)b * MH_C : nullptr;
-  unsigned short* ib = img + (int64_t)b * SK_NSLICE * MH_SLICE;
-  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < PAIRS;
-       e += (int64_t)gridDim.x * blockDim.x) {
-    const int kkp = (int)(e & 15);
-    const int r = (int)((e >> 4) & 15);
-    const int t = (int)((e >> 8) & 1);
-    const int ks = (int)((e >> 9) & 3);
-    const int kh = (int)((e >> 11) & 1);
-    const int j = (int)(e >> 12);
-    const int kk = 2 * kkp;
-    const int g = (kk >> 3) ^ mh_swz(r);
-    const int k = 128 * kh + 32 * ks + 8 * g + (kk & 7);
-    const int row = 32 * j + 16 * t + r;
-    const float* src = W + (int64_t)row * MH_C + k;
-    const float sc = rs[(int64_t)b * MH_C + row];
-    uint32_t t0, t1;
-    if (xsb)
-      split2h(src[0] / xsb[k] * sc, src[1] / xsb[k + 1] * sc, t0, t1);
-    else
-      split2h(src[0] * sc, src[1] * sc, t0, t1);
-    uint32_t* o = reinterpret_cast<uint32_t*>(
-        ib + (int64_t)(j * 2 + kh) * MH_SLICE + ((ks * 2 + t) * 16 + r) * 32 + kk);
-    o[0] = t0;
-    o[MH_PLANE / 2] = t1;
+  if (k == 0) {
+    rs[(int64_t)b * MH_C + c] = sc;
+    inv_rs[(int64_t)b * MH_C + c] = 1.f / sc;
   }
+  if (k >= 128) return;
+  const int k0 = 2 * k;  // the pair (k0, k0 + 1): one kh, ks, 8-channel group
+  const int j = c >> 5, t = (c >> 4) & 1, r = c & 15;
+  const int kh = k0 >> 7, ks = (k0 >> 5) & 3, gq = (k0 >> 3) & 3;
+  const int kk = 8 * (gq ^ mh_swz(r)) + (k0 & 7);  // its stored position in the 32-wide row
+  uint32_t t0, t1;
+  if (xsb)
+    split2h(row[k0] / xsb[k0] * sc, row[k0 + 1] / xsb[k0 + 1] * sc, t0, t1);
+  else
+    split2h(row[k0] * sc, row[k0 + 1] * sc, t0, t1);
+  unsigned short* ib = img + (int64_t)b * SK_NSLICE * MH_SLICE;
+  uint32_t* o = reinterpret_cast<uint32_t*>(ib + (int64_t)(j * 2 + kh) * MH_SLICE + ((ks * 2 + t) * 16 + r) * 32 + kk);
+  o[0] = t0;
+  o[MH_PLANE / 2] = t1;
 }
 
 template <int NS, int MINB>
@@ -1123,10 +1112,8 @@ int launch_skip_h(const float* W, const float* xs, const float* x, float* out, c
   unsigned short* img = static_cast<unsigned short*>(ws);
   float* rs = reinterpret_cast<float*>(img + (int64_t)B * SK_NSLICE * MH_SLICE);
   float* inv_rs = rs + (int64_t)B * MH_C;
-  hipLaunchKernelGGL(sk_scale_kernel, dim3(MH_C, B), dim3(256), 0, s, W, xs, rs, inv_rs);
-  MSFNO_TRY(launch_check("sk_scale"));
-  hipLaunchKernelGGL(sk_image_kernel, dim3(64, B), dim3(256), 0, s, W, xs, rs, img);
-  MSFNO_TRY(launch_check("sk_image"));
+  hipLaunchKernelGGL(sk_prep_kernel, dim3(MH_C, B), dim3(256), 0, s, W, xs, rs, inv_rs, img);
+  MSFNO_TRY(launch_check("sk_prep"));
   SkipHParams p{};
   p.x = x; p.xs = xs; p.out = out; p.img = img; p.inv_rs = inv_rs; p.bias = bias; p.P = P;
   p.tiles_per_field = (int)cdiv(P, 64);
