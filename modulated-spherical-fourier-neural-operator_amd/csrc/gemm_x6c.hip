@@ -951,6 +951,20 @@ int gemm_x3c(const unsigned short* Aw, int co, int ci, const float* Sin, int ldS
       hipLaunchKernelGGL((gemm_x6c_kernel<false, 2, 2, false, 0, 1, 2, 2, 64>), g64, dim3(256), 0, s, p);
     return launch_check("gemm_x3c");
   }
+  // layer 0 (fp32 rows in) on the small grids too: 64-row tiles, 8 waves of 32 x 32 (the
+  // fp32 staging needs 512 threads), two stages, two workgroups per CU: config 3 131.7 /
+  // 132.3 / 132.1 vs 131.3 / 131.8 / 131.5 steps/s (three interleaved pairs,
+  // profiles/r06_ac; MSFNO_X3C_L0_BM64=0 keeps the 128-row tiles)
+  static const bool l0_bm64 = [] {
+    const char* e = getenv("MSFNO_X3C_L0_BM64");
+    return !(e && e[0] == '0');
+  }();
+  if (Sin && l0_bm64 && bm64_on && (int64_t)p.tiles_m * p.tiles_n * B < 2 * 256) {
+    p.tiles_m = p.Mp / 64;
+    const dim3 g64(p.tiles_m * p.tiles_n, 1, B);
+    hipLaunchKernelGGL((gemm_x6c_kernel<true, 2, 4, true, 0, 2, 2, 2, 64>), g64, dim3(512), 0, s, p);
+    return launch_check("gemm_x3c");
+  }
   if (Sin)
     hipLaunchKernelGGL((gemm_x6c_kernel<true, 4, 2, true, 0, 2, 2>), grid, dim3(512), 0, s, p);
   else if (Y && ns == 3)
