@@ -162,14 +162,17 @@ def pmc_traffic(stage):
         tag = os.path.basename(os.path.dirname(path))
         return [int(t) if t.isdigit() else t for t in re.split(r"(\d+)", tag)]
 
+    files = []
     for f in sorted(glob.glob(os.path.join(REPO, "profiles", "*", "pmc_traffic.json")),
                     key=newest_first, reverse=True):
         try:
             with open(f) as fh:
-                ks = json.load(fh)["kernels"]
+                files.append((f, json.load(fh)["kernels"]))
         except (OSError, ValueError, KeyError):
             continue
-        for sy in syms:
+    # the current kernel symbol in any profile first, then the older names of the same kernel
+    for sy in syms:
+        for f, ks in files:
             k = ks.get(sy)
             if k and k.get("hbm_bytes"):
                 return round(k["hbm_bytes"]), os.path.relpath(f, REPO)
