@@ -37,6 +37,8 @@ CASES = [
     (73, 0, 256, 256, 38436, 2, "broadcast", True),
     (73, 0, 256, 256, 38436, 2, None, False),
     (96, 0, 256, 256, 3000, 2, "batched", True),     # Ct = 96: no padded channels
+    (73, 0, 256, 256, 60, 3, "broadcast", True),     # one partial 60-pixel tile per field
+    (73, 0, 256, 250, 3000, 2, "batched", False),    # Cout 250: output rows past Cout dropped
 ]
 # the persistent kernel's cases (mlp_gen_hp_kernel vs mlp_gen_h_kernel, bitwise)
 PCASES = [c for c in CASES if c[1] == 0 and c[4] % 4 == 0]
