@@ -537,27 +537,29 @@ __global__ __launch_bounds__(256, 2) void mlp_gen_h_kernel(MlpGParams p) {
 // mlp_gen_h_kernel runs one 64-pixel tile per workgroup: the x and addend loads, the
 // slice steps and the 4-byte output stores are three phases that every CU enters at
 // nearly the same time (PMC: MFMA busy 19 %, 56 % of wave cycles waiting on memory).
-// Here one workgroup of four waves per CU (one per SIMD, the whole register file) walks a
-// contiguous range of 128-pixel tiles, 32 pixels per wave as two 16-pixel groups, so each
-// A fragment read from LDS feeds two MFMA triples; and the loop order is changed so that
-// no HBM phase is left outside the slice steps:
+// Here one workgroup per CU walks a contiguous range of 128-pixel tiles (PG = 2, the
+// default: four waves, one per SIMD with the whole register file, 32 pixels per wave as
+// two 16-pixel groups, so each A fragment read from LDS feeds two MFMA triples; PG = 1:
+// eight waves of 16 pixels, see GpShape); and the loop order is changed so that no HBM
+// phase is left outside the slice steps:
 //   - fc1 for all 8 hidden blocks first (6 slices), the GELU'd hidden activation of the
 //     whole tile kept in registers as fc2 B fragments (fp16x2 pairs, 128 VGPRs);
 //   - then fc2 one 16-row output tile per slice (the slice holds W2' rows 16 ot..+15 for
 //     all 256 hidden channels), so an output tile is final after its own step: its
 //     epilogue runs in the next step (scaled, + b2, transposed through a per-wave LDS
 //     patch, + addend, 16-B stores of 128-B lines), under that step's MFMAs;
-//   - every ring slot carries, besides its 16-KB weight slice, one 2-KB piece per wave:
-//     in the fc1 steps 16 channels of the NEXT tile's x (raw fp32 into registers; split
-//     at the tile end, when the pixel's range scale over all its channels is known), in
-//     the fc2 steps the 16 addend rows of this tile's output tile (read back by the lane
-//     that stores them).  Each wave's pieces hold only its own pixels.
+//   - the DMA group of a step carries, besides its 16-KB weight slice, PG-KB pieces per
+//     wave: in the first fc1 steps 16 channels of the NEXT tile's x (raw fp32, into a
+//     per-wave LDS buffer that is split into fp16 terms at the tile end, when the pixel's
+//     range scale over all its channels is known), in the fc2 steps the 16 addend rows of
+//     this tile's output tile (into the ring slot, read back by the lane that stores
+//     them).  Each wave's pieces hold only its own pixels.
 // Arithmetic per output element is that of mlp_gen_h_kernel (same MFMA order, same
 // epilogue), so the two kernels agree bit for bit.
 //
-// vmcnt accounting (each wave, in issue order): group n = 4 weight DMAs + 2 piece DMAs
-// when step n has a piece, issued in step n - (NS - 1) after that step's epilogue stores
-// (2 per lane).  The wait for group n counts the stores and groups of the NS - 2 steps
+// vmcnt accounting (each wave, in issue order): group n = WD weight DMAs + PG per piece
+// of step n (GpShape::grp), issued in step n - (NS - 1) after that step's epilogue stores
+// (PG per lane, GpShape::sto).  The wait for group n counts the stores and groups of the NS - 2 steps
 // in between (GpShape::younger, compile-time per step).  Groups 0..NS-2 are drained in
 // the prologue; the last tile issues dummy groups (its own slices and pieces again) and
 // the kernel drains every DMA before it exits.

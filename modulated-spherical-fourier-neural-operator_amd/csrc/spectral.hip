@@ -5,6 +5,7 @@
 //   * weight preparation (complex block expansion, norm/FiLM folding into fc1),
 //   * the linear filter's per-mode complex contraction (HBM weight stream),
 //   * S-layout conversions (reference dense (l,m) / torch.tril_indices order).
+#include <cstring>
 #include <string>
 
 #include "bf16x3.h"
@@ -352,22 +353,73 @@ __device__ __forceinline__ void split_h2(float a, float b, uint32_t& t0, uint32_
   t1 = __builtin_bit_cast(uint32_t, h1);
 }
 
+// Block order of the symmetric transposes (XR): the spectra rows (mmax float2 = 2888 B at
+// 721x1440) and the slab rows start off the 128-B line grid, so two neighbouring tiles
+// share the lines at their common edge; the hardware deals blocks round-robin over the
+// 8 XCDs, which puts neighbours in different L2s, and each fetches the shared line from
+// HBM (PMC: reads 1.5x the algorithmic bytes, profiles/r06_v).  XR = 1 / 2: a 1-D grid
+// whose ids tr_remap makes contiguous per XCD, decoded m-tile fastest (1) or
+// latitude-tile fastest (2: the hardware's own order, but with neighbours in one XCD).
+// XR = 0: the plain 3-D grid.
+__device__ __forceinline__ int tr_remap(int orig, int nwg) {  // = gemm_common.h xcd_remap
+  const int xcd = orig & 7;
+  const int q = nwg >> 3, r = nwg & 7;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
+}
+
+template <int XR>
+__device__ __forceinline__ int3 tr_block(int nx, int ny) {
+  if constexpr (XR == 0) {
+    return make_int3((int)blockIdx.x, (int)blockIdx.y, (int)blockIdx.z);
+  } else if constexpr (XR == 1) {
+    const int lin = tr_remap((int)blockIdx.x, (int)gridDim.x);
+    const int y = lin % ny, r = lin / ny;
+    return make_int3(r % nx, y, r / nx);
+  } else {
+    const int lin = tr_remap((int)blockIdx.x, (int)gridDim.x);
+    const int x = lin % nx, r = lin / nx;
+    return make_int3(x, r % ny, r / ny);
+  }
+}
+
+static dim3 tr_grid(int xr, int nx, int ny, int nz) {
+  return xr ? dim3((unsigned)(nx * ny * nz)) : dim3((unsigned)nx, (unsigned)ny, (unsigned)nz);
+}
+
+// MSFNO_TR_XCD = "<forward><inverse>" block orders (A/B; "00": the plain 3-D grids)
+static int tr_xcd(int which) {
+  static const std::string v = [] {
+    const char* e = getenv("MSFNO_TR_XCD");
+    return std::string(e && strlen(e) == 2 ? e : "22");
+  }();
+  const int d = v[which] - '0';
+  return d >= 0 && d <= 2 ? d : 2;
+}
+
 template <int TKx, int TMx>
+static void fwd_sym4h_launch(const float2* Xn, unsigned short* Xp, int B, int C, const LatGeom& g,
+                             int mmax, const float* nscale, const float* nshift,
+                             const float* lsig, float* isr, const int* perm, int kext,
+                             hipStream_t s);
+
+template <int TKx, int TMx, int XR>
 __global__ __launch_bounds__(256) void transpose_fwd_sym4h_kernel(
     const float2* __restrict__ Xn, unsigned short* __restrict__ Xp, int B, int C,
     LatGeom g, int mmax, const float* __restrict__ nscale, const float* __restrict__ nshift,
-    const float* __restrict__ lsig, float* __restrict__ isr, const int* __restrict__ slab) {
+    const float* __restrict__ lsig, float* __restrict__ isr, const int* __restrict__ slab,
+    int nx, int ny) {
   constexpr int LD = TKx + 4;
   __shared__ __attribute__((aligned(16))) float tile[4 * TMx * LD];  // [h][c][m][k]
-  const int k0 = blockIdx.x * TKx, m0 = blockIdx.y * TMx;
-  const int bc = blockIdx.z;
+  const int3 blk = tr_block<XR>(nx, ny);
+  const int k0 = blk.x * TKx, m0 = blk.y * TMx;
+  const int bc = blk.z;
   const int b = bc / C, c = bc - b * C;
   const float2* src = Xn + (int64_t)bc * g.nlat * mmax;
   const float sc = nscale[bc];
   const float sh = nshift[bc] * kTwoPi;
   const float sig = lsig[bc];
   const int64_t R = 2LL * B * C;
-  if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x < 2)
+  if (blk.x == 0 && blk.y == 0 && threadIdx.x < 2)
     isr[(int64_t)(b * 2 + threadIdx.x) * C + c] = 1.f / sig;
   for (int i = threadIdx.x; i < TKx * TMx; i += 256) {
     const int kk = i / TMx, mm = i - kk * TMx;
@@ -420,9 +472,7 @@ int launch_transpose_fwd_sym_h(const float2* Xn, unsigned short* Xp, int B, int 
   if (!nscale || !nshift || !lsig || !isr || !g.sym || (g.ldke & 7) || (g.ldk & 7) ||
       std::max(g.ldke, g.ldk - g.ldke) > cdiv(g.Ke, 64) * 64)
     return MSFNO_EINVAL;
-  dim3 grid((unsigned)cdiv(g.Ke, 64), (unsigned)cdiv(mmax, 32), (unsigned)(B * C));
-  hipLaunchKernelGGL((transpose_fwd_sym4h_kernel<64, 32>), grid, dim3(256), 0, s, Xn, Xp, B, C,
-                     g, mmax, nscale, nshift, lsig, isr, nullptr);
+  fwd_sym4h_launch<64, 32>(Xn, Xp, B, C, g, mmax, nscale, nshift, lsig, isr, nullptr, g.Ke, s);
   return launch_check("transpose_fwd_sym_h");
 }
 
@@ -436,23 +486,42 @@ int launch_band_pack_h(const float2* Xn, unsigned short* send, int B, int C, con
   MSFNO_REQUIRE(g.sym && nscale && nshift && lsig && isr && perm && W % 8 == 0 &&
                     g.ldke == W && g.ldk == 2 * W,
                 MSFNO_EINVAL, "band_pack_h: symmetric band geometry with W % 8 == 0");
-  dim3 grid((unsigned)cdiv(std::max(g.Ke, W), 64), (unsigned)cdiv(mmax, 32), (unsigned)(B * C));
-  hipLaunchKernelGGL((transpose_fwd_sym4h_kernel<64, 32>), grid, dim3(256), 0, s, Xn, send, B, C,
-                     g, mmax, nscale, nshift, lsig, isr, perm);
+  fwd_sym4h_launch<64, 32>(Xn, send, B, C, g, mmax, nscale, nshift, lsig, isr, perm,
+                           std::max(g.Ke, W), s);
   return launch_check("band_pack_h");
 }
 
 template <int TKx, int TMx>
+static void fwd_sym4h_launch(const float2* Xn, unsigned short* Xp, int B, int C, const LatGeom& g,
+                             int mmax, const float* nscale, const float* nshift,
+                             const float* lsig, float* isr, const int* perm, int kext,
+                             hipStream_t s) {
+  const int nx = cdiv(kext, TKx), ny = cdiv(mmax, TMx), xr = tr_xcd(0);
+  const dim3 grid = tr_grid(xr, nx, ny, B * C);
+  if (xr == 1)
+    hipLaunchKernelGGL((transpose_fwd_sym4h_kernel<TKx, TMx, 1>), grid, dim3(256), 0, s, Xn, Xp,
+                       B, C, g, mmax, nscale, nshift, lsig, isr, perm, nx, ny);
+  else if (xr == 2)
+    hipLaunchKernelGGL((transpose_fwd_sym4h_kernel<TKx, TMx, 2>), grid, dim3(256), 0, s, Xn, Xp,
+                       B, C, g, mmax, nscale, nshift, lsig, isr, perm, nx, ny);
+  else
+    hipLaunchKernelGGL((transpose_fwd_sym4h_kernel<TKx, TMx, 0>), grid, dim3(256), 0, s, Xn, Xp,
+                       B, C, g, mmax, nscale, nshift, lsig, isr, perm, nx, ny);
+}
+
+template <int TKx, int TMx, int XR>
 __global__ __launch_bounds__(256) void transpose_inv_sym2_kernel(const float* __restrict__ Yt,
                                                                  float2* __restrict__ Yn, int B,
                                                                  int C, LatGeom g, int mmax,
                                                                  int mact,
-                                                                 const int* __restrict__ slab) {
+                                                                 const int* __restrict__ slab,
+                                                                 int nx, int ny) {
   constexpr int PER = TKx * TMx / 256;
   static_assert(PER * 256 == TKx * TMx, "tile");
   __shared__ float2 tile[TMx][TKx + 1];
-  const int k0 = blockIdx.x * TKx, m0 = blockIdx.y * TMx;
-  const int bc = blockIdx.z;
+  const int3 blk = tr_block<XR>(nx, ny);
+  const int k0 = blk.x * TKx, m0 = blk.y * TMx;
+  const int bc = blk.z;
   const int b = bc / C, c = bc - b * C;
   const int64_t R = 2LL * B * C;
   const int64_t rre = (int64_t)(b * 2 + 0) * C + c;
@@ -629,9 +698,18 @@ static void inv_sym_dispatch(const float* Yt, float2* Yn, int B, int C, const La
     case 1: inv_sym_launch<TK_INV, TM_INV>(Yt, Yn, B, C, g, mmax, mact, perm, s); break;
     case 2: inv_sym_launch<32, 128>(Yt, Yn, B, C, g, mmax, mact, perm, s); break;
     case 4: {
-      dim3 grid((unsigned)cdiv(g.Ke, 32), (unsigned)cdiv(mmax, 128), (unsigned)(B * C));
-      hipLaunchKernelGGL((transpose_inv_sym2_kernel<32, 128>), grid, dim3(256), 0, s, Yt, Yn, B,
-                         C, g, mmax, mact, perm);
+      const int nx = cdiv(g.Ke, 32), ny = cdiv(mmax, 128);
+      const int xr = tr_xcd(1);
+      const dim3 grid = tr_grid(xr, nx, ny, B * C);
+      if (xr == 1)
+        hipLaunchKernelGGL((transpose_inv_sym2_kernel<32, 128, 1>), grid, dim3(256), 0, s, Yt,
+                           Yn, B, C, g, mmax, mact, perm, nx, ny);
+      else if (xr == 2)
+        hipLaunchKernelGGL((transpose_inv_sym2_kernel<32, 128, 2>), grid, dim3(256), 0, s, Yt,
+                           Yn, B, C, g, mmax, mact, perm, nx, ny);
+      else
+        hipLaunchKernelGGL((transpose_inv_sym2_kernel<32, 128, 0>), grid, dim3(256), 0, s, Yt,
+                           Yn, B, C, g, mmax, mact, perm, nx, ny);
       break;
     }
     default: inv_sym_launch<16, 128>(Yt, Yn, B, C, g, mmax, mact, perm, s);
