@@ -402,7 +402,7 @@ static void fwd_sym4h_launch(const float2* Xn, unsigned short* Xp, int B, int C,
                              const float* lsig, float* isr, const int* perm, int kext,
                              hipStream_t s);
 
-template <int TKx, int TMx, int XR>
+template <int TKx, int TMx, int XR, bool PRE>
 __global__ __launch_bounds__(256) void transpose_fwd_sym4h_kernel(
     const float2* __restrict__ Xn, unsigned short* __restrict__ Xp, int B, int C,
     LatGeom g, int mmax, const float* __restrict__ nscale, const float* __restrict__ nshift,
@@ -421,14 +421,10 @@ __global__ __launch_bounds__(256) void transpose_fwd_sym4h_kernel(
   const int64_t R = 2LL * B * C;
   if (blk.x == 0 && blk.y == 0 && threadIdx.x < 2)
     isr[(int64_t)(b * 2 + threadIdx.x) * C + c] = 1.f / sig;
-  for (int i = threadIdx.x; i < TKx * TMx; i += 256) {
-    const int kk = i / TMx, mm = i - kk * TMx;
+  // the tile's values: every load of a thread issued before the first is used (PRE; the
+  // rolled loop kept two 8-B loads per wave in flight), then folded into the LDS tile
+  auto put = [&](int kk, int mm, float2 n, float2 t) {
     const int k = k0 + kk, m = m0 + mm;
-    float2 n = make_float2(0.f, 0.f), t = n;
-    if (k < g.Ke && m < mmax) {
-      n = src[(int64_t)k * mmax + m];
-      if (k < g.nh) t = src[(int64_t)(g.nlat - 1 - k) * mmax + m];
-    }
     const bool pair = k < g.nh;
     const float shm = (m == 0) ? sh : 0.f;
     const float sre = pair ? fmaf(sc, n.x + t.x, 2.f * shm) : (k < g.Ke ? fmaf(sc, n.x, shm) : 0.f);
@@ -437,6 +433,36 @@ __global__ __launch_bounds__(256) void transpose_fwd_sym4h_kernel(
     tile[(1 * TMx + mm) * LD + kk] = sim * sig;
     tile[(2 * TMx + mm) * LD + kk] = pair ? sc * (n.x - t.x) * sig : 0.f;
     tile[(3 * TMx + mm) * LD + kk] = pair ? sc * (n.y - t.y) * sig : 0.f;
+  };
+  auto fetch = [&](int kk, int mm, float2& n, float2& t) {
+    const int k = k0 + kk, m = m0 + mm;
+    n = make_float2(0.f, 0.f);
+    t = n;
+    if (k < g.Ke && m < mmax) {
+      n = src[(int64_t)k * mmax + m];
+      if (k < g.nh) t = src[(int64_t)(g.nlat - 1 - k) * mmax + m];
+    }
+  };
+  if constexpr (PRE) {
+    constexpr int PER = TKx * TMx / 256;
+    static_assert(PER * 256 == TKx * TMx, "tile");
+    float2 nv[PER], tv[PER];
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+      const int i = threadIdx.x + 256 * q;
+      fetch(i / TMx, i % TMx, nv[q], tv[q]);
+    }
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+      const int i = threadIdx.x + 256 * q;
+      put(i / TMx, i % TMx, nv[q], tv[q]);
+    }
+  } else {
+    for (int i = threadIdx.x; i < TKx * TMx; i += 256) {
+      float2 n, t;
+      fetch(i / TMx, i % TMx, n, t);
+      put(i / TMx, i % TMx, n, t);
+    }
   }
   __syncthreads();
   // 8 k per thread: one 16-B store per plane (ldke, ldk are multiples of 8)
@@ -498,15 +524,18 @@ static void fwd_sym4h_launch(const float2* Xn, unsigned short* Xp, int B, int C,
                              hipStream_t s) {
   const int nx = cdiv(kext, TKx), ny = cdiv(mmax, TMx), xr = tr_xcd(0);
   const dim3 grid = tr_grid(xr, nx, ny, B * C);
-  if (xr == 1)
-    hipLaunchKernelGGL((transpose_fwd_sym4h_kernel<TKx, TMx, 1>), grid, dim3(256), 0, s, Xn, Xp,
-                       B, C, g, mmax, nscale, nshift, lsig, isr, perm, nx, ny);
-  else if (xr == 2)
-    hipLaunchKernelGGL((transpose_fwd_sym4h_kernel<TKx, TMx, 2>), grid, dim3(256), 0, s, Xn, Xp,
-                       B, C, g, mmax, nscale, nshift, lsig, isr, perm, nx, ny);
-  else
-    hipLaunchKernelGGL((transpose_fwd_sym4h_kernel<TKx, TMx, 0>), grid, dim3(256), 0, s, Xn, Xp,
-                       B, C, g, mmax, nscale, nshift, lsig, isr, perm, nx, ny);
+  static const bool pre = [] {
+    const char* e = getenv("MSFNO_TR_FWD_PRE");
+    return !(e && e[0] == '0');
+  }();
+#define MSFNO_SYM4H(XR, PRE)                                                                     \
+  hipLaunchKernelGGL((transpose_fwd_sym4h_kernel<TKx, TMx, XR, PRE>), grid, dim3(256), 0, s, Xn, \
+                     Xp, B, C, g, mmax, nscale, nshift, lsig, isr, perm, nx, ny)
+  if (xr == 2 && pre) MSFNO_SYM4H(2, true);
+  else if (xr == 2) MSFNO_SYM4H(2, false);
+  else if (xr == 1) MSFNO_SYM4H(1, false);
+  else MSFNO_SYM4H(0, false);
+#undef MSFNO_SYM4H
 }
 
 template <int TKx, int TMx, int XR>
