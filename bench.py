@@ -98,6 +98,14 @@ STAGE_KERNEL_X3H = dict(STAGE_KERNEL_X6, **{
     "legendre_inv": "msfno::(anonymous namespace)::legendre_x3r_kernel("
                     "msfno::(anonymous namespace)::X3DParams)",
 })
+# the network line (config 3): one encoder and one decoder launch per step, default
+# kernels of the x3h engine at 721 x 1440 (their PMC bytes are summed per step)
+STAGE_KERNEL_X3H["mlp_gen"] = (
+    "void msfno::(anonymous namespace)::mlp_gen_hp_kernel<3, 16, true, 4, 2>"
+    "(msfno::(anonymous namespace)::MlpGParams)",
+    "void msfno::(anonymous namespace)::mlp_gen_h_kernel<11, 5, false, true>"
+    "(msfno::(anonymous namespace)::MlpGParams)")
+
 # the linear filter's weight stream at batch 1 (any engine)
 STAGE_KERNEL_LINEAR = {
     "linear_contract": "void msfno::compl_contract_dma_kernel<2>(float const*, float const*, "
@@ -158,9 +166,13 @@ def pmc_traffic(stage):
     import glob
     import re
 
-    def newest_first(path):  # r01_v10 after r01_v9: compare the numbers, not the text
+    def newest_first(path):  # r01_v10 after r01_v9: compare the numbers, not the text;
+        # a round's closing profile (rNN_end) after every other profile of that round
         tag = os.path.basename(os.path.dirname(path))
-        return [int(t) if t.isdigit() else t for t in re.split(r"(\d+)", tag)]
+        m = re.match(r"r(\d+)_(.*)", tag)
+        rnd, rest = (int(m.group(1)), m.group(2)) if m else (-1, tag)
+        return (rnd, rest.startswith("end"),
+                [(0, int(t), "") if t.isdigit() else (1, 0, t) for t in re.split(r"(\d+)", rest)])
 
     files = []
     for f in sorted(glob.glob(os.path.join(REPO, "profiles", "*", "pmc_traffic.json")),
@@ -170,6 +182,12 @@ def pmc_traffic(stage):
                 files.append((f, json.load(fh)["kernels"]))
         except (OSError, ValueError, KeyError):
             continue
+    if stage == "mlp_gen":  # the network's encoder + decoder launches: both from one profile
+        for f, ks in files:
+            b = [ks.get(sy, {}).get("hbm_bytes") for sy in syms]
+            if all(b):
+                return round(sum(b)), os.path.relpath(f, REPO)
+        return None, None
     # the current kernel symbol in any profile first, then the older names of the same kernel
     for sy in syms:
         for f, ks in files:
@@ -601,8 +619,14 @@ def net_roofline(stages, args, B):
     name, (ms, cnt) = max(known.items(), key=lambda kv: kv[1][0])
     ach = work[name] / (ms / 1000.0) / 1e12
     peak, engine = mfma_peak(name)
+    # HBM bytes per step of the encoder + decoder launches (stored PMC profile; default
+    # kernels at the full grid only)
+    tr, tr_src = (pmc_traffic(name) if name == "mlp_gen" and B == 1 and C == 256 and
+                  args.nlat == 721 and args.nlon == 1440 and cnt == 2 else (None, None))
     return {"bound": "mfma", "achieved": round(ach, 2), "peak": round(peak, 1),
-            "unit": "TFLOP/s", "frac": round(ach / peak, 4), "traffic": None,
+            "unit": "TFLOP/s", "frac": round(ach / peak, 4), "traffic": tr,
+            "traffic_source": (f"stored PMC profile {tr_src} (encoder + decoder per step; "
+                               "not measured in this run)" if tr_src else None),
             "kernel": name, "engine": engine, "launches_per_step": cnt,
             "ms_per_step": round(ms, 4), "work_per_step": f"{work[name] / 1e9:.1f} GFLOP",
             "all_stages_ms": {k: round(v[0], 3) for k, v in
