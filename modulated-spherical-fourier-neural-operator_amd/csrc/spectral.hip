@@ -538,7 +538,10 @@ static void fwd_sym4h_launch(const float2* Xn, unsigned short* Xp, int B, int C,
 #undef MSFNO_SYM4H
 }
 
-template <int TKx, int TMx, int XR>
+// BF: the loads are branch-free (clamped addresses, the values selected afterwards), so a
+// thread's 64 loads are all in flight at once; with the range tests as branches the
+// compiler drained them per branch (33 vmcnt(0) waits, at most 4 loads in flight)
+template <int TKx, int TMx, int XR, bool BF>
 __global__ __launch_bounds__(256) void transpose_inv_sym2_kernel(const float* __restrict__ Yt,
                                                                  float2* __restrict__ Yn, int B,
                                                                  int C, LatGeom g, int mmax,
@@ -556,26 +559,62 @@ __global__ __launch_bounds__(256) void transpose_inv_sym2_kernel(const float* __
   const int64_t rre = (int64_t)(b * 2 + 0) * C + c;
   const int64_t rim = (int64_t)(b * 2 + 1) * C + c;
   float2 yn[PER], ys[PER];
+  if constexpr (BF) {
+    // the slab of every m first (one wait), then all 4 PER loads at clamped addresses;
+    // the empty asm uses each value unconditionally, so the compiler cannot sink a
+    // load into the branch of its range test
+    int slq[PER];
 #pragma unroll
-  for (int q = 0; q < PER; ++q) {
-    const int i = threadIdx.x + 256 * q;
-    const int mm = i / TKx, kk = i - mm * TKx;
-    const int k = k0 + kk, m = m0 + mm;
-    float2 n = make_float2(0.f, 0.f), t = n;
-    const int sl = (m < mact) ? (slab ? slab[m] : m) : -1;
-    if (k < g.Ke && sl >= 0) {
-      const float* srcp = Yt + (int64_t)sl * R * g.ldk;
-      const float2 e = make_float2(srcp[rre * g.ldk + k], srcp[rim * g.ldk + k]);
-      if (k < g.nh) {
-        const float2 o = make_float2(srcp[rre * g.ldk + g.ldke + k], srcp[rim * g.ldk + g.ldke + k]);
-        n = make_float2(e.x + o.x, e.y + o.y);
-        t = make_float2(e.x - o.x, e.y - o.y);
-      } else {
-        n = e;
-      }
+    for (int q = 0; q < PER; ++q) {
+      const int m = m0 + (threadIdx.x + 256 * q) / TKx;
+      slq[q] = (m < mact) ? (slab ? slab[min(m, mact - 1)] : m) : -1;
     }
-    yn[q] = n;
-    ys[q] = t;
+    float er[PER], ei[PER], orr[PER], oi[PER];
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+      const int i = threadIdx.x + 256 * q;
+      const int k = k0 + (i % TKx);
+      const bool ok = k < g.Ke && slq[q] >= 0, pr = ok && k < g.nh;
+      const float* srcp = Yt + (int64_t)(ok ? slq[q] : 0) * R * g.ldk;
+      const int ke = ok ? k : 0, ko = g.ldke + (pr ? k : 0);
+      er[q] = srcp[rre * g.ldk + ke];
+      ei[q] = srcp[rim * g.ldk + ke];
+      orr[q] = srcp[rre * g.ldk + ko];
+      oi[q] = srcp[rim * g.ldk + ko];
+    }
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+      asm volatile("" : "+v"(er[q]), "+v"(ei[q]), "+v"(orr[q]), "+v"(oi[q]));
+      const int i = threadIdx.x + 256 * q;
+      const int k = k0 + (i % TKx);
+      const bool ok = k < g.Ke && slq[q] >= 0, pr = ok && k < g.nh;
+      const float2 e = ok ? make_float2(er[q], ei[q]) : make_float2(0.f, 0.f);
+      const float2 o = pr ? make_float2(orr[q], oi[q]) : make_float2(0.f, 0.f);
+      yn[q] = make_float2(e.x + o.x, e.y + o.y);
+      ys[q] = pr ? make_float2(e.x - o.x, e.y - o.y) : make_float2(0.f, 0.f);
+    }
+  } else {
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+      const int i = threadIdx.x + 256 * q;
+      const int mm = i / TKx, kk = i - mm * TKx;
+      const int k = k0 + kk, m = m0 + mm;
+      float2 n = make_float2(0.f, 0.f), t = n;
+      const int sl = (m < mact) ? (slab ? slab[m] : m) : -1;
+      if (k < g.Ke && sl >= 0) {
+        const float* srcp = Yt + (int64_t)sl * R * g.ldk;
+        const float2 e = make_float2(srcp[rre * g.ldk + k], srcp[rim * g.ldk + k]);
+        if (k < g.nh) {
+          const float2 o = make_float2(srcp[rre * g.ldk + g.ldke + k], srcp[rim * g.ldk + g.ldke + k]);
+          n = make_float2(e.x + o.x, e.y + o.y);
+          t = make_float2(e.x - o.x, e.y - o.y);
+        } else {
+          n = e;
+        }
+      }
+      yn[q] = n;
+      ys[q] = t;
+    }
   }
   float2* dst = Yn + (int64_t)bc * g.nlat * mmax;
 #pragma unroll
@@ -730,14 +769,21 @@ static void inv_sym_dispatch(const float* Yt, float2* Yn, int B, int C, const La
       const int nx = cdiv(g.Ke, 32), ny = cdiv(mmax, 128);
       const int xr = tr_xcd(1);
       const dim3 grid = tr_grid(xr, nx, ny, B * C);
-      if (xr == 1)
-        hipLaunchKernelGGL((transpose_inv_sym2_kernel<32, 128, 1>), grid, dim3(256), 0, s, Yt,
-                           Yn, B, C, g, mmax, mact, perm, nx, ny);
+      static const bool bf = [] {
+        const char* e = getenv("MSFNO_TR_INV_BF");
+        return !(e && e[0] == '0');
+      }();
+      if (xr == 2 && bf)
+        hipLaunchKernelGGL((transpose_inv_sym2_kernel<32, 128, 2, true>), grid, dim3(256), 0, s,
+                           Yt, Yn, B, C, g, mmax, mact, perm, nx, ny);
+      else if (xr == 1)
+        hipLaunchKernelGGL((transpose_inv_sym2_kernel<32, 128, 1, false>), grid, dim3(256), 0, s,
+                           Yt, Yn, B, C, g, mmax, mact, perm, nx, ny);
       else if (xr == 2)
-        hipLaunchKernelGGL((transpose_inv_sym2_kernel<32, 128, 2>), grid, dim3(256), 0, s, Yt,
-                           Yn, B, C, g, mmax, mact, perm, nx, ny);
+        hipLaunchKernelGGL((transpose_inv_sym2_kernel<32, 128, 2, false>), grid, dim3(256), 0, s,
+                           Yt, Yn, B, C, g, mmax, mact, perm, nx, ny);
       else
-        hipLaunchKernelGGL((transpose_inv_sym2_kernel<32, 128, 0>), grid, dim3(256), 0, s, Yt,
+        hipLaunchKernelGGL((transpose_inv_sym2_kernel<32, 128, 0, false>), grid, dim3(256), 0, s, Yt,
                            Yn, B, C, g, mmax, mact, perm, nx, ny);
       break;
     }
