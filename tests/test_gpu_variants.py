@@ -48,6 +48,14 @@ VARIANTS = [
     {"MSFNO_X3F_NS": "2"},
     {"MSFNO_SKIP_H": "0"},
     {"MSFNO_X3C_BM64": "0"},
+    # round 6
+    {"MSFNO_MH_ILV": "0"},
+    {"MSFNO_MH_BUF": "1"},
+    {"MSFNO_X3C_L0_BM64": "0"},
+    {"MSFNO_SKIP_GRID": "2"},
+    {"MSFNO_TR_XCD": "00"},
+    {"MSFNO_TR_XCD": "11"},
+    {"MSFNO_TR_FWD_PRE": "0", "MSFNO_TR_INV_BF": "0"},
 ]
 
 
