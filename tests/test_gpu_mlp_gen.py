@@ -105,18 +105,23 @@ def test_fused_x3h_mlp_matches_fp64_like_x6():
         assert rg < 4 * rx + 1e-7, c
 
 
-def test_persistent_encoder_equals_tile_kernel_bitwise(tmp_path):
-    """mlp_gen_hp_kernel (persistent, pipelined; the default for the encoder shape) does
-    each output element's arithmetic in the order mlp_gen_h_kernel does: the two agree
-    bit for bit (MSFNO_MG_P=0 selects the one-tile-per-workgroup kernel, child process)."""
-    dump = tmp_path / "tile.pt"
-    env = dict(os.environ, MSFNO_MG_P="0")
-    out = subprocess.run([sys.executable, os.path.abspath(__file__), "--dump", str(dump)], env=env,
-                         cwd=HERE, capture_output=True, text=True, timeout=300)
+@pytest.mark.parametrize("env", [{"MSFNO_MG_P": "0"}, {"MSFNO_MG_PG": "1"}, {"MSFNO_MG_EARLY": "0"}],
+                         ids=lambda e: ",".join(f"{k}={v}" for k, v in e.items()))
+def test_kernel_variants_equal_default_bitwise(tmp_path, env):
+    """mlp_gen_hp_kernel (persistent, pipelined; the default for the encoder shape, PCASES)
+    does each output element's arithmetic in the order mlp_gen_h_kernel does, at either
+    pixel-group count, and the tile kernel's early addend loads change no arithmetic: every
+    case agrees bit for bit with the child process's variant (MSFNO_MG_P=0: the
+    one-tile-per-workgroup kernel; MSFNO_MG_PG=1: one 16-pixel group per wave, 8 waves;
+    MSFNO_MG_EARLY=0: the addend loaded under the last unit's MFMAs)."""
+    dump = tmp_path / "variant.pt"
+    out = subprocess.run([sys.executable, os.path.abspath(__file__), "--dump", str(dump)],
+                         env=dict(os.environ, **env), cwd=HERE, capture_output=True, text=True,
+                         timeout=300)
     assert out.returncode == 0, out.stderr[-2000:]
     ref = torch.load(dump, weights_only=True)
-    for i, c in enumerate(PCASES):
-        got = _run(*c, seed=CASES.index(c))[0]
+    for i, c in enumerate(CASES):
+        got = _run(*c, seed=i)[0]
         nd = (got != ref[i]).sum().item()
         print(f"{c[:6]}: {nd} of {got.numel()} differ, max-abs {(got - ref[i]).abs().max().item():.3e}")
         assert nd == 0, c
@@ -176,6 +181,6 @@ if __name__ == "__main__":
     sys.path.insert(0, HERE)
     import conftest  # noqa: F401  (puts the package on sys.path)
     if len(sys.argv) > 2 and sys.argv[1] == "--dump":
-        torch.save([_run(*c, seed=CASES.index(c))[0] for c in PCASES], sys.argv[2])
+        torch.save([_run(*c, seed=i)[0] for i, c in enumerate(CASES)], sys.argv[2])
     else:
         print(json.dumps(_errors()))

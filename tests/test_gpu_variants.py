@@ -56,6 +56,16 @@ VARIANTS = [
     {"MSFNO_TR_XCD": "00"},
     {"MSFNO_TR_XCD": "11"},
     {"MSFNO_TR_FWD_PRE": "0", "MSFNO_TR_INV_BF": "0"},
+    # older switches no test exercised before
+    {"MSFNO_FFT_DMA": "0"},
+    {"MSFNO_FFT_TILE": "1", "MSFNO_NO_SYM": "1"},
+    {"MSFNO_SIDE_PRIO": "normal"},
+    {"MSFNO_SPEC_4M": "1"},
+    {"MSFNO_SPEC_X6": "0", "MSFNO_C3M_TILE": "0"},
+    {"MSFNO_WCACHE": "0"},
+    {"MSFNO_ENGINE": "x6", "MSFNO_MF_SCHED": "0"},
+    {"MSFNO_ENGINE": "x6", "MSFNO_MF_AHEAD": "3"},
+    {"MSFNO_ENGINE": "x6", "MSFNO_X6_TILE": "4"},
 ]
 
 
