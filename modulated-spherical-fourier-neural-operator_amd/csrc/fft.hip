@@ -676,15 +676,22 @@ __global__ __launch_bounds__(64 * WV) void fft_r2c_dma_kernel(const float* __res
         }
       }
     }
-    if (rowstats) {
+    if (rowstats) {  // two-pass mean / M2 over the lane's values held in registers (one LDS pass)
+      constexpr int NV = (H + 63) / 64;
+      float2 v[NV];
       float s = 0.f;
-      for (int n = lane; n < H; n += 64) s += buf[n].x + buf[n].y;
+#pragma unroll
+      for (int j = 0; j < NV; ++j) {
+        const int n = lane + 64 * j;
+        v[j] = (H % 64 == 0 || n < H) ? buf[n] : make_float2(0.f, 0.f);
+        if (H % 64 == 0 || n < H) s += v[j].x + v[j].y;
+      }
       const float mean = wave_sum(s) / (float)N;
       float q = 0.f;
-      for (int n = lane; n < H; n += 64) {
-        const float2 v = buf[n];
-        q += (v.x - mean) * (v.x - mean) + (v.y - mean) * (v.y - mean);
-      }
+#pragma unroll
+      for (int j = 0; j < NV; ++j)
+        if (H % 64 == 0 || lane + 64 * j < H)
+          q += (v[j].x - mean) * (v[j].x - mean) + (v[j].y - mean) * (v[j].y - mean);
       q = wave_sum(q);
       if (lane == 0) rowstats[row] = make_float2(mean, q);
     }
@@ -832,10 +839,15 @@ __global__ __launch_bounds__(64 * WV) void fft_c2r_dma_kernel(const float2* __re
       ps = (int64_t)pp.C * P;
       xq = pp.xp + b * 3 * ps + c * P + lat * N;
     }
+    // the output values stay in registers for the row statistics' second pass (no LDS
+    // write-back and re-read)
+    constexpr int NV4 = (N / 4 + 63) / 64;
+    float4 vout[NV4];
     float s = 0.f;
 #pragma unroll
     for (int j = 0; j < NST; ++j) {
       const int n = lane + 64 * j;
+      if (j < NV4) vout[j] = make_float4(0.f, 0.f, 0.f, 0.f);
       if (n < N / 4) {
         float2 a = buf[2 * n], b = buf[2 * n + 1];
         if constexpr (ADD) {
@@ -846,10 +858,7 @@ __global__ __launch_bounds__(64 * WV) void fft_c2r_dma_kernel(const float2* __re
           a.x = gelu_erf_f(a.x); a.y = gelu_erf_f(a.y);
           b.x = gelu_erf_f(b.x); b.y = gelu_erf_f(b.y);
         }
-        if (ADD || act == 1) {
-          buf[2 * n] = a;
-          buf[2 * n + 1] = b;
-        }
+        if (j < NV4) vout[j] = make_float4(a.x, a.y, b.x, b.y);
         if constexpr (PL) {
           uint32_t a0, a1, a2, b0, b1, b2;
           split2(a.x, a.y, a0, a1, a2);
@@ -865,12 +874,15 @@ __global__ __launch_bounds__(64 * WV) void fft_c2r_dma_kernel(const float2* __re
       }
     }
     if (rowstats) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
       const float mean = wave_sum(s) / (float)N;
       float q = 0.f;
-      for (int n = lane; n < H; n += 64) {
-        const float2 v = buf[n];
-        q += (v.x - mean) * (v.x - mean) + (v.y - mean) * (v.y - mean);
+#pragma unroll
+      for (int j = 0; j < NV4; ++j) {
+        if (lane + 64 * j < N / 4) {
+          const float4 v = vout[j];
+          q += (v.x - mean) * (v.x - mean) + (v.y - mean) * (v.y - mean) +
+               ((v.z - mean) * (v.z - mean) + (v.w - mean) * (v.w - mean));
+        }
       }
       q = wave_sum(q);
       if (lane == 0) rowstats[row] = make_float2(mean, q);
