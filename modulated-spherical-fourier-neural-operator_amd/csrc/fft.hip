@@ -192,9 +192,14 @@ __device__ __forceinline__ void apply_twiddles(float2 (&v)[R], const float2* tw,
 // have returned — they feed the arithmetic) writes the outputs.  LDS accesses
 // of one wavefront are performed in order, so no barrier is needed: each row
 // belongs to exactly one wave.
-template <int R, int IT, bool INV>
+// ST (first pass of the forward transform only): the (mean, M2) of the row's 2 H real
+// values from the inputs the lane has just read, before the butterflies overwrite them:
+// each lane's own two-pass mean / M2 over its registers, combined over the wave with
+// Chan's formula M2 = sum_l (M2_l + n_l (mean_l - mean)^2); no LDS pass of its own.
+template <int R, int IT, bool INV, bool ST = false>
 __device__ __forceinline__ void stockham_pass_inplace(float2* buf, int H, int Ns,
-                                                      const float2* tw, int lane) {
+                                                      const float2* tw, int lane,
+                                                      float2* stats = nullptr) {
   const int nb = H / R;
   const int step = H / (Ns * R);
   float2 v[IT][R];
@@ -205,6 +210,37 @@ __device__ __forceinline__ void stockham_pass_inplace(float2* buf, int H, int Ns
 #pragma unroll
       for (int r = 0; r < R; ++r) v[it][r] = buf[j + r * nb];
     }
+  }
+  if constexpr (ST) {
+    float s = 0.f;
+    int cnt = 0;
+#pragma unroll
+    for (int it = 0; it < IT; ++it) {
+      if (lane + 64 * it < nb) {
+#pragma unroll
+        for (int r = 0; r < R; ++r) s += v[it][r].x + v[it][r].y;
+        cnt += 2 * R;
+      }
+    }
+    const float ml = cnt ? s / (float)cnt : 0.f;
+    float q = 0.f;
+#pragma unroll
+    for (int it = 0; it < IT; ++it) {
+      if (lane + 64 * it < nb) {
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+          q += (v[it][r].x - ml) * (v[it][r].x - ml) + (v[it][r].y - ml) * (v[it][r].y - ml);
+      }
+    }
+    float tot = s;
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) tot += __shfl_xor(tot, o);
+    const float mean = tot / (float)(2 * H);
+    const float d = ml - mean;
+    float m2 = q + (float)cnt * d * d;
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) m2 += __shfl_xor(m2, o);
+    *stats = make_float2(mean, m2);
   }
 #pragma unroll
   for (int it = 0; it < IT; ++it) {
@@ -279,6 +315,19 @@ struct FixedFFT {
                              int lane) {
     int Ns = 1;
     ((stockham_pass_inplace<Rs, pass_iters(H, Rs), INV>(buf, H, Ns, tw, lane), Ns *= Rs), ...);
+  }
+  // the forward transform with the row's (mean, M2) taken in its first pass
+  __device__ __forceinline__ static float2 run_stats(float2* buf, const float2* tw, int lane) {
+    float2 st = make_float2(0.f, 0.f);
+    run_stats_impl<Rs...>(buf, tw, lane, st);
+    return st;
+  }
+  template <int R0, int... Rr>
+  __device__ __forceinline__ static void run_stats_impl(float2* buf, const float2* tw, int lane,
+                                                        float2& st) {
+    stockham_pass_inplace<R0, pass_iters(H, R0), false, true>(buf, H, 1, tw, lane, &st);
+    int Ns = R0;
+    ((stockham_pass_inplace<Rr, pass_iters(H, Rr), false>(buf, H, Ns, tw, lane), Ns *= Rr), ...);
   }
 };
 
@@ -676,26 +725,12 @@ __global__ __launch_bounds__(64 * WV) void fft_r2c_dma_kernel(const float* __res
         }
       }
     }
-    if (rowstats) {  // two-pass mean / M2 over the lane's values held in registers (one LDS pass)
-      constexpr int NV = (H + 63) / 64;
-      float2 v[NV];
-      float s = 0.f;
-#pragma unroll
-      for (int j = 0; j < NV; ++j) {
-        const int n = lane + 64 * j;
-        v[j] = (H % 64 == 0 || n < H) ? buf[n] : make_float2(0.f, 0.f);
-        if (H % 64 == 0 || n < H) s += v[j].x + v[j].y;
-      }
-      const float mean = wave_sum(s) / (float)N;
-      float q = 0.f;
-#pragma unroll
-      for (int j = 0; j < NV; ++j)
-        if (H % 64 == 0 || lane + 64 * j < H)
-          q += (v[j].x - mean) * (v[j].x - mean) + (v[j].y - mean) * (v[j].y - mean);
-      q = wave_sum(q);
-      if (lane == 0) rowstats[row] = make_float2(mean, q);
+    if (rowstats) {  // (mean, M2) from the first FFT pass's registers (stockham_pass_inplace)
+      const float2 st = CL::run_stats(buf, tw, lane);
+      if (lane == 0) rowstats[row] = st;
+    } else {
+      CL::template run<false>(buf, nullptr, f, tw, lane);
     }
-    CL::template run<false>(buf, nullptr, f, tw, lane);
     float2* o = out + row * mmax;
     auto bin = [&](int k) {
       const float2 zk = buf[k % H];
