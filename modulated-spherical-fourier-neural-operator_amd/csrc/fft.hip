@@ -12,6 +12,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdlib>
+#include <type_traits>
 
 #include "bf16x3.h"
 #include "dma.h"
@@ -196,10 +197,17 @@ __device__ __forceinline__ void apply_twiddles(float2 (&v)[R], const float2* tw,
 // values from the inputs the lane has just read, before the butterflies overwrite them:
 // each lane's own two-pass mean / M2 over its registers, combined over the wave with
 // Chan's formula M2 = sum_l (M2_l + n_l (mean_l - mean)^2); no LDS pass of its own.
-template <int R, int IT, bool INV, bool ST = false>
+// LD (first pass only): the pass's inputs come from ld(k) instead of buf[k] (the
+// inverse transform's Hermitian pre-twiddle computed straight from the spectrum row, so
+// the row is not written to buf and read back)
+struct NoLoader {};
+// SO (last pass only): the pass's outputs go to so(it, r, k, value) instead of buf[k] (the
+// inverse transform's output row stored from registers)
+template <int R, int IT, bool INV, bool ST = false, class LD = NoLoader, class SO = NoLoader>
 __device__ __forceinline__ void stockham_pass_inplace(float2* buf, int H, int Ns,
                                                       const float2* tw, int lane,
-                                                      float2* stats = nullptr) {
+                                                      float2* stats = nullptr,
+                                                      const LD& ld = LD{}, const SO& so = SO{}) {
   const int nb = H / R;
   const int step = H / (Ns * R);
   float2 v[IT][R];
@@ -208,7 +216,12 @@ __device__ __forceinline__ void stockham_pass_inplace(float2* buf, int H, int Ns
     const int j = lane + 64 * it;
     if (j < nb) {
 #pragma unroll
-      for (int r = 0; r < R; ++r) v[it][r] = buf[j + r * nb];
+      for (int r = 0; r < R; ++r) {
+        if constexpr (std::is_same<LD, NoLoader>::value)
+          v[it][r] = buf[j + r * nb];
+        else
+          v[it][r] = ld(j + r * nb);
+      }
     }
   }
   if constexpr (ST) {
@@ -250,6 +263,18 @@ __device__ __forceinline__ void stockham_pass_inplace(float2* buf, int H, int Ns
       if (Ns > 1) apply_twiddles<R, INV>(v[it], tw, k * step);
       butterfly<R, INV>(v[it], tw, H);
     }
+  }
+  if constexpr (!std::is_same<SO, NoLoader>::value) {
+#pragma unroll
+    for (int it = 0; it < IT; ++it) {
+      const int j = lane + 64 * it;
+      if (j < nb) {
+        const int base = (j / Ns) * Ns * R + j % Ns;
+#pragma unroll
+        for (int r = 0; r < R; ++r) so(it, r, base + r * Ns, v[it][r]);
+      }
+    }
+    return;
   }
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
 #pragma unroll
@@ -328,6 +353,50 @@ struct FixedFFT {
     stockham_pass_inplace<R0, pass_iters(H, R0), false, true>(buf, H, 1, tw, lane, &st);
     int Ns = R0;
     ((stockham_pass_inplace<Rr, pass_iters(H, Rr), false>(buf, H, Ns, tw, lane), Ns *= Rr), ...);
+  }
+  static constexpr int NPASS = sizeof...(Rs);
+  static constexpr int RADS[NPASS] = {Rs...};
+  static constexpr int RL = RADS[NPASS - 1];            // last radix
+  static constexpr int ITL = pass_iters(H, RL);         // its butterflies per lane
+  // the transform with its first pass reading ld(k) and its last pass handing every
+  // output to so(it, r, k, value) instead of buf (NPASS >= 2); after() runs once the
+  // first pass is done
+  template <bool INV, class LD, class AF, class SO>
+  __device__ __forceinline__ static void run_io(float2* buf, const float2* tw, int lane,
+                                                const LD& ld, const AF& after, const SO& so) {
+    static_assert(NPASS >= 2, "run_io: a first and a last pass");
+    run_io_step<INV, 0>(buf, tw, lane, 1, ld, after, so);
+  }
+  template <bool INV, int I, class LD, class AF, class SO>
+  __device__ __forceinline__ static void run_io_step(float2* buf, const float2* tw, int lane,
+                                                     int Ns, const LD& ld, const AF& after,
+                                                     const SO& so) {
+    constexpr int R = RADS[I];
+    if constexpr (I == 0) {
+      stockham_pass_inplace<R, pass_iters(H, R), INV, false, LD>(buf, H, Ns, tw, lane, nullptr, ld);
+      after();
+    } else if constexpr (I == NPASS - 1) {
+      stockham_pass_inplace<R, pass_iters(H, R), INV, false, NoLoader, SO>(buf, H, Ns, tw, lane,
+                                                                          nullptr, NoLoader{}, so);
+    } else {
+      stockham_pass_inplace<R, pass_iters(H, R), INV>(buf, H, Ns, tw, lane);
+    }
+    if constexpr (I + 1 < NPASS) run_io_step<INV, I + 1>(buf, tw, lane, Ns * R, ld, after, so);
+  }
+  // the transform with its first pass reading ld(k) instead of buf; after() runs once the
+  // first pass is done (its reads of whatever ld reads have returned)
+  template <bool INV, class LD, class AF>
+  __device__ __forceinline__ static void run_loaded(float2* buf, const float2* tw, int lane,
+                                                    const LD& ld, const AF& after) {
+    run_loaded_impl<INV, LD, AF, Rs...>(buf, tw, lane, ld, after);
+  }
+  template <bool INV, class LD, class AF, int R0, int... Rr>
+  __device__ __forceinline__ static void run_loaded_impl(float2* buf, const float2* tw, int lane,
+                                                         const LD& ld, const AF& after) {
+    stockham_pass_inplace<R0, pass_iters(H, R0), INV, false, LD>(buf, H, 1, tw, lane, nullptr, ld);
+    after();
+    int Ns = R0;
+    ((stockham_pass_inplace<Rr, pass_iters(H, Rr), INV>(buf, H, Ns, tw, lane), Ns *= Rr), ...);
   }
 };
 
@@ -820,7 +889,10 @@ __global__ __launch_bounds__(64 * WV) void fft_c2r_dma_kernel(const float2* __re
     issue_y(row0 + stride, 1);
     if constexpr (ADMA) issue_a(row0 + stride, 1);
   }
-  const int nst = NST + (rowstats ? 1 : 0);
+  // store instructions per row: the plane path's NST, or one 8-B store per output of the
+  // last pass's butterflies (every butterfly iteration has an active lane)
+  constexpr int NSTR = PL ? NST : CL::ITL * CL::RL;
+  const int nst = NSTR + (rowstats ? 1 : 0);
   const int na = ADMA ? NCA : 0;
   int i = 0;
   for (int64_t row = row0; row < rows; row += stride, ++i) {
@@ -832,7 +904,8 @@ __global__ __launch_bounds__(64 * WV) void fft_c2r_dma_kernel(const float2* __re
     else
       wait_vmcnt(na + (i >= 1 ? nst : 0));
     const float2* yr = reinterpret_cast<const float2*>(yst + sl * YS) + (((int64_t)row * YB) & 15) / 8;
-    for (int k = lane; k < H; k += 64) {
+    // the Hermitian pre-twiddle of bin k, read by the first FFT pass straight from the Yn slot
+    auto pre = [&](int k) -> float2 {
       float2 xk = k < mmax ? yr[k] : make_float2(0.f, 0.f);
       if (k == 0) xk.y = 0.f;
       const int k2 = H - k;
@@ -842,11 +915,77 @@ __global__ __launch_bounds__(64 * WV) void fft_c2r_dma_kernel(const float2* __re
       const float2 A = cadd(xk, xc);
       const float2 D = csub(xk, xc);
       const float2 T = cmul(cconj(twN[k]), D);
-      buf[k] = make_float2(A.x - T.y, A.y + T.x);
+      return make_float2(A.x - T.y, A.y + T.x);
+    };
+    if constexpr (!PL) {
+      // the last pass hands its outputs over in registers: + skip, activation, 8-B stores
+      // of the row (lanes contiguous), the row statistics from the same registers; the
+      // skip values (AR) are loaded after the first pass, under the middle passes
+      constexpr int RL = CL::RL, ITL = CL::ITL, NsL = H / RL;
+      float2 skv[AR ? ITL : 1][AR ? RL : 1];
+      float2 vo[ITL][RL];
+      float s = 0.f;
+      const float2* a2 = reinterpret_cast<const float2*>(ast + sl * NCA * 1024);
+      float2* x2 = reinterpret_cast<float2*>(x + row * N);
+      auto after = [&]() {
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+        if (AH == 2 ? e2 : e1) issue_y(row + AH * stride, sl);  // this Yn slot was consumed
+        if constexpr (ADMA) {  // skip row landed (counts as in the plane path below)
+          if (AH == 2)
+            wait_vmcnt((e1 ? ncy + na : 0) + (i >= 1 ? nst : 0) + (e2 ? ncy : 0));
+          else
+            wait_vmcnt(e1 ? ncy : 0);
+        }
+        if constexpr (AR) {
+          const float2* g2 = reinterpret_cast<const float2*>(addsrc + row * N);
+#pragma unroll
+          for (int it = 0; it < ITL; ++it)
+#pragma unroll
+            for (int r = 0; r < RL; ++r) {
+              const int j = lane + 64 * it;
+              skv[it][r] = j < NsL ? g2[j + r * NsL] : make_float2(0.f, 0.f);
+            }
+        }
+      };
+      auto so = [&](int it, int r, int k, float2 a) {
+        if constexpr (ADD) {
+          const float2 sv = AR ? skv[AR ? it : 0][AR ? r : 0] : a2[k];
+          a.x += sv.x;
+          a.y += sv.y;
+        }
+        if (act == 1) {
+          a.x = gelu_erf_f(a.x);
+          a.y = gelu_erf_f(a.y);
+        }
+        x2[k] = a;
+        vo[it][r] = a;
+        s += a.x + a.y;
+      };
+      CL::template run_io<true>(buf, tw, lane, pre, after, so);
+      if (rowstats) {
+        const float mean = wave_sum(s) / (float)N;
+        float q = 0.f;
+#pragma unroll
+        for (int it = 0; it < ITL; ++it)
+          if (lane + 64 * it < NsL) {
+#pragma unroll
+            for (int r = 0; r < RL; ++r)
+              q += (vo[it][r].x - mean) * (vo[it][r].x - mean) +
+                   (vo[it][r].y - mean) * (vo[it][r].y - mean);
+          }
+        q = wave_sum(q);
+        if (lane == 0) rowstats[row] = make_float2(mean, q);
+      }
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+      if constexpr (ADMA) {
+        if (AH == 2 ? e2 : e1) issue_a(row + AH * stride, sl);  // this skip slot was consumed
+      }
+      continue;
     }
-    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-    if (AH == 2 ? e2 : e1) issue_y(row + AH * stride, sl);  // this Yn slot was consumed above
-    CL::template run<true>(buf, nullptr, f, tw, lane);
+    CL::template run_loaded<true>(buf, tw, lane, pre, [&]() {
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+      if (AH == 2 ? e2 : e1) issue_y(row + AH * stride, sl);  // this Yn slot was consumed
+    });
     constexpr int NA4 = (N / 4 + 63) / 64;  // skip-row float4 per lane
     float4 areg[AR ? NA4 : 1];
     if constexpr (AR) {  // all of this lane's skip values in flight at once
