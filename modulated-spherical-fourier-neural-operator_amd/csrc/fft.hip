@@ -203,7 +203,11 @@ __device__ __forceinline__ void apply_twiddles(float2 (&v)[R], const float2* tw,
 struct NoLoader {};
 // SO (last pass only): the pass's outputs go to so(it, r, k, value) instead of buf[k] (the
 // inverse transform's output row stored from registers)
-template <int R, int IT, bool INV, bool ST = false, class LD = NoLoader, class SO = NoLoader>
+// SWI / SWO: the pass reads / writes buf through fft_swz (pass 2 -> pass 3 of the
+// 4 x 4 x ... codelets, FixedFFT::SWZ)
+__device__ __forceinline__ int fft_swz(int a) { return a ^ (((a >> 5) & 3) << 2); }
+template <int R, int IT, bool INV, bool ST = false, class LD = NoLoader, class SO = NoLoader,
+          bool SWI = false, bool SWO = false>
 __device__ __forceinline__ void stockham_pass_inplace(float2* buf, int H, int Ns,
                                                       const float2* tw, int lane,
                                                       float2* stats = nullptr,
@@ -217,10 +221,12 @@ __device__ __forceinline__ void stockham_pass_inplace(float2* buf, int H, int Ns
     if (j < nb) {
 #pragma unroll
       for (int r = 0; r < R; ++r) {
-        if constexpr (std::is_same<LD, NoLoader>::value)
-          v[it][r] = buf[j + r * nb];
-        else
+        if constexpr (!std::is_same<LD, NoLoader>::value)
           v[it][r] = ld(j + r * nb);
+        else if constexpr (SWI)
+          v[it][r] = buf[fft_swz(j + r * nb)];
+        else
+          v[it][r] = buf[j + r * nb];
       }
     }
   }
@@ -292,7 +298,7 @@ __device__ __forceinline__ void stockham_pass_inplace(float2* buf, int H, int Ns
               make_float4(v[it][r].x, v[it][r].y, v[it][r + 1].x, v[it][r + 1].y);
       } else {
 #pragma unroll
-        for (int r = 0; r < R; ++r) buf[base + r * Ns] = v[it][r];
+        for (int r = 0; r < R; ++r) buf[SWO ? fft_swz(base + r * Ns) : base + r * Ns] = v[it][r];
       }
     }
   }
@@ -335,68 +341,60 @@ template <int... Rs>
 struct FixedFFT {
   static constexpr int H = (Rs * ...);
   static constexpr int kBufs = 1;
-  template <bool INV>
-  __device__ __forceinline__ static void run(float2* buf, float2*, const struct FFTArgs& f, const float2* tw,
-                             int lane) {
-    int Ns = 1;
-    ((stockham_pass_inplace<Rs, pass_iters(H, Rs), INV>(buf, H, Ns, tw, lane), Ns *= Rs), ...);
-  }
-  // the forward transform with the row's (mean, M2) taken in its first pass
-  __device__ __forceinline__ static float2 run_stats(float2* buf, const float2* tw, int lane) {
-    float2 st = make_float2(0.f, 0.f);
-    run_stats_impl<Rs...>(buf, tw, lane, st);
-    return st;
-  }
-  template <int R0, int... Rr>
-  __device__ __forceinline__ static void run_stats_impl(float2* buf, const float2* tw, int lane,
-                                                        float2& st) {
-    stockham_pass_inplace<R0, pass_iters(H, R0), false, true>(buf, H, 1, tw, lane, &st);
-    int Ns = R0;
-    ((stockham_pass_inplace<Rr, pass_iters(H, Rr), false>(buf, H, Ns, tw, lane), Ns *= Rr), ...);
-  }
   static constexpr int NPASS = sizeof...(Rs);
   static constexpr int RADS[NPASS] = {Rs...};
   static constexpr int RL = RADS[NPASS - 1];            // last radix
   static constexpr int ITL = pass_iters(H, RL);         // its butterflies per lane
-  // the transform with its first pass reading ld(k) and its last pass handing every
-  // output to so(it, r, k, value) instead of buf (NPASS >= 2); after() runs once the
-  // first pass is done
-  template <bool INV, class LD, class AF, class SO>
-  __device__ __forceinline__ static void run_io(float2* buf, const float2* tw, int lane,
-                                                const LD& ld, const AF& after, const SO& so) {
-    static_assert(NPASS >= 2, "run_io: a first and a last pass");
-    run_io_step<INV, 0>(buf, tw, lane, 1, ld, after, so);
+  // pass 2 of a 4 x 4 x ... codelet writes at base + 4 r (base = 16 (j >> 2) + (j & 3)):
+  // for one r, the 8 lane quads of a half-wave fall on 2 bank groups (4-way conflicts);
+  // through fft_swz (bits 2-3 of the index XORed with bits 5-6, a permutation of every
+  // 16-aligned block, so H % 16 == 0) the 8 quads fall on 8 distinct groups.  Pass 3
+  // reads through the same map; every other pass is untouched.
+  static constexpr bool SWZ = NPASS >= 3 && RADS[0] == 4 && RADS[1] == 4 && H % 16 == 0;
+  template <bool INV>
+  __device__ __forceinline__ static void run(float2* buf, float2*, const struct FFTArgs& f, const float2* tw,
+                             int lane) {
+    step<INV, 0, false>(buf, tw, lane, 1, nullptr, NoLoader{}, [] {}, NoLoader{});
   }
-  template <bool INV, int I, class LD, class AF, class SO>
-  __device__ __forceinline__ static void run_io_step(float2* buf, const float2* tw, int lane,
-                                                     int Ns, const LD& ld, const AF& after,
-                                                     const SO& so) {
-    constexpr int R = RADS[I];
-    if constexpr (I == 0) {
-      stockham_pass_inplace<R, pass_iters(H, R), INV, false, LD>(buf, H, Ns, tw, lane, nullptr, ld);
-      after();
-    } else if constexpr (I == NPASS - 1) {
-      stockham_pass_inplace<R, pass_iters(H, R), INV, false, NoLoader, SO>(buf, H, Ns, tw, lane,
-                                                                          nullptr, NoLoader{}, so);
-    } else {
-      stockham_pass_inplace<R, pass_iters(H, R), INV>(buf, H, Ns, tw, lane);
-    }
-    if constexpr (I + 1 < NPASS) run_io_step<INV, I + 1>(buf, tw, lane, Ns * R, ld, after, so);
+  // the forward transform with the row's (mean, M2) taken in its first pass
+  __device__ __forceinline__ static float2 run_stats(float2* buf, const float2* tw, int lane) {
+    float2 st = make_float2(0.f, 0.f);
+    step<false, 0, true>(buf, tw, lane, 1, &st, NoLoader{}, [] {}, NoLoader{});
+    return st;
   }
   // the transform with its first pass reading ld(k) instead of buf; after() runs once the
   // first pass is done (its reads of whatever ld reads have returned)
   template <bool INV, class LD, class AF>
   __device__ __forceinline__ static void run_loaded(float2* buf, const float2* tw, int lane,
                                                     const LD& ld, const AF& after) {
-    run_loaded_impl<INV, LD, AF, Rs...>(buf, tw, lane, ld, after);
+    step<INV, 0, false>(buf, tw, lane, 1, nullptr, ld, after, NoLoader{});
   }
-  template <bool INV, class LD, class AF, int R0, int... Rr>
-  __device__ __forceinline__ static void run_loaded_impl(float2* buf, const float2* tw, int lane,
-                                                         const LD& ld, const AF& after) {
-    stockham_pass_inplace<R0, pass_iters(H, R0), INV, false, LD>(buf, H, 1, tw, lane, nullptr, ld);
-    after();
-    int Ns = R0;
-    ((stockham_pass_inplace<Rr, pass_iters(H, Rr), INV>(buf, H, Ns, tw, lane), Ns *= Rr), ...);
+  // ... and its last pass handing every output to so(it, r, k, value) instead of buf
+  template <bool INV, class LD, class AF, class SO>
+  __device__ __forceinline__ static void run_io(float2* buf, const float2* tw, int lane,
+                                                const LD& ld, const AF& after, const SO& so) {
+    static_assert(NPASS >= 2, "run_io: a first and a last pass");
+    step<INV, 0, false>(buf, tw, lane, 1, nullptr, ld, after, so);
+  }
+  template <bool INV, int I, bool STATS, class LD, class AF, class SO>
+  __device__ __forceinline__ static void step(float2* buf, const float2* tw, int lane, int Ns,
+                                              float2* st, const LD& ld, const AF& after,
+                                              const SO& so) {
+    constexpr int R = RADS[I], IT = pass_iters(H, R);
+    // (forward only: in the inverse kernel, at 4 waves per SIMD, the swizzle's address
+    // arithmetic pushed it past 128 VGPRs into scratch: irfft 0.58 -> 0.66 ms)
+    constexpr bool SWI = SWZ && !INV && I == 2, SWO = SWZ && !INV && I == 1;
+    if constexpr (I == 0 && I == NPASS - 1)
+      stockham_pass_inplace<R, IT, INV, STATS, LD, SO>(buf, H, Ns, tw, lane, st, ld, so);
+    else if constexpr (I == 0)
+      stockham_pass_inplace<R, IT, INV, STATS, LD>(buf, H, Ns, tw, lane, st, ld);
+    else if constexpr (I == NPASS - 1)
+      stockham_pass_inplace<R, IT, INV, false, NoLoader, SO, SWI>(buf, H, Ns, tw, lane, nullptr,
+                                                                  NoLoader{}, so);
+    else
+      stockham_pass_inplace<R, IT, INV, false, NoLoader, NoLoader, SWI, SWO>(buf, H, Ns, tw, lane);
+    if constexpr (I == 0) after();
+    if constexpr (I + 1 < NPASS) step<INV, I + 1, STATS>(buf, tw, lane, Ns * R, st, ld, after, so);
   }
 };
 
