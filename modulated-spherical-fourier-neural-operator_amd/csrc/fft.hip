@@ -370,20 +370,22 @@ struct FixedFFT {
     step<INV, 0, false>(buf, tw, lane, 1, nullptr, ld, after, NoLoader{});
   }
   // ... and its last pass handing every output to so(it, r, k, value) instead of buf
-  template <bool INV, class LD, class AF, class SO>
+  template <bool INV, class LD, class AF, class SO, bool SWINV = false>
   __device__ __forceinline__ static void run_io(float2* buf, const float2* tw, int lane,
                                                 const LD& ld, const AF& after, const SO& so) {
     static_assert(NPASS >= 2, "run_io: a first and a last pass");
-    step<INV, 0, false>(buf, tw, lane, 1, nullptr, ld, after, so);
+    step<INV, 0, false, LD, AF, SO, SWINV>(buf, tw, lane, 1, nullptr, ld, after, so);
   }
-  template <bool INV, int I, bool STATS, class LD, class AF, class SO>
+  template <bool INV, int I, bool STATS, class LD, class AF, class SO, bool SWINV = false>
   __device__ __forceinline__ static void step(float2* buf, const float2* tw, int lane, int Ns,
                                               float2* st, const LD& ld, const AF& after,
                                               const SO& so) {
     constexpr int R = RADS[I], IT = pass_iters(H, R);
-    // (forward only: in the inverse kernel, at 4 waves per SIMD, the swizzle's address
-    // arithmetic pushed it past 128 VGPRs into scratch: irfft 0.58 -> 0.66 ms)
-    constexpr bool SWI = SWZ && !INV && I == 2, SWO = SWZ && !INV && I == 1;
+    // (the forward transform; the inverse only where its kernel asks for it, SWINV: at 4
+    // waves per SIMD the swizzle's address arithmetic pushed the inverse kernel past 128
+    // VGPRs into scratch, irfft 0.58 -> 0.66 ms)
+    constexpr bool SW = SWZ && (!INV || SWINV);
+    constexpr bool SWI = SW && I == 2, SWO = SW && I == 1;
     if constexpr (I == 0 && I == NPASS - 1)
       stockham_pass_inplace<R, IT, INV, STATS, LD, SO>(buf, H, Ns, tw, lane, st, ld, so);
     else if constexpr (I == 0)
@@ -394,7 +396,8 @@ struct FixedFFT {
     else
       stockham_pass_inplace<R, IT, INV, false, NoLoader, NoLoader, SWI, SWO>(buf, H, Ns, tw, lane);
     if constexpr (I == 0) after();
-    if constexpr (I + 1 < NPASS) step<INV, I + 1, STATS>(buf, tw, lane, Ns * R, st, ld, after, so);
+    if constexpr (I + 1 < NPASS)
+      step<INV, I + 1, STATS, LD, AF, SO, SWINV>(buf, tw, lane, Ns * R, st, ld, after, so);
   }
 };
 
@@ -835,7 +838,9 @@ __global__ __launch_bounds__(64 * WV) void fft_r2c_dma_kernel(const float* __res
 // CU matter more than bytes in flight.
 // AR: the skip row is read into registers after the FFT instead of an LDS slot
 // (8.8 instead of 14.8 KB of LDS per wave: more waves per CU)
-template <class CL, bool ADD, int WV, int AH, bool PL, bool AR = false>
+// SWI_: the FFT codelet's pass-2 swizzle in this inverse kernel too (FixedFFT::SWZ; for
+// wave counts that leave the registers it needs)
+template <class CL, bool ADD, int WV, int AH, bool PL, bool AR = false, bool SWI_ = false>
 __global__ __launch_bounds__(64 * WV) void fft_c2r_dma_kernel(const float2* __restrict__ in,
                                                               float* x, const float* addsrc,
                                                               float2* __restrict__ rowstats,
@@ -959,7 +964,8 @@ __global__ __launch_bounds__(64 * WV) void fft_c2r_dma_kernel(const float2* __re
         vo[it][r] = a;
         s += a.x + a.y;
       };
-      CL::template run_io<true>(buf, tw, lane, pre, after, so);
+      CL::template run_io<true, decltype(pre), decltype(after), decltype(so), SWI_>(buf, tw, lane,
+                                                                                pre, after, so);
       if (rowstats) {
         const float mean = wave_sum(s) / (float)N;
         float q = 0.f;
@@ -1381,6 +1387,14 @@ static int launch_r2c(const FFTArgs& a, const float* x, float2* out, float2* row
   return launch_check("fft_r2c_rows");
 }
 
+static bool c2r_swz() {
+  static const bool on = [] {
+    const char* e = getenv("MSFNO_C2R_SWZ");
+    return e && e[0] == '1';
+  }();
+  return on;
+}
+
 template <class CL>
 static int launch_c2r(const FFTArgs& a, const float2* in, float* x, const float* addsrc,
                       float2* rowstats, int64_t rows, int mmax, int act, hipStream_t s,
@@ -1428,6 +1442,9 @@ static int launch_c2r(const FFTArgs& a, const float2* in, float* x, const float*
         MSFNO_TRY(go(fft_c2r_dma_kernel<CL, true, 4, 1, true>, 4, per));
       else if (planes)
         MSFNO_TRY(go(fft_c2r_dma_kernel<CL, false, 4, 1, true>, 4, per));
+      else if (addsrc && areg && c2r_swz() && tw + 12 * per_reg <= 160 * 1024)
+        // MSFNO_C2R_SWZ=1 (A/B): 12 waves with the codelet's pass-2 swizzle
+        MSFNO_TRY(go(fft_c2r_dma_kernel<CL, true, 12, 1, false, true, true>, 12, per_reg));
       else if (addsrc && areg && tw + 16 * per_reg <= 160 * 1024)
         // fp32 x1 for the fused MLP: the same 16-wave register-skip kernel
         MSFNO_TRY(go(fft_c2r_dma_kernel<CL, true, 16, 1, false, true>, 16, per_reg));

@@ -66,6 +66,7 @@ VARIANTS = [
     {"MSFNO_ENGINE": "x6", "MSFNO_MF_SCHED": "0"},
     {"MSFNO_ENGINE": "x6", "MSFNO_MF_AHEAD": "3"},
     {"MSFNO_ENGINE": "x6", "MSFNO_X6_TILE": "4"},
+    {"MSFNO_C2R_SWZ": "1"},
 ]
 
 
